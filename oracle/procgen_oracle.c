@@ -1,0 +1,1412 @@
+/*
+ * procgen_oracle.c -- scalar CPU restatement of the reference step path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see procgen_oracle.h): this is the checker the HIP
+ * engine is compared against, never the product.  Every function cites the
+ * reference file:line it restates (paths relative to /root/reference/procgen/src).
+ *
+ * Build: oracle/Makefile, -O2 -march=x86-64 -ffp-contract=off (no FMA
+ * contraction: the reference's float/double arithmetic must be reproduced
+ * operation by operation).
+ *
+ * Floating point: C promotion rules are kept exactly as the reference C++ has
+ * them (e.g. `.9 * vx` is a double multiply then a float store).  libm calls use
+ * the precision the reference TU resolves to: double sqrt
+ * in basic_step_object, double `sign` in push_obj.
+ */
+#include "procgen_oracle.h"
+
+#include <math.h>
+#include <stdbool.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ constants */
+/* game.h:25-28 */
+#define RES_W 64
+#define RES_H 64
+/* object-ids.h:9-27 */
+#define INVALID_OBJ (-1)
+#define INVALID_IDX (-2)
+#define PLAYER 0
+#define SPACE 100
+#define WALL_OBJ 51
+#define EXIT_OBJ 52
+#define AGENT_OBJ 53
+#define EXPLOSION 54
+#define EXPLOSION5 58
+#define TRAIL 59
+/* basic-abstract-game.cpp:6-20 */
+static const float PI_F = 3.14159265358979323846264338327950288f; /* cpp-utils.h:12 */
+#define MIXRATEROT 0.5f
+#define POS_EPS (-0.001f)
+#define RENDER_EPS 0.02f
+#define USE_ASSET_THRESHOLD 100
+#define MAX_ASSETS 100
+#define MAX_IMAGE_THEMES 10
+/* game.h:34-39 */
+enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
+
+#define MAX_ENTS 8192
+#define MAX_GRID (64 * 64)
+
+enum { GAME_COINRUN = 5 };
+
+static void fatal_msg(const char *m) {
+    fprintf(stderr, "oracle fatal: %s\n", m);
+    abort();
+}
+#define fassert(c)                                  \
+    do {                                            \
+        if (!(c)) fatal_msg("fassert failed: " #c); \
+    } while (0)
+
+/* ================================================================== MT19937
+ * std::mt19937 as libstdc++ implements it (standard-defined; randgen.h:12). */
+typedef struct {
+    uint32_t mt[624];
+    int mti;
+    bool is_seeded;
+} MT;
+
+static void mt_seed(MT *m, uint32_t s) { /* std::mersenne_twister_engine::seed */
+    m->mt[0] = s;
+    for (int i = 1; i < 624; i++) m->mt[i] = 1812433253u * (m->mt[i - 1] ^ (m->mt[i - 1] >> 30)) + (uint32_t)i;
+    m->mti = 624;
+    m->is_seeded = true;
+}
+
+static void mt_twist(MT *m) {
+    for (int i = 0; i < 624; i++) {
+        uint32_t y = (m->mt[i] & 0x80000000u) | (m->mt[(i + 1) % 624] & 0x7fffffffu);
+        m->mt[i] = m->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    m->mti = 0;
+}
+
+static uint32_t mt_next(MT *m) {
+    if (m->mti >= 624) mt_twist(m);
+    uint32_t y = m->mt[m->mti++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+/* ================================================================== RandGen (randgen.cpp) */
+static int rg_randint(MT *m, int low, int high) { /* randgen.cpp:6-11 */
+    fassert(m->is_seeded);
+    uint32_t x = mt_next(m);
+    uint32_t range = (uint32_t)high - (uint32_t)low;
+    return (int)((uint32_t)low + (x % range));
+}
+static int rg_randn(MT *m, int high) { /* randgen.cpp:13-17 */
+    fassert(m->is_seeded);
+    uint32_t x = mt_next(m);
+    return (int)(x % (uint32_t)high);
+}
+static float rg_rand01(MT *m) { /* randgen.cpp:19-23 */
+    fassert(m->is_seeded);
+    uint32_t x = mt_next(m);
+    return (float)((double)x / ((double)0xffffffffu + 1));
+}
+static bool rg_randbool(MT *m) { return (double)rg_rand01(m) > .5; }                          /* :25-27 */
+static float rg_randrange(MT *m, float lo, float hi) { return rg_rand01(m) * (hi - lo) + lo; } /* :29-31 */
+static int rg_randint0(MT *m) { /* randgen.cpp:90-93 */
+    fassert(m->is_seeded);
+    return (int)mt_next(m);
+}
+static void rg_seed(MT *m, int seed) { mt_seed(m, (uint32_t)seed); } /* :95-98 */
+
+/* ================================================================== Entity (entity.h/.cpp) */
+typedef struct {
+    float x, y, vx, vy, rx, ry;
+    int type, image_type, image_theme, render_z;
+    bool will_erase, collides_with_entities;
+    float collision_margin, rotation, vrot;
+    bool is_reflected;
+    int fire_time, spawn_time, life_time, expire_time;
+    bool use_abs_coords;
+    float friction;
+    bool smart_step, avoids_collisions, auto_erase;
+    float alpha, health, theta, grow_rate, alpha_decay, climber_spawn_x;
+} Entity;
+
+static void entity_init(Entity *e, float x, float y, float vx, float vy, float rx, float ry, int type) {
+    /* entity.cpp:8-47 */
+    memset(e, 0, sizeof(*e));
+    e->x = x; e->y = y; e->vx = vx; e->vy = vy; e->rx = rx; e->ry = ry;
+    e->type = type; e->image_type = type; e->image_theme = 0;
+    e->will_erase = false; e->collides_with_entities = false;
+    e->collision_margin = 0.0f; e->rotation = 0.0f; e->is_reflected = false; e->vrot = 0.0f;
+    e->alpha = 1.0f; e->grow_rate = 1.0f; e->alpha_decay = 1.0f;
+    e->fire_time = -1; e->spawn_time = -1; e->expire_time = -1; e->life_time = 0;
+    e->health = 1; e->theta = -100;
+    e->friction = 1; e->smart_step = false; e->avoids_collisions = false; e->auto_erase = true;
+    e->render_z = 0; e->use_abs_coords = false; e->climber_spawn_x = 0;
+    if (type == EXPLOSION) {
+        e->grow_rate = 1.4f;
+        e->expire_time = 4;
+    } else if (type == TRAIL) {
+        e->grow_rate = 1.05f;
+        e->alpha_decay = 0.8f;
+    }
+}
+
+static void entity_step(Entity *e) { /* entity.cpp:57-82 */
+    if (!e->smart_step) {
+        e->x += e->vx;
+        e->y += e->vy;
+    }
+    e->rotation += e->vrot;
+    e->vx *= e->friction;
+    e->vy *= e->friction;
+    e->life_time += 1;
+    if (e->expire_time > 0 && e->life_time > e->expire_time) e->will_erase = true;
+    if (e->type == EXPLOSION) {
+        if (e->image_type < EXPLOSION5) e->image_type++;
+    }
+    e->rx *= e->grow_rate;
+    e->ry *= e->grow_rate;
+    e->alpha = e->alpha_decay * e->alpha;
+}
+
+/* ================================================================== game state */
+typedef struct {
+    /* GameOptions (game.h:47-61) */
+    bool paint_vel_info, use_generated_assets, use_monochrome_assets, restrict_themes;
+    bool use_backgrounds, center_agent, use_sequential_levels;
+    int debug_mode, distribution_mode;
+} GameOptions;
+
+typedef struct {
+    int game_id;
+    GameOptions options;
+    /* Game (game.h:64-134) */
+    bool grid_step;
+    int level_seed_low, level_seed_high, game_n;
+    MT level_seed_rand_gen, rand_gen;
+    float sd_reward;
+    bool sd_done, sd_level_complete;
+    int action, timeout, current_level_seed, prev_level_seed, episodes_remaining;
+    bool episode_done;
+    int last_reward_timer;
+    float last_reward;
+    int default_action, cur_time, reset_count;
+    float total_reward;
+    /* BasicAbstractGame (basic-abstract-game.h) */
+    int grid_size, grid_w, grid_h;
+    int grid[MAX_GRID];
+    Entity *ents;
+    int num_ents;
+    bool agent_erased; /* agent removed from `entities` but still referenced by `agent` */
+    Entity agent_ghost;
+    int background_index;
+    float bg_tile_ratio, bg_pct_x, char_dim;
+    int last_move_action, move_action, special_action;
+    float mixrate, maxspeed, max_jump;
+    float action_vx, action_vy, action_vrot;
+    float center_x, center_y;
+    bool random_agent_start, has_useful_vel_info;
+    int step_rand_int;
+    int main_width, main_height, out_of_bounds_object;
+    float unit, view_dim, x_off, y_off, visibility, min_visibility;
+    /* coinrun (coinrun.cpp:38-47) */
+    float last_agent_y;
+    int wall_theme;
+    bool has_support, facing_right, is_on_crate;
+    float gravity, air_control;
+    /* observation of the last step */
+    uint32_t canvas[RES_W * RES_H];
+} Game;
+
+typedef struct {
+    int count, offset;
+    Game *games;
+    const or_atlas *atlas;
+} Vec;
+
+static Entity *AG(Game *g) { return g->agent_erased ? &g->agent_ghost : &g->ents[0]; }
+
+/* ------------------------------------------------------------------ grid (grid.h) */
+static bool grid_contains(Game *g, int x, int y) { return 0 <= y && y < g->grid_h && 0 <= x && x < g->grid_w; }
+static void grid_set(Game *g, int x, int y, int v) {
+    fassert(grid_contains(g, x, y));
+    g->grid[y * g->grid_w + x] = v;
+}
+static int get_obj(Game *g, int x, int y) { /* basic-abstract-game.cpp:180-185 */
+    if (!grid_contains(g, x, y)) return g->out_of_bounds_object;
+    return g->grid[y * g->grid_w + x];
+}
+static void set_obj(Game *g, int x, int y, int v) { grid_set(g, x, y, v); } /* :229-231 */
+static int get_obj_from_floats(Game *g, float i, float j) { /* :167-174 */
+    if (i < 0) return g->out_of_bounds_object;
+    if (j < 0) return g->out_of_bounds_object;
+    return get_obj(g, (int)floorf(i), (int)floorf(j));
+}
+static void fill_elem(Game *g, int x, int y, int dx, int dy, int elem) { /* :125-131 (char elem) */
+    signed char c = (signed char)elem;
+    for (int j = 0; j < dx; j++)
+        for (int k = 0; k < dy; k++) grid_set(g, x + j, y + k, c);
+}
+
+/* ------------------------------------------------------------------ entity list */
+static int add_entity_rxy(Game *g, float x, float y, float vx, float vy, float rx, float ry, int type) {
+    fassert(g->num_ents < MAX_ENTS);
+    entity_init(&g->ents[g->num_ents], x, y, vx, vy, rx, ry, type);
+    return g->num_ents++;
+}
+static int add_entity(Game *g, float x, float y, float vx, float vy, float r, int type) { /* :575-579 */
+    return add_entity_rxy(g, x, y, vx, vy, r, r, type);
+}
+
+static bool is_out_of_bounds(Game *g, const Entity *e) { /* :1077-1093 */
+    float x = e->x, y = e->y, rx = e->rx, ry = e->ry;
+    if (x + rx < 0) return true;
+    if (y + ry < 0) return true;
+    if (x - rx > g->main_width) return true;
+    if (y - ry > g->main_height) return true;
+    return false;
+}
+
+static void erase_if_needed(Game *g) { /* :757-765 */
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *e = &g->ents[i];
+        if (e->will_erase || (e->auto_erase && is_out_of_bounds(g, e))) {
+            if (i == 0 && !g->agent_erased) {
+                g->agent_ghost = *e;
+                g->agent_erased = true;
+            }
+            memmove(&g->ents[i], &g->ents[i + 1], sizeof(Entity) * (size_t)(g->num_ents - i - 1));
+            g->num_ents--;
+        }
+    }
+}
+
+static bool has_collision(const Entity *e1, const Entity *e2, float margin) { /* :1154-1159 */
+    float threshold_x = (e1->rx + e2->rx) + margin;
+    float threshold_y = (e1->ry + e2->ry) + margin;
+    return (fabsf(e1->x - e2->x) < threshold_x) && (fabsf(e1->y - e2->y) < threshold_y);
+}
+
+static bool has_agent_collision(Game *g, const Entity *e1) { /* :1135-1140 */
+    if (e1->type == PLAYER) return false;
+    return has_collision(e1, AG(g), e1->collision_margin);
+}
+
+/* ================================================================== per-game hooks */
+/* coinrun object ids, coinrun.cpp:13-30 */
+#define CR_GOAL 1
+#define CR_SAW 2
+#define CR_SAW2 3
+#define CR_ENEMY 5
+#define CR_ENEMY1 6
+#define CR_ENEMY2 7
+#define CR_PLAYER_JUMP 9
+#define CR_PLAYER_RIGHT1 12
+#define CR_PLAYER_RIGHT2 13
+#define CR_WALL_MID 15
+#define CR_WALL_TOP 16
+#define CR_LAVA_MID 17
+#define CR_LAVA_TOP 18
+#define CR_ENEMY_BARRIER 19
+#define CR_CRATE 20
+static const float CR_GOAL_REWARD = 10.0f;
+static bool cr_is_wall(int t) { return t == CR_WALL_MID || t == CR_WALL_TOP; } /* :175-177 */
+static bool cr_is_lava(int t) { return t == CR_LAVA_MID || t == CR_LAVA_TOP; } /* :179-181 */
+
+static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_horizontal) {
+    (void)is_horizontal;
+    /* basic-abstract-game.cpp:494-501 */
+    bool base = (target == WALL_OBJ) || (target == g->out_of_bounds_object);
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:204-211 */
+        if (base) return true;
+        if (src->type == PLAYER && cr_is_wall(target)) return true;
+        return false;
+    }
+    return base;
+}
+
+static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *target, bool is_horizontal) {
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:187-202 */
+        if (target->type == CR_CRATE && !is_horizontal) {
+            Entity *agent = AG(g);
+            if (agent->vy >= 0) return false;
+            if (g->action_vy < 0) return false;
+            if (g->last_agent_y < (target->y + target->ry + agent->ry)) return false;
+            g->is_on_crate = true;
+            return true;
+        }
+    }
+    return hook_is_blocked(g, src, target->type, is_horizontal); /* :503-505 */
+}
+
+static bool hook_will_reflect(Game *g, int src, int target) {
+    if (g->game_id == GAME_COINRUN) /* coinrun.cpp:140-142 */
+        return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    return false;
+}
+
+static void hook_handle_agent_collision(Game *g, Entity *obj) {
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:123-131 */
+        if (obj->type == CR_ENEMY) g->sd_done = true;
+        else if (obj->type == CR_SAW) g->sd_done = true;
+    }
+}
+
+static void hook_handle_grid_collision(Game *g, Entity *obj, int type, int i, int j) {
+    (void)i; (void)j;
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:144-154 */
+        if (obj->type == PLAYER) {
+            if (type == CR_GOAL) {
+                g->sd_reward += CR_GOAL_REWARD;
+                g->sd_done = true;
+                g->sd_level_complete = true;
+            } else if (cr_is_lava(type)) {
+                g->sd_done = true;
+            }
+        }
+    }
+}
+
+static int hook_image_for_type(Game *g, int type) {
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:213-225 */
+        if (type == PLAYER) {
+            Entity *agent = AG(g);
+            if (fabs((double)agent->vx) < .01 && g->action_vx == 0 && g->has_support) {
+                return PLAYER;
+            } else {
+                return (g->cur_time / 5 % 2 == 0 || !g->has_support) ? CR_PLAYER_RIGHT1 : CR_PLAYER_RIGHT2;
+            }
+        } else if (type == CR_ENEMY_BARRIER) {
+            return -1;
+        }
+    }
+    return abs(type); /* basic-abstract-game.cpp:446-448 */
+}
+
+static int hook_theme_for_grid_obj(Game *g, int type) {
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:133-138 */
+        if (cr_is_wall(type)) return g->wall_theme;
+        return 0;
+    }
+    return 0;
+}
+
+static bool is_player_image(int t) {
+    return t == PLAYER || t == CR_PLAYER_JUMP || t == CR_PLAYER_RIGHT1 || t == CR_PLAYER_RIGHT2;
+}
+
+/* ================================================================== physics (basic-abstract-game.cpp) */
+static bool sub_step(Game *g, int obj_i, float _vx, float _vy, int depth);
+
+static double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); } /* cpp-utils.h:42-44 */
+
+static bool push_obj(Game *g, int src_i, int target_i, bool is_horizontal, int depth) { /* :248-276 */
+    Entity *src = &g->ents[src_i], *target = &g->ents[target_i];
+    float rsum = is_horizontal ? (src->rx + target->rx) : (src->ry + target->ry);
+    float delx = target->x - src->x;
+    float dely = target->y - src->y;
+    float t_vx = 0, t_vy = 0;
+    if (is_horizontal) {
+        t_vx = (float)((double)src->x + dsign(delx) * (double)rsum - (double)target->x);
+    } else {
+        t_vy = (float)((double)src->y + dsign(dely) * (double)rsum - (double)target->y);
+    }
+    bool block = false;
+    if (depth < 5) block = sub_step(g, target_i, t_vx, t_vy, depth + 1);
+    target = &g->ents[target_i];
+    if (is_horizontal) target->vx = 0;
+    else target->vy = 0;
+    return block;
+}
+
+static bool sub_step(Game *g, int obj_i, float _vx, float _vy, int depth) { /* :278-380 */
+    Entity *obj = &g->ents[obj_i];
+    if (obj->will_erase) return false;
+    float ny = obj->y + _vy;
+    float nx = obj->x + _vx;
+    float margin = 0.98f;
+    bool is_horizontal = _vx != 0;
+    bool block = false, reflect = false;
+    for (int i = 0; i < 2; i++) {
+        for (int j = 0; j < 2; j++) {
+            int type2 = get_obj_from_floats(g, nx + obj->rx * margin * (float)(2 * i - 1),
+                                            ny + obj->ry * margin * (float)(2 * j - 1));
+            block = block || hook_is_blocked(g, obj, type2, is_horizontal);
+            reflect = reflect || hook_will_reflect(g, obj->type, type2);
+        }
+    }
+    if (reflect) {
+        if (is_horizontal) {
+            float delta;
+            if (_vx < 0) delta = ceilf(nx - obj->rx) - (nx - obj->rx);
+            else delta = floorf(nx + obj->rx) - (nx + obj->rx);
+            obj->vx = -1 * obj->vx;
+            nx = nx + 2 * delta;
+        } else {
+            float delta;
+            if (_vy < 0) delta = ceilf(ny - obj->ry) - (ny - obj->ry);
+            else delta = floorf(ny + obj->ry) - (ny + obj->ry);
+            obj->vy = -1 * obj->vy;
+            ny = ny + 2 * delta;
+        }
+    } else if (block) {
+        if (is_horizontal) {
+            if (g->grid_step) nx = obj->x;
+            else nx = _vx > 0 ? (floorf(nx + obj->rx) - obj->rx) : (ceilf(nx - obj->rx) + obj->rx);
+        } else {
+            if (g->grid_step) ny = obj->y;
+            else ny = _vy > 0 ? (floorf(ny + obj->ry) - obj->ry) : (ceilf(ny - obj->ry) + obj->ry);
+        }
+    }
+    obj->x = nx;
+    obj->y = ny;
+    bool block2 = false;
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        obj = &g->ents[obj_i];
+        Entity *m = &g->ents[i];
+        if (i == obj_i || m->will_erase) continue;
+        bool curr_block = false;
+        if (has_collision(obj, m, POS_EPS)) {
+            if (hook_is_blocked_ents(g, obj, m, is_horizontal)) {
+                curr_block = true;
+            } else if (hook_will_reflect(g, obj->type, m->type)) {
+                if (is_horizontal) {
+                    float delx = m->x - obj->x;
+                    float rsum = m->rx + obj->rx;
+                    obj->x += _vx > 0 ? -2 * (rsum - delx) : 2 * (rsum + delx);
+                    obj->vx = -1 * obj->vx;
+                } else {
+                    float dely = m->y - obj->y;
+                    float rsum = m->ry + obj->ry;
+                    obj->y += _vy > 0 ? -2 * (rsum - dely) : 2 * (rsum + dely);
+                    obj->vy = -1 * obj->vy;
+                }
+            }
+            if (curr_block) push_obj(g, i, obj_i, is_horizontal, depth);
+        }
+        block2 = block2 || curr_block;
+    }
+    return block || block2;
+}
+
+static void basic_step_object(Game *g, int obj_i) { /* :602-665 */
+    Entity *obj = &g->ents[obj_i];
+    if (obj->will_erase) return;
+    int num_sub_steps;
+    if (g->grid_step) {
+        num_sub_steps = 1;
+    } else {
+        /* double sqrt: the TU resolves the unqualified sqrt to the C double function */
+        num_sub_steps = (int)(4 * sqrt((double)(obj->vx * obj->vx + obj->vy * obj->vy)));
+        if (num_sub_steps < 4) num_sub_steps = 4;
+    }
+    float pct = (float)(1.0 / num_sub_steps);
+    float cmp = fabsf(obj->vx) - fabsf(obj->vy);
+    bool step_x_first = cmp == 0 ? g->step_rand_int % 2 == 0 : (cmp > 0);
+    if (obj->type == PLAYER) {
+        if (g->action_vx != 0) step_x_first = true;
+        if (g->action_vy != 0) step_x_first = false;
+    }
+    float vx_pct = 0, vy_pct = 0;
+    for (int s = 0; s < num_sub_steps; s++) {
+        bool block_x = false, block_y = false;
+        if (step_x_first) {
+            block_x = sub_step(g, obj_i, g->ents[obj_i].vx * pct, 0, 0);
+            block_y = sub_step(g, obj_i, 0, g->ents[obj_i].vy * pct, 0);
+        } else {
+            block_y = sub_step(g, obj_i, 0, g->ents[obj_i].vy * pct, 0);
+            block_x = sub_step(g, obj_i, g->ents[obj_i].vx * pct, 0, 0);
+        }
+        if (!block_x) vx_pct += 1;
+        if (!block_y) vy_pct += 1;
+        if (block_x && block_y) break;
+    }
+    vx_pct = vx_pct / (float)num_sub_steps;
+    vy_pct = vy_pct / (float)num_sub_steps;
+    obj = &g->ents[obj_i];
+    obj->vx *= vx_pct;
+    obj->vy *= vy_pct;
+}
+
+static void check_grid_collisions(Game *g, int ent_i) { /* :145-165 */
+    Entity *ent = &g->ents[ent_i];
+    float ax = ent->x, ay = ent->y, arx = ent->rx, ary = ent->ry;
+    int min_x = (int)(ax - (arx + POS_EPS));
+    int max_x = (int)(ax + (arx + POS_EPS));
+    int min_y = (int)(ay - (ary + POS_EPS));
+    int max_y = (int)(ay + (ary + POS_EPS));
+    for (int x = min_x; x <= max_x; x++) {
+        for (int y = min_y; y <= max_y; y++) {
+            int grid_type = get_obj_from_floats(g, (float)x, (float)y);
+            if (grid_type != SPACE) hook_handle_grid_collision(g, &g->ents[ent_i], grid_type, x, y);
+        }
+    }
+}
+
+static void step_entities(Game *g) { /* :1095-1107 */
+    int count = g->num_ents;
+    for (int i = count - 1; i >= 0; i--) {
+        if (g->ents[i].smart_step) basic_step_object(g, i);
+        entity_step(&g->ents[i]);
+    }
+}
+
+/* ------------------------------------------------------------------ agent control */
+static void coinrun_set_action_xy(Game *g, int move_action) { /* coinrun.cpp:451-472 */
+    g->action_vx = (float)(move_action / 3 - 1);
+    g->action_vy = (float)((move_action % 3) - 1);
+    if (g->action_vx > 0) g->facing_right = true;
+    if (g->action_vx < 0) g->facing_right = false;
+    Entity *agent = AG(g);
+    int obj_below_1 = get_obj_from_floats(g, (float)((double)agent->x - ((double)agent->rx - .01)),
+                                          (float)((double)agent->y - ((double)agent->ry + .01)));
+    int obj_below_2 = get_obj_from_floats(g, (float)((double)agent->x + ((double)agent->rx - .01)),
+                                          (float)((double)agent->y - ((double)agent->ry + .01)));
+#define CAN_SUPPORT(o) (cr_is_wall(o) || (o) == g->out_of_bounds_object) /* coinrun.cpp:447-449 */
+    g->has_support = (g->is_on_crate || CAN_SUPPORT(obj_below_1) || CAN_SUPPORT(obj_below_2)) && agent->vy == 0;
+#undef CAN_SUPPORT
+    g->is_on_crate = false;
+    if (g->action_vy == 1) {
+        if (!g->has_support) g->action_vy = 0;
+    }
+}
+
+static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_COINRUN) {
+        coinrun_set_action_xy(g, move_action);
+        return;
+    }
+    g->action_vx = (float)(move_action / 3 - 1); /* basic-abstract-game.cpp:667-671 */
+    g->action_vy = (float)(move_action % 3 - 1);
+    g->action_vrot = 0;
+}
+
+static float clip_abs(float x, float y) { /* cpp-utils.h:46-52 */
+    if (x > y) return y;
+    if (x < -y) return -y;
+    return x;
+}
+
+static void update_agent_velocity(Game *g) {
+    Entity *agent = AG(g);
+    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:156-173 */
+        float mixrate_x = g->has_support ? g->mixrate : (g->mixrate * g->air_control);
+        agent->vx = (1 - mixrate_x) * agent->vx + mixrate_x * g->maxspeed * g->action_vx;
+        if (fabsf(agent->vx) < mixrate_x * g->maxspeed) agent->vx = 0;
+        if (g->action_vy > 0) {
+            agent->vy = g->max_jump;
+        } else {
+            if (g->has_support) agent->vy = (float)((double)agent->vy + .2 * (double)g->action_vy);
+        }
+        if (!(g->has_support && g->action_vy > 0)) {
+            agent->vy -= g->gravity;
+            agent->vy = clip_abs(agent->vy, g->max_jump);
+        }
+        return;
+    }
+    /* basic-abstract-game.cpp:678-693 */
+    float v_scale = 1.0f;
+    agent->vx = (1 - g->mixrate) * agent->vx;
+    agent->vy = (1 - g->mixrate) * agent->vy;
+    agent->vx += g->mixrate * g->maxspeed * g->action_vx * v_scale;
+    agent->vy += g->mixrate * g->maxspeed * g->action_vy * v_scale;
+    agent->vx = (float)(.9 * (double)agent->vx);
+    agent->vy = (float)(.9 * (double)agent->vy);
+}
+
+/* ------------------------------------------------------------------ base game_step */
+static void basic_game_step(Game *g) { /* basic-abstract-game.cpp:695-755 */
+    g->step_rand_int = rg_randint(&g->rand_gen, 0, 1000000);
+    g->move_action = g->action % 9;
+    g->special_action = 0;
+    if (g->action >= 9) {
+        g->special_action = g->action - 8;
+        g->move_action = 4;
+    }
+    if (g->move_action != 4) g->last_move_action = g->move_action;
+    g->action_vrot = 0;
+    g->action_vx = 0;
+    g->action_vy = 0;
+    set_action_xy(g, g->move_action);
+    Entity *agent = AG(g);
+    if (g->grid_step) {
+        agent->vx = g->action_vx;
+        agent->vy = g->action_vy;
+    } else {
+        update_agent_velocity(g);
+        agent->vrot = MIXRATEROT * agent->vrot;
+        agent->vrot += MIXRATEROT * (15 * PI_F / 180) * g->action_vrot;
+    }
+    step_entities(g);
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *ent = &g->ents[i];
+        if (has_agent_collision(g, ent)) hook_handle_agent_collision(g, ent);
+        if (ent->collides_with_entities) {
+            /* no coinrun entity sets collides_with_entities; other games: later rounds */
+            fatal_msg("collides_with_entities not restated yet");
+        }
+        if (g->ents[i].smart_step) check_grid_collisions(g, i);
+    }
+    erase_if_needed(g);
+    g->sd_done = g->sd_done || is_out_of_bounds(g, AG(g));
+}
+
+/* ------------------------------------------------------------------ coinrun level generation */
+static void choose_random_theme(Game *g, Entity *e, const or_atlas *at) { /* :1047-1050 */
+    int nt = at->num_themes[e->image_type];
+    fassert(nt > 0);
+    e->image_theme = rg_randn(&g->rand_gen, nt);
+}
+
+static void cr_fill_block_top(Game *g, int x, int y, int dx, int dy, int fill, int top) { /* coinrun.cpp:227-231 */
+    fassert(dy > 0);
+    fill_elem(g, x, y, dx, dy - 1, fill);
+    fill_elem(g, x, y + dy - 1, dx, 1, top);
+}
+static void cr_fill_ground_block(Game *g, int x, int y, int dx, int dy) {
+    cr_fill_block_top(g, x, y, dx, dy, CR_WALL_MID, CR_WALL_TOP);
+}
+static void cr_fill_lava_block(Game *g, int x, int y, int dx, int dy) {
+    cr_fill_block_top(g, x, y, dx, dy, CR_LAVA_MID, CR_LAVA_TOP);
+}
+static void cr_create_saw_enemy(Game *g, int x, int y) { /* :248-250 */
+    add_entity(g, (float)(x + .5), (float)(y + .5), 0, 0, (float).5, CR_SAW);
+}
+static void cr_create_enemy(Game *g, int x, int y, const or_atlas *at) { /* :252-258 */
+    int i = add_entity(g, (float)(x + .5), (float)(y + .5), (float)(.15 * (rg_randn(&g->rand_gen, 2) * 2 - 1)), 0,
+                       (float).5, CR_ENEMY);
+    Entity *e = &g->ents[i];
+    e->smart_step = true;
+    e->image_type = CR_ENEMY1;
+    e->render_z = 1;
+    choose_random_theme(g, e, at);
+}
+static void cr_create_crate(Game *g, int x, int y, const or_atlas *at) { /* :260-263 */
+    int i = add_entity(g, (float)(x + .5), (float)(y + .5), 0, 0, (float).5, CR_CRATE);
+    choose_random_theme(g, &g->ents[i], at);
+}
+
+static void cr_generate_coin_to_the_right(Game *g, const or_atlas *at) { /* coinrun.cpp:265-414 */
+    MT *r = &g->rand_gen;
+    int max_difficulty = 3;
+    int dif = rg_randn(r, max_difficulty) + 1;
+    int num_sections = rg_randn(r, dif) + dif;
+    int curr_x = 5;
+    int curr_y = 1;
+    int pit_threshold = dif;
+    int danger_type = rg_randn(r, 3);
+    bool allow_pit = (g->options.debug_mode & (1 << 1)) == 0;
+    bool allow_crate = (g->options.debug_mode & (1 << 2)) == 0;
+    bool allow_dy = (g->options.debug_mode & (1 << 3)) == 0;
+    int w = g->main_width;
+    float _max_dy = g->max_jump * g->max_jump / (2 * g->gravity);
+    float _max_dx = g->maxspeed * 2 * g->max_jump / g->gravity;
+    int max_dy = (int)((double)_max_dy - .5);
+    int max_dx = (int)((double)_max_dx - .5);
+    bool allow_monsters = true;
+    if (g->options.distribution_mode == EasyMode) allow_monsters = false;
+
+    for (int section_idx = 0; section_idx < num_sections; section_idx++) {
+        if (curr_x + 15 >= w) break;
+        int dy = rg_randn(r, 4) + 1 + (int)(dif / 3);
+        if (!allow_dy) dy = 0;
+        if (dy > max_dy) dy = max_dy;
+        if (curr_y >= 20) {
+            dy *= -1;
+        } else if (curr_y >= 5 && rg_randn(r, 2) == 1) {
+            dy *= -1;
+        }
+        int dx = rg_randn(r, 2 * dif) + 3 + (int)(dif / 3);
+        curr_y += dy;
+        if (curr_y < 1) curr_y = 1;
+        bool use_pit = allow_pit && (dx > 7) && (curr_y > 3) && (rg_randn(r, 20) >= pit_threshold);
+        if (use_pit) {
+            int x1 = rg_randn(r, 3) + 1;
+            int x2 = rg_randn(r, 3) + 1;
+            int pit_width = dx - x1 - x2;
+            if (pit_width > max_dx) {
+                pit_width = max_dx;
+                x2 = dx - x1 - pit_width;
+            }
+            cr_fill_ground_block(g, curr_x, 0, x1, curr_y);
+            cr_fill_ground_block(g, curr_x + dx - x2, 0, x2, curr_y);
+            int lava_height = rg_randn(r, curr_y - 3) + 1;
+            if (danger_type == 0) {
+                cr_fill_lava_block(g, curr_x + x1, 1, pit_width, lava_height);
+            } else if (danger_type == 1) {
+                for (int ei = 0; ei < pit_width; ei++) cr_create_saw_enemy(g, curr_x + x1 + ei, 1);
+            } else if (danger_type == 2) {
+                for (int ei = 0; ei < pit_width; ei++) cr_create_enemy(g, curr_x + x1 + ei, 1, at);
+            }
+            if (pit_width > 4) {
+                int x3, w1;
+                if (pit_width == 5) {
+                    x3 = 1 + rg_randn(r, 2);
+                    w1 = 1 + rg_randn(r, 2);
+                } else if (pit_width == 6) {
+                    x3 = 2 + rg_randn(r, 2);
+                    w1 = 1 + rg_randn(r, 2);
+                } else {
+                    x3 = 2 + rg_randn(r, 2);
+                    int x4 = 2 + rg_randn(r, 2);
+                    w1 = pit_width - x3 - x4;
+                }
+                cr_fill_ground_block(g, curr_x + x1 + x3, curr_y - 1, w1, 1);
+            }
+        } else {
+            cr_fill_ground_block(g, curr_x, 0, dx, curr_y);
+            int ob1_x = -1;
+            int ob2_x = -1;
+            if (rg_randn(r, 10) < (2 * dif) && dx > 3) {
+                ob1_x = curr_x + rg_randn(r, dx - 2) + 1;
+                cr_create_saw_enemy(g, ob1_x, curr_y);
+            }
+            if (rg_randn(r, 10) < dif && dx > 3 && (max_dx >= 4) && allow_monsters) {
+                ob2_x = curr_x + rg_randn(r, dx - 2) + 1;
+                cr_create_enemy(g, ob2_x, curr_y, at);
+            }
+            if (allow_crate) {
+                for (int i = 0; i < 2; i++) {
+                    int crate_x = curr_x + rg_randn(r, dx - 2) + 1;
+                    if (rg_randn(r, 2) == 1 && ob1_x != crate_x && ob2_x != crate_x) {
+                        int pile_height = rg_randn(r, 3) + 1;
+                        for (int j = 0; j < pile_height; j++) cr_create_crate(g, crate_x, curr_y + j, at);
+                    }
+                }
+            }
+        }
+        if (!cr_is_wall(get_obj(g, curr_x - 1, curr_y))) set_obj(g, curr_x - 1, curr_y, CR_ENEMY_BARRIER);
+        curr_x += dx;
+        set_obj(g, curr_x, curr_y, CR_ENEMY_BARRIER);
+    }
+    set_obj(g, curr_x, curr_y, CR_GOAL);
+    cr_fill_ground_block(g, curr_x, 0, 1, curr_y);
+    fill_elem(g, curr_x + 1, 0, g->main_width - curr_x - 1, g->main_height, CR_WALL_MID);
+}
+
+static void basic_game_reset(Game *g, const or_atlas *at) { /* basic-abstract-game.cpp:767-806 */
+    fassert(g->main_width > 0 && g->main_height > 0);
+    g->bg_pct_x = rg_rand01(&g->rand_gen);
+    g->grid_size = g->main_width * g->main_height;
+    fassert(g->grid_size <= MAX_GRID);
+    g->grid_w = g->main_width;
+    g->grid_h = g->main_height;
+    memset(g->grid, 0, sizeof(g->grid));
+    g->background_index = rg_randn(&g->rand_gen, at->num_backgrounds);
+    g->num_ents = 0;
+    g->agent_erased = false;
+    float ax, ay;
+    float a_r = 0.4f;
+    if (g->random_agent_start) {
+        ax = rg_rand01(&g->rand_gen) * (g->main_width - 2 * a_r) + a_r;
+        ay = rg_rand01(&g->rand_gen) * (g->main_height - 2 * a_r) + a_r;
+    } else {
+        ax = a_r;
+        ay = a_r;
+    }
+    int ai = add_entity(g, ax, ay, 0, 0, a_r, PLAYER);
+    fassert(ai == 0);
+    g->ents[0].smart_step = true;
+    g->ents[0].render_z = 1;
+    erase_if_needed(g);
+    fill_elem(g, 0, 0, g->main_width, g->main_height, SPACE);
+}
+
+static void coinrun_game_reset(Game *g, const or_atlas *at) { /* coinrun.cpp:416-445 */
+    basic_game_reset(g, at);
+    g->gravity = 0.2f;
+    g->max_jump = 1.5f;
+    g->air_control = 0.15f;
+    g->maxspeed = .5f;
+    g->has_support = false;
+    g->facing_right = true;
+    Entity *agent = AG(g);
+    if (g->options.distribution_mode == EasyMode) {
+        agent->image_theme = 0;
+        g->wall_theme = 0;
+        g->background_index = 0;
+    } else {
+        choose_random_theme(g, agent, at);
+        g->wall_theme = rg_randn(&g->rand_gen, 6);
+    }
+    agent->rx = .5f;
+    agent->ry = 0.5787f;
+    agent->x = 1 + agent->rx;
+    agent->y = 1 + agent->ry;
+    g->last_agent_y = agent->y;
+    g->is_on_crate = false;
+    /* init_floor_and_walls, coinrun.cpp:241-246 */
+    fill_elem(g, 0, 0, g->main_width, 1, CR_WALL_TOP);
+    fill_elem(g, 0, 0, 1, g->main_height, CR_WALL_MID);
+    fill_elem(g, g->main_width - 1, 0, 1, g->main_height, CR_WALL_MID);
+    fill_elem(g, 0, g->main_height - 1, g->main_width, 1, CR_WALL_MID);
+    cr_generate_coin_to_the_right(g, at);
+}
+
+static void coinrun_game_step(Game *g) { /* coinrun.cpp:474-498 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *ent = &g->ents[i];
+        if (ent->type == CR_ENEMY) {
+            float ex = ent->x, ey = (float)((double)ent->y - (double)ent->ry * .5);
+            int ti = add_entity_rxy(g, ex, ey, 0, 0.01f, 0.3f, 0.2f, TRAIL);
+            g->ents[ti].expire_time = 8;
+            g->ents[ti].alpha = .5f;
+            ent = &g->ents[i];
+            ent->image_type = g->cur_time / 5 % 2 == 0 ? CR_ENEMY1 : CR_ENEMY2;
+            ent->is_reflected = ent->vx > 0;
+        } else if (ent->type == CR_SAW) {
+            ent->image_type = g->cur_time % 2 == 0 ? CR_SAW : CR_SAW2;
+        }
+    }
+    g->last_agent_y = AG(g)->y;
+}
+
+/* ================================================================== Game (game.cpp) */
+static void game_reset_dispatch(Game *g, const or_atlas *at) {
+    if (g->game_id == GAME_COINRUN) coinrun_game_reset(g, at);
+    else fatal_msg("game not restated");
+}
+static void game_step_dispatch(Game *g) {
+    if (g->game_id == GAME_COINRUN) coinrun_game_step(g);
+    else fatal_msg("game not restated");
+}
+
+static void game_reset(Game *g, const or_atlas *at) { /* game.cpp:109-134 */
+    g->reset_count++;
+    if (g->episodes_remaining == 0) {
+        if (g->options.use_sequential_levels && g->sd_level_complete) {
+            g->current_level_seed = (int32_t)((uint32_t)g->current_level_seed + 997u);
+        } else {
+            g->current_level_seed = rg_randint(&g->level_seed_rand_gen, g->level_seed_low, g->level_seed_high);
+        }
+        g->episodes_remaining = 1;
+    } else {
+        g->sd_reward = 0;
+        g->sd_done = false;
+        g->sd_level_complete = false;
+    }
+    rg_seed(&g->rand_gen, g->current_level_seed);
+    game_reset_dispatch(g, at);
+    g->cur_time = 0;
+    g->total_reward = 0;
+    g->episodes_remaining -= 1;
+    g->action = g->default_action;
+}
+
+static void render(Game *g, const or_atlas *at);
+
+static void game_step(Game *g, const or_atlas *at) { /* game.cpp:136-171 */
+    g->cur_time += 1;
+    bool will_force_reset = false;
+    if (g->action == -1) {
+        g->action = g->default_action;
+        will_force_reset = true;
+    }
+    g->sd_reward = 0;
+    g->sd_done = false;
+    g->sd_level_complete = false;
+    game_step_dispatch(g);
+    g->sd_done = g->sd_done || will_force_reset || (g->cur_time >= g->timeout);
+    g->total_reward += g->sd_reward;
+    if (g->sd_reward != 0) {
+        g->last_reward_timer = 10;
+        g->last_reward = g->sd_reward;
+    }
+    g->prev_level_seed = g->current_level_seed;
+    if (g->sd_done) game_reset(g, at);
+    if (g->options.use_sequential_levels && g->sd_level_complete) g->sd_done = false;
+    g->episode_done = g->sd_done;
+    render(g, at); /* observe(), game.cpp:173-191 */
+}
+
+/* ================================================================== Qt raster restatement
+ * Qt 5 raster engine semantics for the painter calls the games make
+ * (QPainter::fillRect, QPainter::drawImage(QRectF, QImage) with and without
+ * setOpacity) onto a 64x64 Format_RGB32 image.  Pinned by tests/golden/qt_raster_*.npz
+ * produced by the real Qt 5.9.7 (tools/qt_raster_golden.cpp). */
+static int qRound(double d) {
+    return d >= 0.0 ? (int)(d + 0.5) : (int)(d - (double)((int)(d - 1)) + 0.5) + (int)(d - 1);
+}
+static int qFloor(double v) { return (int)floor(v); }
+static int qCeil(double v) { return (int)ceil(v); }
+
+static inline uint32_t BYTE_MUL(uint32_t x, uint32_t a) {
+    uint32_t t = (x & 0xff00ffu) * a;
+    t = (t + ((t >> 8) & 0xff00ffu) + 0x800080u) >> 8;
+    t &= 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a;
+    x = (x + ((x >> 8) & 0xff00ffu) + 0x800080u);
+    x &= 0xff00ff00u;
+    return x | t;
+}
+static inline uint32_t INTERPOLATE_PIXEL_255(uint32_t x, uint32_t a, uint32_t y, uint32_t b) {
+    uint32_t t = (x & 0xff00ffu) * a + (y & 0xff00ffu) * b;
+    t = (t + ((t >> 8) & 0xff00ffu) + 0x800080u) >> 8;
+    t &= 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a + ((y >> 8) & 0xff00ffu) * b;
+    x = (x + ((x >> 8) & 0xff00ffu) + 0x800080u);
+    x &= 0xff00ff00u;
+    return x | t;
+}
+
+enum { QFMT_RGB32 = 4, QFMT_ARGB32_PM = 6 };
+
+/* intOpacity of the raster paint state for QPainter::setOpacity(o) */
+static int qt_int_opacity(double opacity) {
+    if (opacity < 0) opacity = 0;
+    if (opacity > 1) opacity = 1;
+    return (int)(opacity * 256);
+}
+
+/* one pixel write of the scale blit's blender */
+static inline void qt_blend(uint32_t *dst, uint32_t src, int fmt, int const_alpha) {
+    if (fmt == QFMT_RGB32) {
+        if (const_alpha == 256) {
+            *dst = src;
+        } else {
+            uint32_t a = (uint32_t)(const_alpha * 255) >> 8;
+            *dst = INTERPOLATE_PIXEL_255(src, a, *dst, 255 - a);
+        }
+    } else {
+        if (const_alpha == 256) {
+            *dst = src + BYTE_MUL(*dst, (~src) >> 24);
+        } else {
+            uint32_t a = (uint32_t)(const_alpha * 255) >> 8;
+            uint32_t s = BYTE_MUL(src, a);
+            *dst = s + BYTE_MUL(*dst, (~s) >> 24);
+        }
+    }
+}
+
+/* QPainter::drawImage(QRectF target, QImage img) with identity transform
+ * (qpaintengine_raster.cpp drawImage -> qt_scale_image_32bit). */
+static void qt_draw_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
+                          int ih, int fmt, bool mirrored, double opacity) {
+    if (rw <= 0 || rh <= 0) return; /* QRectF::isEmpty */
+    if (iw <= 0 || ih <= 0) return;
+    int const_alpha = qt_int_opacity(opacity);
+    /* qt_mapRect_non_normalizing(r, identity): QRectF(topLeft, bottomRight) */
+    double tl_x = rx, tl_y = ry;
+    double br_x = rx + rw, br_y = ry + rh;
+    double t_left = tl_x, t_top = tl_y;
+    double t_w = br_x - tl_x, t_h = br_y - tl_y;
+    double t_right = t_left + t_w, t_bottom = t_top + t_h;
+    double sx = t_w / (double)iw;
+    double sy = t_h / (double)ih;
+    int ix = (int)(65536.0 / sx);
+    int iy = (int)(65536.0 / sy);
+    int cx1 = 0, cx2 = RES_W, cy1 = 0, cy2 = RES_H;
+    int tx1 = qRound(t_left), tx2 = qRound(t_right);
+    int ty1 = qRound(t_top), ty2 = qRound(t_bottom);
+    if (tx2 < tx1) { int t = tx2; tx2 = tx1; tx1 = t; }
+    if (ty2 < ty1) { int t = ty2; ty2 = ty1; ty1 = t; }
+    if (tx1 < cx1) tx1 = cx1;
+    if (tx2 >= cx2) tx2 = cx2;
+    if (tx1 >= tx2) return;
+    if (ty1 < cy1) ty1 = cy1;
+    if (ty2 >= cy2) ty2 = cy2;
+    if (ty1 >= ty2) return;
+    int h = ty2 - ty1;
+    int w = tx2 - tx1;
+    uint32_t basex, srcy;
+    {
+        int dstx = qCeil((tx1 + 0.5 - t_left) * ix) - 1;
+        basex = (uint32_t)(0.0 * 65536) + (uint32_t)dstx;
+        int dsty = qCeil((ty1 + 0.5 - t_top) * iy) - 1;
+        srcy = (uint32_t)(0.0 * 65536) + (uint32_t)dsty;
+    }
+    const int ystart = (int)(srcy >> 16);
+    if (ystart >= ih && iy < 0) {
+        srcy += iy;
+        --h;
+    }
+    const int xstart = (int)(basex >> 16);
+    if (xstart >= iw && ix < 0) {
+        basex += ix;
+        --w;
+    }
+    int yend = (int)((srcy + (uint32_t)(iy * (h - 1))) >> 16);
+    if (yend < 0 || yend >= ih) --h;
+    int xend = (int)((basex + (uint32_t)(ix * (w - 1))) >> 16);
+    if (xend < 0 || xend >= iw) --w;
+    for (int yy = 0; yy < h; yy++) {
+        int srow = (int)(srcy >> 16);
+        uint32_t *drow = canvas + (ty1 + yy) * RES_W + tx1;
+        uint32_t srcx = basex;
+        for (int xx = 0; xx < w; xx++) {
+            int scol = (int)(srcx >> 16);
+            if (mirrored) scol = iw - 1 - scol;
+            qt_blend(&drow[xx], px[srow * iw + scol], fmt, const_alpha);
+            srcx += (uint32_t)ix;
+        }
+        srcy += (uint32_t)iy;
+    }
+}
+
+/* QPainter::fillRect(QRect, QColor) with an opaque color on RGB32 */
+static void qt_fill_rect_int(uint32_t *canvas, int x, int y, int w, int h, uint32_t argb) {
+    int x1 = x < 0 ? 0 : x, y1 = y < 0 ? 0 : y;
+    int x2 = x + w > RES_W ? RES_W : x + w, y2 = y + h > RES_H ? RES_H : y + h;
+    for (int yy = y1; yy < y2; yy++)
+        for (int xx = x1; xx < x2; xx++) canvas[yy * RES_W + xx] = argb | 0xff000000u;
+}
+
+/* ================================================================== render (basic-abstract-game.cpp) */
+typedef struct { double x, y, w, h; } RectD;
+
+static void prepare_for_drawing(Game *g, float rect_height) { /* :828-847 */
+    g->center_x = (float)(g->main_width * .5);
+    g->center_y = (float)(g->main_height * .5);
+    if (g->options.center_agent) {
+        Entity *agent = AG(g); /* choose_center, :673-676 */
+        g->center_x = agent->x;
+        g->center_y = agent->y;
+    } else {
+        g->visibility = (float)(g->main_width > g->main_height ? g->main_width : g->main_height);
+        if (g->visibility < g->min_visibility) g->visibility = g->min_visibility;
+    }
+    float raw_unit = 64 / g->visibility;
+    g->unit = (float)((double)raw_unit * ((double)rect_height / 64.0));
+    g->view_dim = (float)(64.0 / (double)raw_unit);
+    g->x_off = g->unit * (g->center_x - g->view_dim / 2);
+    g->y_off = g->unit * (g->center_y - g->view_dim / 2);
+}
+
+static RectD get_screen_rect(Game *g, float x, float y, float dx, float dy, float render_eps) { /* :808-810 */
+    RectD r;
+    r.x = (double)((x - render_eps) * g->unit - g->x_off);
+    r.y = (double)((g->view_dim - y - render_eps) * g->unit + g->y_off);
+    r.w = (double)((dx + 2 * render_eps) * g->unit);
+    r.h = (double)((dy + 2 * render_eps) * g->unit);
+    return r;
+}
+
+static RectD adjust_rect(RectD b, RectD a) { /* qt-utils.h:12-19 */
+    RectD r;
+    r.x = b.x + b.w * a.x;
+    r.y = b.y + b.h * a.y;
+    r.w = b.w * a.w;
+    r.h = b.h * a.h;
+    return r;
+}
+
+static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, bool is_reflected, int base_type,
+                       int theme, float alpha) { /* :886-922 (tile_ratio == 0 for coinrun) */
+    int img_type = hook_image_for_type(g, base_type);
+    if (img_type < 0) return;
+    if (g->options.use_monochrome_assets || img_type >= USE_ASSET_THRESHOLD) {
+        /* draw_grid_obj: SPACE draws nothing; monochrome fills are restated in a later round */
+        if (img_type == SPACE) return;
+        fatal_msg("draw_grid_obj / monochrome not restated yet");
+    }
+    fassert(theme < MAX_IMAGE_THEMES);
+    if (g->options.restrict_themes) theme = 0; /* mask_theme_if_necessary, :458-462 */
+    int img_idx = img_type + theme * MAX_ASSETS;
+    RectD r = base;
+    if (g->game_id == GAME_COINRUN && is_player_image(img_type)) { /* coinrun.cpp:64-70 */
+        RectD adj = {0, -.7415, 1, 1.7415};
+        r = adjust_rect(base, adj);
+    }
+    const or_image *im = &at->sprites[img_idx];
+    if (im->w <= 0) fatal_msg("missing sprite (generated assets are not restated yet)");
+    fassert(rotation == 0);
+    qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + im->offset, im->w, im->h, QFMT_ARGB32_PM, is_reflected,
+                  alpha != 1 ? (double)alpha : 1.0);
+}
+
+static void draw_entities(Game *g, const or_atlas *at, int render_z) { /* :1061-1075 */
+    for (int i = 0; i < g->num_ents; i++) {
+        Entity *e = &g->ents[i];
+        if (e->render_z != render_z) continue;
+        RectD r1;
+        if (e->use_abs_coords) {
+            fatal_msg("use_abs_coords not restated yet");
+        }
+        r1 = get_screen_rect(g, e->x - e->rx, e->y + e->ry, 2 * e->rx, 2 * e->ry, 0); /* :820-826 */
+        draw_image(g, at, r1, e->rotation, e->is_reflected, e->image_type, e->image_theme, e->alpha);
+    }
+}
+
+static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
+    qt_fill_rect_int(g->canvas, 0, 0, RES_W, RES_H, 0xff000000u);
+    prepare_for_drawing(g, 64);
+    if (!g->options.use_backgrounds) return;
+    RectD main_rect = get_screen_rect(g, 0, (float)g->main_height, (float)g->main_width, (float)g->main_height, 0);
+    const or_image *bg = &at->backgrounds[g->background_index];
+    fassert(g->bg_tile_ratio >= 0);
+    float bgw = (float)bg->w;
+    float bgh = (float)bg->h;
+    float bg_ar = bgw / bgh;
+    float world_ar = (float)(g->main_width * 1.0 / g->main_height);
+    float extra_w = bg_ar - world_ar;
+    float offset_x = g->bg_pct_x * extra_w;
+    RectD adj = {(double)(-offset_x), 0, (double)(bg_ar / world_ar), 1};
+    RectD r = adjust_rect(main_rect, adj);
+    qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0);
+}
+
+static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
+    prepare_for_drawing(g, 64);
+    draw_entities(g, at, -1);
+    int low_x, high_x, low_y, high_y;
+    if (g->options.center_agent) {
+        double margin = (double)g->visibility / 2.0 + 1;
+        low_x = (int)((double)g->center_x - margin);
+        high_x = (int)((double)g->center_x + margin);
+        low_y = (int)((double)g->center_y - margin);
+        high_y = (int)((double)g->center_y + margin);
+    } else {
+        low_x = 0;
+        high_x = g->main_width - 1;
+        low_y = 0;
+        high_y = g->main_height - 1;
+    }
+    for (int x = low_x; x <= high_x; x++) {
+        for (int y = low_y; y <= high_y; y++) {
+            int type = get_obj(g, x, y);
+            if (type == INVALID_OBJ) continue;
+            int theme = hook_theme_for_grid_obj(g, type);
+            RectD r2 = get_screen_rect(g, (float)x, (float)(y + 1), 1, 1, RENDER_EPS);
+            draw_image(g, at, r2, 0, false, type, theme, 1.0f);
+        }
+    }
+    draw_entities(g, at, 0);
+    draw_entities(g, at, 1);
+    if (g->has_useful_vel_info && g->options.paint_vel_info) fatal_msg("paint_vel_info not restated yet");
+}
+
+static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
+    draw_background(g, at);
+    draw_foreground(g, at);
+}
+
+/* ================================================================== construction (vecgame.cpp) */
+static int game_id_of(const char *name) {
+    if (strcmp(name, "coinrun") == 0) return GAME_COINRUN;
+    return -1;
+}
+
+static void basic_ctor(Game *g) { /* Game ctor game.cpp:25-39 + BasicAbstractGame ctor :22-46 */
+    g->timeout = 1000;
+    g->episodes_remaining = 0;
+    g->last_reward = -1;
+    g->default_action = 0;
+    g->reset_count = 0;
+    g->current_level_seed = 0;
+    g->sd_reward = 0;
+    g->sd_done = true;
+    g->sd_level_complete = false;
+    g->char_dim = 5;
+    g->main_width = 0;
+    g->main_height = 0;
+    g->visibility = 16;
+    g->min_visibility = 0;
+    g->mixrate = 0.5f;
+    g->maxspeed = 0.5f;
+    g->max_jump = g->maxspeed;
+    g->default_action = 4;
+    g->last_move_action = 7;
+    g->bg_tile_ratio = 0;
+    g->out_of_bounds_object = INVALID_OBJ;
+    g->has_useful_vel_info = true;
+    g->random_agent_start = true;
+}
+
+static void coinrun_ctor(Game *g) { /* coinrun.cpp:49-58 */
+    g->visibility = 13;
+    g->mixrate = 0.2f;
+    g->main_width = 64;
+    g->main_height = 64;
+    g->out_of_bounds_object = CR_WALL_MID;
+}
+
+void *oracle_make(const char *env_name, int count, int env_offset, const or_options *opt, const or_atlas *atlas) {
+    int gid = game_id_of(env_name);
+    if (gid < 0 || count <= 0) return NULL;
+    int dm = opt->distribution_mode;
+    if (!(dm == EasyMode || dm == HardMode)) return NULL; /* game.cpp:76-86 for coinrun */
+    Vec *v = (Vec *)calloc(1, sizeof(Vec));
+    v->count = count;
+    v->offset = env_offset;
+    v->atlas = atlas;
+    v->games = (Game *)calloc((size_t)count, sizeof(Game));
+    int level_seed_low = 0, level_seed_high = 0; /* vecgame.cpp:332-341 */
+    if (opt->num_levels == 0) {
+        level_seed_low = 0;
+        level_seed_high = 2147483647;
+    } else if (opt->num_levels > 0) {
+        level_seed_low = opt->start_level;
+        level_seed_high = opt->start_level + opt->num_levels;
+    }
+    MT seed_gen; /* vecgame.cpp:349-350 */
+    rg_seed(&seed_gen, opt->rand_seed);
+    for (int n = 0; n < env_offset; n++) (void)rg_randint0(&seed_gen);
+    for (int n = 0; n < count; n++) {
+        Game *g = &v->games[n];
+        g->game_id = gid;
+        g->ents = (Entity *)calloc(MAX_ENTS, sizeof(Entity));
+        basic_ctor(g);
+        coinrun_ctor(g);
+        rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
+        g->level_seed_high = level_seed_high;
+        g->level_seed_low = level_seed_low;
+        g->game_n = env_offset + n;
+        /* parse_options, game.cpp:62-95 */
+        g->options.paint_vel_info = opt->paint_vel_info;
+        g->options.use_generated_assets = false;
+        g->options.use_monochrome_assets = opt->use_monochrome_assets;
+        g->options.restrict_themes = opt->restrict_themes;
+        g->options.use_backgrounds = opt->use_backgrounds;
+        g->options.center_agent = opt->center_agent;
+        g->options.use_sequential_levels = opt->use_sequential_levels;
+        g->options.distribution_mode = dm;
+        g->options.debug_mode = opt->debug_mode;
+    }
+    return v;
+}
+
+void oracle_close(void *h) {
+    Vec *v = (Vec *)h;
+    if (!v) return;
+    for (int n = 0; n < v->count; n++) free(v->games[n].ents);
+    free(v->games);
+    free(v);
+}
+
+void oracle_start(void *h) { /* vecgame.cpp:126-131 (initial reset + observe) */
+    Vec *v = (Vec *)h;
+    for (int n = 0; n < v->count; n++) {
+        game_reset(&v->games[n], v->atlas);
+        render(&v->games[n], v->atlas);
+    }
+}
+
+void oracle_step(void *h, const int32_t *actions) {
+    Vec *v = (Vec *)h;
+    for (int n = 0; n < v->count; n++) {
+        v->games[n].action = actions[n];
+        game_step(&v->games[n], v->atlas);
+    }
+}
+
+void oracle_observe(void *h, uint8_t *rgb, float *rew, uint8_t *first, int32_t *prev_level_seed,
+                    uint8_t *prev_level_complete, int32_t *level_seed) {
+    Vec *v = (Vec *)h;
+    for (int n = 0; n < v->count; n++) {
+        Game *g = &v->games[n];
+        if (rgb) { /* bgr32_to_rgb888, game.cpp:8-23 */
+            uint8_t *d = rgb + (size_t)n * RES_W * RES_H * 3;
+            for (int p = 0; p < RES_W * RES_H; p++) {
+                uint32_t c = g->canvas[p];
+                d[3 * p + 0] = (uint8_t)(c >> 16);
+                d[3 * p + 1] = (uint8_t)(c >> 8);
+                d[3 * p + 2] = (uint8_t)c;
+            }
+        }
+        if (rew) rew[n] = g->sd_reward;
+        if (first) first[n] = (uint8_t)g->sd_done;
+        if (prev_level_seed) prev_level_seed[n] = g->prev_level_seed;
+        if (prev_level_complete) prev_level_complete[n] = (uint8_t)g->sd_level_complete;
+        if (level_seed) level_seed[n] = g->current_level_seed;
+    }
+}
+
+int oracle_debug(void *h, int i, int32_t *out, int n) {
+    Vec *v = (Vec *)h;
+    Game *g = &v->games[i];
+    Entity *a = AG(g);
+    int32_t vals[16];
+    float fv[4] = {a->x, a->y, a->vx, a->vy};
+    vals[0] = g->num_ents;
+    vals[1] = g->cur_time;
+    memcpy(&vals[2], fv, sizeof(fv));
+    vals[6] = g->background_index;
+    vals[7] = g->wall_theme;
+    vals[8] = g->step_rand_int;
+    vals[9] = g->has_support;
+    vals[10] = g->current_level_seed;
+    vals[11] = g->rand_gen.mti;
+    memcpy(&vals[12], &g->bg_pct_x, 4);
+    vals[13] = a->image_theme;
+    vals[14] = g->agent_erased;
+    vals[15] = g->reset_count;
+    int k = n < 16 ? n : 16;
+    memcpy(out, vals, (size_t)k * 4);
+    return 16;
+}
+
+/* ================================================================== pinning helpers */
+void oracle_mt_stream(uint32_t seed, uint32_t *out, int n) {
+    MT m;
+    mt_seed(&m, seed);
+    for (int i = 0; i < n; i++) out[i] = mt_next(&m);
+}
+
+/* ops: kind 0 randint(a,b) 1 randn(a) 2 rand01 (float bits) 3 randbool 4 randrange(a/8, b/8) 5 randint() */
+void oracle_randgen_script(uint32_t seed, const int32_t *ops, int nops, int32_t *out) {
+    MT m;
+    rg_seed(&m, (int)seed);
+    for (int i = 0; i < nops; i++) {
+        int k = ops[3 * i], a = ops[3 * i + 1], b = ops[3 * i + 2];
+        float f;
+        switch (k) {
+        case 0: out[i] = rg_randint(&m, a, b); break;
+        case 1: out[i] = rg_randn(&m, a); break;
+        case 2: f = rg_rand01(&m); memcpy(&out[i], &f, 4); break;
+        case 3: out[i] = rg_randbool(&m); break;
+        case 4: f = rg_randrange(&m, a / 8.0f, b / 8.0f); memcpy(&out[i], &f, 4); break;
+        default: out[i] = rg_randint0(&m); break;
+        }
+    }
+}
+
+typedef struct {
+    const uint8_t *p, *end;
+} Rd;
+static uint32_t rd_u32(Rd *r) {
+    uint32_t v;
+    if (r->p + 4 > r->end) fatal_msg("replay: short");
+    memcpy(&v, r->p, 4);
+    r->p += 4;
+    return v;
+}
+static double rd_f64(Rd *r) {
+    double v;
+    if (r->p + 8 > r->end) fatal_msg("replay: short");
+    memcpy(&v, r->p, 8);
+    r->p += 8;
+    return v;
+}
+
+/* replays ONE case body (after the canvas words) of tools/qt_raster_golden.cpp's format */
+int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas) {
+    Rd r = {cmds, cmds + nbytes};
+    uint32_t ncmds = rd_u32(&r);
+    for (uint32_t k = 0; k < ncmds; k++) {
+        uint32_t kind = rd_u32(&r);
+        double x = rd_f64(&r), y = rd_f64(&r), w = rd_f64(&r), h = rd_f64(&r);
+        double opacity = rd_f64(&r);
+        uint32_t mirrored = rd_u32(&r);
+        int32_t rot = (int32_t)rd_u32(&r);
+        if (kind == 0) {
+            uint32_t fmt = rd_u32(&r), iw = rd_u32(&r), ih = rd_u32(&r);
+            const uint32_t *px = (const uint32_t *)r.p;
+            r.p += 4 * (size_t)iw * ih;
+            if (rot != 0) return -1;
+            qt_draw_image(canvas, x, y, w, h, px, (int)iw, (int)ih, (int)fmt, mirrored != 0, opacity);
+        } else {
+            uint32_t col = rd_u32(&r);
+            if (kind == 2) qt_fill_rect_int(canvas, (int)x, (int)y, (int)w, (int)h, col);
+            else return -2;
+        }
+    }
+    return (int)(r.p - cmds);
+}

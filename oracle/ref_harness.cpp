@@ -1,0 +1,82 @@
+// Driver for the reference-source pins (TEST INFRASTRUCTURE ONLY).
+//
+// Compiled together with the reference's own, unmodified sources read in place
+// from /root/reference/procgen/src (randgen.cpp, entity.cpp, mazegen.cpp,
+// cpp-utils.cpp) by `make -C oracle ref`; output only to oracle/_ref/ (git-ignored).
+// Those translation units need neither <cheerp/client.h> nor Qt, so they build
+// from their own few files.  The rest of the reference's step path does not
+// (game.h includes <cheerp/client.h>, absent here) and is pinned differently
+// (see oracle/procgen_oracle.h).
+#include <cstdint>
+#include <cstring>
+#include "randgen.h"
+#include "entity.h"
+#include "mazegen.h"
+
+extern "C" {
+
+// successive raw 32-bit draws of the reference RandGen::randint() after seed(seed)
+void ref_mt_stream(int32_t seed, uint32_t *out, int n) {
+    RandGen r;
+    r.seed(seed);
+    for (int i = 0; i < n; i++) out[i] = (uint32_t)r.randint();
+}
+
+// same op encoding as oracle_randgen_script (procgen_oracle.c)
+void ref_randgen_script(int32_t seed, const int32_t *ops, int nops, int32_t *out) {
+    RandGen r;
+    r.seed(seed);
+    for (int i = 0; i < nops; i++) {
+        int k = ops[3 * i], a = ops[3 * i + 1], b = ops[3 * i + 2];
+        float f;
+        switch (k) {
+        case 0: out[i] = r.randint(a, b); break;
+        case 1: out[i] = r.randn(a); break;
+        case 2: f = r.rand01(); memcpy(&out[i], &f, 4); break;
+        case 3: out[i] = r.randbool(); break;
+        case 4: f = r.randrange(a / 8.0f, b / 8.0f); memcpy(&out[i], &f, 4); break;
+        default: out[i] = r.randint(); break;
+        }
+    }
+}
+
+// Entity(x, y, vx, vy, rx, ry, type) followed by `steps` Entity::step() calls;
+// fields written as 32-bit words in declaration order of the oracle's probe
+// (x, y, vx, vy, rx, ry, rotation, alpha, life_time, will_erase, image_type).
+void ref_entity_steps(const float *init, int type, int smart_step, float friction, float vrot, int expire_time,
+                      int steps, uint32_t *out) {
+    Entity e(init[0], init[1], init[2], init[3], init[4], init[5], type);
+    e.smart_step = smart_step != 0;
+    e.friction = friction;
+    e.vrot = vrot;
+    if (expire_time != 0) e.expire_time = expire_time;
+    for (int s = 0; s < steps; s++) {
+        e.step();
+        float f[8] = {e.x, e.y, e.vx, e.vy, e.rx, e.ry, e.rotation, e.alpha};
+        memcpy(out, f, 32);
+        out[8] = (uint32_t)e.life_time;
+        out[9] = (uint32_t)e.will_erase;
+        out[10] = (uint32_t)e.image_type;
+        out += 11;
+    }
+}
+
+// MazeGen: seed a RandGen, build a maze of dim `maze_dim`, run `mode`
+// (0 generate_maze, 1 generate_maze_no_dead_ends, 2 generate_maze_with_doors(num_doors)),
+// then place_objects(start_obj, num_objs) if num_objs > 0.  Writes the grid
+// (array_dim^2 ints, row-major) and returns array_dim.
+int ref_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
+                uint32_t *next_draw) {
+    RandGen r;
+    r.seed(seed);
+    MazeGen m(&r, maze_dim);
+    if (mode == 0) m.generate_maze();
+    else if (mode == 1) m.generate_maze_no_dead_ends();
+    else m.generate_maze_with_doors(num_doors);
+    if (num_objs > 0) m.place_objects(start_obj, num_objs);
+    int n = m.grid.w;
+    for (int i = 0; i < m.grid.w * m.grid.h; i++) out[i] = m.grid.data[i];
+    *next_draw = (uint32_t)r.randint();
+    return n;
+}
+}

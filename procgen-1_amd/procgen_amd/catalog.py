@@ -1,0 +1,146 @@
+"""Asset catalogue: which images each game draws, and in which order.
+
+This is DATA restated from the reference, not code: the order of every list
+below drives RNG draw counts (``choose_random_theme`` draws ``randn(#themes)``,
+reference ``procgen/src/basic-abstract-game.cpp:1047-1050``) and background
+indices (``randn(#backgrounds)``, ``basic-abstract-game.cpp:776``), so it must
+match the reference exactly.
+
+Background groups: ``procgen/src/resources.cpp:837-952``; the platform group
+gets every space background appended (``resources.cpp:972-975``) and ``caves``
+is ``platform[2, 3, 13]`` (``resources.cpp:977-979``).
+
+Per-game sprite tables: ``asset_for_type`` of each game (coinrun:
+``procgen/src/games/coinrun.cpp:72-121``) plus the reserved engine sprites
+(``basic-abstract-game.cpp:424-438``).
+"""
+
+# Image slot of an (image type, theme) pair, as in the reference
+# (``img_idx = img_type + theme * MAX_ASSETS``, basic-abstract-game.cpp:896).
+MAX_ASSETS = 100
+MAX_IMAGE_THEMES = 10
+NUM_IMAGE_SLOTS = MAX_ASSETS * MAX_IMAGE_THEMES
+
+SPACE_BACKGROUNDS = [
+    "space_backgrounds/deep_space_01.png",
+    "space_backgrounds/spacegen_01.png",
+    "space_backgrounds/milky_way_01.png",
+    "space_backgrounds/ez_space_lite_01.png",
+    "space_backgrounds/meyespace_v1_01.png",
+    "space_backgrounds/eye_nebula_01.png",
+    "space_backgrounds/deep_sky_01.png",
+    "space_backgrounds/space_nebula_01.png",
+    "space_backgrounds/Background-1.png",
+    "space_backgrounds/Background-2.png",
+    "space_backgrounds/Background-3.png",
+    "space_backgrounds/Background-4.png",
+    "space_backgrounds/parallax-space-backgound.png",
+]
+
+_PLATFORM_ONLY = (
+    ["platform_backgrounds/%s.png" % n for n in (
+        "alien_bg", "another_world_bg", "back_cave", "caverns", "cyberpunk_bg",
+        "parallax_forest", "scifi_bg", "scifi2_bg", "living_tissue_bg",
+        "airadventurelevel1", "airadventurelevel2", "airadventurelevel3",
+        "airadventurelevel4", "cave_background", "blue_desert", "blue_grass",
+        "blue_land", "blue_shroom", "colored_desert", "colored_grass",
+        "colored_land", "colored_shroom", "landscape1", "landscape2",
+        "landscape3", "landscape4")]
+    + ["platform_backgrounds/battleback%d.png" % i for i in range(1, 11)]
+    + ["platform_backgrounds/sunrise.png"]
+    + ["platform_backgrounds_2/%s%d.png" % (n, i)
+       for n in ("beach", "fantasy", "candy") for i in range(1, 5)]
+)
+
+# resources.cpp:972-975: the space backgrounds are appended to the platform group
+PLATFORM_BACKGROUNDS = _PLATFORM_ONLY + SPACE_BACKGROUNDS
+
+TOPDOWN_BACKGROUNDS = ["topdown_backgrounds/floortiles.png"] + [
+    "topdown_backgrounds/backgrounddetailed%d.png" % i for i in range(1, 9)]
+TOPDOWN_SIMPLE_BACKGROUNDS = ["topdown_backgrounds/floortiles.png"]
+WATER_BACKGROUNDS = ["water_backgrounds/water%d.png" % i for i in range(1, 5)] + [
+    "water_backgrounds/underwater%d.png" % i for i in range(1, 4)]
+WATER_SURFACE_BACKGROUNDS = ["water_backgrounds/water%d.png" % i for i in range(1, 5)]
+CAVES = [PLATFORM_BACKGROUNDS[2], PLATFORM_BACKGROUNDS[3], PLATFORM_BACKGROUNDS[13]]
+
+BACKGROUND_GROUPS = {
+    "platform": PLATFORM_BACKGROUNDS,
+    "space": SPACE_BACKGROUNDS,
+    "topdown": TOPDOWN_BACKGROUNDS,
+    "topdown_simple": TOPDOWN_SIMPLE_BACKGROUNDS,
+    "water": WATER_BACKGROUNDS,
+    "water_surface": WATER_SURFACE_BACKGROUNDS,
+    "caves": CAVES,
+}
+
+# ---------------------------------------------------------------- object ids
+# procgen/src/object-ids.h:9-27
+EXPLOSION, EXPLOSION2, EXPLOSION3, EXPLOSION4, EXPLOSION5, TRAIL = 54, 55, 56, 57, 58, 59
+
+# basic-abstract-game.cpp:424-438 (reserved engine sprites)
+RESERVED_SPRITES = {
+    EXPLOSION: ["misc_assets/explosion1.png"],
+    EXPLOSION2: ["misc_assets/explosion2.png"],
+    EXPLOSION3: ["misc_assets/explosion3.png"],
+    EXPLOSION4: ["misc_assets/explosion4.png"],
+    EXPLOSION5: ["misc_assets/explosion5.png"],
+    TRAIL: ["misc_assets/iconCircle_white.png"],
+}
+
+# ---------------------------------------------------------------- coinrun
+# procgen/src/games/coinrun.cpp:13-34
+_WALKING_ENEMIES = ["slimeBlock", "slimePurple", "slimeBlue", "slimeGreen", "mouse",
+                    "snail", "ladybug", "wormGreen", "wormPink"]
+_PLAYER_COLORS = ["Beige", "Blue", "Green", "Pink", "Yellow"]
+_GROUND_THEMES = ["Dirt", "Grass", "Planet", "Sand", "Snow", "Stone"]
+
+
+def _player(kind):
+    return ["kenney/Players/128x256/%s/alien%s_%s.png" % (c, c, kind) for c in _PLAYER_COLORS]
+
+
+COINRUN_SPRITES = {
+    0: _player("stand"),                 # PLAYER
+    9: _player("jump"),                  # PLAYER_JUMP
+    12: _player("walk1"),                # PLAYER_RIGHT1
+    13: _player("walk2"),                # PLAYER_RIGHT2
+    6: ["kenney/Enemies/%s.png" % e for e in _WALKING_ENEMIES],       # ENEMY1
+    7: ["kenney/Enemies/%s_move.png" % e for e in _WALKING_ENEMIES],  # ENEMY2
+    1: ["kenney/Items/coinGold.png"],    # GOAL
+    16: ["kenney/Ground/%s/%sMid.png" % (g, g.lower()) for g in _GROUND_THEMES],     # WALL_TOP
+    15: ["kenney/Ground/%s/%sCenter.png" % (g, g.lower()) for g in _GROUND_THEMES],  # WALL_MID
+    18: ["kenney/Tiles/lavaTop_low.png"],  # LAVA_TOP
+    17: ["kenney/Tiles/lava.png"],         # LAVA_MID
+    2: ["kenney/Enemies/sawHalf.png"],     # SAW
+    3: ["kenney/Enemies/sawHalf_move.png"],  # SAW2
+    20: ["kenney/Tiles/boxCrate.png", "kenney/Tiles/boxCrate_double.png",
+         "kenney/Tiles/boxCrate_single.png", "kenney/Tiles/boxCrate_warning.png"],  # CRATE
+}
+
+GAMES = {
+    # game name -> (sprite table, background group)
+    "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
+}
+
+# Game ids used across the C ABI (procgen/env.py:15-32 ordering).
+ENV_NAMES = [
+    "bigfish", "bossfight", "caveflyer", "chaser", "climber", "coinrun",
+    "dodgeball", "fruitbot", "heist", "jumper", "leaper", "maze", "miner",
+    "ninja", "plunder", "starpilot",
+]
+SUPPORTED_GAMES = sorted(GAMES)
+
+
+def sprite_table(game):
+    """type -> [names] for a game, engine-reserved sprites included.
+
+    The reserved list only applies where the game itself defines no sprite for
+    the type (basic-abstract-game.cpp:94-98)."""
+    table = dict(RESERVED_SPRITES)
+    table.update(GAMES[game][0])
+    return table
+
+
+def num_themes(game):
+    """asset_num_themes[type] for every type with a sprite (basic-abstract-game.cpp:113-119)."""
+    return {t: len(v) for t, v in sprite_table(game).items()}
