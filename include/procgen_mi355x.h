@@ -1,0 +1,76 @@
+/*
+ * procgen_mi355x.h -- extensions of libprocgen_mi355x.so beyond the libenv ABI.
+ *
+ * The reference loads its sprite atlas from PNG files inside libenv_make
+ * (vecgame.cpp:144-153 global_init -> images_load, resources.cpp:20-30); this
+ * build receives the decoded atlas from the host instead (procgen_upload_atlas),
+ * keeps every env's state resident in HBM, and can hand out device pointers so a
+ * consumer on the same GPU never copies observations to the host.
+ *
+ * Call order for a libenv host:  libenv_make -> procgen_upload_atlas ->
+ *   libenv_get_tensortypes -> libenv_set_buffers -> (libenv_act, libenv_observe)* -> libenv_close.
+ * Device-resident order:          libenv_make -> procgen_upload_atlas ->
+ *   procgen_start -> (procgen_act_device | procgen_act_hashed, procgen_wait)* -> libenv_close.
+ */
+#pragma once
+#include <stdint.h>
+#include "libenv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* atlas image descriptor: pixels[offset .. offset + w*h) row-major 0xAARRGGBB */
+struct pg_image {
+    uint32_t offset;
+    int32_t w, h;
+    int32_t pad;
+};
+
+/* Device pointers of the observation / reward / info tensors (row = env). */
+struct pg_device_buffers {
+    uint8_t *rgb;                /* [num_envs][64][64][3] */
+    float *rew;                  /* [num_envs] */
+    uint8_t *first;              /* [num_envs] */
+    int32_t *prev_level_seed;    /* [num_envs] */
+    uint8_t *prev_level_complete;/* [num_envs] */
+    int32_t *level_seed;         /* [num_envs] */
+    int32_t *actions;            /* [num_envs] action staging buffer read by the step kernel */
+    void *stream;                /* hipStream_t every kernel of this env is enqueued on */
+};
+
+/* Upload the decoded sprite atlas (reference: images_load + asset_for_type tables).
+ * sprites: [1000] slots (type + 100*theme), backgrounds: [num_backgrounds],
+ * num_themes: [100].  Returns 0 on success. */
+LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int64_t num_pixels,
+                                    const struct pg_image *sprites, const struct pg_image *backgrounds,
+                                    int num_backgrounds, const int32_t *num_themes);
+/* Initial reset + render of every env (what libenv_set_buffers triggers). */
+LIBENV_API int procgen_start(libenv_env *env);
+/* Step with actions already on the device (d_actions: int32[num_envs]); asynchronous. */
+LIBENV_API int procgen_act_device(libenv_env *env, const int32_t *d_actions);
+/* Step with actions generated on the device: a = splitmix64(seed ^ ((u64)global_env << 32) ^ t) % num_actions. */
+LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t);
+/* Block until every enqueued step finished (the device half of libenv_observe). */
+LIBENV_API int procgen_wait(libenv_env *env);
+LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers *out);
+/* Sticky error: 0 ok; otherwise a code (see PG_ERR_*), message via procgen_error_string. */
+LIBENV_API int procgen_last_error(libenv_env *env);
+LIBENV_API const char *procgen_error_string(libenv_env *env);
+/* Per-kernel timing of the last `n` steps measured with HIP events on the env's stream:
+ * out[0] = step kernel ms, out[1] = reset kernel ms, out[2] = render kernel ms (averages). */
+LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n);
+LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
+/* Debug read-back of one env's scalar state, see pg_engine.h PGEnv (returns bytes copied). */
+LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length);
+
+#define PG_ERR_NONE 0
+#define PG_ERR_ENTITY_OVERFLOW 1
+#define PG_ERR_BAD_OPTION 2
+#define PG_ERR_NO_ATLAS 3
+#define PG_ERR_HIP 4
+#define PG_ERR_GRID 5
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,660 @@
+// pg_capi.cpp -- the drop-in C ABI (include/libenv.h + include/procgen_mi355x.h).
+//
+// Host half of the reference's VecGame (procgen/src/vecgame.cpp): option parsing with the
+// reference's consume-once semantics (vecoptions.cpp:47-94), tensor types
+// (vecgame.cpp:212-330), level-seed derivation (vecgame.cpp:332-378), the act/observe
+// hand-off (vecgame.cpp:411-449) -- with the per-env work replaced by three HIP launches
+// per act on one stream: pg_step (all envs) -> pg_reset (queued envs) -> pg_render.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/libenv.h"
+#include "../../include/procgen_mi355x.h"
+#include "pg_engine.h"
+
+extern "C" {
+void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t);
+void pg_launch_reset(const PGDev *d, hipStream_t s, int all_envs, int grid);
+void pg_launch_render(const PGDev *d, hipStream_t s);
+}
+
+namespace {
+
+std::string g_last_make_error;
+
+// ------------------------------------------------------------------ host MT19937 (level seeds)
+struct HostMT {
+    uint32_t mt[624];
+    int mti;
+    void seed(uint32_t s) {
+        mt[0] = s;
+        for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+        mti = 624;
+    }
+    uint32_t next() {
+        if (mti >= 624) {
+            for (int i = 0; i < 624; i++) {
+                uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+                mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            mti = 0;
+        }
+        uint32_t y = mt[mti++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+};
+
+// ------------------------------------------------------------------ options (vecoptions.cpp:47-94)
+struct Options {
+    std::vector<libenv_option> items;
+    std::string error;
+    bool find(const char *name, libenv_dtype dt, libenv_option *out) {
+        for (size_t i = 0; i < items.size(); i++) {
+            if (strncmp(items[i].name, name, LIBENV_MAX_NAME_LEN) == 0) {
+                if (items[i].dtype != dt) {
+                    if (error.empty()) error = std::string("invalid dtype for option ") + name;
+                    return false;
+                }
+                *out = items[i];
+                items.erase(items.begin() + i);
+                return true;
+            }
+        }
+        return false;
+    }
+    void consume_string(const char *name, std::string *v) {
+        libenv_option o;
+        if (find(name, LIBENV_DTYPE_UINT8, &o) && o.data) *v = std::string((const char *)o.data, o.count);
+    }
+    void consume_int(const char *name, int32_t *v) {
+        libenv_option o;
+        if (find(name, LIBENV_DTYPE_INT32, &o) && o.data) *v = *(const int32_t *)o.data;
+    }
+    void consume_bool(const char *name, bool *v) {
+        libenv_option o;
+        if (find(name, LIBENV_DTYPE_UINT8, &o) && o.data) {
+            uint8_t b = *(const uint8_t *)o.data;
+            if (b != 0 && b != 1 && error.empty()) error = std::string("bool option not 0/1: ") + name;
+            *v = b != 0;
+        }
+    }
+};
+
+int game_id(const std::string &name) {
+    if (name == "coinrun") return PG_GAME_COINRUN;
+    return -1;
+}
+
+struct VecEnv {
+    int num_envs = 0;
+    int env_offset = 0;
+    int num_actions = 15;
+    bool render_human = false;
+    PGDev dev{};
+    hipStream_t stream = nullptr;
+    std::vector<libenv_tensortype> ob_types, ac_types, info_types;
+    // host buffers from libenv_set_buffers (per env pointers, reference convert_bufs layout)
+    std::vector<void *> ob_ptrs, ac_ptrs, info_ptrs;
+    float *rew_host = nullptr;
+    uint8_t *first_host = nullptr;
+    bool buffers_set = false;
+    bool atlas = false;
+    bool started = false;
+    // device allocations
+    std::vector<void *> allocs;
+    uint32_t *d_pixels = nullptr;
+    int32_t *d_sprites = nullptr, *d_bgs = nullptr, *d_themes = nullptr;
+    std::vector<int32_t> h_actions;
+    std::vector<uint8_t> h_staging;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[4] = {};
+    float t_sum[3] = {0, 0, 0};
+    int t_n = 0;
+    bool t_pending = false;
+    int error = 0;
+    std::string error_msg;
+};
+
+#define HIPCHECK(x)                                                                      \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "procgen_mi355x: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return fail(v, PG_ERR_HIP, hipGetErrorString(e_));                           \
+        }                                                                                \
+    } while (0)
+
+int fail(VecEnv *v, int code, const char *msg) {
+    if (v && !v->error) {
+        v->error = code;
+        v->error_msg = msg ? msg : "";
+    }
+    return -code;
+}
+
+template <typename T>
+int dalloc(VecEnv *v, T **p, size_t count) {
+    void *q = nullptr;
+    HIPCHECK(hipMalloc(&q, count * sizeof(T) > 0 ? count * sizeof(T) : 16));
+    HIPCHECK(hipMemsetAsync(q, 0, count * sizeof(T) > 0 ? count * sizeof(T) : 16, v->stream));
+    v->allocs.push_back(q);
+    *p = (T *)q;
+    return 0;
+}
+
+libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> shape, int lo, int hi) {
+    libenv_tensortype s;
+    memset(&s, 0, sizeof(s));
+    snprintf(s.name, sizeof(s.name), "%s", name);
+    s.scalar_type = LIBENV_SCALAR_TYPE_DISCRETE;
+    s.dtype = dt;
+    s.ndim = (int)shape.size();
+    for (size_t i = 0; i < shape.size(); i++) s.shape[i] = shape[i];
+    if (dt == LIBENV_DTYPE_UINT8) {
+        s.low.uint8 = (uint8_t)lo;
+        s.high.uint8 = (uint8_t)hi;
+    } else {
+        s.low.int32 = lo;
+        s.high.int32 = hi;
+    }
+    return s;
+}
+
+int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
+    if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
+    bool tm = v->timing;
+    if (tm && v->t_pending) {
+        // fold the previous step's timings in (events are complete once the stream passed them)
+        float a, b, c;
+        if (hipEventSynchronize(v->ev[3]) == hipSuccess && hipEventElapsedTime(&a, v->ev[0], v->ev[1]) == hipSuccess &&
+            hipEventElapsedTime(&b, v->ev[1], v->ev[2]) == hipSuccess &&
+            hipEventElapsedTime(&c, v->ev[2], v->ev[3]) == hipSuccess) {
+            v->t_sum[0] += a; v->t_sum[1] += b; v->t_sum[2] += c; v->t_n++;
+        }
+        v->t_pending = false;
+    }
+    HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t), v->stream));
+    if (tm) HIPCHECK(hipEventRecord(v->ev[0], v->stream));
+    pg_launch_step(&v->dev, v->stream, use_hash, seed, t);
+    if (tm) HIPCHECK(hipEventRecord(v->ev[1], v->stream));
+    pg_launch_reset(&v->dev, v->stream, 0, 0);
+    if (tm) HIPCHECK(hipEventRecord(v->ev[2], v->stream));
+    pg_launch_render(&v->dev, v->stream);
+    if (tm) {
+        HIPCHECK(hipEventRecord(v->ev[3], v->stream));
+        v->t_pending = true;
+    }
+    HIPCHECK(hipGetLastError());
+    return 0;
+}
+
+int copy_out(VecEnv *v) {
+    // device -> the caller's per-env host pointers (contiguous runs become one copy)
+    int n = v->num_envs;
+    auto copy_plane = [&](const void *dsrc, size_t elem, void **ptrs) -> int {
+        int e = 0;
+        while (e < n) {
+            int k = e + 1;
+            while (k < n && (char *)ptrs[k] == (char *)ptrs[k - 1] + elem) k++;
+            HIPCHECK(hipMemcpyAsync(ptrs[e], (const char *)dsrc + elem * e, elem * (k - e), hipMemcpyDeviceToHost, v->stream));
+            e = k;
+        }
+        return 0;
+    };
+    if (copy_plane(v->dev.rgb, PG_OBS_BYTES, &v->ob_ptrs[0])) return -1;
+    HIPCHECK(hipMemcpyAsync(v->rew_host, v->dev.rew, sizeof(float) * n, hipMemcpyDeviceToHost, v->stream));
+    HIPCHECK(hipMemcpyAsync(v->first_host, v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
+    if (copy_plane(v->dev.prev_level_seed, 4, &v->info_ptrs[0 * (size_t)n])) return -1;
+    if (copy_plane(v->dev.prev_level_complete, 1, &v->info_ptrs[1 * (size_t)n])) return -1;
+    if (copy_plane(v->dev.level_seed, 4, &v->info_ptrs[2 * (size_t)n])) return -1;
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    return 0;
+}
+
+int check_device_errors(VecEnv *v) {
+    int32_t flags = 0;
+    HIPCHECK(hipMemcpy(&flags, v->dev.error_any, 4, hipMemcpyDeviceToHost));
+    if (flags && !v->error) {
+        int code = __builtin_ctz((unsigned)flags);
+        const char *msg = code == PG_ERR_ENTITY_OVERFLOW ? "entity capacity exceeded"
+                          : code == PG_ERR_GRID        ? "grid write out of range"
+                                                       : "unsupported feature reached on device";
+        fail(v, code, msg);
+    }
+    return 0;
+}
+
+} // namespace
+
+extern "C" {
+
+LIBENV_API int libenv_version(void) { return LIBENV_VERSION; }
+
+LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options options) {
+    g_last_make_error.clear();
+    Options opts;
+    for (int i = 0; i < options.count; i++) opts.items.push_back(options.items[i]);
+    std::string env_name, resource_root;
+    int32_t num_levels = 0, start_level = -1, num_actions = -1, rand_seed = 0, num_threads = 4, env_offset = 0;
+    bool render_human = false;
+    // VecGame options (vecgame.cpp:183-190) + this build's shard offset
+    opts.consume_string("env_name", &env_name);
+    opts.consume_int("num_levels", &num_levels);
+    opts.consume_int("start_level", &start_level);
+    opts.consume_int("num_actions", &num_actions);
+    opts.consume_int("rand_seed", &rand_seed);
+    opts.consume_int("num_threads", &num_threads);
+    opts.consume_string("resource_root", &resource_root);
+    opts.consume_bool("render_human", &render_human);
+    opts.consume_int("env_offset", &env_offset);
+    // game options (game.cpp:62-95), consumed once for all envs
+    bool paint_vel_info = false, use_generated_assets = false, use_monochrome_assets = false,
+         restrict_themes = false, use_backgrounds = true, center_agent = false, use_sequential_levels = false,
+         use_easy_jump = false;
+    int32_t distribution_mode = PG_EASY, plain_assets = 0, physics_mode = 0, debug_mode = 0, game_type = 0;
+    opts.consume_bool("use_easy_jump", &use_easy_jump);
+    opts.consume_bool("paint_vel_info", &paint_vel_info);
+    opts.consume_bool("use_generated_assets", &use_generated_assets);
+    opts.consume_bool("use_monochrome_assets", &use_monochrome_assets);
+    opts.consume_bool("restrict_themes", &restrict_themes);
+    opts.consume_bool("use_backgrounds", &use_backgrounds);
+    opts.consume_bool("center_agent", &center_agent);
+    opts.consume_bool("use_sequential_levels", &use_sequential_levels);
+    opts.consume_int("distribution_mode", &distribution_mode);
+    opts.consume_int("plain_assets", &plain_assets);
+    opts.consume_int("physics_mode", &physics_mode);
+    opts.consume_int("debug_mode", &debug_mode);
+    opts.consume_int("game_type", &game_type);
+
+    auto bad = [&](const std::string &m) -> libenv_env * {
+        g_last_make_error = m;
+        fprintf(stderr, "procgen_mi355x: libenv_make: %s\n", m.c_str());
+        return nullptr;
+    };
+    if (!opts.error.empty()) return bad(opts.error);
+    if (!opts.items.empty()) return bad(std::string("unused options found, first unused option: ") + opts.items[0].name);
+    if (env_name.empty()) return bad("env_name missing");
+    if (num_actions <= 0) return bad("num_actions must be > 0");
+    if (num_levels < 0) return bad("num_levels must be >= 0");
+    if (start_level < 0) return bad("start_level must be >= 0");
+    if (num_envs <= 0) return bad("num_envs must be > 0");
+    if (env_name.find(',') != std::string::npos) return bad("mixed env batches are not in this build yet");
+    int gid = game_id(env_name);
+    if (gid < 0) return bad("env '" + env_name + "' is not in this build (supported: coinrun)");
+    // game.cpp:76-86 distribution mode validity
+    if (!(distribution_mode == PG_EASY || distribution_mode == PG_HARD)) return bad("invalid distribution_mode for " + env_name);
+    if (use_generated_assets) return bad("use_generated_assets is not in this build yet");
+    if (use_monochrome_assets) return bad("use_monochrome_assets is not in this build yet");
+    if (paint_vel_info) return bad("paint_vel_info is not in this build yet");
+    if (render_human) return bad("render_mode=rgb_array (render_human) is not in this build yet");
+
+    VecEnv *v = new VecEnv();
+    v->num_envs = num_envs;
+    v->env_offset = env_offset;
+    v->num_actions = num_actions;
+    v->render_human = render_human;
+    if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete v;
+        return bad("hipStreamCreate failed");
+    }
+    for (auto &e : v->ev) hipEventCreate(&e);
+
+    // spaces (vecgame.cpp:212-316)
+    v->ob_types.push_back(make_type("rgb", LIBENV_DTYPE_UINT8, {64, 64, 3}, 0, 255));
+    v->ac_types.push_back(make_type("action", LIBENV_DTYPE_INT32, {}, 0, num_actions - 1));
+    v->info_types.push_back(make_type("prev_level_seed", LIBENV_DTYPE_INT32, {}, 0, INT32_MAX));
+    v->info_types.push_back(make_type("prev_level_complete", LIBENV_DTYPE_UINT8, {}, 0, 1));
+    v->info_types.push_back(make_type("level_seed", LIBENV_DTYPE_INT32, {}, 0, INT32_MAX));
+    v->info_types.push_back(make_type("grid_size", LIBENV_DTYPE_INT32, {2}, 0, 35));
+    v->info_types.push_back(make_type("grid", LIBENV_DTYPE_INT32, {35 * 35}, 0, INT32_MAX));
+    v->info_types.push_back(make_type("agent_pos", LIBENV_DTYPE_INT32, {2}, 0, 35));
+    v->info_types.push_back(make_type("exit_pos", LIBENV_DTYPE_INT32, {2}, 0, 35));
+
+    // level seed bounds (vecgame.cpp:332-341)
+    int level_seed_low = 0, level_seed_high = 0;
+    if (num_levels == 0) {
+        level_seed_low = 0;
+        level_seed_high = INT32_MAX;
+    } else {
+        level_seed_low = start_level;
+        level_seed_high = start_level + num_levels;
+    }
+
+    size_t n = (size_t)num_envs;
+    PGDev &d = v->dev;
+    d.num_envs = num_envs;
+    d.env_offset = env_offset;
+    d.num_actions = num_actions;
+    int rc = 0;
+    rc |= dalloc(v, &d.envs, n);
+    rc |= dalloc(v, &d.ents, (size_t)PG_NF * n * PG_CAP);
+    rc |= dalloc(v, &d.grid, n * PG_GRID_MAX);
+    rc |= dalloc(v, &d.mt, n * 2 * PG_MT_WORDS);
+    rc |= dalloc(v, &d.actions, n);
+    rc |= dalloc(v, &d.rgb, n * PG_OBS_BYTES);
+    rc |= dalloc(v, &d.rew, n);
+    rc |= dalloc(v, &d.first, n);
+    rc |= dalloc(v, &d.prev_level_seed, n);
+    rc |= dalloc(v, &d.prev_level_complete, n);
+    rc |= dalloc(v, &d.level_seed, n);
+    rc |= dalloc(v, &d.reset_queue, n);
+    rc |= dalloc(v, &d.reset_count, 1);
+    rc |= dalloc(v, &d.error_any, 1);
+    if (rc) {
+        libenv_close(v);
+        return bad("device allocation failed");
+    }
+
+    // per-env construction: Game + BasicAbstractGame + CoinRun ctors (game.cpp:25-39,
+    // basic-abstract-game.cpp:22-46, coinrun.cpp:49-58) and level-seed generator seeding
+    // from rand_seed's MT, global env index n taking the n-th draw (vecgame.cpp:349-362)
+    std::vector<PGEnv> h(n);
+    std::vector<uint32_t> hmt(n * 2 * PG_MT_WORDS, 0);
+    HostMT seed_gen;
+    seed_gen.seed((uint32_t)rand_seed);
+    for (int k = 0; k < env_offset; k++) (void)seed_gen.next();
+    for (size_t e = 0; e < n; e++) {
+        PGEnv &s = h[e];
+        memset(&s, 0, sizeof(s));
+        s.game_id = gid;
+        s.timeout = 1000;
+        s.episodes_remaining = 0;
+        s.last_reward = -1;
+        s.reset_count = 0;
+        s.current_level_seed = 0;
+        s.sd_reward = 0;
+        s.sd_done = 1;
+        s.sd_level_complete = 0;
+        s.char_dim = 5;
+        s.visibility = 16;
+        s.min_visibility = 0;
+        s.mixrate = 0.5f;
+        s.maxspeed = 0.5f;
+        s.max_jump = s.maxspeed;
+        s.default_action = 4;
+        s.last_move_action = 7;
+        s.bg_tile_ratio = 0;
+        s.out_of_bounds_object = -1;
+        s.has_useful_vel_info = 1;
+        s.random_agent_start = 1;
+        // coinrun ctor
+        s.visibility = 13;
+        s.mixrate = 0.2f;
+        s.main_width = 64;
+        s.main_height = 64;
+        s.out_of_bounds_object = 15; // WALL_MID
+        s.level_seed_low = level_seed_low;
+        s.level_seed_high = level_seed_high;
+        s.game_n = env_offset + (int)e;
+        s.opt_distribution_mode = distribution_mode;
+        s.opt_center_agent = center_agent;
+        s.opt_use_backgrounds = use_backgrounds;
+        s.opt_restrict_themes = restrict_themes;
+        s.opt_use_sequential_levels = use_sequential_levels;
+        s.opt_debug_mode = debug_mode;
+        s.opt_paint_vel_info = paint_vel_info;
+        s.opt_use_monochrome_assets = use_monochrome_assets;
+        s.rg_mti = PG_MT_N;
+        HostMT lsg;
+        lsg.seed(seed_gen.next());
+        memcpy(&hmt[(e * 2 + 1) * PG_MT_WORDS], lsg.mt, sizeof(lsg.mt));
+        s.lsg_mti = lsg.mti;
+    }
+    if (hipMemcpyAsync(d.envs, h.data(), sizeof(PGEnv) * n, hipMemcpyHostToDevice, v->stream) != hipSuccess ||
+        hipMemcpyAsync(d.mt, hmt.data(), hmt.size() * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess ||
+        hipStreamSynchronize(v->stream) != hipSuccess) {
+        libenv_close(v);
+        return bad("device upload failed");
+    }
+    v->h_actions.assign(n, 0);
+    return (libenv_env *)v;
+}
+
+LIBENV_API int libenv_get_tensortypes(libenv_env *env, enum libenv_space_name name, struct libenv_tensortype *out) {
+    VecEnv *v = (VecEnv *)env;
+    const std::vector<libenv_tensortype> *t;
+    if (name == LIBENV_SPACE_OBSERVATION) t = &v->ob_types;
+    else if (name == LIBENV_SPACE_ACTION) t = &v->ac_types;
+    else if (name == LIBENV_SPACE_INFO) t = &v->info_types;
+    else return 0;
+    if (out) memcpy(out, t->data(), t->size() * sizeof(libenv_tensortype));
+    return (int)t->size();
+}
+
+LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int64_t num_pixels,
+                                    const struct pg_image *sprites, const struct pg_image *backgrounds,
+                                    int num_backgrounds, const int32_t *num_themes) {
+    VecEnv *v = (VecEnv *)env;
+    if (num_backgrounds <= 0 || num_backgrounds > PG_MAX_BG) return fail(v, PG_ERR_NO_ATLAS, "bad background count");
+    if (dalloc(v, &v->d_pixels, (size_t)num_pixels) || dalloc(v, &v->d_sprites, PG_NUM_SLOTS * 4) ||
+        dalloc(v, &v->d_bgs, (size_t)num_backgrounds * 4) || dalloc(v, &v->d_themes, 100))
+        return -PG_ERR_HIP;
+    HIPCHECK(hipMemcpy(v->d_pixels, pixels, (size_t)num_pixels * 4, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(v->d_sprites, sprites, PG_NUM_SLOTS * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(v->d_bgs, backgrounds, (size_t)num_backgrounds * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(v->d_themes, num_themes, 100 * 4, hipMemcpyHostToDevice));
+    v->dev.pixels = v->d_pixels;
+    v->dev.sprites = v->d_sprites;
+    v->dev.backgrounds = v->d_bgs;
+    v->dev.num_backgrounds = num_backgrounds;
+    v->dev.num_themes = v->d_themes;
+    v->atlas = true;
+    return 0;
+}
+
+LIBENV_API int procgen_start(libenv_env *env) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
+    if (v->started) return 0;
+    pg_launch_reset(&v->dev, v->stream, 1, 0);
+    pg_launch_render(&v->dev, v->stream);
+    HIPCHECK(hipGetLastError());
+    v->started = true;
+    return 0;
+}
+
+LIBENV_API void libenv_set_buffers(libenv_env *env, struct libenv_buffers *bufs) {
+    VecEnv *v = (VecEnv *)env;
+    size_t n = (size_t)v->num_envs;
+    v->ob_ptrs.assign(bufs->ob, bufs->ob + v->ob_types.size() * n);
+    v->ac_ptrs.assign(bufs->ac, bufs->ac + v->ac_types.size() * n);
+    v->info_ptrs.assign(bufs->info, bufs->info + v->info_types.size() * n);
+    v->rew_host = bufs->rew;
+    v->first_host = bufs->first;
+    v->buffers_set = true;
+    // latent-state info tensors (grid_size, grid, agent_pos, exit_pos) are only filled by
+    // maze/miner (maze.cpp:152-165, miner.cpp:378-396); zero them for this game
+    for (size_t k = 3; k < v->info_types.size(); k++) {
+        size_t bytes = 4;
+        for (int dd = 0; dd < v->info_types[k].ndim; dd++) bytes *= (size_t)v->info_types[k].shape[dd];
+        for (size_t e = 0; e < n; e++) memset(v->info_ptrs[k * n + e], 0, bytes);
+    }
+    if (procgen_start(env) == 0) copy_out(v);
+}
+
+LIBENV_API void libenv_act(libenv_env *env) {
+    VecEnv *v = (VecEnv *)env;
+    size_t n = (size_t)v->num_envs;
+    for (size_t e = 0; e < n; e++) v->h_actions[e] = *(const int32_t *)v->ac_ptrs[e];
+    if (hipMemcpyAsync(v->dev.actions, v->h_actions.data(), n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess) {
+        fail(v, PG_ERR_HIP, "action upload failed");
+        return;
+    }
+    launch_step(v, 0, 0, 0);
+}
+
+LIBENV_API void libenv_observe(libenv_env *env) {
+    VecEnv *v = (VecEnv *)env;
+    if (v->buffers_set) copy_out(v);
+    else hipStreamSynchronize(v->stream);
+    check_device_errors(v);
+}
+
+LIBENV_API void libenv_close(libenv_env *env) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v) return;
+    if (v->stream) hipStreamSynchronize(v->stream);
+    for (void *p : v->allocs) hipFree(p);
+    for (auto &e : v->ev)
+        if (e) hipEventDestroy(e);
+    if (v->stream) hipStreamDestroy(v->stream);
+    delete v;
+}
+
+LIBENV_API int procgen_act_device(libenv_env *env, const int32_t *d_actions) {
+    VecEnv *v = (VecEnv *)env;
+    if (d_actions != v->dev.actions)
+        HIPCHECK(hipMemcpyAsync(v->dev.actions, d_actions, (size_t)v->num_envs * 4, hipMemcpyDeviceToDevice, v->stream));
+    return launch_step(v, 0, 0, 0);
+}
+
+LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t) {
+    return launch_step((VecEnv *)env, 1, seed, t);
+}
+
+LIBENV_API int procgen_wait(libenv_env *env) {
+    VecEnv *v = (VecEnv *)env;
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    check_device_errors(v);
+    return v->error ? -v->error : 0;
+}
+
+LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers *out) {
+    VecEnv *v = (VecEnv *)env;
+    out->rgb = v->dev.rgb;
+    out->rew = v->dev.rew;
+    out->first = v->dev.first;
+    out->prev_level_seed = v->dev.prev_level_seed;
+    out->prev_level_complete = v->dev.prev_level_complete;
+    out->level_seed = v->dev.level_seed;
+    out->actions = v->dev.actions;
+    out->stream = (void *)v->stream;
+    return 0;
+}
+
+LIBENV_API int procgen_last_error(libenv_env *env) {
+    if (!env) return g_last_make_error.empty() ? 0 : PG_ERR_BAD_OPTION;
+    return ((VecEnv *)env)->error;
+}
+
+LIBENV_API const char *procgen_error_string(libenv_env *env) {
+    if (!env) return g_last_make_error.c_str();
+    return ((VecEnv *)env)->error_msg.c_str();
+}
+
+LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
+    VecEnv *v = (VecEnv *)env;
+    v->timing = enabled != 0;
+    v->t_sum[0] = v->t_sum[1] = v->t_sum[2] = 0;
+    v->t_n = 0;
+    v->t_pending = false;
+    return 0;
+}
+
+LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
+    VecEnv *v = (VecEnv *)env;
+    if (v->t_pending) {
+        float a, b, c;
+        hipEventSynchronize(v->ev[3]);
+        if (hipEventElapsedTime(&a, v->ev[0], v->ev[1]) == hipSuccess &&
+            hipEventElapsedTime(&b, v->ev[1], v->ev[2]) == hipSuccess &&
+            hipEventElapsedTime(&c, v->ev[2], v->ev[3]) == hipSuccess) {
+            v->t_sum[0] += a; v->t_sum[1] += b; v->t_sum[2] += c; v->t_n++;
+        }
+        v->t_pending = false;
+    }
+    for (int i = 0; i < n && i < 3; i++) out[i] = v->t_n ? v->t_sum[i] / v->t_n : 0.f;
+    return v->t_n;
+}
+
+LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length) {
+    VecEnv *v = (VecEnv *)env;
+    if (env_idx < 0 || env_idx >= v->num_envs || length < (int)sizeof(PGEnv)) return -1;
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    HIPCHECK(hipMemcpy(out, v->dev.envs + env_idx, sizeof(PGEnv), hipMemcpyDeviceToHost));
+    return (int)sizeof(PGEnv);
+}
+
+// ---- get_state / set_state (vecgame.cpp:485-505): this build's own snapshot format
+// [u32 magic][u32 version][PGEnv][num_ents x PG_NF words][grid cells int16][2 x 625 mt words][END]
+static const uint32_t STATE_MAGIC = 0x50474d33u; // "PGM3"
+static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
+
+LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
+    VecEnv *v = (VecEnv *)env;
+    if (env_idx < 0 || env_idx >= v->num_envs) return -1;
+    if (hipStreamSynchronize(v->stream) != hipSuccess) return -1;
+    PGEnv s;
+    if (hipMemcpy(&s, v->dev.envs + env_idx, sizeof(s), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    size_t ents = (size_t)s.num_ents;
+    size_t cells = (size_t)s.main_width * s.main_height;
+    size_t need = 8 + sizeof(PGEnv) + ents * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    if ((size_t)length < need) return -1;
+    char *p = data;
+    memcpy(p, &STATE_MAGIC, 4); p += 4;
+    uint32_t ver = 1; memcpy(p, &ver, 4); p += 4;
+    memcpy(p, &s, sizeof(s)); p += sizeof(s);
+    size_t plane = (size_t)v->num_envs * PG_CAP;
+    for (int f = 0; f < PG_NF; f++) {
+        if (ents && hipMemcpy(p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        p += ents * 4;
+    }
+    if (cells && hipMemcpy(p, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, cells * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    p += cells * 2;
+    if (hipMemcpy(p, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, 2 * PG_MT_WORDS * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    p += 2 * PG_MT_WORDS * 4;
+    memcpy(p, &END_OF_BUFFER, 4); p += 4;
+    return (int)(p - data);
+}
+
+LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) {
+    VecEnv *v = (VecEnv *)env;
+    if (env_idx < 0 || env_idx >= v->num_envs || length < (int)(8 + sizeof(PGEnv) + 4)) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: bad arguments");
+        return;
+    }
+    hipStreamSynchronize(v->stream);
+    const char *p = data;
+    uint32_t magic, ver;
+    memcpy(&magic, p, 4); p += 4;
+    memcpy(&ver, p, 4); p += 4;
+    PGEnv s;
+    memcpy(&s, p, sizeof(s)); p += sizeof(s);
+    size_t ents = (size_t)s.num_ents, cells = (size_t)s.main_width * s.main_height;
+    size_t need = 8 + sizeof(PGEnv) + ents * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    int32_t end = 0;
+    if (magic != STATE_MAGIC || ver != 1 || (size_t)length < need || ents > PG_CAP || cells > PG_GRID_MAX) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: not a state of this build");
+        return;
+    }
+    memcpy(&end, data + need - 4, 4);
+    if (end != END_OF_BUFFER) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: missing END_OF_BUFFER");
+        return;
+    }
+    size_t plane = (size_t)v->num_envs * PG_CAP;
+    hipMemcpy(v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
+    for (int f = 0; f < PG_NF; f++) {
+        if (ents) hipMemcpy(v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);
+        p += ents * 4;
+    }
+    if (cells) hipMemcpy(v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
+    p += cells * 2;
+    hipMemcpy(v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, p, 2 * PG_MT_WORDS * 4, hipMemcpyHostToDevice);
+    // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
+    // harmless (render is a pure function of state)
+    pg_launch_render(&v->dev, v->stream);
+    hipStreamSynchronize(v->stream);
+}
+
+} // extern "C"

@@ -1,0 +1,206 @@
+// pg_device.h -- device-side helpers shared by the step / reset / render kernels.
+//
+// Execution model: one 64-lane wavefront per env (64-thread workgroups, so
+// __syncthreads() is a single-wave barrier).  Game logic runs wave-uniform (every
+// lane computes the same value, uniform state updates are stored by all lanes with
+// the same value, so every later read of that word is a same-lane read); entity
+// scans, entity updates, compaction, grid fills and pixel work run lane-parallel
+// (lane = entity slot / cell / pixel), followed by a barrier before any other lane
+// reads what they wrote.
+//
+// Floating point follows the reference's C++ promotion rules operation by
+// operation; the build uses -ffp-contract=off so no mul+add is fused.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pg_engine.h"
+
+#define DEV __device__ __forceinline__
+#define LANE ((int)threadIdx.x)
+
+// ------------------------------------------------------------------ reference constants
+// object-ids.h:9-27
+#define INVALID_OBJ (-1)
+#define PLAYER 0
+#define SPACE 100
+#define WALL_OBJ 51
+#define EXPLOSION 54
+#define EXPLOSION5 58
+#define TRAIL 59
+// basic-abstract-game.cpp:6-20
+#define POS_EPS (-0.001f)
+#define RENDER_EPS 0.02f
+#define MIXRATEROT 0.5f
+#define USE_ASSET_THRESHOLD 100
+#define MAX_ASSETS 100
+// coinrun.cpp:13-30
+#define CR_GOAL 1
+#define CR_SAW 2
+#define CR_SAW2 3
+#define CR_ENEMY 5
+#define CR_ENEMY1 6
+#define CR_ENEMY2 7
+#define CR_PLAYER_JUMP 9
+#define CR_PLAYER_RIGHT1 12
+#define CR_PLAYER_RIGHT2 13
+#define CR_WALL_MID 15
+#define CR_WALL_TOP 16
+#define CR_LAVA_MID 17
+#define CR_LAVA_TOP 18
+#define CR_ENEMY_BARRIER 19
+#define CR_CRATE 20
+
+DEV bool cr_is_wall(int t) { return t == CR_WALL_MID || t == CR_WALL_TOP; }
+DEV bool cr_is_lava(int t) { return t == CR_LAVA_MID || t == CR_LAVA_TOP; }
+
+DEV void wave_sync() { __syncthreads(); }
+
+DEV unsigned long long ballot(bool p) { return __ballot(p); }
+DEV int top_bit(unsigned long long m) { return 63 - __clzll(m); }
+
+// ------------------------------------------------------------------ MT19937 (std::mt19937)
+DEV uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+// In-place twist of 624 words in LDS.  Ascending 64-word chunks, each read-then-write:
+// word i reads i+1 (not yet rewritten) and (i+397)%624, which for i >= 227 is a word
+// rewritten >= 163 positions earlier, i.e. in an earlier chunk -- exactly the
+// sequential generator's data flow.
+DEV void mt_twist_lds(uint32_t *mt) {
+    for (int base = 0; base < PG_MT_N; base += 64) {
+        int i = base + LANE;
+        uint32_t nv = 0;
+        if (i < PG_MT_N) {
+            uint32_t a = mt[i], b = mt[(i + 1) % PG_MT_N], c = mt[(i + 397) % PG_MT_N];
+            uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+            nv = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        wave_sync();
+        if (i < PG_MT_N) mt[i] = nv;
+        wave_sync();
+    }
+}
+
+// std::mersenne_twister_engine::seed(s) into LDS (serial recurrence, uniform)
+DEV void mt_seed_lds(uint32_t *mt, uint32_t s) {
+    uint32_t x = s;
+    if (LANE == 0) mt[0] = x;
+    for (int i = 1; i < PG_MT_N; i++) {
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+        if (LANE == (i & 63)) mt[i] = x;
+    }
+    wave_sync();
+}
+
+// Generator whose words live in HBM (`g`, 624 words) with its position in *mti:
+// one uniform load per draw; the rare twist is staged through LDS.
+DEV uint32_t mt_next_global(uint32_t *g, int32_t &mti, uint32_t *lds) {
+    uint32_t y;
+    if (mti >= PG_MT_N) {
+        for (int i = LANE; i < PG_MT_N; i += 64) lds[i] = g[i];
+        wave_sync();
+        mt_twist_lds(lds);
+        for (int i = LANE; i < PG_MT_N; i += 64) g[i] = lds[i];
+        y = lds[0];
+        mti = 1;
+        wave_sync();
+    } else {
+        y = g[mti];
+        mti += 1;
+    }
+    return mt_temper(y);
+}
+
+// Generator resident in LDS
+DEV uint32_t mt_next_lds(uint32_t *lds, int32_t &mti) {
+    if (mti >= PG_MT_N) {
+        mt_twist_lds(lds);
+        mti = 0;
+    }
+    uint32_t y = lds[mti];
+    mti += 1;
+    return mt_temper(y);
+}
+
+// RandGen helpers over a raw draw (randgen.cpp:6-23)
+DEV int rg_randint_of(uint32_t x, int low, int high) {
+    uint32_t range = (uint32_t)high - (uint32_t)low;
+    return (int)((uint32_t)low + (x % range));
+}
+DEV int rg_randn_of(uint32_t x, int high) { return (int)(x % (uint32_t)high); }
+DEV float rg_rand01_of(uint32_t x) { return (float)((double)x / ((double)0xffffffffu + 1)); }
+
+// ------------------------------------------------------------------ Qt raster restatement
+// qRound / qFloor / qCeil (qglobal.h) and the scale blit of qblendfunctions_p.h
+// (qt_scale_image_32bit), as pinned by tests/golden/qt_raster_goldens.npz.
+DEV int qRound(double d) {
+    return d >= 0.0 ? (int)(d + 0.5) : (int)(d - (double)((int)(d - 1)) + 0.5) + (int)(d - 1);
+}
+
+DEV uint32_t BYTE_MUL(uint32_t x, uint32_t a) {
+    uint32_t t = (x & 0xff00ffu) * a;
+    t = (t + ((t >> 8) & 0xff00ffu) + 0x800080u) >> 8;
+    t &= 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a;
+    x = (x + ((x >> 8) & 0xff00ffu) + 0x800080u);
+    x &= 0xff00ff00u;
+    return x | t;
+}
+
+// SourceOver of a premultiplied ARGB32 texel with painter opacity `const_alpha` (0..256)
+DEV uint32_t blend_argb_pm(uint32_t dst, uint32_t src, int const_alpha) {
+    if (const_alpha == 256) return src + BYTE_MUL(dst, (~src) >> 24);
+    uint32_t a = (uint32_t)(const_alpha * 255) >> 8;
+    uint32_t s = BYTE_MUL(src, a);
+    return s + BYTE_MUL(dst, (~s) >> 24);
+}
+
+DEV int qt_int_opacity(double o) {
+    if (o < 0) o = 0;
+    if (o > 1) o = 1;
+    return (int)(o * 256);
+}
+
+// Geometry of QPainter::drawImage(QRectF(rx,ry,rw,rh), image iw x ih) on the 64x64 device.
+struct Blit {
+    int tx1, ty1, w, h;
+    uint32_t basex, srcy;
+    int ix, iy;
+};
+
+DEV bool qt_blit_setup(double rx, double ry, double rw, double rh, int iw, int ih, Blit &b) {
+    if (!(rw > 0) || !(rh > 0) || iw <= 0 || ih <= 0) return false; // QRectF::isEmpty
+    // qt_mapRect_non_normalizing(r, identity) == QRectF(topLeft, bottomRight)
+    double t_w = (rx + rw) - rx, t_h = (ry + rh) - ry;
+    double t_right = rx + t_w, t_bottom = ry + t_h;
+    double sx = t_w / (double)iw, sy = t_h / (double)ih;
+    int ix = (int)(65536.0 / sx);
+    int iy = (int)(65536.0 / sy);
+    int tx1 = qRound(rx), tx2 = qRound(t_right), ty1 = qRound(ry), ty2 = qRound(t_bottom);
+    if (tx2 < tx1) { int t = tx2; tx2 = tx1; tx1 = t; }
+    if (ty2 < ty1) { int t = ty2; ty2 = ty1; ty1 = t; }
+    if (tx1 < 0) tx1 = 0;
+    if (tx2 >= PG_RES) tx2 = PG_RES;
+    if (tx1 >= tx2) return false;
+    if (ty1 < 0) ty1 = 0;
+    if (ty2 >= PG_RES) ty2 = PG_RES;
+    if (ty1 >= ty2) return false;
+    int h = ty2 - ty1, w = tx2 - tx1;
+    uint32_t basex = (uint32_t)((int)ceil((tx1 + 0.5 - rx) * ix) - 1);
+    uint32_t srcy = (uint32_t)((int)ceil((ty1 + 0.5 - ry) * iy) - 1);
+    if ((int)(srcy >> 16) >= ih && iy < 0) { srcy += iy; --h; }
+    if ((int)(basex >> 16) >= iw && ix < 0) { basex += ix; --w; }
+    int yend = (int)((srcy + (uint32_t)(iy * (h - 1))) >> 16);
+    if (yend < 0 || yend >= ih) --h;
+    int xend = (int)((basex + (uint32_t)(ix * (w - 1))) >> 16);
+    if (xend < 0 || xend >= iw) --w;
+    if (w <= 0 || h <= 0) return false;
+    b.tx1 = tx1; b.ty1 = ty1; b.w = w; b.h = h; b.basex = basex; b.srcy = srcy; b.ix = ix; b.iy = iy;
+    return true;
+}

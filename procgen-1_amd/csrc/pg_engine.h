@@ -1,0 +1,158 @@
+// pg_engine.h -- HBM layout of the MI355X Procgen engine (shared by kernels and host glue).
+//
+// One env = one wavefront.  Per-env state lives in HBM, resident across steps:
+//   PGEnv        per-env scalars (Game + BasicAbstractGame + per-game members), 512 B
+//   entity SoA   PG_NF field planes, each [num_envs][PG_CAP] (lane = entity slot)
+//   grid         int16 [num_envs][PG_GRID_MAX] (row-major y*w+x, reference grid.h:14-79)
+//   mt           uint32 [num_envs][2][PG_MT_WORDS] (rand_gen, level_seed_rand_gen)
+// Field and member names follow the reference (game.h, basic-abstract-game.h,
+// entity.h, games/coinrun.cpp).
+#pragma once
+#include <stdint.h>
+
+#define PG_RES 64
+#define PG_OBS_BYTES (64 * 64 * 3)
+#define PG_CAP 512            // entity slots per env (coinrun worst case < 400)
+#define PG_GRID_MAX (64 * 64) // largest world (coinrun, ninja 64x64)
+#define PG_MT_N 624
+#define PG_MT_WORDS 625       // 624 state words + index
+#define PG_NUM_SLOTS 1000     // image slots: type + 100 * theme
+#define PG_MAX_BG 64
+
+enum PGGame { PG_GAME_COINRUN = 5 };
+
+// error codes (mirrored in include/procgen_mi355x.h)
+#ifndef PG_ERR_NONE
+#define PG_ERR_NONE 0
+#define PG_ERR_ENTITY_OVERFLOW 1
+#define PG_ERR_BAD_OPTION 2
+#define PG_ERR_NO_ATLAS 3
+#define PG_ERR_HIP 4
+#define PG_ERR_GRID 5
+#endif
+
+// reference DistributionMode (game.h:34-39)
+enum { PG_EASY = 0, PG_HARD = 1, PG_EXTREME = 2, PG_MEMORY = 10 };
+
+// entity flag bits (entity.h bools)
+enum {
+    EF_WILL_ERASE = 1,
+    EF_COLLIDES = 2,
+    EF_REFLECTED = 4,
+    EF_ABS_COORDS = 8,
+    EF_SMART_STEP = 16,
+    EF_AVOIDS = 32,
+    EF_AUTO_ERASE = 64,
+};
+
+// entity field planes
+enum {
+    F_X, F_Y, F_VX, F_VY, F_RX, F_RY,
+    F_ROTATION, F_VROT, F_ALPHA, F_ALPHA_DECAY, F_GROW_RATE, F_FRICTION,
+    F_COLLISION_MARGIN, F_HEALTH, F_THETA, F_CLIMBER_SPAWN_X,
+    F_TYPE, F_IMAGE_TYPE, F_IMAGE_THEME, F_RENDER_Z,
+    F_LIFE_TIME, F_EXPIRE_TIME, F_FIRE_TIME, F_SPAWN_TIME,
+    F_FLAGS,
+    PG_NF
+};
+
+struct PGEnv {
+    // ---- Game (game.h:64-134)
+    int32_t game_id;
+    int32_t action;
+    int32_t cur_time;
+    int32_t timeout;
+    int32_t current_level_seed;
+    int32_t prev_level_seed;
+    int32_t episodes_remaining;
+    int32_t episode_done;
+    int32_t last_reward_timer;
+    float last_reward;
+    int32_t default_action;
+    int32_t reset_count;
+    float total_reward;
+    float sd_reward;          // step_data
+    int32_t sd_done;
+    int32_t sd_level_complete;
+    int32_t level_seed_low;
+    int32_t level_seed_high;
+    int32_t game_n;
+    // ---- options (GameOptions, game.h:47-61)
+    int32_t opt_distribution_mode;
+    int32_t opt_center_agent;
+    int32_t opt_use_backgrounds;
+    int32_t opt_restrict_themes;
+    int32_t opt_use_sequential_levels;
+    int32_t opt_debug_mode;
+    int32_t opt_paint_vel_info;
+    int32_t opt_use_monochrome_assets;
+    // ---- BasicAbstractGame (basic-abstract-game.h:128-176)
+    int32_t num_ents;
+    int32_t agent_erased;
+    int32_t background_index;
+    float bg_pct_x;
+    float bg_tile_ratio;
+    int32_t last_move_action;
+    int32_t move_action;
+    int32_t special_action;
+    float mixrate;
+    float maxspeed;
+    float max_jump;
+    float action_vx;
+    float action_vy;
+    float action_vrot;
+    float visibility;
+    float min_visibility;
+    int32_t main_width;
+    int32_t main_height;
+    int32_t out_of_bounds_object;
+    int32_t step_rand_int;
+    int32_t grid_step;
+    int32_t random_agent_start;
+    int32_t has_useful_vel_info;
+    float char_dim;
+    // ghost of the agent after erase_if_needed removed it (shared_ptr keeps it alive in the reference)
+    float ghost_x, ghost_y, ghost_vx, ghost_vy, ghost_rx, ghost_ry;
+    // ---- coinrun (coinrun.cpp:38-47)
+    float last_agent_y;
+    int32_t wall_theme;
+    int32_t has_support;
+    int32_t facing_right;
+    int32_t is_on_crate;
+    float gravity;
+    float air_control;
+    // ---- bookkeeping
+    int32_t rg_mti;           // rand_gen position (mt words live in the mt plane)
+    int32_t lsg_mti;          // level_seed_rand_gen position
+    int32_t error;            // PG_ERR_* of this env (sticky)
+    int32_t pad[128 - 67];
+};
+
+static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
+
+// Everything a kernel needs, passed by value.
+struct PGDev {
+    int32_t num_envs;
+    int32_t env_offset;       // global index of env 0 (multi-GPU shard)
+    int32_t num_actions;
+    PGEnv *envs;
+    float *ents;              // PG_NF planes of num_envs * PG_CAP words (int planes reinterpret)
+    int16_t *grid;            // num_envs * PG_GRID_MAX
+    uint32_t *mt;             // num_envs * 2 * PG_MT_WORDS
+    int32_t *actions;         // num_envs
+    uint8_t *rgb;             // num_envs * PG_OBS_BYTES
+    float *rew;
+    uint8_t *first;
+    int32_t *prev_level_seed;
+    uint8_t *prev_level_complete;
+    int32_t *level_seed;
+    int32_t *reset_queue;     // [num_envs] env ids needing a reset this step
+    int32_t *reset_count;     // [1]
+    int32_t *error_any;       // [1] OR of all env errors
+    // atlas
+    const uint32_t *pixels;
+    const int32_t *sprites;   // [PG_NUM_SLOTS][4] (offset, w, h, pad)
+    const int32_t *backgrounds; // [num_bg][4]
+    int32_t num_backgrounds;
+    const int32_t *num_themes;  // [100]
+};

@@ -1,0 +1,603 @@
+// pg_step.hip -- per-env step kernel: Game::step + BasicAbstractGame::game_step + coinrun
+// game_step (reference game.cpp:136-171, basic-abstract-game.cpp:602-765, 1095-1159,
+// games/coinrun.cpp:123-211, 451-498).  One wavefront per env; done envs are queued for
+// pg_reset (level generation) and every env is then drawn by pg_render.
+#include "pg_device.h"
+
+namespace {
+
+struct Ctx {
+    PGDev d;
+    int env;
+    PGEnv s;        // uniform copy of this env's scalars
+    float *E;       // entity planes
+    size_t plane;   // num_envs * PG_CAP
+    size_t eb;      // env * PG_CAP
+    const int16_t *G; // this env's grid
+    uint32_t *lds;  // 624-word twist staging
+};
+
+DEV float &EF(Ctx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
+DEV int &EI(Ctx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
+
+// A whole entity held in registers (uniform).
+struct Ent {
+    float x, y, vx, vy, rx, ry, rotation, vrot, alpha, alpha_decay, grow_rate, friction;
+    float collision_margin, health, theta, climber_spawn_x;
+    int type, image_type, image_theme, render_z, life_time, expire_time, fire_time, spawn_time, flags;
+};
+
+DEV void load_ent(Ctx &c, int i, Ent &e) {
+    e.x = EF(c, F_X, i); e.y = EF(c, F_Y, i); e.vx = EF(c, F_VX, i); e.vy = EF(c, F_VY, i);
+    e.rx = EF(c, F_RX, i); e.ry = EF(c, F_RY, i); e.rotation = EF(c, F_ROTATION, i); e.vrot = EF(c, F_VROT, i);
+    e.alpha = EF(c, F_ALPHA, i); e.alpha_decay = EF(c, F_ALPHA_DECAY, i); e.grow_rate = EF(c, F_GROW_RATE, i);
+    e.friction = EF(c, F_FRICTION, i); e.collision_margin = EF(c, F_COLLISION_MARGIN, i);
+    e.health = EF(c, F_HEALTH, i); e.theta = EF(c, F_THETA, i); e.climber_spawn_x = EF(c, F_CLIMBER_SPAWN_X, i);
+    e.type = EI(c, F_TYPE, i); e.image_type = EI(c, F_IMAGE_TYPE, i); e.image_theme = EI(c, F_IMAGE_THEME, i);
+    e.render_z = EI(c, F_RENDER_Z, i); e.life_time = EI(c, F_LIFE_TIME, i); e.expire_time = EI(c, F_EXPIRE_TIME, i);
+    e.fire_time = EI(c, F_FIRE_TIME, i); e.spawn_time = EI(c, F_SPAWN_TIME, i); e.flags = EI(c, F_FLAGS, i);
+}
+
+DEV void store_ent(Ctx &c, int i, const Ent &e) {
+    EF(c, F_X, i) = e.x; EF(c, F_Y, i) = e.y; EF(c, F_VX, i) = e.vx; EF(c, F_VY, i) = e.vy;
+    EF(c, F_RX, i) = e.rx; EF(c, F_RY, i) = e.ry; EF(c, F_ROTATION, i) = e.rotation; EF(c, F_VROT, i) = e.vrot;
+    EF(c, F_ALPHA, i) = e.alpha; EF(c, F_ALPHA_DECAY, i) = e.alpha_decay; EF(c, F_GROW_RATE, i) = e.grow_rate;
+    EF(c, F_FRICTION, i) = e.friction; EF(c, F_COLLISION_MARGIN, i) = e.collision_margin;
+    EF(c, F_HEALTH, i) = e.health; EF(c, F_THETA, i) = e.theta; EF(c, F_CLIMBER_SPAWN_X, i) = e.climber_spawn_x;
+    EI(c, F_TYPE, i) = e.type; EI(c, F_IMAGE_TYPE, i) = e.image_type; EI(c, F_IMAGE_THEME, i) = e.image_theme;
+    EI(c, F_RENDER_Z, i) = e.render_z; EI(c, F_LIFE_TIME, i) = e.life_time; EI(c, F_EXPIRE_TIME, i) = e.expire_time;
+    EI(c, F_FIRE_TIME, i) = e.fire_time; EI(c, F_SPAWN_TIME, i) = e.spawn_time; EI(c, F_FLAGS, i) = e.flags;
+}
+
+// Entity::step (entity.cpp:57-82)
+DEV void entity_step(Ent &e) {
+    if (!(e.flags & EF_SMART_STEP)) {
+        e.x += e.vx;
+        e.y += e.vy;
+    }
+    e.rotation += e.vrot;
+    e.vx *= e.friction;
+    e.vy *= e.friction;
+    e.life_time += 1;
+    if (e.expire_time > 0 && e.life_time > e.expire_time) e.flags |= EF_WILL_ERASE;
+    if (e.type == EXPLOSION) {
+        if (e.image_type < EXPLOSION5) e.image_type++;
+    }
+    e.rx *= e.grow_rate;
+    e.ry *= e.grow_rate;
+    e.alpha = e.alpha_decay * e.alpha;
+}
+
+// ------------------------------------------------------------------ grid queries (basic-abstract-game.cpp:167-185)
+DEV int get_obj(Ctx &c, int x, int y) {
+    if (!(0 <= y && y < c.s.main_height && 0 <= x && x < c.s.main_width)) return c.s.out_of_bounds_object;
+    return c.G[y * c.s.main_width + x];
+}
+DEV int get_obj_from_floats(Ctx &c, float i, float j) {
+    if (i < 0) return c.s.out_of_bounds_object;
+    if (j < 0) return c.s.out_of_bounds_object;
+    return get_obj(c, (int)floorf(i), (int)floorf(j));
+}
+
+// ------------------------------------------------------------------ per-game hooks (coinrun)
+DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coinrun.cpp:204-211
+    if (target == WALL_OBJ) return true;
+    if (target == c.s.out_of_bounds_object) return true;
+    if (src_type == PLAYER && cr_is_wall(target)) return true;
+    return false;
+}
+DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142
+    return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+}
+
+struct AgentView { float x, y, vx, vy, rx, ry; };
+
+// coinrun.cpp:187-202 ; `agent` is the current agent state (registers if it is the stepped object)
+DEV bool is_blocked_ents(Ctx &c, int src_type, int t_type, float t_y, float t_ry, bool is_h, const AgentView &agent) {
+    if (t_type == CR_CRATE && !is_h) {
+        if (agent.vy >= 0) return false;
+        if (c.s.action_vy < 0) return false;
+        if (c.s.last_agent_y < (t_y + t_ry + agent.ry)) return false;
+        c.s.is_on_crate = 1;
+        return true;
+    }
+    return is_blocked(c, src_type, t_type);
+}
+
+DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
+    AgentView a;
+    if (oi == 0) {
+        a.x = o.x; a.y = o.y; a.vx = o.vx; a.vy = o.vy; a.rx = o.rx; a.ry = o.ry;
+    } else {
+        a.x = EF(c, F_X, 0); a.y = EF(c, F_Y, 0); a.vx = EF(c, F_VX, 0); a.vy = EF(c, F_VY, 0);
+        a.rx = EF(c, F_RX, 0); a.ry = EF(c, F_RY, 0);
+    }
+    return a;
+}
+
+// ------------------------------------------------------------------ collision scan
+// Largest index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
+// basic-abstract-game.cpp:345-354 (reverse iteration), lane-parallel in 64-slot chunks.
+DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
+    for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+        int i = base + LANE;
+        bool hit = false;
+        if (i < upper && i != oi) {
+            int fl = EI(c, F_FLAGS, i);
+            if (!(fl & EF_WILL_ERASE)) {
+                float tx = (o.rx + EF(c, F_RX, i)) + POS_EPS;
+                float ty = (o.ry + EF(c, F_RY, i)) + POS_EPS;
+                hit = (fabsf(o.x - EF(c, F_X, i)) < tx) && (fabsf(o.y - EF(c, F_Y, i)) < ty);
+            }
+        }
+        unsigned long long m = ballot(hit);
+        if (m) return base + top_bit(m);
+    }
+    return -1;
+}
+
+DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
+
+template <int D>
+DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy);
+
+// basic-abstract-game.cpp:248-276 (target is always the stepped object)
+template <int D>
+DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
+    float sx = EF(c, F_X, src), sy = EF(c, F_Y, src);
+    float rsum = is_h ? (EF(c, F_RX, src) + o.rx) : (EF(c, F_RY, src) + o.ry);
+    float delx = o.x - sx;
+    float dely = o.y - sy;
+    float t_vx = 0, t_vy = 0;
+    if (is_h) t_vx = (float)((double)sx + dsign(delx) * (double)rsum - (double)o.x);
+    else t_vy = (float)((double)sy + dsign(dely) * (double)rsum - (double)o.y);
+    if constexpr (D < 5) (void)sub_step<D + 1>(c, oi, o, t_vx, t_vy);
+    if (is_h) o.vx = 0;
+    else o.vy = 0;
+}
+
+// basic-abstract-game.cpp:278-380
+template <int D>
+DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
+    if (o.flags & EF_WILL_ERASE) return false;
+    float ny = o.y + _vy;
+    float nx = o.x + _vx;
+    const float margin = 0.98f;
+    bool is_h = _vx != 0;
+    bool block = false, reflect = false;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
+            block = block || is_blocked(c, o.type, type2);
+            reflect = reflect || will_reflect(o.type, type2);
+        }
+    }
+    if (reflect) {
+        if (is_h) {
+            float delta;
+            if (_vx < 0) delta = ceilf(nx - o.rx) - (nx - o.rx);
+            else delta = floorf(nx + o.rx) - (nx + o.rx);
+            o.vx = -1 * o.vx;
+            nx = nx + 2 * delta;
+        } else {
+            float delta;
+            if (_vy < 0) delta = ceilf(ny - o.ry) - (ny - o.ry);
+            else delta = floorf(ny + o.ry) - (ny + o.ry);
+            o.vy = -1 * o.vy;
+            ny = ny + 2 * delta;
+        }
+    } else if (block) {
+        if (is_h) {
+            if (c.s.grid_step) nx = o.x;
+            else nx = _vx > 0 ? (floorf(nx + o.rx) - o.rx) : (ceilf(nx - o.rx) + o.rx);
+        } else {
+            if (c.s.grid_step) ny = o.y;
+            else ny = _vy > 0 ? (floorf(ny + o.ry) - o.ry) : (ceilf(ny - o.ry) + o.ry);
+        }
+    }
+    o.x = nx;
+    o.y = ny;
+    bool block2 = false;
+    int upper = c.s.num_ents;
+    while (true) {
+        int m = next_collider(c, oi, upper, o);
+        if (m < 0) break;
+        upper = m;
+        int mtype = EI(c, F_TYPE, m);
+        bool curr_block = false;
+        AgentView av = agent_view(c, oi, o);
+        if (is_blocked_ents(c, o.type, mtype, EF(c, F_Y, m), EF(c, F_RY, m), is_h, av)) {
+            curr_block = true;
+        } else if (will_reflect(o.type, mtype)) {
+            if (is_h) {
+                float delx = EF(c, F_X, m) - o.x;
+                float rsum = EF(c, F_RX, m) + o.rx;
+                o.x += _vx > 0 ? -2 * (rsum - delx) : 2 * (rsum + delx);
+                o.vx = -1 * o.vx;
+            } else {
+                float dely = EF(c, F_Y, m) - o.y;
+                float rsum = EF(c, F_RY, m) + o.ry;
+                o.y += _vy > 0 ? -2 * (rsum - dely) : 2 * (rsum + dely);
+                o.vy = -1 * o.vy;
+            }
+        }
+        if (curr_block) push_obj<D>(c, m, oi, o, is_h);
+        block2 = block2 || curr_block;
+    }
+    return block || block2;
+}
+
+// basic-abstract-game.cpp:602-665
+DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
+    if (o.flags & EF_WILL_ERASE) return;
+    int num_sub_steps;
+    if (c.s.grid_step) {
+        num_sub_steps = 1;
+    } else {
+        num_sub_steps = (int)(4 * sqrt((double)(o.vx * o.vx + o.vy * o.vy)));
+        if (num_sub_steps < 4) num_sub_steps = 4;
+    }
+    float pct = (float)(1.0 / num_sub_steps);
+    float cmp = fabsf(o.vx) - fabsf(o.vy);
+    bool step_x_first = cmp == 0 ? c.s.step_rand_int % 2 == 0 : (cmp > 0);
+    if (o.type == PLAYER) {
+        if (c.s.action_vx != 0) step_x_first = true;
+        if (c.s.action_vy != 0) step_x_first = false;
+    }
+    float vx_pct = 0, vy_pct = 0;
+    for (int s = 0; s < num_sub_steps; s++) {
+        bool block_x, block_y;
+        if (step_x_first) {
+            block_x = sub_step<0>(c, oi, o, o.vx * pct, 0);
+            block_y = sub_step<0>(c, oi, o, 0, o.vy * pct);
+        } else {
+            block_y = sub_step<0>(c, oi, o, 0, o.vy * pct);
+            block_x = sub_step<0>(c, oi, o, o.vx * pct, 0);
+        }
+        if (!block_x) vx_pct += 1;
+        if (!block_y) vy_pct += 1;
+        if (block_x && block_y) break;
+    }
+    vx_pct = vx_pct / (float)num_sub_steps;
+    vy_pct = vy_pct / (float)num_sub_steps;
+    o.vx *= vx_pct;
+    o.vy *= vy_pct;
+}
+
+// basic-abstract-game.cpp:1095-1107: reverse order; runs of non-smart entities are
+// independent (Entity::step touches only its own entity) and are stepped lane-parallel
+// with slot i always owned by lane i % 64.
+DEV void step_entities(Ctx &c) {
+    int hi = c.s.num_ents - 1;
+    while (hi >= 0) {
+        int sm = -1;
+        for (int base = hi & ~63; base >= 0; base -= 64) {
+            int i = base + LANE;
+            bool smart = i <= hi && (EI(c, F_FLAGS, i) & EF_SMART_STEP);
+            unsigned long long m = ballot(smart);
+            if (m) {
+                sm = base + top_bit(m);
+                break;
+            }
+        }
+        for (int base = (sm + 1) & ~63; base <= hi; base += 64) {
+            int i = base + LANE;
+            if (i > sm && i <= hi) {
+                Ent e;
+                load_ent(c, i, e);
+                entity_step(e);
+                store_ent(c, i, e);
+            }
+        }
+        wave_sync();
+        if (sm < 0) break;
+        Ent o;
+        load_ent(c, sm, o);
+        basic_step_object(c, sm, o);
+        entity_step(o);
+        store_ent(c, sm, o);
+        wave_sync();
+        hi = sm - 1;
+    }
+}
+
+DEV bool is_out_of_bounds(Ctx &c, float x, float y, float rx, float ry) { // :1077-1093
+    if (x + rx < 0) return true;
+    if (y + ry < 0) return true;
+    if (x - rx > c.s.main_width) return true;
+    if (y - ry > c.s.main_height) return true;
+    return false;
+}
+
+// basic-abstract-game.cpp:757-765: order-preserving removal, lane-parallel compaction
+DEV void erase_if_needed(Ctx &c) {
+    int n = c.s.num_ents;
+    if (n > 0 && !c.s.agent_erased) {
+        // the reference's `agent` shared_ptr outlives its removal from `entities`
+        Ent a;
+        load_ent(c, 0, a);
+        bool er = (a.flags & EF_WILL_ERASE) || ((a.flags & EF_AUTO_ERASE) && is_out_of_bounds(c, a.x, a.y, a.rx, a.ry));
+        if (er) {
+            c.s.agent_erased = 1;
+            c.s.ghost_x = a.x; c.s.ghost_y = a.y; c.s.ghost_vx = a.vx; c.s.ghost_vy = a.vy;
+            c.s.ghost_rx = a.rx; c.s.ghost_ry = a.ry;
+        }
+    }
+    int kept = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        bool keep = false;
+        Ent e;
+        if (i < n) {
+            load_ent(c, i, e);
+            bool er = (e.flags & EF_WILL_ERASE) ||
+                      ((e.flags & EF_AUTO_ERASE) && is_out_of_bounds(c, e.x, e.y, e.rx, e.ry));
+            keep = !er;
+        }
+        unsigned long long km = ballot(keep);
+        int dst = kept + __popcll(km & ((1ull << LANE) - 1ull));
+        wave_sync();
+        if (keep && dst != i) store_ent(c, dst, e);
+        wave_sync();
+        kept += __popcll(km);
+    }
+    c.s.num_ents = kept;
+}
+
+// ------------------------------------------------------------------ agent control (coinrun)
+DEV void set_action_xy(Ctx &c, int move_action) { // coinrun.cpp:451-472
+    c.s.action_vx = (float)(move_action / 3 - 1);
+    c.s.action_vy = (float)((move_action % 3) - 1);
+    if (c.s.action_vx > 0) c.s.facing_right = 1;
+    if (c.s.action_vx < 0) c.s.facing_right = 0;
+    float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0), avy = EF(c, F_VY, 0);
+    int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+    int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+    bool s1 = cr_is_wall(b1) || b1 == c.s.out_of_bounds_object;
+    bool s2 = cr_is_wall(b2) || b2 == c.s.out_of_bounds_object;
+    c.s.has_support = (c.s.is_on_crate || s1 || s2) && avy == 0;
+    c.s.is_on_crate = 0;
+    if (c.s.action_vy == 1) {
+        if (!c.s.has_support) c.s.action_vy = 0;
+    }
+}
+
+DEV float clip_abs(float x, float y) {
+    if (x > y) return y;
+    if (x < -y) return -y;
+    return x;
+}
+
+DEV void update_agent_velocity(Ctx &c) { // coinrun.cpp:156-173
+    float vx = EF(c, F_VX, 0), vy = EF(c, F_VY, 0);
+    float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
+    vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
+    if (fabsf(vx) < mixrate_x * c.s.maxspeed) vx = 0;
+    if (c.s.action_vy > 0) {
+        vy = c.s.max_jump;
+    } else {
+        if (c.s.has_support) vy = (float)((double)vy + .2 * (double)c.s.action_vy);
+    }
+    if (!(c.s.has_support && c.s.action_vy > 0)) {
+        vy -= c.s.gravity;
+        vy = clip_abs(vy, c.s.max_jump);
+    }
+    EF(c, F_VX, 0) = vx;
+    EF(c, F_VY, 0) = vy;
+}
+
+// ------------------------------------------------------------------ game_step
+DEV void coinrun_game_step(Ctx &c) {
+    // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
+    uint32_t *rg = c.d.mt + (size_t)c.env * 2 * PG_MT_WORDS;
+    c.s.step_rand_int = rg_randint_of(mt_next_global(rg, c.s.rg_mti, c.lds), 0, 1000000);
+    c.s.move_action = c.s.action % 9;
+    c.s.special_action = 0;
+    if (c.s.action >= 9) {
+        c.s.special_action = c.s.action - 8;
+        c.s.move_action = 4;
+    }
+    if (c.s.move_action != 4) c.s.last_move_action = c.s.move_action;
+    c.s.action_vrot = 0;
+    c.s.action_vx = 0;
+    c.s.action_vy = 0;
+    set_action_xy(c, c.s.move_action);
+    if (c.s.grid_step) {
+        EF(c, F_VX, 0) = c.s.action_vx;
+        EF(c, F_VY, 0) = c.s.action_vy;
+    } else {
+        update_agent_velocity(c);
+        float vrot = EF(c, F_VROT, 0);
+        vrot = MIXRATEROT * vrot;
+        vrot += MIXRATEROT * (15 * 3.14159265358979323846264338327950288f / 180) * c.s.action_vrot;
+        EF(c, F_VROT, 0) = vrot;
+    }
+    wave_sync();
+    step_entities(c);
+
+    // agent / entity collisions (:728-750).  coinrun effects are order-free flags:
+    // ENEMY or SAW touching the agent ends the episode; only the agent reacts to grid cells.
+    {
+        float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+        bool any = false, unsupported = false;
+        for (int base = 0; base < c.s.num_ents; base += 64) {
+            int i = base + LANE;
+            bool hit = false;
+            if (i < c.s.num_ents) {
+                int t = EI(c, F_TYPE, i);
+                if (t != PLAYER) {
+                    float mrg = EF(c, F_COLLISION_MARGIN, i);
+                    float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
+                    bool col = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
+                    hit = col && (t == CR_ENEMY || t == CR_SAW);
+                }
+                if (EI(c, F_FLAGS, i) & EF_COLLIDES) unsupported = true;
+            }
+            any = any || ballot(hit) != 0;
+            unsupported = unsupported || ballot(unsupported) != 0;
+        }
+        if (any) c.s.sd_done = 1;
+        if (unsupported) c.s.error = PG_ERR_BAD_OPTION;
+        // check_grid_collisions(agent) (:145-165 -> coinrun.cpp:144-154); other smart
+        // entities (enemies) have no grid-collision effect in coinrun.
+        int min_x = (int)(ax - (arx + POS_EPS));
+        int max_x = (int)(ax + (arx + POS_EPS));
+        int min_y = (int)(ay - (ary + POS_EPS));
+        int max_y = (int)(ay + (ary + POS_EPS));
+        for (int x = min_x; x <= max_x; x++) {
+            for (int y = min_y; y <= max_y; y++) {
+                int t = get_obj_from_floats(c, (float)x, (float)y);
+                if (t == SPACE) continue;
+                if (t == CR_GOAL) {
+                    c.s.sd_reward += 10.0f;
+                    c.s.sd_done = 1;
+                    c.s.sd_level_complete = 1;
+                } else if (cr_is_lava(t)) {
+                    c.s.sd_done = 1;
+                }
+            }
+        }
+    }
+    erase_if_needed(c);
+    float gx, gy, grx, gry;
+    if (c.s.agent_erased) {
+        gx = c.s.ghost_x; gy = c.s.ghost_y; grx = c.s.ghost_rx; gry = c.s.ghost_ry;
+    } else {
+        gx = EF(c, F_X, 0); gy = EF(c, F_Y, 0); grx = EF(c, F_RX, 0); gry = EF(c, F_RY, 0);
+    }
+    c.s.sd_done = c.s.sd_done || is_out_of_bounds(c, gx, gy, grx, gry);
+
+    // ---- coinrun game_step tail (coinrun.cpp:474-498)
+    if (!c.s.agent_erased) {
+        int fl = EI(c, F_FLAGS, 0);
+        if (c.s.action_vx > 0) fl &= ~EF_REFLECTED;
+        if (c.s.action_vx < 0) fl |= EF_REFLECTED;
+        EI(c, F_FLAGS, 0) = fl;
+    }
+    wave_sync();
+    int n = c.s.num_ents;
+    // enemies (reverse order) each append a trail; trail k belongs to the k-th enemy from the top
+    int total_enemies = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        total_enemies += __popcll(ballot(i < n && EI(c, F_TYPE, i) == CR_ENEMY));
+    }
+    if (n + total_enemies > PG_CAP) {
+        c.s.error = PG_ERR_ENTITY_OVERFLOW;
+        total_enemies = 0;
+    }
+    int above = 0; // enemies at indices greater than the current chunk
+    for (int base = (n - 1) & ~63; base >= 0 && total_enemies > 0; base -= 64) {
+        int i = base + LANE;
+        int t = i < n ? EI(c, F_TYPE, i) : -1;
+        unsigned long long em = ballot(t == CR_ENEMY);
+        if (t == CR_ENEMY) {
+            int rank = above + __popcll(em >> LANE) - 1; // enemies at >= i in this chunk, minus self
+            int ti = n + rank;
+            float ex = EF(c, F_X, i);
+            float ey = (float)((double)EF(c, F_Y, i) - (double)EF(c, F_RY, i) * .5);
+            // Entity(x, y, 0, 0.01f, 0.3f, 0.2f, TRAIL) (entity.cpp:8-47) + expire_time 8, alpha .5
+            EF(c, F_X, ti) = ex; EF(c, F_Y, ti) = ey; EF(c, F_VX, ti) = 0; EF(c, F_VY, ti) = 0.01f;
+            EF(c, F_RX, ti) = 0.3f; EF(c, F_RY, ti) = 0.2f; EF(c, F_ROTATION, ti) = 0; EF(c, F_VROT, ti) = 0;
+            EF(c, F_ALPHA, ti) = .5f; EF(c, F_ALPHA_DECAY, ti) = 0.8f; EF(c, F_GROW_RATE, ti) = 1.05f;
+            EF(c, F_FRICTION, ti) = 1; EF(c, F_COLLISION_MARGIN, ti) = 0; EF(c, F_HEALTH, ti) = 1;
+            EF(c, F_THETA, ti) = -100; EF(c, F_CLIMBER_SPAWN_X, ti) = 0;
+            EI(c, F_TYPE, ti) = TRAIL; EI(c, F_IMAGE_TYPE, ti) = TRAIL; EI(c, F_IMAGE_THEME, ti) = 0;
+            EI(c, F_RENDER_Z, ti) = 0; EI(c, F_LIFE_TIME, ti) = 0; EI(c, F_EXPIRE_TIME, ti) = 8;
+            EI(c, F_FIRE_TIME, ti) = -1; EI(c, F_SPAWN_TIME, ti) = -1; EI(c, F_FLAGS, ti) = EF_AUTO_ERASE;
+            EI(c, F_IMAGE_TYPE, i) = c.s.cur_time / 5 % 2 == 0 ? CR_ENEMY1 : CR_ENEMY2;
+            int fl = EI(c, F_FLAGS, i);
+            if (EF(c, F_VX, i) > 0) fl |= EF_REFLECTED;
+            else fl &= ~EF_REFLECTED;
+            EI(c, F_FLAGS, i) = fl;
+        } else if (t == CR_SAW) {
+            EI(c, F_IMAGE_TYPE, i) = c.s.cur_time % 2 == 0 ? CR_SAW : CR_SAW2;
+        }
+        above += __popcll(em);
+    }
+    if (total_enemies == 0) { // saws still animate when there is no enemy
+        for (int base = 0; base < n; base += 64) {
+            int i = base + LANE;
+            if (i < n && EI(c, F_TYPE, i) == CR_SAW) EI(c, F_IMAGE_TYPE, i) = c.s.cur_time % 2 == 0 ? CR_SAW : CR_SAW2;
+        }
+    }
+    c.s.num_ents = n + total_enemies;
+    wave_sync();
+    c.s.last_agent_y = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+}
+
+// splitmix64 counter hash used for synthetic random actions (bench / parity tests)
+DEV uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+} // namespace
+
+// Game::step (game.cpp:136-171) minus reset (queued) and observe (pg_render).
+extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use_hash, uint64_t hash_seed, int32_t hash_t) {
+    __shared__ uint32_t lds_mt[PG_MT_N];
+    Ctx c;
+    c.d = d;
+    c.env = blockIdx.x;
+    c.s = d.envs[c.env];
+    c.E = d.ents;
+    c.plane = (size_t)d.num_envs * PG_CAP;
+    c.eb = (size_t)c.env * PG_CAP;
+    c.G = d.grid + (size_t)c.env * PG_GRID_MAX;
+    c.lds = lds_mt;
+
+    int action;
+    if (use_hash) {
+        uint64_t g = (uint64_t)(uint32_t)(d.env_offset + c.env);
+        action = (int)(splitmix64(hash_seed ^ (g << 32) ^ (uint64_t)(uint32_t)hash_t) % (uint64_t)d.num_actions);
+        if (LANE == 0) d.actions[c.env] = action;
+    } else {
+        action = d.actions[c.env];
+    }
+    c.s.action = action;
+
+    c.s.cur_time += 1;
+    bool will_force_reset = false;
+    if (c.s.action == -1) {
+        c.s.action = c.s.default_action;
+        will_force_reset = true;
+    }
+    c.s.sd_reward = 0;
+    c.s.sd_done = 0;
+    c.s.sd_level_complete = 0;
+    coinrun_game_step(c);
+    c.s.sd_done = c.s.sd_done || will_force_reset || (c.s.cur_time >= c.s.timeout);
+    c.s.total_reward += c.s.sd_reward;
+    if (c.s.sd_reward != 0) {
+        c.s.last_reward_timer = 10;
+        c.s.last_reward = c.s.sd_reward;
+    }
+    c.s.prev_level_seed = c.s.current_level_seed;
+    bool done = c.s.sd_done;
+    bool first = done;
+    if (c.s.opt_use_sequential_levels && c.s.sd_level_complete) first = false;
+    c.s.episode_done = first;
+
+    if (LANE == 0) {
+        if (done) {
+            int q = atomicAdd(d.reset_count, 1);
+            d.reset_queue[q] = c.env;
+        }
+        d.rew[c.env] = c.s.sd_reward;
+        d.first[c.env] = (uint8_t)first;
+        d.prev_level_seed[c.env] = c.s.prev_level_seed;
+        d.prev_level_complete[c.env] = (uint8_t)c.s.sd_level_complete;
+        d.level_seed[c.env] = c.s.current_level_seed;
+        if (c.s.error) atomicOr(d.error_any, 1 << c.s.error);
+        d.envs[c.env] = c.s;
+    }
+}
+
+extern "C" void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t) {
+    hipLaunchKernelGGL(pg_step_kernel, dim3(d->num_envs), dim3(64), 0, s, *d, use_hash, seed, t);
+}

@@ -1,0 +1,295 @@
+"""``ProcgenGym3Env`` over the MI355X engine -- same constructor, options and
+act/observe/get_info/callmethod surface as the reference (procgen/env.py:90-290),
+without the gym3 dependency (absent here): the libenv C ABI is driven directly
+through ctypes (procgen_amd/_lib.py).
+
+Two modes:
+* host mode (default, the reference's contract): observations land in numpy buffers
+  after every ``observe()`` (a device->host copy per step);
+* device mode (``device_buffers=True``): observations stay in HBM; ``device_ptrs()``
+  exposes them and ``act_hashed`` steps with on-device synthetic actions.
+"""
+import ctypes
+import random
+
+import numpy as np
+
+from . import _lib
+from .assets import atlas_for
+
+MAX_STATE_SIZE = 2 ** 20  # procgen/env.py:13
+
+ENV_NAMES = [
+    "bigfish", "bossfight", "caveflyer", "chaser", "climber", "coinrun", "dodgeball", "fruitbot",
+    "heist", "jumper", "leaper", "maze", "miner", "ninja", "plunder", "starpilot",
+]
+
+# procgen/env.py:51-60
+EXPLORATION_LEVEL_SEEDS = {
+    "coinrun": 1949448038, "caveflyer": 1259048185, "leaper": 1318677581, "jumper": 1434825276,
+    "maze": 158988835, "heist": 876640971, "climber": 1561126160, "ninja": 1123500215,
+}
+
+# procgen/env.py:64-70
+DISTRIBUTION_MODE_DICT = {"easy": 0, "hard": 1, "extreme": 2, "memory": 10, "exploration": 20}
+
+# procgen/env.py:179-196
+COMBOS = [("LEFT", "DOWN"), ("LEFT",), ("LEFT", "UP"), ("DOWN",), (), ("UP",), ("RIGHT", "DOWN"), ("RIGHT",),
+          ("RIGHT", "UP"), ("D",), ("A",), ("W",), ("S",), ("Q",), ("E",)]
+
+
+def create_random_seed():  # procgen/env.py:73-82 (no mpi4py here)
+    return random.SystemRandom().randint(0, 2 ** 31 - 1)
+
+
+class Discrete:
+    def __init__(self, n):
+        self.n = n
+
+
+class TensorType:
+    def __init__(self, shape, eltype):
+        self.shape = tuple(shape)
+        self.eltype = eltype
+
+
+class ProcgenError(RuntimeError):
+    pass
+
+
+def _check(lib, handle, rc=0):
+    err = lib.procgen_last_error(handle)
+    if rc < 0 or err:
+        msg = lib.procgen_error_string(handle)
+        raise ProcgenError("procgen_mi355x error %d: %s" % (err or -rc, msg.decode() if msg else ""))
+
+
+class BaseProcgenEnv:
+    """procgen/env.py:87-227 over libprocgen_mi355x.so."""
+
+    def __init__(self, num, env_name, options, debug=False, rand_seed=None, num_levels=0, start_level=0,
+                 use_sequential_levels=False, debug_mode=0, resource_root=None, num_threads=4, render_mode=None,
+                 device_buffers=False, env_offset=0):
+        lib = _lib.load()
+        self._lib = lib
+        if render_mode is None:
+            render_human = False
+        elif render_mode == "rgb_array":
+            render_human = True
+        else:
+            raise Exception(f"invalid render mode {render_mode}")
+        if rand_seed is None:
+            rand_seed = create_random_seed()
+        self.combos = self.get_combos()
+        options = dict(options)
+        options.update({
+            "env_name": env_name,
+            "num_levels": num_levels,
+            "start_level": start_level,
+            "num_actions": len(self.combos),
+            "use_sequential_levels": bool(use_sequential_levels),
+            "debug_mode": debug_mode,
+            "rand_seed": rand_seed,
+            "num_threads": num_threads,
+            "render_human": render_human,
+        })
+        if resource_root is not None:
+            options["resource_root"] = resource_root
+        if env_offset:
+            options["env_offset"] = int(env_offset)
+        self.options = options
+        self.num = num
+        self.env_name = env_name
+        opts = _lib.OptionList(options)
+        self._handle = lib.libenv_make(num, opts.struct)
+        if not self._handle:
+            msg = lib.procgen_error_string(None)
+            raise ProcgenError("libenv_make failed: %s" % (msg.decode() if msg else "unknown"))
+        atlas = atlas_for(env_name)
+        self._atlas = atlas
+        rc = lib.procgen_upload_atlas(self._handle, atlas.pixels.ctypes.data, atlas.pixels.size,
+                                      atlas.sprites.ctypes.data, atlas.backgrounds.ctypes.data,
+                                      atlas.backgrounds.shape[0], atlas.num_themes.ctypes.data)
+        _check(lib, self._handle, rc)
+
+        self.ob_types = self._types(_lib.SPACE_OBSERVATION)
+        self.ac_types = self._types(_lib.SPACE_ACTION)
+        self.info_types = self._types(_lib.SPACE_INFO)
+        act = self.ac_types[0]
+        self.ac_space = TensorType((), Discrete(act[3] + 1))
+        self.ob_space = {"rgb": TensorType(self.ob_types[0][2], Discrete(256))}
+        self.device_buffers = device_buffers
+        if device_buffers:
+            rc = lib.procgen_start(self._handle)
+            _check(lib, self._handle, rc)
+            self._dev = _lib.pg_device_buffers()
+            lib.procgen_device_buffers(self._handle, ctypes.byref(self._dev))
+        else:
+            self._alloc_host_buffers()
+
+    # ------------------------------------------------------------------ buffers
+    def _types(self, space):
+        lib = self._lib
+        n = lib.libenv_get_tensortypes(self._handle, space, None)
+        arr = (_lib.libenv_tensortype * n)()
+        lib.libenv_get_tensortypes(self._handle, space, arr)
+        out = []
+        for t in arr:
+            shape = tuple(t.shape[i] for i in range(t.ndim))
+            hi = t.high.uint8 if t.dtype == _lib.DTYPE_UINT8 else t.high.int32
+            out.append((t.name.decode(), _lib.NP_DTYPE[t.dtype], shape, hi))
+        return out
+
+    def _alloc_host_buffers(self):
+        n = self.num
+        self._ob = {name: np.zeros((n,) + shape, dtype=dt) for name, dt, shape, _ in self.ob_types}
+        self._ac = {name: np.zeros((n,) + shape, dtype=dt) for name, dt, shape, _ in self.ac_types}
+        self._info = {name: np.zeros((n,) + shape, dtype=dt) for name, dt, shape, _ in self.info_types}
+        self._rew = np.zeros(n, dtype=np.float32)
+        self._first = np.zeros(n, dtype=np.uint8)
+
+        def ptrs(bufs, types):
+            arr = (ctypes.c_void_p * (len(types) * n))()
+            for s, (name, dt, shape, _) in enumerate(types):
+                b = bufs[name]
+                stride = b.strides[0]
+                for e in range(n):
+                    arr[s * n + e] = b.ctypes.data + e * stride
+            return arr
+
+        self._ob_ptrs = ptrs(self._ob, self.ob_types)
+        self._ac_ptrs = ptrs(self._ac, self.ac_types)
+        self._info_ptrs = ptrs(self._info, self.info_types)
+        bufs = _lib.libenv_buffers(self._ob_ptrs, self._ac_ptrs, self._info_ptrs, self._rew.ctypes.data,
+                                   self._first.ctypes.data)
+        self._lib.libenv_set_buffers(self._handle, ctypes.byref(bufs))
+        _check(self._lib, self._handle)
+
+    # ------------------------------------------------------------------ gym3 surface
+    def get_combos(self):
+        return list(COMBOS)
+
+    def keys_to_act(self, keys_list):  # procgen/env.py:198-221
+        result = []
+        for keys in keys_list:
+            action, max_len = None, -1
+            for i, combo in enumerate(self.get_combos()):
+                pressed = all(key in keys for key in combo)
+                if pressed and max_len < len(combo):
+                    action, max_len = i, len(combo)
+            result.append(None if action is None else np.array([action]))
+        return result
+
+    def act(self, ac):
+        # procgen/env.py:223-226: always cast actions to int32
+        ac = np.asarray(ac).astype(np.int32).reshape(self.num)
+        if self.device_buffers:
+            raise ProcgenError("device-buffer env: use act_device / act_hashed")
+        self._ac["action"][:] = ac
+        self._lib.libenv_act(self._handle)
+        _check(self._lib, self._handle)
+
+    def observe(self):
+        if self.device_buffers:
+            rc = self._lib.procgen_wait(self._handle)
+            _check(self._lib, self._handle, rc)
+            return None
+        self._lib.libenv_observe(self._handle)
+        _check(self._lib, self._handle)
+        return self._rew.copy(), {k: v.copy() for k, v in self._ob.items()}, self._first.astype(bool)
+
+    def get_info(self):
+        if self.device_buffers:
+            raise ProcgenError("device-buffer env: read device_ptrs() instead")
+        return [{k: v[i].copy() for k, v in self._info.items()} for i in range(self.num)]
+
+    def callmethod(self, method, *args, **kwargs):
+        return getattr(self, method)(*args, **kwargs)
+
+    def get_state(self):  # procgen/env.py:164-171
+        buf = ctypes.create_string_buffer(MAX_STATE_SIZE)
+        out = []
+        for i in range(self.num):
+            n = self._lib.get_state(self._handle, i, buf, MAX_STATE_SIZE)
+            if n < 0:
+                raise ProcgenError("get_state failed for env %d" % i)
+            out.append(bytes(buf.raw[:n]))
+        return out
+
+    def set_state(self, states):  # procgen/env.py:173-177
+        assert len(states) == self.num
+        for i, s in enumerate(states):
+            self._lib.set_state(self._handle, i, s, len(s))
+        _check(self._lib, self._handle)
+        if not self.device_buffers:
+            self._lib.libenv_observe(self._handle)
+
+    # ------------------------------------------------------------------ device extensions
+    def act_hashed(self, seed, t):
+        rc = self._lib.procgen_act_hashed(self._handle, seed, t)
+        _check(self._lib, self._handle, rc)
+
+    def act_device(self, ptr):
+        rc = self._lib.procgen_act_device(self._handle, ptr)
+        _check(self._lib, self._handle, rc)
+
+    def wait(self):
+        rc = self._lib.procgen_wait(self._handle)
+        _check(self._lib, self._handle, rc)
+
+    def device_ptrs(self):
+        d = _lib.pg_device_buffers()
+        self._lib.procgen_device_buffers(self._handle, ctypes.byref(d))
+        return d
+
+    def set_timing(self, on):
+        self._lib.procgen_set_timing(self._handle, int(on))
+
+    def kernel_times(self):
+        out = (ctypes.c_float * 3)()
+        n = self._lib.procgen_kernel_times(self._handle, out, 3)
+        return n, list(out)
+
+    def debug_env(self, i):
+        buf = np.zeros(128, dtype=np.int32)
+        self._lib.procgen_debug_env(self._handle, i, buf.ctypes.data, buf.nbytes)
+        return buf
+
+    def close(self):
+        if getattr(self, "_handle", None):
+            self._lib.libenv_close(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ProcgenGym3Env(BaseProcgenEnv):
+    """procgen/env.py:229-273."""
+
+    def __init__(self, num, env_name, center_agent=True, use_backgrounds=True, use_monochrome_assets=False,
+                 restrict_themes=False, use_generated_assets=False, paint_vel_info=False, distribution_mode="hard",
+                 **kwargs):
+        assert distribution_mode in DISTRIBUTION_MODE_DICT, f'"{distribution_mode}" is not a valid distribution mode.'
+        if distribution_mode == "exploration":
+            assert env_name in EXPLORATION_LEVEL_SEEDS, f"{env_name} does not support exploration mode"
+            distribution_mode = DISTRIBUTION_MODE_DICT["hard"]
+            assert "num_levels" not in kwargs, "exploration mode overrides num_levels"
+            kwargs["num_levels"] = 1
+            assert "start_level" not in kwargs, "exploration mode overrides start_level"
+            kwargs["start_level"] = EXPLORATION_LEVEL_SEEDS[env_name]
+        else:
+            distribution_mode = DISTRIBUTION_MODE_DICT[distribution_mode]
+        options = {
+            "center_agent": bool(center_agent),
+            "use_generated_assets": bool(use_generated_assets),
+            "use_monochrome_assets": bool(use_monochrome_assets),
+            "restrict_themes": bool(restrict_themes),
+            "use_backgrounds": bool(use_backgrounds),
+            "paint_vel_info": bool(paint_vel_info),
+            "distribution_mode": distribution_mode,
+        }
+        super().__init__(num, env_name, options, **kwargs)

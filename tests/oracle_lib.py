@@ -1,0 +1,133 @@
+"""ctypes wrapper of the CPU oracle (oracle/procgen_oracle.c) -- the parity checker.
+
+Test infrastructure only: the product path never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref.so")
+
+
+class or_image(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint32), ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class or_atlas(ctypes.Structure):
+    _fields_ = [("pixels", ctypes.c_void_p), ("sprites", ctypes.c_void_p), ("backgrounds", ctypes.c_void_p),
+                ("num_backgrounds", ctypes.c_int32), ("num_themes", ctypes.c_void_p)]
+
+
+OPTION_FIELDS = ["num_levels", "start_level", "rand_seed", "distribution_mode", "center_agent", "use_backgrounds",
+                 "restrict_themes", "use_sequential_levels", "use_monochrome_assets", "paint_vel_info", "debug_mode"]
+
+
+class or_options(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in OPTION_FIELDS]
+
+
+_LIB = None
+
+
+def load():
+    global _LIB
+    if _LIB is None:
+        src = os.path.join(ORACLE_DIR, "procgen_oracle.c")
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+            subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+        lib = ctypes.CDLL(ORACLE_SO)
+        lib.oracle_make.restype = ctypes.c_void_p
+        lib.oracle_make.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(or_options),
+                                    ctypes.POINTER(or_atlas)]
+        for n in ["oracle_close", "oracle_start"]:
+            getattr(lib, n).argtypes = [ctypes.c_void_p]
+        lib.oracle_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_observe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
+        lib.oracle_debug.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        lib.oracle_mt_stream.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
+        lib.oracle_randgen_script.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        lib.oracle_qt_replay.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p]
+        lib.oracle_qt_replay.restype = ctypes.c_int
+        _LIB = lib
+    return _LIB
+
+
+def splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def hashed_actions(seed, env_ids, t, num_actions=15):
+    """Same counter hash as the engine's procgen_act_hashed (pg_step.hip splitmix64), vectorised."""
+    with np.errstate(over="ignore"):
+        g = np.asarray(env_ids, dtype=np.uint64) & np.uint64(0xFFFFFFFF)
+        x = np.uint64(seed) ^ (g << np.uint64(32)) ^ np.uint64(t & 0xFFFFFFFF)
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return (x % np.uint64(num_actions)).astype(np.int32)
+
+
+class OracleEnv:
+    """`count` envs with global indices env_offset.. of a vec env (same seeds as the engine)."""
+
+    def __init__(self, env_name, count, env_offset=0, atlas=None, **kw):
+        import sys
+        sys.path.insert(0, os.path.join(REPO, "procgen-1_amd"))
+        from procgen_amd.assets import atlas_for
+        self.lib = load()
+        self.atlas = atlas or atlas_for(env_name)
+        a = self.atlas
+        self._at = or_atlas(a.pixels.ctypes.data, a.sprites.ctypes.data, a.backgrounds.ctypes.data,
+                            a.backgrounds.shape[0], a.num_themes.ctypes.data)
+        opts = dict(num_levels=0, start_level=0, rand_seed=0, distribution_mode=1, center_agent=1, use_backgrounds=1,
+                    restrict_themes=0, use_sequential_levels=0, use_monochrome_assets=0, paint_vel_info=0,
+                    debug_mode=0)
+        opts.update(kw)
+        self._opt = or_options(*[int(opts[n]) for n in OPTION_FIELDS])
+        self.count = count
+        self.h = self.lib.oracle_make(env_name.encode(), count, env_offset, ctypes.byref(self._opt),
+                                      ctypes.byref(self._at))
+        if not self.h:
+            raise ValueError("oracle_make rejected the options")
+        self.lib.oracle_start(self.h)
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        self.lib.oracle_step(self.h, a.ctypes.data)
+
+    def observe(self):
+        n = self.count
+        rgb = np.zeros((n, 64, 64, 3), np.uint8)
+        rew = np.zeros(n, np.float32)
+        first = np.zeros(n, np.uint8)
+        pls = np.zeros(n, np.int32)
+        plc = np.zeros(n, np.uint8)
+        ls = np.zeros(n, np.int32)
+        self.lib.oracle_observe(self.h, rgb.ctypes.data, rew.ctypes.data, first.ctypes.data, pls.ctypes.data,
+                                plc.ctypes.data, ls.ctypes.data)
+        return dict(rgb=rgb, rew=rew, first=first, prev_level_seed=pls, prev_level_complete=plc, level_seed=ls)
+
+    def debug(self, i):
+        out = np.zeros(16, np.int32)
+        self.lib.oracle_debug(self.h, i, out.ctypes.data, 16)
+        return out
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
