@@ -117,10 +117,9 @@ struct VecEnv {
     std::vector<uint8_t> h_staging;
     // timing
     bool timing = false;
-    hipEvent_t ev[4] = {};
-    float t_sum[3] = {0, 0, 0};
-    int t_n = 0;
-    bool t_pending = false;
+    std::vector<hipEvent_t> ev; // 4 per timed step: before step, after step, after reset, after render
+    int t_used = 0;             // timed steps recorded since procgen_set_timing
+    int device = 0;
     int error = 0;
     std::string error_msg;
 };
@@ -172,28 +171,26 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
 
 int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
-    bool tm = v->timing;
-    if (tm && v->t_pending) {
-        // fold the previous step's timings in (events are complete once the stream passed them)
-        float a, b, c;
-        if (hipEventSynchronize(v->ev[3]) == hipSuccess && hipEventElapsedTime(&a, v->ev[0], v->ev[1]) == hipSuccess &&
-            hipEventElapsedTime(&b, v->ev[1], v->ev[2]) == hipSuccess &&
-            hipEventElapsedTime(&c, v->ev[2], v->ev[3]) == hipSuccess) {
-            v->t_sum[0] += a; v->t_sum[1] += b; v->t_sum[2] += c; v->t_n++;
+    HIPCHECK(hipSetDevice(v->device));
+    hipEvent_t *e = nullptr;
+    if (v->timing) {
+        size_t need = (size_t)(v->t_used + 1) * 4;
+        while (v->ev.size() < need) {
+            hipEvent_t x;
+            HIPCHECK(hipEventCreate(&x));
+            v->ev.push_back(x);
         }
-        v->t_pending = false;
+        e = &v->ev[(size_t)v->t_used * 4];
+        v->t_used++;
     }
     HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t), v->stream));
-    if (tm) HIPCHECK(hipEventRecord(v->ev[0], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[0], v->stream));
     pg_launch_step(&v->dev, v->stream, use_hash, seed, t);
-    if (tm) HIPCHECK(hipEventRecord(v->ev[1], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[1], v->stream));
     pg_launch_reset(&v->dev, v->stream, 0, 0);
-    if (tm) HIPCHECK(hipEventRecord(v->ev[2], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[2], v->stream));
     pg_launch_render(&v->dev, v->stream);
-    if (tm) {
-        HIPCHECK(hipEventRecord(v->ev[3], v->stream));
-        v->t_pending = true;
-    }
+    if (e) HIPCHECK(hipEventRecord(e[3], v->stream));
     HIPCHECK(hipGetLastError());
     return 0;
 }
@@ -307,7 +304,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         delete v;
         return bad("hipStreamCreate failed");
     }
-    for (auto &e : v->ev) hipEventCreate(&e);
+    (void)hipGetDevice(&v->device);
 
     // spaces (vecgame.cpp:212-316)
     v->ob_types.push_back(make_type("rgb", LIBENV_DTYPE_UINT8, {64, 64, 3}, 0, 255));
@@ -495,6 +492,7 @@ LIBENV_API void libenv_act(libenv_env *env) {
 
 LIBENV_API void libenv_observe(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
+    (void)hipSetDevice(v->device);
     if (v->buffers_set) copy_out(v);
     else hipStreamSynchronize(v->stream);
     check_device_errors(v);
@@ -524,6 +522,7 @@ LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t) {
 
 LIBENV_API int procgen_wait(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
+    HIPCHECK(hipSetDevice(v->device));
     HIPCHECK(hipStreamSynchronize(v->stream));
     check_device_errors(v);
     return v->error ? -v->error : 0;
@@ -555,26 +554,28 @@ LIBENV_API const char *procgen_error_string(libenv_env *env) {
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
     VecEnv *v = (VecEnv *)env;
     v->timing = enabled != 0;
-    v->t_sum[0] = v->t_sum[1] = v->t_sum[2] = 0;
-    v->t_n = 0;
-    v->t_pending = false;
+    v->t_used = 0;
     return 0;
 }
 
+// Averages over the steps timed since procgen_set_timing(env, 1): out[0] step kernel,
+// out[1] reset kernel, out[2] render kernel, out[3] whole step (ms).
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
-    if (v->t_pending) {
-        float a, b, c;
-        hipEventSynchronize(v->ev[3]);
-        if (hipEventElapsedTime(&a, v->ev[0], v->ev[1]) == hipSuccess &&
-            hipEventElapsedTime(&b, v->ev[1], v->ev[2]) == hipSuccess &&
-            hipEventElapsedTime(&c, v->ev[2], v->ev[3]) == hipSuccess) {
-            v->t_sum[0] += a; v->t_sum[1] += b; v->t_sum[2] += c; v->t_n++;
+    double sum[4] = {0, 0, 0, 0};
+    if (v->t_used > 0) {
+        HIPCHECK(hipEventSynchronize(v->ev[(size_t)v->t_used * 4 - 1]));
+        for (int k = 0; k < v->t_used; k++) {
+            hipEvent_t *e = &v->ev[(size_t)k * 4];
+            float a = 0, b = 0, c = 0;
+            HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));
+            HIPCHECK(hipEventElapsedTime(&b, e[1], e[2]));
+            HIPCHECK(hipEventElapsedTime(&c, e[2], e[3]));
+            sum[0] += a; sum[1] += b; sum[2] += c; sum[3] += a + b + c;
         }
-        v->t_pending = false;
     }
-    for (int i = 0; i < n && i < 3; i++) out[i] = v->t_n ? v->t_sum[i] / v->t_n : 0.f;
-    return v->t_n;
+    for (int i = 0; i < n && i < 4; i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;
+    return v->t_used;
 }
 
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length) {

@@ -2,12 +2,15 @@
 // 97-107, 173-191; basic-abstract-game.cpp:808-1075; games/coinrun.cpp:64-70, 133-138, 213-225).
 //
 // One wavefront per env, a 16 KB RGB32 framebuffer in LDS.  The painter's algorithm of
-// the reference is kept exactly, but each layer is rasterised the way the GPU likes:
-//   * background + grid tiles: pixel-centric -- lane = screen column, loop over rows; a
-//     pixel blends every tile covering it (<= 2 columns x 2 rows because of RENDER_EPS
-//     overlap) in the reference's x-major / y-minor draw order;
-//   * entities: sprite-centric -- one entity at a time in list order, lanes = the
-//     entity's footprint pixels.
+// the reference is kept exactly, but each layer is rasterised the way a wave64 likes:
+//   * background + grid tiles: pixel-centric -- lane = screen column, loop over rows.  A
+//     pixel blends every tile covering it (<= 2 columns x 2 rows because of the RENDER_EPS
+//     overlap) in the reference's x-major / y-minor draw order.  The Qt blit geometry of
+//     every tile column (per lane) and tile row (lane = screen row, broadcast with
+//     readlane) is computed once per frame; grid type -> sprite is an LDS table.
+//   * entities: sprite-centric -- blit geometry of 64 entities at a time is computed
+//     lane-parallel, then the entities are stamped one by one in list order (lanes =
+//     footprint pixels), which is the only order-dependent part.
 // Every blit reproduces Qt's raster scale blit (qt_scale_image_32bit fixed-point
 // stepping, SourceOver on premultiplied ARGB32, painter opacity) bit for bit.
 #include "pg_device.h"
@@ -34,16 +37,17 @@ DEV void screen_rect(const View &v, float x, float y, float dx, float dy, float 
     rh = (double)((dy + 2 * eps) * v.unit);
 }
 
-// One axis of qt_blit_setup (the x and y halves are independent).
+// One axis of Qt's scale blit setup (qt_scale_image_32bit); the x and y halves are independent.
 struct Axis {
     int t1, n;       // first device pixel, pixel count (after clip and bound checks)
-    uint32_t base;   // fixed-point source coordinate of pixel t1
+    uint32_t base;   // 16.16 source coordinate of pixel t1
     int step;
 };
 
 DEV bool axis_setup(double r, double rw, int iw, Axis &a) {
+    a.n = 0;
     if (!(rw > 0) || iw <= 0) return false;
-    double t_w = (r + rw) - r;
+    double t_w = (r + rw) - r;  // qt_mapRect_non_normalizing: QRectF(topLeft, bottomRight)
     double t_right = r + t_w;
     double sx = t_w / (double)iw;
     int ix = (int)(65536.0 / sx);
@@ -62,32 +66,26 @@ DEV bool axis_setup(double r, double rw, int iw, Axis &a) {
     return true;
 }
 
-// image_for_type (coinrun.cpp:213-225, basic-abstract-game.cpp:446-448)
-DEV int image_for_type(const PGEnv &s, float agent_vx, int type) {
-    if (type == PLAYER) {
-        if (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support) return PLAYER;
-        return (s.cur_time / 5 % 2 == 0 || !s.has_support) ? CR_PLAYER_RIGHT1 : CR_PLAYER_RIGHT2;
-    } else if (type == CR_ENEMY_BARRIER) {
-        return -1;
-    }
-    return type < 0 ? -type : type;
-}
 DEV bool is_player_image(int t) {
     return t == PLAYER || t == CR_PLAYER_JUMP || t == CR_PLAYER_RIGHT1 || t == CR_PLAYER_RIGHT2;
 }
 
-DEV int4 sprite_of(const PGDev &d, int slot) {
-    return reinterpret_cast<const int4 *>(d.sprites)[slot];
-}
+DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// Size of the per-type grid sprite table (grid values 0..127 take the fast path).
+#define NTYPES 128
+// Tile images all have this size in coinrun; other sizes take the exact slow path.
+#define TILE_PX 128
 
 } // namespace
 
 extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
+    __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, -2: slow path
     const int env = blockIdx.x;
     const PGEnv s = d.envs[env];
     const int16_t *G = d.grid + (size_t)env * PG_GRID_MAX;
-    int err = 0;
+    bool err = false;
 
     float agent_x, agent_y, agent_vx;
     if (s.agent_erased) {
@@ -95,6 +93,10 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     } else {
         agent_x = EFr(d, F_X, env, 0); agent_y = EFr(d, F_Y, env, 0); agent_vx = EFr(d, F_VX, env, 0);
     }
+    // image_for_type(PLAYER) (coinrun.cpp:213-219): one animation frame for the whole frame
+    const int player_img = (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
+                               ? PLAYER
+                               : ((s.cur_time / 5 % 2 == 0 || !s.has_support) ? CR_PLAYER_RIGHT1 : CR_PLAYER_RIGHT2);
 
     // ---- prepare_for_drawing(rect_height = 64) (basic-abstract-game.cpp:828-847)
     View v;
@@ -114,7 +116,27 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     v.x_off = v.unit * (v.center_x - v.view_dim / 2);
     v.y_off = v.unit * (v.center_y - v.view_dim / 2);
 
-    const int col = LANE;
+    const int lane = LANE;
+
+    // ---- grid type -> sprite table (theme_for_grid_obj coinrun.cpp:133-138, image_for_type :213-225,
+    //      draw_image basic-abstract-game.cpp:886-922)
+    for (int t = lane; t < NTYPES; t += 64) {
+        int off = -1;
+        int img = t == PLAYER ? player_img : (t == CR_ENEMY_BARRIER ? -1 : t);
+        if (img >= 0) {
+            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+                off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
+            } else {
+                int theme = cr_is_wall(t) ? s.wall_theme : 0;
+                if (s.opt_restrict_themes) theme = 0;
+                int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                if (sp.y == TILE_PX && sp.z == TILE_PX) off = sp.x;
+                else if (sp.y > 0) off = -2;
+                else off = -3; // generated assets: not in this build
+            }
+        }
+        tile_off[t] = off;
+    }
 
     // ---- draw_background (basic-abstract-game.cpp:988-1016): black fill + one scaled blit
     Axis bx, by;
@@ -134,10 +156,10 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         double rx = mx + mw * ax, ry = my + mh * 0.0, rw = mw * aw, rh = mh * 1.0;
         bg_ok = axis_setup(rx, rw, bgi.y, bx) && axis_setup(ry, rh, bgi.z, by);
     }
-    bool bg_col = bg_ok && col >= bx.t1 && col < bx.t1 + bx.n;
-    int bg_scol = bg_col ? (int)((bx.base + (uint32_t)((col - bx.t1) * bx.step)) >> 16) : 0;
+    const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
+    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
 
-    // ---- grid tile columns covering this lane's screen column
+    // ---- visible tile window (basic-abstract-game.cpp:937-948)
     int low_x, high_x, low_y, high_y;
     if (s.opt_center_agent) {
         double margin = (double)v.visibility / 2.0 + 1;
@@ -148,77 +170,73 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     } else {
         low_x = 0; high_x = s.main_width - 1; low_y = 0; high_y = s.main_height - 1;
     }
-    const float tile_eps = RENDER_EPS;
-    // candidate tile columns: the one under the pixel and its neighbours; keep those whose
-    // Qt pixel span (for the 128-px tile images used by every coinrun grid type) covers col
-    int cand_x[2];
-    Axis cand_ax[2];
-    int ncx = 0;
-    int iw_cached = 128;
+
+    // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images
+    int cx0 = 0, cx1 = 0, ncx = 0;
+    Axis ax0, ax1;
+    ax0.n = ax1.n = 0;
     {
-        int xg = (int)floorf(((float)col + 0.5f + v.x_off) / v.unit);
+        int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
         for (int x = xg - 2; x <= xg + 2; x++) {
             if (x < low_x || x > high_x || ncx == 2) continue;
             double rx, ry, rw, rh;
-            screen_rect(v, (float)x, 0.0f, 1, 1, tile_eps, rx, ry, rw, rh);
+            screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
             Axis a;
-            if (axis_setup(rx, rw, iw_cached, a) && col >= a.t1 && col < a.t1 + a.n) {
-                cand_x[ncx] = x;
-                cand_ax[ncx] = a;
+            if (axis_setup(rx, rw, TILE_PX, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+                if (ncx == 0) { cx0 = x; ax0 = a; } else { cx1 = x; ax1 = a; }
                 ncx++;
             }
         }
     }
-
-    // ---- pixel-centric background + tiles, row by row (row-uniform tile rows)
-    for (int row = 0; row < PG_RES; row++) {
-        uint32_t px = 0xff000000u;
-        if (bg_col && row >= by.t1 && row < by.t1 + by.n) {
-            int srow = (int)((by.base + (uint32_t)((row - by.t1) * by.step)) >> 16);
-            px = d.pixels[(uint32_t)bgi.x + (uint32_t)(srow * bgi.y + bg_scol)];
-        }
-        // tile rows covering this row (uniform): draw order is y ascending
-        int yg = (int)floorf((v.view_dim - ((float)row + 0.5f - v.y_off) / v.unit));
-        int cand_y[2];
-        Axis cand_ay[2];
-        int ncy = 0;
+    const int scol0 = ncx > 0 ? (int)((ax0.base + (uint32_t)((lane - ax0.t1) * ax0.step)) >> 16) : 0;
+    const int scol1 = ncx > 1 ? (int)((ax1.base + (uint32_t)((lane - ax1.t1) * ax1.step)) >> 16) : 0;
+    // tile rows covering screen row `lane` (<= 2, ascending y = the reference's draw order)
+    int ry0 = 0, ry1 = 0, ncy = 0, srow0 = 0, srow1 = 0;
+    {
+        int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
         for (int y = yg - 2; y <= yg + 2; y++) {
             if (y < low_y || y > high_y || ncy == 2) continue;
             double rx, ry, rw, rh;
-            screen_rect(v, 0.0f, (float)(y + 1), 1, 1, tile_eps, rx, ry, rw, rh);
+            screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
             Axis a;
-            if (axis_setup(ry, rh, 128, a) && row >= a.t1 && row < a.t1 + a.n) {
-                cand_y[ncy] = y;
-                cand_ay[ncy] = a;
+            if (axis_setup(ry, rh, TILE_PX, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+                int sr = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
+                if (ncy == 0) { ry0 = y; srow0 = sr; } else { ry1 = y; srow1 = sr; }
                 ncy++;
             }
         }
+    }
+    wave_sync();
+
+    // ---- pixel-centric background + tiles, row by row
+    const bool wide = s.main_width > 0;
+    for (int row = 0; row < PG_RES; row++) {
+        uint32_t px = 0xff000000u;
+        if (bg_col && row >= by.t1 && row < by.t1 + by.n) {
+            uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
+            px = d.pixels[bg_col_base + srow * (uint32_t)bgi.y];
+        }
+        const int nr = readlane(ncy, row);
+        const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
+        const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
         for (int k = 0; k < ncx; k++) {
-            for (int l = 0; l < ncy; l++) {
-                int x = cand_x[k], y = cand_y[l];
+            const int x = k == 0 ? cx0 : cx1;
+            const int scol = k == 0 ? scol0 : scol1;
+            for (int l = 0; l < nr; l++) {
+                const int y = l == 0 ? y_a : y_b;
+                const int srow = l == 0 ? sr_a : sr_b;
                 int type;
-                if (!(0 <= y && y < s.main_height && 0 <= x && x < s.main_width)) type = s.out_of_bounds_object;
+                if (!(wide && 0 <= y && y < s.main_height && 0 <= x && x < s.main_width)) type = s.out_of_bounds_object;
                 else type = G[y * s.main_width + x];
                 if (type == INVALID_OBJ) continue;
-                int theme = cr_is_wall(type) ? s.wall_theme : 0; // theme_for_grid_obj (coinrun.cpp:133-138)
-                int img = image_for_type(s, agent_vx, type);
-                if (img < 0) continue;
-                if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                    if (img != SPACE) err = PG_ERR_BAD_OPTION; // draw_grid_obj fills: not in this build
-                    continue;
-                }
-                if (s.opt_restrict_themes) theme = 0;
-                int4 sp = sprite_of(d, img + theme * MAX_ASSETS);
-                if (sp.y != iw_cached || sp.z != 128) { err = PG_ERR_NO_ATLAS; continue; }
-                const Axis &ax = cand_ax[k];
-                const Axis &ay = cand_ay[l];
-                int scol = (int)((ax.base + (uint32_t)((col - ax.t1) * ax.step)) >> 16);
-                int srow = (int)((ay.base + (uint32_t)((row - ay.t1) * ay.step)) >> 16);
-                uint32_t src = d.pixels[(uint32_t)sp.x + (uint32_t)(srow * sp.y + scol)];
+                int off = (type >= 0 && type < NTYPES) ? tile_off[type] : -2;
+                if (off == -1) continue;
+                if (off < 0) { err = true; continue; }
+                uint32_t src = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
                 px = src + BYTE_MUL(px, (~src) >> 24);
             }
         }
-        fb[row * PG_RES + col] = px;
+        fb[row * PG_RES + lane] = px;
     }
     wave_sync();
 
@@ -226,79 +244,86 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     const int n = s.num_ents;
     for (int z = 0; z <= 1; z++) {
         for (int base = 0; base < n; base += 64) {
-            int i = base + LANE;
-            unsigned long long m = ballot(i < n && EIr(d, F_RENDER_Z, env, i) == z);
+            // lane-parallel blit setup of entity base + lane
+            const int i = base + lane;
+            bool draw = false;
+            Axis ex, ey;
+            int soff = 0, sw = 0, ca = 256, mir = 0;
+            if (i < n && EIr(d, F_RENDER_Z, env, i) == z) {
+                float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
+                float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
+                int flags = EIr(d, F_FLAGS, env, i);
+                float alpha = EFr(d, F_ALPHA, env, i);
+                float rotation = EFr(d, F_ROTATION, env, i);
+                int itype = EIr(d, F_IMAGE_TYPE, env, i);
+                int theme = EIr(d, F_IMAGE_THEME, env, i);
+                int img = itype == PLAYER ? player_img : (itype == CR_ENEMY_BARRIER ? -1 : (itype < 0 ? -itype : itype));
+                if (img >= 0) {
+                    if ((flags & EF_ABS_COORDS) || rotation != 0 || s.opt_use_monochrome_assets ||
+                        img >= USE_ASSET_THRESHOLD) {
+                        if (img != SPACE) err = true; // not in this build
+                    } else {
+                        if (s.opt_restrict_themes) theme = 0;
+                        double rx, ry, rw, rh;
+                        screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+                        if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
+                            rx = rx + rw * 0.0;
+                            ry = ry + rh * -.7415;
+                            rw = rw * 1.0;
+                            rh = rh * 1.7415;
+                        }
+                        int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                        if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
+                            draw = true;
+                            soff = sp.x;
+                            sw = sp.y;
+                            ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
+                            mir = (flags & EF_REFLECTED) != 0;
+                        }
+                    }
+                }
+            }
+            unsigned long long m = ballot(draw);
             while (m) {
-                int e = base + __ffsll((long long)m) - 1;
+                const int j = __ffsll((long long)m) - 1;
                 m &= m - 1;
-                float ex = EFr(d, F_X, env, e), ey = EFr(d, F_Y, env, e);
-                float erx = EFr(d, F_RX, env, e), ery = EFr(d, F_RY, env, e);
-                int flags = EIr(d, F_FLAGS, env, e);
-                float alpha = EFr(d, F_ALPHA, env, e);
-                float rotation = EFr(d, F_ROTATION, env, e);
-                int itype = EIr(d, F_IMAGE_TYPE, env, e);
-                int theme = EIr(d, F_IMAGE_THEME, env, e);
-                if (flags & EF_ABS_COORDS) { err = PG_ERR_BAD_OPTION; continue; }
-                double rx, ry, rw, rh;
-                screen_rect(v, ex - erx, ey + ery, 2 * erx, 2 * ery, 0, rx, ry, rw, rh);
-                int img = image_for_type(s, agent_vx, itype);
-                if (img < 0) continue;
-                if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                    if (img != SPACE) err = PG_ERR_BAD_OPTION;
-                    continue;
-                }
-                if (rotation != 0) { err = PG_ERR_BAD_OPTION; continue; }
-                if (s.opt_restrict_themes) theme = 0;
-                if (is_player_image(img)) { // coinrun get_adjusted_image_rect: adjust_rect(r, (0, -.7415, 1, 1.7415))
-                    rx = rx + rw * 0.0;
-                    ry = ry + rh * -.7415;
-                    rw = rw * 1.0;
-                    rh = rh * 1.7415;
-                }
-                int4 sp = sprite_of(d, img + theme * MAX_ASSETS);
-                Axis ax, ay;
-                if (!(axis_setup(rx, rw, sp.y, ax) && axis_setup(ry, rh, sp.z, ay))) continue;
-                int ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
-                bool mir = (flags & EF_REFLECTED) != 0;
-                int npx = ax.n * ay.n;
-                for (int p = LANE; p < npx; p += 64) {
-                    int py = p / ax.n, pxx = p - py * ax.n;
-                    int scol = (int)((ax.base + (uint32_t)(pxx * ax.step)) >> 16);
-                    int srow = (int)((ay.base + (uint32_t)(py * ay.step)) >> 16);
-                    if (mir) scol = sp.y - 1 - scol;
-                    uint32_t src = d.pixels[(uint32_t)sp.x + (uint32_t)(srow * sp.y + scol)];
-                    int o = (ay.t1 + py) * PG_RES + ax.t1 + pxx;
-                    fb[o] = blend_argb_pm(fb[o], src, ca);
+                const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
+                const int tx = readlane(ex.t1, j), ty = readlane(ey.t1, j);
+                const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
+                const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
+                const uint32_t offj = (uint32_t)readlane(soff, j);
+                const int swj = readlane(sw, j), caj = readlane(ca, j), mirj = readlane(mir, j);
+                const int npx = nx * ny;
+                const float inv = 1.0f / (float)nx;
+                for (int p = lane; p < npx; p += 64) {
+                    int py = (int)(((float)p + 0.5f) * inv);
+                    int pxx = p - py * nx;
+                    int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
+                    int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
+                    if (mirj) scol = swj - 1 - scol;
+                    uint32_t src = d.pixels[offj + (uint32_t)(srow * swj + scol)];
+                    int o = (ty + py) * PG_RES + tx + pxx;
+                    fb[o] = blend_argb_pm(fb[o], src, caj);
                 }
                 wave_sync();
             }
         }
     }
-    wave_sync();
 
-    // ---- bgr32_to_rgb888 (game.cpp:8-23): 768 x 16-byte chunks per env
+    // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
     uint8_t *out = d.rgb + (size_t)env * PG_OBS_BYTES;
-    for (int ch = LANE; ch < PG_OBS_BYTES / 16; ch += 64) {
-        uint32_t w4[4];
-        int b0 = ch * 16;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; bb++) {
-                int byte = b0 + q * 4 + bb;
-                int p = byte / 3, c3 = byte - p * 3;
-                uint32_t pxv = fb[p];
-                uint32_t v8 = c3 == 0 ? (pxv >> 16) & 0xff : (c3 == 1 ? (pxv >> 8) & 0xff : pxv & 0xff);
-                word |= v8 << (8 * bb);
-            }
-            w4[q] = word;
-        }
-        reinterpret_cast<uint4 *>(out)[ch] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    for (int q = lane; q < PG_RES * PG_RES / 4; q += 64) {
+        uint4 p4 = reinterpret_cast<const uint4 *>(fb)[q];
+        // bytes r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
+        uint32_t w0 = ((p4.x >> 16) & 0xff) | (p4.x & 0xff00) | ((p4.x & 0xff) << 16) | (((p4.y >> 16) & 0xff) << 24);
+        uint32_t w1 = ((p4.y >> 8) & 0xff) | ((p4.y & 0xff) << 8) | (((p4.z >> 16) & 0xff) << 16) | (((p4.z >> 8) & 0xff) << 24);
+        uint32_t w2 = (p4.z & 0xff) | (((p4.w >> 16) & 0xff) << 8) | (((p4.w >> 8) & 0xff) << 16) | ((p4.w & 0xff) << 24);
+        uint32_t *o = reinterpret_cast<uint32_t *>(out + (size_t)q * 12);
+        o[0] = w0;
+        o[1] = w1;
+        o[2] = w2;
     }
-    if (err) {
-        if (LANE == 0) atomicOr(d.error_any, 1 << err);
-    }
+    if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
 }
 
 extern "C" void pg_launch_render(const PGDev *d, hipStream_t s) {

@@ -15,6 +15,8 @@ struct Ctx {
     size_t eb;      // env * PG_CAP
     const int16_t *G; // this env's grid
     uint32_t *lds;  // 624-word twist staging
+    int16_t *ilist; // LDS: ascending indices of entities that can interact in sub_step
+    int nlist;
 };
 
 DEV float &EF(Ctx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
@@ -116,12 +118,23 @@ DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
 }
 
 // ------------------------------------------------------------------ collision scan
-// Largest index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
-// basic-abstract-game.cpp:345-354 (reverse iteration), lane-parallel in 64-slot chunks.
+// The body of sub_step's entity loop (basic-abstract-game.cpp:345-377) has an effect only
+// when is_blocked_ents() or will_reflect() fires.  For coinrun those reduce to: target is
+// a CRATE and the move is vertical (coinrun.cpp:187-211; base is_blocked needs WALL_OBJ /
+// out_of_bounds_object / a wall type, will_reflect needs a wall or ENEMY_BARRIER type --
+// no coinrun entity has such a type).  Every other (obj, m) pair is a no-op, so the scan
+// visits only the "interactors" (crates), collected once per step into LDS; entity indices
+// do not change during step_entities (no insertion or erase there).
+DEV bool scan_needed(bool is_h) { return !is_h; }
+DEV bool is_interactor(int type) { return type == CR_CRATE; }
+
+// Largest interactor index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
+// i.e. the next entity the reference's reverse loop would act on; lane-parallel over the list.
 DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
-    for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
-        int i = base + LANE;
+    for (int base = (c.nlist - 1) & ~63; base >= 0; base -= 64) {
+        int k = base + LANE;
         bool hit = false;
+        int i = k < c.nlist ? c.ilist[k] : PG_CAP;
         if (i < upper && i != oi) {
             int fl = EI(c, F_FLAGS, i);
             if (!(fl & EF_WILL_ERASE)) {
@@ -131,9 +144,22 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
             }
         }
         unsigned long long m = ballot(hit);
-        if (m) return base + top_bit(m);
+        if (m) return __builtin_amdgcn_readlane(i, top_bit(m)); // list is ascending by index
     }
     return -1;
+}
+
+DEV void build_interactor_list(Ctx &c) {
+    int cnt = 0;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        int i = base + LANE;
+        bool in = i < c.s.num_ents && is_interactor(EI(c, F_TYPE, i));
+        unsigned long long m = ballot(in);
+        if (in) c.ilist[cnt + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        cnt += __popcll(m);
+    }
+    c.nlist = cnt;
+    wave_sync();
 }
 
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
@@ -201,7 +227,7 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
     o.y = ny;
     bool block2 = false;
     int upper = c.s.num_ents;
-    while (true) {
+    while (scan_needed(is_h)) {
         int m = next_collider(c, oi, upper, o);
         if (m < 0) break;
         upper = m;
@@ -415,6 +441,7 @@ DEV void coinrun_game_step(Ctx &c) {
         EF(c, F_VROT, 0) = vrot;
     }
     wave_sync();
+    build_interactor_list(c);
     step_entities(c);
 
     // agent / entity collisions (:728-750).  coinrun effects are order-free flags:
@@ -541,6 +568,7 @@ DEV uint64_t splitmix64(uint64_t x) {
 // Game::step (game.cpp:136-171) minus reset (queued) and observe (pg_render).
 extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use_hash, uint64_t hash_seed, int32_t hash_t) {
     __shared__ uint32_t lds_mt[PG_MT_N];
+    __shared__ int16_t lds_list[PG_CAP];
     Ctx c;
     c.d = d;
     c.env = blockIdx.x;
@@ -550,6 +578,8 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
     c.eb = (size_t)c.env * PG_CAP;
     c.G = d.grid + (size_t)c.env * PG_GRID_MAX;
     c.lds = lds_mt;
+    c.ilist = lds_list;
+    c.nlist = 0;
 
     int action;
     if (use_hash) {
