@@ -156,3 +156,25 @@ def test_full_size_sampled_parity():
             o.step(act[k:k + 1])
             assert_same(g, o.observe(), t, idx=slice(k, k + 1))
     env.close()
+
+
+def test_gpu_vs_committed_fixture():
+    """Engine vs the committed trajectory fixture (tests/golden/coinrun_oracle_traj.npz):
+    global envs of the 65,536-env config (env_offset places a 1-env shard at that index)."""
+    import os
+    import zlib
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "coinrun_oracle_traj.npz"), allow_pickle=False)
+    seed = int(z["action_seed"])
+    frames_at = list(z["frame_steps"])
+    for k, e in enumerate(z["envs"]):
+        env = make_gpu(1, num_levels=200, start_level=0, rand_seed=0, env_offset=int(e))
+        for t in range(int(z["steps"]) + 1):
+            if t:
+                env.act(hashed_actions(seed, [int(e)], t))
+            g = gpu_obs(env)
+            assert g["rew"][0] == z["rew"][t, k] and g["first"][0] == z["first"][t, k], (e, t)
+            assert g["level_seed"][0] == z["level_seed"][t, k] and g["prev_level_seed"][0] == z["prev_level_seed"][t, k]
+            assert zlib.crc32(g["rgb"][0].tobytes()) == z["rgb_crc32"][t, k], "env %d step %d" % (e, t)
+            if t in frames_at:
+                np.testing.assert_array_equal(g["rgb"][0], z["frames"][frames_at.index(t), k])
+        env.close()

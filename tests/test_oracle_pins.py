@@ -1,0 +1,174 @@
+"""Pins of the CPU oracle (the parity checker) -- CPU only.
+
+* MT19937 / RandGen draws: against the reference's own randgen.cpp compiled from
+  /root/reference (oracle/_ref, built by `make -C oracle ref`) and the C++ standard's
+  known answer ([rand.predef]: the 10000th output of a default-seeded mt19937 is 4123659995).
+* Entity::step: against the reference's entity.cpp (oracle/_ref).
+* Qt raster compositing: against canvases produced by the real Qt 5.9.7 raster engine
+  (tests/golden/qt_raster_goldens.npz, made by tools/make_raster_goldens.py).
+* Oracle trajectories: regression fixture tests/golden/coinrun_oracle_traj.npz
+  (tools/make_oracle_goldens.py).
+"""
+import ctypes
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from golden_io import encode_cmds
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def ref_lib():
+    if not os.path.exists(oracle_lib.REF_SO):
+        pytest.skip("oracle/_ref/libref.so not built (needs /root/reference at build time)")
+    lib = ctypes.CDLL(oracle_lib.REF_SO)
+    lib.ref_mt_stream.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int]
+    lib.ref_randgen_script.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lib.ref_entity_steps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return lib
+
+
+def test_mt_known_answer():
+    lib = oracle_lib.load()
+    out = np.zeros(10000, np.uint32)
+    lib.oracle_mt_stream(5489, out.ctypes.data, 10000)
+    assert int(out[-1]) == 4123659995
+
+
+@pytest.mark.parametrize("seed", [0, 1, 5489, 199, 2147483646, -1, -123456])
+def test_mt_stream_vs_reference(seed):
+    ref = ref_lib()
+    lib = oracle_lib.load()
+    n = 3000  # crosses several twists
+    a = np.zeros(n, np.uint32)
+    b = np.zeros(n, np.uint32)
+    lib.oracle_mt_stream(seed & 0xFFFFFFFF, a.ctypes.data, n)
+    ref.ref_mt_stream(seed, b.ctypes.data, n)
+    np.testing.assert_array_equal(a, b)
+
+
+def random_ops(rng, n):
+    ops = np.zeros((n, 3), np.int32)
+    for i in range(n):
+        k = int(rng.integers(0, 6))
+        if k == 0:
+            lo = int(rng.integers(-1000, 1000))
+            ops[i] = (0, lo, lo + int(rng.integers(1, 1 << 30)))
+        elif k == 1:
+            ops[i] = (1, int(rng.integers(1, 100000)), 0)
+        elif k == 4:
+            lo = int(rng.integers(-800, 800))
+            ops[i] = (4, lo, lo + int(rng.integers(1, 800)))
+        else:
+            ops[i] = (k, 0, 0)
+    return ops
+
+
+@pytest.mark.parametrize("seed", [0, 7, 424242])
+def test_randgen_helpers_vs_reference(seed):
+    ref = ref_lib()
+    lib = oracle_lib.load()
+    rng = np.random.default_rng(seed)
+    ops = random_ops(rng, 4000)
+    a = np.zeros(len(ops), np.int32)
+    b = np.zeros(len(ops), np.int32)
+    lib.oracle_randgen_script(seed, ops.ctypes.data, len(ops), a.ctypes.data)
+    ref.ref_randgen_script(seed, ops.ctypes.data, len(ops), b.ctypes.data)
+    np.testing.assert_array_equal(a, b)
+
+
+def oracle_entity_steps(init, etype, smart, friction, vrot, expire, steps):
+    """Entity::step restated in numpy float32 with the oracle's operation order."""
+    f = np.float32
+    x, y, vx, vy, rx, ry = (f(v) for v in init)
+    rot = f(0)
+    alpha, grow, decay = f(1), f(1), f(1)
+    life, erase, img = 0, 0, etype
+    if etype == 54:
+        grow = f(1.4)
+        expire_t = 4
+    else:
+        expire_t = -1
+    if etype == 59:
+        grow, decay = f(1.05), f(0.8)
+    if expire:
+        expire_t = expire
+    out = []
+    for _ in range(steps):
+        if not smart:
+            x = f(x + vx)
+            y = f(y + vy)
+        rot = f(rot + f(vrot))
+        vx = f(vx * f(friction))
+        vy = f(vy * f(friction))
+        life += 1
+        if expire_t > 0 and life > expire_t:
+            erase = 1
+        if etype == 54 and img < 58:
+            img += 1
+        rx = f(rx * grow)
+        ry = f(ry * grow)
+        alpha = f(decay * alpha)
+        words = np.array([x, y, vx, vy, rx, ry, rot, alpha], np.float32).view(np.uint32).tolist()
+        out.append(words + [life, erase, img])
+    return np.array(out, np.uint32)
+
+
+@pytest.mark.parametrize("etype,smart,friction,vrot,expire", [
+    (59, 0, 1.0, 0.0, 8), (54, 0, 1.0, 0.1, 0), (5, 1, 1.0, 0.0, 0), (2, 0, 0.9, 0.3, 0), (20, 0, 0.95, -0.2, 30)])
+def test_entity_step_vs_reference(etype, smart, friction, vrot, expire):
+    ref = ref_lib()
+    init = np.array([10.5, 3.25, 0.15, 0.01, 0.3, 0.2], np.float32)
+    steps = 40
+    b = np.zeros((steps, 11), np.uint32)
+    ref.ref_entity_steps(init.ctypes.data, etype, smart, friction, vrot, expire, steps, b.ctypes.data)
+    a = oracle_entity_steps(init, etype, smart, friction, vrot, expire, steps)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_qt_raster_goldens():
+    """Every painter case replayed through the oracle's Qt restatement equals real Qt 5.9.7."""
+    from procgen_amd.assets import atlas_for
+    lib = oracle_lib.load()
+    z = np.load(os.path.join(GOLDEN, "qt_raster_goldens.npz"), allow_pickle=False)
+    cmds, synth, cin, cout = z["cmds"], z["synth"], z["canvas_in"], z["canvas_out"]
+    atlas = atlas_for("coinrun")
+    bad = []
+    for i in range(cin.shape[0]):
+        b = encode_cmds(cmds[cmds["case"] == i], synth, atlas)
+        canvas = cin[i].copy()
+        rc = lib.oracle_qt_replay(b, len(b), canvas.ctypes.data)
+        assert rc == len(b)
+        if not np.array_equal(canvas, cout[i]):
+            bad.append(i)
+    assert not bad, "Qt raster mismatch in cases %s" % bad[:10]
+
+
+def test_oracle_trajectory_fixture():
+    """Regression pin of the oracle itself (tests/golden/coinrun_oracle_traj.npz)."""
+    path = os.path.join(GOLDEN, "coinrun_oracle_traj.npz")
+    z = np.load(path, allow_pickle=False)
+    envs = z["envs"]
+    steps = int(z["steps"])
+    orcs = [oracle_lib.OracleEnv("coinrun", 1, env_offset=int(e), num_levels=200, start_level=0, rand_seed=0)
+            for e in envs]
+    frames_at = list(z["frame_steps"])
+    fi = 0
+    for t in range(steps + 1):
+        for k, (e, o) in enumerate(zip(envs, orcs)):
+            if t:
+                o.step(oracle_lib.hashed_actions(int(z["action_seed"]), [e], t))
+            ob = o.observe()
+            assert ob["rew"][0] == z["rew"][t, k]
+            assert ob["first"][0] == z["first"][t, k]
+            assert ob["level_seed"][0] == z["level_seed"][t, k]
+            assert ob["prev_level_seed"][0] == z["prev_level_seed"][t, k]
+            assert zlib.crc32(ob["rgb"][0].tobytes()) == z["rgb_crc32"][t, k], "crc at step %d env %d" % (t, e)
+            if t in frames_at:
+                np.testing.assert_array_equal(ob["rgb"][0], z["frames"][frames_at.index(t), k])
+        fi += 1
