@@ -74,14 +74,20 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Size of the per-type grid sprite table (grid values 0..127 take the fast path).
 #define NTYPES 128
-// Tile images all have this size in coinrun; other sizes take the exact slow path.
+// Tile images all have this size in coinrun (other sizes are flagged, not drawn wrongly).
 #define TILE_PX 128
+// Largest visible grid window cached in LDS (centred views span visibility + 3 cells).
+#define WIN 24
+// Rows per batch of the pixel-centric pass, entities per stamping group.
+#define RB 8
+#define EG 8
 
 } // namespace
 
 extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
-    __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, -2: slow path
+    __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, <= -2: unsupported
+    __shared__ int win[WIN * WIN];    // tile_off of every cell of the visible window
     const int env = blockIdx.x;
     const PGEnv s = d.envs[env];
     const int16_t *G = d.grid + (size_t)env * PG_GRID_MAX;
@@ -208,35 +214,67 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     }
     wave_sync();
 
-    // ---- pixel-centric background + tiles, row by row
-    const bool wide = s.main_width > 0;
-    for (int row = 0; row < PG_RES; row++) {
-        uint32_t px = 0xff000000u;
-        if (bg_col && row >= by.t1 && row < by.t1 + by.n) {
-            uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-            px = d.pixels[bg_col_base + srow * (uint32_t)bgi.y];
+    // ---- visible grid window -> sprite offsets in LDS (one lookup per tile candidate)
+    const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
+    const bool use_win = ww > 0 && wh > 0 && ww <= WIN && wh <= WIN;
+    if (use_win) {
+        for (int idx = lane; idx < ww * wh; idx += 64) {
+            int yy = idx / ww, xx = idx - yy * ww;
+            int x = low_x + xx, y = low_y + yy;
+            int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
+                                                                                   : s.out_of_bounds_object;
+            win[idx] = type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
         }
-        const int nr = readlane(ncy, row);
-        const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
-        const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
-        for (int k = 0; k < ncx; k++) {
-            const int x = k == 0 ? cx0 : cx1;
-            const int scol = k == 0 ? scol0 : scol1;
-            for (int l = 0; l < nr; l++) {
-                const int y = l == 0 ? y_a : y_b;
-                const int srow = l == 0 ? sr_a : sr_b;
-                int type;
-                if (!(wide && 0 <= y && y < s.main_height && 0 <= x && x < s.main_width)) type = s.out_of_bounds_object;
-                else type = G[y * s.main_width + x];
-                if (type == INVALID_OBJ) continue;
-                int off = (type >= 0 && type < NTYPES) ? tile_off[type] : -2;
-                if (off == -1) continue;
-                if (off < 0) { err = true; continue; }
-                uint32_t src = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
-                px = src + BYTE_MUL(px, (~src) >> 24);
+    }
+    wave_sync();
+    auto tile_lookup = [&](int x, int y) -> int {
+        if (use_win) return win[(y - low_y) * ww + (x - low_x)];
+        int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
+                                                                               : s.out_of_bounds_object;
+        return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
+    };
+
+    // ---- pixel-centric background + tiles, RB rows per batch: every texel load of the batch
+    //      is issued before the first blend, so one memory round trip serves RB rows
+    for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+        uint32_t bgv[RB], tex[RB][4];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int k = 0; k < RB; k++) {
+            const int row = r0 + k;
+            const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
+            bgv[k] = 0xff000000u;
+            if (inb) {
+                uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
+                bgv[k] = d.pixels[bg_col_base + srow * (uint32_t)bgi.y];
+            }
+            const int nr = readlane(ncy, row);
+            const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
+            const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int kk = c >> 1, l = c & 1;
+                tex[k][c] = 0;
+                if (kk < ncx && l < nr) {
+                    const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
+                    const int off = tile_lookup(x, y);
+                    if (off <= -2) err = true;
+                    if (off >= 0) {
+                        const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
+                        tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
+                        valid |= 1u << (k * 4 + c);
+                    }
+                }
             }
         }
-        fb[row * PG_RES + lane] = px;
+#pragma unroll
+        for (int k = 0; k < RB; k++) {
+            uint32_t px = bgv[k];
+#pragma unroll
+            for (int c = 0; c < 4; c++) // draw order: (x0,y0) (x0,y1) (x1,y0) (x1,y1)
+                if (valid & (1u << (k * 4 + c))) px = tex[k][c] + BYTE_MUL(px, (~tex[k][c]) >> 24);
+            fb[(r0 + k) * PG_RES + lane] = px;
+        }
     }
     wave_sync();
 
@@ -283,29 +321,75 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
                     }
                 }
             }
+            // Stamp in list order, EG entities per group: the texel of this lane's footprint
+            // pixel is loaded for every entity of the group first (loads are order-free), then
+            // the group is blended into the framebuffer strictly in order.  Footprints wider
+            // than one wave (> 64 px) fall back to an in-order loop with inline loads.
+            const float inv_l = 1.0f / (float)(draw ? ex.n : 1);
             unsigned long long m = ballot(draw);
             while (m) {
-                const int j = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
-                const int tx = readlane(ex.t1, j), ty = readlane(ey.t1, j);
-                const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
-                const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
-                const uint32_t offj = (uint32_t)readlane(soff, j);
-                const int swj = readlane(sw, j), caj = readlane(ca, j), mirj = readlane(mir, j);
-                const int npx = nx * ny;
-                const float inv = 1.0f / (float)nx;
-                for (int p = lane; p < npx; p += 64) {
-                    int py = (int)(((float)p + 0.5f) * inv);
-                    int pxx = p - py * nx;
-                    int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
-                    int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
-                    if (mirj) scol = swj - 1 - scol;
-                    uint32_t src = d.pixels[offj + (uint32_t)(srow * swj + scol)];
-                    int o = (ty + py) * PG_RES + tx + pxx;
-                    fb[o] = blend_argb_pm(fb[o], src, caj);
+                int js[EG];
+#pragma unroll
+                for (int g = 0; g < EG; g++) {
+                    js[g] = m ? __ffsll((long long)m) - 1 : -1;
+                    if (m) m &= m - 1;
                 }
-                wave_sync();
+                uint32_t tv[EG];
+                int fo[EG];
+                bool on[EG];
+#pragma unroll
+                for (int g = 0; g < EG; g++) {
+                    on[g] = false;
+                    tv[g] = 0;
+                    fo[g] = 0;
+                    const int j = js[g];
+                    if (j < 0) continue;
+                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
+                    if (nx * ny > 64) continue;
+                    const int p = lane;
+                    if (p < nx * ny) {
+                        const float inv = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, inv_l), j));
+                        const int py = (int)(((float)p + 0.5f) * inv);
+                        const int pxx = p - py * nx;
+                        const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
+                        const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
+                        const int swj = readlane(sw, j);
+                        int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
+                        const int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
+                        if (readlane(mir, j)) scol = swj - 1 - scol;
+                        tv[g] = d.pixels[(uint32_t)readlane(soff, j) + (uint32_t)(srow * swj + scol)];
+                        fo[g] = (readlane(ey.t1, j) + py) * PG_RES + readlane(ex.t1, j) + pxx;
+                        on[g] = true;
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < EG; g++) {
+                    const int j = js[g];
+                    if (j < 0) continue;
+                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
+                    const int caj = readlane(ca, j);
+                    if (nx * ny <= 64) {
+                        if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
+                    } else {
+                        const int tx = readlane(ex.t1, j), ty = readlane(ey.t1, j);
+                        const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
+                        const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
+                        const uint32_t offj = (uint32_t)readlane(soff, j);
+                        const int swj = readlane(sw, j), mirj = readlane(mir, j);
+                        const float inv = 1.0f / (float)nx;
+                        for (int p = lane; p < nx * ny; p += 64) {
+                            int py = (int)(((float)p + 0.5f) * inv);
+                            int pxx = p - py * nx;
+                            int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
+                            int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
+                            if (mirj) scol = swj - 1 - scol;
+                            uint32_t src = d.pixels[offj + (uint32_t)(srow * swj + scol)];
+                            int o = (ty + py) * PG_RES + tx + pxx;
+                            fb[o] = blend_argb_pm(fb[o], src, caj);
+                        }
+                    }
+                    wave_sync();
+                }
             }
         }
     }
