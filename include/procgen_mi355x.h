@@ -61,6 +61,8 @@ LIBENV_API const char *procgen_error_string(libenv_env *env);
  * out[0] = step kernel ms, out[1] = reset kernel ms, out[2] = render kernel ms (averages). */
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n);
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
+/* Diagnostic builds only (libprocgen_mi355x_prof.so): per-phase cycle sums, out[16]. */
+LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out);
 /* Debug read-back of one env's scalar state, see pg_engine.h PGEnv (returns bytes copied). */
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length);
 

@@ -347,6 +347,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.reset_queue, n);
     rc |= dalloc(v, &d.reset_count, 1);
     rc |= dalloc(v, &d.error_any, 1);
+    rc |= dalloc(v, &d.prof, n * 16); // written only by PG_PROFILE (diagnostic) builds
     if (rc) {
         libenv_close(v);
         return bad("device allocation failed");
@@ -576,6 +577,19 @@ LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     }
     for (int i = 0; i < n && i < 4; i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;
     return v->t_used;
+}
+
+// Diagnostic builds (make PROFILE=1): per-phase s_memtime cycle sums over all envs since
+// creation; out[0..7] step-kernel phases, out[8..15] render-kernel phases.
+LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out) {
+    VecEnv *v = (VecEnv *)env;
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    std::vector<uint64_t> h((size_t)v->num_envs * 16);
+    HIPCHECK(hipMemcpy(h.data(), v->dev.prof, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 16; k++) out[k] = 0;
+    for (size_t e = 0; e < (size_t)v->num_envs; e++)
+        for (int k = 0; k < 16; k++) out[k] += h[e * 16 + k];
+    return 0;
 }
 
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length) {

@@ -56,6 +56,30 @@ DEV bool cr_is_lava(int t) { return t == CR_LAVA_MID || t == CR_LAVA_TOP; }
 
 DEV void wave_sync() { __syncthreads(); }
 
+// Per-phase cycle accounting for diagnostic builds (make PROFILE=1): never in the product .so.
+struct PTimer {
+#ifdef PG_PROFILE
+    uint64_t last, acc[8];
+    DEV void start() {
+        last = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < 8; k++) acc[k] = 0;
+    }
+    DEV void mark(int k) {
+        uint64_t t = __builtin_amdgcn_s_memtime();
+        acc[k] += t - last;
+        last = t;
+    }
+    DEV void flush(uint64_t *p) {
+        if (LANE == 0 && p)
+            for (int k = 0; k < 8; k++) p[k] += acc[k];
+    }
+#else
+    DEV void start() {}
+    DEV void mark(int) {}
+    DEV void flush(uint64_t *) {}
+#endif
+};
+
 DEV unsigned long long ballot(bool p) { return __ballot(p); }
 DEV int top_bit(unsigned long long m) { return 63 - __clzll(m); }
 

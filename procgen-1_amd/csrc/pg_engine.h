@@ -149,6 +149,7 @@ struct PGDev {
     int32_t *reset_queue;     // [num_envs] env ids needing a reset this step
     int32_t *reset_count;     // [1]
     int32_t *error_any;       // [1] OR of all env errors
+    uint64_t *prof;           // [num_envs][16] per-phase s_memtime sums (PG_PROFILE builds only)
     // atlas
     const uint32_t *pixels;
     const int32_t *sprites;   // [PG_NUM_SLOTS][4] (offset, w, h, pad)

@@ -123,6 +123,8 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     v.y_off = v.unit * (v.center_y - v.view_dim / 2);
 
     const int lane = LANE;
+    PTimer pt;
+    pt.start();
 
     // ---- grid type -> sprite table (theme_for_grid_obj coinrun.cpp:133-138, image_for_type :213-225,
     //      draw_image basic-abstract-game.cpp:886-922)
@@ -227,15 +229,18 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         }
     }
     wave_sync();
-    auto tile_lookup = [&](int x, int y) -> int {
-        if (use_win) return win[(y - low_y) * ww + (x - low_x)];
+    auto lookup_win = [&](int x, int y) -> int { return win[(y - low_y) * ww + (x - low_x)]; };
+    auto lookup_grid = [&](int x, int y) -> int {
         int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
                                                                                : s.out_of_bounds_object;
         return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
     };
 
+    pt.mark(0);
     // ---- pixel-centric background + tiles, RB rows per batch: every texel load of the batch
-    //      is issued before the first blend, so one memory round trip serves RB rows
+    //      is issued before the first blend, so one memory round trip serves RB rows.  Two
+    //      instantiations so the common (windowed) one has no grid load between texel loads.
+    auto tile_pass = [&](auto tile_lookup) {
     for (int r0 = 0; r0 < PG_RES; r0 += RB) {
         uint32_t bgv[RB], tex[RB][4];
         uint32_t valid = 0;
@@ -243,10 +248,10 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         for (int k = 0; k < RB; k++) {
             const int row = r0 + k;
             const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
-            bgv[k] = 0xff000000u;
-            if (inb) {
+            {   // branch-free: an out-of-blit pixel loads pixels[0] and discards it
                 uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-                bgv[k] = d.pixels[bg_col_base + srow * (uint32_t)bgi.y];
+                uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
+                bgv[k] = inb ? v : 0xff000000u;
             }
             const int nr = readlane(ncy, row);
             const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
@@ -254,17 +259,15 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 const int kk = c >> 1, l = c & 1;
+                const bool cand = kk < ncx && l < nr;
+                const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
+                const int off = cand ? tile_lookup(x, y) : -1;
+                if (off <= -2) err = true;
+                const bool on = off >= 0;
+                const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
                 tex[k][c] = 0;
-                if (kk < ncx && l < nr) {
-                    const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
-                    const int off = tile_lookup(x, y);
-                    if (off <= -2) err = true;
-                    if (off >= 0) {
-                        const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
-                        tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
-                        valid |= 1u << (k * 4 + c);
-                    }
-                }
+                if (on) tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
+                valid |= (on ? 1u : 0u) << (k * 4 + c);
             }
         }
 #pragma unroll
@@ -276,8 +279,12 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
             fb[(r0 + k) * PG_RES + lane] = px;
         }
     }
+    };
+    if (use_win) tile_pass(lookup_win);
+    else tile_pass(lookup_grid);
     wave_sync();
 
+    pt.mark(1);
     // ---- entities, render_z 0 then 1, in list order (basic-abstract-game.cpp:966-967, 1061-1075)
     const int n = s.num_ents;
     for (int z = 0; z <= 1; z++) {
@@ -394,6 +401,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         }
     }
 
+    pt.mark(2);
     // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
     uint8_t *out = d.rgb + (size_t)env * PG_OBS_BYTES;
     for (int q = lane; q < PG_RES * PG_RES / 4; q += 64) {
@@ -408,6 +416,8 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         o[2] = w2;
     }
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
+    pt.mark(3);
+    pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 
 extern "C" void pg_launch_render(const PGDev *d, hipStream_t s) {

@@ -17,6 +17,13 @@ struct Ctx {
     uint32_t *lds;  // 624-word twist staging
     int16_t *ilist; // LDS: ascending indices of entities that can interact in sub_step
     int nlist;
+    int8_t *grid8;  // LDS copy of the grid
+    bool grid8_ok;
+    bool ireg;      // interactors cached per lane (see build_interactor_list)
+    int i_idx;
+    float i_x, i_y, i_rx, i_ry;
+    bool i_erase;
+    PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
 };
 
 DEV float &EF(Ctx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
@@ -70,10 +77,81 @@ DEV void entity_step(Ent &e) {
     e.alpha = e.alpha_decay * e.alpha;
 }
 
+// Entity::step of one slot in place (lane-parallel form): reads the fields the update
+// depends on and writes back only the words whose bits changed.
+DEV void entity_step_slot(Ctx &c, int i) {
+    int flags = EI(c, F_FLAGS, i);
+    float x = EF(c, F_X, i), y = EF(c, F_Y, i), vx = EF(c, F_VX, i), vy = EF(c, F_VY, i);
+    float rx = EF(c, F_RX, i), ry = EF(c, F_RY, i), rot = EF(c, F_ROTATION, i), vrot = EF(c, F_VROT, i);
+    float fr = EF(c, F_FRICTION, i), alpha = EF(c, F_ALPHA, i), decay = EF(c, F_ALPHA_DECAY, i);
+    float grow = EF(c, F_GROW_RATE, i);
+    int life = EI(c, F_LIFE_TIME, i), expire = EI(c, F_EXPIRE_TIME, i), type = EI(c, F_TYPE, i);
+    int img = EI(c, F_IMAGE_TYPE, i);
+    float nx = x, ny = y;
+    if (!(flags & EF_SMART_STEP)) {
+        nx = x + vx;
+        ny = y + vy;
+    }
+    float nrot = rot + vrot;
+    float nvx = vx * fr, nvy = vy * fr;
+    life += 1;
+    int nflags = flags;
+    if (expire > 0 && life > expire) nflags |= EF_WILL_ERASE;
+    int nimg = img;
+    if (type == EXPLOSION && img < EXPLOSION5) nimg = img + 1;
+    float nrx = rx * grow, nry = ry * grow;
+    float nalpha = decay * alpha;
+#define PG_SET_IF_CHANGED(F, oldv, newv) \
+    if (__float_as_uint(newv) != __float_as_uint(oldv)) EF(c, F, i) = newv;
+    PG_SET_IF_CHANGED(F_X, x, nx)
+    PG_SET_IF_CHANGED(F_Y, y, ny)
+    PG_SET_IF_CHANGED(F_ROTATION, rot, nrot)
+    PG_SET_IF_CHANGED(F_VX, vx, nvx)
+    PG_SET_IF_CHANGED(F_VY, vy, nvy)
+    PG_SET_IF_CHANGED(F_RX, rx, nrx)
+    PG_SET_IF_CHANGED(F_RY, ry, nry)
+    PG_SET_IF_CHANGED(F_ALPHA, alpha, nalpha)
+#undef PG_SET_IF_CHANGED
+    EI(c, F_LIFE_TIME, i) = life;
+    if (nflags != flags) EI(c, F_FLAGS, i) = nflags;
+    if (nimg != img) EI(c, F_IMAGE_TYPE, i) = nimg;
+}
+
 // ------------------------------------------------------------------ grid queries (basic-abstract-game.cpp:167-185)
+// The step reads the grid (never writes it), so the env's grid is copied once into LDS as
+// int8 (every coinrun cell value is a `char` from fill_elem or a small id from set_obj;
+// any value outside int8 falls back to HBM reads) and all probes hit LDS.
 DEV int get_obj(Ctx &c, int x, int y) {
     if (!(0 <= y && y < c.s.main_height && 0 <= x && x < c.s.main_width)) return c.s.out_of_bounds_object;
-    return c.G[y * c.s.main_width + x];
+    return c.grid8_ok ? (int)c.grid8[y * c.s.main_width + x] : (int)c.G[y * c.s.main_width + x];
+}
+
+DEV void load_grid_lds(Ctx &c) {
+    int cells = c.s.main_width * c.s.main_height;
+    bool bad = cells > PG_GRID_MAX;
+    if (!bad) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(c.G); // 8 int16 cells per 16 B
+        for (int k = LANE; k < (cells + 7) / 8; k += 64) {
+            uint4 v = src[k];
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t packed[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                uint32_t p = 0;
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    uint32_t word = w[h * 2 + q];
+                    int lo = (int16_t)(word & 0xffff), hi = (int16_t)(word >> 16);
+                    if (lo < -128 || lo > 127 || hi < -128 || hi > 127) bad = true;
+                    p |= ((uint32_t)(uint8_t)lo | ((uint32_t)(uint8_t)hi << 8)) << (16 * q);
+                }
+                packed[h] = p;
+            }
+            reinterpret_cast<uint2 *>(c.grid8)[k] = make_uint2(packed[0], packed[1]);
+        }
+    }
+    c.grid8_ok = ballot(bad) == 0;
+    wave_sync();
 }
 DEV int get_obj_from_floats(Ctx &c, float i, float j) {
     if (i < 0) return c.s.out_of_bounds_object;
@@ -131,6 +209,17 @@ DEV bool is_interactor(int type) { return type == CR_CRATE; }
 // Largest interactor index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
 // i.e. the next entity the reference's reverse loop would act on; lane-parallel over the list.
 DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
+    if (c.ireg) { // <= 64 static interactors: lane k holds interactor k in registers
+        int i = LANE < c.nlist ? c.i_idx : PG_CAP;
+        bool hit = false;
+        if (i < upper && i != oi && !c.i_erase) {
+            float tx = (o.rx + c.i_rx) + POS_EPS;
+            float ty = (o.ry + c.i_ry) + POS_EPS;
+            hit = (fabsf(o.x - c.i_x) < tx) && (fabsf(o.y - c.i_y) < ty);
+        }
+        unsigned long long m = ballot(hit);
+        return m ? __builtin_amdgcn_readlane(i, top_bit(m)) : -1;
+    }
     for (int base = (c.nlist - 1) & ~63; base >= 0; base -= 64) {
         int k = base + LANE;
         bool hit = false;
@@ -160,6 +249,23 @@ DEV void build_interactor_list(Ctx &c) {
     }
     c.nlist = cnt;
     wave_sync();
+    // Interactors whose Entity::step cannot change x, y, rx, ry or will_erase during this
+    // step (not smart, zero velocity, grow_rate 1, no expiry -- coinrun's crates) are held
+    // in registers for the whole step: lane k <-> interactor k.
+    c.ireg = false;
+    if (cnt <= 64) {
+        bool stat = true;
+        if (LANE < cnt) {
+            int i = c.ilist[LANE];
+            c.i_idx = i;
+            c.i_x = EF(c, F_X, i); c.i_y = EF(c, F_Y, i); c.i_rx = EF(c, F_RX, i); c.i_ry = EF(c, F_RY, i);
+            int fl = EI(c, F_FLAGS, i);
+            c.i_erase = (fl & EF_WILL_ERASE) != 0;
+            stat = !(fl & EF_SMART_STEP) && EF(c, F_VX, i) == 0 && EF(c, F_VY, i) == 0 &&
+                   EF(c, F_GROW_RATE, i) == 1 && EI(c, F_EXPIRE_TIME, i) <= 0;
+        }
+        c.ireg = ballot(!stat) == 0;
+    }
 }
 
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
@@ -310,12 +416,7 @@ DEV void step_entities(Ctx &c) {
         }
         for (int base = (sm + 1) & ~63; base <= hi; base += 64) {
             int i = base + LANE;
-            if (i > sm && i <= hi) {
-                Ent e;
-                load_ent(c, i, e);
-                entity_step(e);
-                store_ent(c, i, e);
-            }
+            if (i > sm && i <= hi) entity_step_slot(c, i);
         }
         wave_sync();
         if (sm < 0) break;
@@ -355,17 +456,19 @@ DEV void erase_if_needed(Ctx &c) {
     for (int base = 0; base < n; base += 64) {
         int i = base + LANE;
         bool keep = false;
-        Ent e;
         if (i < n) {
-            load_ent(c, i, e);
-            bool er = (e.flags & EF_WILL_ERASE) ||
-                      ((e.flags & EF_AUTO_ERASE) && is_out_of_bounds(c, e.x, e.y, e.rx, e.ry));
+            int fl = EI(c, F_FLAGS, i);
+            bool er = (fl & EF_WILL_ERASE) ||
+                      ((fl & EF_AUTO_ERASE) && is_out_of_bounds(c, EF(c, F_X, i), EF(c, F_Y, i), EF(c, F_RX, i), EF(c, F_RY, i)));
             keep = !er;
         }
         unsigned long long km = ballot(keep);
         int dst = kept + __popcll(km & ((1ull << LANE) - 1ull));
+        bool move = keep && dst != i;
+        Ent e;
+        if (move) load_ent(c, i, e); // only entities that shift are read whole
         wave_sync();
-        if (keep && dst != i) store_ent(c, dst, e);
+        if (move) store_ent(c, dst, e);
         wave_sync();
         kept += __popcll(km);
     }
@@ -419,6 +522,7 @@ DEV void coinrun_game_step(Ctx &c) {
     // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
     uint32_t *rg = c.d.mt + (size_t)c.env * 2 * PG_MT_WORDS;
     c.s.step_rand_int = rg_randint_of(mt_next_global(rg, c.s.rg_mti, c.lds), 0, 1000000);
+    c.pt.mark(0);
     c.s.move_action = c.s.action % 9;
     c.s.special_action = 0;
     if (c.s.action >= 9) {
@@ -441,8 +545,10 @@ DEV void coinrun_game_step(Ctx &c) {
         EF(c, F_VROT, 0) = vrot;
     }
     wave_sync();
+    c.pt.mark(1);
     build_interactor_list(c);
     step_entities(c);
+    c.pt.mark(2);
 
     // agent / entity collisions (:728-750).  coinrun effects are order-free flags:
     // ENEMY or SAW touching the agent ends the episode; only the agent reacts to grid cells.
@@ -487,7 +593,9 @@ DEV void coinrun_game_step(Ctx &c) {
             }
         }
     }
+    c.pt.mark(3);
     erase_if_needed(c);
+    c.pt.mark(4);
     float gx, gy, grx, gry;
     if (c.s.agent_erased) {
         gx = c.s.ghost_x; gy = c.s.ghost_y; grx = c.s.ghost_rx; gry = c.s.ghost_ry;
@@ -553,6 +661,7 @@ DEV void coinrun_game_step(Ctx &c) {
     c.s.num_ents = n + total_enemies;
     wave_sync();
     c.s.last_agent_y = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+    c.pt.mark(5);
 }
 
 // splitmix64 counter hash used for synthetic random actions (bench / parity tests)
@@ -569,6 +678,7 @@ DEV uint64_t splitmix64(uint64_t x) {
 extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use_hash, uint64_t hash_seed, int32_t hash_t) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
+    __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     Ctx c;
     c.d = d;
     c.env = blockIdx.x;
@@ -580,6 +690,10 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
     c.lds = lds_mt;
     c.ilist = lds_list;
     c.nlist = 0;
+    c.grid8 = lds_grid;
+    c.grid8_ok = false;
+    c.pt.start();
+    load_grid_lds(c);
 
     int action;
     if (use_hash) {
@@ -624,8 +738,19 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
         d.prev_level_complete[c.env] = (uint8_t)c.s.sd_level_complete;
         d.level_seed[c.env] = c.s.current_level_seed;
         if (c.s.error) atomicOr(d.error_any, 1 << c.s.error);
-        d.envs[c.env] = c.s;
+        // write back only the PGEnv members this kernel can change (the rest is read-only here)
+        PGEnv *o = d.envs + c.env;
+#define PG_W(f) o->f = c.s.f;
+        PG_W(action) PG_W(cur_time) PG_W(sd_reward) PG_W(sd_done) PG_W(sd_level_complete) PG_W(total_reward)
+        PG_W(last_reward_timer) PG_W(last_reward) PG_W(prev_level_seed) PG_W(episode_done) PG_W(num_ents)
+        PG_W(agent_erased) PG_W(ghost_x) PG_W(ghost_y) PG_W(ghost_vx) PG_W(ghost_vy) PG_W(ghost_rx) PG_W(ghost_ry)
+        PG_W(move_action) PG_W(special_action) PG_W(last_move_action) PG_W(action_vx) PG_W(action_vy)
+        PG_W(action_vrot) PG_W(step_rand_int) PG_W(rg_mti) PG_W(has_support) PG_W(facing_right)
+        PG_W(is_on_crate) PG_W(last_agent_y) PG_W(error)
+#undef PG_W
     }
+    c.pt.mark(6);
+    c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 }
 
 extern "C" void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t) {

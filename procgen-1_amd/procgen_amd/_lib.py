@@ -11,7 +11,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libprocgen_mi355x.so")
+# PROCGEN_MI355X_LIB=prof selects the diagnostic build (per-phase cycle counters)
+LIB_PATH = os.path.join(HERE, "libprocgen_mi355x_prof.so" if os.environ.get("PROCGEN_MI355X_LIB") == "prof"
+                        else "libprocgen_mi355x.so")
 
 LIBENV_MAX_NAME_LEN = 128
 LIBENV_MAX_NDIM = 16
@@ -78,6 +80,7 @@ SIGNATURES = {
     "procgen_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "procgen_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "procgen_debug_env": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "procgen_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _LIB = None

@@ -1,0 +1,10 @@
+# tests -> bench -> phase profile (diagnostic build), each under its own time limit
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/tests.log 2>&1
+rc=$?; tail -3 gpurun_out/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
+timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phase.json 2>/dev/null
+rc=$?; cat gpurun_out/phase.json; exit $rc
