@@ -336,6 +336,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.envs, n);
     rc |= dalloc(v, &d.ents, (size_t)PG_NF * n * PG_CAP);
     rc |= dalloc(v, &d.grid, n * PG_GRID_MAX);
+    rc |= dalloc(v, &d.grid8, n * PG_GRID_MAX);
     rc |= dalloc(v, &d.mt, n * 2 * PG_MT_WORDS);
     rc |= dalloc(v, &d.actions, n);
     rc |= dalloc(v, &d.rgb, n * PG_OBS_BYTES);
@@ -658,6 +659,7 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
         return;
     }
     size_t plane = (size_t)v->num_envs * PG_CAP;
+    s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
     hipMemcpy(v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     for (int f = 0; f < PG_NF; f++) {
         if (ents) hipMemcpy(v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);

@@ -125,7 +125,8 @@ struct PGEnv {
     int32_t rg_mti;           // rand_gen position (mt words live in the mt plane)
     int32_t lsg_mti;          // level_seed_rand_gen position
     int32_t error;            // PG_ERR_* of this env (sticky)
-    int32_t pad[128 - 67];
+    int32_t grid8_ok;         // the int8 grid mirror is current (written at reset)
+    int32_t pad[128 - 68];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
@@ -138,6 +139,7 @@ struct PGDev {
     PGEnv *envs;
     float *ents;              // PG_NF planes of num_envs * PG_CAP words (int planes reinterpret)
     int16_t *grid;            // num_envs * PG_GRID_MAX
+    int8_t *grid8;            // num_envs * PG_GRID_MAX: int8 mirror for the step kernel's LDS copy
     uint32_t *mt;             // num_envs * 2 * PG_MT_WORDS
     int32_t *actions;         // num_envs
     uint8_t *rgb;             // num_envs * PG_OBS_BYTES

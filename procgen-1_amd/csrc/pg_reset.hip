@@ -311,6 +311,26 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool 
     const uint4 *src = reinterpret_cast<const uint4 *>(lds_grid);
     uint4 *dst = reinterpret_cast<uint4 *>(g);
     for (int i = LANE; i < (cells + 7) / 8; i += 64) dst[i] = src[i];
+    // int8 mirror for the step kernel (valid when every cell fits, always for coinrun)
+    bool fits = true;
+    int8_t *g8 = d.grid8 + (size_t)env * PG_GRID_MAX;
+    for (int i = LANE; i < (cells + 15) / 16; i += 64) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                int cell = i * 16 + q * 4 + b;
+                int v = cell < cells ? (int)lds_grid[cell] : 0;
+                if (v < -128 || v > 127) fits = false;
+                word |= (uint32_t)(uint8_t)v << (8 * b);
+            }
+            w[q] = word;
+        }
+        reinterpret_cast<uint4 *>(g8)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    c.s.grid8_ok = ballot(!fits) == 0;
     if (LANE == 0) {
         d.level_seed[env] = c.s.current_level_seed;
         if (initial) { // first observation of set_buffers (vecgame.cpp:381-409): step_data from the ctor

@@ -17,6 +17,7 @@ struct Ctx {
     uint32_t *lds;  // 624-word twist staging
     int16_t *ilist; // LDS: ascending indices of entities that can interact in sub_step
     int nlist;
+    int16_t *slist; // LDS: smart entity indices (fast step_entities path)
     int8_t *grid8;  // LDS copy of the grid
     bool grid8_ok;
     bool ireg;      // interactors cached per lane (see build_interactor_list)
@@ -129,6 +130,13 @@ DEV int get_obj(Ctx &c, int x, int y) {
 DEV void load_grid_lds(Ctx &c) {
     int cells = c.s.main_width * c.s.main_height;
     bool bad = cells > PG_GRID_MAX;
+    if (!bad && c.s.grid8_ok) { // int8 mirror written by the last reset: 4 KB per env
+        const uint4 *src = reinterpret_cast<const uint4 *>(c.d.grid8 + (size_t)c.env * PG_GRID_MAX);
+        for (int k = LANE; k < (cells + 15) / 16; k += 64) reinterpret_cast<uint4 *>(c.grid8)[k] = src[k];
+        c.grid8_ok = true;
+        wave_sync();
+        return;
+    }
     if (!bad) {
         const uint4 *src = reinterpret_cast<const uint4 *>(c.G); // 8 int16 cells per 16 B
         for (int k = LANE; k < (cells + 7) / 8; k += 64) {
@@ -401,7 +409,66 @@ DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
 // basic-abstract-game.cpp:1095-1107: reverse order; runs of non-smart entities are
 // independent (Entity::step touches only its own entity) and are stepped lane-parallel
 // with slot i always owned by lane i % 64.
-DEV void step_entities(Ctx &c) {
+DEV float rlf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+DEV int rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+DEV void ent_readlane(const Ent &m, int l, Ent &o) {
+    o.x = rlf(m.x, l); o.y = rlf(m.y, l); o.vx = rlf(m.vx, l); o.vy = rlf(m.vy, l);
+    o.rx = rlf(m.rx, l); o.ry = rlf(m.ry, l); o.rotation = rlf(m.rotation, l); o.vrot = rlf(m.vrot, l);
+    o.alpha = rlf(m.alpha, l); o.alpha_decay = rlf(m.alpha_decay, l); o.grow_rate = rlf(m.grow_rate, l);
+    o.friction = rlf(m.friction, l); o.collision_margin = rlf(m.collision_margin, l);
+    o.health = rlf(m.health, l); o.theta = rlf(m.theta, l); o.climber_spawn_x = rlf(m.climber_spawn_x, l);
+    o.type = rli(m.type, l); o.image_type = rli(m.image_type, l); o.image_theme = rli(m.image_theme, l);
+    o.render_z = rli(m.render_z, l); o.life_time = rli(m.life_time, l); o.expire_time = rli(m.expire_time, l);
+    o.fire_time = rli(m.fire_time, l); o.spawn_time = rli(m.spawn_time, l); o.flags = rli(m.flags, l);
+}
+
+// Fast path of step_entities.  Within step_entities an entity's fields are written only
+// by its own basic_step_object / Entity::step (push_obj moves the stepped object itself,
+// the scans read only the register-cached static interactors), so every smart entity can
+// be loaded lane-parallel up front (lane k <-> k-th smart entity), stepped from registers
+// in the reference's reverse order, and stored lane-parallel at the end.
+DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
+    int n = c.s.num_ents;
+    int nsm = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        bool smart = i < n && (EI(c, F_FLAGS, i) & EF_SMART_STEP);
+        unsigned long long m = ballot(smart);
+        int pos = nsm + __popcll(m & ((1ull << LANE) - 1ull));
+        if (smart && pos < 64) slist[pos] = (int16_t)i;
+        nsm += __popcll(m);
+    }
+    if (nsm > 64 || !c.ireg) return false;
+    wave_sync();
+    Ent mine;
+    int my_i = LANE < nsm ? slist[LANE] : 0;
+    if (LANE < nsm) load_ent(c, my_i, mine);
+    int hi = n - 1;
+    for (int j = nsm - 1; j >= 0; j--) {
+        int sm = rli(my_i, j);
+        for (int base = (sm + 1) & ~63; base <= hi; base += 64) {
+            int i = base + LANE;
+            if (i > sm && i <= hi) entity_step_slot(c, i);
+        }
+        Ent o;
+        ent_readlane(mine, j, o);
+        basic_step_object(c, sm, o);
+        entity_step(o);
+        if (LANE == j) mine = o;
+        hi = sm - 1;
+    }
+    for (int base = 0; base <= hi; base += 64) {
+        int i = base + LANE;
+        if (i <= hi) entity_step_slot(c, i);
+    }
+    if (LANE < nsm) store_ent(c, my_i, mine);
+    wave_sync();
+    return true;
+}
+
+DEV void step_entities(Ctx &c, int16_t *slist) {
+    if (step_entities_fast(c, slist)) return;
     int hi = c.s.num_ents - 1;
     while (hi >= 0) {
         int sm = -1;
@@ -547,7 +614,7 @@ DEV void coinrun_game_step(Ctx &c) {
     wave_sync();
     c.pt.mark(1);
     build_interactor_list(c);
-    step_entities(c);
+    step_entities(c, c.slist);
     c.pt.mark(2);
 
     // agent / entity collisions (:728-750).  coinrun effects are order-free flags:
@@ -678,6 +745,7 @@ DEV uint64_t splitmix64(uint64_t x) {
 extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use_hash, uint64_t hash_seed, int32_t hash_t) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
+    __shared__ int16_t lds_slist[64];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     Ctx c;
     c.d = d;
@@ -689,6 +757,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
     c.G = d.grid + (size_t)c.env * PG_GRID_MAX;
     c.lds = lds_mt;
     c.ilist = lds_list;
+    c.slist = lds_slist;
     c.nlist = 0;
     c.grid8 = lds_grid;
     c.grid8_ok = false;
