@@ -6,5 +6,5 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_
 rc=$?; tail -3 gpurun_out/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; cat gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; }
-timeout -k 10 300 python tools/phase_profile.py > gpurun_out/phase.json 2>/dev/null
+timeout -k 10 300 python scripts/phase_profile.py > gpurun_out/phase.json 2>/dev/null
 rc=$?; cat gpurun_out/phase.json; exit $rc

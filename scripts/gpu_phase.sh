@@ -1,4 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python tools/phase_profile.py 2>&1 | tee gpurun_out/phase.json | tail -30
+timeout -k 10 300 python scripts/phase_profile.py 2>&1 | tee gpurun_out/phase.json | tail -30
