@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/libenv.h"
@@ -115,6 +116,8 @@ struct VecEnv {
     int32_t *d_sprites = nullptr, *d_bgs = nullptr, *d_themes = nullptr;
     std::vector<int32_t> h_actions;
     std::vector<uint8_t> h_staging;
+    uint8_t *pinned = nullptr;  // page-locked landing zone of copy_out (all output planes)
+    size_t pinned_bytes = 0;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev; // 4 per timed step: before step, after step, after reset, after render
@@ -195,26 +198,61 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     return 0;
 }
 
+// Host memcpy, split over a few threads for large frames (805 MB at 65,536 envs).
+static void host_copy(void *dst, const void *src, size_t bytes) {
+    const size_t chunk = 32u << 20;
+    if (bytes <= 2 * chunk) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 2 ? 2 : (nt > 8 ? 8 : nt);
+    std::vector<std::thread> th;
+    size_t per = (bytes + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; t++) {
+        size_t lo = per * t, hi = lo + per < bytes ? lo + per : bytes;
+        if (lo >= hi) break;
+        th.emplace_back([=] { memcpy((char *)dst + lo, (const char *)src + lo, hi - lo); });
+    }
+    for (auto &x : th) x.join();
+}
+
 int copy_out(VecEnv *v) {
-    // device -> the caller's per-env host pointers (contiguous runs become one copy)
-    int n = v->num_envs;
-    auto copy_plane = [&](const void *dsrc, size_t elem, void **ptrs) -> int {
-        int e = 0;
+    // device planes -> one page-locked landing zone (DMA, ordered on the env's stream) ->
+    // the caller's per-env host pointers (contiguous runs become one memcpy).  Landing in
+    // pinned memory first keeps the caller's pageable buffers out of the async copy path.
+    const size_t n = (size_t)v->num_envs;
+    const size_t sizes[6] = {PG_OBS_BYTES, 4, 1, 4, 1, 4};
+    const void *dsrc[6] = {v->dev.rgb, v->dev.rew, v->dev.first, v->dev.prev_level_seed,
+                           v->dev.prev_level_complete, v->dev.level_seed};
+    size_t off[7];
+    off[0] = 0;
+    for (int k = 0; k < 6; k++) off[k + 1] = off[k] + ((sizes[k] * n + 255) & ~(size_t)255);
+    if (v->pinned_bytes < off[6]) {
+        if (v->pinned) (void)hipHostFree(v->pinned);
+        v->pinned = nullptr;
+        v->pinned_bytes = 0;
+        HIPCHECK(hipHostMalloc((void **)&v->pinned, off[6], hipHostMallocDefault));
+        v->pinned_bytes = off[6];
+    }
+    for (int k = 0; k < 6; k++)
+        HIPCHECK(hipMemcpyAsync(v->pinned + off[k], dsrc[k], sizes[k] * n, hipMemcpyDeviceToHost, v->stream));
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    auto scatter = [&](const uint8_t *src, size_t elem, void **ptrs) {
+        size_t e = 0;
         while (e < n) {
-            int k = e + 1;
+            size_t k = e + 1;
             while (k < n && (char *)ptrs[k] == (char *)ptrs[k - 1] + elem) k++;
-            HIPCHECK(hipMemcpyAsync(ptrs[e], (const char *)dsrc + elem * e, elem * (k - e), hipMemcpyDeviceToHost, v->stream));
+            host_copy(ptrs[e], src + elem * e, elem * (k - e));
             e = k;
         }
-        return 0;
     };
-    if (copy_plane(v->dev.rgb, PG_OBS_BYTES, &v->ob_ptrs[0])) return -1;
-    HIPCHECK(hipMemcpyAsync(v->rew_host, v->dev.rew, sizeof(float) * n, hipMemcpyDeviceToHost, v->stream));
-    HIPCHECK(hipMemcpyAsync(v->first_host, v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
-    if (copy_plane(v->dev.prev_level_seed, 4, &v->info_ptrs[0 * (size_t)n])) return -1;
-    if (copy_plane(v->dev.prev_level_complete, 1, &v->info_ptrs[1 * (size_t)n])) return -1;
-    if (copy_plane(v->dev.level_seed, 4, &v->info_ptrs[2 * (size_t)n])) return -1;
-    HIPCHECK(hipStreamSynchronize(v->stream));
+    scatter(v->pinned + off[0], PG_OBS_BYTES, &v->ob_ptrs[0]);
+    memcpy(v->rew_host, v->pinned + off[1], 4 * n);
+    memcpy(v->first_host, v->pinned + off[2], n);
+    scatter(v->pinned + off[3], 4, &v->info_ptrs[0 * n]);
+    scatter(v->pinned + off[4], 1, &v->info_ptrs[1 * n]);
+    scatter(v->pinned + off[5], 4, &v->info_ptrs[2 * n]);
     return 0;
 }
 
@@ -505,6 +543,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     if (!v) return;
     if (v->stream) hipStreamSynchronize(v->stream);
     for (void *p : v->allocs) hipFree(p);
+    if (v->pinned) (void)hipHostFree(v->pinned);
     for (auto &e : v->ev)
         if (e) hipEventDestroy(e);
     if (v->stream) hipStreamDestroy(v->stream);

@@ -76,8 +76,8 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 #define NTYPES 128
 // Tile images all have this size in coinrun (other sizes are flagged, not drawn wrongly).
 #define TILE_PX 128
-// Largest visible grid window cached in LDS (centred views span visibility + 3 cells).
-#define WIN 24
+// Most tile rows a frame may span on the fast path (centred coinrun views span 14-15).
+#define CROWS 16
 // Rows per batch of the pixel-centric pass, entities per stamping group.
 #define RB 8
 #define EG 8
@@ -87,7 +87,7 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
     __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, <= -2: unsupported
-    __shared__ int win[WIN * WIN];    // tile_off of every cell of the visible window
+    __shared__ int colb[CROWS * 64];  // fast path: texel base of lane's first tile column per tile row
     const int env = blockIdx.x;
     const PGEnv s = d.envs[env];
     const int16_t *G = d.grid + (size_t)env * PG_GRID_MAX;
@@ -214,74 +214,151 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
             }
         }
     }
-    wave_sync();
 
-    // ---- visible grid window -> sprite offsets in LDS (one lookup per tile candidate)
-    const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
-    const bool use_win = ww > 0 && wh > 0 && ww <= WIN && wh <= WIN;
-    if (use_win) {
-        for (int idx = lane; idx < ww * wh; idx += 64) {
-            int yy = idx / ww, xx = idx - yy * ww;
-            int x = low_x + xx, y = low_y + yy;
-            int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
-                                                                                   : s.out_of_bounds_object;
-            win[idx] = type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
-        }
+    // ---- lookups for the fast path: every screen row's tile rows lie in [jy0, jy1]; for
+    //      each of those rows the texel base of this lane's first tile column goes to LDS
+    //      (colb), so a pixel costs one LDS read + one texel load + one blend.
+    int jlo = ncy > 0 ? ry0 : 0x7fffffff, jhi = ncy > 1 ? ry1 : (ncy > 0 ? ry0 : -0x7fffffff);
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        jlo = min(jlo, __shfl_xor(jlo, sh));
+        jhi = max(jhi, __shfl_xor(jhi, sh));
     }
-    wave_sync();
-    auto lookup_win = [&](int x, int y) -> int { return win[(y - low_y) * ww + (x - low_x)]; };
+    const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
+    const bool fast = nrows <= CROWS;
     auto lookup_grid = [&](int x, int y) -> int {
         int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
                                                                                : s.out_of_bounds_object;
         return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
     };
-
-    pt.mark(0);
-    // ---- pixel-centric background + tiles, RB rows per batch: every texel load of the batch
-    //      is issued before the first blend, so one memory round trip serves RB rows.  Two
-    //      instantiations so the common (windowed) one has no grid load between texel loads.
-    auto tile_pass = [&](auto tile_lookup) {
-    for (int r0 = 0; r0 < PG_RES; r0 += RB) {
-        uint32_t bgv[RB], tex[RB][4];
-        uint32_t valid = 0;
+    wave_sync(); // tile_off complete
+    if (fast) {
+        int code[CROWS];
 #pragma unroll
-        for (int k = 0; k < RB; k++) {
-            const int row = r0 + k;
-            const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
-            {   // branch-free: an out-of-blit pixel loads pixels[0] and discards it
-                uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-                uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
-                bgv[k] = inb ? v : 0xff000000u;
-            }
-            const int nr = readlane(ncy, row);
-            const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
-            const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const int kk = c >> 1, l = c & 1;
-                const bool cand = kk < ncx && l < nr;
-                const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
-                const int off = cand ? tile_lookup(x, y) : -1;
-                if (off <= -2) err = true;
-                const bool on = off >= 0;
-                const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
-                tex[k][c] = 0;
-                if (on) tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
-                valid |= (on ? 1u : 0u) << (k * 4 + c);
+        for (int j = 0; j < CROWS; j++) {
+            code[j] = -1;
+            if (j < nrows && ncx > 0) {
+                const int y = jy0 + j, x = cx0;
+                if (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) code[j] = G[y * s.main_width + x];
+                else code[j] = s.out_of_bounds_object;
             }
         }
 #pragma unroll
-        for (int k = 0; k < RB; k++) {
-            uint32_t px = bgv[k];
-#pragma unroll
-            for (int c = 0; c < 4; c++) // draw order: (x0,y0) (x0,y1) (x1,y0) (x1,y1)
-                if (valid & (1u << (k * 4 + c))) px = tex[k][c] + BYTE_MUL(px, (~tex[k][c]) >> 24);
-            fb[(r0 + k) * PG_RES + lane] = px;
+        for (int j = 0; j < CROWS; j++) {
+            if (j < nrows) {
+                int t = code[j];
+                int c = (ncx == 0 || t == INVALID_OBJ) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
+                if (c <= -2) err = true;
+                colb[j * 64 + lane] = c >= 0 ? c + scol0 : -1;
+            }
         }
     }
-    };
-    if (use_win) tile_pass(lookup_win);
-    else tile_pass(lookup_grid);
+    wave_sync();
+
+    pt.mark(0);
+    if (fast) {
+        // ---- background + first tile column, pixel-centric, RB rows per batch (all loads of
+        //      a batch are issued before the first blend).  A transparent texel (0) blends to
+        //      the unchanged pixel exactly, so lanes without a tile carry 0.
+        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+            uint32_t bgv[RB], ta[RB], tb[RB];
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int row = r0 + k;
+                const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
+                {   // branch-free: an out-of-blit pixel loads pixels[0] and discards it
+                    uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
+                    uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
+                    bgv[k] = inb ? v : 0xff000000u;
+                }
+                const int nr = readlane(ncy, row);
+                ta[k] = 0;
+                tb[k] = 0;
+                if (nr > 0) {
+                    const int ja = readlane(ry0, row) - jy0, sra = readlane(srow0, row);
+                    const int cb = colb[ja * 64 + lane];
+                    if (cb >= 0) ta[k] = d.pixels[(uint32_t)cb + (uint32_t)(sra * TILE_PX)];
+                }
+                if (nr > 1) {
+                    const int jb = readlane(ry1, row) - jy0, srb = readlane(srow1, row);
+                    const int cb = colb[jb * 64 + lane];
+                    if (cb >= 0) tb[k] = d.pixels[(uint32_t)cb + (uint32_t)(srb * TILE_PX)];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int nr = readlane(ncy, r0 + k);
+                uint32_t px = bgv[k];
+                if (nr > 0) px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
+                if (nr > 1) px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
+                fb[(r0 + k) * PG_RES + lane] = px;
+            }
+        }
+        wave_sync();
+        // ---- second tile column of the few screen columns two tiles overlap (RENDER_EPS):
+        //      drawn after the first column's tiles, which is the reference's x-major order.
+        //      Lane = screen row here, so the row tables are lane-local.
+        unsigned long long m2 = ballot(ncx > 1);
+        while (m2) {
+            const int c = __ffsll((long long)m2) - 1;
+            m2 &= m2 - 1;
+            const int x1 = readlane(cx1, c), sc1 = readlane(scol1, c);
+            const int row = lane;
+            if (ncy > 0) {
+                uint32_t px = fb[row * PG_RES + c];
+                for (int l = 0; l < ncy; l++) {
+                    const int code = lookup_grid(x1, l ? ry1 : ry0);
+                    if (code <= -2) err = true;
+                    if (code >= 0) {
+                        const uint32_t t = d.pixels[(uint32_t)code + (uint32_t)((l ? srow1 : srow0) * TILE_PX + sc1)];
+                        px = t + BYTE_MUL(px, (~t) >> 24);
+                    }
+                }
+                fb[row * PG_RES + c] = px;
+            }
+        }
+    } else {
+        // ---- generic pixel-centric pass (uncentred / very large views): a pixel blends every
+        //      tile covering it (<= 2 columns x 2 rows) in the reference's x-major order.
+        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+            uint32_t bgv[RB], tex[RB][4];
+            uint32_t valid = 0;
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int row = r0 + k;
+                const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
+                {
+                    uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
+                    uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
+                    bgv[k] = inb ? v : 0xff000000u;
+                }
+                const int nr = readlane(ncy, row);
+                const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
+                const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const int kk = c >> 1, l = c & 1;
+                    const bool cand = kk < ncx && l < nr;
+                    const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
+                    const int off = cand ? lookup_grid(x, y) : -1;
+                    if (off <= -2) err = true;
+                    const bool on = off >= 0;
+                    const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
+                    tex[k][c] = 0;
+                    if (on) tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
+                    valid |= (on ? 1u : 0u) << (k * 4 + c);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                uint32_t px = bgv[k];
+#pragma unroll
+                for (int c = 0; c < 4; c++) // draw order: (x0,y0) (x0,y1) (x1,y0) (x1,y1)
+                    if (valid & (1u << (k * 4 + c))) px = tex[k][c] + BYTE_MUL(px, (~tex[k][c]) >> 24);
+                fb[(r0 + k) * PG_RES + lane] = px;
+            }
+        }
+    }
     wave_sync();
 
     pt.mark(1);

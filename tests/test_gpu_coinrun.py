@@ -34,9 +34,11 @@ def assert_same(g, o, step, idx=None):
     for k in KEYS:
         np.testing.assert_array_equal(g[k][sel], o[k], err_msg="%s differs at step %d" % (k, step))
     if not np.array_equal(g["rgb"][sel], o["rgb"]):
-        diff = np.argwhere(np.any(g["rgb"][sel] != o["rgb"], axis=-1))
-        raise AssertionError("rgb differs at step %d: %d pixels, first (env,row,col) %s"
-                             % (step, len(diff), diff[:5].tolist()))
+        gg = g["rgb"][sel]
+        diff = np.argwhere(np.any(gg != o["rgb"], axis=-1))
+        vals = ["%s: %s vs %s" % (tuple(p), gg[tuple(p)].tolist(), o["rgb"][tuple(p)].tolist()) for p in diff[:8]]
+        raise AssertionError("rgb differs at step %d (idx %s): %d pixels, (env,row,col): engine vs oracle\n  %s"
+                             % (step, sel, len(diff), "\n  ".join(vals)))
 
 
 def run_pair(num, steps, oracle_kw, gpu_kw, seed=0):
@@ -178,3 +180,23 @@ def test_gpu_vs_committed_fixture():
             if t in frames_at:
                 np.testing.assert_array_equal(g["rgb"][0], z["frames"][frames_at.index(t), k])
         env.close()
+
+
+def test_gpu_determinism_two_engines():
+    """Two identical engines driven with the same actions produce identical outputs
+    (reference env_test.py determinism check, at scale: 16,384 envs, after other envs in
+    this process have dirtied device memory)."""
+    num = 16384
+    a = make_gpu(num, num_levels=200, start_level=0, rand_seed=0)
+    b = make_gpu(num, num_levels=200, start_level=0, rand_seed=0)
+    rng = np.random.RandomState(7)
+    for t in range(60):
+        if t:
+            act = rng.randint(0, 15, size=num).astype(np.int32)
+            a.act(act)
+            b.act(act)
+        ga, gb = gpu_obs(a), gpu_obs(b)
+        for k in KEYS + ["rgb"]:
+            np.testing.assert_array_equal(ga[k], gb[k], err_msg="%s differs at step %d" % (k, t))
+    a.close()
+    b.close()
