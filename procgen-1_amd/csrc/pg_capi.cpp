@@ -22,6 +22,18 @@ extern "C" {
 void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t);
 void pg_launch_reset(const PGDev *d, hipStream_t s, int all_envs, int grid);
 void pg_launch_render(const PGDev *d, hipStream_t s);
+void pg_launch_poison(hipStream_t s, uint32_t pattern);
+
+// PROCGEN_MI355X_POISON_LDS=1: scribble over LDS before every engine kernel (debug aid, see
+// pg_poison_lds_kernel); off by default
+static bool poison_lds() {
+    static const bool on = getenv("PROCGEN_MI355X_POISON_LDS") && getenv("PROCGEN_MI355X_POISON_LDS")[0] == '1';
+    return on;
+}
+#define PG_POISON(stream) \
+    do {                  \
+        if (poison_lds()) pg_launch_poison(stream, 0xFFFFFFFFu); \
+    } while (0)
 }
 
 namespace {
@@ -114,7 +126,7 @@ struct VecEnv {
     std::vector<void *> allocs;
     uint32_t *d_pixels = nullptr;
     int32_t *d_sprites = nullptr, *d_bgs = nullptr, *d_themes = nullptr;
-    std::vector<int32_t> h_actions;
+    int32_t *h_actions = nullptr; // page-locked staging of libenv_act's actions
     std::vector<uint8_t> h_staging;
     uint8_t *pinned = nullptr;  // page-locked landing zone of copy_out (all output planes)
     size_t pinned_bytes = 0;
@@ -135,6 +147,15 @@ struct VecEnv {
             return fail(v, PG_ERR_HIP, hipGetErrorString(e_));                           \
         }                                                                                \
     } while (0)
+
+// Every other host<->device copy is ordered on the env's own (non-blocking) stream and complete
+// on return: a null-stream hipMemcpy is not ordered with that stream, and from pageable
+// memory it may return before its DMA has landed (kernels could read half-written data).
+static hipError_t copy_sync(VecEnv *v, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, v->stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(v->stream);
+}
 
 int fail(VecEnv *v, int code, const char *msg) {
     if (v && !v->error) {
@@ -188,10 +209,13 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     }
     HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t), v->stream));
     if (e) HIPCHECK(hipEventRecord(e[0], v->stream));
+    PG_POISON(v->stream);
     pg_launch_step(&v->dev, v->stream, use_hash, seed, t);
     if (e) HIPCHECK(hipEventRecord(e[1], v->stream));
+    PG_POISON(v->stream);
     pg_launch_reset(&v->dev, v->stream, 0, 0);
     if (e) HIPCHECK(hipEventRecord(e[2], v->stream));
+    PG_POISON(v->stream);
     pg_launch_render(&v->dev, v->stream);
     if (e) HIPCHECK(hipEventRecord(e[3], v->stream));
     HIPCHECK(hipGetLastError());
@@ -258,7 +282,7 @@ int copy_out(VecEnv *v) {
 
 int check_device_errors(VecEnv *v) {
     int32_t flags = 0;
-    HIPCHECK(hipMemcpy(&flags, v->dev.error_any, 4, hipMemcpyDeviceToHost));
+    HIPCHECK(copy_sync(v, &flags, v->dev.error_any, 4, hipMemcpyDeviceToHost));
     if (flags && !v->error) {
         int code = __builtin_ctz((unsigned)flags);
         const char *msg = code == PG_ERR_ENTITY_OVERFLOW ? "entity capacity exceeded"
@@ -453,7 +477,11 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         libenv_close(v);
         return bad("device upload failed");
     }
-    v->h_actions.assign(n, 0);
+    if (hipHostMalloc((void **)&v->h_actions, (size_t)n * 4 + 4, hipHostMallocDefault) != hipSuccess) {
+        v->h_actions = nullptr;
+        libenv_close(v);
+        return bad("pinned host allocation failed");
+    }
     return (libenv_env *)v;
 }
 
@@ -476,10 +504,10 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
     if (dalloc(v, &v->d_pixels, (size_t)num_pixels) || dalloc(v, &v->d_sprites, PG_NUM_SLOTS * 4) ||
         dalloc(v, &v->d_bgs, (size_t)num_backgrounds * 4) || dalloc(v, &v->d_themes, 100))
         return -PG_ERR_HIP;
-    HIPCHECK(hipMemcpy(v->d_pixels, pixels, (size_t)num_pixels * 4, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(v->d_sprites, sprites, PG_NUM_SLOTS * sizeof(pg_image), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(v->d_bgs, backgrounds, (size_t)num_backgrounds * sizeof(pg_image), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(v->d_themes, num_themes, 100 * 4, hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_pixels, pixels, (size_t)num_pixels * 4, hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_sprites, sprites, PG_NUM_SLOTS * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_bgs, backgrounds, (size_t)num_backgrounds * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_themes, num_themes, 100 * 4, hipMemcpyHostToDevice));
     v->dev.pixels = v->d_pixels;
     v->dev.sprites = v->d_sprites;
     v->dev.backgrounds = v->d_bgs;
@@ -493,7 +521,9 @@ LIBENV_API int procgen_start(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     if (v->started) return 0;
+    PG_POISON(v->stream);
     pg_launch_reset(&v->dev, v->stream, 1, 0);
+    PG_POISON(v->stream);
     pg_launch_render(&v->dev, v->stream);
     HIPCHECK(hipGetLastError());
     v->started = true;
@@ -523,7 +553,7 @@ LIBENV_API void libenv_act(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     size_t n = (size_t)v->num_envs;
     for (size_t e = 0; e < n; e++) v->h_actions[e] = *(const int32_t *)v->ac_ptrs[e];
-    if (hipMemcpyAsync(v->dev.actions, v->h_actions.data(), n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess) {
+    if (hipMemcpyAsync(v->dev.actions, v->h_actions, n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess) {
         fail(v, PG_ERR_HIP, "action upload failed");
         return;
     }
@@ -544,6 +574,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     if (v->stream) hipStreamSynchronize(v->stream);
     for (void *p : v->allocs) hipFree(p);
     if (v->pinned) (void)hipHostFree(v->pinned);
+    if (v->h_actions) (void)hipHostFree(v->h_actions);
     for (auto &e : v->ev)
         if (e) hipEventDestroy(e);
     if (v->stream) hipStreamDestroy(v->stream);
@@ -625,7 +656,7 @@ LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out) {
     VecEnv *v = (VecEnv *)env;
     HIPCHECK(hipStreamSynchronize(v->stream));
     std::vector<uint64_t> h((size_t)v->num_envs * 16);
-    HIPCHECK(hipMemcpy(h.data(), v->dev.prof, h.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHECK(copy_sync(v, h.data(), v->dev.prof, h.size() * 8, hipMemcpyDeviceToHost));
     for (int k = 0; k < 16; k++) out[k] = 0;
     for (size_t e = 0; e < (size_t)v->num_envs; e++)
         for (int k = 0; k < 16; k++) out[k] += h[e * 16 + k];
@@ -636,7 +667,7 @@ LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int le
     VecEnv *v = (VecEnv *)env;
     if (env_idx < 0 || env_idx >= v->num_envs || length < (int)sizeof(PGEnv)) return -1;
     HIPCHECK(hipStreamSynchronize(v->stream));
-    HIPCHECK(hipMemcpy(out, v->dev.envs + env_idx, sizeof(PGEnv), hipMemcpyDeviceToHost));
+    HIPCHECK(copy_sync(v, out, v->dev.envs + env_idx, sizeof(PGEnv), hipMemcpyDeviceToHost));
     return (int)sizeof(PGEnv);
 }
 
@@ -650,7 +681,7 @@ LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
     if (env_idx < 0 || env_idx >= v->num_envs) return -1;
     if (hipStreamSynchronize(v->stream) != hipSuccess) return -1;
     PGEnv s;
-    if (hipMemcpy(&s, v->dev.envs + env_idx, sizeof(s), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (copy_sync(v, &s, v->dev.envs + env_idx, sizeof(s), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     size_t ents = (size_t)s.num_ents;
     size_t cells = (size_t)s.main_width * s.main_height;
     size_t need = 8 + sizeof(PGEnv) + ents * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
@@ -661,12 +692,12 @@ LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
     memcpy(p, &s, sizeof(s)); p += sizeof(s);
     size_t plane = (size_t)v->num_envs * PG_CAP;
     for (int f = 0; f < PG_NF; f++) {
-        if (ents && hipMemcpy(p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (ents && copy_sync(v, p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
         p += ents * 4;
     }
-    if (cells && hipMemcpy(p, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, cells * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (cells && copy_sync(v, p, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, cells * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     p += cells * 2;
-    if (hipMemcpy(p, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, 2 * PG_MT_WORDS * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (copy_sync(v, p, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, 2 * PG_MT_WORDS * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     p += 2 * PG_MT_WORDS * 4;
     memcpy(p, &END_OF_BUFFER, 4); p += 4;
     return (int)(p - data);
@@ -699,14 +730,14 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     }
     size_t plane = (size_t)v->num_envs * PG_CAP;
     s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
-    hipMemcpy(v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
+    copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     for (int f = 0; f < PG_NF; f++) {
-        if (ents) hipMemcpy(v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);
+        if (ents) copy_sync(v, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);
         p += ents * 4;
     }
-    if (cells) hipMemcpy(v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
+    if (cells) copy_sync(v, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
     p += cells * 2;
-    hipMemcpy(v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, p, 2 * PG_MT_WORDS * 4, hipMemcpyHostToDevice);
+    copy_sync(v, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, p, 2 * PG_MT_WORDS * 4, hipMemcpyHostToDevice);
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
     pg_launch_render(&v->dev, v->stream);

@@ -79,15 +79,24 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 // Most tile rows a frame may span on the fast path (centred coinrun views span 14-15).
 #define CROWS 16
 // Rows per batch of the pixel-centric pass, entities per stamping group.
+#ifndef RB
 #define RB 8
+#endif
+#ifndef EG
 #define EG 8
+#endif
 
 } // namespace
 
 extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
     __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, <= -2: unsupported
-    __shared__ int colb[CROWS * 64];  // fast path: texel base of lane's first tile column per tile row
+    // fast path: texel base of lane's first tile column per tile row.  Before it is built, the
+    // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row.
+    __shared__ __attribute__((aligned(16))) int colb[CROWS * 64];
+    static_assert(CROWS * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
+    int4 *const colax = reinterpret_cast<int4 *>(colb);
+    int4 *const rowax = colax + 64;
     const int env = blockIdx.x;
     const PGEnv s = d.envs[env];
     const int16_t *G = d.grid + (size_t)env * PG_GRID_MAX;
@@ -146,27 +155,6 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         tile_off[t] = off;
     }
 
-    // ---- draw_background (basic-abstract-game.cpp:988-1016): black fill + one scaled blit
-    Axis bx, by;
-    bool bg_ok = false;
-    int4 bgi = make_int4(0, 0, 0, 0);
-    if (s.opt_use_backgrounds) {
-        double mx, my, mw, mh;
-        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
-        bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
-        float bgw = (float)bgi.y, bgh = (float)bgi.z;
-        float bg_ar = bgw / bgh;
-        float world_ar = (float)(s.main_width * 1.0 / s.main_height);
-        float extra_w = bg_ar - world_ar;
-        float offset_x = s.bg_pct_x * extra_w;
-        // adjust_rect(main_rect, QRectF(-offset_x, 0, bg_ar / world_ar, 1)) (qt-utils.h:12-19)
-        double ax = (double)(-offset_x), aw = (double)(bg_ar / world_ar);
-        double rx = mx + mw * ax, ry = my + mh * 0.0, rw = mw * aw, rh = mh * 1.0;
-        bg_ok = axis_setup(rx, rw, bgi.y, bx) && axis_setup(ry, rh, bgi.z, by);
-    }
-    const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
-    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
-
     // ---- visible tile window (basic-abstract-game.cpp:937-948)
     int low_x, high_x, low_y, high_y;
     if (s.opt_center_agent) {
@@ -178,6 +166,61 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     } else {
         low_x = 0; high_x = s.main_width - 1; low_y = 0; high_y = s.main_height - 1;
     }
+    const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
+    // every tile column / row of the window gets its own lane for its Qt blit setup (lane 63:
+    // the background), so the double-precision setup runs once per tile, not per pixel
+    const bool tab = ww <= 63 && wh <= 63;
+
+    // ---- draw_background (basic-abstract-game.cpp:988-1016): black fill + one scaled blit
+    Axis bx, by;
+    bool bg_ok = false;
+    int4 bgi = make_int4(0, 0, 0, 0);
+    double bg_rx = 0, bg_ry = 0, bg_rw = 0, bg_rh = 0;
+    if (s.opt_use_backgrounds) {
+        double mx, my, mw, mh;
+        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
+        bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
+        float bgw = (float)bgi.y, bgh = (float)bgi.z;
+        float bg_ar = bgw / bgh;
+        float world_ar = (float)(s.main_width * 1.0 / s.main_height);
+        float extra_w = bg_ar - world_ar;
+        float offset_x = s.bg_pct_x * extra_w;
+        // adjust_rect(main_rect, QRectF(-offset_x, 0, bg_ar / world_ar, 1)) (qt-utils.h:12-19)
+        double ax = (double)(-offset_x), aw = (double)(bg_ar / world_ar);
+        bg_rx = mx + mw * ax; bg_ry = my + mh * 0.0; bg_rw = mw * aw; bg_rh = mh * 1.0;
+    }
+    if (tab) {
+        // one x-axis and one y-axis setup per lane: tile column low_x + lane, tile row
+        // low_y + lane, or (lane 63) the background
+        double xr = 0, xw = 0, yr = 0, yh = 0;
+        int xiw = 0, yih = 0;
+        if (lane == 63) {
+            if (s.opt_use_backgrounds) { xr = bg_rx; xw = bg_rw; xiw = bgi.y; yr = bg_ry; yh = bg_rh; yih = bgi.z; }
+        } else {
+            double rx, ry, rw, rh;
+            if (lane < ww) {
+                screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                xr = rx; xw = rw; xiw = TILE_PX;
+            }
+            if (lane < wh) {
+                screen_rect(v, 0.0f, (float)(low_y + lane + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                yr = ry; yh = rh; yih = TILE_PX;
+            }
+        }
+        Axis a, b;
+        const bool okx = axis_setup(xr, xw, xiw, a);
+        const bool oky = axis_setup(yr, yh, yih, b);
+        colax[lane] = make_int4(a.t1, okx ? a.n : 0, (int)a.base, a.step);
+        rowax[lane] = make_int4(b.t1, oky ? b.n : 0, (int)b.base, b.step);
+        bg_ok = readlane(okx && oky ? 1 : 0, 63) != 0;
+        bx.t1 = readlane(a.t1, 63); bx.n = readlane(a.n, 63); bx.base = (uint32_t)readlane((int)a.base, 63); bx.step = readlane(a.step, 63);
+        by.t1 = readlane(b.t1, 63); by.n = readlane(b.n, 63); by.base = (uint32_t)readlane((int)b.base, 63); by.step = readlane(b.step, 63);
+        wave_sync();
+    } else if (s.opt_use_backgrounds) {
+        bg_ok = axis_setup(bg_rx, bg_rw, bgi.y, bx) && axis_setup(bg_ry, bg_rh, bgi.z, by);
+    }
+    const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
+    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
 
     // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images
     int cx0 = 0, cx1 = 0, ncx = 0;
@@ -187,10 +230,18 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
         for (int x = xg - 2; x <= xg + 2; x++) {
             if (x < low_x || x > high_x || ncx == 2) continue;
-            double rx, ry, rw, rh;
-            screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
             Axis a;
-            if (axis_setup(rx, rw, TILE_PX, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+            bool ok;
+            if (tab) {
+                const int4 t = colax[x - low_x];
+                a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
+                ok = t.y > 0;
+            } else {
+                double rx, ry, rw, rh;
+                screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                ok = axis_setup(rx, rw, TILE_PX, a);
+            }
+            if (ok && lane >= a.t1 && lane < a.t1 + a.n) {
                 if (ncx == 0) { cx0 = x; ax0 = a; } else { cx1 = x; ax1 = a; }
                 ncx++;
             }
@@ -204,10 +255,18 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
         for (int y = yg - 2; y <= yg + 2; y++) {
             if (y < low_y || y > high_y || ncy == 2) continue;
-            double rx, ry, rw, rh;
-            screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
             Axis a;
-            if (axis_setup(ry, rh, TILE_PX, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+            bool ok;
+            if (tab) {
+                const int4 t = rowax[y - low_y];
+                a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
+                ok = t.y > 0;
+            } else {
+                double rx, ry, rw, rh;
+                screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                ok = axis_setup(ry, rh, TILE_PX, a);
+            }
+            if (ok && lane >= a.t1 && lane < a.t1 + a.n) {
                 int sr = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
                 if (ncy == 0) { ry0 = y; srow0 = sr; } else { ry1 = y; srow1 = sr; }
                 ncy++;
@@ -260,34 +319,46 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         // ---- background + first tile column, pixel-centric, RB rows per batch (all loads of
         //      a batch are issued before the first blend).  A transparent texel (0) blends to
         //      the unchanged pixel exactly, so lanes without a tile carry 0.
+        // per screen row (lane = row), packed for one readlane per row: source rows of its
+        // tile rows (7 bits each), their colb rows (5 bits each), tile-row count (2 bits);
+        // and the background source row offset (-1: outside the background blit)
+        const int prow = lane;
+        const int rinfo = ncy == 0 ? 0
+                        : (srow0 | ((ncy > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
+                           ((ncy > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy << 24));
+        const int bgrow = (bg_ok && prow >= by.t1 && prow < by.t1 + by.n)
+                              ? (int)(((by.base + (uint32_t)((prow - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
+                              : -1;
         for (int r0 = 0; r0 < PG_RES; r0 += RB) {
             uint32_t bgv[RB], ta[RB], tb[RB];
+            int info[RB], bgr[RB], ca[RB], cbv[RB];
 #pragma unroll
             for (int k = 0; k < RB; k++) {
-                const int row = r0 + k;
-                const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
-                {   // branch-free: an out-of-blit pixel loads pixels[0] and discards it
-                    uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-                    uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
-                    bgv[k] = inb ? v : 0xff000000u;
-                }
-                const int nr = readlane(ncy, row);
-                ta[k] = 0;
-                tb[k] = 0;
-                if (nr > 0) {
-                    const int ja = readlane(ry0, row) - jy0, sra = readlane(srow0, row);
-                    const int cb = colb[ja * 64 + lane];
-                    if (cb >= 0) ta[k] = d.pixels[(uint32_t)cb + (uint32_t)(sra * TILE_PX)];
-                }
-                if (nr > 1) {
-                    const int jb = readlane(ry1, row) - jy0, srb = readlane(srow1, row);
-                    const int cb = colb[jb * 64 + lane];
-                    if (cb >= 0) tb[k] = d.pixels[(uint32_t)cb + (uint32_t)(srb * TILE_PX)];
-                }
+                info[k] = readlane(rinfo, r0 + k);
+                bgr[k] = readlane(bgrow, r0 + k);
+            }
+#pragma unroll
+            for (int k = 0; k < RB; k++) { // LDS reads of the whole batch first
+                ca[k] = colb[((info[k] >> 14) & 31) * 64 + lane];
+                cbv[k] = colb[((info[k] >> 19) & 31) * 64 + lane];
+            }
+#pragma unroll
+            for (int k = 0; k < RB; k++) { // branch-free: an out-of-blit pixel loads pixels[0] and discards it
+                const bool inb = bg_col && bgr[k] >= 0;
+                uint32_t v = d.pixels[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
+                bgv[k] = inb ? v : 0xff000000u;
             }
 #pragma unroll
             for (int k = 0; k < RB; k++) {
-                const int nr = readlane(ncy, r0 + k);
+                const int nr = info[k] >> 24;
+                ta[k] = 0;
+                tb[k] = 0;
+                if (nr > 0 && ca[k] >= 0) ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((info[k] & 127) * TILE_PX)];
+                if (nr > 1 && cbv[k] >= 0) tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((info[k] >> 7) & 127) * TILE_PX)];
+            }
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int nr = info[k] >> 24;
                 uint32_t px = bgv[k];
                 if (nr > 0) px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
                 if (nr > 1) px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
@@ -364,43 +435,51 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     pt.mark(1);
     // ---- entities, render_z 0 then 1, in list order (basic-abstract-game.cpp:966-967, 1061-1075)
     const int n = s.num_ents;
+    const bool one_chunk = n <= 64; // blit setups computed once and reused by both z passes
+    bool draw = false;
+    int ez = 0;
+    Axis ex, ey;
+    int soff = 0, sw = 0, ca = 256, mir = 0;
     for (int z = 0; z <= 1; z++) {
         for (int base = 0; base < n; base += 64) {
             // lane-parallel blit setup of entity base + lane
             const int i = base + lane;
-            bool draw = false;
-            Axis ex, ey;
-            int soff = 0, sw = 0, ca = 256, mir = 0;
-            if (i < n && EIr(d, F_RENDER_Z, env, i) == z) {
-                float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
-                float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
-                int flags = EIr(d, F_FLAGS, env, i);
-                float alpha = EFr(d, F_ALPHA, env, i);
-                float rotation = EFr(d, F_ROTATION, env, i);
-                int itype = EIr(d, F_IMAGE_TYPE, env, i);
-                int theme = EIr(d, F_IMAGE_THEME, env, i);
-                int img = itype == PLAYER ? player_img : (itype == CR_ENEMY_BARRIER ? -1 : (itype < 0 ? -itype : itype));
-                if (img >= 0) {
-                    if ((flags & EF_ABS_COORDS) || rotation != 0 || s.opt_use_monochrome_assets ||
-                        img >= USE_ASSET_THRESHOLD) {
-                        if (img != SPACE) err = true; // not in this build
-                    } else {
-                        if (s.opt_restrict_themes) theme = 0;
-                        double rx, ry, rw, rh;
-                        screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
-                        if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
-                            rx = rx + rw * 0.0;
-                            ry = ry + rh * -.7415;
-                            rw = rw * 1.0;
-                            rh = rh * 1.7415;
-                        }
-                        int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                        if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
-                            draw = true;
-                            soff = sp.x;
-                            sw = sp.y;
-                            ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
-                            mir = (flags & EF_REFLECTED) != 0;
+            if (!one_chunk || z == 0) {
+                draw = false;
+                ez = 0;
+                soff = 0; sw = 0; ca = 256; mir = 0;
+                if (i < n) {
+                    ez = EIr(d, F_RENDER_Z, env, i);
+                    float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
+                    float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
+                    int flags = EIr(d, F_FLAGS, env, i);
+                    float alpha = EFr(d, F_ALPHA, env, i);
+                    float rotation = EFr(d, F_ROTATION, env, i);
+                    int itype = EIr(d, F_IMAGE_TYPE, env, i);
+                    int theme = EIr(d, F_IMAGE_THEME, env, i);
+                    int img = itype == PLAYER ? player_img : (itype == CR_ENEMY_BARRIER ? -1 : (itype < 0 ? -itype : itype));
+                    if (img >= 0 && (ez == 0 || ez == 1)) {
+                        if ((flags & EF_ABS_COORDS) || rotation != 0 || s.opt_use_monochrome_assets ||
+                            img >= USE_ASSET_THRESHOLD) {
+                            if (img != SPACE) err = true; // not in this build
+                        } else {
+                            if (s.opt_restrict_themes) theme = 0;
+                            double rx, ry, rw, rh;
+                            screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+                            if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
+                                rx = rx + rw * 0.0;
+                                ry = ry + rh * -.7415;
+                                rw = rw * 1.0;
+                                rh = rh * 1.7415;
+                            }
+                            int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                            if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
+                                draw = true;
+                                soff = sp.x;
+                                sw = sp.y;
+                                ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
+                                mir = (flags & EF_REFLECTED) != 0;
+                            }
                         }
                     }
                 }
@@ -410,7 +489,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
             // the group is blended into the framebuffer strictly in order.  Footprints wider
             // than one wave (> 64 px) fall back to an in-order loop with inline loads.
             const float inv_l = 1.0f / (float)(draw ? ex.n : 1);
-            unsigned long long m = ballot(draw);
+            unsigned long long m = ballot(draw && ez == z);
             while (m) {
                 int js[EG];
 #pragma unroll
@@ -472,11 +551,12 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
                             fb[o] = blend_argb_pm(fb[o], src, caj);
                         }
                     }
-                    wave_sync();
+                    // no barrier between entities: one wave issues its LDS operations in order
                 }
             }
         }
     }
+    wave_sync();
 
     pt.mark(2);
     // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
@@ -499,4 +579,16 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
 
 extern "C" void pg_launch_render(const PGDev *d, hipStream_t s) {
     hipLaunchKernelGGL(pg_render_kernel, dim3(d->num_envs), dim3(64), 0, s, *d);
+}
+
+// Debug aid (PROCGEN_MI355X_POISON_LDS=1): fill the LDS of every CU with a pattern before each
+// engine kernel, so a kernel that reads LDS before writing it shows up as a parity failure
+// instead of silently inheriting the previous wave's data.
+extern "C" __global__ __launch_bounds__(256) void pg_poison_lds_kernel(uint32_t pattern) {
+    __shared__ volatile uint32_t buf[16384]; // 64 KB
+    for (int k = threadIdx.x; k < 16384; k += 256) buf[k] = pattern ^ (uint32_t)(k * 0x9E3779B9u);
+}
+
+extern "C" void pg_launch_poison(hipStream_t s, uint32_t pattern) {
+    hipLaunchKernelGGL(pg_poison_lds_kernel, dim3(2048), dim3(256), 0, s, pattern);
 }

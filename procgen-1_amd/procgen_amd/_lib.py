@@ -11,9 +11,10 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# PROCGEN_MI355X_LIB=prof selects the diagnostic build (per-phase cycle counters)
-LIB_PATH = os.path.join(HERE, "libprocgen_mi355x_prof.so" if os.environ.get("PROCGEN_MI355X_LIB") == "prof"
-                        else "libprocgen_mi355x.so")
+# PROCGEN_MI355X_LIB=prof selects the diagnostic build (per-phase cycle counters); any other
+# name selects an experiment build libprocgen_mi355x_<name>.so (csrc/Makefile VARIANT=)
+_variant = os.environ.get("PROCGEN_MI355X_LIB", "")
+LIB_PATH = os.path.join(HERE, "libprocgen_mi355x_%s.so" % _variant if _variant else "libprocgen_mi355x.so")
 
 LIBENV_MAX_NAME_LEN = 128
 LIBENV_MAX_NDIM = 16

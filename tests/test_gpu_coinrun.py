@@ -5,6 +5,8 @@ RGB for coinrun (its game logic has no transcendental libm call).  Cases mirror 
 reference's own tests (procgen/env_test.py: seeding, determinism) plus option coverage
 and sampled envs of the full 65,536-env configuration.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -39,6 +41,25 @@ def assert_same(g, o, step, idx=None):
         vals = ["%s: %s vs %s" % (tuple(p), gg[tuple(p)].tolist(), o["rgb"][tuple(p)].tolist()) for p in diff[:8]]
         raise AssertionError("rgb differs at step %d (idx %s): %d pixels, (env,row,col): engine vs oracle\n  %s"
                              % (step, sel, len(diff), "\n  ".join(vals)))
+
+
+PGENV_FIELDS = {1: "action", 2: "cur_time", 27: "num_ents", 28: "agent_erased", 33: "move_action",
+                34: "special_action", 38: "action_vx", 39: "action_vy", 59: "has_support", 60: "facing_right",
+                61: "is_on_crate", 64: "rg_mti", 67: "grid8_ok"}
+FLOAT_FIELDS = {38, 39}
+
+
+def describe_engine_env(env, i):
+    """A few PGEnv members of engine env i (procgen_debug_env), for failure messages."""
+    try:
+        buf = env.debug_env(i)
+    except Exception as e:  # pragma: no cover - diagnostics only
+        return "debug_env failed: %s" % e
+    out = []
+    for k, name in PGENV_FIELDS.items():
+        v = buf[k:k + 1].view(np.float32)[0] if k in FLOAT_FIELDS else int(buf[k])
+        out.append("%s=%s" % (name, v))
+    return " ".join(out)
 
 
 def run_pair(num, steps, oracle_kw, gpu_kw, seed=0):
@@ -156,7 +177,18 @@ def test_full_size_sampled_parity():
         g = gpu_obs(env)
         for k, o in zip(sample, orcs):
             o.step(act[k:k + 1])
-            assert_same(g, o.observe(), t, idx=slice(k, k + 1))
+            try:
+                assert_same(g, o.observe(), t, idx=slice(k, k + 1))
+            except AssertionError as e:
+                dump = os.environ.get("PG_FLAKE_DUMP")
+                if dump:  # diagnostics: frames + engine snapshot of the failing env
+                    import ctypes
+                    buf = ctypes.create_string_buffer(1 << 20)
+                    nb = env._lib.get_state(env._handle, k, buf, 1 << 20)
+                    np.savez(dump, engine=g["rgb"][k], oracle=o.observe()["rgb"][0], step=t, env=k,
+                             state=np.frombuffer(buf.raw[:max(nb, 0)], np.uint8), odebug=o.debug(0))
+                raise AssertionError("%s\n  global env %d, action %d\n  engine: %s\n  oracle debug: %s"
+                                     % (e, k, act[k], describe_engine_env(env, k), o.debug(0).tolist()))
     env.close()
 
 
