@@ -37,6 +37,8 @@
 #define EXPLOSION 54
 #define EXPLOSION5 58
 #define TRAIL 59
+#define DOOR_OBJ 200
+#define KEY_OBJ 300
 /* basic-abstract-game.cpp:6-20 */
 static const float PI_F = 3.14159265358979323846264338327950288f; /* cpp-utils.h:12 */
 #define MIXRATEROT 0.5f
@@ -50,8 +52,11 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 
 #define MAX_ENTS 8192
 #define MAX_GRID (64 * 64)
+/* MazeGen arrays: array_dim = maze_dim + 2 <= world 31 (memory maze) + 2 */
+#define MAZE_MAX_CELLS (33 * 33)
 
-enum { GAME_COINRUN = 5 };
+/* game ids: index in the reference's env list (procgen/env.py:15-32) */
+enum { GAME_BIGFISH = 0, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -218,6 +223,12 @@ typedef struct {
     int wall_theme;
     bool has_support, facing_right, is_on_crate;
     float gravity, air_control;
+    /* bigfish (bigfish.cpp:20-22) */
+    int fish_eaten;
+    float r_inc;
+    /* maze (maze.cpp:16-18) / heist (heist.cpp:18-21) */
+    int maze_dim, world_dim, num_keys;
+    bool has_keys[4];
     /* observation of the last step */
     uint32_t canvas[RES_W * RES_H];
 } Game;
@@ -329,7 +340,27 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
     return base;
 }
 
+/* bigfish object ids / constants (bigfish.cpp:7-17) */
+#define BF_FISH 2
+static const int BF_COMPLETION_BONUS = 10;
+static const int BF_POSITIVE_REWARD = 1;
+static const float BF_FISH_MIN_R = .25f;
+static const float BF_FISH_MAX_R = 2;
+static const int BF_FISH_QUOTA = 30;
+/* maze (maze.cpp:6-12) */
+static const float MZ_REWARD = 10.0f;
+#define MZ_GOAL 2
+/* heist (heist.cpp:10-15) */
+static const float HS_COMPLETION_BONUS = 10.0f;
+#define HS_LOCKED_DOOR 1
+#define HS_KEY 2
+#define HS_EXIT 9
+#define HS_KEY_ON_RING 11
+
 static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *target, bool is_horizontal) {
+    if (g->game_id == GAME_HEIST) { /* heist.cpp:66-71 */
+        if (target->type == HS_LOCKED_DOOR) return !g->has_keys[target->image_theme];
+    }
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:187-202 */
         if (target->type == CR_CRATE && !is_horizontal) {
             Entity *agent = AG(g);
@@ -353,7 +384,45 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:123-131 */
         if (obj->type == CR_ENEMY) g->sd_done = true;
         else if (obj->type == CR_SAW) g->sd_done = true;
+    } else if (g->game_id == GAME_BIGFISH) { /* bigfish.cpp:45-59 */
+        if (obj->type == BF_FISH) {
+            Entity *agent = AG(g);
+            if (obj->rx > agent->rx) {
+                g->sd_done = true;
+            } else {
+                g->sd_reward += BF_POSITIVE_REWARD;
+                obj->will_erase = true;
+                agent->rx += g->r_inc;
+                agent->ry += g->r_inc;
+                g->fish_eaten += 1;
+            }
+        }
+    } else if (g->game_id == GAME_HEIST) { /* heist.cpp:80-96 */
+        if (obj->type == HS_EXIT) {
+            g->sd_done = true;
+            g->sd_reward = HS_COMPLETION_BONUS;
+            g->sd_level_complete = true;
+        } else if (obj->type == HS_KEY) {
+            obj->will_erase = true;
+            g->has_keys[obj->image_theme] = true;
+        } else if (obj->type == HS_LOCKED_DOOR) {
+            int door_num = obj->image_theme;
+            if (g->has_keys[door_num]) obj->will_erase = true;
+        }
     }
+}
+
+/* should_preserve_type_themes + mask_theme_if_necessary (basic-abstract-game.cpp:454-462, heist.cpp:42-44) */
+static int mask_theme(Game *g, int theme, int type) {
+    bool preserve = g->game_id == GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR);
+    if (g->options.restrict_themes && !preserve) return 0;
+    return theme;
+}
+
+/* should_draw_entity (basic-abstract-game.cpp:1052-1054, heist.cpp:73-78) */
+static bool hook_should_draw_entity(Game *g, const Entity *e) {
+    if (g->game_id == GAME_HEIST && e->type == HS_KEY_ON_RING) return g->has_keys[e->image_theme];
+    return true;
 }
 
 static void hook_handle_grid_collision(Game *g, Entity *obj, int type, int i, int j) {
@@ -583,6 +652,9 @@ static void set_action_xy(Game *g, int move_action) {
     g->action_vx = (float)(move_action / 3 - 1); /* basic-abstract-game.cpp:667-671 */
     g->action_vy = (float)(move_action % 3 - 1);
     g->action_vrot = 0;
+    if (g->game_id == GAME_MAZE) { /* maze.cpp:107-111 */
+        if (g->action_vx != 0) g->action_vy = 0;
+    }
 }
 
 static float clip_abs(float x, float y) { /* cpp-utils.h:46-52 */
@@ -869,13 +941,478 @@ static void coinrun_game_step(Game *g) { /* coinrun.cpp:474-498 */
     g->last_agent_y = AG(g)->y;
 }
 
+/* ================================================================== spawn helpers (basic-abstract-game.cpp) */
+/* asset_aspect_ratios[img_idx] (:79-123): width * 1.0 / height of the image loaded for the slot,
+ * after mask_theme_if_necessary picked the theme actually loaded. */
+static float asset_aspect_ratio(Game *g, const or_atlas *at, int img_idx) {
+    int type = img_idx % MAX_ASSETS, theme = img_idx / MAX_ASSETS;
+    theme = mask_theme(g, theme, type);
+    const or_image *im = &at->sprites[type + theme * MAX_ASSETS];
+    fassert(im->w > 0 && im->h > 0);
+    return (float)(im->w * 1.0 / im->h);
+}
+
+static void match_aspect_ratio(Game *g, const or_atlas *at, Entity *e) { /* :1023-1033, match_width = true */
+    int img_idx = e->image_type + e->image_theme * MAX_ASSETS;
+    e->ry = e->rx / asset_aspect_ratio(g, at, img_idx);
+}
+
+static float rand_pos(Game *g, float r, float min, float max) { /* :1109-1117 */
+    fassert(min <= max);
+    if (max - min <= 2 * r) return (max + min) / 2;
+    float range = max - min;
+    fassert(range >= 2 * r);
+    return (range - 2 * r) * rg_rand01(&g->rand_gen) + r + min;
+}
+
+static bool has_any_collision(Game *g, const Entity *e1, float margin) { /* :1123-1133 */
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        const Entity *ent = &g->ents[i];
+        if (!ent->avoids_collisions && has_collision(e1, ent, margin)) return true;
+    }
+    return false;
+}
+
+/* reposition (:548-569); `e` is not in `entities` yet */
+static void reposition(Game *g, Entity *e, float x, float y, float w, float h, bool check_collisions) {
+    float rx = e->rx, ry = e->ry;
+    e->x = rand_pos(g, rx, x, x + w);
+    e->y = rand_pos(g, ry, y, y + h);
+    int count = 0;
+    while ((has_agent_collision(g, e) || (check_collisions && has_any_collision(g, e, 0))) && (count < 100)) {
+        e->x = rand_pos(g, rx, x, x + w);
+        e->y = rand_pos(g, ry, y, y + h);
+        count++;
+    }
+}
+
+/* spawn_entity / spawn_entity_rxy (:520-527, 571-573) */
+static int spawn_entity(Game *g, float r, int type, float x, float y, float w, float h) {
+    Entity e;
+    entity_init(&e, 0, 0, 0, 0, r, r, type);
+    reposition(g, &e, x, y, w, h, true);
+    fassert(g->num_ents < MAX_ENTS);
+    g->ents[g->num_ents] = e;
+    return g->num_ents++;
+}
+
+/* ================================================================== MazeGen (mazegen.cpp) */
+#define MAZE_OFFSET 1
+typedef struct {
+    MT *rand_gen;
+    int maze_dim, array_dim;
+    int grid[MAZE_MAX_CELLS];              /* Grid<int> array_dim x array_dim */
+    int cell_sets_idxs[MAZE_MAX_CELLS];    /* set label of maze cell maze_dim*y+x */
+    int num_free_cells;
+    int free_cells[MAZE_MAX_CELLS];
+    bool in_free_set[MAZE_MAX_CELLS];
+} MazeGen;
+
+static void mg_init(MazeGen *m, MT *r, int maze_dim) { /* :12-20 */
+    memset(m, 0, sizeof(*m));
+    m->rand_gen = r;
+    m->maze_dim = maze_dim;
+    m->array_dim = maze_dim + 2;
+    fassert(m->array_dim * m->array_dim <= MAZE_MAX_CELLS);
+}
+static void mg_set(MazeGen *m, int x, int y, int v) {
+    fassert(0 <= x && x < m->array_dim && 0 <= y && y < m->array_dim);
+    m->grid[y * m->array_dim + x] = v;
+}
+static int mg_gridget(MazeGen *m, int x, int y) {
+    fassert(0 <= x && x < m->array_dim && 0 <= y && y < m->array_dim);
+    return m->grid[y * m->array_dim + x];
+}
+static void mg_set_index(MazeGen *m, int idx, int v) {
+    fassert(0 <= idx && idx < m->array_dim * m->array_dim);
+    m->grid[idx] = v;
+}
+static void mg_set_free_cell(MazeGen *m, int x, int y) { /* :26-34 */
+    mg_set(m, x + MAZE_OFFSET, y + MAZE_OFFSET, SPACE);
+    int cell = m->maze_dim * y + x;
+    if (!m->in_free_set[cell]) {
+        m->free_cells[m->num_free_cells] = cell;
+        m->in_free_set[cell] = true;
+        m->num_free_cells += 1;
+    }
+}
+static int mg_get_obj(MazeGen *m, int idx) { /* :36-47 */
+    int x = idx % m->array_dim, y = idx / m->array_dim;
+    if (x <= 0 || x >= m->array_dim - 1) return INVALID_OBJ;
+    if (y <= 0 || y >= m->array_dim - 1) return INVALID_OBJ;
+    return mg_gridget(m, x, y);
+}
+/* get_neighbors (:49-67): order (-1,0) (0,-1) (0,1) (1,0) */
+static int mg_neighbors(MazeGen *m, int idx, int type, int *out) {
+    int x = idx % m->array_dim, y = idx / m->array_dim, n = 0;
+    for (int dx = -1; dx <= 1; dx++) {
+        for (int dy = -1; dy <= 1; dy++) {
+            if (dx == 0 && dy == 0) continue;
+            if (dx != 0 && dy != 0) continue;
+            int n_idx = (y + dy) * m->array_dim + (x + dx);
+            if (mg_get_obj(m, n_idx) == type) out[n++] = n_idx;
+        }
+    }
+    return n;
+}
+
+/* expand_to_type (:69-98) over ascending std::set<int> iteration, sets as bitmaps */
+static int mg_expand_to_type(MazeGen *m, const bool *s0, bool *s1, int type) {
+    int cells = m->array_dim * m->array_dim;
+    static bool curr[MAZE_MAX_CELLS], next[MAZE_MAX_CELLS];
+    memcpy(curr, s0, (size_t)cells);
+    bool any = false;
+    for (int i = 0; i < cells; i++) any = any || curr[i];
+    while (any) {
+        memset(next, 0, (size_t)cells);
+        for (int elem = 0; elem < cells; elem++) {
+            if (!curr[elem]) continue;
+            int targets[4], adj[4];
+            int nt = mg_neighbors(m, elem, type, targets);
+            int na = mg_neighbors(m, elem, SPACE, adj);
+            for (int k = 0; k < na; k++) {
+                int j = adj[k];
+                if (!s0[j] && !s1[j]) {
+                    next[j] = true;
+                    s1[j] = true;
+                }
+            }
+            if (nt > 0) return targets[0];
+        }
+        any = false;
+        for (int i = 0; i < cells; i++) {
+            curr[i] = next[i];
+            any = any || next[i];
+        }
+    }
+    return -1;
+}
+
+static void mg_generate_maze(MazeGen *m) { /* :112-188 */
+    int md = m->maze_dim;
+    for (int i = 0; i < m->array_dim; i++)
+        for (int j = 0; j < m->array_dim; j++) mg_set(m, i, j, WALL_OBJ);
+    mg_set(m, MAZE_OFFSET, MAZE_OFFSET, 0);
+    static int walls[2 * MAZE_MAX_CELLS][4];
+    int nw = 0;
+    m->num_free_cells = 0;
+    memset(m->in_free_set, 0, sizeof(m->in_free_set));
+    for (int i = 0; i < md * md; i++) m->cell_sets_idxs[i] = i;
+    for (int i = 1; i < md; i += 2)
+        for (int j = 0; j < md; j += 2)
+            if (i > 0 && i < md - 1) {
+                walls[nw][0] = i - 1; walls[nw][1] = j; walls[nw][2] = i + 1; walls[nw][3] = j;
+                nw++;
+            }
+    for (int i = 0; i < md; i += 2)
+        for (int j = 1; j < md; j += 2)
+            if (j > 0 && j < md - 1) {
+                walls[nw][0] = i; walls[nw][1] = j - 1; walls[nw][2] = i; walls[nw][3] = j + 1;
+                nw++;
+            }
+    while (nw > 0) {
+        int n = rg_randn(m->rand_gen, nw);
+        int x1 = walls[n][0], y1 = walls[n][1], x2 = walls[n][2], y2 = walls[n][3];
+        int s0_idx = m->cell_sets_idxs[md * y1 + x1];
+        int s1_idx = m->cell_sets_idxs[md * y2 + x2];
+        int x0 = (x1 + x2) / 2, y0 = (y1 + y2) / 2;
+        int center = md * y0 + x0;
+        bool can_remove = (mg_gridget(m, x0 + MAZE_OFFSET, y0 + MAZE_OFFSET) == WALL_OBJ) && (s0_idx != s1_idx);
+        if (can_remove) {
+            mg_set_free_cell(m, x1, y1);
+            mg_set_free_cell(m, x0, y0);
+            mg_set_free_cell(m, x2, y2);
+            /* s1 |= s0 | {center}; every member relabelled s1_idx */
+            for (int c = 0; c < md * md; c++)
+                if (m->cell_sets_idxs[c] == s0_idx) m->cell_sets_idxs[c] = s1_idx;
+            m->cell_sets_idxs[center] = s1_idx;
+        }
+        memmove(walls[n], walls[n + 1], sizeof(walls[0]) * (size_t)(nw - n - 1));
+        nw--;
+    }
+}
+
+static void mg_generate_maze_with_doors(MazeGen *m, int num_doors) { /* :213-290 */
+    mg_generate_maze(m);
+    int cells = m->array_dim * m->array_dim;
+    static int forks[MAZE_MAX_CELLS], rem[MAZE_MAX_CELLS], chosen[MAZE_MAX_CELLS], space_cells[MAZE_MAX_CELLS];
+    int nf = 0;
+    for (int i = 0; i < cells; i++) {
+        if (mg_get_obj(m, i) == SPACE) {
+            int adj[4];
+            if (mg_neighbors(m, i, SPACE, adj) > 2) forks[nf++] = i;
+        }
+    }
+    /* RandGen::choose_n (randgen.cpp:49-68) */
+    int nc = 0;
+    if (num_doors > nf) {
+        for (int i = 0; i < nf; i++) chosen[nc++] = forks[i];
+    } else {
+        int nr = nf;
+        memcpy(rem, forks, sizeof(int) * (size_t)nf);
+        while (nc < num_doors) {
+            int k = rg_randn(m->rand_gen, nr);
+            chosen[nc++] = rem[k];
+            memmove(&rem[k], &rem[k + 1], sizeof(int) * (size_t)(nr - k - 1));
+            nr--;
+        }
+    }
+    num_doors = nc;
+    for (int i = 0; i < nc; i++) mg_set_index(m, chosen[i], DOOR_OBJ);
+    int agent_cell;
+    {
+        int ns = 0;
+        for (int i = 0; i < cells; i++)
+            if (mg_get_obj(m, i) == SPACE) space_cells[ns++] = i;
+        int dn[4];
+        do {
+            fassert(ns > 0);
+            agent_cell = space_cells[rg_randn(m->rand_gen, ns)];
+        } while (mg_neighbors(m, agent_cell, DOOR_OBJ, dn) > 0);
+        mg_set_index(m, agent_cell, AGENT_OBJ);
+    }
+    static bool s0[MAZE_MAX_CELLS], s1[MAZE_MAX_CELLS];
+    memset(s0, 0, sizeof(s0));
+    s0[agent_cell] = true;
+    for (int door_num = 0; door_num < num_doors + 1; door_num++) {
+        memset(s1, 0, sizeof(s1));
+        int found_door = -1;
+        if (door_num < num_doors) {
+            found_door = mg_expand_to_type(m, s0, s1, DOOR_OBJ);
+            mg_set_index(m, found_door, DOOR_OBJ + door_num + 1);
+            for (int i = 0; i < cells; i++) s0[i] = s0[i] || s1[i];
+        }
+        mg_expand_to_type(m, s0, s1, -999);
+        int ns = 0;
+        for (int i = 0; i < cells; i++)
+            if (s1[i]) space_cells[ns++] = i;
+        fassert(ns > 0);
+        int key_cell = space_cells[rg_randn(m->rand_gen, ns)];
+        mg_set_index(m, key_cell, door_num == num_doors ? EXIT_OBJ : (KEY_OBJ + door_num + 1));
+        for (int i = 0; i < cells; i++) s0[i] = s0[i] || s1[i];
+        if (found_door >= 0) s0[found_door] = true;
+    }
+}
+
+static void mg_generate_maze_no_dead_ends(MazeGen *m) { /* :190-211 */
+    mg_generate_maze(m);
+    int cells = m->array_dim * m->array_dim;
+    for (int i = 0; i < cells; i++) {
+        if (mg_get_obj(m, i) == SPACE) {
+            int adj_space[4], adj_wall[4];
+            if (mg_neighbors(m, i, SPACE, adj_space) == 1) {
+                int nw = mg_neighbors(m, i, WALL_OBJ, adj_wall);
+                if (nw > 0) mg_set_index(m, adj_wall[rg_randn(m->rand_gen, nw)], SPACE);
+            }
+        }
+    }
+}
+
+static void mg_place_objects(MazeGen *m, int start_obj, int num_objs) { /* :292-306 */
+    for (int j = 0; j < num_objs; j++) {
+        int mm = rg_randn(m->rand_gen, m->num_free_cells);
+        while (m->free_cells[mm] == -1 || m->free_cells[mm] == 0) mm = rg_randn(m->rand_gen, m->num_free_cells);
+        int coin_cell = m->free_cells[mm];
+        m->free_cells[mm] = -1;
+        mg_set(m, coin_cell % m->maze_dim + MAZE_OFFSET, coin_cell / m->maze_dim + MAZE_OFFSET, start_obj + j);
+    }
+}
+
+/* ================================================================== bigfish (games/bigfish.cpp) */
+static void bigfish_game_reset(Game *g, const or_atlas *at) { /* :62-78 */
+    basic_game_reset(g, at);
+    g->options.center_agent = false;
+    g->fish_eaten = 0;
+    float start_r = .5f;
+    if (g->options.distribution_mode == EasyMode) start_r = 1;
+    g->r_inc = (BF_FISH_MAX_R - start_r) / BF_FISH_QUOTA;
+    Entity *agent = AG(g);
+    agent->rx = start_r;
+    agent->ry = start_r;
+    agent->y = 1 + agent->ry;
+}
+
+static void bigfish_game_step(Game *g, const or_atlas *at) { /* :80-106 */
+    basic_game_step(g);
+    MT *r = &g->rand_gen;
+    if (rg_randn(r, 10) == 1) {
+        /* pow(float, 1.4) is the double pow */
+        float ent_r = (float)((double)(BF_FISH_MAX_R - BF_FISH_MIN_R) * pow((double)rg_rand01(r), 1.4) +
+                              (double)BF_FISH_MIN_R);
+        float ent_y = rg_rand01(r) * (g->main_height - 2 * ent_r);
+        float moves_right = (double)rg_rand01(r) < .5;
+        float ent_vx = (float)((.15 + (double)rg_rand01(r) * .25) * (moves_right ? 1 : -1));
+        float ent_x = moves_right ? -1 * ent_r : g->main_width + ent_r;
+        int i = add_entity(g, ent_x, ent_y, ent_vx, 0, ent_r, BF_FISH);
+        Entity *ent = &g->ents[i];
+        choose_random_theme(g, ent, at);
+        match_aspect_ratio(g, at, ent);
+        ent->is_reflected = !moves_right;
+    }
+    if (g->fish_eaten >= BF_FISH_QUOTA) {
+        g->sd_done = true;
+        g->sd_reward += BF_COMPLETION_BONUS;
+        g->sd_level_complete = true;
+    }
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+}
+
+/* ================================================================== maze (games/maze.cpp) */
+static void maze_choose_world_dim(Game *g) { /* :45-58 */
+    int d = g->options.distribution_mode;
+    if (d == EasyMode) g->world_dim = 15;
+    else if (d == HardMode) g->world_dim = 25;
+    else if (d == MemoryMode) g->world_dim = 31;
+    g->main_width = g->world_dim;
+    g->main_height = g->world_dim;
+}
+
+static void maze_game_reset(Game *g, const or_atlas *at) { /* :60-105 */
+    maze_choose_world_dim(g);
+    basic_game_reset(g, at);
+    g->grid_step = true;
+    g->maze_dim = rg_randn(&g->rand_gen, (g->world_dim - 1) / 2) * 2 + 3;
+    int margin = (g->world_dim - g->maze_dim) / 2;
+    static MazeGen mg;
+    mg_init(&mg, &g->rand_gen, g->maze_dim);
+    g->options.center_agent = g->options.distribution_mode == MemoryMode;
+    Entity *agent = AG(g);
+    agent->rx = .5f;
+    agent->ry = .5f;
+    agent->x = (float)(margin + .5);
+    agent->y = (float)(margin + .5);
+    mg_generate_maze(&mg);
+    mg_place_objects(&mg, MZ_GOAL, 1);
+    for (int i = 0; i < g->grid_size; i++) g->grid[i] = WALL_OBJ;
+    for (int i = 0; i < g->maze_dim; i++)
+        for (int j = 0; j < g->maze_dim; j++)
+            set_obj(g, margin + i, margin + j, mg_gridget(&mg, i + MAZE_OFFSET, j + MAZE_OFFSET));
+    if (margin > 0) {
+        for (int i = 0; i < g->maze_dim + 2; i++) {
+            set_obj(g, margin - 1, margin + i - 1, WALL_OBJ);
+            set_obj(g, margin + g->maze_dim, margin + i - 1, WALL_OBJ);
+            set_obj(g, margin + i - 1, margin - 1, WALL_OBJ);
+            set_obj(g, margin + i - 1, margin + g->maze_dim, WALL_OBJ);
+        }
+    }
+}
+
+static void maze_game_step(Game *g) { /* :113-131 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = true;
+    if (g->action_vx < 0) agent->is_reflected = false;
+    int ix = (int)agent->x;
+    int iy = (int)agent->y;
+    if (get_obj(g, ix, iy) == MZ_GOAL) {
+        set_obj(g, ix, iy, SPACE);
+        g->sd_reward += MZ_REWARD;
+        g->sd_level_complete = true;
+    }
+    g->sd_done = g->sd_reward > 0;
+}
+
+/* ================================================================== heist (games/heist.cpp) */
+static void heist_choose_world_dim(Game *g) { /* :98-113 */
+    int d = g->options.distribution_mode;
+    if (d == EasyMode) g->world_dim = 9;
+    else if (d == HardMode) g->world_dim = 13;
+    else if (d == MemoryMode) g->world_dim = 23;
+    g->maxspeed = .75f;
+    g->main_width = g->world_dim;
+    g->main_height = g->world_dim;
+}
+
+static void heist_game_reset(Game *g, const or_atlas *at) { /* :115-203 */
+    heist_choose_world_dim(g);
+    basic_game_reset(g, at);
+    MT *r = &g->rand_gen;
+    int min_maze_dim = 5;
+    int max_diff = (g->world_dim - min_maze_dim) / 2;
+    int difficulty = rg_randn(r, max_diff + 1);
+    g->options.center_agent = g->options.distribution_mode == MemoryMode;
+    if (g->options.distribution_mode == MemoryMode) g->num_keys = rg_randn(r, 4);
+    else g->num_keys = difficulty + rg_randn(r, 2);
+    if (g->num_keys > 3) g->num_keys = 3;
+    for (int i = 0; i < 4; i++) g->has_keys[i] = false;
+    int maze_dim = difficulty * 2 + min_maze_dim;
+    float maze_scale = (float)(g->main_height / (g->world_dim * 1.0));
+    Entity *agent = AG(g);
+    agent->rx = (float)(.375 * maze_scale);
+    agent->ry = (float)(.375 * maze_scale);
+    float r_ent = maze_scale / 2;
+    static MazeGen mg;
+    mg_init(&mg, r, maze_dim);
+    mg_generate_maze_with_doors(&mg, g->num_keys);
+    agent->x = -1;
+    agent->y = -1;
+    int off_x = rg_randn(r, g->world_dim - maze_dim + 1);
+    int off_y = rg_randn(r, g->world_dim - maze_dim + 1);
+    for (int i = 0; i < g->grid_size; i++) g->grid[i] = WALL_OBJ;
+    for (int i = 0; i < maze_dim; i++) {
+        for (int j = 0; j < maze_dim; j++) {
+            int x = off_x + i, y = off_y + j;
+            int obj = mg_gridget(&mg, i + MAZE_OFFSET, j + MAZE_OFFSET);
+            float obj_x = (float)((x + .5) * maze_scale);
+            float obj_y = (float)((y + .5) * maze_scale);
+            if (obj != WALL_OBJ) set_obj(g, x, y, SPACE);
+            if (obj >= KEY_OBJ) {
+                int k = spawn_entity(g, (float)(.375 * maze_scale), HS_KEY, maze_scale * x, maze_scale * y, maze_scale,
+                                     maze_scale);
+                g->ents[k].image_theme = obj - KEY_OBJ - 1;
+                match_aspect_ratio(g, at, &g->ents[k]);
+            } else if (obj >= DOOR_OBJ) {
+                int k = add_entity(g, obj_x, obj_y, 0, 0, r_ent, HS_LOCKED_DOOR);
+                g->ents[k].image_theme = obj - DOOR_OBJ - 1;
+            } else if (obj == EXIT_OBJ) {
+                int k = spawn_entity(g, (float)(.375 * maze_scale), HS_EXIT, maze_scale * x, maze_scale * y, maze_scale,
+                                     maze_scale);
+                match_aspect_ratio(g, at, &g->ents[k]);
+            } else if (obj == AGENT_OBJ) {
+                agent = AG(g);
+                agent->x = obj_x;
+                agent->y = obj_y;
+            }
+        }
+    }
+    float ring_key_r = 0.03f;
+    for (int i = 0; i < g->num_keys; i++) {
+        int k = add_entity(g, (float)(1 - ring_key_r * (2 * i + 1.25)), (float)(ring_key_r * .75), 0, 0, ring_key_r,
+                           HS_KEY_ON_RING);
+        Entity *e = &g->ents[k];
+        e->image_theme = i;
+        e->image_type = HS_KEY;
+        e->rotation = PI_F / 2;
+        e->render_z = 1;
+        e->use_abs_coords = true;
+        match_aspect_ratio(g, at, e);
+    }
+}
+
+static void heist_game_step(Game *g) { /* :205-209 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    /* Entity::face_direction (entity.cpp:84-88): entity.cpp includes <math.h>, so atan2 of
+     * floats is atan2f */
+    float dx = g->action_vx, dy = g->action_vy;
+    if (dx != 0 || dy != 0) agent->rotation = -1 * atan2f(dy, dx) + 0.0f;
+}
+
 /* ================================================================== Game (game.cpp) */
 static void game_reset_dispatch(Game *g, const or_atlas *at) {
     if (g->game_id == GAME_COINRUN) coinrun_game_reset(g, at);
+    else if (g->game_id == GAME_BIGFISH) bigfish_game_reset(g, at);
+    else if (g->game_id == GAME_MAZE) maze_game_reset(g, at);
+    else if (g->game_id == GAME_HEIST) heist_game_reset(g, at);
     else fatal_msg("game not restated");
 }
-static void game_step_dispatch(Game *g) {
+static void game_step_dispatch(Game *g, const or_atlas *at) {
     if (g->game_id == GAME_COINRUN) coinrun_game_step(g);
+    else if (g->game_id == GAME_BIGFISH) bigfish_game_step(g, at);
+    else if (g->game_id == GAME_MAZE) maze_game_step(g);
+    else if (g->game_id == GAME_HEIST) heist_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -913,7 +1450,7 @@ static void game_step(Game *g, const or_atlas *at) { /* game.cpp:136-171 */
     g->sd_reward = 0;
     g->sd_done = false;
     g->sd_level_complete = false;
-    game_step_dispatch(g);
+    game_step_dispatch(g, at);
     g->sd_done = g->sd_done || will_force_reset || (g->cur_time >= g->timeout);
     g->total_reward += g->sd_reward;
     if (g->sd_reward != 0) {
@@ -988,9 +1525,16 @@ static inline void qt_blend(uint32_t *dst, uint32_t src, int fmt, int const_alph
 
 /* QPainter::drawImage(QRectF target, QImage img) with identity transform
  * (qpaintengine_raster.cpp drawImage -> qt_scale_image_32bit). */
+static void qt_scale_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
+                           int ih, int fmt, bool mirrored, double opacity);
 static void qt_draw_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
                           int ih, int fmt, bool mirrored, double opacity) {
     if (rw <= 0 || rh <= 0) return; /* QRectF::isEmpty */
+    qt_scale_image(canvas, rx, ry, rw, rh, px, iw, ih, fmt, mirrored, opacity);
+}
+/* qt_scale_image_32bit on the already-mapped target rect (width/height may be negative) */
+static void qt_scale_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
+                           int ih, int fmt, bool mirrored, double opacity) {
     if (iw <= 0 || ih <= 0) return;
     int const_alpha = qt_int_opacity(opacity);
     /* qt_mapRect_non_normalizing(r, identity): QRectF(topLeft, bottomRight) */
@@ -1051,6 +1595,181 @@ static void qt_draw_image(uint32_t *canvas, double rx, double ry, double rw, dou
     }
 }
 
+/* QTransform::rotate(a) applied to translate(tx, ty) (qtransform.cpp): exact special cases for
+ * +-90 / 180 / 270, otherwise qSin/qCos (glibc sin/cos) of deg2rad * a. */
+typedef struct { double m11, m12, m21, m22, dx, dy; } QtXform;
+static QtXform qt_translate_rotate(double tx, double ty, double a) {
+    QtXform t = {1, 0, 0, 1, tx, ty};
+    if (a == 0) return t;
+    double sina = 0, cosa = 0;
+    if (a == 90. || a == -270.) sina = 1;
+    else if (a == 270. || a == -90.) sina = -1;
+    else if (a == 180.) cosa = -1;
+    else {
+        const double deg2rad = 0.017453292519943295769;
+        double b = deg2rad * a;
+        sina = sin(b);
+        cosa = cos(b);
+    }
+    t.m11 = cosa; t.m12 = sina; t.m21 = -sina; t.m22 = cosa;
+    return t;
+}
+static void qt_map(const QtXform *t, double x, double y, double *nx, double *ny) {
+    *nx = t->m11 * x + t->m21 * y + t->dx;
+    *ny = t->m12 * x + t->m22 * y + t->dy;
+}
+
+typedef struct { double x, y, u, v; } QtVtx; /* QTransformImageVertex */
+
+/* qt_transform_image_rasterize (qblendfunctions_p.h) for 32-bit source/destination */
+static void qt_xform_rasterize(uint32_t *canvas, const uint32_t *px, int iw, bool mirrored, QtVtx tl, QtVtx bl,
+                               QtVtx tr, QtVtx br, int sl, int st, int sw, int sh, double topY, double bottomY,
+                               int dudx, int dvdx, int dudy, int dvdy, int u0, int v0, int const_alpha) {
+    int fromY = qRound(topY);
+    if (fromY < 0) fromY = 0;
+    int toY = qRound(bottomY);
+    if (toY > RES_H) toY = RES_H;
+    if (fromY >= toY) return;
+    double leftSlope = (bl.x - tl.x) / (bl.y - tl.y);
+    double rightSlope = (br.x - tr.x) / (br.y - tr.y);
+    int dx_l = (int)(leftSlope * 0x10000);
+    int dx_r = (int)(rightSlope * 0x10000);
+    int x_l = (int)((tl.x + (0.5 + fromY - tl.y) * leftSlope + 0.5) * 0x10000);
+    int x_r = (int)((tr.x + (0.5 + fromY - tr.y) * rightSlope + 0.5) * 0x10000);
+#define SRC_AT(uu, vv) px[(vv) * iw + (mirrored ? iw - 1 - (uu) : (uu))]
+    for (int y = fromY; y < toY; ++y) {
+        uint32_t *line = canvas + y * RES_W;
+        int fromX = x_l >> 16;
+        if (fromX < 0) fromX = 0;
+        int toX = x_r >> 16;
+        if (toX > RES_W) toX = RES_W;
+        if (fromX < toX) {
+            int x1 = fromX;
+            int u = x1 * dudx + y * dudy + u0;
+            int v = x1 * dvdx + y * dvdy + v0;
+            for (; x1 < toX; ++x1) {
+                int uu = u >> 16, vv = v >> 16;
+                if (uu >= sl && uu < sl + sw && vv >= st && vv < st + sh) break;
+                u += dudx;
+                v += dvdx;
+            }
+            int x2 = toX;
+            u = (x2 - 1) * dudx + y * dudy + u0;
+            v = (x2 - 1) * dvdx + y * dvdy + v0;
+            for (; x2 > x1; --x2) {
+                int uu = u >> 16, vv = v >> 16;
+                if (uu >= sl && uu < sl + sw && vv >= st && vv < st + sh) break;
+                u -= dudx;
+                v -= dvdx;
+            }
+            u = fromX * dudx + y * dudy + u0;
+            v = fromX * dvdx + y * dvdy + v0;
+            for (int x = fromX; x < toX; ++x) {
+                int uu = u >> 16, vv = v >> 16;
+                if (x < x1 || x >= x2) { /* clamped ends of the scan line */
+                    if (uu < sl) uu = sl;
+                    if (uu > sl + sw - 1) uu = sl + sw - 1;
+                    if (vv < st) vv = st;
+                    if (vv > st + sh - 1) vv = st + sh - 1;
+                }
+                qt_blend(&line[x], SRC_AT(uu, vv), QFMT_ARGB32_PM, const_alpha);
+                u += dudx;
+                v += dvdx;
+            }
+        }
+        x_l += dx_l;
+        x_r += dx_r;
+    }
+#undef SRC_AT
+}
+
+/* QPainter::drawImage(QRectF target, QImage img) under a rotation (qpaintengine_raster.cpp drawImage ->
+ * qTransformFunctions[RGB32][ARGB32PM] -> qt_transform_image, qblendfunctions_p.h) */
+static void qt_draw_image_xform(uint32_t *canvas, const QtXform *t, double rx, double ry, double rw, double rh,
+                                const uint32_t *px, int iw, int ih, bool mirrored, double opacity) {
+    if (iw <= 0 || ih <= 0) return;
+    int const_alpha = qt_int_opacity(opacity);
+    enum { TopLeft, TopRight, BottomRight, BottomLeft };
+    QtVtx v[4];
+    double sl = 0, st = 0, sr = iw, sb = ih; /* sourceRect QRectF(0, 0, iw, ih) */
+    v[TopLeft].u = v[BottomLeft].u = sl;
+    v[TopLeft].v = v[TopRight].v = st;
+    v[TopRight].u = v[BottomRight].u = sr;
+    v[BottomLeft].v = v[BottomRight].v = sb;
+    double right = rx + rw, bottom = ry + rh;
+    qt_map(t, rx, ry, &v[TopLeft].x, &v[TopLeft].y);
+    qt_map(t, right, ry, &v[TopRight].x, &v[TopRight].y);
+    qt_map(t, rx, bottom, &v[BottomLeft].x, &v[BottomLeft].y);
+    qt_map(t, right, bottom, &v[BottomRight].x, &v[BottomRight].y);
+    int topmost = 0;
+    for (int i = 1; i < 4; ++i)
+        if (v[i].y < v[topmost].y) topmost = i;
+    QtVtx tmp;
+    switch (topmost) {
+    case 1:
+        tmp = v[0];
+        for (int i = 0; i < 3; ++i) v[i] = v[i + 1];
+        v[3] = tmp;
+        break;
+    case 2:
+        tmp = v[0]; v[0] = v[2]; v[2] = tmp;
+        tmp = v[1]; v[1] = v[3]; v[3] = tmp;
+        break;
+    case 3:
+        tmp = v[3];
+        for (int i = 3; i > 0; --i) v[i] = v[i - 1];
+        v[0] = tmp;
+        break;
+    }
+    double dx1 = v[1].x - v[0].x, dy1 = v[1].y - v[0].y;
+    double dx2 = v[3].x - v[0].x, dy2 = v[3].y - v[0].y;
+    if (dx1 * dy2 - dx2 * dy1 > 0) {
+        tmp = v[1]; v[1] = v[3]; v[3] = tmp;
+    }
+    QtVtx u = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].u - v[0].u, v[1].v - v[0].v};
+    QtVtx w = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].u - v[0].u, v[2].v - v[0].v};
+    double det = u.x * w.y - u.y * w.x;
+    if (det == 0) return;
+    double invDet = 1.0 / det;
+    double m11 = (u.u * w.y - u.y * w.u) * invDet;
+    double m12 = (u.x * w.u - u.u * w.x) * invDet;
+    double m21 = (u.v * w.y - u.y * w.v) * invDet;
+    double m22 = (u.x * w.v - u.v * w.x) * invDet;
+    double mdx = v[0].u - m11 * v[0].x - m12 * v[0].y;
+    double mdy = v[0].v - m21 * v[0].x - m22 * v[0].y;
+    int dudx = (int)(m11 * 0x10000), dvdx = (int)(m21 * 0x10000);
+    int dudy = (int)(m12 * 0x10000), dvdy = (int)(m22 * 0x10000);
+    int u0 = qCeil((0.5 * m11 + 0.5 * m12 + mdx) * 0x10000) - 1;
+    int v0 = qCeil((0.5 * m21 + 0.5 * m22 + mdy) * 0x10000) - 1;
+    int x1 = qFloor(sl), y1 = qFloor(st), x2 = qCeil(sr), y2 = qCeil(sb);
+    int sw = x2 - x1, sh = y2 - y1;
+    if (v[1].y < v[3].y) {
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[0], v[1], v[0], v[3], x1, y1, sw, sh, v[0].y, v[1].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[1], v[2], v[0], v[3], x1, y1, sw, sh, v[1].y, v[3].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[1], v[2], v[3], v[2], x1, y1, sw, sh, v[3].y, v[2].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+    } else {
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[0], v[1], v[0], v[3], x1, y1, sw, sh, v[0].y, v[3].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[0], v[1], v[3], v[2], x1, y1, sw, sh, v[3].y, v[1].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+        qt_xform_rasterize(canvas, px, iw, mirrored, v[1], v[2], v[3], v[2], x1, y1, sw, sh, v[1].y, v[2].y, dudx, dvdx, dudy, dvdy, u0, v0, const_alpha);
+    }
+}
+
+/* basic-abstract-game.cpp:908-916: save; translate(center); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)) */
+static void qt_draw_image_rotated(uint32_t *canvas, double x, double y, double w, double h, double deg,
+                                  const uint32_t *px, int iw, int ih, bool mirrored, double opacity) {
+    QtXform t = qt_translate_rotate(x + w / 2, y + h / 2, deg);
+    double rx = -w / 2, ry = -h / 2;
+    if (w <= 0 || h <= 0) return; /* QRectF::isEmpty */
+    if (t.m12 == 0 && t.m21 == 0) { /* TxScale (or translate): qt_scale_image_32bit on the mapped rect */
+        double ax, ay, bx, by;
+        qt_map(&t, rx, ry, &ax, &ay);
+        qt_map(&t, rx + w, ry + h, &bx, &by);
+        qt_scale_image(canvas, ax, ay, bx - ax, by - ay, px, iw, ih, QFMT_ARGB32_PM, mirrored, opacity);
+        return;
+    }
+    qt_draw_image_xform(canvas, &t, rx, ry, w, h, px, iw, ih, mirrored, opacity);
+}
+
 /* QPainter::fillRect(QRect, QColor) with an opaque color on RGB32 */
 static void qt_fill_rect_int(uint32_t *canvas, int x, int y, int w, int h, uint32_t argb) {
     int x1 = x < 0 ? 0 : x, y1 = y < 0 ? 0 : y;
@@ -1108,7 +1827,7 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
         fatal_msg("draw_grid_obj / monochrome not restated yet");
     }
     fassert(theme < MAX_IMAGE_THEMES);
-    if (g->options.restrict_themes) theme = 0; /* mask_theme_if_necessary, :458-462 */
+    theme = mask_theme(g, theme, img_type); /* the image initialize_asset_if_necessary loaded, :79-123 */
     int img_idx = img_type + theme * MAX_ASSETS;
     RectD r = base;
     if (g->game_id == GAME_COINRUN && is_player_image(img_type)) { /* coinrun.cpp:64-70 */
@@ -1117,20 +1836,33 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
     }
     const or_image *im = &at->sprites[img_idx];
     if (im->w <= 0) fatal_msg("missing sprite (generated assets are not restated yet)");
-    fassert(rotation == 0);
-    qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + im->offset, im->w, im->h, QFMT_ARGB32_PM, is_reflected,
-                  alpha != 1 ? (double)alpha : 1.0);
+    double opacity = alpha != 1 ? (double)alpha : 1.0;
+    if (rotation == 0) {
+        qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + im->offset, im->w, im->h, QFMT_ARGB32_PM,
+                      is_reflected, opacity);
+    } else { /* :908-916: p.rotate(rotation * 180 / PI) */
+        float deg = rotation * 180 / PI_F;
+        qt_draw_image_rotated(g->canvas, r.x, r.y, r.w, r.h, (double)deg, at->pixels + im->offset, im->w, im->h,
+                              is_reflected, opacity);
+    }
 }
 
 static void draw_entities(Game *g, const or_atlas *at, int render_z) { /* :1061-1075 */
     for (int i = 0; i < g->num_ents; i++) {
         Entity *e = &g->ents[i];
         if (e->render_z != render_z) continue;
+        if (!hook_should_draw_entity(g, e)) continue;
         RectD r1;
-        if (e->use_abs_coords) {
-            fatal_msg("use_abs_coords not restated yet");
+        if (e->use_abs_coords) { /* get_abs_rect (:812-814) via get_object_rect (:820-826) */
+            float vd = g->view_dim;
+            float ax = vd * (e->x - e->rx), ay = vd * (e->y + e->ry), aw = 2 * vd * e->rx, ah = 2 * vd * e->ry;
+            r1.x = (double)(ax * g->unit);
+            r1.y = (double)(ay * g->unit);
+            r1.w = (double)(aw * g->unit);
+            r1.h = (double)(ah * g->unit);
+        } else {
+            r1 = get_screen_rect(g, e->x - e->rx, e->y + e->ry, 2 * e->rx, 2 * e->ry, 0); /* :820-826 */
         }
-        r1 = get_screen_rect(g, e->x - e->rx, e->y + e->ry, 2 * e->rx, 2 * e->ry, 0); /* :820-826 */
         draw_image(g, at, r1, e->rotation, e->is_reflected, e->image_type, e->image_theme, e->alpha);
     }
 }
@@ -1191,6 +1923,9 @@ static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_dra
 /* ================================================================== construction (vecgame.cpp) */
 static int game_id_of(const char *name) {
     if (strcmp(name, "coinrun") == 0) return GAME_COINRUN;
+    if (strcmp(name, "bigfish") == 0) return GAME_BIGFISH;
+    if (strcmp(name, "maze") == 0) return GAME_MAZE;
+    if (strcmp(name, "heist") == 0) return GAME_HEIST;
     return -1;
 }
 
@@ -1227,12 +1962,33 @@ static void coinrun_ctor(Game *g) { /* coinrun.cpp:49-58 */
     g->main_height = 64;
     g->out_of_bounds_object = CR_WALL_MID;
 }
+static void bigfish_ctor(Game *g) { /* bigfish.cpp:24-29 */
+    g->timeout = 6000;
+    g->main_width = 20;
+    g->main_height = 20;
+}
+static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
+    g->timeout = 500;
+    g->random_agent_start = false;
+    g->has_useful_vel_info = false;
+    g->out_of_bounds_object = WALL_OBJ;
+    g->visibility = 8.0f;
+}
+static void heist_ctor(Game *g) { /* heist.cpp:23-35 */
+    g->has_useful_vel_info = false;
+    g->main_width = 20;
+    g->main_height = 20;
+    g->out_of_bounds_object = WALL_OBJ;
+    g->visibility = 8.0f;
+}
 
 void *oracle_make(const char *env_name, int count, int env_offset, const or_options *opt, const or_atlas *atlas) {
     int gid = game_id_of(env_name);
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
-    if (!(dm == EasyMode || dm == HardMode)) return NULL; /* game.cpp:76-86 for coinrun */
+    /* game.cpp:76-86: easy and hard for every game; memory for heist and maze (of those restated) */
+    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE));
+    if (!dm_ok) return NULL;
     Vec *v = (Vec *)calloc(1, sizeof(Vec));
     v->count = count;
     v->offset = env_offset;
@@ -1254,7 +2010,10 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         g->game_id = gid;
         g->ents = (Entity *)calloc(MAX_ENTS, sizeof(Entity));
         basic_ctor(g);
-        coinrun_ctor(g);
+        if (gid == GAME_COINRUN) coinrun_ctor(g);
+        else if (gid == GAME_BIGFISH) bigfish_ctor(g);
+        else if (gid == GAME_MAZE) maze_ctor(g);
+        else if (gid == GAME_HEIST) heist_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;
@@ -1316,6 +2075,29 @@ void oracle_observe(void *h, uint8_t *rgb, float *rew, uint8_t *first, int32_t *
         if (prev_level_seed) prev_level_seed[n] = g->prev_level_seed;
         if (prev_level_complete) prev_level_complete[n] = (uint8_t)g->sd_level_complete;
         if (level_seed) level_seed[n] = g->current_level_seed;
+    }
+}
+
+/* Fork latent-state info (vecgame.cpp:270-316; maze.cpp:152-165): grid_size, the grid row-major
+ * (zero padded to 35*35), agent_pos = int(agent->x), int(agent->y); exit_pos is miner-only.
+ * Games without a latent state leave everything zero. */
+void oracle_latent(void *h, int32_t *grid_size, int32_t *grid, int32_t *agent_pos, int32_t *exit_pos) {
+    Vec *v = (Vec *)h;
+    for (int n = 0; n < v->count; n++) {
+        Game *g = &v->games[n];
+        int32_t *gs = grid_size + 2 * n, *gr = grid + 35 * 35 * n, *ap = agent_pos + 2 * n, *ep = exit_pos + 2 * n;
+        memset(gs, 0, 8);
+        memset(gr, 0, 35 * 35 * 4);
+        memset(ap, 0, 8);
+        memset(ep, 0, 8);
+        if (g->game_id == GAME_MAZE) {
+            gs[0] = g->grid_w;
+            gs[1] = g->grid_h;
+            for (int i = 0; i < g->grid_w * g->grid_h && i < 35 * 35; i++) gr[i] = g->grid[i];
+            Entity *a = AG(g);
+            ap[0] = (int)a->x;
+            ap[1] = (int)a->y;
+        }
     }
 }
 
@@ -1387,6 +2169,23 @@ static double rd_f64(Rd *r) {
 }
 
 /* replays ONE case body (after the canvas words) of tools/qt_raster_golden.cpp's format */
+/* MazeGen pin, same contract as oracle/ref_harness.cpp ref_mazegen */
+int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
+                   uint32_t *next_draw) {
+    static MazeGen m;
+    MT r;
+    rg_seed(&r, seed);
+    mg_init(&m, &r, maze_dim);
+    if (mode == 0) mg_generate_maze(&m);
+    else if (mode == 1) mg_generate_maze_no_dead_ends(&m);
+    else mg_generate_maze_with_doors(&m, num_doors);
+    if (num_objs > 0) mg_place_objects(&m, start_obj, num_objs);
+    int n = m.array_dim;
+    for (int i = 0; i < n * n; i++) out[i] = m.grid[i];
+    *next_draw = mt_next(&r);
+    return n;
+}
+
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas) {
     Rd r = {cmds, cmds + nbytes};
     uint32_t ncmds = rd_u32(&r);
@@ -1402,6 +2201,13 @@ int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas) {
             r.p += 4 * (size_t)iw * ih;
             if (rot != 0) return -1;
             qt_draw_image(canvas, x, y, w, h, px, (int)iw, (int)ih, (int)fmt, mirrored != 0, opacity);
+        } else if (kind == 3) { /* drawImage under translate(x + w/2, y + h/2) + rotate(deg) */
+            double deg = rd_f64(&r);
+            uint32_t fmt = rd_u32(&r), iw = rd_u32(&r), ih = rd_u32(&r);
+            const uint32_t *px = (const uint32_t *)r.p;
+            r.p += 4 * (size_t)iw * ih;
+            if (fmt != QFMT_ARGB32_PM) return -3;
+            qt_draw_image_rotated(canvas, x, y, w, h, deg, px, (int)iw, (int)ih, mirrored != 0, opacity);
         } else {
             uint32_t col = rd_u32(&r);
             if (kind == 2) qt_fill_rect_int(canvas, (int)x, (int)y, (int)w, (int)h, col);

@@ -61,6 +61,8 @@ void oracle_step(void *h, const int32_t *actions);
 /* copy the last observation set out (any pointer may be NULL) */
 void oracle_observe(void *h, uint8_t *rgb, float *rew, uint8_t *first,
                     int32_t *prev_level_seed, uint8_t *prev_level_complete, int32_t *level_seed);
+/* fork latent-state info per env: grid_size[2], grid[35*35], agent_pos[2], exit_pos[2] */
+void oracle_latent(void *h, int32_t *grid_size, int32_t *grid, int32_t *agent_pos, int32_t *exit_pos);
 /* debug: a few scalars of env i: [num_entities, cur_time, agent_x_bits, agent_y_bits,
  * background_index, wall_theme, episodes... ] (see .c) */
 int oracle_debug(void *h, int i, int32_t *out, int n);
@@ -70,6 +72,10 @@ int oracle_debug(void *h, int i, int32_t *out, int n);
 void oracle_mt_stream(uint32_t seed, uint32_t *out, int n);
 /* run a scripted RandGen sequence: ops[i] = (kind, a, b) ; writes one i32 (or float bits) per op */
 void oracle_randgen_script(uint32_t seed, const int32_t *ops, int nops, int32_t *out);
+/* MazeGen (mazegen.cpp) restatement: mode 0 generate_maze, 1 no_dead_ends, 2 with_doors(num_doors),
+ * then place_objects if num_objs > 0; writes the array_dim^2 grid, returns array_dim */
+int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
+                   uint32_t *next_draw);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);
 

@@ -11,7 +11,8 @@ gets every space background appended (``resources.cpp:972-975``) and ``caves``
 is ``platform[2, 3, 13]`` (``resources.cpp:977-979``).
 
 Per-game sprite tables: ``asset_for_type`` of each game (coinrun:
-``procgen/src/games/coinrun.cpp:72-121``) plus the reserved engine sprites
+``procgen/src/games/coinrun.cpp:72-121``, bigfish ``bigfish.cpp:34-43``, maze
+``maze.cpp:33-41``, heist ``heist.cpp:46-64``) plus the reserved engine sprites
 (``basic-abstract-game.cpp:424-438``).
 """
 
@@ -117,9 +118,37 @@ COINRUN_SPRITES = {
          "kenney/Tiles/boxCrate_single.png", "kenney/Tiles/boxCrate_warning.png"],  # CRATE
 }
 
+# ---------------------------------------------------------------- bigfish
+# procgen/src/games/bigfish.cpp:34-43 (PLAYER 0, FISH 2)
+BIGFISH_SPRITES = {
+    0: ["misc_assets/fishTile_072.png"],
+    2: ["misc_assets/fishTile_074.png", "misc_assets/fishTile_078.png", "misc_assets/fishTile_080.png"],
+}
+
+# ---------------------------------------------------------------- maze
+# procgen/src/games/maze.cpp:33-41 (WALL_OBJ 51, GOAL 2, PLAYER 0)
+MAZE_SPRITES = {
+    51: ["kenney/Ground/Sand/sandCenter.png"],
+    2: ["misc_assets/cheese.png"],
+    0: ["kenney/Enemies/mouse_move.png"],
+}
+
+# ---------------------------------------------------------------- heist
+# procgen/src/games/heist.cpp:46-64 (WALL_OBJ 51, EXIT 9, PLAYER 0, KEY 2, LOCKED_DOOR 1)
+HEIST_SPRITES = {
+    51: ["kenney/Ground/Dirt/dirtCenter.png"],
+    9: ["misc_assets/gemYellow.png"],
+    0: ["misc_assets/spaceAstronauts_008.png"],
+    2: ["misc_assets/keyBlue.png", "misc_assets/keyGreen.png", "misc_assets/keyRed.png"],
+    1: ["misc_assets/lock_blue.png", "misc_assets/lock_green.png", "misc_assets/lock_red.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
+    "bigfish": (BIGFISH_SPRITES, "water"),      # bigfish.cpp:30-32
+    "maze": (MAZE_SPRITES, "topdown"),          # maze.cpp:29-31
+    "heist": (HEIST_SPRITES, "topdown"),        # heist.cpp:37-39
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

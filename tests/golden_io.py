@@ -13,6 +13,8 @@ CMD_DTYPE = np.dtype([
     # 2 = atlas background index ; for fills `color` holds 0xAARRGGBB
     ("src", "<i4"), ("ref", "<i8"), ("iw", "<i4"), ("ih", "<i4"), ("color", "<u4"),
 ])
+# kind 3 (rotated drawImage) carries its angle in degrees
+CMD_ROT_DTYPE = np.dtype(CMD_DTYPE.descr + [("deg", "<f8")])
 
 
 def image_of(cmd, synth, atlas):
@@ -30,7 +32,9 @@ def encode_cmds(cmds, synth, atlas):
     for c in cmds:
         out.append(struct.pack("<Iddddd", int(c["kind"]), c["x"], c["y"], c["w"], c["h"], c["opacity"]))
         out.append(struct.pack("<Ii", int(c["mirrored"]), 0))
-        if c["kind"] == 0:
+        if c["kind"] == 3:
+            out.append(struct.pack("<d", float(c["deg"])))
+        if c["kind"] in (0, 3):
             px, iw, ih = image_of(c, synth, atlas)
             out.append(struct.pack("<III", int(c["fmt"]), iw, ih))
             out.append(np.ascontiguousarray(px, dtype="<u4").tobytes())

@@ -53,6 +53,9 @@ def load():
         lib.oracle_randgen_script.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         lib.oracle_qt_replay.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p]
         lib.oracle_qt_replay.restype = ctypes.c_int
+        lib.oracle_mazegen.argtypes = [ctypes.c_int32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_latent.argtypes = [ctypes.c_void_p] * 5
         _LIB = lib
     return _LIB
 
@@ -115,6 +118,15 @@ class OracleEnv:
         self.lib.oracle_observe(self.h, rgb.ctypes.data, rew.ctypes.data, first.ctypes.data, pls.ctypes.data,
                                 plc.ctypes.data, ls.ctypes.data)
         return dict(rgb=rgb, rew=rew, first=first, prev_level_seed=pls, prev_level_complete=plc, level_seed=ls)
+
+    def latent(self):
+        n = self.count
+        gs = np.zeros((n, 2), np.int32)
+        grid = np.zeros((n, 35 * 35), np.int32)
+        ap = np.zeros((n, 2), np.int32)
+        ep = np.zeros((n, 2), np.int32)
+        self.lib.oracle_latent(self.h, gs.ctypes.data, grid.ctypes.data, ap.ctypes.data, ep.ctypes.data)
+        return dict(grid_size=gs, grid=grid, agent_pos=ap, exit_pos=ep)
 
     def debug(self, i):
         out = np.zeros(16, np.int32)

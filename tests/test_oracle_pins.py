@@ -149,6 +149,26 @@ def test_qt_raster_goldens():
     assert not bad, "Qt raster mismatch in cases %s" % bad[:10]
 
 
+def test_qt_raster_rotation_goldens():
+    """Rotated drawImage (translate + rotate + drawImage, basic-abstract-game.cpp:908-916) replayed
+    through the oracle's qt_transform_image restatement equals real Qt 5.9.7
+    (tests/golden/qt_raster_rot_goldens.npz, tools/make_raster_rot_goldens.py)."""
+    from procgen_amd.assets import atlas_for
+    lib = oracle_lib.load()
+    z = np.load(os.path.join(GOLDEN, "qt_raster_rot_goldens.npz"), allow_pickle=False)
+    cmds, synth, cin, cout = z["cmds"], z["synth"], z["canvas_in"], z["canvas_out"]
+    atlas = atlas_for(str(z["atlas_game"]))
+    bad = []
+    for i in range(cin.shape[0]):
+        b = encode_cmds(cmds[cmds["case"] == i], synth, atlas)
+        canvas = cin[i].copy()
+        rc = lib.oracle_qt_replay(b, len(b), canvas.ctypes.data)
+        assert rc == len(b)
+        if not np.array_equal(canvas, cout[i]):
+            bad.append(i)
+    assert not bad, "Qt rotated raster mismatch in %d cases, first %s" % (len(bad), bad[:10])
+
+
 def test_oracle_trajectory_fixture():
     """Regression pin of the oracle itself (tests/golden/coinrun_oracle_traj.npz)."""
     path = os.path.join(GOLDEN, "coinrun_oracle_traj.npz")
@@ -172,3 +192,27 @@ def test_oracle_trajectory_fixture():
             if t in frames_at:
                 np.testing.assert_array_equal(ob["rgb"][0], z["frames"][frames_at.index(t), k])
         fi += 1
+
+
+MAZE_CASES = [(mode, dim, 0) for mode in (0, 1) for dim in (3, 5, 7, 11, 13, 15, 25)] + \
+             [(2, dim, doors) for dim in (5, 7, 9, 11, 13, 23) for doors in (0, 1, 2, 3)]
+
+
+@pytest.mark.parametrize("mode,dim,doors", MAZE_CASES)
+def test_mazegen_vs_reference(mode, dim, doors):
+    """MazeGen (Kruskal, no-dead-ends, doors + BFS keys, place_objects) against the reference's own
+    mazegen.cpp compiled from /root/reference (oracle/_ref), grid and next RNG draw bit-exact."""
+    ref = ref_lib()
+    ref.ref_mazegen.argtypes = [ctypes.c_int32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_void_p, ctypes.c_void_p]
+    lib = oracle_lib.load()
+    n = (dim + 2) ** 2
+    for seed in range(40):
+        objs = 1 if mode == 0 else 0
+        a, b = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        da, db = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        ra = lib.oracle_mazegen(seed * 7919 + dim, dim, mode, doors, 2, objs, a.ctypes.data, da.ctypes.data)
+        rb = ref.ref_mazegen(seed * 7919 + dim, dim, mode, doors, 2, objs, b.ctypes.data, db.ctypes.data)
+        assert ra == rb == dim + 2
+        np.testing.assert_array_equal(a, b, err_msg="seed %d" % seed)
+        assert da[0] == db[0]

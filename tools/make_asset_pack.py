@@ -62,7 +62,10 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         tool = os.path.join(td, "qt_asset_dump")
         build_dumper(tool)
+        only = sys.argv[1:]
         for game in catalog.SUPPORTED_GAMES:
+            if only and game not in only:
+                continue
             names = sorted({n for v in catalog.sprite_table(game).values() for n in v})
             imgs = dump(tool, [("S", n) for n in names])
             np.savez_compressed(os.path.join(OUT_DIR, "sprites_%s.npz" % game),

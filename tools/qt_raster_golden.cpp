@@ -14,6 +14,8 @@
 //     f64 x, y, w, h ; f64 opacity ; u32 mirrored ; u32 rotate_deg_x1000 (signed, 0 = none)
 //     kind 0: u32 img_fmt (6 = ARGB32_Premultiplied, 4 = RGB32), u32 w, u32 h, u32 pixels[w*h]
 //     kind 1/2: u32 color (0xAARRGGBB)
+//     kind 3: f64 deg, then as kind 0: drawImage(QRectF(-w/2, -h/2, w, h)) after
+//             translate(x + w/2, y + h/2) and rotate(deg) (basic-abstract-game.cpp:908-916)
 // stdout: per case u32 canvas[64*64] after painting.
 #include <QImage>
 #include <QPainter>
@@ -45,7 +47,9 @@ int main() {
                 double opacity = rd<double>();
                 uint32_t mirrored = rd<uint32_t>();
                 int32_t rot = (int32_t)rd<uint32_t>();
-                if (kind == 0) {
+                double deg = 0;
+                if (kind == 3) deg = rd<double>();
+                if (kind == 0 || kind == 3) {
                     uint32_t ifmt = rd<uint32_t>(), iw = rd<uint32_t>(), ih = rd<uint32_t>();
                     QImage img(iw, ih, (QImage::Format)ifmt);
                     for (uint32_t yy = 0; yy < ih; yy++) {
@@ -55,7 +59,13 @@ int main() {
                     QImage use = mirrored ? img.mirrored(true, false) : img;
                     bool st = opacity != 1.0;
                     if (st) { p.save(); p.setOpacity(opacity); }
-                    if (rot == 0) {
+                    if (kind == 3) {
+                        p.save();
+                        p.translate(x + w / 2, y + h / 2);
+                        p.rotate(deg);
+                        p.drawImage(QRectF(-w / 2, -h / 2, w, h), use);
+                        p.restore();
+                    } else if (rot == 0) {
                         p.drawImage(QRectF(x, y, w, h), use);
                     } else {
                         p.save();
