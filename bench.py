@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Headline benchmark: env-steps/s of the MI355X Procgen engine (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): coinrun, num_envs = 65,536 per GPU, start_level=0,
+Workload (BASELINE.json configs[1], the default): coinrun, num_envs = 65,536 per GPU, start_level=0,
 num_levels=200, hard, center_agent, backgrounds -- ProcgenGym3Env defaults
 (procgen/env.py:229-246) -- with uniform random actions from an on-device counter hash
 (splitmix64).  One "step" = one libenv act on every env: game step + auto-reset/level
 generation + 64x64 render into the HBM-resident observation tensor.
 
     python bench.py --gpus N --steps K --warmup W
+    python bench.py --env-name bigfish                      (configs[2]; maze / heist: --num-envs 32768)
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
 Each rank owns the contiguous global env range [rank*E, (rank+1)*E) (level-seed draws of
@@ -32,11 +33,11 @@ HBM_PEAK = 8.0e12  # MI355X_MICROARCH.md: 8 TB/s spec
 
 
 def _cpu_worker(args):
-    n_envs, steps, seed = args
+    n_envs, steps, seed, game, num_levels = args
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import numpy as np
     from oracle_lib import OracleEnv
-    env = OracleEnv("coinrun", n_envs, num_levels=200, start_level=0, rand_seed=seed)
+    env = OracleEnv(game, n_envs, num_levels=num_levels, start_level=0, rand_seed=seed)
     rng = np.random.RandomState(seed)
     acts = rng.randint(0, 15, size=(steps, n_envs)).astype(np.int32)
     t0 = time.perf_counter()
@@ -45,20 +46,21 @@ def _cpu_worker(args):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(max_workers=16):
+def cpu_baseline(game, num_levels, max_workers=16, steps=3000):
     """The CPU oracle (scalar C restatement of the reference step path, parity-checked)
-    on this host: `cores` worker processes, each 64 coinrun envs x 400 steps."""
+    on this host: `cores` worker processes, each 64 envs x `steps` random steps (~10 s of
+    CPU work per worker for coinrun)."""
     cores = min(len(os.sched_getaffinity(0)), max_workers)
-    envs, steps = 64, 400
+    envs = 64
     with mp.get_context("spawn").Pool(cores) as pool:
         t0 = time.perf_counter()
-        times = pool.map(_cpu_worker, [(envs, steps, 1000 + i) for i in range(cores)])
+        times = pool.map(_cpu_worker, [(envs, steps, 1000 + i, game, num_levels) for i in range(cores)])
         wall = time.perf_counter() - t0
     rate = cores * envs * steps / max(times)
     return {"value": round(rate, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": "coinrun %d envs x %d random steps per worker, %d worker processes (oracle/procgen_oracle.c, "
-                      "-O2 -march=x86-64 -ffp-contract=off); rate = total env-steps / slowest worker (%.1f s wall)"
-                      % (envs, steps, cores, wall)}
+            "sample": "%s %d envs x %d random steps per worker, %d worker processes (oracle/procgen_oracle.c, "
+                      "-O2 -march=x86-64 -ffp-contract=off); rate = total env-steps / slowest worker "
+                      "(%.1f s wall, slowest worker %.1f s)" % (game, envs, steps, cores, wall, max(times))}
 
 
 def pmc_traffic():
@@ -80,6 +82,10 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--env-name", default="coinrun",
+                    help="game (or comma list = mixed batch); the headline metric is coinrun (BASELINE configs[1])")
+    ap.add_argument("--num-levels", type=int, default=None,
+                    help="default: 200 for coinrun (configs[1]), 0 = unbounded otherwise (SURVEY 8d)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -98,7 +104,9 @@ def main():
 
     from procgen_amd import ProcgenGym3Env
     E = args.num_envs
-    env = ProcgenGym3Env(num=E, env_name="coinrun", num_levels=200, start_level=0, rand_seed=0,
+    game = args.env_name
+    num_levels = args.num_levels if args.num_levels is not None else (200 if game == "coinrun" else 0)
+    env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
                          distribution_mode="hard", device_buffers=True, env_offset=rank * E)
     seed = 0x5EED
     t = 0
@@ -149,7 +157,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline()
+                cpu = cpu_baseline(game.split(",")[0], num_levels)
             except Exception as e:  # the baseline must never hide the GPU number
                 cpu = {"error": repr(e)}
         line = {
@@ -157,9 +165,10 @@ def main():
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
-            "config": {"workload": "coinrun num_envs=%d per GPU, start_level=0 num_levels=200, hard, "
-                                   "center_agent, backgrounds, random actions (device counter hash)" % E,
-                       "env_name": "coinrun", "num_envs_per_gpu": E, "global_envs": world * E,
+            "config": {"workload": "%s num_envs=%d per GPU, start_level=0 num_levels=%d, hard, "
+                                   "center_agent, backgrounds, random actions (device counter hash)"
+                                   % (game, E, num_levels),
+                       "env_name": game, "num_envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": "env-sharded x%d" % world},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -39,12 +39,18 @@ struct pg_device_buffers {
     void *stream;                /* hipStream_t every kernel of this env is enqueued on */
 };
 
-/* Upload the decoded sprite atlas (reference: images_load + asset_for_type tables).
- * sprites: [1000] slots (type + 100*theme), backgrounds: [num_backgrounds],
- * num_themes: [100].  Returns 0 on success. */
+#define PG_NUM_GAMES 16   /* game id = index in procgen/env.py:15-32 (bigfish 0 ... starpilot 15) */
+#define PG_NUM_SLOTS 1000 /* image slot = type + 100 * theme (basic-abstract-game.cpp:896) */
+#define PG_MAX_BG 64
+
+/* Upload the decoded sprite atlas (reference: images_load + each game's asset_for_type and
+ * background group, resources.cpp:20-30, 837-979).  One pixel array for all games; per-game
+ * tables indexed by game id: sprites [PG_NUM_GAMES][PG_NUM_SLOTS], backgrounds
+ * [PG_NUM_GAMES][PG_MAX_BG], num_backgrounds [PG_NUM_GAMES], num_themes [PG_NUM_GAMES][100].
+ * Only the games of the batch need to be filled.  Returns 0 on success. */
 LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int64_t num_pixels,
                                     const struct pg_image *sprites, const struct pg_image *backgrounds,
-                                    int num_backgrounds, const int32_t *num_themes);
+                                    const int32_t *num_backgrounds, const int32_t *num_themes);
 /* Initial reset + render of every env (what libenv_set_buffers triggers). */
 LIBENV_API int procgen_start(libenv_env *env);
 /* Step with actions already on the device (d_actions: int32[num_envs]); asynchronous. */
@@ -63,6 +69,9 @@ LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n);
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
 /* Diagnostic builds only (libprocgen_mi355x_prof.so): per-phase cycle sums, out[16]. */
 LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out);
+/* Self-test of libm-dependent device arithmetic on device buffers (tests/test_gpu_libm.py):
+ * which = 0: bigfish fish radius 1.75 * pow(u, 1.4) + .25 (bigfish.cpp:84) for n floats u. */
+LIBENV_API int procgen_selftest_libm(int which, const float *d_in, float *d_out, int64_t n, void *stream);
 /* Debug read-back of one env's scalar state, see pg_engine.h PGEnv (returns bytes copied). */
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length);
 

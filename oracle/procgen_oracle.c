@@ -2169,6 +2169,12 @@ static double rd_f64(Rd *r) {
 }
 
 /* replays ONE case body (after the canvas words) of tools/qt_raster_golden.cpp's format */
+/* bigfish.cpp:84 fish radius through the C library's pow (the checker of the device pow) */
+void oracle_bigfish_radius(const float *u, float *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++)
+        out[i] = (float)((double)(BF_FISH_MAX_R - BF_FISH_MIN_R) * pow((double)u[i], 1.4) + (double)BF_FISH_MIN_R);
+}
+
 /* MazeGen pin, same contract as oracle/ref_harness.cpp ref_mazegen */
 int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
                    uint32_t *next_draw) {

@@ -76,6 +76,8 @@ void oracle_randgen_script(uint32_t seed, const int32_t *ops, int nops, int32_t 
  * then place_objects if num_objs > 0; writes the array_dim^2 grid, returns array_dim */
 int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
                    uint32_t *next_draw);
+/* bigfish.cpp:84 fish radius 1.75 * pow(u, 1.4) + .25 with the C library's pow */
+void oracle_bigfish_radius(const float *u, float *out, int64_t n);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);
 

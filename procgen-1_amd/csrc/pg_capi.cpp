@@ -3,10 +3,12 @@
 // Host half of the reference's VecGame (procgen/src/vecgame.cpp): option parsing with the
 // reference's consume-once semantics (vecoptions.cpp:47-94), tensor types
 // (vecgame.cpp:212-330), level-seed derivation (vecgame.cpp:332-378), the act/observe
-// hand-off (vecgame.cpp:411-449) -- with the per-env work replaced by three HIP launches
-// per act on one stream: pg_step (all envs) -> pg_reset (queued envs) -> pg_render.
+// hand-off (vecgame.cpp:411-449) -- with the per-env work replaced by HIP launches on one
+// stream: pg_step (all envs) -> pg_reset (queued envs) -> pg_render, one launch of each per
+// game of the batch (mixed batches: env n plays game n % #games, vecgame.cpp:357-358).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -19,9 +21,11 @@
 #include "pg_engine.h"
 
 extern "C" {
-void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t);
-void pg_launch_reset(const PGDev *d, hipStream_t s, int all_envs, int grid);
-void pg_launch_render(const PGDev *d, hipStream_t s);
+void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int use_hash,
+                    uint64_t seed, int32_t t);
+void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
+                     int grid);
+void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s);
 void pg_launch_poison(hipStream_t s, uint32_t pattern);
 
 // PROCGEN_MI355X_POISON_LDS=1: scribble over LDS before every engine kernel (debug aid, see
@@ -104,7 +108,114 @@ struct Options {
 
 int game_id(const std::string &name) {
     if (name == "coinrun") return PG_GAME_COINRUN;
+    if (name == "bigfish") return PG_GAME_BIGFISH;
+    if (name == "maze") return PG_GAME_MAZE;
+    if (name == "heist") return PG_GAME_HEIST;
     return -1;
+}
+const char *SUPPORTED_GAMES = "bigfish, coinrun, heist, maze";
+
+std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
+    std::vector<std::string> out;
+    size_t p = 0;
+    while (true) {
+        size_t q = s.find(',', p);
+        out.push_back(s.substr(p, q == std::string::npos ? std::string::npos : q - p));
+        if (q == std::string::npos) break;
+        p = q + 1;
+    }
+    return out;
+}
+
+// Game ctor (game.cpp:25-39) + BasicAbstractGame ctor (basic-abstract-game.cpp:22-46) + the
+// game's own ctor
+void construct_env(PGEnv &s, int gid) {
+    memset(&s, 0, sizeof(s));
+    s.game_id = gid;
+    s.timeout = 1000;
+    s.episodes_remaining = 0;
+    s.last_reward = -1;
+    s.reset_count = 0;
+    s.current_level_seed = 0;
+    s.sd_reward = 0;
+    s.sd_done = 1;
+    s.sd_level_complete = 0;
+    s.char_dim = 5;
+    s.visibility = 16;
+    s.min_visibility = 0;
+    s.mixrate = 0.5f;
+    s.maxspeed = 0.5f;
+    s.max_jump = s.maxspeed;
+    s.default_action = 4;
+    s.last_move_action = 7;
+    s.bg_tile_ratio = 0;
+    s.out_of_bounds_object = -1; // INVALID_OBJ
+    s.has_useful_vel_info = 1;
+    s.random_agent_start = 1;
+    if (gid == PG_GAME_COINRUN) { // coinrun.cpp:49-58
+        s.visibility = 13;
+        s.mixrate = 0.2f;
+        s.main_width = 64;
+        s.main_height = 64;
+        s.out_of_bounds_object = 15; // WALL_MID
+    } else if (gid == PG_GAME_BIGFISH) { // bigfish.cpp:24-29
+        s.timeout = 6000;
+        s.main_width = 20;
+        s.main_height = 20;
+    } else if (gid == PG_GAME_MAZE) { // maze.cpp:20-28
+        s.timeout = 500;
+        s.random_agent_start = 0;
+        s.has_useful_vel_info = 0;
+        s.out_of_bounds_object = 51; // WALL_OBJ
+        s.visibility = 8.0f;
+    } else if (gid == PG_GAME_HEIST) { // heist.cpp:23-35
+        s.has_useful_vel_info = 0;
+        s.main_width = 20;
+        s.main_height = 20;
+        s.out_of_bounds_object = 51; // WALL_OBJ
+        s.visibility = 8.0f;
+    }
+}
+
+// Rotations the games draw at (entity rotation values, radians) and the QTransform each one
+// becomes: draw_image's p.rotate(rotation * 180 / PI) (basic-abstract-game.cpp:908-916) ->
+// QTransform::rotate (exact special cases for +-90 / 180 / 270, otherwise qSin / qCos of
+// deg2rad * a -- the C library's sin / cos, evaluated here on the host so the device matrix
+// is bit-identical).  Slots (dx + 1) * 3 + (dy + 1): Entity::face_direction(dx, dy) =
+// -atan2f(dy, dx) + 0 (entity.cpp:84-88, heist.cpp:208); slot 9: heist's ring keys (PI / 2,
+// heist.cpp:195).
+void build_rot_table(float *angles, double *table) {
+    const float PI_F = 3.14159265358979323846264338327950288f;
+    for (int k = 0; k < PG_ROT_N; k++) {
+        uint32_t nan_bits = 0x7fc00000u + (uint32_t)k;
+        memcpy(&angles[k], &nan_bits, 4); // unused slots match no entity rotation
+        table[4 * k + 0] = 1; table[4 * k + 1] = 0; table[4 * k + 2] = 0; table[4 * k + 3] = 1;
+    }
+    for (int dx = -1; dx <= 1; dx++)
+        for (int dy = -1; dy <= 1; dy++)
+            if (dx != 0 || dy != 0) angles[(dx + 1) * 3 + (dy + 1)] = -1 * atan2f((float)dy, (float)dx) + 0.0f;
+    angles[9] = PI_F / 2;
+    for (int k = 0; k < PG_ROT_N; k++) {
+        float rot = angles[k];
+        if (std::isnan(rot)) continue;
+        double a = (double)(rot * 180 / PI_F);
+        double sina = 0, cosa = 0;
+        if (a == 0) {
+            cosa = 1;
+        } else if (a == 90. || a == -270.) {
+            sina = 1;
+        } else if (a == 270. || a == -90.) {
+            sina = -1;
+        } else if (a == 180.) {
+            cosa = -1;
+        } else {
+            const double deg2rad = 0.017453292519943295769;
+            double b = deg2rad * a;
+            sina = std::sin(b);
+            cosa = std::cos(b);
+        }
+        table[4 * k + 0] = cosa; table[4 * k + 1] = sina; table[4 * k + 2] = -sina; table[4 * k + 3] = cosa;
+    }
 }
 
 struct VecEnv {
@@ -137,6 +248,14 @@ struct VecEnv {
     int device = 0;
     int error = 0;
     std::string error_msg;
+    // games of the batch: env n plays games[n % games.size()]
+    std::vector<int> games;
+    int32_t *d_lists = nullptr;            // [games.size()][num_envs / games.size()] env ids (mixed only)
+    bool has_latent = false;               // maze fills the fork's latent-state info
+    const int32_t *list_of(size_t k) const {
+        return games.size() > 1 ? d_lists + k * (size_t)(num_envs / games.size()) : nullptr;
+    }
+    int count_of() const { return num_envs / (int)games.size(); }
 };
 
 #define HIPCHECK(x)                                                                      \
@@ -207,16 +326,22 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         e = &v->ev[(size_t)v->t_used * 4];
         v->t_used++;
     }
-    HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t), v->stream));
+    HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t) * PG_NUM_GAMES, v->stream));
     if (e) HIPCHECK(hipEventRecord(e[0], v->stream));
-    PG_POISON(v->stream);
-    pg_launch_step(&v->dev, v->stream, use_hash, seed, t);
+    for (size_t k = 0; k < v->games.size(); k++) {
+        PG_POISON(v->stream);
+        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, use_hash, seed, t);
+    }
     if (e) HIPCHECK(hipEventRecord(e[1], v->stream));
-    PG_POISON(v->stream);
-    pg_launch_reset(&v->dev, v->stream, 0, 0);
+    for (size_t k = 0; k < v->games.size(); k++) {
+        PG_POISON(v->stream);
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, 0);
+    }
     if (e) HIPCHECK(hipEventRecord(e[2], v->stream));
-    PG_POISON(v->stream);
-    pg_launch_render(&v->dev, v->stream);
+    for (size_t k = 0; k < v->games.size(); k++) {
+        PG_POISON(v->stream);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
+    }
     if (e) HIPCHECK(hipEventRecord(e[3], v->stream));
     HIPCHECK(hipGetLastError());
     return 0;
@@ -277,6 +402,15 @@ int copy_out(VecEnv *v) {
     scatter(v->pinned + off[3], 4, &v->info_ptrs[0 * n]);
     scatter(v->pinned + off[4], 1, &v->info_ptrs[1 * n]);
     scatter(v->pinned + off[5], 4, &v->info_ptrs[2 * n]);
+    if (v->has_latent) { // grid_size, grid, agent_pos, exit_pos (vecgame.cpp:270-316)
+        const size_t row = (size_t)PG_LATENT_N * 4;
+        std::vector<int32_t> lat((size_t)PG_LATENT_N * n);
+        HIPCHECK(copy_sync(v, lat.data(), v->dev.latent, row * n, hipMemcpyDeviceToHost));
+        const size_t parts[4][2] = {{0, 2}, {2, PG_LATENT_GRID}, {2 + PG_LATENT_GRID, 2}, {4 + PG_LATENT_GRID, 2}};
+        for (int k = 0; k < 4; k++)
+            for (size_t e = 0; e < n; e++)
+                memcpy(v->info_ptrs[(3 + k) * n + e], &lat[e * PG_LATENT_N + parts[k][0]], parts[k][1] * 4);
+    }
     return 0;
 }
 
@@ -347,11 +481,18 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     if (num_levels < 0) return bad("num_levels must be >= 0");
     if (start_level < 0) return bad("start_level must be >= 0");
     if (num_envs <= 0) return bad("num_envs must be > 0");
-    if (env_name.find(',') != std::string::npos) return bad("mixed env batches are not in this build yet");
-    int gid = game_id(env_name);
-    if (gid < 0) return bad("env '" + env_name + "' is not in this build (supported: coinrun)");
-    // game.cpp:76-86 distribution mode validity
-    if (!(distribution_mode == PG_EASY || distribution_mode == PG_HARD)) return bad("invalid distribution_mode for " + env_name);
+    std::vector<std::string> names = split_names(env_name);
+    std::vector<int> gids;
+    for (const std::string &nm : names) {
+        int gid = game_id(nm);
+        if (gid < 0) return bad("env '" + nm + "' is not in this build (supported: " + SUPPORTED_GAMES + ")");
+        // game.cpp:76-86 distribution mode validity
+        bool dm_ok = distribution_mode == PG_EASY || distribution_mode == PG_HARD ||
+                     (distribution_mode == PG_MEMORY && (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE));
+        if (!dm_ok) return bad("invalid distribution_mode for " + nm);
+        gids.push_back(gid);
+    }
+    if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
     if (use_generated_assets) return bad("use_generated_assets is not in this build yet");
     if (use_monochrome_assets) return bad("use_monochrome_assets is not in this build yet");
     if (paint_vel_info) return bad("paint_vel_info is not in this build yet");
@@ -359,6 +500,8 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
 
     VecEnv *v = new VecEnv();
     v->num_envs = num_envs;
+    v->games = gids;
+    for (int g : gids) v->has_latent = v->has_latent || g == PG_GAME_MAZE;
     v->env_offset = env_offset;
     v->num_actions = num_actions;
     v->render_human = render_human;
@@ -407,8 +550,16 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.prev_level_seed, n);
     rc |= dalloc(v, &d.prev_level_complete, n);
     rc |= dalloc(v, &d.level_seed, n);
-    rc |= dalloc(v, &d.reset_queue, n);
-    rc |= dalloc(v, &d.reset_count, 1);
+    rc |= dalloc(v, &d.reset_queue, n * PG_NUM_GAMES);
+    rc |= dalloc(v, &d.reset_count, PG_NUM_GAMES);
+    if (v->has_latent) rc |= dalloc(v, &d.latent, n * PG_LATENT_N);
+    if (gids.size() > 1) rc |= dalloc(v, &v->d_lists, n);
+    float *d_rot_angles = nullptr;
+    double *d_rot_table = nullptr;
+    rc |= dalloc(v, &d_rot_angles, PG_ROT_N);
+    rc |= dalloc(v, &d_rot_table, PG_ROT_N * 4);
+    d.rot_angles = d_rot_angles;
+    d.rot_table = d_rot_table;
     rc |= dalloc(v, &d.error_any, 1);
     rc |= dalloc(v, &d.prof, n * 16); // written only by PG_PROFILE (diagnostic) builds
     if (rc) {
@@ -426,34 +577,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     for (int k = 0; k < env_offset; k++) (void)seed_gen.next();
     for (size_t e = 0; e < n; e++) {
         PGEnv &s = h[e];
-        memset(&s, 0, sizeof(s));
-        s.game_id = gid;
-        s.timeout = 1000;
-        s.episodes_remaining = 0;
-        s.last_reward = -1;
-        s.reset_count = 0;
-        s.current_level_seed = 0;
-        s.sd_reward = 0;
-        s.sd_done = 1;
-        s.sd_level_complete = 0;
-        s.char_dim = 5;
-        s.visibility = 16;
-        s.min_visibility = 0;
-        s.mixrate = 0.5f;
-        s.maxspeed = 0.5f;
-        s.max_jump = s.maxspeed;
-        s.default_action = 4;
-        s.last_move_action = 7;
-        s.bg_tile_ratio = 0;
-        s.out_of_bounds_object = -1;
-        s.has_useful_vel_info = 1;
-        s.random_agent_start = 1;
-        // coinrun ctor
-        s.visibility = 13;
-        s.mixrate = 0.2f;
-        s.main_width = 64;
-        s.main_height = 64;
-        s.out_of_bounds_object = 15; // WALL_MID
+        construct_env(s, gids[e % gids.size()]);
         s.level_seed_low = level_seed_low;
         s.level_seed_high = level_seed_high;
         s.game_n = env_offset + (int)e;
@@ -471,8 +595,22 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         memcpy(&hmt[(e * 2 + 1) * PG_MT_WORDS], lsg.mt, sizeof(lsg.mt));
         s.lsg_mti = lsg.mti;
     }
+    // env lists of a mixed batch: game k owns envs k, k + G, k + 2G, ...
+    std::vector<int32_t> lists;
+    const size_t ng = gids.size();
+    if (ng > 1) {
+        lists.resize(n);
+        for (size_t k = 0; k < ng; k++)
+            for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + k);
+    }
+    float rot_angles[PG_ROT_N];
+    double rot_table[PG_ROT_N * 4];
+    build_rot_table(rot_angles, rot_table);
     if (hipMemcpyAsync(d.envs, h.data(), sizeof(PGEnv) * n, hipMemcpyHostToDevice, v->stream) != hipSuccess ||
         hipMemcpyAsync(d.mt, hmt.data(), hmt.size() * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess ||
+        (ng > 1 && hipMemcpyAsync(v->d_lists, lists.data(), n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess) ||
+        hipMemcpyAsync(d_rot_angles, rot_angles, sizeof(rot_angles), hipMemcpyHostToDevice, v->stream) != hipSuccess ||
+        hipMemcpyAsync(d_rot_table, rot_table, sizeof(rot_table), hipMemcpyHostToDevice, v->stream) != hipSuccess ||
         hipStreamSynchronize(v->stream) != hipSuccess) {
         libenv_close(v);
         return bad("device upload failed");
@@ -498,21 +636,24 @@ LIBENV_API int libenv_get_tensortypes(libenv_env *env, enum libenv_space_name na
 
 LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int64_t num_pixels,
                                     const struct pg_image *sprites, const struct pg_image *backgrounds,
-                                    int num_backgrounds, const int32_t *num_themes) {
+                                    const int32_t *num_backgrounds, const int32_t *num_themes) {
     VecEnv *v = (VecEnv *)env;
-    if (num_backgrounds <= 0 || num_backgrounds > PG_MAX_BG) return fail(v, PG_ERR_NO_ATLAS, "bad background count");
-    if (dalloc(v, &v->d_pixels, (size_t)num_pixels) || dalloc(v, &v->d_sprites, PG_NUM_SLOTS * 4) ||
-        dalloc(v, &v->d_bgs, (size_t)num_backgrounds * 4) || dalloc(v, &v->d_themes, 100))
+    for (int g : v->games)
+        if (num_backgrounds[g] <= 0 || num_backgrounds[g] > PG_MAX_BG)
+            return fail(v, PG_ERR_NO_ATLAS, "bad background count for a game of the batch");
+    const size_t slots = (size_t)PG_NUM_GAMES * PG_NUM_SLOTS, bgs = (size_t)PG_NUM_GAMES * PG_MAX_BG;
+    if (dalloc(v, &v->d_pixels, (size_t)num_pixels) || dalloc(v, &v->d_sprites, slots * 4) ||
+        dalloc(v, &v->d_bgs, bgs * 4) || dalloc(v, &v->d_themes, (size_t)PG_NUM_GAMES * 100))
         return -PG_ERR_HIP;
     HIPCHECK(copy_sync(v, v->d_pixels, pixels, (size_t)num_pixels * 4, hipMemcpyHostToDevice));
-    HIPCHECK(copy_sync(v, v->d_sprites, sprites, PG_NUM_SLOTS * sizeof(pg_image), hipMemcpyHostToDevice));
-    HIPCHECK(copy_sync(v, v->d_bgs, backgrounds, (size_t)num_backgrounds * sizeof(pg_image), hipMemcpyHostToDevice));
-    HIPCHECK(copy_sync(v, v->d_themes, num_themes, 100 * 4, hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_sprites, sprites, slots * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_bgs, backgrounds, bgs * sizeof(pg_image), hipMemcpyHostToDevice));
+    HIPCHECK(copy_sync(v, v->d_themes, num_themes, (size_t)PG_NUM_GAMES * 100 * 4, hipMemcpyHostToDevice));
     v->dev.pixels = v->d_pixels;
     v->dev.sprites = v->d_sprites;
     v->dev.backgrounds = v->d_bgs;
-    v->dev.num_backgrounds = num_backgrounds;
     v->dev.num_themes = v->d_themes;
+    for (int g = 0; g < PG_NUM_GAMES; g++) v->dev.num_bg[g] = num_backgrounds[g];
     v->atlas = true;
     return 0;
 }
@@ -521,10 +662,14 @@ LIBENV_API int procgen_start(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     if (v->started) return 0;
-    PG_POISON(v->stream);
-    pg_launch_reset(&v->dev, v->stream, 1, 0);
-    PG_POISON(v->stream);
-    pg_launch_render(&v->dev, v->stream);
+    for (size_t k = 0; k < v->games.size(); k++) {
+        PG_POISON(v->stream);
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0);
+    }
+    for (size_t k = 0; k < v->games.size(); k++) {
+        PG_POISON(v->stream);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
+    }
     HIPCHECK(hipGetLastError());
     v->started = true;
     return 0;
@@ -540,7 +685,8 @@ LIBENV_API void libenv_set_buffers(libenv_env *env, struct libenv_buffers *bufs)
     v->first_host = bufs->first;
     v->buffers_set = true;
     // latent-state info tensors (grid_size, grid, agent_pos, exit_pos) are only filled by
-    // maze/miner (maze.cpp:152-165, miner.cpp:378-396); zero them for this game
+    // maze/miner (maze.cpp:152-165, miner.cpp:378-396); zero them for the other games (copy_out
+    // overwrites them every observe when a game of the batch has a latent state)
     for (size_t k = 3; k < v->info_types.size(); k++) {
         size_t bytes = 4;
         for (int dd = 0; dd < v->info_types[k].ndim; dd++) bytes *= (size_t)v->info_types[k].shape[dd];
@@ -736,11 +882,28 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
         p += ents * 4;
     }
     if (cells) copy_sync(v, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
+    if (v->has_latent && s.game_id == PG_GAME_MAZE) { // the latent info mirrors the restored grid
+        std::vector<int32_t> lat(PG_LATENT_N, 0);
+        lat[0] = s.main_width;
+        lat[1] = s.main_height;
+        for (size_t k = 0; k < cells && k < PG_LATENT_GRID; k++) {
+            int16_t cv;
+            memcpy(&cv, p + 2 * k, 2);
+            lat[2 + k] = cv;
+        }
+        float ax, ay;
+        memcpy(&ax, p - PG_NF * ents * 4 + (size_t)F_X * ents * 4, 4); // entity 0 = the agent
+        memcpy(&ay, p - PG_NF * ents * 4 + (size_t)F_Y * ents * 4, 4);
+        lat[2 + PG_LATENT_GRID] = ents ? (int)ax : 0;
+        lat[3 + PG_LATENT_GRID] = ents ? (int)ay : 0;
+        copy_sync(v, v->dev.latent + (size_t)env_idx * PG_LATENT_N, lat.data(), PG_LATENT_N * 4, hipMemcpyHostToDevice);
+    }
     p += cells * 2;
     copy_sync(v, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, p, 2 * PG_MT_WORDS * 4, hipMemcpyHostToDevice);
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
-    pg_launch_render(&v->dev, v->stream);
+    for (size_t k = 0; k < v->games.size(); k++)
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
     hipStreamSynchronize(v->stream);
 }
 

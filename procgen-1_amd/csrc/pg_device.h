@@ -51,6 +51,27 @@
 #define CR_ENEMY_BARRIER 19
 #define CR_CRATE 20
 
+// bigfish.cpp:7-17
+#define BF_FISH 2
+#define BF_FISH_MIN_R .25f
+#define BF_FISH_MAX_R 2.0f
+#define BF_FISH_QUOTA 30
+// maze.cpp:6-12
+#define MZ_GOAL 2
+// heist.cpp:10-15
+#define HS_LOCKED_DOOR 1
+#define HS_KEY 2
+#define HS_EXIT 9
+#define HS_KEY_ON_RING 11
+// object-ids.h
+#define EXIT_OBJ 52
+#define AGENT_OBJ 53
+#define DOOR_OBJ 200
+#define KEY_OBJ 300
+// rot_table slots: face_direction(dx, dy) -> (dx + 1) * 3 + (dy + 1); ring keys (PI / 2)
+#define PG_ROT_RING_KEY 9
+#define PI_F 3.14159265358979323846264338327950288f
+
 DEV bool cr_is_wall(int t) { return t == CR_WALL_MID || t == CR_WALL_TOP; }
 DEV bool cr_is_lava(int t) { return t == CR_LAVA_MID || t == CR_LAVA_TOP; }
 

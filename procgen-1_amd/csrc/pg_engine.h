@@ -9,6 +9,7 @@
 // entity.h, games/coinrun.cpp).
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 
 #define PG_RES 64
 #define PG_OBS_BYTES (64 * 64 * 3)
@@ -19,7 +20,12 @@
 #define PG_NUM_SLOTS 1000     // image slots: type + 100 * theme
 #define PG_MAX_BG 64
 
-enum PGGame { PG_GAME_COINRUN = 5 };
+// game ids = index in the reference's env list (procgen/env.py:15-32)
+enum PGGame { PG_GAME_BIGFISH = 0, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11 };
+#ifndef PG_NUM_GAMES
+#define PG_NUM_GAMES 16
+#endif
+#define PG_LATENT_GRID (35 * 35) // fork latent-state grid info (vecgame.cpp:280-291)
 
 // error codes (mirrored in include/procgen_mi355x.h)
 #ifndef PG_ERR_NONE
@@ -126,7 +132,15 @@ struct PGEnv {
     int32_t lsg_mti;          // level_seed_rand_gen position
     int32_t error;            // PG_ERR_* of this env (sticky)
     int32_t grid8_ok;         // the int8 grid mirror is current (written at reset)
-    int32_t pad[128 - 68];
+    // ---- bigfish (bigfish.cpp:20-22)
+    int32_t fish_eaten;
+    float r_inc;
+    // ---- maze (maze.cpp:16-18) / heist (heist.cpp:18-21)
+    int32_t maze_dim;
+    int32_t world_dim;
+    int32_t num_keys;
+    int32_t has_keys;         // bit k = has_keys[k]
+    int32_t pad[128 - 74];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
@@ -152,10 +166,28 @@ struct PGDev {
     int32_t *reset_count;     // [1]
     int32_t *error_any;       // [1] OR of all env errors
     uint64_t *prof;           // [num_envs][16] per-phase s_memtime sums (PG_PROFILE builds only)
-    // atlas
+    // atlas: one pixel array, per-game tables (a kernel of game G sees its own via game_view)
     const uint32_t *pixels;
-    const int32_t *sprites;   // [PG_NUM_SLOTS][4] (offset, w, h, pad)
-    const int32_t *backgrounds; // [num_bg][4]
-    int32_t num_backgrounds;
-    const int32_t *num_themes;  // [100]
+    const int32_t *sprites;   // [PG_NUM_GAMES][PG_NUM_SLOTS][4] (offset, w, h, pad)
+    const int32_t *backgrounds; // [PG_NUM_GAMES][PG_MAX_BG][4]
+    int32_t num_backgrounds;    // of the viewed game
+    const int32_t *num_themes;  // [PG_NUM_GAMES][100]
+    int32_t num_bg[PG_NUM_GAMES];
+    // rotation transforms of QTransform::rotate for the angles the games draw at (host-built
+    // with the C library's sin/cos, exactly as Qt's qSin/qCos; see pg_capi.cpp rot_table)
+    const double *rot_table;    // [PG_ROT_N][4] = m11, m12, m21, m22
+    const float *rot_angles;    // [PG_ROT_N] entity rotation values (radians, float) of the table
+    int32_t *latent;            // [num_envs][PG_LATENT_N] grid_size, grid, agent_pos, exit_pos (maze)
 };
+#define PG_ROT_N 16
+#define PG_LATENT_N (2 + PG_LATENT_GRID + 2 + 2)
+
+// The tables of game G (kernels are instantiated per game).
+static inline __host__ __device__ PGDev game_view(const PGDev &d, int g) {
+    PGDev v = d;
+    v.sprites = d.sprites + (size_t)g * PG_NUM_SLOTS * 4;
+    v.backgrounds = d.backgrounds + (size_t)g * PG_MAX_BG * 4;
+    v.num_themes = d.num_themes + (size_t)g * 100;
+    v.num_backgrounds = d.num_bg[g];
+    return v;
+}

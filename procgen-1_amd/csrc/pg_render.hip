@@ -1,5 +1,6 @@
 // pg_render.hip -- Game::observe: 64x64 render + bgr32_to_rgb888 (reference game.cpp:8-23,
-// 97-107, 173-191; basic-abstract-game.cpp:808-1075; games/coinrun.cpp:64-70, 133-138, 213-225).
+// 97-107, 173-191; basic-abstract-game.cpp:808-1075; games/coinrun.cpp:64-70, 133-138, 213-225;
+// heist.cpp:42-44, 73-78).  A template over the game id (per-game hooks are `if constexpr`).
 //
 // One wavefront per env, a 16 KB RGB32 framebuffer in LDS.  The painter's algorithm of
 // the reference is kept exactly, but each layer is rasterised the way a wave64 likes:
@@ -74,7 +75,8 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Size of the per-type grid sprite table (grid values 0..127 take the fast path).
 #define NTYPES 128
-// Tile images all have this size in coinrun (other sizes are flagged, not drawn wrongly).
+// Most grid tile images have this size ("class 0"); one other size per game is handled by the
+// generic pass (maze's 27 px cheese), anything else is flagged, never drawn wrongly.
 #define TILE_PX 128
 // Most tile rows a frame may span on the fast path (centred coinrun views span 14-15).
 #define CROWS 16
@@ -86,20 +88,173 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 #define EG 8
 #endif
 
+
+// ------------------------------------------------------------------ per-game render hooks
+// image_for_type (basic :446-448; coinrun.cpp:213-225): coinrun animates the player for the
+// whole frame and hides ENEMY_BARRIER
+template <int G>
+DEV int player_image(const PGEnv &s, float agent_vx) {
+    if constexpr (G == PG_GAME_COINRUN)
+        return (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
+                   ? PLAYER
+                   : ((s.cur_time / 5 % 2 == 0 || !s.has_support) ? CR_PLAYER_RIGHT1 : CR_PLAYER_RIGHT2);
+    return PLAYER;
+}
+template <int G>
+DEV int image_for_type(int type, int player_img) {
+    if constexpr (G == PG_GAME_COINRUN) {
+        if (type == PLAYER) return player_img;
+        if (type == CR_ENEMY_BARRIER) return -1;
+    }
+    return type < 0 ? -type : type;
+}
+template <int G>
+DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cpp:133-138)
+    if constexpr (G == PG_GAME_COINRUN) return cr_is_wall(type) ? s.wall_theme : 0;
+    return 0;
+}
+template <int G>
+DEV int mask_theme(const PGEnv &s, int theme, int img_type) { // mask_theme_if_necessary (:454-462, heist.cpp:42-44)
+    bool preserve = G == PG_GAME_HEIST && (img_type == HS_KEY || img_type == HS_LOCKED_DOOR);
+    return (s.opt_restrict_themes && !preserve) ? 0 : theme;
+}
+template <int G>
+DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entity (heist.cpp:73-78)
+    if constexpr (G == PG_GAME_HEIST)
+        if (type == HS_KEY_ON_RING) return (s.has_keys >> theme) & 1;
+    return true;
+}
+template <int G>
+DEV bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
+// grid types whose tile image is not TILE_PX square but is drawn as a tile (class 1)
+template <int G>
+DEV bool odd_size_tile(int type) {
+    if constexpr (G == PG_GAME_MAZE) return type == MZ_GOAL; // cheese.png, 27 x 27
+    return false;
+}
+
+// ------------------------------------------------------------------ rotated drawImage
+// save(); translate(center); rotate(rotation * 180 / PI); drawImage(QRectF(-w/2, -h/2, w, h))
+// (basic-abstract-game.cpp:908-916) -> Qt's qt_transform_image (qblendfunctions_p.h): the quad
+// is split into 3 trapezoids, each scan line covers [x_l >> 16, x_r >> 16) with 16.16
+// fixed-point texture stepping.  Along a scan line the in-source texels form one interval and
+// the reference clamps the ones outside it, so a pixel's texel is clamp(u >> 16), clamp(v >> 16)
+// with u = x * dudx + y * dudy + u0 -- evaluated per pixel (lane = column, loop over rows).
+// The rotation matrix comes from the host table (exact C-library sin/cos, as Qt's qSin/qCos).
+struct Trap { int from_y, to_y, x_l, dx_l, x_r, dx_r; };
+struct QV { double x, y, u, v; };
+
+DEV void trap_setup(const QV &tl, const QV &bl, const QV &tr, const QV &br, double topY, double bottomY, Trap &t) {
+    t.from_y = max(qRound(topY), 0);
+    t.to_y = min(qRound(bottomY), PG_RES);
+    t.x_l = t.x_r = t.dx_l = t.dx_r = 0;
+    if (t.from_y >= t.to_y) return;
+    double leftSlope = (bl.x - tl.x) / (bl.y - tl.y);
+    double rightSlope = (br.x - tr.x) / (br.y - tr.y);
+    t.dx_l = (int)(leftSlope * 0x10000);
+    t.dx_r = (int)(rightSlope * 0x10000);
+    t.x_l = (int)((tl.x + (0.5 + t.from_y - tl.y) * leftSlope + 0.5) * 0x10000);
+    t.x_r = (int)((tr.x + (0.5 + t.from_y - tr.y) * rightSlope + 0.5) * 0x10000);
+}
+
+// returns false when the transform is not a rotation this path reproduces
+DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, double x, double y, double w, double h, double m11,
+                      double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
+    if (!(w > 0) || !(h > 0) || iw <= 0 || ih <= 0) return true; // QRectF::isEmpty: nothing drawn
+    if (m12 == 0 && m21 == 0) return false;                      // TxScale (rotate(180)): scale path
+    const double dx = x + w / 2, dy = y + h / 2;
+    const double rx = -w / 2, ry = -h / 2, right = rx + w, bottom = ry + h;
+    QV v[4]; // TopLeft, TopRight, BottomRight, BottomLeft
+    auto map = [&](double px, double py, QV &o) {
+        o.x = m11 * px + m21 * py + dx;
+        o.y = m12 * px + m22 * py + dy;
+    };
+    map(rx, ry, v[0]); map(right, ry, v[1]); map(right, bottom, v[2]); map(rx, bottom, v[3]);
+    v[0].u = 0; v[0].v = 0; v[1].u = iw; v[1].v = 0; v[2].u = iw; v[2].v = ih; v[3].u = 0; v[3].v = ih;
+    int topmost = 0;
+    for (int i = 1; i < 4; ++i)
+        if (v[i].y < v[topmost].y) topmost = i;
+    QV t;
+    if (topmost == 1) {
+        t = v[0]; v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = t;
+    } else if (topmost == 2) {
+        t = v[0]; v[0] = v[2]; v[2] = t;
+        t = v[1]; v[1] = v[3]; v[3] = t;
+    } else if (topmost == 3) {
+        t = v[3]; v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = t;
+    }
+    double dx1 = v[1].x - v[0].x, dy1 = v[1].y - v[0].y;
+    double dx2 = v[3].x - v[0].x, dy2 = v[3].y - v[0].y;
+    if (dx1 * dy2 - dx2 * dy1 > 0) {
+        t = v[1]; v[1] = v[3]; v[3] = t;
+    }
+    QV u = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].u - v[0].u, v[1].v - v[0].v};
+    QV ww = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].u - v[0].u, v[2].v - v[0].v};
+    double det = u.x * ww.y - u.y * ww.x;
+    if (det == 0) return true;
+    double invDet = 1.0 / det;
+    double n11 = (u.u * ww.y - u.y * ww.u) * invDet;
+    double n12 = (u.x * ww.u - u.u * ww.x) * invDet;
+    double n21 = (u.v * ww.y - u.y * ww.v) * invDet;
+    double n22 = (u.x * ww.v - u.v * ww.x) * invDet;
+    double mdx = v[0].u - n11 * v[0].x - n12 * v[0].y;
+    double mdy = v[0].v - n21 * v[0].x - n22 * v[0].y;
+    const int dudx = (int)(n11 * 0x10000), dvdx = (int)(n21 * 0x10000);
+    const int dudy = (int)(n12 * 0x10000), dvdy = (int)(n22 * 0x10000);
+    const int u0 = (int)ceil((0.5 * n11 + 0.5 * n12 + mdx) * 0x10000) - 1;
+    const int v0 = (int)ceil((0.5 * n21 + 0.5 * n22 + mdy) * 0x10000) - 1;
+    Trap tr[3];
+    if (v[1].y < v[3].y) {
+        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[1].y, tr[0]);
+        trap_setup(v[1], v[2], v[0], v[3], v[1].y, v[3].y, tr[1]);
+        trap_setup(v[1], v[2], v[3], v[2], v[3].y, v[2].y, tr[2]);
+    } else {
+        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[3].y, tr[0]);
+        trap_setup(v[0], v[1], v[3], v[2], v[3].y, v[1].y, tr[1]);
+        trap_setup(v[1], v[2], v[3], v[2], v[1].y, v[2].y, tr[2]);
+    }
+    const int lane = LANE;
+    for (int k = 0; k < 3; k++) {
+        const Trap T = tr[k];
+        for (int yy = T.from_y; yy < T.to_y; yy++) {
+            const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
+            const int fromX = max(xl >> 16, 0), toX = min(xr >> 16, PG_RES);
+            if (lane >= fromX && lane < toX) {
+                int uu = (lane * dudx + yy * dudy + u0) >> 16;
+                int vv = (lane * dvdx + yy * dvdy + v0) >> 16;
+                uu = min(max(uu, 0), iw - 1);
+                vv = min(max(vv, 0), ih - 1);
+                if (mir) uu = iw - 1 - uu;
+                uint32_t src = pixels[soff + (uint32_t)(vv * iw + uu)];
+                fb[yy * PG_RES + lane] = blend_argb_pm(fb[yy * PG_RES + lane], src, ca);
+            }
+        }
+    }
+    return true;
+}
+
 } // namespace
 
-extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
+template <int G>
+__global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *env_list) {
+    const PGDev d = game_view(dg, G);
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
-    __shared__ int tile_off[NTYPES];  // sprite pixel offset of a grid type, -1: draws nothing, <= -2: unsupported
+    // grid type -> sprite pixel offset: >= 0 a TILE_PX x TILE_PX image ("class 0"), -1 draws nothing,
+    // -4 the game's one other tile size ("class 1", offset in tile_off1), <= -2 otherwise unsupported
+    __shared__ int tile_off[NTYPES];
+    __shared__ int tile_off1[NTYPES];
     // fast path: texel base of lane's first tile column per tile row.  Before it is built, the
-    // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row.
+    // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row
+    // (class 0 at [0, 128), class 1 at [128, 256) in int4 units).
     __shared__ __attribute__((aligned(16))) int colb[CROWS * 64];
-    static_assert(CROWS * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
+    static_assert(CROWS * 64 >= 4 * 64 * 4, "colb doubles as the axis tables");
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
-    const int env = blockIdx.x;
+    int4 *const colax1 = colax + 128;
+    int4 *const rowax1 = colax + 192;
+    const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     const PGEnv s = d.envs[env];
-    const int16_t *G = d.grid + (size_t)env * PG_GRID_MAX;
+    const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
     bool err = false;
 
     float agent_x, agent_y, agent_vx;
@@ -108,10 +263,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     } else {
         agent_x = EFr(d, F_X, env, 0); agent_y = EFr(d, F_Y, env, 0); agent_vx = EFr(d, F_VX, env, 0);
     }
-    // image_for_type(PLAYER) (coinrun.cpp:213-219): one animation frame for the whole frame
-    const int player_img = (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
-                               ? PLAYER
-                               : ((s.cur_time / 5 % 2 == 0 || !s.has_support) ? CR_PLAYER_RIGHT1 : CR_PLAYER_RIGHT2);
+    const int player_img = player_image<G>(s, agent_vx);
 
     // ---- prepare_for_drawing(rect_height = 64) (basic-abstract-game.cpp:828-847)
     View v;
@@ -135,24 +287,46 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     PTimer pt;
     pt.start();
 
-    // ---- grid type -> sprite table (theme_for_grid_obj coinrun.cpp:133-138, image_for_type :213-225,
-    //      draw_image basic-abstract-game.cpp:886-922)
-    for (int t = lane; t < NTYPES; t += 64) {
-        int off = -1;
-        int img = t == PLAYER ? player_img : (t == CR_ENEMY_BARRIER ? -1 : t);
-        if (img >= 0) {
-            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
-            } else {
-                int theme = cr_is_wall(t) ? s.wall_theme : 0;
-                if (s.opt_restrict_themes) theme = 0;
-                int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                if (sp.y == TILE_PX && sp.z == TILE_PX) off = sp.x;
-                else if (sp.y > 0) off = -2;
-                else off = -3; // generated assets: not in this build
+    // ---- grid type -> sprite table (theme_for_grid_obj, image_for_type, draw_image :886-922)
+    int cls1_w = 0, cls1_h = 0;
+    bool any_cls1 = false;
+    {
+        int my_w = 0, my_h = 0;
+        bool my1 = false;
+        for (int t = lane; t < NTYPES; t += 64) {
+            int off = -1, off1 = 0;
+            int img = image_for_type<G>(t, player_img);
+            if (img >= 0) {
+                if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+                    off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
+                } else {
+                    int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
+                    int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                    if (sp.y == TILE_PX && sp.z == TILE_PX) {
+                        off = sp.x;
+                    } else if (sp.y > 0 && sp.z > 0 && odd_size_tile<G>(t)) {
+                        off = -4;
+                        off1 = sp.x;
+                        if (my1 && (my_w != sp.y || my_h != sp.z)) err = true; // one extra size per lane
+                        my1 = true; my_w = sp.y; my_h = sp.z;
+                    } else if (sp.y > 0) {
+                        off = -2; // a tile size this build does not expect for the game (flagged if drawn)
+                    } else {
+                        off = -3; // generated assets: not in this build
+                    }
+                }
             }
+            tile_off[t] = off;
+            tile_off1[t] = off1;
         }
-        tile_off[t] = off;
+        unsigned long long m1 = ballot(my1);
+        any_cls1 = m1 != 0;
+        if (any_cls1) {
+            int l = __ffsll((long long)m1) - 1;
+            cls1_w = readlane(my_w, l);
+            cls1_h = readlane(my_h, l);
+            if (my1 && (my_w != cls1_w || my_h != cls1_h)) err = true;
+        }
     }
 
     // ---- visible tile window (basic-abstract-game.cpp:937-948)
@@ -191,7 +365,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     }
     if (tab) {
         // one x-axis and one y-axis setup per lane: tile column low_x + lane, tile row
-        // low_y + lane, or (lane 63) the background
+        // low_y + lane, or (lane 63) the background; class-1 tiles get a second pair
         double xr = 0, xw = 0, yr = 0, yh = 0;
         int xiw = 0, yih = 0;
         if (lane == 63) {
@@ -212,6 +386,13 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         const bool oky = axis_setup(yr, yh, yih, b);
         colax[lane] = make_int4(a.t1, okx ? a.n : 0, (int)a.base, a.step);
         rowax[lane] = make_int4(b.t1, oky ? b.n : 0, (int)b.base, b.step);
+        if (any_cls1) {
+            Axis a1, b1;
+            const bool ok1x = lane < 63 && lane < ww && axis_setup(xr, xw, cls1_w, a1);
+            const bool ok1y = lane < 63 && lane < wh && axis_setup(yr, yh, cls1_h, b1);
+            colax1[lane] = ok1x ? make_int4(a1.t1, a1.n, (int)a1.base, a1.step) : make_int4(0, 0, 0, 0);
+            rowax1[lane] = ok1y ? make_int4(b1.t1, b1.n, (int)b1.base, b1.step) : make_int4(0, 0, 0, 0);
+        }
         bg_ok = readlane(okx && oky ? 1 : 0, 63) != 0;
         bx.t1 = readlane(a.t1, 63); bx.n = readlane(a.n, 63); bx.base = (uint32_t)readlane((int)a.base, 63); bx.step = readlane(a.step, 63);
         by.t1 = readlane(b.t1, 63); by.n = readlane(b.n, 63); by.base = (uint32_t)readlane((int)b.base, 63); by.step = readlane(b.step, 63);
@@ -222,83 +403,85 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
     const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
 
-    // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images
-    int cx0 = 0, cx1 = 0, ncx = 0;
-    Axis ax0, ax1;
-    ax0.n = ax1.n = 0;
-    {
-        int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
-        for (int x = xg - 2; x <= xg + 2; x++) {
-            if (x < low_x || x > high_x || ncx == 2) continue;
-            Axis a;
-            bool ok;
-            if (tab) {
-                const int4 t = colax[x - low_x];
-                a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
-                ok = t.y > 0;
-            } else {
-                double rx, ry, rw, rh;
-                screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
-                ok = axis_setup(rx, rw, TILE_PX, a);
+    // Qt axis of tile column x / row y for image size `px` (class 0: TILE_PX, class 1: cls1 size)
+    auto col_axis = [&](int x, int cls, Axis &a) -> bool {
+        if (tab) {
+            const int4 t = (cls ? colax1 : colax)[x - low_x];
+            a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
+            return t.y > 0;
+        }
+        double rx, ry, rw, rh;
+        screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
+        return axis_setup(rx, rw, cls ? cls1_w : TILE_PX, a);
+    };
+    auto row_axis = [&](int y, int cls, Axis &a) -> bool {
+        if (tab) {
+            const int4 t = (cls ? rowax1 : rowax)[y - low_y];
+            a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
+            return t.y > 0;
+        }
+        double rx, ry, rw, rh;
+        screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+        return axis_setup(ry, rh, cls ? cls1_h : TILE_PX, a);
+    };
+    // tile columns covering screen column `lane` (<= 2 per class, ascending x) and their source columns
+    int cx[2][2] = {{0, 0}, {0, 0}}, sc[2][2] = {{0, 0}, {0, 0}}, ncx[2] = {0, 0};
+    int ry[2][2] = {{0, 0}, {0, 0}}, sr[2][2] = {{0, 0}, {0, 0}}, ncy[2] = {0, 0};
+    const int ncls = any_cls1 ? 2 : 1;
+    if (has_grid_tiles<G>()) {
+        const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
+        const int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
+        for (int k = 0; k < ncls; k++) {
+            for (int x = xg - 2; x <= xg + 2; x++) {
+                if (x < low_x || x > high_x || ncx[k] == 2) continue;
+                Axis a;
+                if (col_axis(x, k, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+                    cx[k][ncx[k]] = x;
+                    sc[k][ncx[k]] = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
+                    ncx[k]++;
+                }
             }
-            if (ok && lane >= a.t1 && lane < a.t1 + a.n) {
-                if (ncx == 0) { cx0 = x; ax0 = a; } else { cx1 = x; ax1 = a; }
-                ncx++;
+            // tile rows covering screen row `lane` (ascending y = the reference's draw order)
+            for (int y = yg - 2; y <= yg + 2; y++) {
+                if (y < low_y || y > high_y || ncy[k] == 2) continue;
+                Axis a;
+                if (row_axis(y, k, a) && lane >= a.t1 && lane < a.t1 + a.n) {
+                    ry[k][ncy[k]] = y;
+                    sr[k][ncy[k]] = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
+                    ncy[k]++;
+                }
             }
         }
     }
-    const int scol0 = ncx > 0 ? (int)((ax0.base + (uint32_t)((lane - ax0.t1) * ax0.step)) >> 16) : 0;
-    const int scol1 = ncx > 1 ? (int)((ax1.base + (uint32_t)((lane - ax1.t1) * ax1.step)) >> 16) : 0;
-    // tile rows covering screen row `lane` (<= 2, ascending y = the reference's draw order)
-    int ry0 = 0, ry1 = 0, ncy = 0, srow0 = 0, srow1 = 0;
-    {
-        int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
-        for (int y = yg - 2; y <= yg + 2; y++) {
-            if (y < low_y || y > high_y || ncy == 2) continue;
-            Axis a;
-            bool ok;
-            if (tab) {
-                const int4 t = rowax[y - low_y];
-                a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
-                ok = t.y > 0;
-            } else {
-                double rx, ry, rw, rh;
-                screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
-                ok = axis_setup(ry, rh, TILE_PX, a);
-            }
-            if (ok && lane >= a.t1 && lane < a.t1 + a.n) {
-                int sr = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
-                if (ncy == 0) { ry0 = y; srow0 = sr; } else { ry1 = y; srow1 = sr; }
-                ncy++;
-            }
-        }
-    }
+    // class-0 aliases used by the fast path
+    const int cx0 = cx[0][0], cx1 = cx[0][1], scol0 = sc[0][0], scol1 = sc[0][1], ncx0 = ncx[0];
+    const int ry0 = ry[0][0], ry1 = ry[0][1], srow0 = sr[0][0], srow1 = sr[0][1], ncy0 = ncy[0];
 
     // ---- lookups for the fast path: every screen row's tile rows lie in [jy0, jy1]; for
     //      each of those rows the texel base of this lane's first tile column goes to LDS
     //      (colb), so a pixel costs one LDS read + one texel load + one blend.
-    int jlo = ncy > 0 ? ry0 : 0x7fffffff, jhi = ncy > 1 ? ry1 : (ncy > 0 ? ry0 : -0x7fffffff);
+    int jlo = ncy0 > 0 ? ry0 : 0x7fffffff, jhi = ncy0 > 1 ? ry1 : (ncy0 > 0 ? ry0 : -0x7fffffff);
 #pragma unroll
     for (int sh = 1; sh < 64; sh <<= 1) {
         jlo = min(jlo, __shfl_xor(jlo, sh));
         jhi = max(jhi, __shfl_xor(jhi, sh));
     }
     const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
-    const bool fast = nrows <= CROWS;
+    const bool fast = has_grid_tiles<G>() && !any_cls1 && nrows <= CROWS;
     auto lookup_grid = [&](int x, int y) -> int {
-        int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? G[y * s.main_width + x]
+        int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
                                                                                : s.out_of_bounds_object;
         return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
     };
-    wave_sync(); // tile_off complete
+    wave_sync(); // tile tables complete
     if (fast) {
         int code[CROWS];
 #pragma unroll
         for (int j = 0; j < CROWS; j++) {
             code[j] = -1;
-            if (j < nrows && ncx > 0) {
+            if (j < nrows && ncx0 > 0) {
                 const int y = jy0 + j, x = cx0;
-                if (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) code[j] = G[y * s.main_width + x];
+                if (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) code[j] = Gd[y * s.main_width + x];
                 else code[j] = s.out_of_bounds_object;
             }
         }
@@ -306,7 +489,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         for (int j = 0; j < CROWS; j++) {
             if (j < nrows) {
                 int t = code[j];
-                int c = (ncx == 0 || t == INVALID_OBJ) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
+                int c = (ncx0 == 0 || t == INVALID_OBJ) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
                 if (c <= -2) err = true;
                 colb[j * 64 + lane] = c >= 0 ? c + scol0 : -1;
             }
@@ -323,9 +506,9 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         // tile rows (7 bits each), their colb rows (5 bits each), tile-row count (2 bits);
         // and the background source row offset (-1: outside the background blit)
         const int prow = lane;
-        const int rinfo = ncy == 0 ? 0
-                        : (srow0 | ((ncy > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
-                           ((ncy > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy << 24));
+        const int rinfo = ncy0 == 0 ? 0
+                        : (srow0 | ((ncy0 > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
+                           ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));
         const int bgrow = (bg_ok && prow >= by.t1 && prow < by.t1 + by.n)
                               ? (int)(((by.base + (uint32_t)((prow - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
                               : -1;
@@ -345,8 +528,8 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
 #pragma unroll
             for (int k = 0; k < RB; k++) { // branch-free: an out-of-blit pixel loads pixels[0] and discards it
                 const bool inb = bg_col && bgr[k] >= 0;
-                uint32_t v = d.pixels[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
-                bgv[k] = inb ? v : 0xff000000u;
+                uint32_t px = d.pixels[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
+                bgv[k] = inb ? px : 0xff000000u;
             }
 #pragma unroll
             for (int k = 0; k < RB; k++) {
@@ -369,15 +552,15 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
         // ---- second tile column of the few screen columns two tiles overlap (RENDER_EPS):
         //      drawn after the first column's tiles, which is the reference's x-major order.
         //      Lane = screen row here, so the row tables are lane-local.
-        unsigned long long m2 = ballot(ncx > 1);
+        unsigned long long m2 = ballot(ncx0 > 1);
         while (m2) {
             const int c = __ffsll((long long)m2) - 1;
             m2 &= m2 - 1;
             const int x1 = readlane(cx1, c), sc1 = readlane(scol1, c);
             const int row = lane;
-            if (ncy > 0) {
+            if (ncy0 > 0) {
                 uint32_t px = fb[row * PG_RES + c];
-                for (int l = 0; l < ncy; l++) {
+                for (int l = 0; l < ncy0; l++) {
                     const int code = lookup_grid(x1, l ? ry1 : ry0);
                     if (code <= -2) err = true;
                     if (code >= 0) {
@@ -389,45 +572,72 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
             }
         }
     } else {
-        // ---- generic pixel-centric pass (uncentred / very large views): a pixel blends every
-        //      tile covering it (<= 2 columns x 2 rows) in the reference's x-major order.
-        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
-            uint32_t bgv[RB], tex[RB][4];
-            uint32_t valid = 0;
-#pragma unroll
-            for (int k = 0; k < RB; k++) {
-                const int row = r0 + k;
+        // ---- generic pixel-centric pass (uncentred / large views, two tile sizes): a pixel
+        //      blends every tile covering it in the reference's x-major / y-minor order.  The
+        //      candidate columns (this lane) and rows (lane = row, broadcast) of both size
+        //      classes are merged; a tile applies when its own class covers the pixel.
+        int xs[4], nxs = 0;
+        for (int k = 0; k < ncls; k++)
+            for (int q = 0; q < ncx[k]; q++) {
+                int xv = cx[k][q];
+                bool dup = false;
+                for (int e = 0; e < nxs; e++) dup = dup || xs[e] == xv;
+                if (!dup) xs[nxs++] = xv;
+            }
+        for (int a = 1; a < nxs; a++) // ascending x
+            for (int b = a; b > 0 && xs[b - 1] > xs[b]; b--) { int t = xs[b]; xs[b] = xs[b - 1]; xs[b - 1] = t; }
+        const int rpack0 = ncy[0] | (ncy[1] << 2);
+        for (int row = 0; row < PG_RES; row++) {
+            uint32_t px;
+            {
                 const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
-                {
-                    uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-                    uint32_t v = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
-                    bgv[k] = inb ? v : 0xff000000u;
+                uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
+                uint32_t bv = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
+                px = inb ? bv : 0xff000000u;
+            }
+            if (has_grid_tiles<G>() && nxs > 0) {
+                const int rp = readlane(rpack0, row);
+                const int n0 = rp & 3, n1 = (rp >> 2) & 3;
+                int ys[2][2], ss[2][2];
+                ys[0][0] = readlane(ry[0][0], row); ys[0][1] = readlane(ry[0][1], row);
+                ss[0][0] = readlane(sr[0][0], row); ss[0][1] = readlane(sr[0][1], row);
+                ys[1][0] = readlane(ry[1][0], row); ys[1][1] = readlane(ry[1][1], row);
+                ss[1][0] = readlane(sr[1][0], row); ss[1][1] = readlane(sr[1][1], row);
+                int yl[4], nyl = 0;
+                for (int q = 0; q < n0; q++) yl[nyl++] = ys[0][q];
+                for (int q = 0; q < n1; q++) {
+                    bool dup = false;
+                    for (int e = 0; e < nyl; e++) dup = dup || yl[e] == ys[1][q];
+                    if (!dup) yl[nyl++] = ys[1][q];
                 }
-                const int nr = readlane(ncy, row);
-                const int y_a = readlane(ry0, row), y_b = readlane(ry1, row);
-                const int sr_a = readlane(srow0, row), sr_b = readlane(srow1, row);
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const int kk = c >> 1, l = c & 1;
-                    const bool cand = kk < ncx && l < nr;
-                    const int x = kk ? cx1 : cx0, y = l ? y_b : y_a;
-                    const int off = cand ? lookup_grid(x, y) : -1;
-                    if (off <= -2) err = true;
-                    const bool on = off >= 0;
-                    const int scol = kk ? scol1 : scol0, srow = l ? sr_b : sr_a;
-                    tex[k][c] = 0;
-                    if (on) tex[k][c] = d.pixels[(uint32_t)off + (uint32_t)(srow * TILE_PX + scol)];
-                    valid |= (on ? 1u : 0u) << (k * 4 + c);
+                for (int a = 1; a < nyl; a++)
+                    for (int b = a; b > 0 && yl[b - 1] > yl[b]; b--) { int t = yl[b]; yl[b] = yl[b - 1]; yl[b - 1] = t; }
+                for (int xi = 0; xi < nxs; xi++) {
+                    const int x = xs[xi];
+                    for (int yi = 0; yi < nyl; yi++) {
+                        const int y = yl[yi];
+                        int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                               : s.out_of_bounds_object;
+                        if (type == INVALID_OBJ) continue;
+                        int code = (type >= 0 && type < NTYPES) ? tile_off[type] : -2;
+                        if (code == -1) continue;
+                        if (code <= -2 && code != -4) { err = true; continue; }
+                        const int k = code == -4 ? 1 : 0;
+                        int scol = -1, srw = -1;
+                        for (int q = 0; q < ncx[k]; q++)
+                            if (cx[k][q] == x) scol = sc[k][q];
+                        const int nk = k ? n1 : n0;
+                        for (int q = 0; q < nk; q++)
+                            if (ys[k][q] == y) srw = ss[k][q];
+                        if (scol < 0 || srw < 0) continue;
+                        const uint32_t off = k ? (uint32_t)tile_off1[type] : (uint32_t)code;
+                        const int iw = k ? cls1_w : TILE_PX;
+                        const uint32_t t = d.pixels[off + (uint32_t)(srw * iw + scol)];
+                        px = t + BYTE_MUL(px, (~t) >> 24);
+                    }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < RB; k++) {
-                uint32_t px = bgv[k];
-#pragma unroll
-                for (int c = 0; c < 4; c++) // draw order: (x0,y0) (x0,y1) (x1,y0) (x1,y1)
-                    if (valid & (1u << (k * 4 + c))) px = tex[k][c] + BYTE_MUL(px, (~tex[k][c]) >> 24);
-                fb[(r0 + k) * PG_RES + lane] = px;
-            }
+            fb[row * PG_RES + lane] = px;
         }
     }
     wave_sync();
@@ -436,18 +646,20 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     // ---- entities, render_z 0 then 1, in list order (basic-abstract-game.cpp:966-967, 1061-1075)
     const int n = s.num_ents;
     const bool one_chunk = n <= 64; // blit setups computed once and reused by both z passes
-    bool draw = false;
+    bool draw = false, rot = false;
     int ez = 0;
     Axis ex, ey;
-    int soff = 0, sw = 0, ca = 256, mir = 0;
+    int soff = 0, sw = 0, sh = 0, ca = 256, mir = 0, rslot = 0;
+    double erx = 0, ery = 0, erw = 0, erh = 0;
     for (int z = 0; z <= 1; z++) {
         for (int base = 0; base < n; base += 64) {
             // lane-parallel blit setup of entity base + lane
             const int i = base + lane;
             if (!one_chunk || z == 0) {
                 draw = false;
+                rot = false;
                 ez = 0;
-                soff = 0; sw = 0; ca = 256; mir = 0;
+                soff = 0; sw = 0; sh = 0; ca = 256; mir = 0; rslot = 0;
                 if (i < n) {
                     ez = EIr(d, F_RENDER_Z, env, i);
                     float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
@@ -455,30 +667,53 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
                     int flags = EIr(d, F_FLAGS, env, i);
                     float alpha = EFr(d, F_ALPHA, env, i);
                     float rotation = EFr(d, F_ROTATION, env, i);
+                    int etype = EIr(d, F_TYPE, env, i);
                     int itype = EIr(d, F_IMAGE_TYPE, env, i);
                     int theme = EIr(d, F_IMAGE_THEME, env, i);
-                    int img = itype == PLAYER ? player_img : (itype == CR_ENEMY_BARRIER ? -1 : (itype < 0 ? -itype : itype));
-                    if (img >= 0 && (ez == 0 || ez == 1)) {
-                        if ((flags & EF_ABS_COORDS) || rotation != 0 || s.opt_use_monochrome_assets ||
-                            img >= USE_ASSET_THRESHOLD) {
-                            if (img != SPACE) err = true; // not in this build
+                    int img = image_for_type<G>(itype, player_img);
+                    if (img >= 0 && (ez == 0 || ez == 1) && should_draw<G>(s, etype, theme)) {
+                        if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+                            if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
                         } else {
-                            if (s.opt_restrict_themes) theme = 0;
+                            theme = mask_theme<G>(s, theme, img);
                             double rx, ry, rw, rh;
-                            screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
-                            if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
-                                rx = rx + rw * 0.0;
-                                ry = ry + rh * -.7415;
-                                rw = rw * 1.0;
-                                rh = rh * 1.7415;
+                            if (flags & EF_ABS_COORDS) { // get_abs_rect (:812-814) via get_object_rect (:820-826)
+                                float vd = v.view_dim;
+                                float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
+                                rx = (double)(ax * v.unit); ry = (double)(ay * v.unit);
+                                rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
+                            } else {
+                                screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+                            }
+                            if constexpr (G == PG_GAME_COINRUN) {
+                                if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
+                                    rx = rx + rw * 0.0;
+                                    ry = ry + rh * -.7415;
+                                    rw = rw * 1.0;
+                                    rh = rh * 1.7415;
+                                }
                             }
                             int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                            if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
+                            ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
+                            mir = (flags & EF_REFLECTED) != 0;
+                            soff = sp.x;
+                            sw = sp.y;
+                            sh = sp.z;
+                            if (sp.y <= 0) {
+                                err = true;
+                            } else if (rotation != 0) {
+                                // rotated: the Qt transform blit runs in order when this entity is stamped
+                                rslot = -1;
+                                for (int k = 0; k < PG_ROT_N; k++)
+                                    if (__float_as_uint(d.rot_angles[k]) == __float_as_uint(rotation)) rslot = k;
+                                if (rslot < 0) err = true;
+                                else {
+                                    draw = true;
+                                    rot = true;
+                                    erx = rx; ery = ry; erw = rw; erh = rh;
+                                }
+                            } else if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
                                 draw = true;
-                                soff = sp.x;
-                                sw = sp.y;
-                                ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
-                                mir = (flags & EF_REFLECTED) != 0;
                             }
                         }
                     }
@@ -487,8 +722,9 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
             // Stamp in list order, EG entities per group: the texel of this lane's footprint
             // pixel is loaded for every entity of the group first (loads are order-free), then
             // the group is blended into the framebuffer strictly in order.  Footprints wider
-            // than one wave (> 64 px) fall back to an in-order loop with inline loads.
-            const float inv_l = 1.0f / (float)(draw ? ex.n : 1);
+            // than one wave (> 64 px) fall back to an in-order loop with inline loads; rotated
+            // entities run the transform blit at their place in the order.
+            const float inv_l = 1.0f / (float)(draw && !rot ? ex.n : 1);
             unsigned long long m = ballot(draw && ez == z);
             while (m) {
                 int js[EG];
@@ -506,7 +742,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
                     tv[g] = 0;
                     fo[g] = 0;
                     const int j = js[g];
-                    if (j < 0) continue;
+                    if (j < 0 || readlane(rot ? 1 : 0, j)) continue;
                     const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
                     if (nx * ny > 64) continue;
                     const int p = lane;
@@ -529,8 +765,22 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
                 for (int g = 0; g < EG; g++) {
                     const int j = js[g];
                     if (j < 0) continue;
-                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
                     const int caj = readlane(ca, j);
+                    if (readlane(rot ? 1 : 0, j)) {
+                        const int k = readlane(rslot, j);
+                        const double *mt = d.rot_table + 4 * k;
+                        auto rld = [&](double x) {
+                            long long b = __builtin_bit_cast(long long, x);
+                            int lo = readlane((int)(b & 0xffffffff), j), hi = readlane((int)(b >> 32), j);
+                            return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+                        };
+                        if (!rotated_blit(fb, d.pixels, rld(erx), rld(ery), rld(erw), rld(erh), mt[0], mt[1], mt[2], mt[3],
+                                          (uint32_t)readlane(soff, j), readlane(sw, j), readlane(sh, j),
+                                          readlane(mir, j) != 0, caj))
+                            err = true;
+                        continue;
+                    }
+                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
                     if (nx * ny <= 64) {
                         if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
                     } else {
@@ -577,8 +827,20 @@ extern "C" __global__ __launch_bounds__(64) void pg_render_kernel(PGDev d) {
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 
-extern "C" void pg_launch_render(const PGDev *d, hipStream_t s) {
-    hipLaunchKernelGGL(pg_render_kernel, dim3(d->num_envs), dim3(64), 0, s, *d);
+extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s) {
+    if (count <= 0) return;
+#define PG_CASE(G)                                                                              \
+    case G:                                                                                     \
+        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list); \
+        break;
+    switch (game) {
+        PG_CASE(PG_GAME_COINRUN)
+        PG_CASE(PG_GAME_BIGFISH)
+        PG_CASE(PG_GAME_MAZE)
+        PG_CASE(PG_GAME_HEIST)
+    default: break;
+    }
+#undef PG_CASE
 }
 
 // Debug aid (PROCGEN_MI355X_POISON_LDS=1): fill the LDS of every CU with a pattern before each

@@ -1,13 +1,35 @@
 // pg_reset.hip -- Game::reset + level generation for the envs the step kernel queued
-// (reference game.cpp:109-134, basic-abstract-game.cpp:767-806, games/coinrun.cpp:227-445).
+// (reference game.cpp:109-134, basic-abstract-game.cpp:767-806; games/coinrun.cpp:227-445,
+// bigfish.cpp:62-78, maze.cpp:45-105, heist.cpp:98-203; mazegen.cpp:12-306).
 //
-// Persistent grid of 64-lane workgroups pulling env ids from the queue.  The
-// freshly seeded rand_gen lives in LDS for the whole level build (hundreds of
-// serial draws at LDS latency), the world grid is assembled in LDS with
-// lane-parallel rectangle fills and written to HBM once.
+// Persistent grid of 64-lane workgroups pulling env ids from the game's queue.  The
+// freshly seeded rand_gen lives in LDS for the whole level build (hundreds of serial draws
+// at LDS latency), the world grid is assembled in LDS with lane-parallel rectangle fills and
+// written to HBM once.  MazeGen runs in LDS too: Kruskal's order-preserving wall erase is a
+// select-the-n-th-live-bit over a wall bitmap, set union a lane-parallel relabel, and the
+// std::set BFS of expand_to_type a lane-parallel frontier over cell bytes that honours the
+// reference's ascending visiting order and early return.
 #include "pg_device.h"
 
 namespace {
+
+// LDS scratch for MazeGen (maze / heist): array_dim <= 33 (memory-mode maze, world 31)
+#define MG_MAX_DIM 33
+#define MG_MAX_CELLS (MG_MAX_DIM * MG_MAX_DIM)
+#define MG_MAX_WALLS 512
+struct MGScratch {
+    int16_t grid[MG_MAX_CELLS];        // Grid<int> array_dim x array_dim
+    int16_t labels[MG_MAX_CELLS];      // cell_sets_idxs (maze cell maze_dim*y+x)
+    int16_t free_cells[MG_MAX_CELLS];  // free_cells, in insertion order
+    int16_t list[MG_MAX_CELLS];        // forks / space cells / choose_n scratch
+    uint8_t in_free[MG_MAX_CELLS];     // free_cell_set
+    uint8_t s0[MG_MAX_CELLS], s1[MG_MAX_CELLS], curr[MG_MAX_CELLS], next[MG_MAX_CELLS];
+    uint32_t walls[MG_MAX_WALLS];      // x1 | y1 << 8 | x2 << 16 | y2 << 24, reference push order
+    unsigned long long alive[MG_MAX_WALLS / 64];
+};
+template <int G> struct Scratch { uint32_t dummy[1]; };
+template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
+template <> struct Scratch<PG_GAME_HEIST> { MGScratch mg; };
 
 struct RCtx {
     PGDev d;
@@ -64,6 +86,23 @@ DEV void choose_random_theme(RCtx &c, int i) {
     EI(c, F_IMAGE_THEME, i) = randn(c, nt);
 }
 
+// match_aspect_ratio (basic-abstract-game.cpp:1023-1033, match_width): ry = rx / aspect ratio of
+// the image loaded for the slot (mask_theme_if_necessary, :454-462; heist keeps KEY / LOCKED_DOOR
+// themes, heist.cpp:42-44)
+template <int G>
+DEV void match_aspect_ratio(RCtx &c, int i) {
+    int type = EI(c, F_IMAGE_TYPE, i), theme = EI(c, F_IMAGE_THEME, i);
+    bool preserve = G == PG_GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR);
+    if (c.s.opt_restrict_themes && !preserve) theme = 0;
+    int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + theme * MAX_ASSETS];
+    if (sp.y <= 0 || sp.z <= 0) {
+        c.s.error = PG_ERR_BAD_OPTION;
+        return;
+    }
+    float ar = (float)(sp.y * 1.0 / sp.z);
+    EF(c, F_RY, i) = EF(c, F_RX, i) / ar;
+}
+
 // grid (grid.h / basic-abstract-game.cpp:125-131, 180-185, 229-231) on the LDS copy
 DEV int get_obj(RCtx &c, int x, int y) {
     if (!(0 <= y && y < c.s.main_height && 0 <= x && x < c.s.main_width)) return c.s.out_of_bounds_object;
@@ -89,6 +128,54 @@ DEV void fill_elem(RCtx &c, int x, int y, int dx, int dy, int elem) {
     }
     if (ballot(bad)) c.s.error = PG_ERR_GRID;
     wave_sync();
+}
+
+// ------------------------------------------------------------------ BasicAbstractGame::game_reset
+template <int G>
+DEV void choose_world_dim(RCtx &c) {
+    if constexpr (G == PG_GAME_MAZE) { // maze.cpp:45-58
+        int d = c.s.opt_distribution_mode;
+        if (d == PG_EASY) c.s.world_dim = 15;
+        else if (d == PG_HARD) c.s.world_dim = 25;
+        else if (d == PG_MEMORY) c.s.world_dim = 31;
+        c.s.main_width = c.s.world_dim;
+        c.s.main_height = c.s.world_dim;
+    }
+    if constexpr (G == PG_GAME_HEIST) { // heist.cpp:98-113
+        int d = c.s.opt_distribution_mode;
+        if (d == PG_EASY) c.s.world_dim = 9;
+        else if (d == PG_HARD) c.s.world_dim = 13;
+        else if (d == PG_MEMORY) c.s.world_dim = 23;
+        c.s.maxspeed = .75f;
+        c.s.main_width = c.s.world_dim;
+        c.s.main_height = c.s.world_dim;
+    }
+}
+
+template <int G>
+DEV void base_game_reset(RCtx &c) { // basic-abstract-game.cpp:767-806
+    choose_world_dim<G>(c);
+    c.s.bg_pct_x = rand01(c);
+    if (c.s.main_width * c.s.main_height > PG_GRID_MAX || c.s.main_width <= 0 || c.s.main_height <= 0)
+        c.s.error = PG_ERR_GRID;
+    fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, 0); // grid.resize -> zeros
+    c.s.background_index = randn(c, c.d.num_backgrounds);
+    c.s.num_ents = 0;
+    c.s.agent_erased = 0;
+    float ax, ay;
+    float a_r = 0.4f;
+    if (c.s.random_agent_start) {
+        ax = rand01(c) * (c.s.main_width - 2 * a_r) + a_r;
+        ay = rand01(c) * (c.s.main_height - 2 * a_r) + a_r;
+    } else {
+        ax = a_r;
+        ay = a_r;
+    }
+    int a = add_entity(c, ax, ay, 0, 0, a_r, PLAYER);
+    EI(c, F_FLAGS, a) = EF_AUTO_ERASE | EF_SMART_STEP;
+    EI(c, F_RENDER_Z, a) = 1;
+    // erase_if_needed(): the agent spawns inside the world, nothing to erase
+    fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, SPACE);
 }
 
 // ------------------------------------------------------------------ coinrun level generation
@@ -211,30 +298,9 @@ DEV void cr_generate_coin_to_the_right(RCtx &c) { // coinrun.cpp:265-414
     fill_elem(c, curr_x + 1, 0, c.s.main_width - curr_x - 1, c.s.main_height, CR_WALL_MID);
 }
 
-DEV void coinrun_game_reset(RCtx &c) {
-    // ---- BasicAbstractGame::game_reset (basic-abstract-game.cpp:767-806)
-    c.s.bg_pct_x = rand01(c);
-    if (c.s.main_width * c.s.main_height > PG_GRID_MAX) c.s.error = PG_ERR_GRID;
-    fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, 0); // grid.resize -> zeros
-    c.s.background_index = randn(c, c.d.num_backgrounds);
-    c.s.num_ents = 0;
-    c.s.agent_erased = 0;
-    float ax, ay;
-    float a_r = 0.4f;
-    if (c.s.random_agent_start) {
-        ax = rand01(c) * (c.s.main_width - 2 * a_r) + a_r;
-        ay = rand01(c) * (c.s.main_height - 2 * a_r) + a_r;
-    } else {
-        ax = a_r;
-        ay = a_r;
-    }
-    int a = add_entity(c, ax, ay, 0, 0, a_r, PLAYER);
-    EI(c, F_FLAGS, a) = EF_AUTO_ERASE | EF_SMART_STEP;
-    EI(c, F_RENDER_Z, a) = 1;
-    // erase_if_needed(): the agent spawns inside the world, nothing to erase
-    fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, SPACE);
 
-    // ---- coinrun (coinrun.cpp:416-445)
+DEV void coinrun_game_reset(RCtx &c) { // coinrun.cpp:416-445
+    base_game_reset<PG_GAME_COINRUN>(c);
     c.s.gravity = 0.2f;
     c.s.max_jump = 1.5f;
     c.s.air_control = 0.15f;
@@ -265,7 +331,440 @@ DEV void coinrun_game_reset(RCtx &c) {
     cr_generate_coin_to_the_right(c);
 }
 
-DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool initial) {
+// ------------------------------------------------------------------ bigfish (bigfish.cpp:62-78)
+DEV void bigfish_game_reset(RCtx &c) {
+    base_game_reset<PG_GAME_BIGFISH>(c);
+    c.s.opt_center_agent = 0;
+    c.s.fish_eaten = 0;
+    float start_r = .5f;
+    if (c.s.opt_distribution_mode == PG_EASY) start_r = 1;
+    c.s.r_inc = (BF_FISH_MAX_R - start_r) / BF_FISH_QUOTA;
+    EF(c, F_RX, 0) = start_r;
+    EF(c, F_RY, 0) = start_r;
+    EF(c, F_Y, 0) = 1 + start_r;
+}
+
+// ------------------------------------------------------------------ MazeGen (mazegen.cpp)
+struct MG {
+    MGScratch *m;
+    int md, ad; // maze_dim, array_dim
+    int num_free;
+};
+
+DEV int mg_get_obj(const MG &g, int idx) { // :36-47
+    int x = idx % g.ad, y = idx / g.ad;
+    if (x <= 0 || x >= g.ad - 1) return INVALID_OBJ;
+    if (y <= 0 || y >= g.ad - 1) return INVALID_OBJ;
+    return g.m->grid[idx];
+}
+// get_neighbors (:49-67) in the reference's order: (-1,0) (0,-1) (0,1) (1,0)
+DEV int mg_first_neighbor(const MG &g, int idx, int type) {
+    const int nb[4] = {idx - 1, idx - g.ad, idx + g.ad, idx + 1};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (mg_get_obj(g, nb[k]) == type) return nb[k];
+    return -1;
+}
+DEV int mg_count_neighbors(const MG &g, int idx, int type) {
+    return (mg_get_obj(g, idx - 1) == type) + (mg_get_obj(g, idx - g.ad) == type) + (mg_get_obj(g, idx + g.ad) == type) +
+           (mg_get_obj(g, idx + 1) == type);
+}
+DEV int mg_nth_neighbor(const MG &g, int idx, int type, int n) {
+    const int nb[4] = {idx - 1, idx - g.ad, idx + g.ad, idx + 1};
+    for (int k = 0; k < 4; k++)
+        if (mg_get_obj(g, nb[k]) == type && n-- == 0) return nb[k];
+    return -1;
+}
+DEV void mg_set_index(const MG &g, int idx, int v) {
+    if (LANE == 0) g.m->grid[idx] = (int16_t)v;
+    wave_sync();
+}
+
+DEV void mg_set_free_cell(MG &g, int x, int y) { // :26-34 (uniform; lane 0 writes)
+    int cell = g.md * y + x;
+    bool was = g.m->in_free[cell] != 0;
+    wave_sync();
+    if (LANE == 0) {
+        g.m->grid[(y + 1) * g.ad + (x + 1)] = SPACE;
+        if (!was) {
+            g.m->free_cells[g.num_free] = (int16_t)cell;
+            g.m->in_free[cell] = 1;
+        }
+    }
+    if (!was) g.num_free += 1;
+    wave_sync();
+}
+
+// index of the n-th (0-based) set bit of the `words`-word bitmap `alive` (uniform)
+DEV int nth_alive(const unsigned long long *alive, int words, int n) {
+    for (int w = 0; w < words; w++) {
+        unsigned long long a = alive[w];
+        int cnt = __popcll(a);
+        if (n < cnt) {
+            bool mine = ((a >> LANE) & 1ull) && __popcll(a & ((1ull << LANE) - 1ull)) == n;
+            return w * 64 + (__ffsll((long long)ballot(mine)) - 1);
+        }
+        n -= cnt;
+    }
+    return -1;
+}
+
+DEV void mg_generate_maze(RCtx &c, MG &g) { // :112-188
+    const int md = g.md, ad = g.ad;
+    MGScratch *m = g.m;
+    for (int i = LANE; i < ad * ad; i += 64) m->grid[i] = WALL_OBJ;
+    for (int i = LANE; i < md * md; i += 64) {
+        m->labels[i] = (int16_t)i;
+        m->in_free[i] = 0;
+    }
+    wave_sync();
+    if (LANE == 0) m->grid[1 * ad + 1] = 0; // grid.set(MAZE_OFFSET, MAZE_OFFSET, 0)
+    g.num_free = 0;
+    // wall list in push order (md odd): first i odd (x), j even (y); then i even, j odd
+    const int A = (md - 1) / 2, B = (md + 1) / 2;
+    const int nw1 = A * B, nw = 2 * A * B;
+    if ((md & 1) == 0 || nw > MG_MAX_WALLS) c.s.error = PG_ERR_GRID;
+    for (int k = LANE; k < nw; k += 64) {
+        int x1, y1, x2, y2;
+        if (k < nw1) {
+            int i = 2 * (k / B) + 1, j = 2 * (k % B);
+            x1 = i - 1; y1 = j; x2 = i + 1; y2 = j;
+        } else {
+            int q = k - nw1;
+            int i = 2 * (q / A), j = 2 * (q % A) + 1;
+            x1 = i; y1 = j - 1; x2 = i; y2 = j + 1;
+        }
+        m->walls[k] = (uint32_t)x1 | ((uint32_t)y1 << 8) | ((uint32_t)x2 << 16) | ((uint32_t)y2 << 24);
+    }
+    const int words = (nw + 63) / 64;
+    for (int w = LANE; w < words; w += 64) {
+        int left = nw - w * 64;
+        m->alive[w] = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+    }
+    wave_sync();
+    for (int rem = nw; rem > 0; rem--) {
+        int n = randn(c, rem);
+        int k = nth_alive(m->alive, words, n);
+        uint32_t wv = m->walls[k];
+        int x1 = wv & 255, y1 = (wv >> 8) & 255, x2 = (wv >> 16) & 255, y2 = wv >> 24;
+        int s0_idx = m->labels[md * y1 + x1];
+        int s1_idx = m->labels[md * y2 + x2];
+        int x0 = (x1 + x2) / 2, y0 = (y1 + y2) / 2;
+        int center = md * y0 + x0;
+        bool can_remove = (m->grid[(y0 + 1) * ad + (x0 + 1)] == WALL_OBJ) && (s0_idx != s1_idx);
+        wave_sync();
+        if (LANE == 0) m->alive[k >> 6] &= ~(1ull << (k & 63)); // walls.erase(walls.begin() + n)
+        if (can_remove) {
+            mg_set_free_cell(g, x1, y1);
+            mg_set_free_cell(g, x0, y0);
+            mg_set_free_cell(g, x2, y2);
+            // s1 |= s0 | {center}; every member relabelled s1_idx
+            for (int i = LANE; i < md * md; i += 64)
+                if (m->labels[i] == s0_idx) m->labels[i] = (int16_t)s1_idx;
+            wave_sync();
+            if (LANE == 0) m->labels[center] = (int16_t)s1_idx;
+        }
+        wave_sync();
+    }
+}
+
+DEV void mg_place_objects(RCtx &c, MG &g, int start_obj, int num_objs) { // :292-306
+    for (int j = 0; j < num_objs; j++) {
+        int mm = randn(c, g.num_free);
+        while (g.m->free_cells[mm] == -1 || g.m->free_cells[mm] == 0) mm = randn(c, g.num_free);
+        int coin_cell = g.m->free_cells[mm];
+        wave_sync();
+        if (LANE == 0) {
+            g.m->free_cells[mm] = -1;
+            g.m->grid[(coin_cell / g.md + 1) * g.ad + (coin_cell % g.md + 1)] = (int16_t)(start_obj + j);
+        }
+        wave_sync();
+    }
+}
+
+// Compact the ascending indices i < n with pred(i) into g.m->list; returns the count.
+template <typename P>
+DEV int mg_compact(const MG &g, int n, P pred) {
+    int cnt = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        bool in = i < n && pred(i);
+        unsigned long long b = ballot(in);
+        if (in) g.m->list[cnt + __popcll(b & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        cnt += __popcll(b);
+    }
+    wave_sync();
+    return cnt;
+}
+
+// expand_to_type (:69-98).  The reference walks `curr` (a std::set) in ascending order, adds
+// every unseen SPACE neighbour to next/s1, and returns the first `type` neighbour of the first
+// element that has one -- after that element's own additions.  So one BFS layer = (1) the
+// smallest curr element e* with a `type` neighbour, (2) s1/next |= unseen SPACE neighbours of
+// curr elements <= e*, computed per cell.  Every curr / s1 element is an interior cell.
+DEV int mg_expand_to_type(MG &g, int type) {
+    MGScratch *m = g.m;
+    const int cells = g.ad * g.ad;
+    for (int i = LANE; i < cells; i += 64) m->curr[i] = m->s0[i];
+    wave_sync();
+    bool any = true;
+    while (any) {
+        int estar = 0x7fffffff;
+        for (int base = 0; base < cells; base += 64) {
+            int i = base + LANE;
+            bool has = i < cells && m->curr[i] && mg_first_neighbor(g, i, type) >= 0;
+            unsigned long long b = ballot(has);
+            if (b) {
+                estar = base + __ffsll((long long)b) - 1;
+                break;
+            }
+        }
+        bool nonempty = false;
+        for (int base = 0; base < cells; base += 64) {
+            int j = base + LANE;
+            bool add = false;
+            if (j < cells) {
+                m->next[j] = 0;
+                if (mg_get_obj(g, j) == SPACE && !m->s0[j] && !m->s1[j]) {
+                    const int nb[4] = {j - 1, j - g.ad, j + g.ad, j + 1};
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        int e = nb[k];
+                        if (e >= 0 && e < cells && e <= estar && m->curr[e]) add = true;
+                    }
+                }
+                if (add) {
+                    m->next[j] = 1;
+                    m->s1[j] = 1;
+                }
+            }
+            nonempty = nonempty || ballot(add) != 0;
+        }
+        wave_sync();
+        if (estar != 0x7fffffff) return mg_first_neighbor(g, estar, type);
+        for (int i = LANE; i < cells; i += 64) m->curr[i] = m->next[i];
+        wave_sync();
+        any = nonempty;
+    }
+    return -1;
+}
+
+DEV void mg_generate_maze_with_doors(RCtx &c, MG &g, int num_doors) { // :213-290
+    mg_generate_maze(c, g);
+    MGScratch *m = g.m;
+    const int cells = g.ad * g.ad;
+    int nf = mg_compact(g, cells, [&](int i) { return mg_get_obj(g, i) == SPACE && mg_count_neighbors(g, i, SPACE) > 2; });
+    // choose_n (randgen.cpp:49-68): order-preserving erase from the fork list = n-th live bit
+    int chosen[4];
+    int nc = 0;
+    if (num_doors > nf) {
+        for (int i = 0; i < nf && i < 4; i++) chosen[nc++] = m->list[i];
+        if (nf > 4) c.s.error = PG_ERR_GRID;
+    } else {
+        const int words = (nf + 63) / 64;
+        for (int w = LANE; w < words; w += 64) {
+            int left = nf - w * 64;
+            m->alive[w] = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+        }
+        wave_sync();
+        for (int rem = nf; nc < num_doors; rem--) {
+            int k = nth_alive(m->alive, words, randn(c, rem));
+            chosen[nc++] = m->list[k];
+            wave_sync();
+            if (LANE == 0) m->alive[k >> 6] &= ~(1ull << (k & 63));
+            wave_sync();
+        }
+    }
+    num_doors = nc;
+    for (int i = 0; i < nc; i++) mg_set_index(g, chosen[i], DOOR_OBJ);
+    int ns = mg_compact(g, cells, [&](int i) { return mg_get_obj(g, i) == SPACE; });
+    int agent_cell;
+    do {
+        if (ns <= 0) {
+            c.s.error = PG_ERR_GRID;
+            return;
+        }
+        agent_cell = m->list[randn(c, ns)];
+    } while (mg_first_neighbor(g, agent_cell, DOOR_OBJ) >= 0);
+    mg_set_index(g, agent_cell, AGENT_OBJ);
+    for (int i = LANE; i < cells; i += 64) m->s0[i] = i == agent_cell;
+    wave_sync();
+    for (int door_num = 0; door_num < num_doors + 1; door_num++) {
+        for (int i = LANE; i < cells; i += 64) m->s1[i] = 0;
+        wave_sync();
+        int found_door = -1;
+        if (door_num < num_doors) {
+            found_door = mg_expand_to_type(g, DOOR_OBJ);
+            if (found_door < 0) {
+                c.s.error = PG_ERR_GRID;
+                return;
+            }
+            mg_set_index(g, found_door, DOOR_OBJ + door_num + 1);
+            for (int i = LANE; i < cells; i += 64) m->s0[i] |= m->s1[i];
+            wave_sync();
+        }
+        mg_expand_to_type(g, -999);
+        int nsp = mg_compact(g, cells, [&](int i) { return m->s1[i] != 0; });
+        if (nsp <= 0) {
+            c.s.error = PG_ERR_GRID;
+            return;
+        }
+        int key_cell = m->list[randn(c, nsp)];
+        mg_set_index(g, key_cell, door_num == num_doors ? EXIT_OBJ : (KEY_OBJ + door_num + 1));
+        for (int i = LANE; i < cells; i += 64) m->s0[i] |= m->s1[i];
+        wave_sync();
+        if (found_door >= 0) {
+            if (LANE == 0) m->s0[found_door] = 1;
+            wave_sync();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ maze (maze.cpp:60-105)
+DEV void maze_game_reset(RCtx &c, MGScratch *scratch) {
+    base_game_reset<PG_GAME_MAZE>(c);
+    c.s.grid_step = 1;
+    c.s.maze_dim = randn(c, (c.s.world_dim - 1) / 2) * 2 + 3;
+    int margin = (c.s.world_dim - c.s.maze_dim) / 2;
+    MG g;
+    g.m = scratch;
+    g.md = c.s.maze_dim;
+    g.ad = g.md + 2;
+    if (g.ad > MG_MAX_DIM) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    c.s.opt_center_agent = c.s.opt_distribution_mode == PG_MEMORY;
+    EF(c, F_RX, 0) = .5f;
+    EF(c, F_RY, 0) = .5f;
+    EF(c, F_X, 0) = (float)(margin + .5);
+    EF(c, F_Y, 0) = (float)(margin + .5);
+    mg_generate_maze(c, g);
+    mg_place_objects(c, g, MZ_GOAL, 1);
+    const int w = c.s.main_width;
+    for (int i = LANE; i < w * c.s.main_height; i += 64) c.grid[i] = WALL_OBJ;
+    wave_sync();
+    for (int k = LANE; k < g.md * g.md; k += 64) { // set_obj(margin + i, margin + j, maze grid (i + 1, j + 1))
+        int i = k / g.md, j = k % g.md;
+        c.grid[(margin + j) * w + margin + i] = scratch->grid[(j + 1) * g.ad + (i + 1)];
+    }
+    wave_sync();
+    if (margin > 0) { // border walls (all WALL_OBJ already; kept for the bounds check of set_obj)
+        if (margin - 1 < 0 || margin + g.md >= w) c.s.error = PG_ERR_GRID;
+    }
+}
+
+// ------------------------------------------------------------------ heist (heist.cpp:115-203)
+DEV float rand_pos(RCtx &c, float r, float min, float max) { // basic-abstract-game.cpp:1109-1117
+    if (max - min <= 2 * r) return (max + min) / 2;
+    float range = max - min;
+    return (range - 2 * r) * rand01(c) + r + min;
+}
+
+// has_agent_collision(e) || has_any_collision(e) for a not-yet-added entity (reposition, :548-569)
+DEV bool spawn_collides(RCtx &c, float x, float y, float rx, float ry) {
+    bool hit = false;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        int i = base + LANE;
+        if (i < c.s.num_ents && !(EI(c, F_FLAGS, i) & EF_AVOIDS)) {
+            float tx = (rx + EF(c, F_RX, i)) + 0.0f, ty = (ry + EF(c, F_RY, i)) + 0.0f;
+            if ((fabsf(x - EF(c, F_X, i)) < tx) && (fabsf(y - EF(c, F_Y, i)) < ty)) hit = true;
+        }
+    }
+    // the agent is entities[0]: has_agent_collision adds nothing beyond has_any_collision
+    return ballot(hit) != 0;
+}
+
+// spawn_entity(r, type, x, y, w, h) (:520-527, 571-573): Entity(0, 0, 0, 0, r, r, type), reposition, push_back
+DEV int spawn_entity(RCtx &c, float r, int type, float x, float y, float w, float h) {
+    float ex = rand_pos(c, r, x, x + w);
+    float ey = rand_pos(c, r, y, y + h);
+    int count = 0;
+    while (spawn_collides(c, ex, ey, r, r) && count < 100) {
+        ex = rand_pos(c, r, x, x + w);
+        ey = rand_pos(c, r, y, y + h);
+        count++;
+    }
+    return add_entity(c, ex, ey, 0, 0, r, type);
+}
+
+DEV void heist_game_reset(RCtx &c, MGScratch *scratch) {
+    base_game_reset<PG_GAME_HEIST>(c);
+    int min_maze_dim = 5;
+    int max_diff = (c.s.world_dim - min_maze_dim) / 2;
+    int difficulty = randn(c, max_diff + 1);
+    c.s.opt_center_agent = c.s.opt_distribution_mode == PG_MEMORY;
+    if (c.s.opt_distribution_mode == PG_MEMORY) c.s.num_keys = randn(c, 4);
+    else c.s.num_keys = difficulty + randn(c, 2);
+    if (c.s.num_keys > 3) c.s.num_keys = 3;
+    c.s.has_keys = 0;
+    int maze_dim = difficulty * 2 + min_maze_dim;
+    float maze_scale = (float)(c.s.main_height / (c.s.world_dim * 1.0));
+    EF(c, F_RX, 0) = (float)(.375 * maze_scale);
+    EF(c, F_RY, 0) = (float)(.375 * maze_scale);
+    float r_ent = maze_scale / 2;
+    MG g;
+    g.m = scratch;
+    g.md = maze_dim;
+    g.ad = maze_dim + 2;
+    if (g.ad > MG_MAX_DIM) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    mg_generate_maze_with_doors(c, g, c.s.num_keys);
+    EF(c, F_X, 0) = -1; // move agent out of the way for maze generation
+    EF(c, F_Y, 0) = -1;
+    int off_x = randn(c, c.s.world_dim - maze_dim + 1);
+    int off_y = randn(c, c.s.world_dim - maze_dim + 1);
+    const int w = c.s.main_width;
+    for (int i = LANE; i < w * c.s.main_height; i += 64) c.grid[i] = WALL_OBJ;
+    wave_sync();
+    // the grid writes are order-free; the entity spawns follow the reference's x-major loop
+    for (int k = LANE; k < maze_dim * maze_dim; k += 64) {
+        int i = k / maze_dim, j = k % maze_dim;
+        int obj = scratch->grid[(j + 1) * g.ad + (i + 1)];
+        int x = off_x + i, y = off_y + j;
+        if (obj != WALL_OBJ && 0 <= x && x < w && 0 <= y && y < c.s.main_height) c.grid[y * w + x] = SPACE;
+    }
+    wave_sync();
+    for (int k = 0; k < maze_dim * maze_dim; k++) {
+        int i = k / maze_dim, j = k % maze_dim;
+        int obj = scratch->grid[(j + 1) * g.ad + (i + 1)];
+        if (obj == WALL_OBJ || obj == SPACE) continue;
+        int x = off_x + i, y = off_y + j;
+        float obj_x = (float)((x + .5) * maze_scale);
+        float obj_y = (float)((y + .5) * maze_scale);
+        if (obj >= KEY_OBJ) {
+            int e = spawn_entity(c, (float)(.375 * maze_scale), HS_KEY, maze_scale * x, maze_scale * y, maze_scale, maze_scale);
+            EI(c, F_IMAGE_THEME, e) = obj - KEY_OBJ - 1;
+            match_aspect_ratio<PG_GAME_HEIST>(c, e);
+        } else if (obj >= DOOR_OBJ) {
+            int e = add_entity(c, obj_x, obj_y, 0, 0, r_ent, HS_LOCKED_DOOR);
+            EI(c, F_IMAGE_THEME, e) = obj - DOOR_OBJ - 1;
+        } else if (obj == EXIT_OBJ) {
+            int e = spawn_entity(c, (float)(.375 * maze_scale), HS_EXIT, maze_scale * x, maze_scale * y, maze_scale, maze_scale);
+            match_aspect_ratio<PG_GAME_HEIST>(c, e);
+        } else if (obj == AGENT_OBJ) {
+            EF(c, F_X, 0) = obj_x;
+            EF(c, F_Y, 0) = obj_y;
+        }
+    }
+    float ring_key_r = 0.03f;
+    for (int i = 0; i < c.s.num_keys; i++) {
+        int e = add_entity(c, (float)(1 - ring_key_r * (2 * i + 1.25)), (float)(ring_key_r * .75), 0, 0, ring_key_r,
+                           HS_KEY_ON_RING);
+        EI(c, F_IMAGE_THEME, e) = i;
+        EI(c, F_IMAGE_TYPE, e) = HS_KEY;
+        EF(c, F_ROTATION, e) = PI_F / 2;
+        EI(c, F_RENDER_Z, e) = 1;
+        EI(c, F_FLAGS, e) = EI(c, F_FLAGS, e) | EF_ABS_COORDS;
+        match_aspect_ratio<PG_GAME_HEIST>(c, e);
+    }
+}
+
+// ------------------------------------------------------------------ Game::reset
+template <int G>
+DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial) {
     RCtx c;
     c.d = d;
     c.env = env;
@@ -296,7 +795,10 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool 
     wave_sync();
     mt_seed_lds(lds_mt, (uint32_t)c.s.current_level_seed);
     c.mti = PG_MT_N;
-    coinrun_game_reset(c);
+    if constexpr (G == PG_GAME_COINRUN) coinrun_game_reset(c);
+    if constexpr (G == PG_GAME_BIGFISH) bigfish_game_reset(c);
+    if constexpr (G == PG_GAME_MAZE) maze_game_reset(c, &scratch->mg);
+    if constexpr (G == PG_GAME_HEIST) heist_game_reset(c, &scratch->mg);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -307,11 +809,12 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool 
     wave_sync();
     for (int i = LANE; i < PG_MT_N; i += 64) rg[i] = lds_mt[i];
     int cells = c.s.main_width * c.s.main_height;
+    if (cells > PG_GRID_MAX) cells = PG_GRID_MAX;
     int16_t *g = d.grid + (size_t)env * PG_GRID_MAX;
     const uint4 *src = reinterpret_cast<const uint4 *>(lds_grid);
     uint4 *dst = reinterpret_cast<uint4 *>(g);
     for (int i = LANE; i < (cells + 7) / 8; i += 64) dst[i] = src[i];
-    // int8 mirror for the step kernel (valid when every cell fits, always for coinrun)
+    // int8 mirror for the step kernel (valid when every cell fits)
     bool fits = true;
     int8_t *g8 = d.grid8 + (size_t)env * PG_GRID_MAX;
     for (int i = LANE; i < (cells + 15) / 16; i += 64) {
@@ -331,6 +834,20 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool 
         reinterpret_cast<uint4 *>(g8)[i] = make_uint4(w[0], w[1], w[2], w[3]);
     }
     c.s.grid8_ok = ballot(!fits) == 0;
+    if constexpr (G == PG_GAME_MAZE) {
+        // fork latent state (maze.cpp:134-165): grid_size, grid (zero padded), agent_pos; the
+        // step kernel keeps agent_pos and consumed goal cells current
+        int32_t *lat = d.latent + (size_t)env * PG_LATENT_N;
+        for (int i = LANE; i < PG_LATENT_GRID; i += 64) lat[2 + i] = i < cells ? (int32_t)lds_grid[i] : 0;
+        if (LANE == 0) {
+            lat[0] = c.s.main_width;
+            lat[1] = c.s.main_height;
+            lat[2 + PG_LATENT_GRID] = (int)EF(c, F_X, 0);
+            lat[3 + PG_LATENT_GRID] = (int)EF(c, F_Y, 0);
+            lat[4 + PG_LATENT_GRID] = 0;
+            lat[5 + PG_LATENT_GRID] = 0;
+        }
+    }
     if (LANE == 0) {
         d.level_seed[env] = c.s.current_level_seed;
         if (initial) { // first observation of set_buffers (vecgame.cpp:381-409): step_data from the ctor
@@ -345,20 +862,38 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, bool 
     wave_sync();
 }
 
-} // namespace
-
-// all_envs != 0: reset every env (initial reset of set_buffers); else drain the step kernel's queue.
-extern "C" __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, int all_envs) {
+// all_envs != 0: reset every env in env_list / 0..count-1 (initial reset of set_buffers);
+// else drain this game's queue filled by the step kernel.
+template <int G>
+__global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int all_envs) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ __attribute__((aligned(16))) int16_t lds_grid[PG_GRID_MAX];
-    int count = all_envs ? d.num_envs : *d.reset_count;
-    for (int q = blockIdx.x; q < count; q += gridDim.x) {
-        int env = all_envs ? q : d.reset_queue[q];
-        reset_env(d, env, lds_mt, lds_grid, all_envs != 0);
+    __shared__ Scratch<G> scratch;
+    int n = all_envs ? count : d.reset_count[G];
+    const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
+    PGDev dv = game_view(d, G);
+    for (int q = blockIdx.x; q < n; q += gridDim.x) {
+        int env = all_envs ? (env_list ? env_list[q] : q) : queue[q];
+        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0);
     }
 }
 
-extern "C" void pg_launch_reset(const PGDev *d, hipStream_t s, int all_envs, int grid) {
-    int g = grid > 0 ? grid : (d->num_envs < 4096 ? d->num_envs : 4096);
-    hipLaunchKernelGGL(pg_reset_kernel, dim3(g), dim3(64), 0, s, *d, all_envs);
+} // namespace
+
+extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
+                                int all_envs, int grid) {
+    if (count <= 0) return;
+    int g = grid > 0 ? grid : (count < 4096 ? count : 4096);
+#define PG_CASE(G)                                                                                      \
+    case G:                                                                                             \
+        hipLaunchKernelGGL(pg_reset_kernel<G>, dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
+        break;
+    switch (game) {
+        PG_CASE(PG_GAME_COINRUN)
+        PG_CASE(PG_GAME_BIGFISH)
+        PG_CASE(PG_GAME_MAZE)
+        PG_CASE(PG_GAME_HEIST)
+    default: break;
+    }
+#undef PG_CASE
 }

@@ -1,7 +1,9 @@
-// pg_step.hip -- per-env step kernel: Game::step + BasicAbstractGame::game_step + coinrun
-// game_step (reference game.cpp:136-171, basic-abstract-game.cpp:602-765, 1095-1159,
-// games/coinrun.cpp:123-211, 451-498).  One wavefront per env; done envs are queued for
-// pg_reset (level generation) and every env is then drawn by pg_render.
+// pg_step.hip -- per-env step kernel: Game::step + BasicAbstractGame::game_step + the per-game
+// game_step (reference game.cpp:136-171, basic-abstract-game.cpp:602-765, 1095-1159;
+// games/coinrun.cpp:123-211, 451-498; bigfish.cpp:45-106; maze.cpp:107-131; heist.cpp:66-96,
+// 205-209).  One wavefront per env; done envs are queued for pg_reset (level generation)
+// and every env is then drawn by pg_render.  The kernel is a template over the game id:
+// the physics core is shared, the reference's virtual hooks are `if constexpr` branches.
 #include "pg_device.h"
 
 namespace {
@@ -24,6 +26,7 @@ struct Ctx {
     int i_idx;
     float i_x, i_y, i_rx, i_ry;
     bool i_erase;
+    int i_theme;
     PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
 };
 
@@ -167,29 +170,40 @@ DEV int get_obj_from_floats(Ctx &c, float i, float j) {
     return get_obj(c, (int)floorf(i), (int)floorf(j));
 }
 
-// ------------------------------------------------------------------ per-game hooks (coinrun)
+// ------------------------------------------------------------------ per-game hooks
+template <int G>
 DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coinrun.cpp:204-211
     if (target == WALL_OBJ) return true;
     if (target == c.s.out_of_bounds_object) return true;
-    if (src_type == PLAYER && cr_is_wall(target)) return true;
+    if constexpr (G == PG_GAME_COINRUN)
+        if (src_type == PLAYER && cr_is_wall(target)) return true;
     return false;
 }
-DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142
-    return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+template <int G>
+DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-509 false
+    if constexpr (G == PG_GAME_COINRUN) return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    return false;
 }
 
 struct AgentView { float x, y, vx, vy, rx, ry; };
 
-// coinrun.cpp:187-202 ; `agent` is the current agent state (registers if it is the stepped object)
-DEV bool is_blocked_ents(Ctx &c, int src_type, int t_type, float t_y, float t_ry, bool is_h, const AgentView &agent) {
-    if (t_type == CR_CRATE && !is_h) {
-        if (agent.vy >= 0) return false;
-        if (c.s.action_vy < 0) return false;
-        if (c.s.last_agent_y < (t_y + t_ry + agent.ry)) return false;
-        c.s.is_on_crate = 1;
-        return true;
+// is_blocked_ents (basic :503-505; coinrun.cpp:187-202; heist.cpp:66-71).  `agent` is the
+// current agent state (registers if it is the stepped object).
+template <int G>
+DEV bool is_blocked_ents(Ctx &c, int src_type, int m, int t_type, bool is_h, const AgentView &agent) {
+    if constexpr (G == PG_GAME_COINRUN) {
+        if (t_type == CR_CRATE && !is_h) {
+            if (agent.vy >= 0) return false;
+            if (c.s.action_vy < 0) return false;
+            if (c.s.last_agent_y < (EF(c, F_Y, m) + EF(c, F_RY, m) + agent.ry)) return false;
+            c.s.is_on_crate = 1;
+            return true;
+        }
     }
-    return is_blocked(c, src_type, t_type);
+    if constexpr (G == PG_GAME_HEIST) {
+        if (t_type == HS_LOCKED_DOOR) return !((c.s.has_keys >> EI(c, F_IMAGE_THEME, m)) & 1);
+    }
+    return is_blocked<G>(c, src_type, t_type);
 }
 
 DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
@@ -205,14 +219,26 @@ DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
 
 // ------------------------------------------------------------------ collision scan
 // The body of sub_step's entity loop (basic-abstract-game.cpp:345-377) has an effect only
-// when is_blocked_ents() or will_reflect() fires.  For coinrun those reduce to: target is
-// a CRATE and the move is vertical (coinrun.cpp:187-211; base is_blocked needs WALL_OBJ /
-// out_of_bounds_object / a wall type, will_reflect needs a wall or ENEMY_BARRIER type --
-// no coinrun entity has such a type).  Every other (obj, m) pair is a no-op, so the scan
-// visits only the "interactors" (crates), collected once per step into LDS; entity indices
-// do not change during step_entities (no insertion or erase there).
-DEV bool scan_needed(bool is_h) { return !is_h; }
-DEV bool is_interactor(int type) { return type == CR_CRATE; }
+// when is_blocked_ents() or will_reflect() fires.  Per game that reduces to a few entity
+// types ("interactors"): coinrun -- a CRATE on a vertical move (coinrun.cpp:187-211; base
+// is_blocked needs WALL_OBJ / out_of_bounds_object / a wall type, will_reflect a wall or
+// ENEMY_BARRIER type, and no coinrun entity has such a type); heist -- LOCKED_DOOR
+// (heist.cpp:66-71); bigfish and maze -- none (no entity type is WALL_OBJ or the
+// out-of-bounds object).  Every other (obj, m) pair is a no-op, so the scan visits only the
+// interactors, collected once per step into LDS; entity indices do not change during
+// step_entities (no insertion or erase there).
+template <int G>
+DEV bool scan_needed(bool is_h) {
+    if constexpr (G == PG_GAME_COINRUN) return !is_h;
+    if constexpr (G == PG_GAME_HEIST) return true;
+    return false;
+}
+template <int G>
+DEV bool is_interactor(int type) {
+    if constexpr (G == PG_GAME_COINRUN) return type == CR_CRATE;
+    if constexpr (G == PG_GAME_HEIST) return type == HS_LOCKED_DOOR;
+    return false;
+}
 
 // Largest interactor index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
 // i.e. the next entity the reference's reverse loop would act on; lane-parallel over the list.
@@ -246,11 +272,15 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
     return -1;
 }
 
+template <int G>
 DEV void build_interactor_list(Ctx &c) {
     int cnt = 0;
+    c.nlist = 0;
+    c.ireg = true;
+    if (!scan_needed<G>(false) && !scan_needed<G>(true)) return;
     for (int base = 0; base < c.s.num_ents; base += 64) {
         int i = base + LANE;
-        bool in = i < c.s.num_ents && is_interactor(EI(c, F_TYPE, i));
+        bool in = i < c.s.num_ents && is_interactor<G>(EI(c, F_TYPE, i));
         unsigned long long m = ballot(in);
         if (in) c.ilist[cnt + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
         cnt += __popcll(m);
@@ -269,6 +299,7 @@ DEV void build_interactor_list(Ctx &c) {
             c.i_x = EF(c, F_X, i); c.i_y = EF(c, F_Y, i); c.i_rx = EF(c, F_RX, i); c.i_ry = EF(c, F_RY, i);
             int fl = EI(c, F_FLAGS, i);
             c.i_erase = (fl & EF_WILL_ERASE) != 0;
+            c.i_theme = EI(c, F_IMAGE_THEME, i);
             stat = !(fl & EF_SMART_STEP) && EF(c, F_VX, i) == 0 && EF(c, F_VY, i) == 0 &&
                    EF(c, F_GROW_RATE, i) == 1 && EI(c, F_EXPIRE_TIME, i) <= 0;
         }
@@ -278,11 +309,11 @@ DEV void build_interactor_list(Ctx &c) {
 
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
 
-template <int D>
+template <int G, int D>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy);
 
 // basic-abstract-game.cpp:248-276 (target is always the stepped object)
-template <int D>
+template <int G, int D>
 DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
     float sx = EF(c, F_X, src), sy = EF(c, F_Y, src);
     float rsum = is_h ? (EF(c, F_RX, src) + o.rx) : (EF(c, F_RY, src) + o.ry);
@@ -291,13 +322,13 @@ DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
     float t_vx = 0, t_vy = 0;
     if (is_h) t_vx = (float)((double)sx + dsign(delx) * (double)rsum - (double)o.x);
     else t_vy = (float)((double)sy + dsign(dely) * (double)rsum - (double)o.y);
-    if constexpr (D < 5) (void)sub_step<D + 1>(c, oi, o, t_vx, t_vy);
+    if constexpr (D < 5) (void)sub_step<G, D + 1>(c, oi, o, t_vx, t_vy);
     if (is_h) o.vx = 0;
     else o.vy = 0;
 }
 
 // basic-abstract-game.cpp:278-380
-template <int D>
+template <int G, int D>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
     if (o.flags & EF_WILL_ERASE) return false;
     float ny = o.y + _vy;
@@ -310,8 +341,8 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
-            block = block || is_blocked(c, o.type, type2);
-            reflect = reflect || will_reflect(o.type, type2);
+            block = block || is_blocked<G>(c, o.type, type2);
+            reflect = reflect || will_reflect<G>(o.type, type2);
         }
     }
     if (reflect) {
@@ -341,16 +372,16 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
     o.y = ny;
     bool block2 = false;
     int upper = c.s.num_ents;
-    while (scan_needed(is_h)) {
+    while (scan_needed<G>(is_h)) {
         int m = next_collider(c, oi, upper, o);
         if (m < 0) break;
         upper = m;
         int mtype = EI(c, F_TYPE, m);
         bool curr_block = false;
         AgentView av = agent_view(c, oi, o);
-        if (is_blocked_ents(c, o.type, mtype, EF(c, F_Y, m), EF(c, F_RY, m), is_h, av)) {
+        if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, av)) {
             curr_block = true;
-        } else if (will_reflect(o.type, mtype)) {
+        } else if (will_reflect<G>(o.type, mtype)) {
             if (is_h) {
                 float delx = EF(c, F_X, m) - o.x;
                 float rsum = EF(c, F_RX, m) + o.rx;
@@ -363,13 +394,14 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 o.vy = -1 * o.vy;
             }
         }
-        if (curr_block) push_obj<D>(c, m, oi, o, is_h);
+        if (curr_block) push_obj<G, D>(c, m, oi, o, is_h);
         block2 = block2 || curr_block;
     }
     return block || block2;
 }
 
 // basic-abstract-game.cpp:602-665
+template <int G>
 DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     if (o.flags & EF_WILL_ERASE) return;
     int num_sub_steps;
@@ -390,11 +422,11 @@ DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     for (int s = 0; s < num_sub_steps; s++) {
         bool block_x, block_y;
         if (step_x_first) {
-            block_x = sub_step<0>(c, oi, o, o.vx * pct, 0);
-            block_y = sub_step<0>(c, oi, o, 0, o.vy * pct);
+            block_x = sub_step<G, 0>(c, oi, o, o.vx * pct, 0);
+            block_y = sub_step<G, 0>(c, oi, o, 0, o.vy * pct);
         } else {
-            block_y = sub_step<0>(c, oi, o, 0, o.vy * pct);
-            block_x = sub_step<0>(c, oi, o, o.vx * pct, 0);
+            block_y = sub_step<G, 0>(c, oi, o, 0, o.vy * pct);
+            block_x = sub_step<G, 0>(c, oi, o, o.vx * pct, 0);
         }
         if (!block_x) vx_pct += 1;
         if (!block_y) vy_pct += 1;
@@ -428,6 +460,7 @@ DEV void ent_readlane(const Ent &m, int l, Ent &o) {
 // the scans read only the register-cached static interactors), so every smart entity can
 // be loaded lane-parallel up front (lane k <-> k-th smart entity), stepped from registers
 // in the reference's reverse order, and stored lane-parallel at the end.
+template <int G>
 DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
     int n = c.s.num_ents;
     int nsm = 0;
@@ -453,7 +486,7 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         }
         Ent o;
         ent_readlane(mine, j, o);
-        basic_step_object(c, sm, o);
+        basic_step_object<G>(c, sm, o);
         entity_step(o);
         if (LANE == j) mine = o;
         hi = sm - 1;
@@ -467,8 +500,9 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
     return true;
 }
 
+template <int G>
 DEV void step_entities(Ctx &c, int16_t *slist) {
-    if (step_entities_fast(c, slist)) return;
+    if (step_entities_fast<G>(c, slist)) return;
     int hi = c.s.num_ents - 1;
     while (hi >= 0) {
         int sm = -1;
@@ -489,7 +523,7 @@ DEV void step_entities(Ctx &c, int16_t *slist) {
         if (sm < 0) break;
         Ent o;
         load_ent(c, sm, o);
-        basic_step_object(c, sm, o);
+        basic_step_object<G>(c, sm, o);
         entity_step(o);
         store_ent(c, sm, o);
         wave_sync();
@@ -542,21 +576,28 @@ DEV void erase_if_needed(Ctx &c) {
     c.s.num_ents = kept;
 }
 
-// ------------------------------------------------------------------ agent control (coinrun)
-DEV void set_action_xy(Ctx &c, int move_action) { // coinrun.cpp:451-472
-    c.s.action_vx = (float)(move_action / 3 - 1);
+// ------------------------------------------------------------------ agent control
+template <int G>
+DEV void set_action_xy(Ctx &c, int move_action) {
+    c.s.action_vx = (float)(move_action / 3 - 1); // basic :667-671
     c.s.action_vy = (float)((move_action % 3) - 1);
-    if (c.s.action_vx > 0) c.s.facing_right = 1;
-    if (c.s.action_vx < 0) c.s.facing_right = 0;
-    float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0), avy = EF(c, F_VY, 0);
-    int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
-    int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
-    bool s1 = cr_is_wall(b1) || b1 == c.s.out_of_bounds_object;
-    bool s2 = cr_is_wall(b2) || b2 == c.s.out_of_bounds_object;
-    c.s.has_support = (c.s.is_on_crate || s1 || s2) && avy == 0;
-    c.s.is_on_crate = 0;
-    if (c.s.action_vy == 1) {
-        if (!c.s.has_support) c.s.action_vy = 0;
+    if constexpr (G == PG_GAME_COINRUN) { // coinrun.cpp:451-472
+        if (c.s.action_vx > 0) c.s.facing_right = 1;
+        if (c.s.action_vx < 0) c.s.facing_right = 0;
+        float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0), avy = EF(c, F_VY, 0);
+        int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        bool s1 = cr_is_wall(b1) || b1 == c.s.out_of_bounds_object;
+        bool s2 = cr_is_wall(b2) || b2 == c.s.out_of_bounds_object;
+        c.s.has_support = (c.s.is_on_crate || s1 || s2) && avy == 0;
+        c.s.is_on_crate = 0;
+        if (c.s.action_vy == 1) {
+            if (!c.s.has_support) c.s.action_vy = 0;
+        }
+    } else {
+        c.s.action_vrot = 0;
+        if constexpr (G == PG_GAME_MAZE) // maze.cpp:107-111
+            if (c.s.action_vx != 0) c.s.action_vy = 0;
     }
 }
 
@@ -566,62 +607,104 @@ DEV float clip_abs(float x, float y) {
     return x;
 }
 
-DEV void update_agent_velocity(Ctx &c) { // coinrun.cpp:156-173
+template <int G>
+DEV void update_agent_velocity(Ctx &c) {
     float vx = EF(c, F_VX, 0), vy = EF(c, F_VY, 0);
-    float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
-    vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
-    if (fabsf(vx) < mixrate_x * c.s.maxspeed) vx = 0;
-    if (c.s.action_vy > 0) {
-        vy = c.s.max_jump;
-    } else {
-        if (c.s.has_support) vy = (float)((double)vy + .2 * (double)c.s.action_vy);
-    }
-    if (!(c.s.has_support && c.s.action_vy > 0)) {
-        vy -= c.s.gravity;
-        vy = clip_abs(vy, c.s.max_jump);
+    if constexpr (G == PG_GAME_COINRUN) { // coinrun.cpp:156-173
+        float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
+        vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
+        if (fabsf(vx) < mixrate_x * c.s.maxspeed) vx = 0;
+        if (c.s.action_vy > 0) {
+            vy = c.s.max_jump;
+        } else {
+            if (c.s.has_support) vy = (float)((double)vy + .2 * (double)c.s.action_vy);
+        }
+        if (!(c.s.has_support && c.s.action_vy > 0)) {
+            vy -= c.s.gravity;
+            vy = clip_abs(vy, c.s.max_jump);
+        }
+    } else { // basic-abstract-game.cpp:678-693 (get_agent_acceleration_scale() = 1)
+        const float v_scale = 1.0f;
+        vx = (1 - c.s.mixrate) * vx;
+        vy = (1 - c.s.mixrate) * vy;
+        vx += c.s.mixrate * c.s.maxspeed * c.s.action_vx * v_scale;
+        vy += c.s.mixrate * c.s.maxspeed * c.s.action_vy * v_scale;
+        vx = (float)(.9 * (double)vx); // decay_agent_velocity
+        vy = (float)(.9 * (double)vy);
     }
     EF(c, F_VX, 0) = vx;
     EF(c, F_VY, 0) = vy;
 }
 
-// ------------------------------------------------------------------ game_step
-DEV void coinrun_game_step(Ctx &c) {
-    // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
-    uint32_t *rg = c.d.mt + (size_t)c.env * 2 * PG_MT_WORDS;
-    c.s.step_rand_int = rg_randint_of(mt_next_global(rg, c.s.rg_mti, c.lds), 0, 1000000);
-    c.pt.mark(0);
-    c.s.move_action = c.s.action % 9;
-    c.s.special_action = 0;
-    if (c.s.action >= 9) {
-        c.s.special_action = c.s.action - 8;
-        c.s.move_action = 4;
+// asset_aspect_ratios of an image slot (basic-abstract-game.cpp:79-123): the image loaded for
+// the slot after mask_theme_if_necessary, width * 1.0 / height
+template <int G>
+DEV bool preserve_theme(int type) { // should_preserve_type_themes (heist.cpp:42-44)
+    if constexpr (G == PG_GAME_HEIST) return type == HS_KEY || type == HS_LOCKED_DOOR;
+    return false;
+}
+template <int G>
+DEV float aspect_ratio(Ctx &c, int type, int theme) {
+    if (c.s.opt_restrict_themes && !preserve_theme<G>(type)) theme = 0;
+    int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + theme * MAX_ASSETS];
+    if (sp.y <= 0 || sp.z <= 0) {
+        c.s.error = PG_ERR_BAD_OPTION;
+        return 1.0f;
     }
-    if (c.s.move_action != 4) c.s.last_move_action = c.s.move_action;
-    c.s.action_vrot = 0;
-    c.s.action_vx = 0;
-    c.s.action_vy = 0;
-    set_action_xy(c, c.s.move_action);
-    if (c.s.grid_step) {
-        EF(c, F_VX, 0) = c.s.action_vx;
-        EF(c, F_VY, 0) = c.s.action_vy;
-    } else {
-        update_agent_velocity(c);
-        float vrot = EF(c, F_VROT, 0);
-        vrot = MIXRATEROT * vrot;
-        vrot += MIXRATEROT * (15 * 3.14159265358979323846264338327950288f / 180) * c.s.action_vrot;
-        EF(c, F_VROT, 0) = vrot;
-    }
-    wave_sync();
-    c.pt.mark(1);
-    build_interactor_list(c);
-    step_entities(c, c.slist);
-    c.pt.mark(2);
+    return (float)(sp.y * 1.0 / sp.z);
+}
 
-    // agent / entity collisions (:728-750).  coinrun effects are order-free flags:
-    // ENEMY or SAW touching the agent ends the episode; only the agent reacts to grid cells.
-    {
+// ------------------------------------------------------------------ agent / entity collisions
+// handle_agent_collision (basic :387-389; coinrun.cpp:123-131; bigfish.cpp:45-59; heist.cpp:80-96)
+template <int G>
+DEV void handle_agent_collision(Ctx &c, int m) {
+    const int t = EI(c, F_TYPE, m);
+    if constexpr (G == PG_GAME_COINRUN) {
+        if (t == CR_ENEMY || t == CR_SAW) c.s.sd_done = 1;
+    } else if constexpr (G == PG_GAME_BIGFISH) {
+        if (t == BF_FISH) {
+            const float arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+            if (EF(c, F_RX, m) > arx) {
+                c.s.sd_done = 1;
+            } else {
+                c.s.sd_reward += 1; // POSITIVE_REWARD
+                EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+                EF(c, F_RX, 0) = arx + c.s.r_inc;
+                EF(c, F_RY, 0) = ary + c.s.r_inc;
+                c.s.fish_eaten += 1;
+            }
+        }
+    } else if constexpr (G == PG_GAME_HEIST) {
+        if (t == HS_EXIT) {
+            c.s.sd_done = 1;
+            c.s.sd_reward = 10.0f; // COMPLETION_BONUS (assignment)
+            c.s.sd_level_complete = 1;
+        } else if (t == HS_KEY) {
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+            c.s.has_keys |= 1 << EI(c, F_IMAGE_THEME, m);
+        } else if (t == HS_LOCKED_DOOR) {
+            if ((c.s.has_keys >> EI(c, F_IMAGE_THEME, m)) & 1) EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+        }
+    }
+}
+
+// The loop of game_step over entities (basic-abstract-game.cpp:728-750), reverse order.
+// coinrun: the effects are order-free flags, one lane-parallel pass.  Other games: the
+// colliding entities are handled one at a time from the top, re-testing below the last one
+// with the current agent (bigfish grows the agent; heist keys open later doors).
+// collides_with_entities is set by none of the games built here (flagged if ever seen);
+// check_grid_collisions has an effect only in coinrun (handle_grid_collision, coinrun.cpp:144-154).
+template <int G>
+DEV void agent_collisions(Ctx &c) {
+    bool unsupported = false;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        int i = base + LANE;
+        if (i < c.s.num_ents && (EI(c, F_FLAGS, i) & EF_COLLIDES)) unsupported = true;
+    }
+    if (ballot(unsupported)) c.s.error = PG_ERR_BAD_OPTION;
+    if constexpr (G == PG_GAME_COINRUN) {
         float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
-        bool any = false, unsupported = false;
+        bool any = false;
         for (int base = 0; base < c.s.num_ents; base += 64) {
             int i = base + LANE;
             bool hit = false;
@@ -633,15 +716,12 @@ DEV void coinrun_game_step(Ctx &c) {
                     bool col = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
                     hit = col && (t == CR_ENEMY || t == CR_SAW);
                 }
-                if (EI(c, F_FLAGS, i) & EF_COLLIDES) unsupported = true;
             }
             any = any || ballot(hit) != 0;
-            unsupported = unsupported || ballot(unsupported) != 0;
         }
         if (any) c.s.sd_done = 1;
-        if (unsupported) c.s.error = PG_ERR_BAD_OPTION;
-        // check_grid_collisions(agent) (:145-165 -> coinrun.cpp:144-154); other smart
-        // entities (enemies) have no grid-collision effect in coinrun.
+        // check_grid_collisions(agent) (:145-165 -> coinrun.cpp:144-154); enemies have no
+        // grid-collision effect in coinrun.
         int min_x = (int)(ax - (arx + POS_EPS));
         int max_x = (int)(ax + (arx + POS_EPS));
         int min_y = (int)(ay - (ary + POS_EPS));
@@ -659,19 +739,58 @@ DEV void coinrun_game_step(Ctx &c) {
                 }
             }
         }
-    }
-    c.pt.mark(3);
-    erase_if_needed(c);
-    c.pt.mark(4);
-    float gx, gy, grx, gry;
-    if (c.s.agent_erased) {
-        gx = c.s.ghost_x; gy = c.s.ghost_y; grx = c.s.ghost_rx; gry = c.s.ghost_ry;
     } else {
-        gx = EF(c, F_X, 0); gy = EF(c, F_Y, 0); grx = EF(c, F_RX, 0); gry = EF(c, F_RY, 0);
+        int upper = c.s.num_ents;
+        while (upper > 0) {
+            const float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+            int m = -1;
+            for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+                int i = base + LANE;
+                bool hit = false;
+                if (i < upper && EI(c, F_TYPE, i) != PLAYER) { // has_agent_collision (:1135-1140)
+                    float mrg = EF(c, F_COLLISION_MARGIN, i);
+                    float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
+                    hit = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
+                }
+                unsigned long long b = ballot(hit);
+                if (b) {
+                    m = base + top_bit(b);
+                    break;
+                }
+            }
+            if (m < 0) break;
+            handle_agent_collision<G>(c, m);
+            upper = m;
+        }
     }
-    c.s.sd_done = c.s.sd_done || is_out_of_bounds(c, gx, gy, grx, gry);
+}
 
-    // ---- coinrun game_step tail (coinrun.cpp:474-498)
+// ------------------------------------------------------------------ per-game step tails
+DEV void flag_reflected(Ctx &c, int slot, bool set) {
+    int fl = EI(c, F_FLAGS, slot);
+    EI(c, F_FLAGS, slot) = set ? (fl | EF_REFLECTED) : (fl & ~EF_REFLECTED);
+}
+
+// Entity(x, y, vx, vy, rx, ry, type) appended to `entities` (entity.cpp:8-47)
+DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type) {
+    int i = c.s.num_ents;
+    if (i >= PG_CAP) {
+        c.s.error = PG_ERR_ENTITY_OVERFLOW;
+        return -1;
+    }
+    c.s.num_ents = i + 1;
+    EF(c, F_X, i) = x; EF(c, F_Y, i) = y; EF(c, F_VX, i) = vx; EF(c, F_VY, i) = vy;
+    EF(c, F_RX, i) = rx; EF(c, F_RY, i) = ry; EF(c, F_ROTATION, i) = 0; EF(c, F_VROT, i) = 0;
+    EF(c, F_ALPHA, i) = 1.0f; EF(c, F_ALPHA_DECAY, i) = 1.0f; EF(c, F_GROW_RATE, i) = 1.0f;
+    EF(c, F_FRICTION, i) = 1; EF(c, F_COLLISION_MARGIN, i) = 0; EF(c, F_HEALTH, i) = 1;
+    EF(c, F_THETA, i) = -100; EF(c, F_CLIMBER_SPAWN_X, i) = 0;
+    EI(c, F_TYPE, i) = type; EI(c, F_IMAGE_TYPE, i) = type; EI(c, F_IMAGE_THEME, i) = 0;
+    EI(c, F_RENDER_Z, i) = 0; EI(c, F_LIFE_TIME, i) = 0; EI(c, F_EXPIRE_TIME, i) = -1;
+    EI(c, F_FIRE_TIME, i) = -1; EI(c, F_SPAWN_TIME, i) = -1; EI(c, F_FLAGS, i) = EF_AUTO_ERASE;
+    return i;
+}
+
+DEV void coinrun_step_tail(Ctx &c) { // coinrun.cpp:474-498
     if (!c.s.agent_erased) {
         int fl = EI(c, F_FLAGS, 0);
         if (c.s.action_vx > 0) fl &= ~EF_REFLECTED;
@@ -728,6 +847,121 @@ DEV void coinrun_game_step(Ctx &c) {
     c.s.num_ents = n + total_enemies;
     wave_sync();
     c.s.last_agent_y = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+}
+
+// bigfish.cpp:84: (FISH_MAX_R - FISH_MIN_R) * pow(rand01(), 1.4) + FISH_MIN_R -- pow(float, double)
+// resolves to the double pow; checked against the C library's pow for
+// every value rand01() can return (tests/test_gpu_libm.py).
+DEV float bigfish_fish_radius(float u) {
+    return (float)((double)(BF_FISH_MAX_R - BF_FISH_MIN_R) * pow((double)u, 1.4) + (double)BF_FISH_MIN_R);
+}
+
+DEV void bigfish_step_tail(Ctx &c, uint32_t *rg) { // bigfish.cpp:80-106
+    if (rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), 10) == 1) {
+        float ent_r = bigfish_fish_radius(rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)));
+        float ent_y = rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) * (c.s.main_height - 2 * ent_r);
+        float moves_right = (double)rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) < .5 ? 1.0f : 0.0f;
+        float ent_vx = (float)((.15 + (double)rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) * .25) *
+                               (moves_right != 0 ? 1 : -1));
+        float ent_x = moves_right != 0 ? -1 * ent_r : c.s.main_width + ent_r;
+        int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[BF_FISH]); // choose_random_theme
+        float ry = ent_r / aspect_ratio<PG_GAME_BIGFISH>(c, BF_FISH, theme);           // match_aspect_ratio
+        int i = append_entity(c, ent_x, ent_y, ent_vx, 0, ent_r, ry, BF_FISH);
+        if (i >= 0) {
+            EI(c, F_IMAGE_THEME, i) = theme;
+            if (moves_right == 0) EI(c, F_FLAGS, i) = EF_AUTO_ERASE | EF_REFLECTED;
+        }
+    }
+    if (c.s.fish_eaten >= BF_FISH_QUOTA) {
+        c.s.sd_done = 1;
+        c.s.sd_reward += 10; // COMPLETION_BONUS
+        c.s.sd_level_complete = 1;
+    }
+    if (c.s.action_vx > 0) flag_reflected(c, 0, false);
+    if (c.s.action_vx < 0) flag_reflected(c, 0, true);
+}
+
+DEV void maze_step_tail(Ctx &c) { // maze.cpp:113-131
+    if (c.s.action_vx > 0) flag_reflected(c, 0, true);
+    if (c.s.action_vx < 0) flag_reflected(c, 0, false);
+    int ix = (int)EF(c, F_X, 0);
+    int iy = (int)EF(c, F_Y, 0);
+    if (get_obj(c, ix, iy) == MZ_GOAL) {
+        // set_obj(ix, iy, SPACE): the HBM grid, its int8 mirror and this step's LDS copy
+        int cell = iy * c.s.main_width + ix;
+        if (LANE == 0) {
+            c.d.grid[(size_t)c.env * PG_GRID_MAX + cell] = SPACE;
+            c.d.grid8[(size_t)c.env * PG_GRID_MAX + cell] = (int8_t)SPACE;
+            c.grid8[cell] = (int8_t)SPACE;
+            if (cell < PG_LATENT_GRID) c.d.latent[(size_t)c.env * PG_LATENT_N + 2 + cell] = SPACE;
+        }
+        wave_sync();
+        c.s.sd_reward += 10.0f; // REWARD
+        c.s.sd_level_complete = 1;
+    }
+    c.s.sd_done = c.s.sd_reward > 0;
+    if (LANE == 0) { // latent agent_pos = int(agent->x), int(agent->y) (maze.cpp:144-145)
+        c.d.latent[(size_t)c.env * PG_LATENT_N + 2 + PG_LATENT_GRID] = ix;
+        c.d.latent[(size_t)c.env * PG_LATENT_N + 3 + PG_LATENT_GRID] = iy;
+    }
+}
+
+DEV void heist_step_tail(Ctx &c) { // heist.cpp:205-209: agent->face_direction(action_vx, action_vy)
+    if (c.s.agent_erased) return;
+    float dx = c.s.action_vx, dy = c.s.action_vy;
+    if (dx != 0 || dy != 0) EF(c, F_ROTATION, 0) = c.d.rot_angles[((int)dx + 1) * 3 + ((int)dy + 1)];
+}
+
+// ------------------------------------------------------------------ game_step
+template <int G>
+DEV void game_step(Ctx &c) {
+    // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
+    uint32_t *rg = c.d.mt + (size_t)c.env * 2 * PG_MT_WORDS;
+    c.s.step_rand_int = rg_randint_of(mt_next_global(rg, c.s.rg_mti, c.lds), 0, 1000000);
+    c.pt.mark(0);
+    c.s.move_action = c.s.action % 9;
+    c.s.special_action = 0;
+    if (c.s.action >= 9) {
+        c.s.special_action = c.s.action - 8;
+        c.s.move_action = 4;
+    }
+    if (c.s.move_action != 4) c.s.last_move_action = c.s.move_action;
+    c.s.action_vrot = 0;
+    c.s.action_vx = 0;
+    c.s.action_vy = 0;
+    set_action_xy<G>(c, c.s.move_action);
+    if (c.s.grid_step) {
+        EF(c, F_VX, 0) = c.s.action_vx;
+        EF(c, F_VY, 0) = c.s.action_vy;
+    } else {
+        update_agent_velocity<G>(c);
+        float vrot = EF(c, F_VROT, 0);
+        vrot = MIXRATEROT * vrot;
+        vrot += MIXRATEROT * (15 * PI_F / 180) * c.s.action_vrot;
+        EF(c, F_VROT, 0) = vrot;
+    }
+    wave_sync();
+    c.pt.mark(1);
+    build_interactor_list<G>(c);
+    step_entities<G>(c, c.slist);
+    c.pt.mark(2);
+    agent_collisions<G>(c);
+    c.pt.mark(3);
+    erase_if_needed(c);
+    c.pt.mark(4);
+    float gx, gy, grx, gry;
+    if (c.s.agent_erased) {
+        gx = c.s.ghost_x; gy = c.s.ghost_y; grx = c.s.ghost_rx; gry = c.s.ghost_ry;
+    } else {
+        gx = EF(c, F_X, 0); gy = EF(c, F_Y, 0); grx = EF(c, F_RX, 0); gry = EF(c, F_RY, 0);
+    }
+    c.s.sd_done = c.s.sd_done || is_out_of_bounds(c, gx, gy, grx, gry);
+    // ---- per-game tail
+    if constexpr (G == PG_GAME_COINRUN) coinrun_step_tail(c);
+    if constexpr (G == PG_GAME_BIGFISH) bigfish_step_tail(c, rg);
+    if constexpr (G == PG_GAME_MAZE) maze_step_tail(c);
+    if constexpr (G == PG_GAME_HEIST) heist_step_tail(c);
+    wave_sync();
     c.pt.mark(5);
 }
 
@@ -739,17 +973,18 @@ DEV uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-} // namespace
-
 // Game::step (game.cpp:136-171) minus reset (queued) and observe (pg_render).
-extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use_hash, uint64_t hash_seed, int32_t hash_t) {
+// env_list: the envs of this game (mixed batches), or null = envs 0..gridDim.x-1.
+template <int G>
+__global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env_list, int use_hash,
+                                                      uint64_t hash_seed, int32_t hash_t) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     Ctx c;
-    c.d = d;
-    c.env = blockIdx.x;
+    c.d = game_view(d, G);
+    c.env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     c.s = d.envs[c.env];
     c.E = d.ents;
     c.plane = (size_t)d.num_envs * PG_CAP;
@@ -783,7 +1018,7 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
     c.s.sd_reward = 0;
     c.s.sd_done = 0;
     c.s.sd_level_complete = 0;
-    coinrun_game_step(c);
+    game_step<G>(c);
     c.s.sd_done = c.s.sd_done || will_force_reset || (c.s.cur_time >= c.s.timeout);
     c.s.total_reward += c.s.sd_reward;
     if (c.s.sd_reward != 0) {
@@ -798,8 +1033,8 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
 
     if (LANE == 0) {
         if (done) {
-            int q = atomicAdd(d.reset_count, 1);
-            d.reset_queue[q] = c.env;
+            int q = atomicAdd(d.reset_count + G, 1);
+            d.reset_queue[(size_t)G * d.num_envs + q] = c.env;
         }
         d.rew[c.env] = c.s.sd_reward;
         d.first[c.env] = (uint8_t)first;
@@ -814,14 +1049,48 @@ extern "C" __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, int use
         PG_W(last_reward_timer) PG_W(last_reward) PG_W(prev_level_seed) PG_W(episode_done) PG_W(num_ents)
         PG_W(agent_erased) PG_W(ghost_x) PG_W(ghost_y) PG_W(ghost_vx) PG_W(ghost_vy) PG_W(ghost_rx) PG_W(ghost_ry)
         PG_W(move_action) PG_W(special_action) PG_W(last_move_action) PG_W(action_vx) PG_W(action_vy)
-        PG_W(action_vrot) PG_W(step_rand_int) PG_W(rg_mti) PG_W(has_support) PG_W(facing_right)
-        PG_W(is_on_crate) PG_W(last_agent_y) PG_W(error)
+        PG_W(action_vrot) PG_W(step_rand_int) PG_W(rg_mti) PG_W(error)
+        if constexpr (G == PG_GAME_COINRUN) {
+            PG_W(has_support) PG_W(facing_right) PG_W(is_on_crate) PG_W(last_agent_y)
+        }
+        if constexpr (G == PG_GAME_BIGFISH) { PG_W(fish_eaten) }
+        if constexpr (G == PG_GAME_HEIST) { PG_W(has_keys) }
 #undef PG_W
     }
     c.pt.mark(6);
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 }
 
-extern "C" void pg_launch_step(const PGDev *d, hipStream_t s, int use_hash, uint64_t seed, int32_t t) {
-    hipLaunchKernelGGL(pg_step_kernel, dim3(d->num_envs), dim3(64), 0, s, *d, use_hash, seed, t);
+} // namespace
+
+extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
+                               int use_hash, uint64_t seed, int32_t t) {
+    if (count <= 0) return;
+#define PG_CASE(G)                                                                                   \
+    case G:                                                                                          \
+        hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, use_hash, seed, t); \
+        break;
+    switch (game) {
+        PG_CASE(PG_GAME_COINRUN)
+        PG_CASE(PG_GAME_BIGFISH)
+        PG_CASE(PG_GAME_MAZE)
+        PG_CASE(PG_GAME_HEIST)
+    default: break;
+    }
+#undef PG_CASE
+}
+
+// Self-test of the libm-dependent device arithmetic (tests/test_gpu_libm.py): which = 0 ->
+// bigfish_fish_radius(in[i]).
+__global__ void pg_selftest_kernel(int which, const float *in, float *out, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (which == 0) out[i] = bigfish_fish_radius(in[i]);
+}
+
+extern "C" int procgen_selftest_libm(int which, const float *d_in, float *d_out, int64_t n, void *stream) {
+    if (which != 0 || n <= 0) return -1;
+    int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(pg_selftest_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, which, d_in, d_out, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -70,7 +70,7 @@ SIGNATURES = {
     "get_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "set_state": (None, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "procgen_upload_atlas": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_start": (ctypes.c_int, [ctypes.c_void_p]),
     "procgen_act_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_act_hashed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32]),
@@ -82,6 +82,8 @@ SIGNATURES = {
     "procgen_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "procgen_debug_env": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "procgen_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "procgen_selftest_libm": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_void_p]),
 }
 
 _LIB = None

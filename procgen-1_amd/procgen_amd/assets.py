@@ -12,6 +12,9 @@ Layout handed to the engine (and, in tests, to the CPU oracle):
 
 Mirrored sprites (``QImage::mirrored(true, false)``, basic-abstract-game.cpp:121)
 are not stored: the compositor flips the source column instead.
+
+``EngineAtlas`` packs several games for the engine's C ABI (procgen_upload_atlas): one
+pixel array, per-game tables indexed by game id (procgen/env.py:15-32 order).
 """
 import functools
 import os
@@ -82,3 +85,42 @@ class Atlas:
 @functools.lru_cache(maxsize=None)
 def atlas_for(game):
     return Atlas(game)
+
+
+class EngineAtlas:
+    """Atlases of every game of a batch in the engine's layout (include/procgen_mi355x.h)."""
+
+    NUM_GAMES = 16
+    MAX_BG = 64
+
+    def __init__(self, games):
+        games = list(dict.fromkeys(games))
+        self.sprites = np.zeros((self.NUM_GAMES, catalog.NUM_IMAGE_SLOTS, 4), dtype=np.int32)
+        self.backgrounds = np.zeros((self.NUM_GAMES, self.MAX_BG, 4), dtype=np.int32)
+        self.num_backgrounds = np.zeros(self.NUM_GAMES, dtype=np.int32)
+        self.num_themes = np.zeros((self.NUM_GAMES, catalog.MAX_ASSETS), dtype=np.int32)
+        chunks, base = [], 0
+        for g in games:
+            a = atlas_for(g)
+            gid = catalog.ENV_NAMES.index(g)
+            sp = a.sprites.copy()
+            sp[:, 0] += np.where(sp[:, 1] > 0, base, 0).astype(np.int32)
+            self.sprites[gid] = sp
+            nb = a.backgrounds.shape[0]
+            assert nb <= self.MAX_BG
+            bg = a.backgrounds.copy()
+            bg[:, 0] += base
+            self.backgrounds[gid, :nb] = bg
+            self.num_backgrounds[gid] = nb
+            self.num_themes[gid] = a.num_themes
+            chunks.append(a.pixels)
+            base += a.pixels.size
+        self.pixels = np.ascontiguousarray(np.concatenate(chunks)).astype(np.uint32)
+        assert self.pixels.size < 2 ** 31
+        self.games = games
+
+
+@functools.lru_cache(maxsize=None)
+def engine_atlas_for(names):
+    """names: tuple of game names (a batch's env_name list)."""
+    return EngineAtlas(names)

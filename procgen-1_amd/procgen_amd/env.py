@@ -15,7 +15,7 @@ import random
 import numpy as np
 
 from . import _lib
-from .assets import atlas_for
+from .assets import engine_atlas_for
 
 MAX_STATE_SIZE = 2 ** 20  # procgen/env.py:13
 
@@ -105,11 +105,11 @@ class BaseProcgenEnv:
         if not self._handle:
             msg = lib.procgen_error_string(None)
             raise ProcgenError("libenv_make failed: %s" % (msg.decode() if msg else "unknown"))
-        atlas = atlas_for(env_name)
+        atlas = engine_atlas_for(tuple(env_name.split(",")))
         self._atlas = atlas
         rc = lib.procgen_upload_atlas(self._handle, atlas.pixels.ctypes.data, atlas.pixels.size,
                                       atlas.sprites.ctypes.data, atlas.backgrounds.ctypes.data,
-                                      atlas.backgrounds.shape[0], atlas.num_themes.ctypes.data)
+                                      atlas.num_backgrounds.ctypes.data, atlas.num_themes.ctypes.data)
         _check(lib, self._handle, rc)
 
         self.ob_types = self._types(_lib.SPACE_OBSERVATION)

@@ -56,6 +56,7 @@ def load():
         lib.oracle_mazegen.argtypes = [ctypes.c_int32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_latent.argtypes = [ctypes.c_void_p] * 5
+        lib.oracle_bigfish_radius.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         _LIB = lib
     return _LIB
 

@@ -90,3 +90,13 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(_lib.libenv_tensortype) == 212
     assert ctypes.sizeof(_lib.libenv_option) == 144
     assert ctypes.sizeof(_lib.pg_image) == 16
+
+
+def test_mixed_batch_size_must_divide():
+    h, msg = make(dict(BASE, env_name="coinrun,maze"), num=5)  # vecgame.cpp:345 num_envs % #games
+    assert not h and "multiple" in msg
+
+
+def test_memory_mode_only_for_memory_games():
+    h, msg = make(dict(BASE, env_name="bigfish", distribution_mode=10))  # game.cpp:83-84
+    assert not h and "distribution_mode" in msg

@@ -47,3 +47,28 @@ def test_hashed_actions_vector_matches_scalar():
     s = [splitmix64((0x5EED ^ ((int(g) & 0xFFFFFFFF) << 32) ^ 12345)) % 15 for g in ids]
     assert v.tolist() == s
     assert v.min() >= 0 and v.max() < 15
+
+
+def test_new_game_theme_counts():
+    from procgen_amd import catalog
+    bf, mz, hs = catalog.num_themes("bigfish"), catalog.num_themes("maze"), catalog.num_themes("heist")
+    assert bf[0] == 1 and bf[2] == 3                      # bigfish.cpp:34-43
+    assert mz[51] == 1 and mz[2] == 1 and mz[0] == 1      # maze.cpp:33-41
+    assert hs[2] == 3 and hs[1] == 3 and hs[9] == 1       # heist.cpp:46-64
+
+
+def test_engine_atlas_tables():
+    from procgen_amd import catalog
+    from procgen_amd.assets import atlas_for, engine_atlas_for
+    ea = engine_atlas_for(("bigfish", "coinrun", "heist", "maze"))
+    for g in ("bigfish", "coinrun", "heist", "maze"):
+        gid = catalog.ENV_NAMES.index(g)
+        a = atlas_for(g)
+        assert ea.num_backgrounds[gid] == a.backgrounds.shape[0]
+        np.testing.assert_array_equal(ea.num_themes[gid], a.num_themes)
+        for slot in np.nonzero(a.sprites[:, 1])[0]:
+            off, w, h, _ = ea.sprites[gid, slot]
+            o2, w2, h2, _ = a.sprites[slot]
+            assert (w, h) == (w2, h2)
+            np.testing.assert_array_equal(ea.pixels[off:off + w * h], a.pixels[o2:o2 + w * h])
+    assert ea.num_backgrounds[catalog.ENV_NAMES.index("maze")] == 9  # topdown group
