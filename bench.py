@@ -46,7 +46,7 @@ def _cpu_worker(args):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(game, num_levels, max_workers=16, steps=3000):
+def cpu_baseline(game, num_levels, max_workers=16, steps=12000):
     """The CPU oracle (scalar C restatement of the reference step path, parity-checked)
     on this host: `cores` worker processes, each 64 envs x `steps` random steps (~10 s of
     CPU work per worker for coinrun)."""

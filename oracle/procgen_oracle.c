@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11 };
+enum { GAME_BIGFISH = 0, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11, GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -229,6 +229,9 @@ typedef struct {
     /* maze (maze.cpp:16-18) / heist (heist.cpp:18-21) */
     int maze_dim, world_dim, num_keys;
     bool has_keys[4];
+    /* miner (miner.cpp:26-28) */
+    int diamonds_remaining, main_area;
+    bool died;
     /* observation of the last step */
     uint32_t canvas[RES_W * RES_H];
 } Game;
@@ -337,6 +340,11 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
         if (src->type == PLAYER && cr_is_wall(target)) return true;
         return false;
     }
+    if (g->game_id == GAME_MINER) { /* miner.cpp:68-75: BOULDER 1, MOVING_BOULDER 3, OOB_WALL 10 */
+        if (base) return true;
+        if (src->type == PLAYER && (target == 1 || target == 3 || target == 10)) return true;
+        return false;
+    }
     return base;
 }
 
@@ -377,6 +385,8 @@ static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *targe
 static bool hook_will_reflect(Game *g, int src, int target) {
     if (g->game_id == GAME_COINRUN) /* coinrun.cpp:140-142 */
         return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    if (g->game_id == GAME_MINER) /* miner.cpp:77-79: ENEMY 5 off BOULDER, DIAMOND, MOVING_BOULDER/DIAMOND, out of bounds */
+        return src == 5 && (target == 1 || target == 2 || target == 3 || target == 4 || target == g->out_of_bounds_object);
     return false;
 }
 
@@ -395,6 +405,16 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->rx += g->r_inc;
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
+            }
+        }
+    } else if (g->game_id == GAME_MINER) { /* miner.cpp:81-93: ENEMY 5, EXIT 6 */
+        if (obj->type == 5) {
+            g->sd_done = true;
+        } else if (obj->type == 6) {
+            if (g->diamonds_remaining == 0) {
+                g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+                g->sd_level_complete = true;
+                g->sd_done = true;
             }
         }
     } else if (g->game_id == GAME_HEIST) { /* heist.cpp:80-96 */
@@ -452,6 +472,10 @@ static int hook_image_for_type(Game *g, int type) {
         } else if (type == CR_ENEMY_BARRIER) {
             return -1;
         }
+    }
+    if (g->game_id == GAME_MINER) { /* miner.cpp:95-103: MOVING_BOULDER -> BOULDER, MOVING_DIAMOND -> DIAMOND */
+        if (type == 3) return 1;
+        if (type == 4) return 2;
     }
     return abs(type); /* basic-abstract-game.cpp:446-448 */
 }
@@ -652,7 +676,7 @@ static void set_action_xy(Game *g, int move_action) {
     g->action_vx = (float)(move_action / 3 - 1); /* basic-abstract-game.cpp:667-671 */
     g->action_vy = (float)(move_action % 3 - 1);
     g->action_vrot = 0;
-    if (g->game_id == GAME_MAZE) { /* maze.cpp:107-111 */
+    if (g->game_id == GAME_MAZE || g->game_id == GAME_MINER) { /* maze.cpp:107-111, miner.cpp:105-109 */
         if (g->action_vx != 0) g->action_vy = 0;
     }
 }
@@ -1400,12 +1424,209 @@ static void heist_game_step(Game *g) { /* :205-209 */
     if (dx != 0 || dy != 0) agent->rotation = -1 * atan2f(dy, dx) + 0.0f;
 }
 
+/* ================================================================== miner (games/miner.cpp, fork-modified) */
+#define MN_BOULDER 1
+#define MN_DIAMOND 2
+#define MN_MOVING_BOULDER 3
+#define MN_MOVING_DIAMOND 4
+#define MN_ENEMY 5
+#define MN_EXIT 6
+#define MN_DIRT 9
+#define MN_OOB_WALL 10
+#define MN_MUD 11
+#define MN_DEAD_PLAYER 12
+static const float MN_DIAMOND_REWARD = 1.0f;
+
+static int get_obj_idx(Game *g, int idx) { /* basic-abstract-game.cpp:194-199 */
+    if (!(0 <= idx && idx < g->grid_w * g->grid_h)) return g->out_of_bounds_object;
+    return g->grid[idx];
+}
+static void set_obj_idx(Game *g, int idx, int v) { /* :225-227 */
+    fassert(0 <= idx && idx < g->grid_w * g->grid_h);
+    g->grid[idx] = v;
+}
+static int mn_agent_index(Game *g) { /* miner.cpp:98-100 */
+    Entity *a = AG(g);
+    return (int)a->y * g->main_width + (int)a->x;
+}
+static int mn_moving_type(int t) { /* :220-227 */
+    if (t == MN_DIAMOND) return MN_MOVING_DIAMOND;
+    if (t == MN_BOULDER) return MN_MOVING_BOULDER;
+    return t;
+}
+static bool mn_is_moving(int t) { return t == MN_MOVING_BOULDER || t == MN_MOVING_DIAMOND; } /* :229-231 */
+static int mn_stationary_type(int t) { /* :233-240 */
+    if (t == MN_MOVING_DIAMOND) return MN_DIAMOND;
+    if (t == MN_MOVING_BOULDER) return MN_BOULDER;
+    return t;
+}
+static bool mn_is_free(Game *g, int idx) { /* :242-244 */
+    return get_obj_idx(g, idx) == SPACE && (mn_agent_index(g) != idx);
+}
+static bool mn_is_round(int t) { /* :246-248 */
+    return t == MN_BOULDER || t == MN_MOVING_BOULDER || t == MN_DIAMOND || t == MN_MOVING_DIAMOND;
+}
+
+static void miner_choose_world_dim(Game *g) { /* :119-132 */
+    int d = g->options.distribution_mode;
+    if (d == EasyMode) { g->main_width = 10; g->main_height = 10; }
+    else if (d == HardMode) { g->main_width = 20; g->main_height = 20; }
+    else if (d == MemoryMode) { g->main_width = 35; g->main_height = 35; }
+    g->main_area = g->main_width * g->main_height;
+}
+
+static void miner_game_reset(Game *g, const or_atlas *at) { /* :134-218 */
+    miner_choose_world_dim(g);
+    basic_game_reset(g, at);
+    MT *r = &g->rand_gen;
+    g->died = false;
+    Entity *agent = AG(g);
+    agent->rx = .5f;
+    agent->ry = .5f;
+    g->options.center_agent = g->options.distribution_mode == MemoryMode;
+    g->grid_step = true;
+    float diamond_pct = 12 / 400.0f;
+    float boulder_pct = 80 / 400.0f;
+    float mud_pct = 12 / 400.0f;
+    int num_diamonds = (int)(diamond_pct * g->grid_size);
+    int num_boulders = (int)(boulder_pct * g->grid_size);
+    int num_mud = (int)(mud_pct * g->grid_size);
+    /* RandGen::simple_choose(main_area, k) (randgen.cpp:70-88): rejection against a std::set */
+    int k = num_diamonds + num_boulders + num_mud + 1;
+    static int obj_idxs[MAX_GRID];
+    static bool taken[MAX_GRID];
+    fassert(k <= g->main_area && g->main_area <= MAX_GRID);
+    memset(taken, 0, sizeof(taken));
+    for (int i = 0; i < k; i++) {
+        int next = rg_randn(r, g->main_area);
+        while (taken[next]) next = rg_randn(r, g->main_area);
+        obj_idxs[i] = next;
+        taken[next] = true;
+    }
+    int agent_x = obj_idxs[0] % g->main_width;
+    int agent_y = obj_idxs[0] / g->main_width;
+    agent->x = (float)(agent_x + .5);
+    agent->y = (float)(agent_y + .5);
+    for (int i = 0; i < g->main_area; ++i) set_obj_idx(g, i, MN_DIRT);
+    for (int i = 0; i < num_diamonds; ++i) set_obj_idx(g, obj_idxs[i + 1], MN_DIAMOND);
+    for (int i = 0; i < num_boulders; ++i) set_obj_idx(g, obj_idxs[i + 1 + num_diamonds], MN_BOULDER);
+    for (int i = 0; i < num_mud; ++i) set_obj_idx(g, obj_idxs[i + 1 + num_diamonds + num_boulders], MN_MUD);
+    static int dirt_cells[MAX_GRID]; /* get_cells_with_type(DIRT) (:203-213): ascending */
+    int nd = 0;
+    for (int i = 0; i < g->grid_size; i++)
+        if (g->grid[i] == MN_DIRT) dirt_cells[nd++] = i;
+    set_obj(g, (int)agent->x, (int)agent->y, SPACE);
+    for (int i = -1; i <= 1; ++i) {
+        for (int j = -1; j <= 1; ++j) {
+            int ox = agent_x + i, oy = agent_y + j;
+            if (get_obj(g, ox, oy) == MN_BOULDER) set_obj(g, ox, oy, MN_DIRT);
+        }
+    }
+    static int exit_candidates[MAX_GRID];
+    int ne = 0;
+    for (int c = 0; c < nd; c++) {
+        int cell = dirt_cells[c];
+        int above_obj = get_obj_idx(g, cell + g->main_width);
+        if (above_obj == MN_DIRT || above_obj == g->out_of_bounds_object) exit_candidates[ne++] = cell;
+    }
+    fassert(ne > 0);
+    int exit_cell = exit_candidates[rg_randn(r, ne)];
+    set_obj_idx(g, exit_cell, SPACE);
+    int e = add_entity(g, (float)((exit_cell % g->main_width) + .5), (float)((exit_cell / g->main_width) + .5), 0, 0,
+                       .5f, MN_EXIT);
+    g->ents[e].render_z = -1;
+}
+
+static void mn_move_cell(Game *g, int x, int y, bool *has_moved) { /* :310-346 */
+    int w = g->main_width;
+    int idx = x + w * y;
+    bool current_moved = has_moved[idx];
+    int obj = get_obj_idx(g, idx);
+    int obj_x = idx % w;
+    int stat_type = mn_stationary_type(obj);
+    int agent_idx = mn_agent_index(g);
+    /* `BOULDER || DIAMOND && !moved`: && binds tighter */
+    if (stat_type == MN_BOULDER || (stat_type == MN_DIAMOND && !current_moved)) {
+        int below_idx = idx - w;
+        int below_object = get_obj_idx(g, below_idx);
+        bool agent_is_below = agent_idx == below_idx;
+        if (below_object == SPACE && !agent_is_below) {
+            set_obj_idx(g, idx, SPACE);
+            int two_below_obj = get_obj_idx(g, below_idx - w);
+            int obj_type = two_below_obj == SPACE ? mn_moving_type(obj) : stat_type;
+            set_obj_idx(g, below_idx, obj_type);
+            has_moved[below_idx] = true;
+        } else if (agent_is_below && mn_is_moving(obj)) {
+            g->died = true;
+            /* entities.erase(entities.begin()): entities[0] is the agent */
+            fassert(!g->agent_erased && g->num_ents > 0);
+            g->agent_ghost = g->ents[0];
+            g->agent_erased = true;
+            memmove(&g->ents[0], &g->ents[1], sizeof(Entity) * (size_t)(g->num_ents - 1));
+            g->num_ents--;
+            set_obj_idx(g, below_idx, MN_DEAD_PLAYER);
+        } else if (mn_is_round(below_object) && obj_x > 0 && mn_is_free(g, idx - 1) && mn_is_free(g, idx - w - 1)) {
+            set_obj_idx(g, idx, SPACE);
+            set_obj_idx(g, idx - 1, stat_type);
+            has_moved[idx - 1] = true;
+        } else if (mn_is_round(below_object) && obj_x < w - 1 && mn_is_free(g, idx + 1) && mn_is_free(g, idx - w + 1)) {
+            set_obj_idx(g, idx, SPACE);
+            set_obj_idx(g, idx + 1, stat_type);
+            has_moved[idx + 1] = true;
+        } else {
+            set_obj_idx(g, idx, stat_type);
+        }
+    }
+}
+
+static void miner_game_step(Game *g) { /* :250-308 */
+    static bool has_moved[MAX_GRID];
+    memset(has_moved, 0, sizeof(has_moved));
+    int w = g->main_width, h = g->main_height;
+    for (int y = 0; (float)y <= AG(g)->y; ++y)
+        for (int x = 0; x < w; ++x) mn_move_cell(g, x, y, has_moved);
+    basic_game_step(g);
+    if (g->died) {
+        g->sd_done = true;
+        return;
+    }
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+    /* handle_push (:262-281) */
+    int agent_idx = mn_agent_index(g);
+    int agentx = agent_idx % w;
+    if (g->action_vx == 1 && (agent->vx == 0) && (agentx < w - 2) && get_obj_idx(g, agent_idx + 1) == MN_BOULDER &&
+        get_obj_idx(g, agent_idx + 2) == SPACE) {
+        set_obj_idx(g, agent_idx + 1, SPACE);
+        set_obj_idx(g, agent_idx + 2, MN_BOULDER);
+        has_moved[agent_idx + 2] = true;
+        agent->x += 1;
+    } else if (g->action_vx == -1 && (agent->vx == 0) && (agentx > 1) && get_obj_idx(g, agent_idx - 1) == MN_BOULDER &&
+               get_obj_idx(g, agent_idx - 2) == SPACE) {
+        set_obj_idx(g, agent_idx - 1, SPACE);
+        set_obj_idx(g, agent_idx - 2, MN_BOULDER);
+        has_moved[agent_idx - 2] = true;
+        agent->x -= 1;
+    }
+    int agent_obj = mn_stationary_type(get_obj(g, (int)agent->x, (int)agent->y));
+    if (agent_obj == MN_DIAMOND) g->sd_reward += MN_DIAMOND_REWARD;
+    if (agent_obj == MN_DIRT || agent_obj == MN_MUD || agent_obj == MN_DIAMOND) set_obj(g, (int)agent->x, (int)agent->y, SPACE);
+    for (int y = (int)(AG(g)->y + 1); y < h; ++y)
+        for (int x = 0; x < w; ++x) mn_move_cell(g, x, y, has_moved);
+    int diamonds = 0; /* count_diamonds (:348-356) */
+    for (int idx = 0; idx < g->main_area; ++idx)
+        if (mn_stationary_type(get_obj_idx(g, idx)) == MN_DIAMOND) ++diamonds;
+    g->diamonds_remaining = diamonds;
+}
+
 /* ================================================================== Game (game.cpp) */
 static void game_reset_dispatch(Game *g, const or_atlas *at) {
     if (g->game_id == GAME_COINRUN) coinrun_game_reset(g, at);
     else if (g->game_id == GAME_BIGFISH) bigfish_game_reset(g, at);
     else if (g->game_id == GAME_MAZE) maze_game_reset(g, at);
     else if (g->game_id == GAME_HEIST) heist_game_reset(g, at);
+    else if (g->game_id == GAME_MINER) miner_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -1413,6 +1634,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_BIGFISH) bigfish_game_step(g, at);
     else if (g->game_id == GAME_MAZE) maze_game_step(g);
     else if (g->game_id == GAME_HEIST) heist_game_step(g);
+    else if (g->game_id == GAME_MINER) miner_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -1835,6 +2057,10 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
         r = adjust_rect(base, adj);
     }
     const or_image *im = &at->sprites[img_idx];
+    /* miner's MUD image (misc_assets/mud.png, resources.cpp:511) is absent from the reference's
+     * asset tree -- the reference cannot draw it at all (load_resource_ptr fatals); this restatement
+     * and the engine both draw nothing for it (parity unpinned for MUD tiles) */
+    if (im->w <= 0 && g->game_id == GAME_MINER && img_type == MN_MUD) return;
     if (im->w <= 0) fatal_msg("missing sprite (generated assets are not restated yet)");
     double opacity = alpha != 1 ? (double)alpha : 1.0;
     if (rotation == 0) {
@@ -1926,6 +2152,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "bigfish") == 0) return GAME_BIGFISH;
     if (strcmp(name, "maze") == 0) return GAME_MAZE;
     if (strcmp(name, "heist") == 0) return GAME_HEIST;
+    if (strcmp(name, "miner") == 0) return GAME_MINER;
     return -1;
 }
 
@@ -1974,6 +2201,17 @@ static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
     g->out_of_bounds_object = WALL_OBJ;
     g->visibility = 8.0f;
 }
+static void miner_ctor(Game *g) { /* miner.cpp:30-43 */
+    g->main_width = 20;
+    g->main_height = 20;
+    g->main_area = g->main_width * g->main_height;
+    g->mixrate = .5f;
+    g->maxspeed = .5f;
+    g->has_useful_vel_info = false;
+    g->out_of_bounds_object = MN_OOB_WALL;
+    g->visibility = 8.0f;
+    g->diamonds_remaining = -1;
+}
 static void heist_ctor(Game *g) { /* heist.cpp:23-35 */
     g->has_useful_vel_info = false;
     g->main_width = 20;
@@ -1987,7 +2225,8 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
     /* game.cpp:76-86: easy and hard for every game; memory for heist and maze (of those restated) */
-    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE));
+    bool dm_ok = dm == EasyMode || dm == HardMode ||
+                 (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE || gid == GAME_MINER));
     if (!dm_ok) return NULL;
     Vec *v = (Vec *)calloc(1, sizeof(Vec));
     v->count = count;
@@ -2014,6 +2253,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_BIGFISH) bigfish_ctor(g);
         else if (gid == GAME_MAZE) maze_ctor(g);
         else if (gid == GAME_HEIST) heist_ctor(g);
+        else if (gid == GAME_MINER) miner_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;
@@ -2090,13 +2330,21 @@ void oracle_latent(void *h, int32_t *grid_size, int32_t *grid, int32_t *agent_po
         memset(gr, 0, 35 * 35 * 4);
         memset(ap, 0, 8);
         memset(ep, 0, 8);
-        if (g->game_id == GAME_MAZE) {
+        if (g->game_id == GAME_MAZE || g->game_id == GAME_MINER) {
             gs[0] = g->grid_w;
             gs[1] = g->grid_h;
             for (int i = 0; i < g->grid_w * g->grid_h && i < 35 * 35; i++) gr[i] = g->grid[i];
             Entity *a = AG(g);
             ap[0] = (int)a->x;
             ap[1] = (int)a->y;
+        }
+        if (g->game_id == GAME_MINER) { /* miner.cpp:378-396: the first EXIT entity */
+            for (int i = 0; i < g->num_ents; i++)
+                if (g->ents[i].type == MN_EXIT) {
+                    ep[0] = (int)g->ents[i].x;
+                    ep[1] = (int)g->ents[i].y;
+                    break;
+                }
         }
     }
 }

@@ -111,9 +111,10 @@ int game_id(const std::string &name) {
     if (name == "bigfish") return PG_GAME_BIGFISH;
     if (name == "maze") return PG_GAME_MAZE;
     if (name == "heist") return PG_GAME_HEIST;
+    if (name == "miner") return PG_GAME_MINER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, coinrun, heist, maze";
+const char *SUPPORTED_GAMES = "bigfish, coinrun, heist, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -168,6 +169,16 @@ void construct_env(PGEnv &s, int gid) {
         s.has_useful_vel_info = 0;
         s.out_of_bounds_object = 51; // WALL_OBJ
         s.visibility = 8.0f;
+    } else if (gid == PG_GAME_MINER) { // miner.cpp:30-43
+        s.main_width = 20;
+        s.main_height = 20;
+        s.main_area = 400;
+        s.mixrate = .5f;
+        s.maxspeed = .5f;
+        s.has_useful_vel_info = 0;
+        s.out_of_bounds_object = 10; // OOB_WALL
+        s.visibility = 8.0f;
+        s.diamonds_remaining = -1;
     } else if (gid == PG_GAME_HEIST) { // heist.cpp:23-35
         s.has_useful_vel_info = 0;
         s.main_width = 20;
@@ -488,7 +499,8 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (gid < 0) return bad("env '" + nm + "' is not in this build (supported: " + SUPPORTED_GAMES + ")");
         // game.cpp:76-86 distribution mode validity
         bool dm_ok = distribution_mode == PG_EASY || distribution_mode == PG_HARD ||
-                     (distribution_mode == PG_MEMORY && (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE));
+                     (distribution_mode == PG_MEMORY &&
+                      (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE || gid == PG_GAME_MINER));
         if (!dm_ok) return bad("invalid distribution_mode for " + nm);
         gids.push_back(gid);
     }
@@ -501,7 +513,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     VecEnv *v = new VecEnv();
     v->num_envs = num_envs;
     v->games = gids;
-    for (int g : gids) v->has_latent = v->has_latent || g == PG_GAME_MAZE;
+    for (int g : gids) v->has_latent = v->has_latent || g == PG_GAME_MAZE || g == PG_GAME_MINER;
     v->env_offset = env_offset;
     v->num_actions = num_actions;
     v->render_human = render_human;
@@ -650,6 +662,7 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
     HIPCHECK(copy_sync(v, v->d_bgs, backgrounds, bgs * sizeof(pg_image), hipMemcpyHostToDevice));
     HIPCHECK(copy_sync(v, v->d_themes, num_themes, (size_t)PG_NUM_GAMES * 100 * 4, hipMemcpyHostToDevice));
     v->dev.pixels = v->d_pixels;
+    v->dev.num_pixels = num_pixels < 0xffffffffLL ? (uint32_t)num_pixels : 0xffffffffu;
     v->dev.sprites = v->d_sprites;
     v->dev.backgrounds = v->d_bgs;
     v->dev.num_themes = v->d_themes;
@@ -882,7 +895,7 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
         p += ents * 4;
     }
     if (cells) copy_sync(v, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
-    if (v->has_latent && s.game_id == PG_GAME_MAZE) { // the latent info mirrors the restored grid
+    if (v->has_latent && (s.game_id == PG_GAME_MAZE || s.game_id == PG_GAME_MINER)) { // latent mirrors the state
         std::vector<int32_t> lat(PG_LATENT_N, 0);
         lat[0] = s.main_width;
         lat[1] = s.main_height;
@@ -894,8 +907,25 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
         float ax, ay;
         memcpy(&ax, p - PG_NF * ents * 4 + (size_t)F_X * ents * 4, 4); // entity 0 = the agent
         memcpy(&ay, p - PG_NF * ents * 4 + (size_t)F_Y * ents * 4, 4);
-        lat[2 + PG_LATENT_GRID] = ents ? (int)ax : 0;
-        lat[3 + PG_LATENT_GRID] = ents ? (int)ay : 0;
+        if (s.agent_erased) {
+            ax = s.ghost_x;
+            ay = s.ghost_y;
+        }
+        lat[2 + PG_LATENT_GRID] = (ents || s.agent_erased) ? (int)ax : 0;
+        lat[3 + PG_LATENT_GRID] = (ents || s.agent_erased) ? (int)ay : 0;
+        if (s.game_id == PG_GAME_MINER) { // the first EXIT entity (type 6)
+            for (size_t e = 0; e < ents; e++) {
+                int32_t ty;
+                float ex, ey;
+                memcpy(&ty, p - PG_NF * ents * 4 + (size_t)F_TYPE * ents * 4 + e * 4, 4);
+                if (ty != 6) continue;
+                memcpy(&ex, p - PG_NF * ents * 4 + (size_t)F_X * ents * 4 + e * 4, 4);
+                memcpy(&ey, p - PG_NF * ents * 4 + (size_t)F_Y * ents * 4 + e * 4, 4);
+                lat[4 + PG_LATENT_GRID] = (int)ex;
+                lat[5 + PG_LATENT_GRID] = (int)ey;
+                break;
+            }
+        }
         copy_sync(v, v->dev.latent + (size_t)env_idx * PG_LATENT_N, lat.data(), PG_LATENT_N * 4, hipMemcpyHostToDevice);
     }
     p += cells * 2;

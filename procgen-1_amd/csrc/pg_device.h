@@ -63,6 +63,17 @@
 #define HS_KEY 2
 #define HS_EXIT 9
 #define HS_KEY_ON_RING 11
+// miner.cpp:10-23 (fork-modified)
+#define MN_BOULDER 1
+#define MN_DIAMOND 2
+#define MN_MOVING_BOULDER 3
+#define MN_MOVING_DIAMOND 4
+#define MN_ENEMY 5
+#define MN_EXIT 6
+#define MN_DIRT 9
+#define MN_OOB_WALL 10
+#define MN_MUD 11
+#define MN_DEAD_PLAYER 12
 // object-ids.h
 #define EXIT_OBJ 52
 #define AGENT_OBJ 53

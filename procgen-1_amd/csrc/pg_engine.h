@@ -21,7 +21,7 @@
 #define PG_MAX_BG 64
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
-enum PGGame { PG_GAME_BIGFISH = 0, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11 };
+enum PGGame { PG_GAME_BIGFISH = 0, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11, PG_GAME_MINER = 12 };
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
 #endif
@@ -140,7 +140,11 @@ struct PGEnv {
     int32_t world_dim;
     int32_t num_keys;
     int32_t has_keys;         // bit k = has_keys[k]
-    int32_t pad[128 - 74];
+    // ---- miner (miner.cpp:26-28)
+    int32_t diamonds_remaining;
+    int32_t died;
+    int32_t main_area;
+    int32_t pad[128 - 77];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
@@ -168,6 +172,7 @@ struct PGDev {
     uint64_t *prof;           // [num_envs][16] per-phase s_memtime sums (PG_PROFILE builds only)
     // atlas: one pixel array, per-game tables (a kernel of game G sees its own via game_view)
     const uint32_t *pixels;
+    uint32_t num_pixels;        // bound of every texel index the stamping paths form
     const int32_t *sprites;   // [PG_NUM_GAMES][PG_NUM_SLOTS][4] (offset, w, h, pad)
     const int32_t *backgrounds; // [PG_NUM_GAMES][PG_MAX_BG][4]
     int32_t num_backgrounds;    // of the viewed game

@@ -106,6 +106,10 @@ DEV int image_for_type(int type, int player_img) {
         if (type == PLAYER) return player_img;
         if (type == CR_ENEMY_BARRIER) return -1;
     }
+    if constexpr (G == PG_GAME_MINER) { // miner.cpp:95-103
+        if (type == MN_MOVING_BOULDER) return MN_BOULDER;
+        if (type == MN_MOVING_DIAMOND) return MN_DIAMOND;
+    }
     return type < 0 ? -type : type;
 }
 template <int G>
@@ -126,12 +130,16 @@ DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entit
 }
 template <int G>
 DEV bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
-// grid types whose tile image is not TILE_PX square but is drawn as a tile (class 1)
+// every grid tile the game draws is a TILE_PX-square image (the fast path's assumption)
 template <int G>
-DEV bool odd_size_tile(int type) {
-    if constexpr (G == PG_GAME_MAZE) return type == MZ_GOAL; // cheese.png, 27 x 27
-    return false;
-}
+DEV bool uniform_tiles() { return G == PG_GAME_COINRUN || G == PG_GAME_HEIST; }
+// the game has render_z = -1 entities (drawn between background and grid, :933)
+template <int G>
+DEV bool has_z_minus1() { return G == PG_GAME_MINER; } // miner's exit (miner.cpp:217)
+// an image the reference lists but the asset tree lacks (miner's mud.png, resources.cpp:511):
+// drawn as nothing (the reference cannot load it; parity unpinned for MUD tiles)
+template <int G>
+DEV bool missing_image_ok(int img) { return G == PG_GAME_MINER && img == MN_MUD; }
 
 // ------------------------------------------------------------------ rotated drawImage
 // save(); translate(center); rotate(rotation * 180 / PI); drawImage(QRectF(-w/2, -h/2, w, h))
@@ -158,8 +166,8 @@ DEV void trap_setup(const QV &tl, const QV &bl, const QV &tr, const QV &br, doub
 }
 
 // returns false when the transform is not a rotation this path reproduces
-DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, double x, double y, double w, double h, double m11,
-                      double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
+DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
+                      double m11, double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
     if (!(w > 0) || !(h > 0) || iw <= 0 || ih <= 0) return true; // QRectF::isEmpty: nothing drawn
     if (m12 == 0 && m21 == 0) return false;                      // TxScale (rotate(180)): scale path
     const double dx = x + w / 2, dy = y + h / 2;
@@ -172,8 +180,13 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, double x, double y, 
     map(rx, ry, v[0]); map(right, ry, v[1]); map(right, bottom, v[2]); map(rx, bottom, v[3]);
     v[0].u = 0; v[0].v = 0; v[1].u = iw; v[1].v = 0; v[2].u = iw; v[2].v = ih; v[3].u = 0; v[3].v = ih;
     int topmost = 0;
+    double top_y = v[0].y;
+#pragma unroll
     for (int i = 1; i < 4; ++i)
-        if (v[i].y < v[topmost].y) topmost = i;
+        if (v[i].y < top_y) {
+            topmost = i;
+            top_y = v[i].y;
+        }
     QV t;
     if (topmost == 1) {
         t = v[0]; v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = t;
@@ -214,6 +227,7 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, double x, double y, 
         trap_setup(v[1], v[2], v[3], v[2], v[1].y, v[2].y, tr[2]);
     }
     const int lane = LANE;
+#pragma unroll
     for (int k = 0; k < 3; k++) {
         const Trap T = tr[k];
         for (int yy = T.from_y; yy < T.to_y; yy++) {
@@ -225,12 +239,200 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, double x, double y, 
                 uu = min(max(uu, 0), iw - 1);
                 vv = min(max(vv, 0), ih - 1);
                 if (mir) uu = iw - 1 - uu;
-                uint32_t src = pixels[soff + (uint32_t)(vv * iw + uu)];
-                fb[yy * PG_RES + lane] = blend_argb_pm(fb[yy * PG_RES + lane], src, ca);
+                const uint32_t idx = soff + (uint32_t)(vv * iw + uu);
+                if (idx >= npix) return false;
+                fb[yy * PG_RES + lane] = blend_argb_pm(fb[yy * PG_RES + lane], pixels[idx], ca);
             }
         }
     }
     return true;
+}
+
+
+// ------------------------------------------------------------------ in-order image stamping
+// The Qt scale blit of up to 64 images whose geometry lanes computed (lane k <-> image k),
+// applied in ascending lane order.  EG images per group: the texel of this lane's footprint
+// pixel is loaded for every image of the group first (loads are order-free), then the group
+// is blended strictly in order.  Footprints wider than one wave (> 64 px) fall back to an
+// in-order loop with inline loads; rotated images run the transform blit in place.
+struct Img {
+    bool draw, rot;
+    Axis ex, ey;
+    int soff, sw, sh, ca, mir, rslot, ez;
+    double rx, ry, rw, rh; // target rect of a rotated image
+};
+
+DEV void img_clear(Img &im) {
+    im.draw = false;
+    im.rot = false;
+    im.ex.t1 = im.ex.n = im.ey.t1 = im.ey.n = 0;
+    im.ex.base = im.ey.base = 0;
+    im.ex.step = im.ey.step = 0;
+    im.soff = im.sw = im.sh = im.mir = im.rslot = 0;
+    im.ca = 256;
+    im.ez = 0x7fffffff;
+    im.rx = im.ry = im.rw = im.rh = 0;
+}
+
+DEV double readlane_d(double x, int j) {
+    long long b = __builtin_bit_cast(long long, x);
+    int lo = readlane((int)(b & 0xffffffff), j), hi = readlane((int)(b >> 32), j);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long long m, bool &err) {
+    const int lane = LANE;
+    const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
+    const uint32_t npix = d.num_pixels;
+    while (m) {
+        int js[EG];
+#pragma unroll
+        for (int g = 0; g < EG; g++) {
+            js[g] = m ? __ffsll((long long)m) - 1 : -1;
+            if (m) m &= m - 1;
+        }
+        uint32_t tv[EG];
+        int fo[EG];
+        bool on[EG];
+#pragma unroll
+        for (int g = 0; g < EG; g++) {
+            on[g] = false;
+            tv[g] = 0;
+            fo[g] = 0;
+            const int j = js[g];
+            if (j < 0 || readlane(im.rot ? 1 : 0, j)) continue;
+            const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
+            if (nx * ny > 64) continue;
+            if (lane < nx * ny) {
+                const float inv = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, inv_l), j));
+                const int py = (int)(((float)lane + 0.5f) * inv);
+                const int pxx = lane - py * nx;
+                const uint32_t bxj = (uint32_t)readlane((int)im.ex.base, j), byj = (uint32_t)readlane((int)im.ey.base, j);
+                const int sxj = readlane(im.ex.step, j), syj = readlane(im.ey.step, j);
+                const int swj = readlane(im.sw, j);
+                int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
+                const int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
+                if (readlane(im.mir, j)) scol = swj - 1 - scol;
+                const uint32_t idx = (uint32_t)readlane(im.soff, j) + (uint32_t)(srow * swj + scol);
+                const int o = (readlane(im.ey.t1, j) + py) * PG_RES + readlane(im.ex.t1, j) + pxx;
+                if (idx < npix && o >= 0 && o < PG_RES * PG_RES) {
+                    tv[g] = d.pixels[idx];
+                    fo[g] = o;
+                    on[g] = true;
+                } else {
+                    err = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < EG; g++) {
+            const int j = js[g];
+            if (j < 0) continue;
+            const int caj = readlane(im.ca, j);
+            if (readlane(im.rot ? 1 : 0, j)) {
+                const int k = readlane(im.rslot, j);
+                const double *mt = d.rot_table + 4 * k;
+                if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
+                                  readlane_d(im.rh, j), mt[0], mt[1], mt[2], mt[3], (uint32_t)readlane(im.soff, j),
+                                  readlane(im.sw, j), readlane(im.sh, j), readlane(im.mir, j) != 0, caj))
+                    err = true;
+                continue;
+            }
+            const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
+            if (nx * ny <= 64) {
+                if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
+            } else {
+                const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
+                const uint32_t bxj = (uint32_t)readlane((int)im.ex.base, j), byj = (uint32_t)readlane((int)im.ey.base, j);
+                const int sxj = readlane(im.ex.step, j), syj = readlane(im.ey.step, j);
+                const uint32_t offj = (uint32_t)readlane(im.soff, j);
+                const int swj = readlane(im.sw, j), mirj = readlane(im.mir, j);
+                const float inv = 1.0f / (float)nx;
+                for (int p = lane; p < nx * ny; p += 64) {
+                    int py = (int)(((float)p + 0.5f) * inv);
+                    int pxx = p - py * nx;
+                    int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
+                    int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
+                    if (mirj) scol = swj - 1 - scol;
+                    const uint32_t idx = offj + (uint32_t)(srow * swj + scol);
+                    const int o = (ty + py) * PG_RES + tx + pxx;
+                    if (idx < npix && o >= 0 && o < PG_RES * PG_RES) fb[o] = blend_argb_pm(fb[o], d.pixels[idx], caj);
+                    else err = true;
+                }
+            }
+            // no barrier between images: one wave issues its LDS operations in order
+        }
+    }
+}
+
+// Blit geometry of entity i (draw_entity -> get_object_rect -> draw_image, basic-abstract-game.cpp
+// :808-826, 886-922, 1056-1059) into this lane's Img.
+template <int G>
+DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, int i, int n, int player_img, Img &im,
+                      bool &err) {
+    img_clear(im);
+    if (i >= n) return;
+    im.ez = EIr(d, F_RENDER_Z, env, i);
+    float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
+    float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
+    int flags = EIr(d, F_FLAGS, env, i);
+    float alpha = EFr(d, F_ALPHA, env, i);
+    float rotation = EFr(d, F_ROTATION, env, i);
+    int etype = EIr(d, F_TYPE, env, i);
+    int itype = EIr(d, F_IMAGE_TYPE, env, i);
+    int theme = EIr(d, F_IMAGE_THEME, env, i);
+    int img = image_for_type<G>(itype, player_img);
+    if (img < 0 || !should_draw<G>(s, etype, theme)) return;
+    if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+        if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
+        return;
+    }
+    theme = mask_theme<G>(s, theme, img);
+    if (theme < 0 || theme >= 10) {
+        err = true;
+        return;
+    }
+    double rx, ry, rw, rh;
+    if (flags & EF_ABS_COORDS) { // get_abs_rect (:812-814) via get_object_rect (:820-826)
+        float vd = v.view_dim;
+        float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
+        rx = (double)(ax * v.unit); ry = (double)(ay * v.unit);
+        rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
+    } else {
+        screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+    }
+    if constexpr (G == PG_GAME_COINRUN) {
+        if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
+            rx = rx + rw * 0.0;
+            ry = ry + rh * -.7415;
+            rw = rw * 1.0;
+            rh = rh * 1.7415;
+        }
+    }
+    int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+    im.ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
+    im.mir = (flags & EF_REFLECTED) != 0;
+    im.soff = sp.x;
+    im.sw = sp.y;
+    im.sh = sp.z;
+    if (sp.y <= 0) {
+        err = true; // missing image
+    } else if (rotation != 0) {
+        // rotated: the Qt transform blit runs in order when this entity is stamped
+        int rslot = -1;
+        for (int k = 0; k < PG_ROT_N; k++)
+            if (__float_as_uint(d.rot_angles[k]) == __float_as_uint(rotation)) rslot = k;
+        if (rslot < 0) {
+            err = true;
+        } else {
+            im.rslot = rslot;
+            im.draw = true;
+            im.rot = true;
+            im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
+        }
+    } else if (axis_setup(rx, rw, sp.y, im.ex) && axis_setup(ry, rh, sp.z, im.ey)) {
+        im.draw = true;
+    }
 }
 
 } // namespace
@@ -239,19 +441,16 @@ template <int G>
 __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *env_list) {
     const PGDev d = game_view(dg, G);
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
-    // grid type -> sprite pixel offset: >= 0 a TILE_PX x TILE_PX image ("class 0"), -1 draws nothing,
-    // -4 the game's one other tile size ("class 1", offset in tile_off1), <= -2 otherwise unsupported
+    // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
+    // <= -2 not drawable on the fast path
     __shared__ int tile_off[NTYPES];
-    __shared__ int tile_off1[NTYPES];
     // fast path: texel base of lane's first tile column per tile row.  Before it is built, the
     // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row
     // (class 0 at [0, 128), class 1 at [128, 256) in int4 units).
     __shared__ __attribute__((aligned(16))) int colb[CROWS * 64];
-    static_assert(CROWS * 64 >= 4 * 64 * 4, "colb doubles as the axis tables");
+    static_assert(CROWS * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
-    int4 *const colax1 = colax + 128;
-    int4 *const rowax1 = colax + 192;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     const PGEnv s = d.envs[env];
     const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
@@ -287,46 +486,24 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     PTimer pt;
     pt.start();
 
-    // ---- grid type -> sprite table (theme_for_grid_obj, image_for_type, draw_image :886-922)
-    int cls1_w = 0, cls1_h = 0;
-    bool any_cls1 = false;
-    {
-        int my_w = 0, my_h = 0;
-        bool my1 = false;
-        for (int t = lane; t < NTYPES; t += 64) {
-            int off = -1, off1 = 0;
-            int img = image_for_type<G>(t, player_img);
-            if (img >= 0) {
-                if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                    off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
-                } else {
-                    int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
-                    int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                    if (sp.y == TILE_PX && sp.z == TILE_PX) {
-                        off = sp.x;
-                    } else if (sp.y > 0 && sp.z > 0 && odd_size_tile<G>(t)) {
-                        off = -4;
-                        off1 = sp.x;
-                        if (my1 && (my_w != sp.y || my_h != sp.z)) err = true; // one extra size per lane
-                        my1 = true; my_w = sp.y; my_h = sp.z;
-                    } else if (sp.y > 0) {
-                        off = -2; // a tile size this build does not expect for the game (flagged if drawn)
-                    } else {
-                        off = -3; // generated assets: not in this build
-                    }
-                }
+    // ---- grid type -> sprite table for the fast path (theme_for_grid_obj, image_for_type,
+    //      draw_image :886-922): TILE_PX-square tiles only; anything else is drawn by the
+    //      generic tile pass (or flagged when met on the fast path)
+    for (int t = lane; t < NTYPES; t += 64) {
+        int off = -1;
+        int img = image_for_type<G>(t, player_img);
+        if (img >= 0) {
+            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+                off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
+            } else {
+                int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
+                int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                if (sp.y == TILE_PX && sp.z == TILE_PX) off = sp.x;
+                else if (sp.y > 0) off = -2;
+                else off = -3; // generated assets: not in this build
             }
-            tile_off[t] = off;
-            tile_off1[t] = off1;
         }
-        unsigned long long m1 = ballot(my1);
-        any_cls1 = m1 != 0;
-        if (any_cls1) {
-            int l = __ffsll((long long)m1) - 1;
-            cls1_w = readlane(my_w, l);
-            cls1_h = readlane(my_h, l);
-            if (my1 && (my_w != cls1_w || my_h != cls1_h)) err = true;
-        }
+        tile_off[t] = off;
     }
 
     // ---- visible tile window (basic-abstract-game.cpp:937-948)
@@ -365,7 +542,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     }
     if (tab) {
         // one x-axis and one y-axis setup per lane: tile column low_x + lane, tile row
-        // low_y + lane, or (lane 63) the background; class-1 tiles get a second pair
+        // low_y + lane, or (lane 63) the background
         double xr = 0, xw = 0, yr = 0, yh = 0;
         int xiw = 0, yih = 0;
         if (lane == 63) {
@@ -386,13 +563,6 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         const bool oky = axis_setup(yr, yh, yih, b);
         colax[lane] = make_int4(a.t1, okx ? a.n : 0, (int)a.base, a.step);
         rowax[lane] = make_int4(b.t1, oky ? b.n : 0, (int)b.base, b.step);
-        if (any_cls1) {
-            Axis a1, b1;
-            const bool ok1x = lane < 63 && lane < ww && axis_setup(xr, xw, cls1_w, a1);
-            const bool ok1y = lane < 63 && lane < wh && axis_setup(yr, yh, cls1_h, b1);
-            colax1[lane] = ok1x ? make_int4(a1.t1, a1.n, (int)a1.base, a1.step) : make_int4(0, 0, 0, 0);
-            rowax1[lane] = ok1y ? make_int4(b1.t1, b1.n, (int)b1.base, b1.step) : make_int4(0, 0, 0, 0);
-        }
         bg_ok = readlane(okx && oky ? 1 : 0, 63) != 0;
         bx.t1 = readlane(a.t1, 63); bx.n = readlane(a.n, 63); bx.base = (uint32_t)readlane((int)a.base, 63); bx.step = readlane(a.step, 63);
         by.t1 = readlane(b.t1, 63); by.n = readlane(b.n, 63); by.base = (uint32_t)readlane((int)b.base, 63); by.step = readlane(b.step, 63);
@@ -403,78 +573,55 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
     const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
 
-    // Qt axis of tile column x / row y for image size `px` (class 0: TILE_PX, class 1: cls1 size)
-    auto col_axis = [&](int x, int cls, Axis &a) -> bool {
-        if (tab) {
-            const int4 t = (cls ? colax1 : colax)[x - low_x];
-            a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
-            return t.y > 0;
-        }
-        double rx, ry, rw, rh;
-        screen_rect(v, (float)x, 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
-        return axis_setup(rx, rw, cls ? cls1_w : TILE_PX, a);
-    };
-    auto row_axis = [&](int y, int cls, Axis &a) -> bool {
-        if (tab) {
-            const int4 t = (cls ? rowax1 : rowax)[y - low_y];
-            a.t1 = t.x; a.n = t.y; a.base = (uint32_t)t.z; a.step = t.w;
-            return t.y > 0;
-        }
-        double rx, ry, rw, rh;
-        screen_rect(v, 0.0f, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
-        return axis_setup(ry, rh, cls ? cls1_h : TILE_PX, a);
-    };
-    // tile columns covering screen column `lane` (<= 2 per class, ascending x) and their source columns
-    int cx[2][2] = {{0, 0}, {0, 0}}, sc[2][2] = {{0, 0}, {0, 0}}, ncx[2] = {0, 0};
-    int ry[2][2] = {{0, 0}, {0, 0}}, sr[2][2] = {{0, 0}, {0, 0}}, ncy[2] = {0, 0};
-    const int ncls = any_cls1 ? 2 : 1;
-    if (has_grid_tiles<G>()) {
-        const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
-        const int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
-        for (int k = 0; k < ncls; k++) {
-            for (int x = xg - 2; x <= xg + 2; x++) {
-                if (x < low_x || x > high_x || ncx[k] == 2) continue;
-                Axis a;
-                if (col_axis(x, k, a) && lane >= a.t1 && lane < a.t1 + a.n) {
-                    cx[k][ncx[k]] = x;
-                    sc[k][ncx[k]] = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
-                    ncx[k]++;
-                }
-            }
-            // tile rows covering screen row `lane` (ascending y = the reference's draw order)
-            for (int y = yg - 2; y <= yg + 2; y++) {
-                if (y < low_y || y > high_y || ncy[k] == 2) continue;
-                Axis a;
-                if (row_axis(y, k, a) && lane >= a.t1 && lane < a.t1 + a.n) {
-                    ry[k][ncy[k]] = y;
-                    sr[k][ncy[k]] = (int)((a.base + (uint32_t)((lane - a.t1) * a.step)) >> 16);
-                    ncy[k]++;
-                }
+    // fast path eligibility: square TILE_PX tiles only (uniform_tiles), no z = -1 entity
+    // (drawn between background and grid), few tile rows per frame
+    const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
+    const int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
+    int cx0 = 0, cx1 = 0, ncx0 = 0, scol0 = 0, scol1 = 0;
+    int ry0 = 0, ry1 = 0, ncy0 = 0, srow0 = 0, srow1 = 0;
+    int nrows = 0, jy0 = 0;
+    bool fast = false;
+    if (uniform_tiles<G>() && !has_z_minus1<G>() && tab) {
+        // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images
+        for (int x = xg - 2; x <= xg + 2; x++) {
+            if (x < low_x || x > high_x || ncx0 == 2) continue;
+            const int4 t = colax[x - low_x];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) {
+                int scv = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+                if (ncx0 == 0) { cx0 = x; scol0 = scv; } else { cx1 = x; scol1 = scv; }
+                ncx0++;
             }
         }
-    }
-    // class-0 aliases used by the fast path
-    const int cx0 = cx[0][0], cx1 = cx[0][1], scol0 = sc[0][0], scol1 = sc[0][1], ncx0 = ncx[0];
-    const int ry0 = ry[0][0], ry1 = ry[0][1], srow0 = sr[0][0], srow1 = sr[0][1], ncy0 = ncy[0];
-
-    // ---- lookups for the fast path: every screen row's tile rows lie in [jy0, jy1]; for
-    //      each of those rows the texel base of this lane's first tile column goes to LDS
-    //      (colb), so a pixel costs one LDS read + one texel load + one blend.
-    int jlo = ncy0 > 0 ? ry0 : 0x7fffffff, jhi = ncy0 > 1 ? ry1 : (ncy0 > 0 ? ry0 : -0x7fffffff);
+        // tile rows covering screen row `lane` (<= 2, ascending y = the reference's draw order)
+        for (int y = yg - 2; y <= yg + 2; y++) {
+            if (y < low_y || y > high_y || ncy0 == 2) continue;
+            const int4 t = rowax[y - low_y];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) {
+                int srv = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+                if (ncy0 == 0) { ry0 = y; srow0 = srv; } else { ry1 = y; srow1 = srv; }
+                ncy0++;
+            }
+        }
+        int jlo = ncy0 > 0 ? ry0 : 0x7fffffff, jhi = ncy0 > 1 ? ry1 : (ncy0 > 0 ? ry0 : -0x7fffffff);
 #pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) {
-        jlo = min(jlo, __shfl_xor(jlo, sh));
-        jhi = max(jhi, __shfl_xor(jhi, sh));
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            jlo = min(jlo, __shfl_xor(jlo, sh));
+            jhi = max(jhi, __shfl_xor(jhi, sh));
+        }
+        jy0 = jlo;
+        nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
+        fast = nrows <= CROWS;
     }
-    const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
-    const bool fast = has_grid_tiles<G>() && !any_cls1 && nrows <= CROWS;
     auto lookup_grid = [&](int x, int y) -> int {
         int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
                                                                                : s.out_of_bounds_object;
         return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
     };
-    wave_sync(); // tile tables complete
+    wave_sync(); // tile table complete
     if (fast) {
+        // ---- lookups for the fast path: every screen row's tile rows lie in [jy0, jy1]; for
+        //      each of those rows the texel base of this lane's first tile column goes to LDS
+        //      (colb), so a pixel costs one LDS read + one texel load + one blend.
         int code[CROWS];
 #pragma unroll
         for (int j = 0; j < CROWS; j++) {
@@ -485,6 +632,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 else code[j] = s.out_of_bounds_object;
             }
         }
+        wave_sync(); // colb's axis-table contents are dead from here
 #pragma unroll
         for (int j = 0; j < CROWS; j++) {
             if (j < nrows) {
@@ -572,241 +720,91 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
             }
         }
     } else {
-        // ---- generic pixel-centric pass (uncentred / large views, two tile sizes): a pixel
-        //      blends every tile covering it in the reference's x-major / y-minor order.  The
-        //      candidate columns (this lane) and rows (lane = row, broadcast) of both size
-        //      classes are merged; a tile applies when its own class covers the pixel.
-        int xs[4], nxs = 0;
-        for (int k = 0; k < ncls; k++)
-            for (int q = 0; q < ncx[k]; q++) {
-                int xv = cx[k][q];
-                bool dup = false;
-                for (int e = 0; e < nxs; e++) dup = dup || xs[e] == xv;
-                if (!dup) xs[nxs++] = xv;
+        // ---- background alone (lane = column), RB rows per batch
+        const int bgrow = (bg_ok && lane >= by.t1 && lane < by.t1 + by.n)
+                              ? (int)(((by.base + (uint32_t)((lane - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
+                              : -1;
+        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+            uint32_t bgv[RB];
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int br = readlane(bgrow, r0 + k);
+                const bool inb = bg_col && br >= 0;
+                uint32_t px = d.pixels[inb ? bg_col_base + (uint32_t)br : 0u];
+                bgv[k] = inb ? px : 0xff000000u;
             }
-        for (int a = 1; a < nxs; a++) // ascending x
-            for (int b = a; b > 0 && xs[b - 1] > xs[b]; b--) { int t = xs[b]; xs[b] = xs[b - 1]; xs[b - 1] = t; }
-        const int rpack0 = ncy[0] | (ncy[1] << 2);
-        for (int row = 0; row < PG_RES; row++) {
-            uint32_t px;
-            {
-                const bool inb = bg_col && row >= by.t1 && row < by.t1 + by.n;
-                uint32_t srow = (by.base + (uint32_t)((row - by.t1) * by.step)) >> 16;
-                uint32_t bv = d.pixels[inb ? bg_col_base + srow * (uint32_t)bgi.y : 0u];
-                px = inb ? bv : 0xff000000u;
-            }
-            if (has_grid_tiles<G>() && nxs > 0) {
-                const int rp = readlane(rpack0, row);
-                const int n0 = rp & 3, n1 = (rp >> 2) & 3;
-                int ys[2][2], ss[2][2];
-                ys[0][0] = readlane(ry[0][0], row); ys[0][1] = readlane(ry[0][1], row);
-                ss[0][0] = readlane(sr[0][0], row); ss[0][1] = readlane(sr[0][1], row);
-                ys[1][0] = readlane(ry[1][0], row); ys[1][1] = readlane(ry[1][1], row);
-                ss[1][0] = readlane(sr[1][0], row); ss[1][1] = readlane(sr[1][1], row);
-                int yl[4], nyl = 0;
-                for (int q = 0; q < n0; q++) yl[nyl++] = ys[0][q];
-                for (int q = 0; q < n1; q++) {
-                    bool dup = false;
-                    for (int e = 0; e < nyl; e++) dup = dup || yl[e] == ys[1][q];
-                    if (!dup) yl[nyl++] = ys[1][q];
-                }
-                for (int a = 1; a < nyl; a++)
-                    for (int b = a; b > 0 && yl[b - 1] > yl[b]; b--) { int t = yl[b]; yl[b] = yl[b - 1]; yl[b - 1] = t; }
-                for (int xi = 0; xi < nxs; xi++) {
-                    const int x = xs[xi];
-                    for (int yi = 0; yi < nyl; yi++) {
-                        const int y = yl[yi];
-                        int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
-                                                                                               : s.out_of_bounds_object;
-                        if (type == INVALID_OBJ) continue;
-                        int code = (type >= 0 && type < NTYPES) ? tile_off[type] : -2;
-                        if (code == -1) continue;
-                        if (code <= -2 && code != -4) { err = true; continue; }
-                        const int k = code == -4 ? 1 : 0;
-                        int scol = -1, srw = -1;
-                        for (int q = 0; q < ncx[k]; q++)
-                            if (cx[k][q] == x) scol = sc[k][q];
-                        const int nk = k ? n1 : n0;
-                        for (int q = 0; q < nk; q++)
-                            if (ys[k][q] == y) srw = ss[k][q];
-                        if (scol < 0 || srw < 0) continue;
-                        const uint32_t off = k ? (uint32_t)tile_off1[type] : (uint32_t)code;
-                        const int iw = k ? cls1_w : TILE_PX;
-                        const uint32_t t = d.pixels[off + (uint32_t)(srw * iw + scol)];
-                        px = t + BYTE_MUL(px, (~t) >> 24);
-                    }
-                }
-            }
-            fb[row * PG_RES + lane] = px;
+#pragma unroll
+            for (int k = 0; k < RB; k++) fb[(r0 + k) * PG_RES + lane] = bgv[k];
         }
     }
     wave_sync();
 
     pt.mark(1);
-    // ---- entities, render_z 0 then 1, in list order (basic-abstract-game.cpp:966-967, 1061-1075)
+    Img im;
+    img_clear(im);
+    // ---- entities of one render_z, in list order (basic-abstract-game.cpp:1061-1075); one
+    //      setup per 64-entity chunk, reused by every z pass when the list fits one chunk
     const int n = s.num_ents;
-    const bool one_chunk = n <= 64; // blit setups computed once and reused by both z passes
-    bool draw = false, rot = false;
-    int ez = 0;
-    Axis ex, ey;
-    int soff = 0, sw = 0, sh = 0, ca = 256, mir = 0, rslot = 0;
-    double erx = 0, ery = 0, erw = 0, erh = 0;
-    for (int z = 0; z <= 1; z++) {
-        for (int base = 0; base < n; base += 64) {
-            // lane-parallel blit setup of entity base + lane
-            const int i = base + lane;
-            if (!one_chunk || z == 0) {
-                draw = false;
-                rot = false;
-                ez = 0;
-                soff = 0; sw = 0; sh = 0; ca = 256; mir = 0; rslot = 0;
-                if (i < n) {
-                    ez = EIr(d, F_RENDER_Z, env, i);
-                    float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
-                    float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
-                    int flags = EIr(d, F_FLAGS, env, i);
-                    float alpha = EFr(d, F_ALPHA, env, i);
-                    float rotation = EFr(d, F_ROTATION, env, i);
-                    int etype = EIr(d, F_TYPE, env, i);
-                    int itype = EIr(d, F_IMAGE_TYPE, env, i);
-                    int theme = EIr(d, F_IMAGE_THEME, env, i);
-                    int img = image_for_type<G>(itype, player_img);
-                    if (img >= 0 && (ez == 0 || ez == 1) && should_draw<G>(s, etype, theme)) {
+    const bool one_chunk = n <= 64;
+    bool ent_setup_valid = false;
+#define PG_DRAW_ENTITIES(Z)                                                                   \
+    for (int base = 0; base < n; base += 64) {                                                \
+        if (!one_chunk || !ent_setup_valid) entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err); \
+        ent_setup_valid = true;                                                               \
+        stamp_images(fb, d, im, ballot(im.draw && im.ez == (Z)), err);                        \
+    }
+
+    if (!fast) {
+        // ---- z = -1 entities, then the grid tiles in the reference's x-major / y-minor order
+        //      (draw_foreground :930-964), stamped like entities: lane k <-> the k-th tile of
+        //      a 64-tile chunk of the window
+        if (has_z_minus1<G>()) {
+            PG_DRAW_ENTITIES(-1)
+        }
+        if (has_grid_tiles<G>()) {
+            const int ntiles = ww * wh;
+            for (int base = 0; base < ntiles; base += 64) {
+                const int k = base + lane;
+                img_clear(im);
+                if (k < ntiles) {
+                    const int x = low_x + k / wh, y = low_y + k % wh;
+                    int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                           : s.out_of_bounds_object;
+                    int img = type == INVALID_OBJ ? -1 : image_for_type<G>(type, player_img);
+                    if (img >= 0) {
                         if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
                             if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
                         } else {
-                            theme = mask_theme<G>(s, theme, img);
-                            double rx, ry, rw, rh;
-                            if (flags & EF_ABS_COORDS) { // get_abs_rect (:812-814) via get_object_rect (:820-826)
-                                float vd = v.view_dim;
-                                float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
-                                rx = (double)(ax * v.unit); ry = (double)(ay * v.unit);
-                                rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
-                            } else {
-                                screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
-                            }
-                            if constexpr (G == PG_GAME_COINRUN) {
-                                if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
-                                    rx = rx + rw * 0.0;
-                                    ry = ry + rh * -.7415;
-                                    rw = rw * 1.0;
-                                    rh = rh * 1.7415;
-                                }
-                            }
+                            int theme = mask_theme<G>(s, grid_theme<G>(s, type), img);
                             int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                            ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
-                            mir = (flags & EF_REFLECTED) != 0;
-                            soff = sp.x;
-                            sw = sp.y;
-                            sh = sp.z;
                             if (sp.y <= 0) {
-                                err = true;
-                            } else if (rotation != 0) {
-                                // rotated: the Qt transform blit runs in order when this entity is stamped
-                                rslot = -1;
-                                for (int k = 0; k < PG_ROT_N; k++)
-                                    if (__float_as_uint(d.rot_angles[k]) == __float_as_uint(rotation)) rslot = k;
-                                if (rslot < 0) err = true;
-                                else {
-                                    draw = true;
-                                    rot = true;
-                                    erx = rx; ery = ry; erw = rw; erh = rh;
+                                if (!missing_image_ok<G>(img)) err = true;
+                            } else {
+                                double rx, ry, rw, rh;
+                                screen_rect(v, (float)x, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                                if (axis_setup(rx, rw, sp.y, im.ex) && axis_setup(ry, rh, sp.z, im.ey)) {
+                                    im.draw = true;
+                                    im.soff = sp.x;
+                                    im.sw = sp.y;
+                                    im.sh = sp.z;
                                 }
-                            } else if (axis_setup(rx, rw, sp.y, ex) && axis_setup(ry, rh, sp.z, ey)) {
-                                draw = true;
                             }
                         }
                     }
                 }
-            }
-            // Stamp in list order, EG entities per group: the texel of this lane's footprint
-            // pixel is loaded for every entity of the group first (loads are order-free), then
-            // the group is blended into the framebuffer strictly in order.  Footprints wider
-            // than one wave (> 64 px) fall back to an in-order loop with inline loads; rotated
-            // entities run the transform blit at their place in the order.
-            const float inv_l = 1.0f / (float)(draw && !rot ? ex.n : 1);
-            unsigned long long m = ballot(draw && ez == z);
-            while (m) {
-                int js[EG];
-#pragma unroll
-                for (int g = 0; g < EG; g++) {
-                    js[g] = m ? __ffsll((long long)m) - 1 : -1;
-                    if (m) m &= m - 1;
-                }
-                uint32_t tv[EG];
-                int fo[EG];
-                bool on[EG];
-#pragma unroll
-                for (int g = 0; g < EG; g++) {
-                    on[g] = false;
-                    tv[g] = 0;
-                    fo[g] = 0;
-                    const int j = js[g];
-                    if (j < 0 || readlane(rot ? 1 : 0, j)) continue;
-                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
-                    if (nx * ny > 64) continue;
-                    const int p = lane;
-                    if (p < nx * ny) {
-                        const float inv = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, inv_l), j));
-                        const int py = (int)(((float)p + 0.5f) * inv);
-                        const int pxx = p - py * nx;
-                        const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
-                        const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
-                        const int swj = readlane(sw, j);
-                        int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
-                        const int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
-                        if (readlane(mir, j)) scol = swj - 1 - scol;
-                        tv[g] = d.pixels[(uint32_t)readlane(soff, j) + (uint32_t)(srow * swj + scol)];
-                        fo[g] = (readlane(ey.t1, j) + py) * PG_RES + readlane(ex.t1, j) + pxx;
-                        on[g] = true;
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < EG; g++) {
-                    const int j = js[g];
-                    if (j < 0) continue;
-                    const int caj = readlane(ca, j);
-                    if (readlane(rot ? 1 : 0, j)) {
-                        const int k = readlane(rslot, j);
-                        const double *mt = d.rot_table + 4 * k;
-                        auto rld = [&](double x) {
-                            long long b = __builtin_bit_cast(long long, x);
-                            int lo = readlane((int)(b & 0xffffffff), j), hi = readlane((int)(b >> 32), j);
-                            return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-                        };
-                        if (!rotated_blit(fb, d.pixels, rld(erx), rld(ery), rld(erw), rld(erh), mt[0], mt[1], mt[2], mt[3],
-                                          (uint32_t)readlane(soff, j), readlane(sw, j), readlane(sh, j),
-                                          readlane(mir, j) != 0, caj))
-                            err = true;
-                        continue;
-                    }
-                    const int nx = readlane(ex.n, j), ny = readlane(ey.n, j);
-                    if (nx * ny <= 64) {
-                        if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
-                    } else {
-                        const int tx = readlane(ex.t1, j), ty = readlane(ey.t1, j);
-                        const uint32_t bxj = (uint32_t)readlane((int)ex.base, j), byj = (uint32_t)readlane((int)ey.base, j);
-                        const int sxj = readlane(ex.step, j), syj = readlane(ey.step, j);
-                        const uint32_t offj = (uint32_t)readlane(soff, j);
-                        const int swj = readlane(sw, j), mirj = readlane(mir, j);
-                        const float inv = 1.0f / (float)nx;
-                        for (int p = lane; p < nx * ny; p += 64) {
-                            int py = (int)(((float)p + 0.5f) * inv);
-                            int pxx = p - py * nx;
-                            int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
-                            int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
-                            if (mirj) scol = swj - 1 - scol;
-                            uint32_t src = d.pixels[offj + (uint32_t)(srow * swj + scol)];
-                            int o = (ty + py) * PG_RES + tx + pxx;
-                            fb[o] = blend_argb_pm(fb[o], src, caj);
-                        }
-                    }
-                    // no barrier between entities: one wave issues its LDS operations in order
-                }
+                stamp_images(fb, d, im, ballot(im.draw), err);
             }
         }
+    } else if (has_z_minus1<G>()) {
+        err = true; // unreachable: the fast path is never taken with z = -1 entities
     }
+    // ---- entities, render_z 0 then 1 (basic-abstract-game.cpp:966-967)
+    ent_setup_valid = false;
+    PG_DRAW_ENTITIES(0)
+    PG_DRAW_ENTITIES(1)
+#undef PG_DRAW_ENTITIES
     wave_sync();
+
 
     pt.mark(2);
     // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
@@ -838,6 +836,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_BIGFISH)
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
+        PG_CASE(PG_GAME_MINER)
     default: break;
     }
 #undef PG_CASE

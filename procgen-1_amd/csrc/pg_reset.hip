@@ -27,7 +27,13 @@ struct MGScratch {
     uint32_t walls[MG_MAX_WALLS];      // x1 | y1 << 8 | x2 << 16 | y2 << 24, reference push order
     unsigned long long alive[MG_MAX_WALLS / 64];
 };
+struct MinerScratch {
+    int16_t obj_idxs[35 * 35];  // simple_choose result
+    int16_t dirt[35 * 35];      // dirt cells, then exit candidates
+    uint8_t taken[35 * 35];     // simple_choose's std::set
+};
 template <int G> struct Scratch { uint32_t dummy[1]; };
+template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
 template <> struct Scratch<PG_GAME_HEIST> { MGScratch mg; };
 
@@ -140,6 +146,13 @@ DEV void choose_world_dim(RCtx &c) {
         else if (d == PG_MEMORY) c.s.world_dim = 31;
         c.s.main_width = c.s.world_dim;
         c.s.main_height = c.s.world_dim;
+    }
+    if constexpr (G == PG_GAME_MINER) { // miner.cpp:119-132
+        int d = c.s.opt_distribution_mode;
+        if (d == PG_EASY) { c.s.main_width = 10; c.s.main_height = 10; }
+        else if (d == PG_HARD) { c.s.main_width = 20; c.s.main_height = 20; }
+        else if (d == PG_MEMORY) { c.s.main_width = 35; c.s.main_height = 35; }
+        c.s.main_area = c.s.main_width * c.s.main_height;
     }
     if constexpr (G == PG_GAME_HEIST) { // heist.cpp:98-113
         int d = c.s.opt_distribution_mode;
@@ -762,6 +775,92 @@ DEV void heist_game_reset(RCtx &c, MGScratch *scratch) {
     }
 }
 
+// ------------------------------------------------------------------ miner (miner.cpp:134-218)
+DEV void miner_game_reset(RCtx &c, MinerScratch *m) {
+    base_game_reset<PG_GAME_MINER>(c);
+    c.s.died = 0;
+    EF(c, F_RX, 0) = .5f;
+    EF(c, F_RY, 0) = .5f;
+    c.s.opt_center_agent = c.s.opt_distribution_mode == PG_MEMORY;
+    c.s.grid_step = 1;
+    const int w = c.s.main_width, area = c.s.main_area, grid_size = c.s.main_width * c.s.main_height;
+    float diamond_pct = 12 / 400.0f;
+    float boulder_pct = 80 / 400.0f;
+    float mud_pct = 12 / 400.0f;
+    int num_diamonds = (int)(diamond_pct * grid_size);
+    int num_boulders = (int)(boulder_pct * grid_size);
+    int num_mud = (int)(mud_pct * grid_size);
+    const int k = num_diamonds + num_boulders + num_mud + 1;
+    if (area > 35 * 35 || k > area) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    // RandGen::simple_choose(main_area, k) (randgen.cpp:70-88): rejection against a set
+    for (int i = LANE; i < area; i += 64) m->taken[i] = 0;
+    wave_sync();
+    for (int i = 0; i < k; i++) {
+        int next = randn(c, area);
+        while (m->taken[next]) next = randn(c, area);
+        wave_sync();
+        if (LANE == 0) {
+            m->obj_idxs[i] = (int16_t)next;
+            m->taken[next] = 1;
+        }
+        wave_sync();
+    }
+    const int agent_x = m->obj_idxs[0] % w, agent_y = m->obj_idxs[0] / w;
+    EF(c, F_X, 0) = (float)(agent_x + .5);
+    EF(c, F_Y, 0) = (float)(agent_y + .5);
+    for (int i = LANE; i < area; i += 64) c.grid[i] = MN_DIRT;
+    wave_sync();
+    for (int i = LANE; i < k - 1; i += 64) { // distinct cells: order-free
+        int v = i < num_diamonds ? MN_DIAMOND : (i < num_diamonds + num_boulders ? MN_BOULDER : MN_MUD);
+        c.grid[m->obj_idxs[i + 1]] = (int16_t)v;
+    }
+    wave_sync();
+    // get_cells_with_type(DIRT) (basic-abstract-game.cpp:203-213), ascending
+    int nd = 0;
+    for (int base = 0; base < grid_size; base += 64) {
+        int i = base + LANE;
+        bool in = i < grid_size && c.grid[i] == MN_DIRT;
+        unsigned long long b = ballot(in);
+        if (in) m->dirt[nd + __popcll(b & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        nd += __popcll(b);
+    }
+    wave_sync();
+    set_obj(c, agent_x, agent_y, SPACE);
+    for (int i = -1; i <= 1; ++i)
+        for (int j = -1; j <= 1; ++j)
+            if (get_obj(c, agent_x + i, agent_y + j) == MN_BOULDER) set_obj(c, agent_x + i, agent_y + j, MN_DIRT);
+    // exit candidates: dirt cells whose cell above is DIRT or out of bounds (idx-based get_obj)
+    int ne = 0;
+    for (int base = 0; base < nd; base += 64) {
+        int q = base + LANE;
+        bool in = false;
+        int cell = 0;
+        if (q < nd) {
+            cell = m->dirt[q];
+            int above = cell + w;
+            int above_obj = (0 <= above && above < grid_size) ? c.grid[above] : c.s.out_of_bounds_object;
+            in = above_obj == MN_DIRT || above_obj == c.s.out_of_bounds_object;
+        }
+        unsigned long long b = ballot(in);
+        wave_sync(); // compaction writes into the list being read (positions <= reads)
+        if (in) m->dirt[ne + __popcll(b & ((1ull << LANE) - 1ull))] = (int16_t)cell;
+        ne += __popcll(b);
+        wave_sync();
+    }
+    if (ne <= 0) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    const int exit_cell = m->dirt[randn(c, ne)];
+    if (LANE == 0) c.grid[exit_cell] = SPACE;
+    wave_sync();
+    int e = add_entity(c, (float)((exit_cell % w) + .5), (float)((exit_cell / w) + .5), 0, 0, .5f, MN_EXIT);
+    EI(c, F_RENDER_Z, e) = -1;
+}
+
 // ------------------------------------------------------------------ Game::reset
 template <int G>
 DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial) {
@@ -799,6 +898,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_BIGFISH) bigfish_game_reset(c);
     if constexpr (G == PG_GAME_MAZE) maze_game_reset(c, &scratch->mg);
     if constexpr (G == PG_GAME_HEIST) heist_game_reset(c, &scratch->mg);
+    if constexpr (G == PG_GAME_MINER) miner_game_reset(c, &scratch->mn);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -834,9 +934,9 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
         reinterpret_cast<uint4 *>(g8)[i] = make_uint4(w[0], w[1], w[2], w[3]);
     }
     c.s.grid8_ok = ballot(!fits) == 0;
-    if constexpr (G == PG_GAME_MAZE) {
-        // fork latent state (maze.cpp:134-165): grid_size, grid (zero padded), agent_pos; the
-        // step kernel keeps agent_pos and consumed goal cells current
+    if constexpr (G == PG_GAME_MAZE || G == PG_GAME_MINER) {
+        // fork latent state (maze.cpp:134-165, miner.cpp:363-396): grid_size, grid (zero padded),
+        // agent_pos, exit_pos (miner: the exit entity); the step kernel keeps them current
         int32_t *lat = d.latent + (size_t)env * PG_LATENT_N;
         for (int i = LANE; i < PG_LATENT_GRID; i += 64) lat[2 + i] = i < cells ? (int32_t)lds_grid[i] : 0;
         if (LANE == 0) {
@@ -846,6 +946,10 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
             lat[3 + PG_LATENT_GRID] = (int)EF(c, F_Y, 0);
             lat[4 + PG_LATENT_GRID] = 0;
             lat[5 + PG_LATENT_GRID] = 0;
+            if constexpr (G == PG_GAME_MINER) { // the exit is the entity after the agent
+                lat[4 + PG_LATENT_GRID] = (int)EF(c, F_X, 1);
+                lat[5 + PG_LATENT_GRID] = (int)EF(c, F_Y, 1);
+            }
         }
     }
     if (LANE == 0) {
@@ -893,6 +997,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_BIGFISH)
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
+        PG_CASE(PG_GAME_MINER)
     default: break;
     }
 #undef PG_CASE

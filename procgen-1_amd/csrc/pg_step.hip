@@ -21,6 +21,7 @@ struct Ctx {
     int nlist;
     int16_t *slist; // LDS: smart entity indices (fast step_entities path)
     int8_t *grid8;  // LDS copy of the grid
+    uint8_t *moved; // LDS has_moved map (miner)
     bool grid8_ok;
     bool ireg;      // interactors cached per lane (see build_interactor_list)
     int i_idx;
@@ -177,11 +178,17 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
     if (target == c.s.out_of_bounds_object) return true;
     if constexpr (G == PG_GAME_COINRUN)
         if (src_type == PLAYER && cr_is_wall(target)) return true;
+    if constexpr (G == PG_GAME_MINER) // miner.cpp:68-75
+        if (src_type == PLAYER && (target == MN_BOULDER || target == MN_MOVING_BOULDER || target == MN_OOB_WALL))
+            return true;
     return false;
 }
 template <int G>
 DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-509 false
     if constexpr (G == PG_GAME_COINRUN) return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    if constexpr (G == PG_GAME_MINER) // miner.cpp:77-79 (out_of_bounds_object = OOB_WALL)
+        return src == MN_ENEMY && (target == MN_BOULDER || target == MN_DIAMOND || target == MN_MOVING_BOULDER ||
+                                   target == MN_MOVING_DIAMOND || target == MN_OOB_WALL);
     return false;
 }
 
@@ -596,7 +603,7 @@ DEV void set_action_xy(Ctx &c, int move_action) {
         }
     } else {
         c.s.action_vrot = 0;
-        if constexpr (G == PG_GAME_MAZE) // maze.cpp:107-111
+        if constexpr (G == PG_GAME_MAZE || G == PG_GAME_MINER) // maze.cpp:107-111, miner.cpp:105-109
             if (c.s.action_vx != 0) c.s.action_vy = 0;
     }
 }
@@ -674,6 +681,16 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 c.s.fish_eaten += 1;
             }
         }
+    } else if constexpr (G == PG_GAME_MINER) { // miner.cpp:81-93
+        if (t == MN_ENEMY) {
+            c.s.sd_done = 1;
+        } else if (t == MN_EXIT) {
+            if (c.s.diamonds_remaining == 0) {
+                c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+                c.s.sd_level_complete = 1;
+                c.s.sd_done = 1;
+            }
+        }
     } else if constexpr (G == PG_GAME_HEIST) {
         if (t == HS_EXIT) {
             c.s.sd_done = 1;
@@ -742,12 +759,15 @@ DEV void agent_collisions(Ctx &c) {
     } else {
         int upper = c.s.num_ents;
         while (upper > 0) {
-            const float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+            // the reference's `agent` (a ghost once erased from `entities`, miner.cpp:329)
+            const bool gh = c.s.agent_erased;
+            const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+            const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
             int m = -1;
             for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
                 int i = base + LANE;
                 bool hit = false;
-                if (i < upper && EI(c, F_TYPE, i) != PLAYER) { // has_agent_collision (:1135-1140)
+                if (i < upper && EI(c, F_TYPE, i) != PLAYER && (gh || i != 0)) { // has_agent_collision (:1135-1140)
                     float mrg = EF(c, F_COLLISION_MARGIN, i);
                     float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
                     hit = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
@@ -912,9 +932,206 @@ DEV void heist_step_tail(Ctx &c) { // heist.cpp:205-209: agent->face_direction(a
     if (dx != 0 || dy != 0) EF(c, F_ROTATION, 0) = c.d.rot_angles[((int)dx + 1) * 3 + ((int)dy + 1)];
 }
 
+// ------------------------------------------------------------------ miner (games/miner.cpp, fork-modified)
+// The grid lives in LDS (int8, c.grid8) for the whole step and is written back once at the end;
+// has_moved is an LDS byte map (c.moved).
+DEV int mn_get(Ctx &c, int idx) { // get_obj(int idx) (basic-abstract-game.cpp:194-199)
+    if (!(0 <= idx && idx < c.s.main_width * c.s.main_height)) return c.s.out_of_bounds_object;
+    return c.grid8[idx];
+}
+DEV void mn_set(Ctx &c, int idx, int v) {
+    if (LANE == 0) c.grid8[idx] = (int8_t)v;
+    wave_sync();
+}
+DEV void mn_mark(Ctx &c, int idx) {
+    if (LANE == 0) c.moved[idx] = 1;
+    wave_sync();
+}
+DEV float mn_ax(Ctx &c) { return c.s.agent_erased ? c.s.ghost_x : EF(c, F_X, 0); }
+DEV float mn_ay(Ctx &c) { return c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0); }
+DEV int mn_agent_index(Ctx &c) { return (int)mn_ay(c) * c.s.main_width + (int)mn_ax(c); } // miner.cpp:98-100
+DEV int mn_moving(int t) { return t == MN_DIAMOND ? MN_MOVING_DIAMOND : (t == MN_BOULDER ? MN_MOVING_BOULDER : t); }
+DEV bool mn_is_moving(int t) { return t == MN_MOVING_BOULDER || t == MN_MOVING_DIAMOND; }
+DEV int mn_stationary(int t) { return t == MN_MOVING_DIAMOND ? MN_DIAMOND : (t == MN_MOVING_BOULDER ? MN_BOULDER : t); }
+DEV bool mn_is_round(int t) {
+    return t == MN_BOULDER || t == MN_MOVING_BOULDER || t == MN_DIAMOND || t == MN_MOVING_DIAMOND;
+}
+DEV bool mn_is_free(Ctx &c, int idx, int agent_idx) { return mn_get(c, idx) == SPACE && agent_idx != idx; }
+
+// entities.erase(entities.begin()) -- entities[0] is the agent; its shared_ptr lives on (ghost)
+DEV void mn_erase_agent(Ctx &c) {
+    if (c.s.agent_erased || c.s.num_ents <= 0) {
+        c.s.error = PG_ERR_BAD_OPTION;
+        return;
+    }
+    c.s.agent_erased = 1;
+    c.s.ghost_x = EF(c, F_X, 0); c.s.ghost_y = EF(c, F_Y, 0); c.s.ghost_vx = EF(c, F_VX, 0);
+    c.s.ghost_vy = EF(c, F_VY, 0); c.s.ghost_rx = EF(c, F_RX, 0); c.s.ghost_ry = EF(c, F_RY, 0);
+    const int n = c.s.num_ents;
+    for (int base = 1; base < n; base += 64) { // order-preserving shift down by one
+        int i = base + LANE;
+        Ent e;
+        if (i < n) load_ent(c, i, e);
+        wave_sync();
+        if (i < n) store_ent(c, i - 1, e);
+        wave_sync();
+    }
+    c.s.num_ents = n - 1;
+}
+
+// move_cell (miner.cpp:310-346) of one cell, uniform
+DEV void mn_move_cell(Ctx &c, int idx) {
+    const int w = c.s.main_width;
+    const bool current_moved = c.moved[idx] != 0;
+    const int obj = mn_get(c, idx);
+    const int obj_x = idx % w;
+    const int stat_type = mn_stationary(obj);
+    const int agent_idx = mn_agent_index(c);
+    // `BOULDER || DIAMOND && !moved`: && binds tighter
+    if (!(stat_type == MN_BOULDER || (stat_type == MN_DIAMOND && !current_moved))) return;
+    const int below_idx = idx - w;
+    const int below_object = mn_get(c, below_idx);
+    const bool agent_is_below = agent_idx == below_idx;
+    if (below_object == SPACE && !agent_is_below) {
+        const int two_below_obj = mn_get(c, below_idx - w);
+        mn_set(c, idx, SPACE);
+        mn_set(c, below_idx, two_below_obj == SPACE ? mn_moving(obj) : stat_type);
+        mn_mark(c, below_idx);
+    } else if (agent_is_below && mn_is_moving(obj)) {
+        c.s.died = 1;
+        mn_erase_agent(c);
+        mn_set(c, below_idx, MN_DEAD_PLAYER);
+    } else if (mn_is_round(below_object) && obj_x > 0 && mn_is_free(c, idx - 1, agent_idx) &&
+               mn_is_free(c, idx - w - 1, agent_idx)) {
+        mn_set(c, idx, SPACE);
+        mn_set(c, idx - 1, stat_type);
+        mn_mark(c, idx - 1);
+    } else if (mn_is_round(below_object) && obj_x < w - 1 && mn_is_free(c, idx + 1, agent_idx) &&
+               mn_is_free(c, idx - w + 1, agent_idx)) {
+        mn_set(c, idx, SPACE);
+        mn_set(c, idx + 1, stat_type);
+        mn_mark(c, idx + 1);
+    } else {
+        mn_set(c, idx, stat_type);
+    }
+}
+
+// move_cell over rows [y0, y1), x ascending.  Only BOULDER / DIAMOND-like cells act, so a row is
+// a ballot (w <= 35 < 64 lanes) for the next acting cell at or right of the cursor, re-taken
+// after every move (a slide to x + 1 makes that cell act next, as in the reference's loop).
+DEV void mn_move_rows(Ctx &c, int y0, int y1) {
+    const int w = c.s.main_width;
+    for (int y = y0; y < y1; y++) {
+        int xc = 0;
+        while (xc < w) {
+            const int x = xc + LANE;
+            bool act = false;
+            if (LANE < w - xc) {
+                const int idx = x + w * y;
+                const int st = mn_stationary(c.grid8[idx]);
+                act = st == MN_BOULDER || (st == MN_DIAMOND && !c.moved[idx]);
+            }
+            const unsigned long long b = ballot(act);
+            if (!b) break;
+            const int xa = xc + __ffsll((long long)b) - 1;
+            mn_move_cell(c, xa + w * y);
+            xc = xa + 1;
+        }
+    }
+}
+
+DEV void miner_pre_step(Ctx &c) {
+    const int cells = c.s.main_width * c.s.main_height;
+    if (!c.grid8_ok || cells > PG_GRID_MAX) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    for (int i = LANE; i < cells; i += 64) c.moved[i] = 0;
+    wave_sync();
+    // for (int y = 0; y <= agent->y; ++y): int y against the float y
+    int y1 = 0;
+    while (y1 < c.s.main_height && (float)y1 <= mn_ay(c)) y1++;
+    mn_move_rows(c, 0, y1);
+}
+
+DEV void miner_step_tail(Ctx &c) { // miner.cpp:262-307
+    const int w = c.s.main_width, h = c.s.main_height;
+    if (c.s.died) {
+        c.s.sd_done = 1;
+    } else {
+        if (c.s.action_vx > 0) flag_reflected(c, 0, false);
+        if (c.s.action_vx < 0) flag_reflected(c, 0, true);
+        // handle_push (miner.cpp:262-281)
+        const int agent_idx = mn_agent_index(c);
+        const int agentx = agent_idx % w;
+        const float avx = EF(c, F_VX, 0);
+        if (c.s.action_vx == 1 && (avx == 0) && (agentx < w - 2) && mn_get(c, agent_idx + 1) == MN_BOULDER &&
+            mn_get(c, agent_idx + 2) == SPACE) {
+            mn_set(c, agent_idx + 1, SPACE);
+            mn_set(c, agent_idx + 2, MN_BOULDER);
+            mn_mark(c, agent_idx + 2);
+            EF(c, F_X, 0) = EF(c, F_X, 0) + 1;
+        } else if (c.s.action_vx == -1 && (avx == 0) && (agentx > 1) && mn_get(c, agent_idx - 1) == MN_BOULDER &&
+                   mn_get(c, agent_idx - 2) == SPACE) {
+            mn_set(c, agent_idx - 1, SPACE);
+            mn_set(c, agent_idx - 2, MN_BOULDER);
+            mn_mark(c, agent_idx - 2);
+            EF(c, F_X, 0) = EF(c, F_X, 0) - 1;
+        }
+        wave_sync();
+        const int ax = (int)EF(c, F_X, 0), ay = (int)EF(c, F_Y, 0);
+        const int agent_obj = mn_stationary(get_obj(c, ax, ay));
+        if (agent_obj == MN_DIAMOND) c.s.sd_reward += 1.0f; // DIAMOND_REWARD
+        if (agent_obj == MN_DIRT || agent_obj == MN_MUD || agent_obj == MN_DIAMOND) {
+            if (0 <= ax && ax < w && 0 <= ay && ay < h) mn_set(c, ay * w + ax, SPACE);
+            else c.s.error = PG_ERR_GRID;
+        }
+        // for (int y = agent->y + 1; y < main_height; ++y)
+        mn_move_rows(c, (int)(mn_ay(c) + 1), h);
+        int diamonds = 0; // count_diamonds (miner.cpp:348-356)
+        for (int base = 0; base < c.s.main_area; base += 64) {
+            int i = base + LANE;
+            diamonds += __popcll(ballot(i < c.s.main_area && mn_stationary(mn_get(c, i)) == MN_DIAMOND));
+        }
+        c.s.diamonds_remaining = diamonds;
+    }
+    // write the grid back: HBM int16 + its int8 mirror + the fork's latent state (miner.cpp:363-396)
+    const int cells = w * h;
+    int16_t *g = c.d.grid + (size_t)c.env * PG_GRID_MAX;
+    int8_t *g8 = c.d.grid8 + (size_t)c.env * PG_GRID_MAX;
+    int32_t *lat = c.d.latent + (size_t)c.env * PG_LATENT_N;
+    for (int i = LANE; i < cells; i += 64) {
+        const int v = c.grid8[i];
+        g[i] = (int16_t)v;
+        g8[i] = (int8_t)v;
+        if (i < PG_LATENT_GRID) lat[2 + i] = v;
+    }
+    int ex = 0, ey = 0;
+    for (int base = 0; base < c.s.num_ents; base += 64) { // the first EXIT entity
+        int i = base + LANE;
+        unsigned long long b = ballot(i < c.s.num_ents && EI(c, F_TYPE, i) == MN_EXIT);
+        if (b) {
+            int e = base + __ffsll((long long)b) - 1;
+            ex = (int)EF(c, F_X, e);
+            ey = (int)EF(c, F_Y, e);
+            break;
+        }
+    }
+    if (LANE == 0) {
+        lat[0] = w;
+        lat[1] = h;
+        lat[2 + PG_LATENT_GRID] = (int)mn_ax(c);
+        lat[3 + PG_LATENT_GRID] = (int)mn_ay(c);
+        lat[4 + PG_LATENT_GRID] = ex;
+        lat[5 + PG_LATENT_GRID] = ey;
+    }
+}
+
 // ------------------------------------------------------------------ game_step
 template <int G>
 DEV void game_step(Ctx &c) {
+    // miner moves the objects at or below the agent's row before the agent (miner.cpp:250-260)
+    if constexpr (G == PG_GAME_MINER) miner_pre_step(c);
     // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
     uint32_t *rg = c.d.mt + (size_t)c.env * 2 * PG_MT_WORDS;
     c.s.step_rand_int = rg_randint_of(mt_next_global(rg, c.s.rg_mti, c.lds), 0, 1000000);
@@ -931,8 +1148,13 @@ DEV void game_step(Ctx &c) {
     c.s.action_vy = 0;
     set_action_xy<G>(c, c.s.move_action);
     if (c.s.grid_step) {
-        EF(c, F_VX, 0) = c.s.action_vx;
-        EF(c, F_VY, 0) = c.s.action_vy;
+        if (c.s.agent_erased) { // the erased agent's shared_ptr still takes the velocity
+            c.s.ghost_vx = c.s.action_vx;
+            c.s.ghost_vy = c.s.action_vy;
+        } else {
+            EF(c, F_VX, 0) = c.s.action_vx;
+            EF(c, F_VY, 0) = c.s.action_vy;
+        }
     } else {
         update_agent_velocity<G>(c);
         float vrot = EF(c, F_VROT, 0);
@@ -961,6 +1183,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_BIGFISH) bigfish_step_tail(c, rg);
     if constexpr (G == PG_GAME_MAZE) maze_step_tail(c);
     if constexpr (G == PG_GAME_HEIST) heist_step_tail(c);
+    if constexpr (G == PG_GAME_MINER) miner_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -982,8 +1205,10 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
+    __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
     Ctx c;
     c.d = game_view(d, G);
+    c.moved = lds_moved;
     c.env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     c.s = d.envs[c.env];
     c.E = d.ents;
@@ -1055,6 +1280,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         }
         if constexpr (G == PG_GAME_BIGFISH) { PG_W(fish_eaten) }
         if constexpr (G == PG_GAME_HEIST) { PG_W(has_keys) }
+        if constexpr (G == PG_GAME_MINER) { PG_W(diamonds_remaining) PG_W(died) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1075,6 +1301,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_BIGFISH)
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
+        PG_CASE(PG_GAME_MINER)
     default: break;
     }
 #undef PG_CASE

@@ -143,12 +143,27 @@ HEIST_SPRITES = {
     1: ["misc_assets/lock_blue.png", "misc_assets/lock_green.png", "misc_assets/lock_red.png"],
 }
 
+# ---------------------------------------------------------------- miner (fork-modified)
+# procgen/src/games/miner.cpp:50-66 (PLAYER 0, DEAD_PLAYER 12, BOULDER 1, DIAMOND 2, EXIT 6,
+# DIRT 9, MUD 11, OOB_WALL 10).  misc_assets/mud.png is listed (resources.cpp:511) but absent
+# from the reference's asset tree: MUD has no image here (drawn as nothing).
+MINER_SPRITES = {
+    0: ["misc_assets/robot_greenDrive1.png"],
+    12: ["misc_assets/fire_1.png"],
+    1: ["misc_assets/elementStone007.png"],
+    2: ["misc_assets/gemBlue.png"],
+    6: ["misc_assets/window.png"],
+    9: ["misc_assets/dirt.png"],
+    10: ["misc_assets/tile_bricksGrey.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
     "bigfish": (BIGFISH_SPRITES, "water"),      # bigfish.cpp:30-32
     "maze": (MAZE_SPRITES, "topdown"),          # maze.cpp:29-31
     "heist": (HEIST_SPRITES, "topdown"),        # heist.cpp:37-39
+    "miner": (MINER_SPRITES, "caves"),          # miner.cpp:45-47
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -6,7 +6,8 @@ integer-coordinate games (maze, heist); bigfish is the "float tolerance" class (
 radius goes through the double pow of bigfish.cpp:84) -- the test still demands bit-exact
 results and reports any difference with the step and env, so a libm ulp would show up here.
 Heist exercises the rotated-sprite path (agent face_direction, ring keys) and MazeGen with
-doors; maze exercises MazeGen, grid_step movement and the fork's latent-state info.
+doors; maze exercises MazeGen, grid_step movement and the fork's latent-state info; miner
+(fork-modified, miner.cpp) exercises the falling-object passes, agent death and latent state.
 """
 import numpy as np
 import pytest
@@ -62,24 +63,34 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
     return episodes, rewards
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist"])
+LATENT = ("maze", "miner")
+
+
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
 def test_parity_hard_unbounded(game):
-    run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=(game == "maze"))
+    run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
 def test_parity_200_levels_easy(game):
     run_pair(game, 8, 200, seed=2, num_levels=200, start_level=0, rand_seed=5, distribution_mode="easy",
-             latent=(game == "maze"))
+             latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["maze", "heist"])
+@pytest.mark.parametrize("game", ["maze", "heist", "miner"])
 def test_parity_memory_mode_centered(game):
-    # memory mode turns center_agent on in game_reset (maze.cpp:70, heist.cpp:124)
-    run_pair(game, 8, 150, seed=3, num_levels=0, rand_seed=9, distribution_mode="memory", latent=(game == "maze"))
+    # memory mode turns center_agent on in game_reset (maze.cpp:70, heist.cpp:124, miner.cpp:145)
+    run_pair(game, 8, 150, seed=3, num_levels=0, rand_seed=9, distribution_mode="memory", latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist"])
+def test_miner_long_run_deaths():
+    """miner: boulders fall on the agent (death leaves DEAD_PLAYER and ends the episode one step
+    later, miner.cpp:326-330, 256-259), diamonds, exits -- 32 envs x 600 steps."""
+    episodes, rewards = run_pair("miner", 32, 600, seed=8, num_levels=0, rand_seed=4, latent=True)
+    assert episodes > 0
+
+
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
 def test_parity_options(game):
     run_pair(game, 8, 150, seed=4, num_levels=20, rand_seed=3, use_backgrounds=False, restrict_themes=True,
              use_sequential_levels=True)
@@ -92,10 +103,10 @@ def test_bigfish_long_episodes():
 
 def test_mixed_batch_parity():
     """env n plays names[n % 4] (vecgame.cpp:357-358), level seeds from the global index."""
-    names = ["bigfish", "coinrun", "heist", "maze"]
-    num = 16
+    names = ["bigfish", "coinrun", "heist", "maze", "miner"]
+    num = 20
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=21)
-    orcs = [OracleEnv(names[n % 4], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
+    orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
     g = gpu_obs(env)
     for n, o in enumerate(orcs):
         assert_same(g, o.observe(), 0, idx=slice(n, n + 1))
@@ -130,7 +141,7 @@ def test_full_size_sampled_parity(game):
     env.close()
 
 
-@pytest.mark.parametrize("game", ["maze", "heist", "bigfish"])
+@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner"])
 def test_state_roundtrip(game):
     env = make_gpu(4, game, num_levels=20, rand_seed=11)
     rng = np.random.RandomState(1)

@@ -72,3 +72,11 @@ def test_engine_atlas_tables():
             assert (w, h) == (w2, h2)
             np.testing.assert_array_equal(ea.pixels[off:off + w * h], a.pixels[o2:o2 + w * h])
     assert ea.num_backgrounds[catalog.ENV_NAMES.index("maze")] == 9  # topdown group
+
+
+def test_miner_catalog():
+    from procgen_amd import catalog
+    mn = catalog.num_themes("miner")
+    assert mn[0] == mn[1] == mn[2] == mn[6] == mn[9] == mn[10] == mn[12] == 1  # miner.cpp:50-66
+    assert 11 not in catalog.MINER_SPRITES  # mud.png is absent from the reference's assets
+    assert len(catalog.BACKGROUND_GROUPS["caves"]) == 3
