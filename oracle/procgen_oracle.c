@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11, GAME_MINER = 12 };
+enum { GAME_BIGFISH = 0, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11, GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -232,6 +232,9 @@ typedef struct {
     /* miner (miner.cpp:26-28) */
     int diamonds_remaining, main_area;
     bool died;
+    /* climber (climber.cpp:30-36; has_support, facing_right, wall_theme, gravity, air_control shared
+     * with coinrun's members above) */
+    int coin_quota, coins_collected;
     /* observation of the last step */
     uint32_t canvas[RES_W * RES_H];
 } Game;
@@ -340,6 +343,11 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
         if (src->type == PLAYER && cr_is_wall(target)) return true;
         return false;
     }
+    if (g->game_id == GAME_CLIMBER) { /* climber.cpp:147-154: WALL_MID 15, WALL_TOP 16 */
+        if (base) return true;
+        if (src->type == PLAYER && (target == 15 || target == 16)) return true;
+        return false;
+    }
     if (g->game_id == GAME_MINER) { /* miner.cpp:68-75: BOULDER 1, MOVING_BOULDER 3, OOB_WALL 10 */
         if (base) return true;
         if (src->type == PLAYER && (target == 1 || target == 3 || target == 10)) return true;
@@ -385,6 +393,8 @@ static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *targe
 static bool hook_will_reflect(Game *g, int src, int target) {
     if (g->game_id == GAME_COINRUN) /* coinrun.cpp:140-142 */
         return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    if (g->game_id == GAME_CLIMBER) /* climber.cpp:113-115: ENEMY 5 off walls and ENEMY_BARRIER 19 */
+        return src == 5 && (target == 15 || target == 16 || target == 19);
     if (g->game_id == GAME_MINER) /* miner.cpp:77-79: ENEMY 5 off BOULDER, DIAMOND, MOVING_BOULDER/DIAMOND, out of bounds */
         return src == 5 && (target == 1 || target == 2 || target == 3 || target == 4 || target == g->out_of_bounds_object);
     return false;
@@ -406,6 +416,14 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
             }
+        }
+    } else if (g->game_id == GAME_CLIMBER) { /* climber.cpp:93-103: ENEMY 5, COIN 1 */
+        if (obj->type == 5) {
+            g->sd_done = true;
+        } else if (obj->type == 1) {
+            g->sd_reward += 1.0f; /* COIN_REWARD */
+            g->coins_collected += 1;
+            obj->will_erase = true;
         }
     } else if (g->game_id == GAME_MINER) { /* miner.cpp:81-93: ENEMY 5, EXIT 6 */
         if (obj->type == 5) {
@@ -473,6 +491,16 @@ static int hook_image_for_type(Game *g, int type) {
             return -1;
         }
     }
+    if (g->game_id == GAME_CLIMBER) { /* climber.cpp:156-170 */
+        if (type == PLAYER) {
+            Entity *agent = AG(g);
+            if (!g->has_support) return 9; /* PLAYER_JUMP */
+            if (fabsf(agent->vx) < .01 && g->action_vx == 0 && g->has_support) return PLAYER;
+            return (g->cur_time / 5 % 2 == 0 || !g->has_support) ? 12 : 13;
+        } else if (type == 19) {
+            return -1;
+        }
+    }
     if (g->game_id == GAME_MINER) { /* miner.cpp:95-103: MOVING_BOULDER -> BOULDER, MOVING_DIAMOND -> DIAMOND */
         if (type == 3) return 1;
         if (type == 4) return 2;
@@ -481,8 +509,8 @@ static int hook_image_for_type(Game *g, int type) {
 }
 
 static int hook_theme_for_grid_obj(Game *g, int type) {
-    if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:133-138 */
-        if (cr_is_wall(type)) return g->wall_theme;
+    if (g->game_id == GAME_COINRUN || g->game_id == GAME_CLIMBER) { /* coinrun.cpp:133-138, climber.cpp:106-111 */
+        if (type == 15 || type == 16) return g->wall_theme;
         return 0;
     }
     return 0;
@@ -668,9 +696,31 @@ static void coinrun_set_action_xy(Game *g, int move_action) { /* coinrun.cpp:451
     }
 }
 
+static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299-318 */
+    g->action_vx = (float)(move_action / 3 - 1);
+    g->action_vy = (float)((move_action % 3) - 1);
+    if (g->action_vy < 0) g->action_vy = 0;
+    if (g->action_vx > 0) g->facing_right = true;
+    if (g->action_vx < 0) g->facing_right = false;
+    Entity *agent = AG(g);
+    int obj_below_1 = get_obj_from_floats(g, (float)((double)agent->x - ((double)agent->rx - .01)),
+                                          (float)((double)agent->y - ((double)agent->ry + .01)));
+    int obj_below_2 = get_obj_from_floats(g, (float)((double)agent->x + ((double)agent->rx - .01)),
+                                          (float)((double)agent->y - ((double)agent->ry + .01)));
+#define CAN_SUPPORT(o) ((o) == 15 || (o) == 16 || (o) == g->out_of_bounds_object) /* :295-297 */
+    g->has_support = CAN_SUPPORT(obj_below_1) || CAN_SUPPORT(obj_below_2);
+#undef CAN_SUPPORT
+    if (g->has_support && g->action_vy == 1) g->action_vy = 1;
+    else g->action_vy = 0;
+}
+
 static void set_action_xy(Game *g, int move_action) {
     if (g->game_id == GAME_COINRUN) {
         coinrun_set_action_xy(g, move_action);
+        return;
+    }
+    if (g->game_id == GAME_CLIMBER) {
+        climber_set_action_xy(g, move_action);
         return;
     }
     g->action_vx = (float)(move_action / 3 - 1); /* basic-abstract-game.cpp:667-671 */
@@ -701,6 +751,15 @@ static void update_agent_velocity(Game *g) {
         if (!(g->has_support && g->action_vy > 0)) {
             agent->vy -= g->gravity;
             agent->vy = clip_abs(agent->vy, g->max_jump);
+        }
+        return;
+    }
+    if (g->game_id == GAME_CLIMBER) { /* climber.cpp:117-128 */
+        float mixrate_x = g->has_support ? g->mixrate : (g->mixrate * g->air_control);
+        agent->vx = (1 - mixrate_x) * agent->vx + mixrate_x * g->maxspeed * g->action_vx;
+        if (g->action_vy > 0) agent->vy = g->max_jump;
+        if (!g->has_support) {
+            if (agent->vy > -2) agent->vy -= g->gravity;
         }
         return;
     }
@@ -1620,6 +1679,127 @@ static void miner_game_step(Game *g) { /* :250-308 */
     g->diamonds_remaining = diamonds;
 }
 
+/* ================================================================== climber (games/climber.cpp) */
+#define CL_COIN 1
+#define CL_ENEMY 5
+#define CL_ENEMY1 6
+#define CL_ENEMY2 7
+#define CL_PLAYER_JUMP 9
+#define CL_PLAYER_RIGHT1 12
+#define CL_PLAYER_RIGHT2 13
+#define CL_WALL_MID 15
+#define CL_WALL_TOP 16
+#define CL_ENEMY_BARRIER 19
+static const float CL_PATROL_RANGE = 4;
+static bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; } /* :139-141 */
+
+static void climber_choose_world_dim(Game *g) { /* :263-266 */
+    g->main_width = g->options.distribution_mode == EasyMode ? 16 : 20;
+    g->main_height = 64;
+}
+
+static int cl_choose_delta_y(Game *g) { /* :171-176 */
+    int max_dy = (int)(g->max_jump * g->max_jump / (2 * g->gravity));
+    int min_dy = 3;
+    return rg_randn(&g->rand_gen, max_dy - min_dy + 1) + min_dy;
+}
+
+static void cl_generate_platforms(Game *g, const or_atlas *at) { /* :178-232 */
+    MT *r = &g->rand_gen;
+    int difficulty = rg_randn(r, 3);
+    int min_platforms = difficulty * difficulty + 1;
+    int max_platforms = (difficulty + 1) * (difficulty + 1) + 1;
+    int num_platforms = rg_randn(r, max_platforms - min_platforms + 1) + min_platforms;
+    g->coin_quota = 0;
+    g->coins_collected = 0;
+    int curr_x = rg_randn(r, g->main_width - 4) + 2;
+    int curr_y = 0;
+    int margin_x = 3;
+    float enemy_prob = g->options.distribution_mode == EasyMode ? .2f : .5f;
+    for (int i = 0; i < num_platforms; i++) {
+        int delta_y = cl_choose_delta_y(g);
+        bool can_spawn_enemy = (curr_x >= margin_x) && (curr_x <= g->main_width - margin_x);
+        if (can_spawn_enemy && ((double)rg_rand01(r) < (double)enemy_prob)) {
+            /* add_entity(curr_x + .5, curr_y + randn(2) + 2 + .5, .15 * (randn(2) * 2 - 1), ...): g++
+             * evaluates the arguments right to left, so the vx draw comes first (pinned by
+             * oracle/ref_harness.cpp ref_climber_enemy_args) */
+            int vdraw = rg_randn(r, 2);
+            int ydraw = rg_randn(r, 2);
+            int e = add_entity(g, (float)(curr_x + .5), (float)(curr_y + ydraw + 2 + .5), (float)(.15 * (vdraw * 2 - 1)), 0,
+                               .5f, CL_ENEMY);
+            Entity *ent = &g->ents[e];
+            ent->image_type = CL_ENEMY1;
+            ent->smart_step = true;
+            ent->climber_spawn_x = (float)(curr_x + .5);
+            match_aspect_ratio(g, at, ent);
+        }
+        curr_y += delta_y;
+        int plat_len = 2 + rg_randn(r, 10);
+        int vx = rg_randn(r, 2) * 2 - 1;
+        if (curr_x < margin_x) vx = 1;
+        if (curr_x > g->main_width - margin_x) vx = -1;
+        int candidates[16], nc = 0;
+        for (int j = 0; j < plat_len; j++) {
+            int nx = curr_x + (j + 1) * vx;
+            if (nx <= 0 || nx >= g->main_width - 1) break;
+            candidates[nc++] = nx;
+            set_obj(g, nx, curr_y, CL_WALL_TOP);
+        }
+        fassert(nc > 0);
+        if ((double)rg_rand01(r) < .5 || i == num_platforms - 1) {
+            int coin_x = candidates[rg_randn(r, nc)];
+            add_entity(g, (float)(coin_x + .5), (float)(curr_y + 1.5), 0, 0, 0.3f, CL_COIN);
+            g->coin_quota += 1;
+        }
+        curr_x = candidates[rg_randn(r, nc)];
+    }
+}
+
+static void climber_game_reset(Game *g, const or_atlas *at) { /* :268-288 */
+    climber_choose_world_dim(g);
+    basic_game_reset(g, at);
+    g->gravity = 0.2f;
+    g->max_jump = 1.5f;
+    g->air_control = 0.15f;
+    g->maxspeed = .5f;
+    g->has_support = false;
+    g->facing_right = true;
+    Entity *agent = AG(g);
+    agent->rx = .5f;
+    agent->ry = .5f;
+    agent->x = 1 + agent->rx;
+    agent->y = 1 + agent->ry;
+    choose_random_theme(g, agent, at);
+    g->wall_theme = rg_randn(&g->rand_gen, 4); /* NUM_WALL_THEMES */
+    /* init_floor_and_walls (:164-169) */
+    fill_elem(g, 0, 0, g->main_width, 1, CL_WALL_TOP);
+    fill_elem(g, 0, 0, 1, g->main_height, CL_WALL_MID);
+    fill_elem(g, g->main_width - 1, 0, 1, g->main_height, CL_WALL_MID);
+    fill_elem(g, 0, g->main_height - 1, g->main_width, 1, CL_WALL_MID);
+    cl_generate_platforms(g, at);
+}
+
+static void climber_game_step(Game *g) { /* :320-346 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *ent = &g->ents[i];
+        if (ent->type == CL_ENEMY) {
+            if (ent->x > ent->climber_spawn_x + CL_PATROL_RANGE) ent->vx = -1 * fabsf(ent->vx);
+            else if (ent->x < ent->climber_spawn_x - CL_PATROL_RANGE) ent->vx = fabsf(ent->vx);
+            ent->image_type = g->cur_time / 5 % 2 == 0 ? CL_ENEMY1 : CL_ENEMY2;
+            ent->is_reflected = ent->vx < 0;
+        }
+    }
+    if (g->coin_quota == g->coins_collected) {
+        g->sd_done = true;
+        g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+        g->sd_level_complete = true;
+    }
+}
+
 /* ================================================================== Game (game.cpp) */
 static void game_reset_dispatch(Game *g, const or_atlas *at) {
     if (g->game_id == GAME_COINRUN) coinrun_game_reset(g, at);
@@ -1627,6 +1807,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_MAZE) maze_game_reset(g, at);
     else if (g->game_id == GAME_HEIST) heist_game_reset(g, at);
     else if (g->game_id == GAME_MINER) miner_game_reset(g, at);
+    else if (g->game_id == GAME_CLIMBER) climber_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -1635,6 +1816,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_MAZE) maze_game_step(g);
     else if (g->game_id == GAME_HEIST) heist_game_step(g);
     else if (g->game_id == GAME_MINER) miner_game_step(g);
+    else if (g->game_id == GAME_CLIMBER) climber_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -2008,8 +2190,14 @@ static void prepare_for_drawing(Game *g, float rect_height) { /* :828-847 */
     g->center_y = (float)(g->main_height * .5);
     if (g->options.center_agent) {
         Entity *agent = AG(g); /* choose_center, :673-676 */
-        g->center_x = agent->x;
-        g->center_y = agent->y;
+        if (g->game_id == GAME_CLIMBER) { /* climber.cpp:291-295 */
+            g->center_x = (float)(g->main_width / 2.0);
+            g->center_y = (float)((double)agent->y + g->main_width / 2.0 - (double)(5 * agent->ry));
+            g->visibility = (float)g->main_width;
+        } else {
+            g->center_x = agent->x;
+            g->center_y = agent->y;
+        }
     } else {
         g->visibility = (float)(g->main_width > g->main_height ? g->main_width : g->main_height);
         if (g->visibility < g->min_visibility) g->visibility = g->min_visibility;
@@ -2153,6 +2341,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "maze") == 0) return GAME_MAZE;
     if (strcmp(name, "heist") == 0) return GAME_HEIST;
     if (strcmp(name, "miner") == 0) return GAME_MINER;
+    if (strcmp(name, "climber") == 0) return GAME_CLIMBER;
     return -1;
 }
 
@@ -2200,6 +2389,9 @@ static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
     g->has_useful_vel_info = false;
     g->out_of_bounds_object = WALL_OBJ;
     g->visibility = 8.0f;
+}
+static void climber_ctor(Game *g) { /* climber.cpp:38-41 */
+    g->out_of_bounds_object = CL_WALL_MID;
 }
 static void miner_ctor(Game *g) { /* miner.cpp:30-43 */
     g->main_width = 20;
@@ -2254,6 +2446,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_MAZE) maze_ctor(g);
         else if (gid == GAME_HEIST) heist_ctor(g);
         else if (gid == GAME_MINER) miner_ctor(g);
+        else if (gid == GAME_CLIMBER) climber_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

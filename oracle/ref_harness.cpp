@@ -9,6 +9,8 @@
 // (see oracle/procgen_oracle.h).
 #include <cstdint>
 #include <cstring>
+#include <memory>
+#include <vector>
 #include "randgen.h"
 #include "entity.h"
 #include "mazegen.h"
@@ -79,4 +81,35 @@ int ref_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_o
     *next_draw = (uint32_t)r.randint();
     return n;
 }
+
+// Argument evaluation order of the reference's compiler for a call with two RNG draws in its
+// arguments (climber.cpp:196: add_entity(curr_x + .5, curr_y + randn(2) + 2 + .5,
+// .15 * (randn(2) * 2 - 1), 0, .5, ENEMY)), compiled here with the same g++ and flags as the
+// reference pins.  Writes y, vx of the entity for curr_x = 3, curr_y = 0 after seed(seed).
+namespace {
+struct ProbeEnt {
+    float x, y, vx, vy, r;
+    int type;
+    ProbeEnt(float a, float b, float c, float d, float e, int t) : x(a), y(b), vx(c), vy(d), r(e), type(t) {}
+};
+struct ProbeGame {
+    RandGen rand_gen;
+    std::vector<std::shared_ptr<ProbeEnt>> entities;
+    std::shared_ptr<ProbeEnt> add_entity(float x, float y, float vx, float vy, float r, int type) {
+        std::shared_ptr<ProbeEnt> e(new ProbeEnt(x, y, vx, vy, r, type));
+        entities.push_back(e);
+        return e;
+    }
+};
+} // namespace
+
+void ref_climber_enemy_args(int32_t seed, float *out) {
+    ProbeGame g;
+    g.rand_gen.seed(seed);
+    int curr_x = 3, curr_y = 0;
+    auto ent = g.add_entity(curr_x + .5, curr_y + g.rand_gen.randn(2) + 2 + .5, .15 * (g.rand_gen.randn(2) * 2 - 1), 0, .5, 5);
+    out[0] = ent->y;
+    out[1] = ent->vx;
 }
+}
+

@@ -112,9 +112,10 @@ int game_id(const std::string &name) {
     if (name == "maze") return PG_GAME_MAZE;
     if (name == "heist") return PG_GAME_HEIST;
     if (name == "miner") return PG_GAME_MINER;
+    if (name == "climber") return PG_GAME_CLIMBER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, coinrun, heist, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, climber, coinrun, heist, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -169,6 +170,8 @@ void construct_env(PGEnv &s, int gid) {
         s.has_useful_vel_info = 0;
         s.out_of_bounds_object = 51; // WALL_OBJ
         s.visibility = 8.0f;
+    } else if (gid == PG_GAME_CLIMBER) { // climber.cpp:38-41
+        s.out_of_bounds_object = 15; // WALL_MID
     } else if (gid == PG_GAME_MINER) { // miner.cpp:30-43
         s.main_width = 20;
         s.main_height = 20;

@@ -74,6 +74,18 @@
 #define MN_OOB_WALL 10
 #define MN_MUD 11
 #define MN_DEAD_PLAYER 12
+// climber.cpp:12-26
+#define CL_COIN 1
+#define CL_ENEMY 5
+#define CL_ENEMY1 6
+#define CL_ENEMY2 7
+#define CL_PLAYER_JUMP 9
+#define CL_PLAYER_RIGHT1 12
+#define CL_PLAYER_RIGHT2 13
+#define CL_WALL_MID 15
+#define CL_WALL_TOP 16
+#define CL_ENEMY_BARRIER 19
+DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 // object-ids.h
 #define EXIT_OBJ 52
 #define AGENT_OBJ 53

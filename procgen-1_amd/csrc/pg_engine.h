@@ -21,7 +21,9 @@
 #define PG_MAX_BG 64
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
-enum PGGame { PG_GAME_BIGFISH = 0, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11, PG_GAME_MINER = 12 };
+enum PGGame {
+    PG_GAME_BIGFISH = 0, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11, PG_GAME_MINER = 12
+};
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
 #endif
@@ -144,7 +146,10 @@ struct PGEnv {
     int32_t diamonds_remaining;
     int32_t died;
     int32_t main_area;
-    int32_t pad[128 - 77];
+    // ---- climber (climber.cpp:30-36; the platformer members are shared with coinrun)
+    int32_t coin_quota;
+    int32_t coins_collected;
+    int32_t pad[128 - 79];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

@@ -94,6 +94,11 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 // whole frame and hides ENEMY_BARRIER
 template <int G>
 DEV int player_image(const PGEnv &s, float agent_vx) {
+    if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:156-166
+        if (!s.has_support) return CL_PLAYER_JUMP;
+        if (fabsf(agent_vx) < .01 && s.action_vx == 0 && s.has_support) return PLAYER;
+        return (s.cur_time / 5 % 2 == 0 || !s.has_support) ? CL_PLAYER_RIGHT1 : CL_PLAYER_RIGHT2;
+    }
     if constexpr (G == PG_GAME_COINRUN)
         return (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
                    ? PLAYER
@@ -102,7 +107,7 @@ DEV int player_image(const PGEnv &s, float agent_vx) {
 }
 template <int G>
 DEV int image_for_type(int type, int player_img) {
-    if constexpr (G == PG_GAME_COINRUN) {
+    if constexpr (G == PG_GAME_COINRUN || G == PG_GAME_CLIMBER) { // ENEMY_BARRIER is 19 in both
         if (type == PLAYER) return player_img;
         if (type == CR_ENEMY_BARRIER) return -1;
     }
@@ -115,6 +120,7 @@ DEV int image_for_type(int type, int player_img) {
 template <int G>
 DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cpp:133-138)
     if constexpr (G == PG_GAME_COINRUN) return cr_is_wall(type) ? s.wall_theme : 0;
+    if constexpr (G == PG_GAME_CLIMBER) return cl_is_wall(type) ? s.wall_theme : 0; // climber.cpp:106-111
     return 0;
 }
 template <int G>
@@ -469,9 +475,16 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     v.center_x = (float)(s.main_width * .5);
     v.center_y = (float)(s.main_height * .5);
     v.visibility = s.visibility;
-    if (s.opt_center_agent) {
-        v.center_x = agent_x;
-        v.center_y = agent_y;
+    if (s.opt_center_agent) { // choose_center (:673-676; climber.cpp:291-295)
+        if constexpr (G == PG_GAME_CLIMBER) {
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
+            v.visibility = (float)s.main_width;
+        } else {
+            v.center_x = agent_x;
+            v.center_y = agent_y;
+        }
     } else {
         v.visibility = (float)(s.main_width > s.main_height ? s.main_width : s.main_height);
         if (v.visibility < s.min_visibility) v.visibility = s.min_visibility;
@@ -837,6 +850,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
+        PG_CASE(PG_GAME_CLIMBER)
     default: break;
     }
 #undef PG_CASE

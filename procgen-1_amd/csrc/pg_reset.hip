@@ -147,6 +147,10 @@ DEV void choose_world_dim(RCtx &c) {
         c.s.main_width = c.s.world_dim;
         c.s.main_height = c.s.world_dim;
     }
+    if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:263-266
+        c.s.main_width = c.s.opt_distribution_mode == PG_EASY ? 16 : 20;
+        c.s.main_height = 64;
+    }
     if constexpr (G == PG_GAME_MINER) { // miner.cpp:119-132
         int d = c.s.opt_distribution_mode;
         if (d == PG_EASY) { c.s.main_width = 10; c.s.main_height = 10; }
@@ -861,6 +865,79 @@ DEV void miner_game_reset(RCtx &c, MinerScratch *m) {
     EI(c, F_RENDER_Z, e) = -1;
 }
 
+// ------------------------------------------------------------------ climber (climber.cpp:164-288)
+DEV void climber_game_reset(RCtx &c) {
+    base_game_reset<PG_GAME_CLIMBER>(c);
+    c.s.gravity = 0.2f;
+    c.s.max_jump = 1.5f;
+    c.s.air_control = 0.15f;
+    c.s.maxspeed = .5f;
+    c.s.has_support = 0;
+    c.s.facing_right = 1;
+    EF(c, F_RX, 0) = .5f;
+    EF(c, F_RY, 0) = .5f;
+    EF(c, F_X, 0) = 1 + .5f;
+    EF(c, F_Y, 0) = 1 + .5f;
+    choose_random_theme(c, 0);
+    c.s.wall_theme = randn(c, 4); // NUM_WALL_THEMES
+    const int w = c.s.main_width, h = c.s.main_height;
+    fill_elem(c, 0, 0, w, 1, CL_WALL_TOP); // init_floor_and_walls (:164-169)
+    fill_elem(c, 0, 0, 1, h, CL_WALL_MID);
+    fill_elem(c, w - 1, 0, 1, h, CL_WALL_MID);
+    fill_elem(c, 0, h - 1, w, 1, CL_WALL_MID);
+    // generate_platforms (:178-232)
+    int difficulty = randn(c, 3);
+    int min_platforms = difficulty * difficulty + 1;
+    int max_platforms = (difficulty + 1) * (difficulty + 1) + 1;
+    int num_platforms = randn(c, max_platforms - min_platforms + 1) + min_platforms;
+    c.s.coin_quota = 0;
+    c.s.coins_collected = 0;
+    int curr_x = randn(c, w - 4) + 2;
+    int curr_y = 0;
+    const int margin_x = 3;
+    float enemy_prob = c.s.opt_distribution_mode == PG_EASY ? .2f : .5f;
+    for (int i = 0; i < num_platforms; i++) {
+        int max_dy = (int)(c.s.max_jump * c.s.max_jump / (2 * c.s.gravity)); // choose_delta_y (:171-176)
+        int delta_y = randn(c, max_dy - 3 + 1) + 3;
+        bool can_spawn_enemy = (curr_x >= margin_x) && (curr_x <= w - margin_x);
+        if (can_spawn_enemy && (rand01(c) < enemy_prob)) {
+            // g++ evaluates add_entity's arguments right to left: the vx draw comes first
+            // (pinned, tests/test_oracle_pins.py::test_argument_evaluation_order_pinned)
+            int vdraw = randn(c, 2);
+            int ydraw = randn(c, 2);
+            int e = add_entity(c, (float)(curr_x + .5), (float)(curr_y + ydraw + 2 + .5), (float)(.15 * (vdraw * 2 - 1)), 0,
+                               .5f, CL_ENEMY);
+            EI(c, F_IMAGE_TYPE, e) = CL_ENEMY1;
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_SMART_STEP;
+            EF(c, F_CLIMBER_SPAWN_X, e) = (float)(curr_x + .5);
+            match_aspect_ratio<PG_GAME_CLIMBER>(c, e);
+        }
+        curr_y += delta_y;
+        int plat_len = 2 + randn(c, 10);
+        int vx = randn(c, 2) * 2 - 1;
+        if (curr_x < margin_x) vx = 1;
+        if (curr_x > w - margin_x) vx = -1;
+        int nc = 0;
+        for (int j = 0; j < plat_len; j++) {
+            int nx = curr_x + (j + 1) * vx;
+            if (nx <= 0 || nx >= w - 1) break;
+            nc++;
+            set_obj(c, nx, curr_y, CL_WALL_TOP);
+        }
+        if (nc <= 0) {
+            c.s.error = PG_ERR_GRID;
+            return;
+        }
+        // candidates[k] = curr_x + (k + 1) * vx
+        if ((double)rand01(c) < .5 || i == num_platforms - 1) {
+            int coin_x = curr_x + (randn(c, nc) + 1) * vx;
+            add_entity(c, (float)(coin_x + .5), (float)(curr_y + 1.5), 0, 0, 0.3f, CL_COIN);
+            c.s.coin_quota += 1;
+        }
+        curr_x = curr_x + (randn(c, nc) + 1) * vx;
+    }
+}
+
 // ------------------------------------------------------------------ Game::reset
 template <int G>
 DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial) {
@@ -899,6 +976,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_MAZE) maze_game_reset(c, &scratch->mg);
     if constexpr (G == PG_GAME_HEIST) heist_game_reset(c, &scratch->mg);
     if constexpr (G == PG_GAME_MINER) miner_game_reset(c, &scratch->mn);
+    if constexpr (G == PG_GAME_CLIMBER) climber_game_reset(c);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -998,6 +1076,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
+        PG_CASE(PG_GAME_CLIMBER)
     default: break;
     }
 #undef PG_CASE

@@ -178,6 +178,8 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
     if (target == c.s.out_of_bounds_object) return true;
     if constexpr (G == PG_GAME_COINRUN)
         if (src_type == PLAYER && cr_is_wall(target)) return true;
+    if constexpr (G == PG_GAME_CLIMBER) // climber.cpp:147-154
+        if (src_type == PLAYER && cl_is_wall(target)) return true;
     if constexpr (G == PG_GAME_MINER) // miner.cpp:68-75
         if (src_type == PLAYER && (target == MN_BOULDER || target == MN_MOVING_BOULDER || target == MN_OOB_WALL))
             return true;
@@ -186,6 +188,8 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
 template <int G>
 DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-509 false
     if constexpr (G == PG_GAME_COINRUN) return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    if constexpr (G == PG_GAME_CLIMBER) // climber.cpp:113-115
+        return src == CL_ENEMY && (cl_is_wall(target) || target == CL_ENEMY_BARRIER);
     if constexpr (G == PG_GAME_MINER) // miner.cpp:77-79 (out_of_bounds_object = OOB_WALL)
         return src == MN_ENEMY && (target == MN_BOULDER || target == MN_DIAMOND || target == MN_MOVING_BOULDER ||
                                    target == MN_MOVING_DIAMOND || target == MN_OOB_WALL);
@@ -601,6 +605,17 @@ DEV void set_action_xy(Ctx &c, int move_action) {
         if (c.s.action_vy == 1) {
             if (!c.s.has_support) c.s.action_vy = 0;
         }
+    } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:299-318
+        if (c.s.action_vy < 0) c.s.action_vy = 0;
+        if (c.s.action_vx > 0) c.s.facing_right = 1;
+        if (c.s.action_vx < 0) c.s.facing_right = 0;
+        float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+        int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        bool s1 = cl_is_wall(b1) || b1 == c.s.out_of_bounds_object; // can_support (:295-297)
+        bool s2 = cl_is_wall(b2) || b2 == c.s.out_of_bounds_object;
+        c.s.has_support = s1 || s2;
+        c.s.action_vy = (c.s.has_support && c.s.action_vy == 1) ? 1.0f : 0.0f;
     } else {
         c.s.action_vrot = 0;
         if constexpr (G == PG_GAME_MAZE || G == PG_GAME_MINER) // maze.cpp:107-111, miner.cpp:105-109
@@ -629,6 +644,13 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!(c.s.has_support && c.s.action_vy > 0)) {
             vy -= c.s.gravity;
             vy = clip_abs(vy, c.s.max_jump);
+        }
+    } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:117-128
+        float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
+        vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
+        if (c.s.action_vy > 0) vy = c.s.max_jump;
+        if (!c.s.has_support) {
+            if (vy > -2) vy -= c.s.gravity;
         }
     } else { // basic-abstract-game.cpp:678-693 (get_agent_acceleration_scale() = 1)
         const float v_scale = 1.0f;
@@ -680,6 +702,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:93-103
+        if (t == CL_ENEMY) {
+            c.s.sd_done = 1;
+        } else if (t == CL_COIN) {
+            c.s.sd_reward += 1.0f; // COIN_REWARD
+            c.s.coins_collected += 1;
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
         }
     } else if constexpr (G == PG_GAME_MINER) { // miner.cpp:81-93
         if (t == MN_ENEMY) {
@@ -923,6 +953,30 @@ DEV void maze_step_tail(Ctx &c) { // maze.cpp:113-131
     if (LANE == 0) { // latent agent_pos = int(agent->x), int(agent->y) (maze.cpp:144-145)
         c.d.latent[(size_t)c.env * PG_LATENT_N + 2 + PG_LATENT_GRID] = ix;
         c.d.latent[(size_t)c.env * PG_LATENT_N + 3 + PG_LATENT_GRID] = iy;
+    }
+}
+
+DEV void climber_step_tail(Ctx &c) { // climber.cpp:320-346
+    if (c.s.action_vx > 0) flag_reflected(c, 0, false);
+    if (c.s.action_vx < 0) flag_reflected(c, 0, true);
+    const int n = c.s.num_ents;
+    for (int base = 0; base < n; base += 64) { // per-entity, order-free
+        int i = base + LANE;
+        if (i < n && EI(c, F_TYPE, i) == CL_ENEMY) {
+            float x = EF(c, F_X, i), vx = EF(c, F_VX, i), sx = EF(c, F_CLIMBER_SPAWN_X, i);
+            if (x > sx + 4.0f) vx = -1 * fabsf(vx); // PATROL_RANGE
+            else if (x < sx - 4.0f) vx = fabsf(vx);
+            EF(c, F_VX, i) = vx;
+            EI(c, F_IMAGE_TYPE, i) = c.s.cur_time / 5 % 2 == 0 ? CL_ENEMY1 : CL_ENEMY2;
+            int fl = EI(c, F_FLAGS, i);
+            EI(c, F_FLAGS, i) = vx < 0 ? (fl | EF_REFLECTED) : (fl & ~EF_REFLECTED);
+        }
+    }
+    wave_sync();
+    if (c.s.coin_quota == c.s.coins_collected) {
+        c.s.sd_done = 1;
+        c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+        c.s.sd_level_complete = 1;
     }
 }
 
@@ -1184,6 +1238,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_MAZE) maze_step_tail(c);
     if constexpr (G == PG_GAME_HEIST) heist_step_tail(c);
     if constexpr (G == PG_GAME_MINER) miner_step_tail(c);
+    if constexpr (G == PG_GAME_CLIMBER) climber_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1281,6 +1336,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_BIGFISH) { PG_W(fish_eaten) }
         if constexpr (G == PG_GAME_HEIST) { PG_W(has_keys) }
         if constexpr (G == PG_GAME_MINER) { PG_W(diamonds_remaining) PG_W(died) }
+        if constexpr (G == PG_GAME_CLIMBER) { PG_W(has_support) PG_W(facing_right) PG_W(coins_collected) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1302,6 +1358,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
+        PG_CASE(PG_GAME_CLIMBER)
     default: break;
     }
 #undef PG_CASE

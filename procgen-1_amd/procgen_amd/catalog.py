@@ -157,6 +157,24 @@ MINER_SPRITES = {
     10: ["misc_assets/tile_bricksGrey.png"],
 }
 
+# ---------------------------------------------------------------- climber
+# procgen/src/games/climber.cpp:47-89 (PLAYER 0, PLAYER_JUMP 9, PLAYER_RIGHT1 12, PLAYER_RIGHT2 13,
+# WALL_TOP 16, WALL_MID 15, ENEMY1 6, ENEMY2 7, COIN 1)
+_CL_COLORS = ["Blue", "Green", "Grey", "Red"]
+CLIMBER_SPRITES = {
+    0: ["platformer/player%s_stand.png" % c for c in _CL_COLORS],
+    9: ["platformer/player%s_walk4.png" % c for c in _CL_COLORS],
+    12: ["platformer/player%s_walk1.png" % c for c in _CL_COLORS],
+    13: ["platformer/player%s_walk2.png" % c for c in _CL_COLORS],
+    16: ["platformer/tileBlue_05.png", "platformer/tileGreen_05.png", "platformer/tileYellow_06.png",
+         "platformer/tileBrown_06.png"],
+    15: ["platformer/tileBlue_08.png", "platformer/tileGreen_08.png", "platformer/tileYellow_09.png",
+         "platformer/tileBrown_09.png"],
+    6: ["platformer/enemySwimming_1.png"],
+    7: ["platformer/enemySwimming_2.png"],
+    1: ["platformer/yellowCrystal.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -164,6 +182,7 @@ GAMES = {
     "maze": (MAZE_SPRITES, "topdown"),          # maze.cpp:29-31
     "heist": (HEIST_SPRITES, "topdown"),        # heist.cpp:37-39
     "miner": (MINER_SPRITES, "caves"),          # miner.cpp:45-47
+    "climber": (CLIMBER_SPRITES, "platform"),   # climber.cpp:43-45
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

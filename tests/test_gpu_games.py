@@ -66,12 +66,12 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
 def test_parity_hard_unbounded(game):
     run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
 def test_parity_200_levels_easy(game):
     run_pair(game, 8, 200, seed=2, num_levels=200, start_level=0, rand_seed=5, distribution_mode="easy",
              latent=game in LATENT)
@@ -90,10 +90,15 @@ def test_miner_long_run_deaths():
     assert episodes > 0
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
 def test_parity_options(game):
     run_pair(game, 8, 150, seed=4, num_levels=20, rand_seed=3, use_backgrounds=False, restrict_themes=True,
              use_sequential_levels=True)
+
+
+def test_climber_uncentered():
+    """climber with center_agent=False: visibility = max(20, 64) (prepare_for_drawing :832-838)."""
+    run_pair("climber", 8, 200, seed=11, num_levels=0, rand_seed=6, center_agent=False)
 
 
 def test_bigfish_long_episodes():
@@ -103,8 +108,8 @@ def test_bigfish_long_episodes():
 
 def test_mixed_batch_parity():
     """env n plays names[n % 4] (vecgame.cpp:357-358), level seeds from the global index."""
-    names = ["bigfish", "coinrun", "heist", "maze", "miner"]
-    num = 20
+    names = ["bigfish", "climber", "coinrun", "heist", "maze", "miner"]
+    num = 24
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=21)
     orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
     g = gpu_obs(env)
@@ -141,7 +146,7 @@ def test_full_size_sampled_parity(game):
     env.close()
 
 
-@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner"])
+@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber"])
 def test_state_roundtrip(game):
     env = make_gpu(4, game, num_levels=20, rand_seed=11)
     rng = np.random.RandomState(1)

@@ -216,3 +216,21 @@ def test_mazegen_vs_reference(mode, dim, doors):
         assert ra == rb == dim + 2
         np.testing.assert_array_equal(a, b, err_msg="seed %d" % seed)
         assert da[0] == db[0]
+
+
+def test_argument_evaluation_order_pinned():
+    """climber.cpp:196 draws two randn(2) inside one call's arguments; C++ leaves their order
+    unspecified.  The oracle (and the engine) take g++'s order -- right to left, the vx draw
+    first -- pinned here against that call compiled by g++ with the reference's RandGen."""
+    ref = ref_lib()
+    ref.ref_climber_enemy_args.argtypes = [ctypes.c_int32, ctypes.c_void_p]
+    lib = oracle_lib.load()
+    for seed in range(64):
+        out = np.zeros(2, np.float32)
+        ref.ref_climber_enemy_args(seed, out.ctypes.data)
+        ops = np.array([[1, 2, 0], [1, 2, 0]], np.int32)  # two randn(2)
+        draws = np.zeros(2, np.int32)
+        lib.oracle_randgen_script(seed & 0xFFFFFFFF, ops.ctypes.data, 2, draws.ctypes.data)
+        vdraw, ydraw = int(draws[0]), int(draws[1])
+        assert out[0] == np.float32(0 + ydraw + 2 + .5)
+        assert out[1] == np.float32(.15 * (vdraw * 2 - 1))
