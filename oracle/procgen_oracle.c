@@ -1965,9 +1965,19 @@ static void qt_scale_image(uint32_t *canvas, double rx, double ry, double rw, do
     int h = ty2 - ty1;
     int w = tx2 - tx1;
     uint32_t basex, srcy;
-    {
+    /* source rect QRectF(0, 0, iw, ih): a negative scale (a mapped TxScale rect) steps back from
+     * its right / bottom edge */
+    if (sx < 0) {
+        int dstx = qFloor((tx1 + 0.5 - t_right) * ix) + 1;
+        basex = (uint32_t)((double)iw * 65536) + (uint32_t)dstx;
+    } else {
         int dstx = qCeil((tx1 + 0.5 - t_left) * ix) - 1;
         basex = (uint32_t)(0.0 * 65536) + (uint32_t)dstx;
+    }
+    if (sy < 0) {
+        int dsty = qFloor((ty1 + 0.5 - t_bottom) * iy) + 1;
+        srcy = (uint32_t)((double)ih * 65536) + (uint32_t)dsty;
+    } else {
         int dsty = qCeil((ty1 + 0.5 - t_top) * iy) - 1;
         srcy = (uint32_t)(0.0 * 65536) + (uint32_t)dsty;
     }
@@ -2158,16 +2168,21 @@ static void qt_draw_image_xform(uint32_t *canvas, const QtXform *t, double rx, d
     }
 }
 
-/* basic-abstract-game.cpp:908-916: save; translate(center); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)) */
+/* qFuzzyIsNull(double) (qglobal.h) */
+static bool qt_fuzzy_null(double d) { return fabs(d) <= 0.000000000001; }
+
+/* basic-abstract-game.cpp:908-916: save; translate(center); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)).
+ * QTransform::type() classifies the matrix with qFuzzyIsNull: a rotation whose sine is within 1e-12
+ * of 0 (e.g. rotate(-180) = cos -1, sin -1.2e-16) is a TxScale (or TxTranslate), drawn by
+ * qt_scale_image_32bit on qt_mapRect_non_normalizing(r, matrix), whose TxScale map ignores m12/m21. */
 static void qt_draw_image_rotated(uint32_t *canvas, double x, double y, double w, double h, double deg,
                                   const uint32_t *px, int iw, int ih, bool mirrored, double opacity) {
     QtXform t = qt_translate_rotate(x + w / 2, y + h / 2, deg);
     double rx = -w / 2, ry = -h / 2;
     if (w <= 0 || h <= 0) return; /* QRectF::isEmpty */
-    if (t.m12 == 0 && t.m21 == 0) { /* TxScale (or translate): qt_scale_image_32bit on the mapped rect */
-        double ax, ay, bx, by;
-        qt_map(&t, rx, ry, &ax, &ay);
-        qt_map(&t, rx + w, ry + h, &bx, &by);
+    if (qt_fuzzy_null(t.m12) && qt_fuzzy_null(t.m21)) { /* TxScale / TxTranslate */
+        double ax = t.m11 * rx + t.dx, ay = t.m22 * ry + t.dy;
+        double bx = t.m11 * (rx + w) + t.dx, by = t.m22 * (ry + h) + t.dy;
         qt_scale_image(canvas, ax, ay, bx - ax, by - ay, px, iw, ih, QFMT_ARGB32_PM, mirrored, opacity);
         return;
     }

@@ -208,7 +208,9 @@ void build_rot_table(float *angles, double *table) {
     for (int dx = -1; dx <= 1; dx++)
         for (int dy = -1; dy <= 1; dy++)
             if (dx != 0 || dy != 0) angles[(dx + 1) * 3 + (dy + 1)] = -1 * atan2f((float)dy, (float)dx) + 0.0f;
-    angles[9] = PI_F / 2;
+    angles[9] = PI_F / 2;   // heist ring keys; leaper frog (1 * PI / 2)
+    angles[10] = -1 * PI_F / 2; // leaper frog facing left (-1 * PI / 2, leaper.cpp:241)
+    angles[11] = PI_F;          // leaper frog facing down / cars moving left (leaper.cpp:245, 186)
     for (int k = 0; k < PG_ROT_N; k++) {
         float rot = angles[k];
         if (std::isnan(rot)) continue;
@@ -229,6 +231,12 @@ void build_rot_table(float *angles, double *table) {
             cosa = std::cos(b);
         }
         table[4 * k + 0] = cosa; table[4 * k + 1] = sina; table[4 * k + 2] = -sina; table[4 * k + 3] = cosa;
+        // QTransform::type(): qFuzzyIsNull(m12) && qFuzzyIsNull(m21) makes it a TxScale, drawn by
+        // the scale blit whose map ignores m12 / m21 (rotate(-180): sin = -1.2e-16)
+        if (std::fabs(sina) <= 0.000000000001) {
+            table[4 * k + 1] = 0;
+            table[4 * k + 2] = 0;
+        }
     }
 }
 

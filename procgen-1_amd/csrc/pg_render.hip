@@ -171,13 +171,59 @@ DEV void trap_setup(const QV &tl, const QV &bl, const QV &tr, const QV &br, doub
     t.x_r = (int)((tr.x + (0.5 + t.from_y - tr.y) * rightSlope + 0.5) * 0x10000);
 }
 
+// One axis of qt_scale_image_32bit for a mapped target rect whose extent may be negative (a
+// TxScale transform from rotate(180), qblendfunctions_p.h: the sx < 0 branch steps back from
+// the source rect's right edge).
+DEV bool axis_setup_signed(double r, double rw, int iw, Axis &a) {
+    a.n = 0;
+    if (iw <= 0) return false;
+    const double right = r + rw;
+    const double sx = rw / (double)iw;
+    const int ix = (int)(65536.0 / sx);
+    int t1 = qRound(r), t2 = qRound(right);
+    if (t2 < t1) { int t = t2; t2 = t1; t1 = t; }
+    if (t1 < 0) t1 = 0;
+    if (t2 >= PG_RES) t2 = PG_RES;
+    if (t1 >= t2) return false;
+    int n = t2 - t1;
+    uint32_t base;
+    if (sx < 0) base = (uint32_t)((double)iw * 65536) + (uint32_t)((int)floor((t1 + 0.5 - right) * ix) + 1);
+    else base = (uint32_t)((int)ceil((t1 + 0.5 - r) * ix) - 1);
+    if ((int)(base >> 16) >= iw && ix < 0) { base += ix; --n; }
+    int end = (int)((base + (uint32_t)(ix * (n - 1))) >> 16);
+    if (end < 0 || end >= iw) --n;
+    if (n <= 0) return false;
+    a.t1 = t1; a.n = n; a.base = base; a.step = ix;
+    return true;
+}
+
 // returns false when the transform is not a rotation this path reproduces
 DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
                       double m11, double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
     if (!(w > 0) || !(h > 0) || iw <= 0 || ih <= 0) return true; // QRectF::isEmpty: nothing drawn
-    if (m12 == 0 && m21 == 0) return false;                      // TxScale (rotate(180)): scale path
     const double dx = x + w / 2, dy = y + h / 2;
     const double rx = -w / 2, ry = -h / 2, right = rx + w, bottom = ry + h;
+    if (m12 == 0 && m21 == 0) {
+        // QTransform::type() says TxScale / TxTranslate (the host zeroed qFuzzyIsNull m12 / m21):
+        // qt_scale_image_32bit on qt_mapRect_non_normalizing(r, matrix) -- the TxScale map
+        const double ax = m11 * rx + dx, ay = m22 * ry + dy;
+        const double bx = m11 * right + dx, by = m22 * bottom + dy;
+        Axis ex, ey;
+        if (!axis_setup_signed(ax, bx - ax, iw, ex) || !axis_setup_signed(ay, by - ay, ih, ey)) return true;
+        const int lane = LANE;
+        if (lane >= ex.t1 && lane < ex.t1 + ex.n) {
+            int scol = (int)((ex.base + (uint32_t)((lane - ex.t1) * ex.step)) >> 16);
+            if (mir) scol = iw - 1 - scol;
+            for (int k = 0; k < ey.n; k++) {
+                const int srow = (int)((ey.base + (uint32_t)(k * ey.step)) >> 16);
+                const uint32_t idx = soff + (uint32_t)(srow * iw + scol);
+                if (idx >= npix) return false;
+                const int o = (ey.t1 + k) * PG_RES + lane;
+                fb[o] = blend_argb_pm(fb[o], pixels[idx], ca);
+            }
+        }
+        return true;
+    }
     QV v[4]; // TopLeft, TopRight, BottomRight, BottomLeft
     auto map = [&](double px, double py, QV &o) {
         o.x = m11 * px + m21 * py + dx;

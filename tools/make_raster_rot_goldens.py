@@ -40,6 +40,11 @@ def game_angles():
             if rot != 0:
                 out.append(float(np.float32(np.float32(rot * np.float32(180)) / PI_F)))
     out.append(float(np.float32(np.float32(np.float32(PI_F / np.float32(2)) * np.float32(180)) / PI_F)))
+    # leaper: frog +-PI/2, 0, PI; cars PI (leaper.cpp:156-158, 240-246) -- and Qt's exact special
+    # cases of QTransform::rotate (+-90, 180 = a scale, 270)
+    for rot in (PI_F, -PI_F, -PI_F / np.float32(2)):
+        out.append(float(np.float32(np.float32(np.float32(rot) * np.float32(180)) / PI_F)))
+    out += [90.0, -90.0, 180.0, -180.0, 270.0, -270.0]
     return out
 
 
