@@ -56,7 +56,8 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_MAZE = 11, GAME_MINER = 12 };
+enum { GAME_BIGFISH = 0, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+       GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -235,6 +236,9 @@ typedef struct {
     /* climber (climber.cpp:30-36; has_support, facing_right, wall_theme, gravity, air_control shared
      * with coinrun's members above) */
     int coin_quota, coins_collected;
+    /* leaper (leaper.cpp:27-32) */
+    int bottom_road_y, bottom_water_y, goal_y, num_road_lanes, num_water_lanes;
+    float road_lane_speeds[8], water_lane_speeds[8];
     /* observation of the last step */
     uint32_t canvas[RES_W * RES_H];
 } Game;
@@ -417,6 +421,15 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 g->fish_eaten += 1;
             }
         }
+    } else if (g->game_id == GAME_LEAPER) { /* leaper.cpp:69-77: CAR 4, FINISH_LINE 5 */
+        Entity *agent = AG(g);
+        if (obj->type == 4) {
+            g->sd_done = true;
+        } else if (obj->type == 5 && agent->vx == 0 && agent->vy == 0) {
+            g->sd_reward += 10; /* GOAL_REWARD (const int) */
+            g->sd_done = true;
+            g->sd_level_complete = true;
+        }
     } else if (g->game_id == GAME_CLIMBER) { /* climber.cpp:93-103: ENEMY 5, COIN 1 */
         if (obj->type == 5) {
             g->sd_done = true;
@@ -452,7 +465,8 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
 
 /* should_preserve_type_themes + mask_theme_if_necessary (basic-abstract-game.cpp:454-462, heist.cpp:42-44) */
 static int mask_theme(Game *g, int theme, int type) {
-    bool preserve = g->game_id == GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR);
+    bool preserve = (g->game_id == GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR)) ||
+                    (g->game_id == GAME_LEAPER && type == PLAYER); /* leaper.cpp:87-89 */
     if (g->options.restrict_themes && !preserve) return 0;
     return theme;
 }
@@ -737,6 +751,7 @@ static float clip_abs(float x, float y) { /* cpp-utils.h:46-52 */
     return x;
 }
 
+static void lp_decay_vel(float *vel);
 static void update_agent_velocity(Game *g) {
     Entity *agent = AG(g);
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:156-173 */
@@ -752,6 +767,22 @@ static void update_agent_velocity(Game *g) {
             agent->vy -= g->gravity;
             agent->vy = clip_abs(agent->vy, g->max_jump);
         }
+        return;
+    }
+    if (g->game_id == GAME_LEAPER) { /* leaper.cpp:228-244 */
+        if (agent->vx == 0 && agent->vy == 0) {
+            if (g->action_vx != 0) {
+                agent->vx = g->maxspeed * g->action_vx;
+                agent->image_theme = 1;
+                agent->rotation = (agent->vx > 0 ? 1 : -1) * PI_F / 2;
+            } else if (g->action_vy != 0) {
+                agent->vy = g->maxspeed * g->action_vy;
+                agent->image_theme = 1;
+                agent->rotation = agent->vy > 0 ? 0 : PI_F;
+            }
+        }
+        lp_decay_vel(&agent->vx);
+        lp_decay_vel(&agent->vy);
         return;
     }
     if (g->game_id == GAME_CLIMBER) { /* climber.cpp:117-128 */
@@ -1800,6 +1831,143 @@ static void climber_game_step(Game *g) { /* :320-346 */
     }
 }
 
+/* ================================================================== leaper (games/leaper.cpp) */
+#define LP_LOG 1
+#define LP_ROAD 2
+#define LP_WATER 3
+#define LP_CAR 4
+#define LP_FINISH_LINE 5
+static const float LP_MONSTER_RADIUS = 0.25f;
+static const float LP_LOG_RADIUS = 0.45f;
+#define LP_NSTEP 5
+static const float LP_MAX_SPEED = (float)(2 / (LP_NSTEP - 1.0));
+static const float LP_VEL_DECAY = (float)(2 / (LP_NSTEP - 1.0)) / LP_NSTEP;
+
+static float lp_sign(float x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); } /* leaper.cpp:21-23 */
+
+static float lp_rand_sign(Game *g) { /* :91-97 */
+    if ((double)rg_rand01(&g->rand_gen) < 0.5) return 1.0f;
+    return -1.0f;
+}
+
+static void leaper_choose_world_dim(Game *g) { /* :99-113 */
+    int world_dim = 20;
+    if (g->options.distribution_mode == EasyMode) world_dim = 9;
+    else if (g->options.distribution_mode == HardMode) world_dim = 15;
+    g->main_width = world_dim;
+    g->main_height = world_dim;
+}
+
+static int lp_choose_extra_space(Game *g) { /* :115-117 */
+    return g->options.distribution_mode == EasyMode ? 0 : rg_randn(&g->rand_gen, 2);
+}
+
+static void lp_spawn_entities(Game *g, const or_atlas *at) { /* :184-218 */
+    for (int lane = 0; lane < g->num_road_lanes; lane++) {
+        float speed = g->road_lane_speeds[lane];
+        float spawn_prob = (float)(fabs(speed) / 6.0);
+        if (rg_rand01(&g->rand_gen) < spawn_prob) {
+            float x = speed > 0 ? (-1 * LP_MONSTER_RADIUS) : (g->main_width + LP_MONSTER_RADIUS);
+            Entity m;
+            entity_init(&m, x, (float)(g->bottom_road_y + lane + 0.5), speed, 0, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS,
+                        LP_CAR);
+            choose_random_theme(g, &m, at);
+            if (speed < 0) m.rotation = PI_F;
+            if (!has_any_collision(g, &m, 0)) {
+                fassert(g->num_ents < MAX_ENTS);
+                g->ents[g->num_ents++] = m;
+            }
+        }
+    }
+    for (int lane = 0; lane < g->num_water_lanes; lane++) {
+        float speed = g->water_lane_speeds[lane];
+        float spawn_prob = (float)(fabs(speed) / 2.0);
+        if (rg_rand01(&g->rand_gen) < spawn_prob) {
+            float x = speed > 0 ? (-1 * LP_LOG_RADIUS) : (g->main_width + LP_LOG_RADIUS);
+            Entity m;
+            entity_init(&m, x, (float)(g->bottom_water_y + lane + 0.5), speed, 0, LP_LOG_RADIUS, LP_LOG_RADIUS, LP_LOG);
+            if (!has_any_collision(g, &m, 0)) {
+                fassert(g->num_ents < MAX_ENTS);
+                g->ents[g->num_ents++] = m;
+            }
+        }
+    }
+}
+
+static void leaper_game_reset(Game *g, const or_atlas *at) { /* :119-182 */
+    leaper_choose_world_dim(g);
+    basic_game_reset(g, at);
+    MT *r = &g->rand_gen;
+    g->options.center_agent = false;
+    Entity *agent = AG(g);
+    agent->y = agent->ry;
+    float min_car_speed = 0.05f, max_car_speed = 0.2f, min_log_speed = 0.05f, max_log_speed = 0.1f;
+    if (g->options.distribution_mode == EasyMode) {
+        min_car_speed = 0.03f; max_car_speed = 0.12f; min_log_speed = 0.025f; max_log_speed = 0.075f;
+    } else if (g->options.distribution_mode == ExtremeMode) {
+        min_car_speed = 0.1f; max_car_speed = 0.3f; min_log_speed = 0.1f; max_log_speed = 0.2f;
+    }
+    g->bottom_road_y = lp_choose_extra_space(g) + 1;
+    int max_diff = g->options.distribution_mode == EasyMode ? 3 : 4;
+    int difficulty = rg_randn(r, max_diff + 1);
+    int extra_lane_option = g->options.distribution_mode == EasyMode ? 0 : rg_randn(r, 4);
+    g->num_road_lanes = difficulty + (extra_lane_option == 2 ? 1 : 0);
+    for (int lane = 0; lane < g->num_road_lanes; lane++) {
+        /* rand_sign() * randrange(...): g++ evaluates the left operand first (pinned,
+         * oracle/ref_harness.cpp ref_leaper_lane_speed) */
+        float sgn = lp_rand_sign(g);
+        float spd = rg_randrange(r, min_car_speed, max_car_speed);
+        g->road_lane_speeds[lane] = sgn * spd;
+        fill_elem(g, 0, g->bottom_road_y + lane, g->main_width, 1, LP_ROAD);
+    }
+    g->bottom_water_y = g->bottom_road_y + g->num_road_lanes + lp_choose_extra_space(g) + 1;
+    g->num_water_lanes = difficulty + (extra_lane_option == 3 ? 1 : 0);
+    int curr_sign = (int)lp_rand_sign(g);
+    for (int lane = 0; lane < g->num_water_lanes; lane++) {
+        g->water_lane_speeds[lane] = curr_sign * rg_randrange(r, min_log_speed, max_log_speed);
+        curr_sign *= -1;
+        fill_elem(g, 0, g->bottom_water_y + lane, g->main_width, 1, LP_WATER);
+    }
+    g->goal_y = g->bottom_water_y + g->num_water_lanes + 1;
+    float mn = min_car_speed < min_log_speed ? min_car_speed : min_log_speed; /* std::min */
+    for (int i = 0; (float)i < g->main_width / mn; i++) {
+        lp_spawn_entities(g, at);
+        step_entities(g);
+    }
+    add_entity_rxy(g, (float)(g->main_width / 2.0), (float)(g->goal_y - .5), 0, 0, (float)(g->main_width / 2.0), .5f,
+                   LP_FINISH_LINE);
+}
+
+static void lp_decay_vel(float *vel) { /* :220-226 */
+    float vel_sign = lp_sign((float)(1.0 * *vel));
+    *vel = (fabsf(*vel) - LP_VEL_DECAY);
+    if (*vel < 0) *vel = 0;
+    *vel = *vel * vel_sign;
+}
+
+static void leaper_game_step(Game *g, const or_atlas *at) { /* :252-288 */
+    Entity *agent = AG(g);
+    if (agent->image_theme >= 1) agent->image_theme = (agent->image_theme + 1) % LP_NSTEP;
+    basic_game_step(g);
+    lp_spawn_entities(g, at);
+    agent = AG(g);
+    bool standing_on_log = false;
+    float log_vx = 0.0f;
+    float margin = -1 * agent->rx;
+    for (int i = 0; i < g->num_ents; i++) {
+        Entity *m = &g->ents[i];
+        if (m->type == LP_LOG && has_collision(agent, m, margin)) {
+            standing_on_log = true;
+            log_vx = m->vx;
+        }
+    }
+    if (get_obj(g, (int)agent->x, (int)agent->y) == LP_WATER) {
+        if (!standing_on_log && agent->vx == 0 && agent->vy == 0) g->sd_done = true;
+    }
+    if (standing_on_log) agent->x += log_vx;
+    if (is_out_of_bounds(g, agent)) g->sd_done = true;
+}
+
 /* ================================================================== Game (game.cpp) */
 static void game_reset_dispatch(Game *g, const or_atlas *at) {
     if (g->game_id == GAME_COINRUN) coinrun_game_reset(g, at);
@@ -1808,6 +1976,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_HEIST) heist_game_reset(g, at);
     else if (g->game_id == GAME_MINER) miner_game_reset(g, at);
     else if (g->game_id == GAME_CLIMBER) climber_game_reset(g, at);
+    else if (g->game_id == GAME_LEAPER) leaper_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -1817,6 +1986,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_HEIST) heist_game_step(g);
     else if (g->game_id == GAME_MINER) miner_game_step(g);
     else if (g->game_id == GAME_CLIMBER) climber_game_step(g);
+    else if (g->game_id == GAME_LEAPER) leaper_game_step(g, at);
     else fatal_msg("game not restated");
 }
 
@@ -2242,8 +2412,39 @@ static RectD adjust_rect(RectD b, RectD a) { /* qt-utils.h:12-19 */
     return r;
 }
 
+static void tile_image(Game *g, const uint32_t *px, int iw, int ih, bool refl, double opacity, RectD rect,
+                       float tile_ratio) { /* basic-abstract-game.cpp:849-877 */
+    if (tile_ratio != 0) {
+        if (tile_ratio < 0) {
+            tile_ratio = -1 * tile_ratio;
+            int num_tiles = (int)(rect.h / (rect.w * tile_ratio));
+            if (num_tiles < 1) num_tiles = 1;
+            float tile_height = (float)(rect.h / num_tiles);
+            float tile_width = (float)rect.w;
+            for (int i = 0; i < num_tiles; i++)
+                qt_draw_image(g->canvas, rect.x, rect.y + tile_height * i, tile_width, tile_height, px, iw, ih,
+                              QFMT_ARGB32_PM, refl, opacity);
+        } else {
+            int num_tiles = (int)(rect.w / (rect.h * tile_ratio));
+            if (num_tiles < 1) num_tiles = 1;
+            float tile_width = (float)(rect.w / num_tiles);
+            float tile_height = (float)rect.h;
+            for (int i = 0; i < num_tiles; i++)
+                qt_draw_image(g->canvas, rect.x + tile_width * i, rect.y, tile_width, tile_height, px, iw, ih,
+                              QFMT_ARGB32_PM, refl, opacity);
+        }
+    } else {
+        qt_draw_image(g->canvas, rect.x, rect.y, rect.w, rect.h, px, iw, ih, QFMT_ARGB32_PM, refl, opacity);
+    }
+}
+
+static float hook_tile_aspect_ratio(Game *g, const Entity *e) {
+    if (g->game_id == GAME_LEAPER && e->type == LP_FINISH_LINE) return 1; /* leaper.cpp:68-74 */
+    return 0;                                                            /* :417-419 */
+}
+
 static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, bool is_reflected, int base_type,
-                       int theme, float alpha) { /* :886-922 (tile_ratio == 0 for coinrun) */
+                       int theme, float alpha, float tile_ratio) { /* :886-922 */
     int img_type = hook_image_for_type(g, base_type);
     if (img_type < 0) return;
     if (g->options.use_monochrome_assets || img_type >= USE_ASSET_THRESHOLD) {
@@ -2258,6 +2459,9 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
     if (g->game_id == GAME_COINRUN && is_player_image(img_type)) { /* coinrun.cpp:64-70 */
         RectD adj = {0, -.7415, 1, 1.7415};
         r = adjust_rect(base, adj);
+    } else if (g->game_id == GAME_LEAPER && img_type == PLAYER) { /* leaper.cpp:244-250 */
+        RectD adj = {0, -.275, 1, 1.55};
+        r = adjust_rect(base, adj);
     }
     const or_image *im = &at->sprites[img_idx];
     /* miner's MUD image (misc_assets/mud.png, resources.cpp:511) is absent from the reference's
@@ -2267,8 +2471,7 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
     if (im->w <= 0) fatal_msg("missing sprite (generated assets are not restated yet)");
     double opacity = alpha != 1 ? (double)alpha : 1.0;
     if (rotation == 0) {
-        qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + im->offset, im->w, im->h, QFMT_ARGB32_PM,
-                      is_reflected, opacity);
+        tile_image(g, at->pixels + im->offset, im->w, im->h, is_reflected, opacity, r, tile_ratio);
     } else { /* :908-916: p.rotate(rotation * 180 / PI) */
         float deg = rotation * 180 / PI_F;
         qt_draw_image_rotated(g->canvas, r.x, r.y, r.w, r.h, (double)deg, at->pixels + im->offset, im->w, im->h,
@@ -2292,7 +2495,8 @@ static void draw_entities(Game *g, const or_atlas *at, int render_z) { /* :1061-
         } else {
             r1 = get_screen_rect(g, e->x - e->rx, e->y + e->ry, 2 * e->rx, 2 * e->ry, 0); /* :820-826 */
         }
-        draw_image(g, at, r1, e->rotation, e->is_reflected, e->image_type, e->image_theme, e->alpha);
+        draw_image(g, at, r1, e->rotation, e->is_reflected, e->image_type, e->image_theme, e->alpha,
+                   hook_tile_aspect_ratio(g, e));
     }
 }
 
@@ -2336,7 +2540,7 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
             if (type == INVALID_OBJ) continue;
             int theme = hook_theme_for_grid_obj(g, type);
             RectD r2 = get_screen_rect(g, (float)x, (float)(y + 1), 1, 1, RENDER_EPS);
-            draw_image(g, at, r2, 0, false, type, theme, 1.0f);
+            draw_image(g, at, r2, 0, false, type, theme, 1.0f, 0);
         }
     }
     draw_entities(g, at, 0);
@@ -2357,6 +2561,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "heist") == 0) return GAME_HEIST;
     if (strcmp(name, "miner") == 0) return GAME_MINER;
     if (strcmp(name, "climber") == 0) return GAME_CLIMBER;
+    if (strcmp(name, "leaper") == 0) return GAME_LEAPER;
     return -1;
 }
 
@@ -2405,6 +2610,10 @@ static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
     g->out_of_bounds_object = WALL_OBJ;
     g->visibility = 8.0f;
 }
+static void leaper_ctor(Game *g) { /* leaper.cpp:34-38 */
+    g->maxspeed = LP_MAX_SPEED;
+    g->timeout = 500;
+}
 static void climber_ctor(Game *g) { /* climber.cpp:38-41 */
     g->out_of_bounds_object = CL_WALL_MID;
 }
@@ -2432,7 +2641,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
     /* game.cpp:76-86: easy and hard for every game; memory for heist and maze (of those restated) */
-    bool dm_ok = dm == EasyMode || dm == HardMode ||
+    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == ExtremeMode && gid == GAME_LEAPER) ||
                  (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE || gid == GAME_MINER));
     if (!dm_ok) return NULL;
     Vec *v = (Vec *)calloc(1, sizeof(Vec));
@@ -2462,6 +2671,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_HEIST) heist_ctor(g);
         else if (gid == GAME_MINER) miner_ctor(g);
         else if (gid == GAME_CLIMBER) climber_ctor(g);
+        else if (gid == GAME_LEAPER) leaper_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

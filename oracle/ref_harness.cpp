@@ -111,5 +111,27 @@ void ref_climber_enemy_args(int32_t seed, float *out) {
     out[0] = ent->y;
     out[1] = ent->vx;
 }
-}
 
+// leaper.cpp:155: road_lane_speeds.push_back(rand_sign() * rand_gen.randrange(min, max)) -- the
+// operand order of a binary `*` is unspecified too; pinned here with the same compiler.
+namespace {
+struct ProbeLeaper {
+    RandGen rand_gen;
+    std::vector<float> road_lane_speeds;
+    float rand_sign() {
+        if (rand_gen.rand01() < 0.5) {
+            return 1.0;
+        } else {
+            return -1.0;
+        }
+    }
+};
+} // namespace
+
+void ref_leaper_lane_speed(int32_t seed, float lo, float hi, float *out) {
+    ProbeLeaper g;
+    g.rand_gen.seed(seed);
+    g.road_lane_speeds.push_back(g.rand_sign() * g.rand_gen.randrange(lo, hi));
+    out[0] = g.road_lane_speeds[0];
+}
+}

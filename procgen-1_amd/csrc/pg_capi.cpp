@@ -113,9 +113,10 @@ int game_id(const std::string &name) {
     if (name == "heist") return PG_GAME_HEIST;
     if (name == "miner") return PG_GAME_MINER;
     if (name == "climber") return PG_GAME_CLIMBER;
+    if (name == "leaper") return PG_GAME_LEAPER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, climber, coinrun, heist, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, climber, coinrun, heist, leaper, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -170,6 +171,9 @@ void construct_env(PGEnv &s, int gid) {
         s.has_useful_vel_info = 0;
         s.out_of_bounds_object = 51; // WALL_OBJ
         s.visibility = 8.0f;
+    } else if (gid == PG_GAME_LEAPER) { // leaper.cpp:34-38 (MAX_SPEED = 2 / (NSTEP - 1.0))
+        s.maxspeed = (float)(2 / (5 - 1.0));
+        s.timeout = 500;
     } else if (gid == PG_GAME_CLIMBER) { // climber.cpp:38-41
         s.out_of_bounds_object = 15; // WALL_MID
     } else if (gid == PG_GAME_MINER) { // miner.cpp:30-43
@@ -510,6 +514,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (gid < 0) return bad("env '" + nm + "' is not in this build (supported: " + SUPPORTED_GAMES + ")");
         // game.cpp:76-86 distribution mode validity
         bool dm_ok = distribution_mode == PG_EASY || distribution_mode == PG_HARD ||
+                     (distribution_mode == PG_EXTREME && gid == PG_GAME_LEAPER) ||
                      (distribution_mode == PG_MEMORY &&
                       (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE || gid == PG_GAME_MINER));
         if (!dm_ok) return bad("invalid distribution_mode for " + nm);

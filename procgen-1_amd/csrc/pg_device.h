@@ -86,6 +86,15 @@
 #define CL_WALL_TOP 16
 #define CL_ENEMY_BARRIER 19
 DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
+// leaper.cpp:6-21
+#define LP_LOG 1
+#define LP_ROAD 2
+#define LP_WATER 3
+#define LP_CAR 4
+#define LP_FINISH_LINE 5
+#define LP_MONSTER_RADIUS 0.25f
+#define LP_LOG_RADIUS 0.45f
+#define LP_NSTEP 5
 // object-ids.h
 #define EXIT_OBJ 52
 #define AGENT_OBJ 53

@@ -22,7 +22,8 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_MAZE = 11, PG_GAME_MINER = 12
+    PG_GAME_BIGFISH = 0, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_MINER = 12
 };
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
@@ -149,7 +150,15 @@ struct PGEnv {
     // ---- climber (climber.cpp:30-36; the platformer members are shared with coinrun)
     int32_t coin_quota;
     int32_t coins_collected;
-    int32_t pad[128 - 79];
+    // ---- leaper (leaper.cpp:27-32): at most 4 + 1 lanes of each kind
+    int32_t bottom_road_y;
+    int32_t bottom_water_y;
+    int32_t goal_y;
+    int32_t num_road_lanes;
+    int32_t num_water_lanes;
+    float road_lane_speeds[5];
+    float water_lane_speeds[5];
+    int32_t pad[128 - 94];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

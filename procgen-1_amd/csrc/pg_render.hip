@@ -125,7 +125,8 @@ DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cp
 }
 template <int G>
 DEV int mask_theme(const PGEnv &s, int theme, int img_type) { // mask_theme_if_necessary (:454-462, heist.cpp:42-44)
-    bool preserve = G == PG_GAME_HEIST && (img_type == HS_KEY || img_type == HS_LOCKED_DOOR);
+    bool preserve = (G == PG_GAME_HEIST && (img_type == HS_KEY || img_type == HS_LOCKED_DOOR)) ||
+                    (G == PG_GAME_LEAPER && img_type == PLAYER); // leaper.cpp:91-93
     return (s.opt_restrict_themes && !preserve) ? 0 : theme;
 }
 template <int G>
@@ -133,6 +134,12 @@ DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entit
     if constexpr (G == PG_GAME_HEIST)
         if (type == HS_KEY_ON_RING) return (s.has_keys >> theme) & 1;
     return true;
+}
+// get_tile_aspect_ratio (basic :417-419; leaper.cpp:68-74): 0 = one image, > 0 tile horizontally
+template <int G>
+DEV float tile_aspect_ratio(int type) {
+    if constexpr (G == PG_GAME_LEAPER) return type == LP_FINISH_LINE ? 1.0f : 0.0f;
+    return 0.0f;
 }
 template <int G>
 DEV bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
@@ -311,12 +318,16 @@ struct Img {
     bool draw, rot;
     Axis ex, ey;
     int soff, sw, sh, ca, mir, rslot, ez;
-    double rx, ry, rw, rh; // target rect of a rotated image
+    int ntile;             // > 0: tile_image with this many tiles (seq path)
+    float tw, th;          // tile size (float, as tile_image computes it)
+    double rx, ry, rw, rh; // target rect of a rotated / tiled image
 };
 
 DEV void img_clear(Img &im) {
     im.draw = false;
     im.rot = false;
+    im.ntile = 0;
+    im.tw = im.th = 0;
     im.ex.t1 = im.ex.n = im.ey.t1 = im.ey.n = 0;
     im.ex.base = im.ey.base = 0;
     im.ex.step = im.ey.step = 0;
@@ -330,6 +341,24 @@ DEV double readlane_d(double x, int j) {
     long long b = __builtin_bit_cast(long long, x);
     int lo = readlane((int)(b & 0xffffffff), j), hi = readlane((int)(b >> 32), j);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+// One scale blit, all lanes cooperating over its footprint (uniform arguments).
+DEV void blit_seq(uint32_t *fb, const PGDev &d, const Axis &ex, const Axis &ey, uint32_t soff, int sw, int mir, int ca,
+                  bool &err) {
+    const int nx = ex.n, ny = ey.n;
+    const float inv = 1.0f / (float)nx;
+    for (int p = LANE; p < nx * ny; p += 64) {
+        int py = (int)(((float)p + 0.5f) * inv);
+        int pxx = p - py * nx;
+        int scol = (int)((ex.base + (uint32_t)(pxx * ex.step)) >> 16);
+        int srow = (int)((ey.base + (uint32_t)(py * ey.step)) >> 16);
+        if (mir) scol = sw - 1 - scol;
+        const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
+        const int o = (ey.t1 + py) * PG_RES + ex.t1 + pxx;
+        if (idx < d.num_pixels && o >= 0 && o < PG_RES * PG_RES) fb[o] = blend_argb_pm(fb[o], d.pixels[idx], ca);
+        else err = true;
+    }
 }
 
 DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long long m, bool &err) {
@@ -352,7 +381,7 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
             tv[g] = 0;
             fo[g] = 0;
             const int j = js[g];
-            if (j < 0 || readlane(im.rot ? 1 : 0, j)) continue;
+            if (j < 0 || readlane(im.rot || im.ntile > 0 ? 1 : 0, j)) continue;
             const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
             if (nx * ny > 64) continue;
             if (lane < nx * ny) {
@@ -390,27 +419,34 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
                     err = true;
                 continue;
             }
+            const int ntile = readlane(im.ntile, j);
+            if (ntile > 0) { // tile_image (basic-abstract-game.cpp:849-877): tiles left to right / top to bottom
+                const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
+                const float tw = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j));
+                const float th = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.th), j));
+                const int vert = readlane(im.rslot, j); // 1: vertical tiling (negative ratio)
+                const uint32_t offj = (uint32_t)readlane(im.soff, j);
+                const int swj = readlane(im.sw, j), shj = readlane(im.sh, j), mirj = readlane(im.mir, j);
+                for (int t = 0; t < ntile; t++) {
+                    const double x = vert ? rx : rx + (double)(tw * (float)t);
+                    const double y = vert ? ry + (double)(th * (float)t) : ry;
+                    Axis ex, ey;
+                    if (axis_setup(x, (double)tw, swj, ex) && axis_setup(y, (double)th, shj, ey))
+                        blit_seq(fb, d, ex, ey, offj, swj, mirj, caj, err);
+                }
+                continue;
+            }
             const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
             if (nx * ny <= 64) {
                 if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
             } else {
-                const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
-                const uint32_t bxj = (uint32_t)readlane((int)im.ex.base, j), byj = (uint32_t)readlane((int)im.ey.base, j);
-                const int sxj = readlane(im.ex.step, j), syj = readlane(im.ey.step, j);
-                const uint32_t offj = (uint32_t)readlane(im.soff, j);
-                const int swj = readlane(im.sw, j), mirj = readlane(im.mir, j);
-                const float inv = 1.0f / (float)nx;
-                for (int p = lane; p < nx * ny; p += 64) {
-                    int py = (int)(((float)p + 0.5f) * inv);
-                    int pxx = p - py * nx;
-                    int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
-                    int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
-                    if (mirj) scol = swj - 1 - scol;
-                    const uint32_t idx = offj + (uint32_t)(srow * swj + scol);
-                    const int o = (ty + py) * PG_RES + tx + pxx;
-                    if (idx < npix && o >= 0 && o < PG_RES * PG_RES) fb[o] = blend_argb_pm(fb[o], d.pixels[idx], caj);
-                    else err = true;
-                }
+                Axis ex, ey;
+                ex.t1 = readlane(im.ex.t1, j); ex.n = nx; ex.base = (uint32_t)readlane((int)im.ex.base, j);
+                ex.step = readlane(im.ex.step, j);
+                ey.t1 = readlane(im.ey.t1, j); ey.n = ny; ey.base = (uint32_t)readlane((int)im.ey.base, j);
+                ey.step = readlane(im.ey.step, j);
+                blit_seq(fb, d, ex, ey, (uint32_t)readlane(im.soff, j), readlane(im.sw, j), readlane(im.mir, j), caj,
+                         err);
             }
             // no barrier between images: one wave issues its LDS operations in order
         }
@@ -461,6 +497,14 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
             rh = rh * 1.7415;
         }
     }
+    if constexpr (G == PG_GAME_LEAPER) {
+        if (img == PLAYER) { // leaper get_adjusted_image_rect (leaper.cpp:244-250)
+            rx = rx + rw * 0.0;
+            ry = ry + rh * -.275;
+            rw = rw * 1.0;
+            rh = rh * 1.55;
+        }
+    }
     int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
     im.ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
     im.mir = (flags & EF_REFLECTED) != 0;
@@ -482,6 +526,26 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
             im.rot = true;
             im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
         }
+    } else if (tile_aspect_ratio<G>(etype) != 0) {
+        float tile_ratio = tile_aspect_ratio<G>(etype);
+        int num_tiles;
+        if (tile_ratio < 0) {
+            tile_ratio = -1 * tile_ratio;
+            num_tiles = (int)(rh / (rw * tile_ratio));
+            if (num_tiles < 1) num_tiles = 1;
+            im.th = (float)(rh / num_tiles);
+            im.tw = (float)rw;
+            im.rslot = 1;
+        } else {
+            num_tiles = (int)(rw / (rh * tile_ratio));
+            if (num_tiles < 1) num_tiles = 1;
+            im.tw = (float)(rw / num_tiles);
+            im.th = (float)rh;
+            im.rslot = 0;
+        }
+        im.ntile = num_tiles;
+        im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
+        im.draw = true;
     } else if (axis_setup(rx, rw, sp.y, im.ex) && axis_setup(ry, rh, sp.z, im.ey)) {
         im.draw = true;
     }
@@ -897,6 +961,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
+        PG_CASE(PG_GAME_LEAPER)
     default: break;
     }
 #undef PG_CASE

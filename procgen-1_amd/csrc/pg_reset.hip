@@ -32,7 +32,16 @@ struct MinerScratch {
     int16_t dirt[35 * 35];      // dirt cells, then exit candidates
     uint8_t taken[35 * 35];     // simple_choose's std::set
 };
+// leaper's level build steps every entity ~300 times before the first frame (leaper.cpp:174-177):
+// the entity list lives in LDS for those steps (slot 0 = the agent) and goes to HBM once
+struct LeaperScratch {
+    float x[PG_CAP], y[PG_CAP], vx[PG_CAP], rx[PG_CAP], ry[PG_CAP];
+    int16_t born[PG_CAP];
+    int8_t theme[PG_CAP], type[PG_CAP];
+    float road[8], water[8]; // lane speeds (copied into PGEnv with static indices)
+};
 template <int G> struct Scratch { uint32_t dummy[1]; };
+template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
 template <> struct Scratch<PG_GAME_HEIST> { MGScratch mg; };
@@ -157,6 +166,14 @@ DEV void choose_world_dim(RCtx &c) {
         else if (d == PG_HARD) { c.s.main_width = 20; c.s.main_height = 20; }
         else if (d == PG_MEMORY) { c.s.main_width = 35; c.s.main_height = 35; }
         c.s.main_area = c.s.main_width * c.s.main_height;
+    }
+    if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:103-113
+        int d = c.s.opt_distribution_mode;
+        int world_dim = 20;
+        if (d == PG_EASY) world_dim = 9;
+        else if (d == PG_HARD) world_dim = 15;
+        c.s.main_width = world_dim;
+        c.s.main_height = world_dim;
     }
     if constexpr (G == PG_GAME_HEIST) { // heist.cpp:98-113
         int d = c.s.opt_distribution_mode;
@@ -938,6 +955,133 @@ DEV void climber_game_reset(RCtx &c) {
     }
 }
 
+// ------------------------------------------------------------------ leaper (leaper.cpp:115-218)
+DEV float lp_rand_sign(RCtx &c) { return (double)rand01(c) < 0.5 ? 1.0f : -1.0f; } // :91-97
+DEV int lp_extra_space(RCtx &c) { return c.s.opt_distribution_mode == PG_EASY ? 0 : randn(c, 2); }
+
+// has_any_collision over the LDS entity list (no leaper entity avoids collisions)
+DEV bool lp_collides(const LeaperScratch *L, int n, float x, float y, float rx, float ry) {
+    bool hit = false;
+    for (int k = LANE; k < n; k += 64) {
+        float tx = (rx + L->rx[k]) + 0.0f, ty = (ry + L->ry[k]) + 0.0f;
+        if ((fabsf(x - L->x[k]) < tx) && (fabsf(y - L->y[k]) < ty)) hit = true;
+    }
+    return ballot(hit) != 0;
+}
+
+DEV void lp_push(LeaperScratch *L, int &n, int cap, float x, float y, float vx, float rx, float ry, int type, int theme,
+                 int born, bool &overflow) {
+    if (n >= cap) {
+        overflow = true;
+        return;
+    }
+    if (LANE == 0) {
+        L->x[n] = x; L->y[n] = y; L->vx[n] = vx; L->rx[n] = rx; L->ry[n] = ry;
+        L->type[n] = (int8_t)type; L->theme[n] = (int8_t)theme; L->born[n] = (int16_t)born;
+    }
+    wave_sync();
+    n++;
+}
+
+DEV void leaper_game_reset(RCtx &c, LeaperScratch *L) {
+    base_game_reset<PG_GAME_LEAPER>(c);
+    c.s.opt_center_agent = 0;
+    EF(c, F_Y, 0) = EF(c, F_RY, 0);
+    const int dm = c.s.opt_distribution_mode;
+    float min_car_speed = 0.05f, max_car_speed = 0.2f, min_log_speed = 0.05f, max_log_speed = 0.1f;
+    if (dm == PG_EASY) {
+        min_car_speed = 0.03f; max_car_speed = 0.12f; min_log_speed = 0.025f; max_log_speed = 0.075f;
+    } else if (dm == PG_EXTREME) {
+        min_car_speed = 0.1f; max_car_speed = 0.3f; min_log_speed = 0.1f; max_log_speed = 0.2f;
+    }
+    const int w = c.s.main_width;
+    c.s.bottom_road_y = lp_extra_space(c) + 1;
+    const int max_diff = dm == PG_EASY ? 3 : 4;
+    const int difficulty = randn(c, max_diff + 1);
+    const int extra_lane_option = dm == PG_EASY ? 0 : randn(c, 4);
+    c.s.num_road_lanes = difficulty + (extra_lane_option == 2 ? 1 : 0);
+    for (int lane = 0; lane < c.s.num_road_lanes; lane++) {
+        // rand_sign() * randrange(): g++ evaluates the left operand first (pinned,
+        // tests/test_oracle_pins.py::test_leaper_operand_order_pinned)
+        const float sgn = lp_rand_sign(c);
+        const float spd = rand01(c) * (max_car_speed - min_car_speed) + min_car_speed;
+        if (LANE == 0) L->road[lane] = sgn * spd;
+        fill_elem(c, 0, c.s.bottom_road_y + lane, w, 1, LP_ROAD);
+    }
+    c.s.bottom_water_y = c.s.bottom_road_y + c.s.num_road_lanes + lp_extra_space(c) + 1;
+    c.s.num_water_lanes = difficulty + (extra_lane_option == 3 ? 1 : 0);
+    int curr_sign = (int)lp_rand_sign(c);
+    for (int lane = 0; lane < c.s.num_water_lanes; lane++) {
+        const float spd = rand01(c) * (max_log_speed - min_log_speed) + min_log_speed;
+        if (LANE == 0) L->water[lane] = curr_sign * spd;
+        curr_sign *= -1;
+        fill_elem(c, 0, c.s.bottom_water_y + lane, w, 1, LP_WATER);
+    }
+    c.s.goal_y = c.s.bottom_water_y + c.s.num_water_lanes + 1;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        c.s.road_lane_speeds[k] = k < c.s.num_road_lanes ? L->road[k] : 0.0f;
+        c.s.water_lane_speeds[k] = k < c.s.num_water_lanes ? L->water[k] : 0.0f;
+    }
+
+    // initial entities: spawn_entities + step_entities (no erase) while i < main_width / min(speed)
+    int n = 0;
+    bool overflow = false;
+    lp_push(L, n, PG_CAP - 1, EF(c, F_X, 0), EF(c, F_Y, 0), 0, EF(c, F_RX, 0), EF(c, F_RY, 0), PLAYER, 0, 0, overflow);
+    const float mn = min_car_speed < min_log_speed ? min_car_speed : min_log_speed;
+    const int ncar_themes = c.d.num_themes[LP_CAR];
+    int iters = 0;
+    for (int i = 0; (float)i < w / mn; i++) {
+        for (int lane = 0; lane < c.s.num_road_lanes; lane++) {
+            const float speed = L->road[lane];
+            const float spawn_prob = (float)(fabs((double)speed) / 6.0);
+            if (rand01(c) < spawn_prob) {
+                const float x = speed > 0 ? (-1 * LP_MONSTER_RADIUS) : (w + LP_MONSTER_RADIUS);
+                const float y = (float)(c.s.bottom_road_y + lane + 0.5);
+                const int theme = randn(c, ncar_themes); // choose_random_theme before the check
+                if (!lp_collides(L, n, x, y, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS))
+                    lp_push(L, n, PG_CAP - 1, x, y, speed, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS, LP_CAR, theme, i,
+                            overflow);
+            }
+        }
+        for (int lane = 0; lane < c.s.num_water_lanes; lane++) {
+            const float speed = L->water[lane];
+            const float spawn_prob = (float)(fabs((double)speed) / 2.0);
+            if (rand01(c) < spawn_prob) {
+                const float x = speed > 0 ? (-1 * LP_LOG_RADIUS) : (w + LP_LOG_RADIUS);
+                const float y = (float)(c.s.bottom_water_y + lane + 0.5);
+                if (!lp_collides(L, n, x, y, LP_LOG_RADIUS, LP_LOG_RADIUS))
+                    lp_push(L, n, PG_CAP - 1, x, y, speed, LP_LOG_RADIUS, LP_LOG_RADIUS, LP_LOG, 0, i, overflow);
+            }
+        }
+        // Entity::step of every non-smart entity: x += vx (vy = 0); the agent (smart, at rest) stays
+        for (int k = 1 + LANE; k < n; k += 64) L->x[k] = L->x[k] + L->vx[k];
+        wave_sync();
+        iters++;
+    }
+    if (overflow) c.s.error = PG_ERR_ENTITY_OVERFLOW;
+    // the list to HBM: Entity ctor defaults (entity.cpp:8-47) + what the build set
+    for (int k = 1 + LANE; k < n; k += 64) {
+        const int type = L->type[k];
+        const float vx = L->vx[k];
+        EF(c, F_X, k) = L->x[k]; EF(c, F_Y, k) = L->y[k]; EF(c, F_VX, k) = vx; EF(c, F_VY, k) = 0;
+        EF(c, F_RX, k) = L->rx[k]; EF(c, F_RY, k) = L->ry[k];
+        EF(c, F_ROTATION, k) = (type == LP_CAR && vx < 0) ? PI_F : 0.0f;
+        EF(c, F_VROT, k) = 0;
+        EF(c, F_ALPHA, k) = 1.0f; EF(c, F_ALPHA_DECAY, k) = 1.0f; EF(c, F_GROW_RATE, k) = 1.0f;
+        EF(c, F_FRICTION, k) = 1; EF(c, F_COLLISION_MARGIN, k) = 0; EF(c, F_HEALTH, k) = 1;
+        EF(c, F_THETA, k) = -100; EF(c, F_CLIMBER_SPAWN_X, k) = 0;
+        EI(c, F_TYPE, k) = type; EI(c, F_IMAGE_TYPE, k) = type; EI(c, F_IMAGE_THEME, k) = L->theme[k];
+        EI(c, F_RENDER_Z, k) = 0; EI(c, F_LIFE_TIME, k) = iters - L->born[k]; EI(c, F_EXPIRE_TIME, k) = -1;
+        EI(c, F_FIRE_TIME, k) = -1; EI(c, F_SPAWN_TIME, k) = -1; EI(c, F_FLAGS, k) = EF_AUTO_ERASE;
+    }
+    if (LANE == 0) EI(c, F_LIFE_TIME, 0) = iters;
+    wave_sync();
+    c.s.num_ents = n;
+    add_entity_rxy(c, (float)(w / 2.0), (float)(c.s.goal_y - .5), 0, 0, (float)(w / 2.0), .5f, LP_FINISH_LINE);
+}
+
 // ------------------------------------------------------------------ Game::reset
 template <int G>
 DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial) {
@@ -977,6 +1121,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_HEIST) heist_game_reset(c, &scratch->mg);
     if constexpr (G == PG_GAME_MINER) miner_game_reset(c, &scratch->mn);
     if constexpr (G == PG_GAME_CLIMBER) climber_game_reset(c);
+    if constexpr (G == PG_GAME_LEAPER) leaper_game_reset(c, &scratch->lp);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1077,6 +1222,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
+        PG_CASE(PG_GAME_LEAPER)
     default: break;
     }
 #undef PG_CASE

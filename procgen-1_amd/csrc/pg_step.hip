@@ -629,6 +629,16 @@ DEV float clip_abs(float x, float y) {
     return x;
 }
 
+// decay_vel (leaper.cpp:220-226); VEL_DECAY = MAX_SPEED / NSTEP in float
+DEV float lp_decay_vel(float vel) {
+    const float vel_decay = (float)(2 / (LP_NSTEP - 1.0)) / LP_NSTEP;
+    float x = (float)(1.0 * vel);
+    float vel_sign = x > 0 ? +1 : (x == 0 ? 0 : -1);
+    vel = fabsf(vel) - vel_decay;
+    if (vel < 0) vel = 0;
+    return vel * vel_sign;
+}
+
 template <int G>
 DEV void update_agent_velocity(Ctx &c) {
     float vx = EF(c, F_VX, 0), vy = EF(c, F_VY, 0);
@@ -652,6 +662,20 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!c.s.has_support) {
             if (vy > -2) vy -= c.s.gravity;
         }
+    } else if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:228-244
+        if (vx == 0 && vy == 0) {
+            if (c.s.action_vx != 0) {
+                vx = c.s.maxspeed * c.s.action_vx;
+                EI(c, F_IMAGE_THEME, 0) = 1;
+                EF(c, F_ROTATION, 0) = (vx > 0 ? 1 : -1) * PI_F / 2;
+            } else if (c.s.action_vy != 0) {
+                vy = c.s.maxspeed * c.s.action_vy;
+                EI(c, F_IMAGE_THEME, 0) = 1;
+                EF(c, F_ROTATION, 0) = vy > 0 ? 0 : PI_F;
+            }
+        }
+        vx = lp_decay_vel(vx);
+        vy = lp_decay_vel(vy);
     } else { // basic-abstract-game.cpp:678-693 (get_agent_acceleration_scale() = 1)
         const float v_scale = 1.0f;
         vx = (1 - c.s.mixrate) * vx;
@@ -702,6 +726,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:76-84
+        if (t == LP_CAR) {
+            c.s.sd_done = 1;
+        } else if (t == LP_FINISH_LINE && EF(c, F_VX, 0) == 0 && EF(c, F_VY, 0) == 0) {
+            c.s.sd_reward += 10; // GOAL_REWARD (const int)
+            c.s.sd_done = 1;
+            c.s.sd_level_complete = 1;
         }
     } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:93-103
         if (t == CL_ENEMY) {
@@ -1181,9 +1213,97 @@ DEV void miner_step_tail(Ctx &c) { // miner.cpp:262-307
     }
 }
 
+// has_any_collision(e, 0) (basic-abstract-game.cpp:1123-1133) of a not-yet-added entity
+DEV bool any_collision(Ctx &c, float x, float y, float rx, float ry) {
+    bool hit = false;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        int i = base + LANE;
+        if (i < c.s.num_ents && !(EI(c, F_FLAGS, i) & EF_AVOIDS)) {
+            float tx = (rx + EF(c, F_RX, i)) + 0.0f, ty = (ry + EF(c, F_RY, i)) + 0.0f;
+            if ((fabsf(x - EF(c, F_X, i)) < tx) && (fabsf(y - EF(c, F_Y, i)) < ty)) hit = true;
+        }
+    }
+    return ballot(hit) != 0;
+}
+
+// spawn_entities (leaper.cpp:184-218)
+DEV void lp_spawn_entities(Ctx &c, uint32_t *rg) {
+    for (int lane = 0; lane < c.s.num_road_lanes; lane++) {
+        const float speed = c.d.envs[c.env].road_lane_speeds[lane]; // read-only here (HBM: no dynamic index into c.s)
+        const float spawn_prob = (float)(fabs((double)speed) / 6.0);
+        if (rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) < spawn_prob) {
+            const float x = speed > 0 ? (-1 * LP_MONSTER_RADIUS) : (c.s.main_width + LP_MONSTER_RADIUS);
+            const float y = (float)(c.s.bottom_road_y + lane + 0.5);
+            const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[LP_CAR]);
+            if (!any_collision(c, x, y, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS)) {
+                int i = append_entity(c, x, y, speed, 0, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS, LP_CAR);
+                if (i >= 0) {
+                    EI(c, F_IMAGE_THEME, i) = theme;
+                    if (speed < 0) EF(c, F_ROTATION, i) = PI_F;
+                }
+            }
+            wave_sync();
+        }
+    }
+    for (int lane = 0; lane < c.s.num_water_lanes; lane++) {
+        const float speed = c.d.envs[c.env].water_lane_speeds[lane];
+        const float spawn_prob = (float)(fabs((double)speed) / 2.0);
+        if (rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) < spawn_prob) {
+            const float x = speed > 0 ? (-1 * LP_LOG_RADIUS) : (c.s.main_width + LP_LOG_RADIUS);
+            const float y = (float)(c.s.bottom_water_y + lane + 0.5);
+            if (!any_collision(c, x, y, LP_LOG_RADIUS, LP_LOG_RADIUS))
+                append_entity(c, x, y, speed, 0, LP_LOG_RADIUS, LP_LOG_RADIUS, LP_LOG);
+            wave_sync();
+        }
+    }
+}
+
+DEV void leaper_pre_step(Ctx &c) { // leaper.cpp:253-256 (frog animation)
+    const int th = EI(c, F_IMAGE_THEME, 0);
+    wave_sync();
+    if (th >= 1) EI(c, F_IMAGE_THEME, 0) = (th + 1) % LP_NSTEP;
+    wave_sync();
+}
+
+DEV void leaper_step_tail(Ctx &c, uint32_t *rg) { // leaper.cpp:258-287
+    lp_spawn_entities(c, rg);
+    const bool gh = c.s.agent_erased; // the reference's `agent` outlives its erase
+    const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+    const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
+    const float avx = gh ? c.s.ghost_vx : EF(c, F_VX, 0), avy = gh ? c.s.ghost_vy : EF(c, F_VY, 0);
+    // the last LOG (list order) the agent stands on gives log_vx
+    const float margin = -1 * arx;
+    int last = -1;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        int i = base + LANE;
+        bool hit = false;
+        if (i < c.s.num_ents && EI(c, F_TYPE, i) == LP_LOG) {
+            float tx = (arx + EF(c, F_RX, i)) + margin, ty = (ary + EF(c, F_RY, i)) + margin;
+            hit = (fabsf(ax - EF(c, F_X, i)) < tx) && (fabsf(ay - EF(c, F_Y, i)) < ty);
+        }
+        unsigned long long b = ballot(hit);
+        if (b) last = base + top_bit(b);
+    }
+    const bool standing_on_log = last >= 0;
+    const float log_vx = standing_on_log ? EF(c, F_VX, last) : 0.0f;
+    if (get_obj(c, (int)ax, (int)ay) == LP_WATER) {
+        if (!standing_on_log && avx == 0 && avy == 0) c.s.sd_done = 1;
+    }
+    float nx = ax;
+    if (standing_on_log) nx = ax + log_vx;
+    wave_sync();
+    if (standing_on_log) {
+        if (gh) c.s.ghost_x = nx;
+        else EF(c, F_X, 0) = nx;
+    }
+    if (is_out_of_bounds(c, nx, ay, arx, ary)) c.s.sd_done = 1;
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ game_step
 template <int G>
 DEV void game_step(Ctx &c) {
+    if constexpr (G == PG_GAME_LEAPER) leaper_pre_step(c);
     // miner moves the objects at or below the agent's row before the agent (miner.cpp:250-260)
     if constexpr (G == PG_GAME_MINER) miner_pre_step(c);
     // ---- BasicAbstractGame::game_step (basic-abstract-game.cpp:695-755)
@@ -1239,6 +1359,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_HEIST) heist_step_tail(c);
     if constexpr (G == PG_GAME_MINER) miner_step_tail(c);
     if constexpr (G == PG_GAME_CLIMBER) climber_step_tail(c);
+    if constexpr (G == PG_GAME_LEAPER) leaper_step_tail(c, rg);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1359,6 +1480,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_HEIST)
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
+        PG_CASE(PG_GAME_LEAPER)
     default: break;
     }
 #undef PG_CASE

@@ -175,6 +175,17 @@ CLIMBER_SPRITES = {
     1: ["platformer/yellowCrystal.png"],
 }
 
+# ---------------------------------------------------------------- leaper
+# procgen/src/games/leaper.cpp:45-66 (LOG 1, ROAD 2, WATER 3, CAR 4, FINISH_LINE 5, PLAYER 0)
+LEAPER_SPRITES = {
+    2: ["misc_assets/roadTile6b.png"],
+    3: ["misc_assets/terrainTile6.png"],
+    4: ["misc_assets/car_%s.png" % c for c in ("yellow_5", "black_1", "blue_2", "green_3", "red_4")],
+    1: ["misc_assets/elementWood044.png"],
+    0: ["misc_assets/frog%d.png" % i for i in (1, 2, 4, 6, 7)],
+    5: ["misc_assets/finish2.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -183,6 +194,7 @@ GAMES = {
     "heist": (HEIST_SPRITES, "topdown"),        # heist.cpp:37-39
     "miner": (MINER_SPRITES, "caves"),          # miner.cpp:45-47
     "climber": (CLIMBER_SPRITES, "platform"),   # climber.cpp:43-45
+    "leaper": (LEAPER_SPRITES, "topdown"),      # leaper.cpp:41-43
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -26,7 +26,7 @@ def make_gpu(num, env_name, **kw):
 def oracle_kw(gpu_kw):
     kw = dict(gpu_kw)
     dm = kw.pop("distribution_mode", "hard")
-    kw["distribution_mode"] = {"easy": 0, "hard": 1, "memory": 10}[dm]
+    kw["distribution_mode"] = {"easy": 0, "hard": 1, "extreme": 2, "memory": 10}[dm]
     for k in ("center_agent", "use_backgrounds", "restrict_themes", "use_sequential_levels"):
         if k in kw:
             kw[k] = int(kw[k])
@@ -66,12 +66,12 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper"])
 def test_parity_hard_unbounded(game):
     run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper"])
 def test_parity_200_levels_easy(game):
     run_pair(game, 8, 200, seed=2, num_levels=200, start_level=0, rand_seed=5, distribution_mode="easy",
              latent=game in LATENT)
@@ -90,7 +90,7 @@ def test_miner_long_run_deaths():
     assert episodes > 0
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper"])
 def test_parity_options(game):
     run_pair(game, 8, 150, seed=4, num_levels=20, rand_seed=3, use_backgrounds=False, restrict_themes=True,
              use_sequential_levels=True)
@@ -101,6 +101,13 @@ def test_climber_uncentered():
     run_pair("climber", 8, 200, seed=11, num_levels=0, rand_seed=6, center_agent=False)
 
 
+def test_leaper_extreme_and_long():
+    """leaper extreme mode (leaper-only, game.cpp:80-81; 20x20 world, fast lanes) and a long
+    hard-mode run: cars (rotated PI when driving left), logs carrying the frog, finish line tiles."""
+    run_pair("leaper", 16, 300, seed=12, num_levels=0, rand_seed=7, distribution_mode="extreme")
+    run_pair("leaper", 32, 500, seed=13, num_levels=0, rand_seed=8)
+
+
 def test_bigfish_long_episodes():
     """bigfish episodes run up to 6,000 steps (bigfish.cpp:25): many fish spawn, grow, leave."""
     run_pair("bigfish", 8, 1200, seed=6, num_levels=0, rand_seed=12)
@@ -108,8 +115,8 @@ def test_bigfish_long_episodes():
 
 def test_mixed_batch_parity():
     """env n plays names[n % 4] (vecgame.cpp:357-358), level seeds from the global index."""
-    names = ["bigfish", "climber", "coinrun", "heist", "maze", "miner"]
-    num = 24
+    names = ["bigfish", "climber", "coinrun", "heist", "leaper", "maze", "miner"]
+    num = 28
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=21)
     orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
     g = gpu_obs(env)
@@ -146,7 +153,7 @@ def test_full_size_sampled_parity(game):
     env.close()
 
 
-@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber"])
+@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber", "leaper"])
 def test_state_roundtrip(game):
     env = make_gpu(4, game, num_levels=20, rand_seed=11)
     rng = np.random.RandomState(1)

@@ -234,3 +234,21 @@ def test_argument_evaluation_order_pinned():
         vdraw, ydraw = int(draws[0]), int(draws[1])
         assert out[0] == np.float32(0 + ydraw + 2 + .5)
         assert out[1] == np.float32(.15 * (vdraw * 2 - 1))
+
+
+def test_leaper_operand_order_pinned():
+    """leaper.cpp:155 multiplies rand_sign() by randrange(): g++ evaluates the left operand
+    first (the sign's rand01 is the first draw); the oracle and engine follow that order."""
+    ref = ref_lib()
+    ref.ref_leaper_lane_speed.argtypes = [ctypes.c_int32, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+    lib = oracle_lib.load()
+    for seed in range(256):
+        out = np.zeros(1, np.float32)
+        ref.ref_leaper_lane_speed(seed, 0.05, 0.2, out.ctypes.data)
+        ops = np.array([[2, 0, 0], [2, 0, 0]], np.int32)
+        draws = np.zeros(2, np.int32)
+        lib.oracle_randgen_script(seed & 0xFFFFFFFF, ops.ctypes.data, 2, draws.ctypes.data)
+        u = draws.view(np.float32)
+        sign = np.float32(1.0) if u[0] < 0.5 else np.float32(-1.0)
+        spd = np.float32(u[1] * np.float32(np.float32(0.2) - np.float32(0.05)) + np.float32(0.05))
+        assert out[0] == sign * spd, seed
