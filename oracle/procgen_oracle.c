@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
@@ -236,6 +236,10 @@ typedef struct {
     /* climber (climber.cpp:30-36; has_support, facing_right, wall_theme, gravity, air_control shared
      * with coinrun's members above) */
     int coin_quota, coins_collected;
+    /* chaser (chaser.cpp:26-35; free_cells / is_space_vec of the last reset) */
+    int eat_timeout, egg_timeout, eat_time, total_enemies, total_orbs, orbs_collected, num_free;
+    int free_list[MAX_GRID];
+    bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
     int bottom_road_y, bottom_water_y, goal_y, num_road_lanes, num_water_lanes;
     float road_lane_speeds[8], water_lane_speeds[8];
@@ -347,6 +351,10 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
         if (src->type == PLAYER && cr_is_wall(target)) return true;
         return false;
     }
+    if (g->game_id == GAME_CHASER) { /* chaser.cpp:94-99: MAZE_WALL 5 */
+        if (target == 5) return true;
+        return base;
+    }
     if (g->game_id == GAME_CLIMBER) { /* climber.cpp:147-154: WALL_MID 15, WALL_TOP 16 */
         if (base) return true;
         if (src->type == PLAYER && (target == 15 || target == 16)) return true;
@@ -420,6 +428,15 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
             }
+        }
+    } else if (g->game_id == GAME_CHASER) { /* chaser.cpp:119-133: LARGE_ORB 2, ENEMY 6 */
+        if (obj->type == 2) {
+            g->eat_time = g->cur_time;
+            g->sd_reward += 0.04f; /* ORB_REWARD */
+            obj->will_erase = true;
+        } else if (obj->type == 6) {
+            if (g->cur_time - g->eat_time < g->eat_timeout) obj->will_erase = true;
+            else g->sd_done = true;
         }
     } else if (g->game_id == GAME_LEAPER) { /* leaper.cpp:69-77: CAR 4, FINISH_LINE 5 */
         Entity *agent = AG(g);
@@ -504,6 +521,12 @@ static int hook_image_for_type(Game *g, int type) {
         } else if (type == CR_ENEMY_BARRIER) {
             return -1;
         }
+    }
+    if (g->game_id == GAME_CHASER && type == 6) { /* chaser.cpp:101-113: ENEMY */
+        if (g->cur_time - g->eat_time < g->eat_timeout) return 3; /* ENEMY_WEAK */
+        int rem = (g->cur_time / 2) % 4;
+        if (rem == 3) rem = 1;
+        return 6 + rem;
     }
     if (g->game_id == GAME_CLIMBER) { /* climber.cpp:156-170 */
         if (type == PLAYER) {
@@ -752,6 +775,7 @@ static float clip_abs(float x, float y) { /* cpp-utils.h:46-52 */
 }
 
 static void lp_decay_vel(float *vel);
+static double cu_sign(double x);
 static void update_agent_velocity(Game *g) {
     Entity *agent = AG(g);
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:156-173 */
@@ -767,6 +791,13 @@ static void update_agent_velocity(Game *g) {
             agent->vy -= g->gravity;
             agent->vy = clip_abs(agent->vy, g->max_jump);
         }
+        return;
+    }
+    if (g->game_id == GAME_CHASER) { /* chaser.cpp:83-92 (cpp-utils sign, double) */
+        if (g->action_vx != 0) agent->vx = g->maxspeed * g->action_vx;
+        if (g->action_vy != 0) agent->vy = g->maxspeed * g->action_vy;
+        agent->vx = (float)(cu_sign(agent->vx) * g->maxspeed);
+        agent->vy = (float)(cu_sign(agent->vy) * g->maxspeed);
         return;
     }
     if (g->game_id == GAME_LEAPER) { /* leaper.cpp:228-244 */
@@ -1831,6 +1862,215 @@ static void climber_game_step(Game *g) { /* :320-346 */
     }
 }
 
+/* ================================================================== chaser (games/chaser.cpp) */
+static const float CH_ORB_REWARD = 0.04f;
+static const float CH_COMPLETION_BONUS = 10.0f;
+static const float CH_ORB_DIM = 0.3f;
+#define CH_LARGE_ORB 2
+#define CH_ENEMY_WEAK 3
+#define CH_ENEMY_EGG 4
+#define CH_MAZE_WALL 5
+#define CH_ENEMY 6
+#define CH_MARKER 1001
+#define CH_ORB 1002
+
+static double cu_sign(double x) { return x > 0 ? 1 : (x == 0 ? 0 : -1); } /* cpp-utils.h:43-45 */
+
+/* RandGen::simple_choose (randgen.cpp:70-88): rejection against a std::set */
+static void rg_simple_choose(MT *r, int n, int k, int *out) {
+    fassert(k <= n);
+    for (int i = 0; i < k; i++) {
+        int next = rg_randn(r, n);
+        for (;;) {
+            bool seen = false;
+            for (int j = 0; j < i; j++)
+                if (out[j] == next) seen = true;
+            if (!seen) break;
+            next = rg_randn(r, n);
+        }
+        out[i] = next;
+    }
+}
+
+static bool ch_can_eat_enemies(Game *g) { return g->cur_time - g->eat_time < g->eat_timeout; } /* :255-257 */
+
+static int ch_to_grid_idx(Game *g, int x, int y) { /* basic-abstract-game.cpp:187-192 */
+    if (!grid_contains(g, x, y)) return -2; /* INVALID_IDX */
+    return y * g->main_width + x;
+}
+
+static void ch_spawn_egg(Game *g, int enemy_cell) { /* :259-262 */
+    int e = add_entity(g, (float)((enemy_cell % g->maze_dim) + .5), (float)((enemy_cell / g->maze_dim) + .5), 0, 0, .5f,
+                       CH_ENEMY_EGG);
+    g->ents[e].health = (float)g->egg_timeout;
+}
+
+static void chaser_game_reset(Game *g, const or_atlas *at) { /* :147-252 */
+    MT *r = &g->rand_gen;
+    int extra_orb_sign = 1;
+    if (g->options.distribution_mode == EasyMode) {
+        g->maze_dim = 11; g->total_enemies = 3; extra_orb_sign = 0;
+    } else if (g->options.distribution_mode == HardMode) {
+        g->maze_dim = 13; g->total_enemies = 3; extra_orb_sign = -1;
+    } else if (g->options.distribution_mode == ExtremeMode) {
+        g->maze_dim = 19; g->total_enemies = 5; extra_orb_sign = 1;
+    } else {
+        fatal_msg("chaser: bad distribution mode");
+    }
+    g->main_width = g->maze_dim; /* choose_world_dim (:141-144) */
+    g->main_height = g->maze_dim;
+    basic_game_reset(g, at);
+    g->options.center_agent = false;
+    Entity *agent = AG(g);
+    agent->rx = .5f;
+    agent->ry = .5f;
+    g->eat_time = -1 * g->eat_timeout;
+    fill_elem(g, 0, 0, g->main_width, g->main_height, CH_MAZE_WALL);
+    static MazeGen mg;
+    mg_init(&mg, r, g->maze_dim);
+    mg_generate_maze_no_dead_ends(&mg);
+    const int md = g->maze_dim;
+    static int quad[4][MAX_GRID];
+    int qn[4] = {0, 0, 0, 0}, orbs_for_quadrant[4];
+    int extra_quad = rg_randn(r, 4);
+    for (int i = 0; i < 4; i++) orbs_for_quadrant[i] = 1 + (i == extra_quad ? extra_orb_sign : 0);
+    for (int i = 0; i < md; i++) {
+        for (int j = 0; j < md; j++) {
+            int obj = mg_gridget(&mg, i + MAZE_OFFSET, j + MAZE_OFFSET);
+            set_obj(g, i, j, obj == WALL_OBJ ? CH_MAZE_WALL : obj);
+            if (obj == SPACE) {
+                int idx = j * md + i;
+                int quad_idx = (i >= md / 2.0 ? 1 : 0) * 2 + (j >= md / 2.0 ? 1 : 0);
+                quad[quad_idx][qn[quad_idx]++] = idx;
+            }
+        }
+    }
+    for (int i = 0; i < 4; i++) {
+        int sel[8];
+        fassert(orbs_for_quadrant[i] <= 8);
+        rg_simple_choose(r, qn[i], orbs_for_quadrant[i], sel);
+        for (int j = 0; j < orbs_for_quadrant[i]; j++) {
+            int cell = quad[i][sel[j]];
+            add_entity(g, (float)((cell % g->main_width) + .5), (float)((cell / g->main_width) + .5), 0, 0, 0.4f,
+                       CH_LARGE_ORB); /* spawn_entity_at_idx (:587-594) */
+            set_obj_idx(g, cell, CH_MARKER);
+        }
+    }
+    static int free_cells[MAX_GRID];
+    int nfree = 0;
+    for (int i = 0; i < g->grid_size; i++)
+        if (g->grid[i] == SPACE) free_cells[nfree++] = i; /* get_cells_with_type (:205-215) */
+    int sel[8];
+    fassert(1 + g->total_enemies <= 8);
+    rg_simple_choose(r, nfree, 1 + g->total_enemies, sel);
+    int start = free_cells[sel[0]];
+    agent->x = (float)((start % md) + .5);
+    agent->y = (float)((start / md) + .5);
+    for (int i = 0; i < g->total_enemies; i++) {
+        int cell = free_cells[sel[i + 1]];
+        set_obj_idx(g, cell, CH_MARKER);
+        ch_spawn_egg(g, cell);
+    }
+    for (int k = 0; k < nfree; k++) set_obj_idx(g, free_cells[k], CH_ORB);
+    g->total_orbs = nfree;
+    g->orbs_collected = 0;
+    for (int i = 0; i < g->grid_size; i++)
+        if (g->grid[i] == CH_MARKER) g->grid[i] = SPACE;
+    g->num_free = 0;
+    for (int i = 0; i < g->grid_size; i++) {
+        bool is_space = g->grid[i] != CH_MAZE_WALL;
+        if (is_space) g->free_list[g->num_free++] = i;
+        g->is_space[i] = is_space;
+    }
+}
+
+static void chaser_game_step(Game *g) { /* :286-376 */
+    basic_game_step(g);
+    int num_enemies = 0;
+    float default_enemy_speed = .5;
+    float vscale = ch_can_eat_enemies(g) ? (default_enemy_speed * .5f) : default_enemy_speed;
+    Entity *agent = AG(g);
+    for (int j = g->num_ents - 1; j >= 0; j--) {
+        Entity *ent = &g->ents[j];
+        if (ent->type == CH_ENEMY_EGG) {
+            num_enemies++;
+            ent->health -= 1;
+            if (ent->health == 0) {
+                ent->will_erase = true;
+                fassert(g->num_ents < MAX_ENTS); /* spawn_child (:233-239) */
+                Entity child;
+                entity_init(&child, ent->x, ent->y, 0, 0, .5f, .5f, CH_ENEMY);
+                child.smart_step = true;
+                g->ents[g->num_ents++] = child;
+                ent = &g->ents[j];
+                agent = AG(g);
+            }
+        } else if (ent->type == CH_ENEMY) {
+            num_enemies++;
+            float x = (float)(ent->x - .5);
+            float y = (float)(ent->y - .5);
+            int dist_scale = ch_can_eat_enemies(g) ? -1 : 1;
+            int enemy_idx = ch_to_grid_idx(g, (int)x, (int)y);
+            int agent_idx = ch_to_grid_idx(g, (int)agent->x, (int)agent->y);
+            bool is_at_junction = fabs(x - round(x)) + fabs(y - round(y)) < .01;
+            bool be_agressive = g->step_rand_int % 2 == 0;
+            if ((ent->vx == 0 && ent->vy == 0) || is_at_junction) {
+                int adj[4], nadj = 0, sn[4], nsn = 0;
+                int prev_idx = ch_to_grid_idx(g, (int)(x - cu_sign(ent->vx)), (int)(y - cu_sign(ent->vy)));
+                int ex = enemy_idx % g->main_width, ey = enemy_idx / g->main_width; /* get_adjacent (:269-284) */
+                for (int i = -1; i <= 1; i++)
+                    for (int jj = -1; jj <= 1; jj++) {
+                        if (i == 0 && jj == 0) continue;
+                        if (i != 0 && jj != 0) continue;
+                        int nb = ch_to_grid_idx(g, ex + i, ey + jj);
+                        if (nb != -2) adj[nadj++] = nb;
+                    }
+                int min_dist = 2 * g->main_width;
+                for (int k = 0; k < nadj; k++) {
+                    int a = adj[k];
+                    if (g->is_space[a] && a != prev_idx) {
+                        int md = (abs((a % g->main_width) - (agent_idx % g->main_width)) +
+                                  abs((a / g->main_width) - (agent_idx / g->main_width))) * dist_scale;
+                        if (be_agressive) {
+                            if (md < min_dist) {
+                                min_dist = md;
+                                nsn = 0;
+                                sn[nsn++] = a;
+                            } else if (md == min_dist) {
+                                sn[nsn++] = a;
+                            }
+                        } else {
+                            sn[nsn++] = a;
+                        }
+                    }
+                }
+                fassert(nsn > 0);
+                int neighbor = sn[(unsigned long)g->step_rand_int % (unsigned long)nsn];
+                int nx = neighbor % g->main_width;
+                int ny = neighbor / g->main_width;
+                ent->vx = (nx - x) * vscale;
+                ent->vy = (ny - y) * vscale;
+            }
+        }
+    }
+    if (num_enemies < g->total_enemies) {
+        int selected_idx = (int)((unsigned long)g->step_rand_int % (unsigned long)g->num_free);
+        ch_spawn_egg(g, g->free_list[selected_idx]);
+    }
+    agent = AG(g);
+    int agent_idx = (int)agent->y * g->main_width + (int)agent->x; /* get_agent_index (:176-178) */
+    if (get_obj_idx(g, agent_idx) == CH_ORB) {
+        set_obj_idx(g, agent_idx, SPACE);
+        g->sd_reward += CH_ORB_REWARD;
+        g->orbs_collected += 1;
+    }
+    if (g->orbs_collected == g->total_orbs) {
+        g->sd_reward += CH_COMPLETION_BONUS;
+        g->sd_level_complete = true;
+        g->sd_done = true;
+    }
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -1977,6 +2217,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_MINER) miner_game_reset(g, at);
     else if (g->game_id == GAME_CLIMBER) climber_game_reset(g, at);
     else if (g->game_id == GAME_LEAPER) leaper_game_reset(g, at);
+    else if (g->game_id == GAME_CHASER) chaser_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -1987,6 +2228,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_MINER) miner_game_step(g);
     else if (g->game_id == GAME_CLIMBER) climber_game_step(g);
     else if (g->game_id == GAME_LEAPER) leaper_game_step(g, at);
+    else if (g->game_id == GAME_CHASER) chaser_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -2367,6 +2609,17 @@ static void qt_fill_rect_int(uint32_t *canvas, int x, int y, int w, int h, uint3
         for (int xx = x1; xx < x2; xx++) canvas[yy * RES_W + xx] = argb | 0xff000000u;
 }
 
+/* QPainter::fillRect(QRectF, QColor) with an opaque colour, no antialiasing, identity transform:
+ * the raster engine fills toNormalizedFillRect(r) = qRound of the four edges, normalised
+ * (qpaintengine_raster.cpp).  Pinned against Qt 5.9.7 (tests/golden/qt_raster_fill_goldens.npz). */
+static void qt_fill_rectf(uint32_t *canvas, double x, double y, double w, double h, uint32_t argb) {
+    int x1 = qRound(x), y1 = qRound(y);
+    int x2 = qRound(x + w), y2 = qRound(y + h);
+    if (x2 < x1) { int t = x1; x1 = x2; x2 = t; }
+    if (y2 < y1) { int t = y1; y1 = y2; y2 = t; }
+    qt_fill_rect_int(canvas, x1, y1, x2 - x1, y2 - y1, argb);
+}
+
 /* ================================================================== render (basic-abstract-game.cpp) */
 typedef struct { double x, y, w, h; } RectD;
 
@@ -2450,6 +2703,12 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
     if (g->options.use_monochrome_assets || img_type >= USE_ASSET_THRESHOLD) {
         /* draw_grid_obj: SPACE draws nothing; monochrome fills are restated in a later round */
         if (img_type == SPACE) return;
+        if (g->game_id == GAME_CHASER && img_type == CH_ORB) { /* chaser.cpp:111-117 */
+            float k = 1 - CH_ORB_DIM;
+            qt_fill_rectf(g->canvas, base.x + base.w * k / 2, base.y + base.h * k / 2, base.w * CH_ORB_DIM,
+                          base.h * CH_ORB_DIM, 0xff00ff00u);
+            return;
+        }
         fatal_msg("draw_grid_obj / monochrome not restated yet");
     }
     fassert(theme < MAX_IMAGE_THEMES);
@@ -2562,6 +2821,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "miner") == 0) return GAME_MINER;
     if (strcmp(name, "climber") == 0) return GAME_CLIMBER;
     if (strcmp(name, "leaper") == 0) return GAME_LEAPER;
+    if (strcmp(name, "chaser") == 0) return GAME_CHASER;
     return -1;
 }
 
@@ -2610,6 +2870,13 @@ static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
     g->out_of_bounds_object = WALL_OBJ;
     g->visibility = 8.0f;
 }
+static void chaser_ctor(Game *g) { /* chaser.cpp:37-47 */
+    g->mixrate = 1;
+    g->maxspeed = .5f;
+    g->eat_timeout = 75;
+    g->egg_timeout = 50;
+    g->has_useful_vel_info = false;
+}
 static void leaper_ctor(Game *g) { /* leaper.cpp:34-38 */
     g->maxspeed = LP_MAX_SPEED;
     g->timeout = 500;
@@ -2641,7 +2908,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
     /* game.cpp:76-86: easy and hard for every game; memory for heist and maze (of those restated) */
-    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == ExtremeMode && gid == GAME_LEAPER) ||
+    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == ExtremeMode && (gid == GAME_LEAPER || gid == GAME_CHASER)) ||
                  (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE || gid == GAME_MINER));
     if (!dm_ok) return NULL;
     Vec *v = (Vec *)calloc(1, sizeof(Vec));
@@ -2672,6 +2939,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_MINER) miner_ctor(g);
         else if (gid == GAME_CLIMBER) climber_ctor(g);
         else if (gid == GAME_LEAPER) leaper_ctor(g);
+        else if (gid == GAME_CHASER) chaser_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;
@@ -2883,6 +3151,7 @@ int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas) {
         } else {
             uint32_t col = rd_u32(&r);
             if (kind == 2) qt_fill_rect_int(canvas, (int)x, (int)y, (int)w, (int)h, col);
+            else if (kind == 1 && (col >> 24) == 0xff && opacity == 1.0) qt_fill_rectf(canvas, x, y, w, h, col);
             else return -2;
         }
     }

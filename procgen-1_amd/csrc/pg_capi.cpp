@@ -114,9 +114,10 @@ int game_id(const std::string &name) {
     if (name == "miner") return PG_GAME_MINER;
     if (name == "climber") return PG_GAME_CLIMBER;
     if (name == "leaper") return PG_GAME_LEAPER;
+    if (name == "chaser") return PG_GAME_CHASER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, climber, coinrun, heist, leaper, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, heist, leaper, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -171,6 +172,12 @@ void construct_env(PGEnv &s, int gid) {
         s.has_useful_vel_info = 0;
         s.out_of_bounds_object = 51; // WALL_OBJ
         s.visibility = 8.0f;
+    } else if (gid == PG_GAME_CHASER) { // chaser.cpp:37-47
+        s.mixrate = 1;
+        s.maxspeed = .5f;
+        s.eat_timeout = 75;
+        s.egg_timeout = 50;
+        s.has_useful_vel_info = 0;
     } else if (gid == PG_GAME_LEAPER) { // leaper.cpp:34-38 (MAX_SPEED = 2 / (NSTEP - 1.0))
         s.maxspeed = (float)(2 / (5 - 1.0));
         s.timeout = 500;
@@ -514,7 +521,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (gid < 0) return bad("env '" + nm + "' is not in this build (supported: " + SUPPORTED_GAMES + ")");
         // game.cpp:76-86 distribution mode validity
         bool dm_ok = distribution_mode == PG_EASY || distribution_mode == PG_HARD ||
-                     (distribution_mode == PG_EXTREME && gid == PG_GAME_LEAPER) ||
+                     (distribution_mode == PG_EXTREME && (gid == PG_GAME_LEAPER || gid == PG_GAME_CHASER)) ||
                      (distribution_mode == PG_MEMORY &&
                       (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE || gid == PG_GAME_MINER));
         if (!dm_ok) return bad("invalid distribution_mode for " + nm);

@@ -86,6 +86,14 @@
 #define CL_WALL_TOP 16
 #define CL_ENEMY_BARRIER 19
 DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
+// chaser.cpp:10-23
+#define CH_LARGE_ORB 2
+#define CH_ENEMY_WEAK 3
+#define CH_ENEMY_EGG 4
+#define CH_MAZE_WALL 5
+#define CH_ENEMY 6
+#define CH_MARKER 1001
+#define CH_ORB 1002
 // leaper.cpp:6-21
 #define LP_LOG 1
 #define LP_ROAD 2

@@ -22,7 +22,7 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
     PG_GAME_MINER = 12
 };
 #ifndef PG_NUM_GAMES
@@ -158,7 +158,15 @@ struct PGEnv {
     int32_t num_water_lanes;
     float road_lane_speeds[5];
     float water_lane_speeds[5];
-    int32_t pad[128 - 94];
+    // ---- chaser (chaser.cpp:26-35; free_cells / is_space_vec are derived from the grid: the
+    //      MAZE_WALL cells never change after the reset)
+    int32_t eat_timeout;
+    int32_t egg_timeout;
+    int32_t eat_time;
+    int32_t total_enemies;
+    int32_t total_orbs;
+    int32_t orbs_collected;
+    int32_t pad[128 - 100];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

@@ -106,7 +106,15 @@ DEV int player_image(const PGEnv &s, float agent_vx) {
     return PLAYER;
 }
 template <int G>
-DEV int image_for_type(int type, int player_img) {
+DEV int image_for_type(const PGEnv &s, int type, int player_img) {
+    if constexpr (G == PG_GAME_CHASER) { // chaser.cpp:101-113
+        if (type == CH_ENEMY) {
+            if (s.cur_time - s.eat_time < s.eat_timeout) return CH_ENEMY_WEAK;
+            int rem = (s.cur_time / 2) % 4;
+            if (rem == 3) rem = 1;
+            return CH_ENEMY + rem;
+        }
+    }
     if constexpr (G == PG_GAME_COINRUN || G == PG_GAME_CLIMBER) { // ENEMY_BARRIER is 19 in both
         if (type == PLAYER) return player_img;
         if (type == CR_ENEMY_BARRIER) return -1;
@@ -316,6 +324,7 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
 // in-order loop with inline loads; rotated images run the transform blit in place.
 struct Img {
     bool draw, rot;
+    uint32_t fill;         // != 0: an opaque fillRect of this colour over the ex / ey footprint
     Axis ex, ey;
     int soff, sw, sh, ca, mir, rslot, ez;
     int ntile;             // > 0: tile_image with this many tiles (seq path)
@@ -328,6 +337,7 @@ DEV void img_clear(Img &im) {
     im.rot = false;
     im.ntile = 0;
     im.tw = im.th = 0;
+    im.fill = 0;
     im.ex.t1 = im.ex.n = im.ey.t1 = im.ey.n = 0;
     im.ex.base = im.ey.base = 0;
     im.ex.step = im.ey.step = 0;
@@ -335,6 +345,35 @@ DEV void img_clear(Img &im) {
     im.ca = 256;
     im.ez = 0x7fffffff;
     im.rx = im.ry = im.rw = im.rh = 0;
+}
+
+// fillRect(QRectF, opaque colour) (qpaintengine_raster toNormalizedFillRect: qRound of the edges,
+// pinned vs Qt 5.9.7 by tests/golden/qt_raster_fill_goldens.npz), clipped to the frame
+DEV bool fill_setup(double x, double y, double w, double h, uint32_t argb, Img &im) {
+    int x1 = qRound(x), y1 = qRound(y), x2 = qRound(x + w), y2 = qRound(y + h);
+    if (x2 < x1) { int t = x1; x1 = x2; x2 = t; }
+    if (y2 < y1) { int t = y1; y1 = y2; y2 = t; }
+    x1 = max(x1, 0); y1 = max(y1, 0); x2 = min(x2, PG_RES); y2 = min(y2, PG_RES);
+    if (x1 >= x2 || y1 >= y2) return false;
+    im.ex.t1 = x1; im.ex.n = x2 - x1; im.ex.base = 0; im.ex.step = 0;
+    im.ey.t1 = y1; im.ey.n = y2 - y1; im.ey.base = 0; im.ey.step = 0;
+    im.fill = argb | 0xff000000u;
+    im.draw = true;
+    return true;
+}
+
+// draw_grid_obj overrides (basic-abstract-game.cpp:924-928): true when the game fills this
+// grid object itself (chaser's orbs, chaser.cpp:111-117)
+template <int G>
+DEV bool grid_obj_fill(int img, double rx, double ry, double rw, double rh, Img &im) {
+    if constexpr (G == PG_GAME_CHASER) {
+        if (img == CH_ORB) {
+            const float dim = 0.3f, k = 1 - dim;
+            fill_setup(rx + rw * k / 2, ry + rh * k / 2, rw * dim, rh * dim, 0xff00ff00u, im);
+            return true;
+        }
+    }
+    return false;
 }
 
 DEV double readlane_d(double x, int j) {
@@ -396,7 +435,12 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
                 if (readlane(im.mir, j)) scol = swj - 1 - scol;
                 const uint32_t idx = (uint32_t)readlane(im.soff, j) + (uint32_t)(srow * swj + scol);
                 const int o = (readlane(im.ey.t1, j) + py) * PG_RES + readlane(im.ex.t1, j) + pxx;
-                if (idx < npix && o >= 0 && o < PG_RES * PG_RES) {
+                const uint32_t fillj = (uint32_t)readlane((int)im.fill, j);
+                if (fillj != 0 && o >= 0 && o < PG_RES * PG_RES) {
+                    tv[g] = fillj;
+                    fo[g] = o;
+                    on[g] = true;
+                } else if (idx < npix && o >= 0 && o < PG_RES * PG_RES) {
                     tv[g] = d.pixels[idx];
                     fo[g] = o;
                     on[g] = true;
@@ -439,6 +483,10 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
             const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
             if (nx * ny <= 64) {
                 if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
+            } else if (readlane((int)im.fill, j) != 0) {
+                const uint32_t col = (uint32_t)readlane((int)im.fill, j);
+                const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
+                for (int p = lane; p < nx * ny; p += 64) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
             } else {
                 Axis ex, ey;
                 ex.t1 = readlane(im.ex.t1, j); ex.n = nx; ex.base = (uint32_t)readlane((int)im.ex.base, j);
@@ -469,7 +517,7 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
     int etype = EIr(d, F_TYPE, env, i);
     int itype = EIr(d, F_IMAGE_TYPE, env, i);
     int theme = EIr(d, F_IMAGE_THEME, env, i);
-    int img = image_for_type<G>(itype, player_img);
+    int img = image_for_type<G>(s, itype, player_img);
     if (img < 0 || !should_draw<G>(s, etype, theme)) return;
     if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
         if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
@@ -614,7 +662,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     //      generic tile pass (or flagged when met on the fast path)
     for (int t = lane; t < NTYPES; t += 64) {
         int off = -1;
-        int img = image_for_type<G>(t, player_img);
+        int img = image_for_type<G>(s, t, player_img);
         if (img >= 0) {
             if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
                 off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
@@ -893,10 +941,13 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                     const int x = low_x + k / wh, y = low_y + k % wh;
                     int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
                                                                                            : s.out_of_bounds_object;
-                    int img = type == INVALID_OBJ ? -1 : image_for_type<G>(type, player_img);
+                    int img = type == INVALID_OBJ ? -1 : image_for_type<G>(s, type, player_img);
                     if (img >= 0) {
                         if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                            if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
+                            double rx, ry, rw, rh;
+                            screen_rect(v, (float)x, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                            if (img != SPACE && (s.opt_use_monochrome_assets || !grid_obj_fill<G>(img, rx, ry, rw, rh, im)))
+                                err = true; // other draw_grid_obj fills: not in this build
                         } else {
                             int theme = mask_theme<G>(s, grid_theme<G>(s, type), img);
                             int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
@@ -962,6 +1013,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
+        PG_CASE(PG_GAME_CHASER)
     default: break;
     }
 #undef PG_CASE

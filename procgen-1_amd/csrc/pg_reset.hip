@@ -40,7 +40,12 @@ struct LeaperScratch {
     int8_t theme[PG_CAP], type[PG_CAP];
     float road[8], water[8]; // lane speeds (copied into PGEnv with static indices)
 };
+struct ChaserScratch {
+    MGScratch mg;
+    int16_t sel[8]; // simple_choose picks
+};
 template <int G> struct Scratch { uint32_t dummy[1]; };
+template <> struct Scratch<PG_GAME_CHASER> { ChaserScratch ch; };
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -955,6 +960,162 @@ DEV void climber_game_reset(RCtx &c) {
     }
 }
 
+// ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
+// MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
+// order and may open a wall next to a later cell, so each step finds the first dead end at or
+// after the scan position in the current grid (ballot), opens one of its walls, and resumes.
+DEV void mg_generate_maze_no_dead_ends(RCtx &c, MG &g) {
+    mg_generate_maze(c, g);
+    const int cells = g.ad * g.ad;
+    int start = 0;
+    while (start < cells) {
+        int found = -1;
+        for (int base = start & ~63; base < cells; base += 64) {
+            int i = base + LANE;
+            bool de = i >= start && i < cells && mg_get_obj(g, i) == SPACE && mg_count_neighbors(g, i, SPACE) == 1;
+            unsigned long long b = ballot(de);
+            if (b) {
+                found = base + __ffsll((long long)b) - 1;
+                break;
+            }
+        }
+        if (found < 0) break;
+        const int nw = mg_count_neighbors(g, found, WALL_OBJ);
+        if (nw > 0) mg_set_index(g, mg_nth_neighbor(g, found, WALL_OBJ, randn(c, nw)), SPACE);
+        start = found + 1;
+    }
+}
+
+// RandGen::simple_choose(n, k) (randgen.cpp:70-88), k <= 8, picks in LDS
+DEV void simple_choose_small(RCtx &c, int n, int k, int16_t *sel) {
+    if (k > 8 || k > n) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    for (int i = 0; i < k; i++) {
+        int next = randn(c, n);
+        for (;;) {
+            bool seen = false;
+            for (int j = 0; j < i; j++)
+                if (sel[j] == next) seen = true;
+            if (!seen) break;
+            next = randn(c, n);
+        }
+        wave_sync();
+        if (LANE == 0) sel[i] = (int16_t)next;
+        wave_sync();
+    }
+}
+
+// index of the n-th (0-based) position p in [0, count) with pred(p) true, in ascending p
+template <typename P>
+DEV int nth_where(int count, int n, P pred) {
+    int seen = 0;
+    for (int base = 0; base < count; base += 64) {
+        int p = base + LANE;
+        bool f = p < count && pred(p);
+        unsigned long long b = ballot(f);
+        int cnt = __popcll(b);
+        if (n < seen + cnt) {
+            bool mine = f && __popcll(b & ((1ull << LANE) - 1ull)) == n - seen;
+            return base + __ffsll((long long)ballot(mine)) - 1;
+        }
+        seen += cnt;
+    }
+    return -1;
+}
+template <typename P>
+DEV int count_where(int count, P pred) {
+    int cnt = 0;
+    for (int base = 0; base < count; base += 64) {
+        int p = base + LANE;
+        cnt += __popcll(ballot(p < count && pred(p)));
+    }
+    return cnt;
+}
+
+DEV void chaser_game_reset(RCtx &c, ChaserScratch *S) {
+    int extra_orb_sign = 1;
+    const int dm = c.s.opt_distribution_mode;
+    if (dm == PG_EASY) { c.s.maze_dim = 11; c.s.total_enemies = 3; extra_orb_sign = 0; }
+    else if (dm == PG_HARD) { c.s.maze_dim = 13; c.s.total_enemies = 3; extra_orb_sign = -1; }
+    else { c.s.maze_dim = 19; c.s.total_enemies = 5; extra_orb_sign = 1; }
+    const int md = c.s.maze_dim;
+    c.s.main_width = md; // choose_world_dim (:141-144)
+    c.s.main_height = md;
+    base_game_reset<PG_GAME_CHASER>(c);
+    c.s.opt_center_agent = 0;
+    EF(c, F_RX, 0) = .5f;
+    EF(c, F_RY, 0) = .5f;
+    c.s.eat_time = -1 * c.s.eat_timeout;
+    MG g;
+    g.m = &S->mg;
+    g.md = md;
+    g.ad = md + 2;
+    if (g.ad > MG_MAX_DIM) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    mg_generate_maze_no_dead_ends(c, g);
+    const int extra_quad = randn(c, 4);
+    // set_obj(i, j, maze (i + 1, j + 1) with WALL_OBJ -> MAZE_WALL)
+    int16_t *mgrid = S->mg.grid;
+    for (int k = LANE; k < md * md; k += 64) {
+        int x = k % md, y = k / md;
+        int obj = mgrid[(y + 1) * g.ad + (x + 1)];
+        c.grid[y * md + x] = (int16_t)(obj == WALL_OBJ ? CH_MAZE_WALL : obj);
+    }
+    wave_sync();
+    // quadrant lists: SPACE cells in the reference's x-major visiting order (i = x outer)
+    for (int q = 0; q < 4; q++) {
+        auto in_q = [&](int k) { // k = i * md + j (x-major)
+            int i = k / md, j = k % md;
+            int qi = ((double)i >= md / 2.0 ? 1 : 0) * 2 + ((double)j >= md / 2.0 ? 1 : 0);
+            return qi == q && mgrid[(j + 1) * g.ad + (i + 1)] == SPACE;
+        };
+        const int qn = count_where(md * md, in_q);
+        const int num_orbs = 1 + (q == extra_quad ? extra_orb_sign : 0);
+        simple_choose_small(c, qn, num_orbs, S->sel);
+        for (int j = 0; j < num_orbs; j++) {
+            const int k = nth_where(md * md, S->sel[j], in_q);
+            const int cell = (k % md) * md + k / md; // idx = j * maze_dim + i
+            add_entity(c, (float)((cell % md) + .5), (float)((cell / md) + .5), 0, 0, 0.4f, CH_LARGE_ORB);
+            wave_sync();
+            if (LANE == 0) c.grid[cell] = CH_MARKER;
+            wave_sync();
+        }
+    }
+    // free_cells = get_cells_with_type(SPACE) (ascending)
+    const int cells = md * md;
+    auto is_free = [&](int i) { return c.grid[i] == SPACE; };
+    const int nfree = count_where(cells, is_free);
+    simple_choose_small(c, nfree, 1 + c.s.total_enemies, S->sel);
+    int cell_of[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) cell_of[k] = k < 1 + c.s.total_enemies ? nth_where(cells, S->sel[k], is_free) : -1;
+    EF(c, F_X, 0) = (float)((cell_of[0] % md) + .5);
+    EF(c, F_Y, 0) = (float)((cell_of[0] / md) + .5);
+    wave_sync();
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+        if (k < 1 + c.s.total_enemies) {
+            const int cell = cell_of[k];
+            int e = add_entity(c, (float)((cell % md) + .5), (float)((cell / md) + .5), 0, 0, .5f, CH_ENEMY_EGG);
+            EF(c, F_HEALTH, e) = (float)c.s.egg_timeout;
+            wave_sync();
+        }
+    }
+    // every free cell (enemy cells included) becomes an ORB; the LARGE_ORB markers become SPACE
+    for (int i = LANE; i < cells; i += 64) {
+        int v = c.grid[i];
+        if (v == SPACE) c.grid[i] = CH_ORB;
+        else if (v == CH_MARKER) c.grid[i] = SPACE;
+    }
+    c.s.total_orbs = nfree;
+    c.s.orbs_collected = 0;
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ leaper (leaper.cpp:115-218)
 DEV float lp_rand_sign(RCtx &c) { return (double)rand01(c) < 0.5 ? 1.0f : -1.0f; } // :91-97
 DEV int lp_extra_space(RCtx &c) { return c.s.opt_distribution_mode == PG_EASY ? 0 : randn(c, 2); }
@@ -1122,6 +1283,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_MINER) miner_game_reset(c, &scratch->mn);
     if constexpr (G == PG_GAME_CLIMBER) climber_game_reset(c);
     if constexpr (G == PG_GAME_LEAPER) leaper_game_reset(c, &scratch->lp);
+    if constexpr (G == PG_GAME_CHASER) chaser_game_reset(c, &scratch->ch);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1223,6 +1385,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
+        PG_CASE(PG_GAME_CHASER)
     default: break;
     }
 #undef PG_CASE

@@ -180,6 +180,8 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
         if (src_type == PLAYER && cr_is_wall(target)) return true;
     if constexpr (G == PG_GAME_CLIMBER) // climber.cpp:147-154
         if (src_type == PLAYER && cl_is_wall(target)) return true;
+    if constexpr (G == PG_GAME_CHASER) // chaser.cpp:94-99
+        if (target == CH_MAZE_WALL) return true;
     if constexpr (G == PG_GAME_MINER) // miner.cpp:68-75
         if (src_type == PLAYER && (target == MN_BOULDER || target == MN_MOVING_BOULDER || target == MN_OOB_WALL))
             return true;
@@ -662,6 +664,11 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!c.s.has_support) {
             if (vy > -2) vy -= c.s.gravity;
         }
+    } else if constexpr (G == PG_GAME_CHASER) { // chaser.cpp:83-92 (cpp-utils double sign)
+        if (c.s.action_vx != 0) vx = c.s.maxspeed * c.s.action_vx;
+        if (c.s.action_vy != 0) vy = c.s.maxspeed * c.s.action_vy;
+        vx = (float)(dsign(vx) * c.s.maxspeed);
+        vy = (float)(dsign(vy) * c.s.maxspeed);
     } else if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:228-244
         if (vx == 0 && vy == 0) {
             if (c.s.action_vx != 0) {
@@ -726,6 +733,15 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_CHASER) { // chaser.cpp:119-133
+        if (t == CH_LARGE_ORB) {
+            c.s.eat_time = c.s.cur_time;
+            c.s.sd_reward += 0.04f; // ORB_REWARD
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+        } else if (t == CH_ENEMY) {
+            if (c.s.cur_time - c.s.eat_time < c.s.eat_timeout) EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+            else c.s.sd_done = 1;
         }
     } else if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:76-84
         if (t == LP_CAR) {
@@ -1300,6 +1316,179 @@ DEV void leaper_step_tail(Ctx &c, uint32_t *rg) { // leaper.cpp:258-287
     wave_sync();
 }
 
+// chaser (chaser.cpp:286-376).  The reference's free_cells / is_space_vec are the non-MAZE_WALL
+// cells of the grid in index order (walls never change after the reset), read from the grid.
+DEV int ch_grid(Ctx &c, int idx) { return c.G[idx]; } // int16 grid in HBM (ORB = 1002 exceeds the int8 mirror)
+DEV int ch_to_grid_idx(Ctx &c, int x, int y) {
+    if (!(0 <= x && x < c.s.main_width && 0 <= y && y < c.s.main_height)) return -2; // INVALID_IDX
+    return y * c.s.main_width + x;
+}
+// n-th (0-based) non-wall cell in index order
+DEV int ch_nth_free(Ctx &c, int n) {
+    const int cells = c.s.main_width * c.s.main_height;
+    int seen = 0;
+    for (int base = 0; base < cells; base += 64) {
+        int i = base + LANE;
+        bool f = i < cells && ch_grid(c, i) != CH_MAZE_WALL;
+        unsigned long long b = ballot(f);
+        int cnt = __popcll(b);
+        if (n < seen + cnt) {
+            bool mine = f && __popcll(b & ((1ull << LANE) - 1ull)) == n - seen;
+            return base + __ffsll((long long)ballot(mine)) - 1;
+        }
+        seen += cnt;
+    }
+    return -1;
+}
+DEV int ch_num_free(Ctx &c) {
+    const int cells = c.s.main_width * c.s.main_height;
+    int cnt = 0;
+    for (int base = 0; base < cells; base += 64) {
+        int i = base + LANE;
+        cnt += __popcll(ballot(i < cells && ch_grid(c, i) != CH_MAZE_WALL));
+    }
+    return cnt;
+}
+DEV void ch_spawn_egg(Ctx &c, int cell) { // spawn_egg (:259-262)
+    const int md = c.s.maze_dim;
+    int i = append_entity(c, (float)((cell % md) + .5), (float)((cell / md) + .5), 0, 0, .5f, .5f, CH_ENEMY_EGG);
+    if (i >= 0) EF(c, F_HEALTH, i) = (float)c.s.egg_timeout;
+    wave_sync();
+}
+
+DEV void chaser_step_tail(Ctx &c) {
+    const int n = c.s.num_ents, w = c.s.main_width;
+    const bool can_eat = c.s.cur_time - c.s.eat_time < c.s.eat_timeout;
+    const float default_enemy_speed = .5;
+    const float vscale = can_eat ? (default_enemy_speed * .5f) : default_enemy_speed;
+    const float ax = c.s.agent_erased ? c.s.ghost_x : EF(c, F_X, 0);
+    const float ay = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+    const int agent_idx = ch_to_grid_idx(c, (int)ax, (int)ay);
+    const bool be_agressive = c.s.step_rand_int % 2 == 0;
+    const int dist_scale = can_eat ? -1 : 1;
+    // every entity of the reverse loop is independent: lane-parallel, hatchlings appended in
+    // the loop's (descending) order
+    int num_enemies = 0, hatch_total = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        int t = i < n ? EI(c, F_TYPE, i) : -1;
+        num_enemies += __popcll(ballot(t == CH_ENEMY_EGG || t == CH_ENEMY));
+        bool hatch = false;
+        if (t == CH_ENEMY_EGG) {
+            float h = EF(c, F_HEALTH, i) - 1;
+            EF(c, F_HEALTH, i) = h;
+            if (h == 0) {
+                hatch = true;
+                EI(c, F_FLAGS, i) = EI(c, F_FLAGS, i) | EF_WILL_ERASE;
+            }
+        } else if (t == CH_ENEMY) {
+            const float evx = EF(c, F_VX, i), evy = EF(c, F_VY, i);
+            const float x = (float)(EF(c, F_X, i) - .5);
+            const float y = (float)(EF(c, F_Y, i) - .5);
+            const int enemy_idx = ch_to_grid_idx(c, (int)x, (int)y);
+            const bool is_at_junction = fabs((double)x - round((double)x)) + fabs((double)y - round((double)y)) < .01;
+            if ((evx == 0 && evy == 0) || is_at_junction) {
+                const int prev_idx = ch_to_grid_idx(c, (int)(x - dsign(evx)), (int)(y - dsign(evy)));
+                const int ex = enemy_idx % w, ey = enemy_idx / w;
+                const int ox[4] = {-1, 0, 0, 1}, oy[4] = {0, -1, 1, 0}; // get_adjacent order (:269-284)
+                int cand[4];
+                bool ok[4];
+                int min_dist = 2 * w;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    cand[k] = ch_to_grid_idx(c, ex + ox[k], ey + oy[k]);
+                    ok[k] = cand[k] != -2 && ch_grid(c, cand[k]) != CH_MAZE_WALL && cand[k] != prev_idx;
+                }
+                int md[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    md[k] = (abs((cand[k] % w) - (agent_idx % w)) + abs((cand[k] / w) - (agent_idx / w))) * dist_scale;
+                    if (ok[k] && be_agressive && md[k] < min_dist) min_dist = md[k];
+                }
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (ok[k] && be_agressive && md[k] != min_dist) ok[k] = false;
+                    cnt += ok[k];
+                }
+                if (cnt == 0) {
+                    c.s.error = PG_ERR_GRID; // the reference divides by zero here
+                } else {
+                    int pick = (int)((unsigned)c.s.step_rand_int % (unsigned)cnt), neighbor = -1;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (ok[k] && pick-- == 0) neighbor = cand[k];
+                    const int nx = neighbor % w, ny = neighbor / w;
+                    EF(c, F_VX, i) = (nx - x) * vscale;
+                    EF(c, F_VY, i) = (ny - y) * vscale;
+                }
+            }
+        }
+        hatch_total += __popcll(ballot(hatch));
+    }
+    if (ballot(c.s.error != 0)) c.s.error = PG_ERR_GRID;
+    wave_sync();
+    // spawn_child(egg, ENEMY, .5) for the hatched eggs, highest index first
+    if (hatch_total > 0) {
+        if (n + hatch_total > PG_CAP) {
+            c.s.error = PG_ERR_ENTITY_OVERFLOW;
+        } else {
+            int done = 0;
+            for (int base = ((n - 1) & ~63); base >= 0; base -= 64) {
+                int i = base + LANE;
+                bool hatch = i < n && EI(c, F_TYPE, i) == CH_ENEMY_EGG && (EI(c, F_FLAGS, i) & EF_WILL_ERASE) &&
+                             EF(c, F_HEALTH, i) == 0;
+                unsigned long long b = ballot(hatch);
+                float hx = 0, hy = 0;
+                if (hatch) { hx = EF(c, F_X, i); hy = EF(c, F_Y, i); }
+                wave_sync();
+                if (hatch) {
+                    // rank among this chunk's hatchlings, counted from the top
+                    int rank = done + __popcll(b >> LANE) - 1;
+                    int slot = n + rank;
+                    EF(c, F_X, slot) = hx; EF(c, F_Y, slot) = hy; EF(c, F_VX, slot) = 0; EF(c, F_VY, slot) = 0;
+                    EF(c, F_RX, slot) = .5f; EF(c, F_RY, slot) = .5f; EF(c, F_ROTATION, slot) = 0; EF(c, F_VROT, slot) = 0;
+                    EF(c, F_ALPHA, slot) = 1.0f; EF(c, F_ALPHA_DECAY, slot) = 1.0f; EF(c, F_GROW_RATE, slot) = 1.0f;
+                    EF(c, F_FRICTION, slot) = 1; EF(c, F_COLLISION_MARGIN, slot) = 0; EF(c, F_HEALTH, slot) = 1;
+                    EF(c, F_THETA, slot) = -100; EF(c, F_CLIMBER_SPAWN_X, slot) = 0;
+                    EI(c, F_TYPE, slot) = CH_ENEMY; EI(c, F_IMAGE_TYPE, slot) = CH_ENEMY; EI(c, F_IMAGE_THEME, slot) = 0;
+                    EI(c, F_RENDER_Z, slot) = 0; EI(c, F_LIFE_TIME, slot) = 0; EI(c, F_EXPIRE_TIME, slot) = -1;
+                    EI(c, F_FIRE_TIME, slot) = -1; EI(c, F_SPAWN_TIME, slot) = -1;
+                    EI(c, F_FLAGS, slot) = EF_AUTO_ERASE | EF_SMART_STEP;
+                }
+                done += __popcll(b);
+            }
+            c.s.num_ents = n + hatch_total;
+        }
+    }
+    wave_sync();
+    if (num_enemies < c.s.total_enemies) {
+        const int nfree = ch_num_free(c);
+        if (nfree <= 0) {
+            c.s.error = PG_ERR_GRID;
+        } else {
+            const int sel = (int)((unsigned)c.s.step_rand_int % (unsigned)nfree);
+            ch_spawn_egg(c, ch_nth_free(c, sel));
+        }
+    }
+    // get_agent_index (:176-178) and the orb under the agent
+    const int aidx = (int)ay * w + (int)ax;
+    const int cells = w * c.s.main_height;
+    if (0 <= aidx && aidx < cells && ch_grid(c, aidx) == CH_ORB) {
+        wave_sync();
+        if (LANE == 0) c.d.grid[(size_t)c.env * PG_GRID_MAX + aidx] = SPACE;
+        wave_sync();
+        c.s.sd_reward += 0.04f; // ORB_REWARD
+        c.s.orbs_collected += 1;
+    }
+    if (c.s.orbs_collected == c.s.total_orbs) {
+        c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+        c.s.sd_level_complete = 1;
+        c.s.sd_done = 1;
+    }
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ game_step
 template <int G>
 DEV void game_step(Ctx &c) {
@@ -1360,6 +1549,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_MINER) miner_step_tail(c);
     if constexpr (G == PG_GAME_CLIMBER) climber_step_tail(c);
     if constexpr (G == PG_GAME_LEAPER) leaper_step_tail(c, rg);
+    if constexpr (G == PG_GAME_CHASER) chaser_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1458,6 +1648,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_HEIST) { PG_W(has_keys) }
         if constexpr (G == PG_GAME_MINER) { PG_W(diamonds_remaining) PG_W(died) }
         if constexpr (G == PG_GAME_CLIMBER) { PG_W(has_support) PG_W(facing_right) PG_W(coins_collected) }
+        if constexpr (G == PG_GAME_CHASER) { PG_W(eat_time) PG_W(orbs_collected) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1481,6 +1672,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
+        PG_CASE(PG_GAME_CHASER)
     default: break;
     }
 #undef PG_CASE

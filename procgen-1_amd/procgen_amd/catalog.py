@@ -186,6 +186,20 @@ LEAPER_SPRITES = {
     5: ["misc_assets/finish2.png"],
 }
 
+# ---------------------------------------------------------------- chaser
+# procgen/src/games/chaser.cpp:54-72 (PLAYER 0, ENEMY 6, ENEMY2 7, ENEMY3 8, LARGE_ORB 2, ENEMY_WEAK 3,
+# ENEMY_EGG 4, MAZE_WALL 5); ORB (1002) is a grid fill, not an image
+CHASER_SPRITES = {
+    0: ["misc_assets/enemyFloating_1b.png"],
+    6: ["misc_assets/enemyFlying_1.png"],
+    7: ["misc_assets/enemyFlying_2.png"],
+    8: ["misc_assets/enemyFlying_3.png"],
+    2: ["misc_assets/yellowCrystal.png"],
+    3: ["misc_assets/enemyWalking_1b.png"],
+    4: ["misc_assets/enemySpikey_1b.png"],
+    5: ["misc_assets/tileStone_slope.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -195,6 +209,7 @@ GAMES = {
     "miner": (MINER_SPRITES, "caves"),          # miner.cpp:45-47
     "climber": (CLIMBER_SPRITES, "platform"),   # climber.cpp:43-45
     "leaper": (LEAPER_SPRITES, "topdown"),      # leaper.cpp:41-43
+    "chaser": (CHASER_SPRITES, "topdown_simple"),  # chaser.cpp:50-52
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

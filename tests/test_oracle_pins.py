@@ -252,3 +252,23 @@ def test_leaper_operand_order_pinned():
         sign = np.float32(1.0) if u[0] < 0.5 else np.float32(-1.0)
         spd = np.float32(u[1] * np.float32(np.float32(0.2) - np.float32(0.05)) + np.float32(0.05))
         assert out[0] == sign * spd, seed
+
+
+def test_qt_raster_fill_goldens():
+    """fillRect(QRectF, opaque QColor) (chaser orbs, bars, draw_grid_obj) replayed through the
+    oracle's restatement equals real Qt 5.9.7 (tests/golden/qt_raster_fill_goldens.npz,
+    tools/make_raster_fill_goldens.py)."""
+    from procgen_amd.assets import atlas_for
+    lib = oracle_lib.load()
+    z = np.load(os.path.join(GOLDEN, "qt_raster_fill_goldens.npz"), allow_pickle=False)
+    cmds, synth, cin, cout = z["cmds"], z["synth"], z["canvas_in"], z["canvas_out"]
+    atlas = atlas_for("coinrun")
+    bad = []
+    for i in range(cin.shape[0]):
+        b = encode_cmds(cmds[cmds["case"] == i], synth, atlas)
+        canvas = cin[i].copy()
+        rc = lib.oracle_qt_replay(b, len(b), canvas.ctypes.data)
+        assert rc == len(b)
+        if not np.array_equal(canvas, cout[i]):
+            bad.append(i)
+    assert not bad, "Qt fillRect mismatch in %d cases, first %s" % (len(bad), bad[:10])
