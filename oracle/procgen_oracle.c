@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
@@ -238,6 +238,7 @@ typedef struct {
     int coin_quota, coins_collected;
     /* chaser (chaser.cpp:26-35; free_cells / is_space_vec of the last reset) */
     int eat_timeout, egg_timeout, eat_time, total_enemies, total_orbs, orbs_collected, num_free;
+    int last_fire_time; /* fruitbot (fruitbot.cpp:26-28) */
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -351,6 +352,8 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
         if (src->type == PLAYER && cr_is_wall(target)) return true;
         return false;
     }
+    if (g->game_id == GAME_FRUITBOT) /* fruitbot.cpp:83-85: PLAYER vs OUT_OF_BOUNDS_WALL 2 */
+        return base || (src->type == PLAYER && target == 2);
     if (g->game_id == GAME_CHASER) { /* chaser.cpp:94-99: MAZE_WALL 5 */
         if (target == 5) return true;
         return base;
@@ -405,11 +408,35 @@ static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *targe
 static bool hook_will_reflect(Game *g, int src, int target) {
     if (g->game_id == GAME_COINRUN) /* coinrun.cpp:140-142 */
         return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
+    if (g->game_id == GAME_FRUITBOT) /* fruitbot.cpp:79-81: BAD_OBJ 4 off BARRIER 1 / WALL_OBJ */
+        return src == 4 && (target == 1 || target == WALL_OBJ);
     if (g->game_id == GAME_CLIMBER) /* climber.cpp:113-115: ENEMY 5 off walls and ENEMY_BARRIER 19 */
         return src == 5 && (target == 15 || target == 16 || target == 19);
     if (g->game_id == GAME_MINER) /* miner.cpp:77-79: ENEMY 5 off BOULDER, DIAMOND, MOVING_BOULDER/DIAMOND, out of bounds */
         return src == 5 && (target == 1 || target == 2 || target == 3 || target == 4 || target == g->out_of_bounds_object);
     return false;
+}
+
+/* handle_collision(src, target) (basic :383-385 is empty) */
+static void hook_handle_collision(Game *g, int si, int ti) {
+    Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:117-134 */
+        if (src->type == 3) { /* PLAYER_BULLET */
+            if (target->type == 1) { /* BARRIER */
+                src->will_erase = true;
+            } else if (target->type == 11) { /* LOCK */
+                src->will_erase = true;
+                target->will_erase = true;
+                for (int k = 0; k < g->num_ents; k++) { /* the door of this lock */
+                    Entity *ent = &g->ents[k];
+                    if (ent->type == 10 && fabsf(ent->y - target->y) < 1) {
+                        ent->will_erase = true;
+                        break;
+                    }
+                }
+            }
+        }
+    }
 }
 
 static void hook_handle_agent_collision(Game *g, Entity *obj) {
@@ -428,6 +455,22 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
             }
+        }
+    } else if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:95-115 */
+        if (obj->type == 1) { /* BARRIER */
+            g->sd_done = true;
+        } else if (obj->type == 4) { /* BAD_OBJ: PENALTY (const int -4) */
+            g->sd_reward += -4;
+            obj->will_erase = true;
+        } else if (obj->type == 10) { /* LOCKED_DOOR */
+            g->sd_done = true;
+        } else if (obj->type == 7) { /* GOOD_OBJ: POSITIVE_REWARD (const int 1) */
+            g->sd_reward += 1;
+            obj->will_erase = true;
+        } else if (obj->type == 12) { /* PRESENT */
+            g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+            g->sd_done = true;
+            g->sd_level_complete = true;
         }
     } else if (g->game_id == GAME_CHASER) { /* chaser.cpp:119-133: LARGE_ORB 2, ENEMY 6 */
         if (obj->type == 2) {
@@ -752,6 +795,12 @@ static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299
 }
 
 static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:154-158 */
+        g->action_vx = (float)(move_action / 3 - 1);
+        g->action_vy = 0.2f;
+        g->action_vrot = 0;
+        return;
+    }
     if (g->game_id == GAME_COINRUN) {
         coinrun_set_action_xy(g, move_action);
         return;
@@ -862,9 +911,13 @@ static void basic_game_step(Game *g) { /* basic-abstract-game.cpp:695-755 */
     for (int i = g->num_ents - 1; i >= 0; i--) {
         Entity *ent = &g->ents[i];
         if (has_agent_collision(g, ent)) hook_handle_agent_collision(g, ent);
-        if (ent->collides_with_entities) {
-            /* no coinrun entity sets collides_with_entities; other games: later rounds */
-            fatal_msg("collides_with_entities not restated yet");
+        if (ent->collides_with_entities) { /* :735-744 */
+            for (int j = g->num_ents - 1; j >= 0; j--) {
+                if (i == j) continue;
+                Entity *e1 = &g->ents[i], *e2 = &g->ents[j];
+                if (has_collision(e1, e2, e1->collision_margin) && !e1->will_erase && !e2->will_erase)
+                    hook_handle_collision(g, i, j);
+            }
         }
         if (g->ents[i].smart_step) check_grid_collisions(g, i);
     }
@@ -2071,6 +2124,108 @@ static void chaser_game_step(Game *g) { /* :286-376 */
     }
 }
 
+/* ================================================================== fruitbot (games/fruitbot.cpp) */
+#define FB_BARRIER 1
+#define FB_OUT_OF_BOUNDS_WALL 2
+#define FB_PLAYER_BULLET 3
+#define FB_BAD_OBJ 4
+#define FB_GOOD_OBJ 7
+#define FB_LOCKED_DOOR 10
+#define FB_LOCK 11
+#define FB_PRESENT 12
+#define FB_KEY_DURATION 8
+static const float FB_DOOR_ASPECT_RATIO = 3.25f;
+
+static void fit_aspect_ratio(Game *g, const or_atlas *at, Entity *e) { /* basic-abstract-game.cpp:1034-1045 */
+    float ar = asset_aspect_ratio(g, at, e->image_type + e->image_theme * MAX_ASSETS);
+    if (ar > 1) e->ry = e->rx / ar;
+    else e->rx = e->ry * ar;
+}
+
+static void fb_add_walls(Game *g, float ry, bool use_door, float min_pct) { /* :157-189 */
+    MT *r = &g->rand_gen;
+    float rw = (float)g->main_width;
+    float wall_ry = 0.3f;
+    float lock_rx = .25;
+    float lock_ry = 0.45f;
+    float pct = (float)(min_pct + .2 * rg_rand01(r));
+    if (use_door) {
+        pct += 0.1f;
+        float lock_pct_w = 2 * lock_rx / g->main_width;
+        float door_pct_w = (wall_ry * 2 * FB_DOOR_ASPECT_RATIO) / g->main_width;
+        int num_doors = (int)ceilf((pct - 2 * lock_pct_w) / door_pct_w);
+        pct = 2 * lock_pct_w + door_pct_w * num_doors;
+    }
+    float gapw = pct * rw;
+    float w1 = rg_rand01(r) * (rw - gapw);
+    float w2 = rw - w1 - gapw;
+    add_entity_rxy(g, w1 / 2, ry, 0, 0, w1 / 2, wall_ry, FB_BARRIER);
+    add_entity_rxy(g, rw - w2 / 2, ry, 0, 0, w2 / 2, wall_ry, FB_BARRIER);
+    if (use_door) {
+        int is_on_right = rg_randn(r, 2);
+        float lock_x = w1 + lock_rx + is_on_right * (gapw - 2 * lock_rx);
+        float door_x = w1 + gapw / 2 - (is_on_right * 2 - 1) * lock_rx;
+        add_entity_rxy(g, door_x, ry, 0, 0, gapw / 2 - lock_rx, wall_ry, FB_LOCKED_DOOR);
+        add_entity_rxy(g, lock_x, ry - lock_ry + wall_ry, 0, 0, lock_rx, lock_ry, FB_LOCK);
+    }
+}
+
+static void fruitbot_game_reset(Game *g, const or_atlas *at) { /* :191-245 */
+    MT *r = &g->rand_gen;
+    g->main_width = g->options.distribution_mode == EasyMode ? 10 : 20; /* choose_world_dim (:144-152) */
+    g->main_height = 60;
+    basic_game_reset(g, at);
+    g->last_fire_time = 0;
+    int min_sep = 4, num_walls = 10, object_group_size = 6, buf_h = 4;
+    float door_prob = .125;
+    float min_pct = .1f;
+    if (g->options.distribution_mode == EasyMode) {
+        num_walls = 5; object_group_size = 2; door_prob = 0; min_pct = .2f;
+    }
+    int partition[16] = {0};
+    fassert(num_walls <= 16);
+    int px = g->main_height - min_sep * num_walls - buf_h; /* RandGen::partition (randgen.cpp:33-41) */
+    for (int i = 0; i < px; i++) partition[rg_randn(r, num_walls)] += 1;
+    int curr_h = 0;
+    for (int k = 0; k < num_walls; k++) {
+        int dy = min_sep + partition[k];
+        curr_h += dy;
+        bool use_door = (dy > 5) && rg_rand01(r) < door_prob;
+        fb_add_walls(g, (float)curr_h, use_door, min_pct);
+    }
+    Entity *agent = AG(g);
+    agent->y = agent->ry;
+    int num_good = rg_randn(r, 10) + 10;
+    int num_bad = rg_randn(r, 10) + 10;
+    for (int i = 0; i < g->main_width; i++) {
+        int e = add_entity_rxy(g, (float)(i + .5), (float)(g->main_height - .5), 0, 0, .5f, .5f, FB_PRESENT);
+        choose_random_theme(g, &g->ents[e], at);
+    }
+    for (int i = 0; i < num_good; i++) spawn_entity(g, .5f, FB_GOOD_OBJ, 0, 0, (float)g->main_width, (float)g->main_height);
+    for (int i = 0; i < num_bad; i++) spawn_entity(g, .5f, FB_BAD_OBJ, 0, 0, (float)g->main_width, (float)g->main_height);
+    for (int i = 0; i < g->num_ents; i++) {
+        Entity *e = &g->ents[i];
+        if (e->type == FB_GOOD_OBJ || e->type == FB_BAD_OBJ) {
+            e->image_theme = rg_randn(r, object_group_size);
+            fit_aspect_ratio(g, at, e);
+        }
+    }
+    AG(g)->rotation = -1 * PI_F / 2;
+}
+
+static void fruitbot_game_step(Game *g) { /* :247-258 */
+    basic_game_step(g);
+    if (g->special_action == 1 && (g->cur_time - g->last_fire_time) >= FB_KEY_DURATION) {
+        float vx = 0, vy = 1;
+        Entity *agent = AG(g);
+        float bullet_vscale = .5;
+        int e = add_entity(g, agent->x, agent->y, vx * bullet_vscale, vy * bullet_vscale, .25f, FB_PLAYER_BULLET);
+        g->ents[e].expire_time = FB_KEY_DURATION;
+        g->ents[e].collides_with_entities = true;
+        g->last_fire_time = g->cur_time;
+    }
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -2218,6 +2373,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_CLIMBER) climber_game_reset(g, at);
     else if (g->game_id == GAME_LEAPER) leaper_game_reset(g, at);
     else if (g->game_id == GAME_CHASER) chaser_game_reset(g, at);
+    else if (g->game_id == GAME_FRUITBOT) fruitbot_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -2229,6 +2385,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_CLIMBER) climber_game_step(g);
     else if (g->game_id == GAME_LEAPER) leaper_game_step(g, at);
     else if (g->game_id == GAME_CHASER) chaser_game_step(g);
+    else if (g->game_id == GAME_FRUITBOT) fruitbot_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -2632,6 +2789,10 @@ static void prepare_for_drawing(Game *g, float rect_height) { /* :828-847 */
             g->center_x = (float)(g->main_width / 2.0);
             g->center_y = (float)((double)agent->y + g->main_width / 2.0 - (double)(5 * agent->ry));
             g->visibility = (float)g->main_width;
+        } else if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:138-142 */
+            g->center_x = (float)(g->main_width / 2.0);
+            g->center_y = (float)((double)agent->y + g->main_width / 2.0 - (double)(2 * agent->ry));
+            g->visibility = (float)g->main_width;
         } else {
             g->center_x = agent->x;
             g->center_y = agent->y;
@@ -2665,8 +2826,8 @@ static RectD adjust_rect(RectD b, RectD a) { /* qt-utils.h:12-19 */
     return r;
 }
 
-static void tile_image(Game *g, const uint32_t *px, int iw, int ih, bool refl, double opacity, RectD rect,
-                       float tile_ratio) { /* basic-abstract-game.cpp:849-877 */
+static void tile_image_fmt(Game *g, const uint32_t *px, int iw, int ih, int fmt, bool refl, double opacity, RectD rect,
+                           float tile_ratio) { /* basic-abstract-game.cpp:849-877 */
     if (tile_ratio != 0) {
         if (tile_ratio < 0) {
             tile_ratio = -1 * tile_ratio;
@@ -2675,24 +2836,32 @@ static void tile_image(Game *g, const uint32_t *px, int iw, int ih, bool refl, d
             float tile_height = (float)(rect.h / num_tiles);
             float tile_width = (float)rect.w;
             for (int i = 0; i < num_tiles; i++)
-                qt_draw_image(g->canvas, rect.x, rect.y + tile_height * i, tile_width, tile_height, px, iw, ih,
-                              QFMT_ARGB32_PM, refl, opacity);
+                qt_draw_image(g->canvas, rect.x, rect.y + tile_height * i, tile_width, tile_height, px, iw, ih, fmt,
+                              refl, opacity);
         } else {
             int num_tiles = (int)(rect.w / (rect.h * tile_ratio));
             if (num_tiles < 1) num_tiles = 1;
             float tile_width = (float)(rect.w / num_tiles);
             float tile_height = (float)rect.h;
             for (int i = 0; i < num_tiles; i++)
-                qt_draw_image(g->canvas, rect.x + tile_width * i, rect.y, tile_width, tile_height, px, iw, ih,
-                              QFMT_ARGB32_PM, refl, opacity);
+                qt_draw_image(g->canvas, rect.x + tile_width * i, rect.y, tile_width, tile_height, px, iw, ih, fmt,
+                              refl, opacity);
         }
     } else {
-        qt_draw_image(g->canvas, rect.x, rect.y, rect.w, rect.h, px, iw, ih, QFMT_ARGB32_PM, refl, opacity);
+        qt_draw_image(g->canvas, rect.x, rect.y, rect.w, rect.h, px, iw, ih, fmt, refl, opacity);
     }
+}
+static void tile_image(Game *g, const uint32_t *px, int iw, int ih, bool refl, double opacity, RectD rect,
+                       float tile_ratio) {
+    tile_image_fmt(g, px, iw, ih, QFMT_ARGB32_PM, refl, opacity, rect, tile_ratio);
 }
 
 static float hook_tile_aspect_ratio(Game *g, const Entity *e) {
     if (g->game_id == GAME_LEAPER && e->type == LP_FINISH_LINE) return 1; /* leaper.cpp:68-74 */
+    if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:87-93 */
+        if (e->type == 1) return 1;
+        if (e->type == 10) return 3.25f;
+    }
     return 0;                                                            /* :417-419 */
 }
 
@@ -2765,7 +2934,10 @@ static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
     if (!g->options.use_backgrounds) return;
     RectD main_rect = get_screen_rect(g, 0, (float)g->main_height, (float)g->main_width, (float)g->main_height, 0);
     const or_image *bg = &at->backgrounds[g->background_index];
-    fassert(g->bg_tile_ratio >= 0);
+    if (g->bg_tile_ratio < 0) { /* :1003-1004 */
+        tile_image_fmt(g, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, main_rect, g->bg_tile_ratio);
+        return;
+    }
     float bgw = (float)bg->w;
     float bgh = (float)bg->h;
     float bg_ar = bgw / bgh;
@@ -2822,6 +2994,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "climber") == 0) return GAME_CLIMBER;
     if (strcmp(name, "leaper") == 0) return GAME_LEAPER;
     if (strcmp(name, "chaser") == 0) return GAME_CHASER;
+    if (strcmp(name, "fruitbot") == 0) return GAME_FRUITBOT;
     return -1;
 }
 
@@ -2869,6 +3042,12 @@ static void maze_ctor(Game *g) { /* maze.cpp:20-28 */
     g->has_useful_vel_info = false;
     g->out_of_bounds_object = WALL_OBJ;
     g->visibility = 8.0f;
+}
+static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
+    g->mixrate = .5f;
+    g->maxspeed = 0.85f;
+    g->bg_tile_ratio = -1;
+    g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
 }
 static void chaser_ctor(Game *g) { /* chaser.cpp:37-47 */
     g->mixrate = 1;
@@ -2940,6 +3119,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_CLIMBER) climber_ctor(g);
         else if (gid == GAME_LEAPER) leaper_ctor(g);
         else if (gid == GAME_CHASER) chaser_ctor(g);
+        else if (gid == GAME_FRUITBOT) fruitbot_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

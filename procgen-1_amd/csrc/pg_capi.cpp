@@ -115,9 +115,10 @@ int game_id(const std::string &name) {
     if (name == "climber") return PG_GAME_CLIMBER;
     if (name == "leaper") return PG_GAME_LEAPER;
     if (name == "chaser") return PG_GAME_CHASER;
+    if (name == "fruitbot") return PG_GAME_FRUITBOT;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, heist, leaper, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, fruitbot, heist, leaper, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -172,6 +173,11 @@ void construct_env(PGEnv &s, int gid) {
         s.has_useful_vel_info = 0;
         s.out_of_bounds_object = 51; // WALL_OBJ
         s.visibility = 8.0f;
+    } else if (gid == PG_GAME_FRUITBOT) { // fruitbot.cpp:30-40
+        s.mixrate = .5f;
+        s.maxspeed = 0.85f;
+        s.bg_tile_ratio = -1;
+        s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
     } else if (gid == PG_GAME_CHASER) { // chaser.cpp:37-47
         s.mixrate = 1;
         s.maxspeed = .5f;

@@ -86,6 +86,16 @@
 #define CL_WALL_TOP 16
 #define CL_ENEMY_BARRIER 19
 DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
+// fruitbot.cpp:12-23
+#define FB_BARRIER 1
+#define FB_OUT_OF_BOUNDS_WALL 2
+#define FB_PLAYER_BULLET 3
+#define FB_BAD_OBJ 4
+#define FB_GOOD_OBJ 7
+#define FB_LOCKED_DOOR 10
+#define FB_LOCK 11
+#define FB_PRESENT 12
+#define FB_KEY_DURATION 8
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3

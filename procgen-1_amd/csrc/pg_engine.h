@@ -22,7 +22,7 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
     PG_GAME_MINER = 12
 };
 #ifndef PG_NUM_GAMES
@@ -166,7 +166,9 @@ struct PGEnv {
     int32_t total_enemies;
     int32_t total_orbs;
     int32_t orbs_collected;
-    int32_t pad[128 - 100];
+    // ---- fruitbot (fruitbot.cpp:26-28)
+    int32_t last_fire_time;
+    int32_t pad[128 - 101];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

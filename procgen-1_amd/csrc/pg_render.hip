@@ -147,6 +147,7 @@ DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entit
 template <int G>
 DEV float tile_aspect_ratio(int type) {
     if constexpr (G == PG_GAME_LEAPER) return type == LP_FINISH_LINE ? 1.0f : 0.0f;
+    if constexpr (G == PG_GAME_FRUITBOT) return type == FB_BARRIER ? 1.0f : (type == FB_LOCKED_DOOR ? 3.25f : 0.0f);
     return 0.0f;
 }
 template <int G>
@@ -639,6 +640,11 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
             v.center_x = (float)(s.main_width / 2.0);
             v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
             v.visibility = (float)s.main_width;
+        } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:138-142
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(2 * agent_ry));
+            v.visibility = (float)s.main_width;
         } else {
             v.center_x = agent_x;
             v.center_y = agent_y;
@@ -741,6 +747,38 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     } else if (s.opt_use_backgrounds) {
         bg_ok = axis_setup(bg_rx, bg_rw, bgi.y, bx) && axis_setup(bg_ry, bg_rh, bgi.z, by);
     }
+    // source row offset of screen row `lane` in the background (-1: outside the blit)
+    int bg_lane_row = (bg_ok && lane >= by.t1 && lane < by.t1 + by.n)
+                          ? (int)(((by.base + (uint32_t)((lane - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
+                          : -1;
+    if (s.opt_use_backgrounds && s.bg_tile_ratio < 0) {
+        // tile_image(main_rect, bg_tile_ratio < 0) (basic-abstract-game.cpp:849-862, 1003-1004): the
+        // background repeated down the world; a screen row shows the last tile covering it
+        double mx, my, mw, mh;
+        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
+        const float tile_ratio = -1 * s.bg_tile_ratio;
+        int num_tiles = (int)(mh / (mw * tile_ratio));
+        if (num_tiles < 1) num_tiles = 1;
+        const float th = (float)(mh / num_tiles), tw = (float)mw;
+        bg_ok = axis_setup(mx, (double)tw, bgi.y, bx);
+        bg_lane_row = -1;
+        for (int t0 = 0; t0 < num_tiles; t0 += 64) {
+            Axis ty;
+            const int t = t0 + lane;
+            const bool okt = t < num_tiles && axis_setup(my + (double)(th * (float)t), (double)th, bgi.z, ty);
+            const int tt1 = okt ? ty.t1 : 0, tn = okt ? ty.n : 0, tstep = okt ? ty.step : 0;
+            const uint32_t tbase = okt ? ty.base : 0u;
+            for (int k = 0; k < 64 && t0 + k < num_tiles; k++) {
+                const int a1 = readlane(tt1, k), an = readlane(tn, k);
+                if (lane >= a1 && lane < a1 + an) {
+                    const uint32_t b = (uint32_t)readlane((int)tbase, k);
+                    const int st = readlane(tstep, k);
+                    bg_lane_row = (int)(((b + (uint32_t)((lane - a1) * st)) >> 16) * (uint32_t)bgi.y);
+                }
+            }
+        }
+        if (!bg_ok) bg_lane_row = -1;
+    }
     const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
     const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
 
@@ -828,9 +866,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         const int rinfo = ncy0 == 0 ? 0
                         : (srow0 | ((ncy0 > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
                            ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));
-        const int bgrow = (bg_ok && prow >= by.t1 && prow < by.t1 + by.n)
-                              ? (int)(((by.base + (uint32_t)((prow - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
-                              : -1;
+        const int bgrow = bg_lane_row;
         for (int r0 = 0; r0 < PG_RES; r0 += RB) {
             uint32_t bgv[RB], ta[RB], tb[RB];
             int info[RB], bgr[RB], ca[RB], cbv[RB];
@@ -892,9 +928,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
     } else {
         // ---- background alone (lane = column), RB rows per batch
-        const int bgrow = (bg_ok && lane >= by.t1 && lane < by.t1 + by.n)
-                              ? (int)(((by.base + (uint32_t)((lane - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
-                              : -1;
+        const int bgrow = bg_lane_row;
         for (int r0 = 0; r0 < PG_RES; r0 += RB) {
             uint32_t bgv[RB];
 #pragma unroll
@@ -1014,6 +1048,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
+        PG_CASE(PG_GAME_FRUITBOT)
     default: break;
     }
 #undef PG_CASE

@@ -46,6 +46,7 @@ struct ChaserScratch {
 };
 template <int G> struct Scratch { uint32_t dummy[1]; };
 template <> struct Scratch<PG_GAME_CHASER> { ChaserScratch ch; };
+template <> struct Scratch<PG_GAME_FRUITBOT> { int16_t part[16]; };
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -171,6 +172,10 @@ DEV void choose_world_dim(RCtx &c) {
         else if (d == PG_HARD) { c.s.main_width = 20; c.s.main_height = 20; }
         else if (d == PG_MEMORY) { c.s.main_width = 35; c.s.main_height = 35; }
         c.s.main_area = c.s.main_width * c.s.main_height;
+    }
+    if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:144-152
+        c.s.main_width = c.s.opt_distribution_mode == PG_EASY ? 10 : 20;
+        c.s.main_height = 60;
     }
     if constexpr (G == PG_GAME_LEAPER) { // leaper.cpp:103-113
         int d = c.s.opt_distribution_mode;
@@ -960,6 +965,99 @@ DEV void climber_game_reset(RCtx &c) {
     }
 }
 
+// ------------------------------------------------------------------ fruitbot (fruitbot.cpp:157-245)
+// fit_aspect_ratio (basic-abstract-game.cpp:1034-1045) of an entity with no preserved themes
+DEV void fit_aspect_ratio(RCtx &c, int i) {
+    int type = EI(c, F_IMAGE_TYPE, i), theme = EI(c, F_IMAGE_THEME, i);
+    if (c.s.opt_restrict_themes) theme = 0;
+    int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + theme * MAX_ASSETS];
+    if (sp.y <= 0 || sp.z <= 0) {
+        c.s.error = PG_ERR_BAD_OPTION;
+        return;
+    }
+    float ar = (float)(sp.y * 1.0 / sp.z);
+    if (ar > 1) EF(c, F_RY, i) = EF(c, F_RX, i) / ar;
+    else EF(c, F_RX, i) = EF(c, F_RY, i) * ar;
+}
+
+DEV void fb_add_walls(RCtx &c, float ry, bool use_door, float min_pct) {
+    const float rw = (float)c.s.main_width;
+    const float wall_ry = 0.3f, lock_rx = .25, lock_ry = 0.45f;
+    float pct = (float)(min_pct + .2 * rand01(c));
+    if (use_door) {
+        pct += 0.1f;
+        float lock_pct_w = 2 * lock_rx / c.s.main_width;
+        float door_pct_w = (wall_ry * 2 * 3.25f) / c.s.main_width; // DOOR_ASPECT_RATIO
+        int num_doors = (int)ceilf((pct - 2 * lock_pct_w) / door_pct_w);
+        pct = 2 * lock_pct_w + door_pct_w * num_doors;
+    }
+    float gapw = pct * rw;
+    float w1 = rand01(c) * (rw - gapw);
+    float w2 = rw - w1 - gapw;
+    add_entity_rxy(c, w1 / 2, ry, 0, 0, w1 / 2, wall_ry, FB_BARRIER);
+    add_entity_rxy(c, rw - w2 / 2, ry, 0, 0, w2 / 2, wall_ry, FB_BARRIER);
+    if (use_door) {
+        int is_on_right = randn(c, 2);
+        float lock_x = w1 + lock_rx + is_on_right * (gapw - 2 * lock_rx);
+        float door_x = w1 + gapw / 2 - (is_on_right * 2 - 1) * lock_rx;
+        add_entity_rxy(c, door_x, ry, 0, 0, gapw / 2 - lock_rx, wall_ry, FB_LOCKED_DOOR);
+        add_entity_rxy(c, lock_x, ry - lock_ry + wall_ry, 0, 0, lock_rx, lock_ry, FB_LOCK);
+    }
+}
+
+DEV void fruitbot_game_reset(RCtx &c, int16_t *part) {
+    base_game_reset<PG_GAME_FRUITBOT>(c);
+    c.s.last_fire_time = 0;
+    int min_sep = 4, num_walls = 10, object_group_size = 6, buf_h = 4;
+    float door_prob = .125, min_pct = .1f;
+    if (c.s.opt_distribution_mode == PG_EASY) {
+        num_walls = 5; object_group_size = 2; door_prob = 0; min_pct = .2f;
+    }
+    // RandGen::partition (randgen.cpp:33-41)
+    for (int k = LANE; k < num_walls; k += 64) part[k] = 0;
+    wave_sync();
+    const int px = c.s.main_height - min_sep * num_walls - buf_h;
+    for (int i = 0; i < px; i++) {
+        int k = randn(c, num_walls);
+        if (LANE == 0) part[k] += 1;
+    }
+    wave_sync();
+    int curr_h = 0;
+    for (int k = 0; k < num_walls; k++) {
+        int dy = min_sep + part[k];
+        curr_h += dy;
+        bool use_door = (dy > 5) && rand01(c) < door_prob;
+        fb_add_walls(c, (float)curr_h, use_door, min_pct);
+    }
+    EF(c, F_Y, 0) = EF(c, F_RY, 0);
+    const int num_good = randn(c, 10) + 10;
+    const int num_bad = randn(c, 10) + 10;
+    for (int i = 0; i < c.s.main_width; i++) {
+        int e = add_entity_rxy(c, (float)(i + .5), (float)(c.s.main_height - .5), 0, 0, .5f, .5f, FB_PRESENT);
+        choose_random_theme(c, e);
+    }
+    wave_sync();
+    for (int i = 0; i < num_good; i++) {
+        spawn_entity(c, .5f, FB_GOOD_OBJ, 0, 0, (float)c.s.main_width, (float)c.s.main_height);
+        wave_sync();
+    }
+    for (int i = 0; i < num_bad; i++) {
+        spawn_entity(c, .5f, FB_BAD_OBJ, 0, 0, (float)c.s.main_width, (float)c.s.main_height);
+        wave_sync();
+    }
+    for (int i = 0; i < c.s.num_ents; i++) {
+        int t = EI(c, F_TYPE, i);
+        if (t == FB_GOOD_OBJ || t == FB_BAD_OBJ) {
+            int theme = randn(c, object_group_size);
+            wave_sync();
+            EI(c, F_IMAGE_THEME, i) = theme;
+            fit_aspect_ratio(c, i);
+            wave_sync();
+        }
+    }
+    EF(c, F_ROTATION, 0) = -1 * PI_F / 2;
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1284,6 +1382,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_CLIMBER) climber_game_reset(c);
     if constexpr (G == PG_GAME_LEAPER) leaper_game_reset(c, &scratch->lp);
     if constexpr (G == PG_GAME_CHASER) chaser_game_reset(c, &scratch->ch);
+    if constexpr (G == PG_GAME_FRUITBOT) fruitbot_game_reset(c, scratch->part);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1386,6 +1485,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
+        PG_CASE(PG_GAME_FRUITBOT)
     default: break;
     }
 #undef PG_CASE

@@ -182,6 +182,8 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
         if (src_type == PLAYER && cl_is_wall(target)) return true;
     if constexpr (G == PG_GAME_CHASER) // chaser.cpp:94-99
         if (target == CH_MAZE_WALL) return true;
+    if constexpr (G == PG_GAME_FRUITBOT) // fruitbot.cpp:83-85
+        if (src_type == PLAYER && target == FB_OUT_OF_BOUNDS_WALL) return true;
     if constexpr (G == PG_GAME_MINER) // miner.cpp:68-75
         if (src_type == PLAYER && (target == MN_BOULDER || target == MN_MOVING_BOULDER || target == MN_OOB_WALL))
             return true;
@@ -192,6 +194,8 @@ DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-5
     if constexpr (G == PG_GAME_COINRUN) return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
     if constexpr (G == PG_GAME_CLIMBER) // climber.cpp:113-115
         return src == CL_ENEMY && (cl_is_wall(target) || target == CL_ENEMY_BARRIER);
+    if constexpr (G == PG_GAME_FRUITBOT) // fruitbot.cpp:79-81
+        return src == FB_BAD_OBJ && (target == FB_BARRIER || target == WALL_OBJ);
     if constexpr (G == PG_GAME_MINER) // miner.cpp:77-79 (out_of_bounds_object = OOB_WALL)
         return src == MN_ENEMY && (target == MN_BOULDER || target == MN_DIAMOND || target == MN_MOVING_BOULDER ||
                                    target == MN_MOVING_DIAMOND || target == MN_OOB_WALL);
@@ -607,6 +611,9 @@ DEV void set_action_xy(Ctx &c, int move_action) {
         if (c.s.action_vy == 1) {
             if (!c.s.has_support) c.s.action_vy = 0;
         }
+    } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:154-158
+        c.s.action_vy = 0.2f;
+        c.s.action_vrot = 0;
     } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:299-318
         if (c.s.action_vy < 0) c.s.action_vy = 0;
         if (c.s.action_vx > 0) c.s.facing_right = 1;
@@ -734,6 +741,20 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 c.s.fish_eaten += 1;
             }
         }
+    } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:95-115
+        if (t == FB_BARRIER || t == FB_LOCKED_DOOR) {
+            c.s.sd_done = 1;
+        } else if (t == FB_BAD_OBJ) {
+            c.s.sd_reward += -4; // PENALTY (const int)
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+        } else if (t == FB_GOOD_OBJ) {
+            c.s.sd_reward += 1; // POSITIVE_REWARD (const int)
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+        } else if (t == FB_PRESENT) {
+            c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+            c.s.sd_done = 1;
+            c.s.sd_level_complete = 1;
+        }
     } else if constexpr (G == PG_GAME_CHASER) { // chaser.cpp:119-133
         if (t == CH_LARGE_ORB) {
             c.s.eat_time = c.s.cur_time;
@@ -787,16 +808,79 @@ DEV void handle_agent_collision(Ctx &c, int m) {
 // coinrun: the effects are order-free flags, one lane-parallel pass.  Other games: the
 // colliding entities are handled one at a time from the top, re-testing below the last one
 // with the current agent (bigfish grows the agent; heist keys open later doors).
-// collides_with_entities is set by none of the games built here (flagged if ever seen);
-// check_grid_collisions has an effect only in coinrun (handle_grid_collision, coinrun.cpp:144-154).
+// Entities with collides_with_entities (fruitbot's bullets) run their inner loop (:735-744) at
+// their place in the same descending walk.  check_grid_collisions has an effect only in coinrun
+// (handle_grid_collision, coinrun.cpp:144-154).
+//
+// handle_collision(src, target) (basic :383-385 empty; fruitbot.cpp:117-134)
+template <int G>
+DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_FRUITBOT) {
+        if (EI(c, F_TYPE, si) == FB_PLAYER_BULLET) {
+            const int tt = EI(c, F_TYPE, ti);
+            if (tt == FB_BARRIER) {
+                EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+            } else if (tt == FB_LOCK) {
+                const float ty = EF(c, F_Y, ti);
+                EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+                // the first LOCKED_DOOR in list order within 1 of the lock's y
+                for (int base = 0; base < c.s.num_ents; base += 64) {
+                    int k = base + LANE;
+                    bool hit = k < c.s.num_ents && EI(c, F_TYPE, k) == FB_LOCKED_DOOR && fabsf(EF(c, F_Y, k) - ty) < 1;
+                    unsigned long long b = ballot(hit);
+                    if (b) {
+                        int d = base + __ffsll((long long)b) - 1;
+                        wave_sync();
+                        EI(c, F_FLAGS, d) = EI(c, F_FLAGS, d) | EF_WILL_ERASE;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+}
+
+// the inner loop of an entity with collides_with_entities: j descending, j != i, while neither
+// side is will_erase
+template <int G>
+DEV void entity_collisions(Ctx &c, int i) {
+    int upper = c.s.num_ents;
+    while (upper > 0) {
+        if (EI(c, F_FLAGS, i) & EF_WILL_ERASE) return;
+        const float x = EF(c, F_X, i), y = EF(c, F_Y, i), rx = EF(c, F_RX, i), ry = EF(c, F_RY, i);
+        const float mrg = EF(c, F_COLLISION_MARGIN, i);
+        int m = -1;
+        for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+            int j = base + LANE;
+            bool hit = false;
+            if (j < upper && j != i && !(EI(c, F_FLAGS, j) & EF_WILL_ERASE)) {
+                float tx = (rx + EF(c, F_RX, j)) + mrg, ty = (ry + EF(c, F_RY, j)) + mrg;
+                hit = (fabsf(x - EF(c, F_X, j)) < tx) && (fabsf(y - EF(c, F_Y, j)) < ty);
+            }
+            unsigned long long b = ballot(hit);
+            if (b) {
+                m = base + top_bit(b);
+                break;
+            }
+        }
+        if (m < 0) return;
+        handle_collision<G>(c, i, m);
+        upper = m;
+    }
+}
+
 template <int G>
 DEV void agent_collisions(Ctx &c) {
-    bool unsupported = false;
-    for (int base = 0; base < c.s.num_ents; base += 64) {
-        int i = base + LANE;
-        if (i < c.s.num_ents && (EI(c, F_FLAGS, i) & EF_COLLIDES)) unsupported = true;
+    if constexpr (G == PG_GAME_COINRUN) {
+        bool unsupported = false; // no coinrun entity has collides_with_entities
+        for (int base = 0; base < c.s.num_ents; base += 64) {
+            int i = base + LANE;
+            if (i < c.s.num_ents && (EI(c, F_FLAGS, i) & EF_COLLIDES)) unsupported = true;
+        }
+        if (ballot(unsupported)) c.s.error = PG_ERR_BAD_OPTION;
     }
-    if (ballot(unsupported)) c.s.error = PG_ERR_BAD_OPTION;
     if constexpr (G == PG_GAME_COINRUN) {
         float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
         bool any = false;
@@ -842,22 +926,29 @@ DEV void agent_collisions(Ctx &c) {
             const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
             const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
             int m = -1;
+            bool agent_hit = false;
             for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
                 int i = base + LANE;
-                bool hit = false;
-                if (i < upper && EI(c, F_TYPE, i) != PLAYER && (gh || i != 0)) { // has_agent_collision (:1135-1140)
-                    float mrg = EF(c, F_COLLISION_MARGIN, i);
-                    float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
-                    hit = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
+                bool hit = false, coll = false;
+                if (i < upper) {
+                    if (EI(c, F_TYPE, i) != PLAYER && (gh || i != 0)) { // has_agent_collision (:1135-1140)
+                        float mrg = EF(c, F_COLLISION_MARGIN, i);
+                        float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
+                        hit = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
+                    }
+                    coll = (EI(c, F_FLAGS, i) & EF_COLLIDES) != 0;
                 }
-                unsigned long long b = ballot(hit);
+                unsigned long long b = ballot(hit || coll);
                 if (b) {
                     m = base + top_bit(b);
+                    agent_hit = ballot(hit && i == m) != 0;
                     break;
                 }
             }
             if (m < 0) break;
-            handle_agent_collision<G>(c, m);
+            if (agent_hit) handle_agent_collision<G>(c, m);
+            wave_sync();
+            if (EI(c, F_FLAGS, m) & EF_COLLIDES) entity_collisions<G>(c, m);
             upper = m;
         }
     }
@@ -1489,6 +1580,22 @@ DEV void chaser_step_tail(Ctx &c) {
     wave_sync();
 }
 
+DEV void fruitbot_step_tail(Ctx &c) { // fruitbot.cpp:247-258
+    if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= FB_KEY_DURATION) {
+        const bool gh = c.s.agent_erased;
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float vx = 0, vy = 1, bullet_vscale = .5;
+        wave_sync();
+        int i = append_entity(c, ax, ay, vx * bullet_vscale, vy * bullet_vscale, .25f, .25f, FB_PLAYER_BULLET);
+        if (i >= 0) {
+            EI(c, F_EXPIRE_TIME, i) = FB_KEY_DURATION;
+            EI(c, F_FLAGS, i) = EF_AUTO_ERASE | EF_COLLIDES;
+        }
+        c.s.last_fire_time = c.s.cur_time;
+        wave_sync();
+    }
+}
+
 // ------------------------------------------------------------------ game_step
 template <int G>
 DEV void game_step(Ctx &c) {
@@ -1550,6 +1657,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_CLIMBER) climber_step_tail(c);
     if constexpr (G == PG_GAME_LEAPER) leaper_step_tail(c, rg);
     if constexpr (G == PG_GAME_CHASER) chaser_step_tail(c);
+    if constexpr (G == PG_GAME_FRUITBOT) fruitbot_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1649,6 +1757,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_MINER) { PG_W(diamonds_remaining) PG_W(died) }
         if constexpr (G == PG_GAME_CLIMBER) { PG_W(has_support) PG_W(facing_right) PG_W(coins_collected) }
         if constexpr (G == PG_GAME_CHASER) { PG_W(eat_time) PG_W(orbs_collected) }
+        if constexpr (G == PG_GAME_FRUITBOT) { PG_W(last_fire_time) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1673,6 +1782,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_CLIMBER)
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
+        PG_CASE(PG_GAME_FRUITBOT)
     default: break;
     }
 #undef PG_CASE

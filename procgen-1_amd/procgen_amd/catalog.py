@@ -200,6 +200,21 @@ CHASER_SPRITES = {
     5: ["misc_assets/tileStone_slope.png"],
 }
 
+# ---------------------------------------------------------------- fruitbot
+# procgen/src/games/fruitbot.cpp:46-76 (PLAYER 0, BARRIER 1, OUT_OF_BOUNDS_WALL 2, PLAYER_BULLET 3,
+# BAD_OBJ 4, GOOD_OBJ 7, LOCKED_DOOR 10, LOCK 11, PRESENT 12)
+FRUITBOT_SPRITES = {
+    0: ["misc_assets/robot_3Dblue.png"],
+    1: ["misc_assets/tileStone_slope.png"],
+    2: ["misc_assets/tileStone_slope.png"],
+    3: ["misc_assets/keyRed2.png"],
+    4: ["misc_assets/food%d.png" % i for i in range(1, 7)],
+    7: ["misc_assets/fruit%d.png" % i for i in range(1, 7)],
+    10: ["misc_assets/fenceYellow.png"],
+    11: ["misc_assets/lockRed2.png"],
+    12: ["misc_assets/present%d.png" % i for i in range(1, 4)],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -210,6 +225,7 @@ GAMES = {
     "climber": (CLIMBER_SPRITES, "platform"),   # climber.cpp:43-45
     "leaper": (LEAPER_SPRITES, "topdown"),      # leaper.cpp:41-43
     "chaser": (CHASER_SPRITES, "topdown_simple"),  # chaser.cpp:50-52
+    "fruitbot": (FRUITBOT_SPRITES, "topdown"),  # fruitbot.cpp:42-44
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

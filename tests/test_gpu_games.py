@@ -66,12 +66,12 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
 def test_parity_hard_unbounded(game):
     run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
 def test_parity_200_levels_easy(game):
     run_pair(game, 8, 200, seed=2, num_levels=200, start_level=0, rand_seed=5, distribution_mode="easy",
              latent=game in LATENT)
@@ -90,7 +90,7 @@ def test_miner_long_run_deaths():
     assert episodes > 0
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser"])
+@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
 def test_parity_options(game):
     run_pair(game, 8, 150, seed=4, num_levels=20, rand_seed=3, use_backgrounds=False, restrict_themes=True,
              use_sequential_levels=True)
@@ -115,6 +115,13 @@ def test_chaser_extreme_and_long():
     run_pair("chaser", 32, 600, seed=15, num_levels=0, rand_seed=4)
 
 
+def test_fruitbot_long_and_uncentered():
+    """fruitbot: key bullets (collides_with_entities) open locked doors, fruit / food rewards,
+    vertically tiled background; a long hard run and an uncentered one (visibility = 60)."""
+    run_pair("fruitbot", 32, 500, seed=16, num_levels=0, rand_seed=5)
+    run_pair("fruitbot", 8, 200, seed=17, num_levels=0, rand_seed=6, center_agent=False)
+
+
 def test_bigfish_long_episodes():
     """bigfish episodes run up to 6,000 steps (bigfish.cpp:25): many fish spawn, grow, leave."""
     run_pair("bigfish", 8, 1200, seed=6, num_levels=0, rand_seed=12)
@@ -122,8 +129,8 @@ def test_bigfish_long_episodes():
 
 def test_mixed_batch_parity():
     """env n plays names[n % 4] (vecgame.cpp:357-358), level seeds from the global index."""
-    names = ["bigfish", "chaser", "climber", "coinrun", "heist", "leaper", "maze", "miner"]
-    num = 32
+    names = ["bigfish", "chaser", "climber", "coinrun", "fruitbot", "heist", "leaper", "maze", "miner"]
+    num = 36
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=21)
     orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
     g = gpu_obs(env)
@@ -160,7 +167,7 @@ def test_full_size_sampled_parity(game):
     env.close()
 
 
-@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber", "leaper", "chaser"])
+@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber", "leaper", "chaser", "fruitbot"])
 def test_state_roundtrip(game):
     env = make_gpu(4, game, num_levels=20, rand_seed=11)
     rng = np.random.RandomState(1)
