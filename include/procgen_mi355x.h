@@ -70,8 +70,10 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
 /* Diagnostic builds only (libprocgen_mi355x_prof.so): per-phase cycle sums, out[16]. */
 LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out);
 /* Self-test of libm-dependent device arithmetic on device buffers (tests/test_gpu_libm.py):
- * which = 0: bigfish fish radius 1.75 * pow(u, 1.4) + .25 (bigfish.cpp:84) for n floats u. */
-LIBENV_API int procgen_selftest_libm(int which, const float *d_in, float *d_out, int64_t n, void *stream);
+ * which = 0: bigfish fish radius 1.75 * pow(u, 1.4) + .25 (bigfish.cpp:84) for n floats u (float out);
+ * 1: QTransform::rotate matrix of an entity rotation (4 doubles out); 2: face_direction rotation of
+ * n (dx, dy) pairs (float out). */
+LIBENV_API int procgen_selftest_libm(int which, const float *d_in, void *d_out, int64_t n, void *stream);
 /* Debug read-back of one env's scalar state, see pg_engine.h PGEnv (returns bytes copied). */
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length);
 

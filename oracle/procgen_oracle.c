@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12 };
 
 static void fatal_msg(const char *m) {
@@ -238,7 +238,10 @@ typedef struct {
     int coin_quota, coins_collected;
     /* chaser (chaser.cpp:26-35; free_cells / is_space_vec of the last reset) */
     int eat_timeout, egg_timeout, eat_time, total_enemies, total_orbs, orbs_collected, num_free;
-    int last_fire_time; /* fruitbot (fruitbot.cpp:26-28) */
+    int last_fire_time; /* fruitbot (fruitbot.cpp:26-28), dodgeball (dodgeball.cpp:33) */
+    /* dodgeball (dodgeball.cpp:28-35) */
+    float db_min_dim, db_hard_min_dim, db_ball_vscale, db_ball_r;
+    int db_num_enemies, db_enemy_fire_delay;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -410,6 +413,8 @@ static bool hook_will_reflect(Game *g, int src, int target) {
         return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
     if (g->game_id == GAME_FRUITBOT) /* fruitbot.cpp:79-81: BAD_OBJ 4 off BARRIER 1 / WALL_OBJ */
         return src == 4 && (target == 1 || target == WALL_OBJ);
+    if (g->game_id == GAME_DODGEBALL) /* dodgeball.cpp:98-100: ENEMY 4 off LAVA_WALL 1 / OOB_WALL 10 */
+        return src == 4 && (target == 1 || target == g->out_of_bounds_object);
     if (g->game_id == GAME_CLIMBER) /* climber.cpp:113-115: ENEMY 5 off walls and ENEMY_BARRIER 19 */
         return src == 5 && (target == 15 || target == 16 || target == 19);
     if (g->game_id == GAME_MINER) /* miner.cpp:77-79: ENEMY 5 off BOULDER, DIAMOND, MOVING_BOULDER/DIAMOND, out of bounds */
@@ -418,8 +423,36 @@ static bool hook_will_reflect(Game *g, int src, int target) {
 }
 
 /* handle_collision(src, target) (basic :383-385 is empty) */
+static int spawn_child(Game *g, int src_i, int type, float obj_r) { /* basic-abstract-game.cpp:233-239, match_vel false */
+    Entity *src = &g->ents[src_i];
+    return add_entity(g, src->x, src->y, 0, 0, obj_r, type);
+}
 static void hook_handle_collision(Game *g, int si, int ti) {
     Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_DODGEBALL) { /* dodgeball.cpp:120-151 */
+        if (target->type == 3) { /* PLAYER_BALL */
+            if (src->type == 1) { /* LAVA_WALL */
+                target->will_erase = true;
+            } else if (src->type == 4) { /* ENEMY */
+                src->health -= 1;
+                target->will_erase = true;
+                if (src->health <= 0 && !src->will_erase) {
+                    src->will_erase = true;
+                    g->sd_reward += 2; /* ENEMY_REWARD (const int 2.0f) */
+                    int c = spawn_child(g, si, 8, src->rx); /* DUST_CLOUD */
+                    Entity *ent = &g->ents[c];
+                    ent->vrot = PI_F / 0.3f;
+                    ent->grow_rate = 1.0f / 1.2f;
+                    ent->expire_time = 4;
+                    ent->alpha_decay = 0.9f;
+                    ent->image_theme = g->step_rand_int % 9; /* choose_step_random_theme: 9 spaceEffect themes */
+                }
+            }
+        } else if (target->type == 6) { /* ENEMY_BALL */
+            if (src->type == 1) target->will_erase = true;
+        }
+        return;
+    }
     if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:117-134 */
         if (src->type == 3) { /* PLAYER_BULLET */
             if (target->type == 1) { /* BARRIER */
@@ -454,6 +487,16 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->rx += g->r_inc;
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
+            }
+        }
+    } else if (g->game_id == GAME_DODGEBALL) { /* dodgeball.cpp:102-118 */
+        if (obj->type == 4 || obj->type == 6 || obj->type == 1) { /* ENEMY, ENEMY_BALL, LAVA_WALL */
+            g->sd_done = true;
+        } else if (obj->type == 5) { /* DOOR */
+            if (g->db_num_enemies == 0) {
+                g->sd_done = true;
+                g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+                g->sd_level_complete = true;
             }
         }
     } else if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:95-115 */
@@ -565,6 +608,8 @@ static int hook_image_for_type(Game *g, int type) {
             return -1;
         }
     }
+    if (g->game_id == GAME_DODGEBALL && type == 5) /* dodgeball.cpp:90-96: DOOR -> DOOR_OPEN 7 when clear */
+        return g->db_num_enemies == 0 ? 7 : 5;
     if (g->game_id == GAME_CHASER && type == 6) { /* chaser.cpp:101-113: ENEMY */
         if (g->cur_time - g->eat_time < g->eat_timeout) return 3; /* ENEMY_WEAK */
         int rem = (g->cur_time / 2) % 4;
@@ -2226,6 +2271,255 @@ static void fruitbot_game_step(Game *g) { /* :247-258 */
     }
 }
 
+/* ================================================================== dodgeball (games/dodgeball.cpp) */
+#define DB_LAVA_WALL 1
+#define DB_PLAYER_BALL 3
+#define DB_ENEMY 4
+#define DB_DOOR 5
+#define DB_ENEMY_BALL 6
+#define DB_DUST_CLOUD 8
+static const float DB_ENEMY_VEL = 0.05f;
+
+static void entity_face_direction(Entity *e, float dx, float dy) { /* entity.cpp:84-88, rotation_offset 0 */
+    if (dx != 0 || dy != 0) e->rotation = -1 * atan2f(dy, dx) + 0.0f;
+}
+
+typedef struct { float x, y, w, h; } DbRoom; /* QRectF of float-valued corners */
+
+static void db_add_room(Game *g, DbRoom *rooms, int *n, DbRoom room) { /* :157-164 */
+    float rw = room.w, rh = room.h;
+    if ((rw >= g->db_min_dim || rh >= g->db_min_dim) && (rw >= g->db_hard_min_dim) && (rh >= g->db_hard_min_dim)) {
+        fassert(*n < 64);
+        rooms[(*n)++] = room;
+    }
+}
+
+static void db_split_room(Game *g, DbRoom *rooms, int *n, DbRoom room, float thickness) { /* :166-224 */
+    MT *r = &g->rand_gen;
+    bool will_split_width = rg_rand01(r) < .5;
+    bool choice2 = rg_rand01(r) < .5;
+    if (room.w < g->db_min_dim) will_split_width = false;
+    if (room.h < g->db_min_dim) will_split_width = true;
+    float rx = room.x, ry = room.y, rw = room.w, rh = room.h;
+    float gap = (float)(.25 * (rg_randn(r, 3) + 1));
+    float pct = 1 - gap;
+    if (!will_split_width) {
+        float wy, wh, remy;
+        if (choice2) {
+            wy = ry;
+            remy = ry + pct * rh;
+            wh = pct * rh;
+        } else {
+            wy = ry + (1 - pct) * rh;
+            remy = ry;
+            wh = pct * rh;
+        }
+        add_entity_rxy(g, rx + rw / 2, wy + wh / 2, 0, 0, thickness, wh / 2, DB_LAVA_WALL);
+        float nextw = rw / 2 - thickness;
+        db_add_room(g, rooms, n, (DbRoom){rx, wy, nextw, wh});
+        db_add_room(g, rooms, n, (DbRoom){rx + rw / 2 + thickness, wy, nextw, wh});
+        db_add_room(g, rooms, n, (DbRoom){rx, remy, rw, rh - wh});
+    } else {
+        float wx, ww, remx;
+        if (choice2) {
+            wx = rx;
+            remx = rx + pct * rw;
+            ww = pct * rw;
+        } else {
+            wx = rx + (1 - pct) * rw;
+            remx = rx;
+            ww = pct * rw;
+        }
+        add_entity_rxy(g, wx + ww / 2, ry + rh / 2, 0, 0, ww / 2, thickness, DB_LAVA_WALL);
+        float nexth = rh / 2 - thickness;
+        db_add_room(g, rooms, n, (DbRoom){wx, ry, ww, nexth});
+        db_add_room(g, rooms, n, (DbRoom){wx, ry + rh / 2 + thickness, ww, nexth});
+        db_add_room(g, rooms, n, (DbRoom){remx, ry, rw - ww, rh});
+    }
+}
+
+static void db_choose_vel(Game *g, Entity *e) { /* :226-238 */
+    MT *r = &g->rand_gen;
+    float vel = DB_ENEMY_VEL * (rg_randn(r, 2) * 2 - 1);
+    if (rg_randn(r, 2) == 0) {
+        e->vx = vel;
+        e->vy = 0;
+    } else {
+        e->vy = vel;
+        e->vx = 0;
+    }
+    e->spawn_time = rg_randn(r, 50) + 25;
+}
+
+static int spawn_entity_rxy(Game *g, float rx, float ry, int type, float x, float y, float w, float h) { /* :520-527 */
+    Entity e;
+    entity_init(&e, 0, 0, 0, 0, rx, ry, type);
+    reposition(g, &e, x, y, w, h, true);
+    fassert(g->num_ents < MAX_ENTS);
+    g->ents[g->num_ents] = e;
+    return g->num_ents++;
+}
+
+static bool agent_has_collision(Game *g) { /* :529-538 */
+    for (int i = 0; i < g->num_ents; i++)
+        if (has_agent_collision(g, &g->ents[i])) return true;
+    return false;
+}
+
+static void reposition_agent(Game *g) { /* :540-546 */
+    Entity *agent = AG(g);
+    int count = 0;
+    do {
+        agent->x = rg_rand01(&g->rand_gen) * (g->main_width - 2 * agent->rx) + agent->rx;
+        agent->y = rg_rand01(&g->rand_gen) * (g->main_height - 2 * agent->ry) + agent->ry;
+        count++;
+    } while (agent_has_collision(g) && (count < 100));
+}
+
+static void dodgeball_game_reset(Game *g, const or_atlas *at) { /* :259-369 */
+    MT *r = &g->rand_gen;
+    int world_dim = g->options.distribution_mode == MemoryMode ? 40 : 20; /* choose_world_dim (:248-257) */
+    g->main_width = world_dim;
+    g->main_height = world_dim;
+    basic_game_reset(g, at);
+    g->options.center_agent = g->options.distribution_mode == MemoryMode;
+    g->last_fire_time = 0;
+    DbRoom rooms[64];
+    int nrooms = 0;
+    rooms[nrooms++] = (DbRoom){0, 0, (float)g->main_width, (float)g->main_height};
+    int dm = g->options.distribution_mode;
+    float thickness = 0.3f, enemy_r = .5, exit_r = .75;
+    g->db_ball_r = .25;
+    g->db_ball_vscale = .25;
+    int num_iterations = 0, max_extra_enemies = 3;
+    Entity *agent = AG(g);
+    if (dm == EasyMode) {
+        num_iterations = 2;
+        thickness *= 2; enemy_r *= 2; g->db_ball_r *= 2; g->db_ball_vscale *= 2;
+        g->maxspeed = .75;
+        agent->rx = 1; agent->ry = 1;
+        exit_r *= 2;
+    } else if (dm == HardMode) {
+        num_iterations = 4;
+        thickness *= 1.5; enemy_r *= 1.5; g->db_ball_r *= 1.5; g->db_ball_vscale *= 1.5;
+        g->maxspeed = .5;
+        agent->rx = .75; agent->ry = .75;
+    } else if (dm == ExtremeMode) {
+        num_iterations = 8;
+        g->maxspeed = .25;
+    } else if (dm == MemoryMode) {
+        num_iterations = 16;
+        thickness *= 1.5; enemy_r *= 1.5; g->db_ball_r *= 1.5; g->db_ball_vscale *= 1.5;
+        g->maxspeed = .5;
+        agent->rx = .75; agent->ry = .75;
+        max_extra_enemies = 16;
+    } else {
+        fatal_msg("dodgeball: bad distribution mode");
+    }
+    g->db_hard_min_dim = 4 * agent->rx + 2 * thickness + .5;
+    g->db_min_dim = agent->rx * 8 + .5;
+    for (int it = 0; it < num_iterations; it++) {
+        if (nrooms == 0) break;
+        int idx = rg_randn(r, nrooms);
+        DbRoom room = rooms[idx];
+        memmove(&rooms[idx], &rooms[idx + 1], sizeof(DbRoom) * (size_t)(nrooms - idx - 1));
+        nrooms--;
+        db_split_room(g, rooms, &nrooms, room, thickness);
+    }
+    float border_r = 0;
+    float doorlen = 2 * exit_r;
+    int exit_wall_choice = rg_randn(r, 4);
+    float mw = (float)g->main_width, mh = (float)g->main_height;
+    if (exit_wall_choice == 0)
+        spawn_entity_rxy(g, doorlen / 2, exit_r, DB_DOOR, 2 * border_r, 2 * border_r, mw - 4 * border_r, 2 * exit_r);
+    else if (exit_wall_choice == 1)
+        spawn_entity_rxy(g, doorlen / 2, exit_r, DB_DOOR, 2 * border_r, mh - 2 * border_r - 2 * exit_r, mw - 4 * border_r,
+                         2 * exit_r);
+    else if (exit_wall_choice == 2)
+        spawn_entity_rxy(g, exit_r, doorlen / 2, DB_DOOR, 2 * border_r, 2 * border_r, 2 * exit_r, mh - 4 * border_r);
+    else
+        spawn_entity_rxy(g, exit_r, doorlen / 2, DB_DOOR, mw - 2 * border_r - 2 * exit_r, 2 * border_r, 2 * exit_r,
+                         mh - 4 * border_r);
+    reposition_agent(g);
+    g->db_num_enemies = rg_randn(r, max_extra_enemies + 1) + 3;
+    for (int i = 0; i < g->db_num_enemies; i++) spawn_entity(g, enemy_r, DB_ENEMY, 0, 0, mw, mh);
+    int enemy_theme = rg_randn(r, 7); /* NUM_ENEMY_THEMES */
+    for (int i = 0; i < g->num_ents; i++) {
+        Entity *e = &g->ents[i];
+        if (e->type == DB_ENEMY) {
+            e->image_theme = enemy_theme;
+            e->health = 1;
+            e->spawn_time = 0;
+            e->fire_time = 10;
+            e->collides_with_entities = true;
+            e->smart_step = true;
+            db_choose_vel(g, e);
+            entity_face_direction(e, e->vx, e->vy);
+        } else if (e->type == DB_LAVA_WALL) {
+            e->collides_with_entities = true;
+        }
+    }
+    entity_face_direction(AG(g), 1, 0);
+}
+
+static void db_fire_ball(Game *g, int ei, float vx, float vy) { /* :371-376 */
+    Entity *ent = &g->ents[ei];
+    float ex = ent->x, ey = ent->y;
+    int b = add_entity(g, ex, ey, vx * g->db_ball_vscale, vy * g->db_ball_vscale, g->db_ball_r, DB_ENEMY_BALL);
+    g->ents[ei].fire_time = g->cur_time + rg_randn(&g->rand_gen, 4);
+    g->ents[b].vrot = PI_F * 0.23f; /* BALL_V_ROT */
+    g->ents[b].expire_time = 50;
+}
+
+static void dodgeball_game_step(Game *g) { /* :378-444 */
+    basic_game_step(g);
+    float vx = (float)(g->last_move_action / 3 - 1);
+    float vy = (float)(g->last_move_action % 3 - 1);
+    entity_face_direction(AG(g), vx, vy);
+    if (g->special_action == 1 && (g->cur_time - g->last_fire_time) >= 7) {
+        Entity *agent = AG(g);
+        int b = add_entity(g, agent->x, agent->y, vx * g->db_ball_vscale, vy * g->db_ball_vscale, g->db_ball_r,
+                           DB_PLAYER_BALL);
+        g->ents[b].collides_with_entities = true;
+        g->ents[b].expire_time = 50;
+        g->ents[b].vrot = PI_F * 0.23f;
+        g->last_fire_time = g->cur_time;
+    }
+    g->db_num_enemies = 0;
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *ent = &g->ents[i];
+        if (ent->type == DB_ENEMY) {
+            g->db_num_enemies++;
+            if (ent->spawn_time == 0) db_choose_vel(g, ent);
+            else ent->spawn_time -= 1;
+            bool can_fire = (g->cur_time - ent->fire_time) >= g->db_enemy_fire_delay;
+            if (can_fire) {
+                Entity *agent = AG(g);
+                float dx = ent->x - agent->x;
+                float dy = ent->y - agent->y;
+                float bvelx = (float)(ent->x < agent->x ? 1 : -1);
+                float bvely = (float)(ent->y < agent->y ? 1 : -1);
+                if (fabs((double)dx) < 1) {
+                    db_fire_ball(g, i, 0, bvely);
+                    ent = &g->ents[i];
+                    ent->vx = 0;
+                    ent->vy = bvely * DB_ENEMY_VEL;
+                } else if (fabs((double)dy) < 1) {
+                    db_fire_ball(g, i, bvelx, 0);
+                    ent = &g->ents[i];
+                    ent->vx = bvelx * DB_ENEMY_VEL;
+                    ent->vy = 0;
+                }
+            }
+            entity_face_direction(ent, ent->vx, ent->vy);
+        } else if (ent->type == DB_PLAYER_BALL || ent->type == DB_ENEMY_BALL) {
+            if (ent->x < ent->rx || ent->x > (g->main_width - ent->rx)) ent->will_erase = true;
+            else if (ent->y < ent->ry || ent->y > (g->main_height - ent->ry)) ent->will_erase = true;
+        }
+    }
+    erase_if_needed(g);
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -2374,6 +2668,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_LEAPER) leaper_game_reset(g, at);
     else if (g->game_id == GAME_CHASER) chaser_game_reset(g, at);
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_reset(g, at);
+    else if (g->game_id == GAME_DODGEBALL) dodgeball_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -2386,6 +2681,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_LEAPER) leaper_game_step(g, at);
     else if (g->game_id == GAME_CHASER) chaser_game_step(g);
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_step(g);
+    else if (g->game_id == GAME_DODGEBALL) dodgeball_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -2858,6 +3154,7 @@ static void tile_image(Game *g, const uint32_t *px, int iw, int ih, bool refl, d
 
 static float hook_tile_aspect_ratio(Game *g, const Entity *e) {
     if (g->game_id == GAME_LEAPER && e->type == LP_FINISH_LINE) return 1; /* leaper.cpp:68-74 */
+    if (g->game_id == GAME_DODGEBALL && e->type == 1) return e->rx > e->ry ? 1 : -1; /* dodgeball.cpp:240-246 */
     if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:87-93 */
         if (e->type == 1) return 1;
         if (e->type == 10) return 3.25f;
@@ -2995,6 +3292,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "leaper") == 0) return GAME_LEAPER;
     if (strcmp(name, "chaser") == 0) return GAME_CHASER;
     if (strcmp(name, "fruitbot") == 0) return GAME_FRUITBOT;
+    if (strcmp(name, "dodgeball") == 0) return GAME_DODGEBALL;
     return -1;
 }
 
@@ -3049,6 +3347,11 @@ static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
     g->bg_tile_ratio = -1;
     g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
 }
+static void dodgeball_ctor(Game *g) { /* dodgeball.cpp:37-44 */
+    g->mixrate = .5;
+    g->db_enemy_fire_delay = 50;
+    g->out_of_bounds_object = 10; /* OOB_WALL */
+}
 static void chaser_ctor(Game *g) { /* chaser.cpp:37-47 */
     g->mixrate = 1;
     g->maxspeed = .5f;
@@ -3086,9 +3389,12 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     int gid = game_id_of(env_name);
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
-    /* game.cpp:76-86: easy and hard for every game; memory for heist and maze (of those restated) */
-    bool dm_ok = dm == EasyMode || dm == HardMode || (dm == ExtremeMode && (gid == GAME_LEAPER || gid == GAME_CHASER)) ||
-                 (dm == MemoryMode && (gid == GAME_HEIST || gid == GAME_MAZE || gid == GAME_MINER));
+    /* game.cpp:76-86: easy and hard for every game; extreme for chaser, dodgeball, leaper, starpilot;
+     * memory for caveflyer, dodgeball, heist, jumper, maze, miner (game ids: procgen/env.py:15-32) */
+    bool dm_ok = dm == EasyMode || dm == HardMode ||
+                 (dm == ExtremeMode && (gid == GAME_CHASER || gid == GAME_DODGEBALL || gid == GAME_LEAPER || gid == 15)) ||
+                 (dm == MemoryMode && (gid == 2 || gid == GAME_DODGEBALL || gid == GAME_HEIST || gid == 9 ||
+                                       gid == GAME_MAZE || gid == GAME_MINER));
     if (!dm_ok) return NULL;
     Vec *v = (Vec *)calloc(1, sizeof(Vec));
     v->count = count;
@@ -3120,6 +3426,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_LEAPER) leaper_ctor(g);
         else if (gid == GAME_CHASER) chaser_ctor(g);
         else if (gid == GAME_FRUITBOT) fruitbot_ctor(g);
+        else if (gid == GAME_DODGEBALL) dodgeball_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;
@@ -3287,6 +3594,20 @@ static double rd_f64(Rd *r) {
 void oracle_bigfish_radius(const float *u, float *out, int64_t n) {
     for (int64_t i = 0; i < n; i++)
         out[i] = (float)((double)(BF_FISH_MAX_R - BF_FISH_MIN_R) * pow((double)u[i], 1.4) + (double)BF_FISH_MIN_R);
+}
+
+/* libm pins of the device's rotation math (tests/test_gpu_libm.py): the QTransform::rotate matrix of
+ * draw_image (m11, m12, m21, m22 before the qFuzzyIsNull clean-up) for each entity rotation, and
+ * -atan2f(dy, dx) of Entity::face_direction */
+void oracle_qt_rotation(const float *rot, double *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) {
+        float deg = rot[i] * 180 / PI_F;
+        QtXform t = qt_translate_rotate(0, 0, (double)deg);
+        out[4 * i + 0] = t.m11; out[4 * i + 1] = t.m12; out[4 * i + 2] = t.m21; out[4 * i + 3] = t.m22;
+    }
+}
+void oracle_face_rotation(const float *dxy, float *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = -1 * atan2f(dxy[2 * i + 1], dxy[2 * i]) + 0.0f;
 }
 
 /* MazeGen pin, same contract as oracle/ref_harness.cpp ref_mazegen */

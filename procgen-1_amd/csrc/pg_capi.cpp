@@ -116,9 +116,10 @@ int game_id(const std::string &name) {
     if (name == "leaper") return PG_GAME_LEAPER;
     if (name == "chaser") return PG_GAME_CHASER;
     if (name == "fruitbot") return PG_GAME_FRUITBOT;
+    if (name == "dodgeball") return PG_GAME_DODGEBALL;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, fruitbot, heist, leaper, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -178,6 +179,10 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_DODGEBALL) { // dodgeball.cpp:37-44
+        s.mixrate = .5;
+        s.enemy_fire_delay = 50;
+        s.out_of_bounds_object = 10; // OOB_WALL
     } else if (gid == PG_GAME_CHASER) { // chaser.cpp:37-47
         s.mixrate = 1;
         s.maxspeed = .5f;
@@ -526,10 +531,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         int gid = game_id(nm);
         if (gid < 0) return bad("env '" + nm + "' is not in this build (supported: " + SUPPORTED_GAMES + ")");
         // game.cpp:76-86 distribution mode validity
+        // (game ids = procgen/env.py:15-32 order: caveflyer 2, jumper 9, starpilot 15)
         bool dm_ok = distribution_mode == PG_EASY || distribution_mode == PG_HARD ||
-                     (distribution_mode == PG_EXTREME && (gid == PG_GAME_LEAPER || gid == PG_GAME_CHASER)) ||
-                     (distribution_mode == PG_MEMORY &&
-                      (gid == PG_GAME_HEIST || gid == PG_GAME_MAZE || gid == PG_GAME_MINER));
+                     (distribution_mode == PG_EXTREME && (gid == PG_GAME_CHASER || gid == PG_GAME_DODGEBALL ||
+                                                          gid == PG_GAME_LEAPER || gid == 15)) ||
+                     (distribution_mode == PG_MEMORY && (gid == 2 || gid == PG_GAME_DODGEBALL || gid == PG_GAME_HEIST ||
+                                                         gid == 9 || gid == PG_GAME_MAZE || gid == PG_GAME_MINER));
         if (!dm_ok) return bad("invalid distribution_mode for " + nm);
         gids.push_back(gid);
     }

@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "pg_engine.h"
+#include "pg_sincos.h"
 
 #define DEV __device__ __forceinline__
 #define LANE ((int)threadIdx.x)
@@ -96,6 +97,16 @@ DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 #define FB_LOCK 11
 #define FB_PRESENT 12
 #define FB_KEY_DURATION 8
+// dodgeball.cpp:10-24
+#define DB_LAVA_WALL 1
+#define DB_PLAYER_BALL 3
+#define DB_ENEMY 4
+#define DB_DOOR 5
+#define DB_ENEMY_BALL 6
+#define DB_DOOR_OPEN 7
+#define DB_DUST_CLOUD 8
+#define DB_OOB_WALL 10
+#define DB_ENEMY_VEL 0.05f
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3
@@ -121,6 +132,50 @@ DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 // rot_table slots: face_direction(dx, dy) -> (dx + 1) * 3 + (dy + 1); ring keys (PI / 2)
 #define PG_ROT_RING_KEY 9
 #define PI_F 3.14159265358979323846264338327950288f
+
+// atan2f as the C library returns it (entity.cpp:86 calls std::atan2(float, float)): the axis and
+// diagonal directions the games face are exact constants (the correctly rounded float of
+// 0, pi/4, pi/2, 3pi/4, pi with the sign of dy; checked against glibc in tests/test_gpu_libm.py);
+// any other direction uses the device atan2f (render-only rotation, pixel tolerance class).
+DEV float pg_atan2f(float dy, float dx) {
+    if (dy == 0) return dx >= 0 && !signbit(dx) ? dy : copysignf(PI_F, dy);
+    if (dx == 0) return copysignf(PI_F / 2, dy);
+    if (fabsf(dx) == fabsf(dy)) return copysignf(dx > 0 ? __uint_as_float(0x3f490fdbu) : __uint_as_float(0x4016cbe4u), dy);
+    return atan2f(dy, dx);
+}
+// Entity::face_direction(dx, dy, rotation_offset = 0) (entity.cpp:84-88)
+DEV float face_rotation(float dx, float dy, float rot) {
+    if (dx != 0 || dy != 0) rot = -1 * pg_atan2f(dy, dx) + 0.0f;
+    return rot;
+}
+
+// QTransform::rotate(rotation * 180 / PI) of draw_image (basic-abstract-game.cpp:912-913; Qt5
+// qtransform.cpp): exact special cases for +-90 / 180 / 270, otherwise sin / cos of deg2rad * a in
+// double (correctly rounded here, pg_sincos.h); QTransform::type() then treats a qFuzzyIsNull sine
+// (|s| <= 1e-12) as no rotation.
+// m = {m11, m12, m21, m22}.  The host builds the same matrices with the C library for the
+// angles of the rotation table; this is the device path for every other angle.
+DEV void qt_rotation_matrix(float rotation, double *m) {
+    const double a = (double)(rotation * 180 / PI_F);
+    double sina = 0, cosa = 0;
+    if (a == 0) {
+        cosa = 1;
+    } else if (a == 90. || a == -270.) {
+        sina = 1;
+    } else if (a == 270. || a == -90.) {
+        sina = -1;
+    } else if (a == 180.) {
+        cosa = -1;
+    } else {
+        const double b = 0.017453292519943295769 * a;
+        pg_sincos_cr(b, &sina, &cosa);
+    }
+    m[0] = cosa; m[1] = sina; m[2] = -sina; m[3] = cosa;
+    if (fabs(sina) <= 0.000000000001) {
+        m[1] = 0;
+        m[2] = 0;
+    }
+}
 
 DEV bool cr_is_wall(int t) { return t == CR_WALL_MID || t == CR_WALL_TOP; }
 DEV bool cr_is_lava(int t) { return t == CR_LAVA_MID || t == CR_LAVA_TOP; }

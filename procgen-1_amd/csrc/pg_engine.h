@@ -22,7 +22,7 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
     PG_GAME_MINER = 12
 };
 #ifndef PG_NUM_GAMES
@@ -167,8 +167,15 @@ struct PGEnv {
     int32_t total_orbs;
     int32_t orbs_collected;
     // ---- fruitbot (fruitbot.cpp:26-28)
-    int32_t last_fire_time;
-    int32_t pad[128 - 101];
+    int32_t last_fire_time;   // (also dodgeball, dodgeball.cpp:33)
+    // ---- dodgeball (dodgeball.cpp:28-35; the rooms list lives only during the reset)
+    float db_min_dim;
+    float db_hard_min_dim;
+    float db_ball_vscale;
+    float db_ball_r;
+    int32_t num_enemies;
+    int32_t enemy_fire_delay;
+    int32_t pad[128 - 107];
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

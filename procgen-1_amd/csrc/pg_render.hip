@@ -119,6 +119,8 @@ DEV int image_for_type(const PGEnv &s, int type, int player_img) {
         if (type == PLAYER) return player_img;
         if (type == CR_ENEMY_BARRIER) return -1;
     }
+    if constexpr (G == PG_GAME_DODGEBALL) // dodgeball.cpp:90-96
+        if (type == DB_DOOR) return s.num_enemies == 0 ? DB_DOOR_OPEN : DB_DOOR;
     if constexpr (G == PG_GAME_MINER) { // miner.cpp:95-103
         if (type == MN_MOVING_BOULDER) return MN_BOULDER;
         if (type == MN_MOVING_DIAMOND) return MN_DIAMOND;
@@ -145,8 +147,9 @@ DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entit
 }
 // get_tile_aspect_ratio (basic :417-419; leaper.cpp:68-74): 0 = one image, > 0 tile horizontally
 template <int G>
-DEV float tile_aspect_ratio(int type) {
+DEV float tile_aspect_ratio(int type, float rx, float ry) {
     if constexpr (G == PG_GAME_LEAPER) return type == LP_FINISH_LINE ? 1.0f : 0.0f;
+    if constexpr (G == PG_GAME_DODGEBALL) return type == DB_LAVA_WALL ? (rx > ry ? 1.0f : -1.0f) : 0.0f; // :240-246
     if constexpr (G == PG_GAME_FRUITBOT) return type == FB_BARRIER ? 1.0f : (type == FB_LOCKED_DOOR ? 3.25f : 0.0f);
     return 0.0f;
 }
@@ -457,7 +460,13 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
             const int caj = readlane(im.ca, j);
             if (readlane(im.rot ? 1 : 0, j)) {
                 const int k = readlane(im.rslot, j);
-                const double *mt = d.rot_table + 4 * k;
+                double mt[4];
+                if (k >= 0) {
+                    const double *tm = d.rot_table + 4 * k;
+                    mt[0] = tm[0]; mt[1] = tm[1]; mt[2] = tm[2]; mt[3] = tm[3];
+                } else {
+                    qt_rotation_matrix(__builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j)), mt);
+                }
                 if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
                                   readlane_d(im.rh, j), mt[0], mt[1], mt[2], mt[3], (uint32_t)readlane(im.soff, j),
                                   readlane(im.sw, j), readlane(im.sh, j), readlane(im.mir, j) != 0, caj))
@@ -567,16 +576,15 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         int rslot = -1;
         for (int k = 0; k < PG_ROT_N; k++)
             if (__float_as_uint(d.rot_angles[k]) == __float_as_uint(rotation)) rslot = k;
-        if (rslot < 0) {
-            err = true;
-        } else {
-            im.rslot = rslot;
-            im.draw = true;
-            im.rot = true;
-            im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
-        }
-    } else if (tile_aspect_ratio<G>(etype) != 0) {
-        float tile_ratio = tile_aspect_ratio<G>(etype);
+        // rslot < 0: an angle outside the host table, its matrix is built on the device at blit
+        // time (qt_rotation_matrix; the rotation value rides in tw)
+        im.rslot = rslot;
+        im.tw = rotation;
+        im.draw = true;
+        im.rot = true;
+        im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
+    } else if (tile_aspect_ratio<G>(etype, prx, pry) != 0) {
+        float tile_ratio = tile_aspect_ratio<G>(etype, prx, pry);
         int num_tiles;
         if (tile_ratio < 0) {
             tile_ratio = -1 * tile_ratio;
@@ -1049,6 +1057,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
+        PG_CASE(PG_GAME_DODGEBALL)
     default: break;
     }
 #undef PG_CASE

@@ -47,6 +47,7 @@ struct ChaserScratch {
 template <int G> struct Scratch { uint32_t dummy[1]; };
 template <> struct Scratch<PG_GAME_CHASER> { ChaserScratch ch; };
 template <> struct Scratch<PG_GAME_FRUITBOT> { int16_t part[16]; };
+template <> struct Scratch<PG_GAME_DODGEBALL> { float4 rooms[64]; }; // QRectF x, y, w, h
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -172,6 +173,11 @@ DEV void choose_world_dim(RCtx &c) {
         else if (d == PG_HARD) { c.s.main_width = 20; c.s.main_height = 20; }
         else if (d == PG_MEMORY) { c.s.main_width = 35; c.s.main_height = 35; }
         c.s.main_area = c.s.main_width * c.s.main_height;
+    }
+    if constexpr (G == PG_GAME_DODGEBALL) { // dodgeball.cpp:248-257
+        const int world_dim = c.s.opt_distribution_mode == PG_MEMORY ? 40 : 20;
+        c.s.main_width = world_dim;
+        c.s.main_height = world_dim;
     }
     if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:144-152
         c.s.main_width = c.s.opt_distribution_mode == PG_EASY ? 10 : 20;
@@ -719,17 +725,47 @@ DEV bool spawn_collides(RCtx &c, float x, float y, float rx, float ry) {
     return ballot(hit) != 0;
 }
 
-// spawn_entity(r, type, x, y, w, h) (:520-527, 571-573): Entity(0, 0, 0, 0, r, r, type), reposition, push_back
-DEV int spawn_entity(RCtx &c, float r, int type, float x, float y, float w, float h) {
-    float ex = rand_pos(c, r, x, x + w);
-    float ey = rand_pos(c, r, y, y + h);
+// spawn_entity_rxy(rx, ry, type, x, y, w, h) (:520-527): Entity(0, 0, 0, 0, rx, ry, type), reposition, push_back
+DEV int spawn_entity_rxy(RCtx &c, float rx, float ry, int type, float x, float y, float w, float h) {
+    float ex = rand_pos(c, rx, x, x + w);
+    float ey = rand_pos(c, ry, y, y + h);
     int count = 0;
-    while (spawn_collides(c, ex, ey, r, r) && count < 100) {
-        ex = rand_pos(c, r, x, x + w);
-        ey = rand_pos(c, r, y, y + h);
+    while (spawn_collides(c, ex, ey, rx, ry) && count < 100) {
+        ex = rand_pos(c, rx, x, x + w);
+        ey = rand_pos(c, ry, y, y + h);
         count++;
     }
-    return add_entity(c, ex, ey, 0, 0, r, type);
+    return add_entity_rxy(c, ex, ey, 0, 0, rx, ry, type);
+}
+// spawn_entity(r, type, x, y, w, h) (:571-573)
+DEV int spawn_entity(RCtx &c, float r, int type, float x, float y, float w, float h) {
+    return spawn_entity_rxy(c, r, r, type, x, y, w, h);
+}
+
+// reposition_agent (:540-546): agent_has_collision() = has_agent_collision(ent) over `entities`
+// (has_collision(ent, agent, ent->collision_margin); PLAYER entities excluded, :1135-1140)
+DEV void reposition_agent(RCtx &c) {
+    const float arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+    int count = 0;
+    bool hit;
+    do {
+        const float ax = rand01(c) * (c.s.main_width - 2 * arx) + arx;
+        const float ay = rand01(c) * (c.s.main_height - 2 * ary) + ary;
+        EF(c, F_X, 0) = ax;
+        EF(c, F_Y, 0) = ay;
+        count++;
+        bool h = false;
+        for (int base = 0; base < c.s.num_ents; base += 64) {
+            const int i = base + LANE;
+            if (i < c.s.num_ents && EI(c, F_TYPE, i) != PLAYER) {
+                const float tx = (EF(c, F_RX, i) + arx) + EF(c, F_COLLISION_MARGIN, i);
+                const float ty = (EF(c, F_RY, i) + ary) + EF(c, F_COLLISION_MARGIN, i);
+                if ((fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty)) h = true;
+            }
+        }
+        hit = ballot(h) != 0;
+    } while (hit && count < 100);
+    wave_sync();
 }
 
 DEV void heist_game_reset(RCtx &c, MGScratch *scratch) {
@@ -1058,6 +1094,168 @@ DEV void fruitbot_game_reset(RCtx &c, int16_t *part) {
     EF(c, F_ROTATION, 0) = -1 * PI_F / 2;
 }
 
+// ------------------------------------------------------------------ dodgeball (dodgeball.cpp:157-369)
+DEV void db_add_room(RCtx &c, float4 *rooms, int &n, float x, float y, float w, float h) { // :157-164
+    if ((w >= c.s.db_min_dim || h >= c.s.db_min_dim) && (w >= c.s.db_hard_min_dim) && (h >= c.s.db_hard_min_dim)) {
+        if (n >= 64) {
+            c.s.error = PG_ERR_GRID;
+            return;
+        }
+        if (LANE == 0) rooms[n] = make_float4(x, y, w, h);
+        n++;
+    }
+}
+
+DEV void db_split_room(RCtx &c, float4 *rooms, int &n, float4 room, float thickness) { // :166-224
+    bool will_split_width = rand01(c) < .5;
+    const bool choice2 = rand01(c) < .5;
+    if (room.z < c.s.db_min_dim) will_split_width = false;
+    if (room.w < c.s.db_min_dim) will_split_width = true;
+    const float rx = room.x, ry = room.y, rw = room.z, rh = room.w;
+    const float gap = (float)(.25 * (randn(c, 3) + 1));
+    const float pct = 1 - gap;
+    if (!will_split_width) {
+        float wy, wh, remy;
+        if (choice2) {
+            wy = ry;
+            remy = ry + pct * rh;
+            wh = pct * rh;
+        } else {
+            wy = ry + (1 - pct) * rh;
+            remy = ry;
+            wh = pct * rh;
+        }
+        add_entity_rxy(c, rx + rw / 2, wy + wh / 2, 0, 0, thickness, wh / 2, DB_LAVA_WALL);
+        const float nextw = rw / 2 - thickness;
+        db_add_room(c, rooms, n, rx, wy, nextw, wh);
+        db_add_room(c, rooms, n, rx + rw / 2 + thickness, wy, nextw, wh);
+        db_add_room(c, rooms, n, rx, remy, rw, rh - wh);
+    } else {
+        float wx, ww, remx;
+        if (choice2) {
+            wx = rx;
+            remx = rx + pct * rw;
+            ww = pct * rw;
+        } else {
+            wx = rx + (1 - pct) * rw;
+            remx = rx;
+            ww = pct * rw;
+        }
+        add_entity_rxy(c, wx + ww / 2, ry + rh / 2, 0, 0, ww / 2, thickness, DB_LAVA_WALL);
+        const float nexth = rh / 2 - thickness;
+        db_add_room(c, rooms, n, wx, ry, ww, nexth);
+        db_add_room(c, rooms, n, wx, ry + rh / 2 + thickness, ww, nexth);
+        db_add_room(c, rooms, n, remx, ry, rw - ww, rh);
+    }
+    wave_sync();
+}
+
+DEV void db_choose_vel(RCtx &c, int i) { // :226-238
+    const float vel = DB_ENEMY_VEL * (randn(c, 2) * 2 - 1);
+    if (randn(c, 2) == 0) {
+        EF(c, F_VX, i) = vel;
+        EF(c, F_VY, i) = 0;
+    } else {
+        EF(c, F_VY, i) = vel;
+        EF(c, F_VX, i) = 0;
+    }
+    EI(c, F_SPAWN_TIME, i) = randn(c, 50) + 25;
+}
+
+DEV void dodgeball_game_reset(RCtx &c, float4 *rooms) { // :259-369
+    base_game_reset<PG_GAME_DODGEBALL>(c);
+    c.s.opt_center_agent = c.s.opt_distribution_mode == PG_MEMORY;
+    c.s.last_fire_time = 0;
+    int n = 0;
+    if (LANE == 0) rooms[0] = make_float4(0, 0, (float)c.s.main_width, (float)c.s.main_height);
+    n = 1;
+    const int dm = c.s.opt_distribution_mode;
+    float thickness = 0.3f, enemy_r = .5, exit_r = .75;
+    float ball_r = .25, ball_vscale = .25;
+    int num_iterations = 0, max_extra_enemies = 3;
+    if (dm == PG_EASY) {
+        num_iterations = 2;
+        thickness *= 2; enemy_r *= 2; ball_r *= 2; ball_vscale *= 2;
+        c.s.maxspeed = .75;
+        EF(c, F_RX, 0) = 1; EF(c, F_RY, 0) = 1;
+        exit_r *= 2;
+    } else if (dm == PG_HARD) {
+        num_iterations = 4;
+        thickness *= 1.5; enemy_r *= 1.5; ball_r *= 1.5; ball_vscale *= 1.5;
+        c.s.maxspeed = .5;
+        EF(c, F_RX, 0) = .75; EF(c, F_RY, 0) = .75;
+    } else if (dm == PG_EXTREME) {
+        num_iterations = 8;
+        c.s.maxspeed = .25;
+    } else { // PG_MEMORY
+        num_iterations = 16;
+        thickness *= 1.5; enemy_r *= 1.5; ball_r *= 1.5; ball_vscale *= 1.5;
+        c.s.maxspeed = .5;
+        EF(c, F_RX, 0) = .75; EF(c, F_RY, 0) = .75;
+        max_extra_enemies = 16;
+    }
+    c.s.db_ball_r = ball_r;
+    c.s.db_ball_vscale = ball_vscale;
+    const float arx = EF(c, F_RX, 0);
+    c.s.db_hard_min_dim = (float)(4 * arx + 2 * thickness + .5);
+    c.s.db_min_dim = (float)(arx * 8 + .5);
+    wave_sync();
+    for (int it = 0; it < num_iterations; it++) {
+        if (n == 0) break;
+        const int idx = randn(c, n);
+        const float4 room = rooms[idx];
+        wave_sync();
+        // rooms.erase(idx): order-preserving shift
+        float4 mv = make_float4(0, 0, 0, 0);
+        const int k = idx + 1 + LANE;
+        if (k < n) mv = rooms[k];
+        wave_sync();
+        if (k < n) rooms[k - 1] = mv;
+        wave_sync();
+        n--;
+        db_split_room(c, rooms, n, room, thickness);
+    }
+    const float border_r = 0;
+    const float doorlen = 2 * exit_r;
+    const int exit_wall_choice = randn(c, 4);
+    const float mw = (float)c.s.main_width, mh = (float)c.s.main_height;
+    if (exit_wall_choice == 0)
+        spawn_entity_rxy(c, doorlen / 2, exit_r, DB_DOOR, 2 * border_r, 2 * border_r, mw - 4 * border_r, 2 * exit_r);
+    else if (exit_wall_choice == 1)
+        spawn_entity_rxy(c, doorlen / 2, exit_r, DB_DOOR, 2 * border_r, mh - 2 * border_r - 2 * exit_r, mw - 4 * border_r,
+                         2 * exit_r);
+    else if (exit_wall_choice == 2)
+        spawn_entity_rxy(c, exit_r, doorlen / 2, DB_DOOR, 2 * border_r, 2 * border_r, 2 * exit_r, mh - 4 * border_r);
+    else
+        spawn_entity_rxy(c, exit_r, doorlen / 2, DB_DOOR, mw - 2 * border_r - 2 * exit_r, 2 * border_r, 2 * exit_r,
+                         mh - 4 * border_r);
+    wave_sync();
+    reposition_agent(c);
+    c.s.num_enemies = randn(c, max_extra_enemies + 1) + 3;
+    for (int i = 0; i < c.s.num_enemies; i++) {
+        spawn_entity(c, enemy_r, DB_ENEMY, 0, 0, mw, mh);
+        wave_sync();
+    }
+    const int enemy_theme = randn(c, 7); // NUM_ENEMY_THEMES
+    for (int i = 0; i < c.s.num_ents; i++) {
+        const int t = EI(c, F_TYPE, i);
+        if (t == DB_ENEMY) {
+            EI(c, F_IMAGE_THEME, i) = enemy_theme;
+            EF(c, F_HEALTH, i) = 1;
+            EI(c, F_SPAWN_TIME, i) = 0;
+            EI(c, F_FIRE_TIME, i) = 10;
+            EI(c, F_FLAGS, i) = EF_AUTO_ERASE | EF_COLLIDES | EF_SMART_STEP;
+            db_choose_vel(c, i);
+            EF(c, F_ROTATION, i) = face_rotation(EF(c, F_VX, i), EF(c, F_VY, i), EF(c, F_ROTATION, i));
+        } else if (t == DB_LAVA_WALL) {
+            EI(c, F_FLAGS, i) = EF_AUTO_ERASE | EF_COLLIDES;
+        }
+        wave_sync();
+    }
+    EF(c, F_ROTATION, 0) = face_rotation(1, 0, EF(c, F_ROTATION, 0));
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1383,6 +1581,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_LEAPER) leaper_game_reset(c, &scratch->lp);
     if constexpr (G == PG_GAME_CHASER) chaser_game_reset(c, &scratch->ch);
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_game_reset(c, scratch->part);
+    if constexpr (G == PG_GAME_DODGEBALL) dodgeball_game_reset(c, scratch->rooms);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1486,6 +1685,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
+        PG_CASE(PG_GAME_DODGEBALL)
     default: break;
     }
 #undef PG_CASE

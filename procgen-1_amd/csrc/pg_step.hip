@@ -196,6 +196,8 @@ DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-5
         return src == CL_ENEMY && (cl_is_wall(target) || target == CL_ENEMY_BARRIER);
     if constexpr (G == PG_GAME_FRUITBOT) // fruitbot.cpp:79-81
         return src == FB_BAD_OBJ && (target == FB_BARRIER || target == WALL_OBJ);
+    if constexpr (G == PG_GAME_DODGEBALL) // dodgeball.cpp:98-100 (out_of_bounds_object = OOB_WALL)
+        return src == DB_ENEMY && (target == DB_LAVA_WALL || target == DB_OOB_WALL);
     if constexpr (G == PG_GAME_MINER) // miner.cpp:77-79 (out_of_bounds_object = OOB_WALL)
         return src == MN_ENEMY && (target == MN_BOULDER || target == MN_DIAMOND || target == MN_MOVING_BOULDER ||
                                    target == MN_MOVING_DIAMOND || target == MN_OOB_WALL);
@@ -244,16 +246,19 @@ DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
 // out-of-bounds object).  Every other (obj, m) pair is a no-op, so the scan visits only the
 // interactors, collected once per step into LDS; entity indices do not change during
 // step_entities (no insertion or erase there).
+// dodgeball: LAVA_WALL reflects ENEMY (dodgeball.cpp:98-100); no entity type blocks.
 template <int G>
 DEV bool scan_needed(bool is_h) {
     if constexpr (G == PG_GAME_COINRUN) return !is_h;
     if constexpr (G == PG_GAME_HEIST) return true;
+    if constexpr (G == PG_GAME_DODGEBALL) return true;
     return false;
 }
 template <int G>
 DEV bool is_interactor(int type) {
     if constexpr (G == PG_GAME_COINRUN) return type == CR_CRATE;
     if constexpr (G == PG_GAME_HEIST) return type == HS_LOCKED_DOOR;
+    if constexpr (G == PG_GAME_DODGEBALL) return type == DB_LAVA_WALL;
     return false;
 }
 
@@ -741,6 +746,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 c.s.fish_eaten += 1;
             }
         }
+    } else if constexpr (G == PG_GAME_DODGEBALL) { // dodgeball.cpp:102-118
+        if (t == DB_ENEMY || t == DB_ENEMY_BALL || t == DB_LAVA_WALL) {
+            c.s.sd_done = 1;
+        } else if (t == DB_DOOR && c.s.num_enemies == 0) {
+            c.s.sd_done = 1;
+            c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+            c.s.sd_level_complete = 1;
+        }
     } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:95-115
         if (t == FB_BARRIER || t == FB_LOCKED_DOOR) {
             c.s.sd_done = 1;
@@ -813,8 +826,39 @@ DEV void handle_agent_collision(Ctx &c, int m) {
 // (handle_grid_collision, coinrun.cpp:144-154).
 //
 // handle_collision(src, target) (basic :383-385 empty; fruitbot.cpp:117-134)
+DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type);
 template <int G>
 DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_DODGEBALL) { // dodgeball.cpp:120-151
+        const int tt = EI(c, F_TYPE, ti), st = EI(c, F_TYPE, si);
+        if (tt == DB_PLAYER_BALL) {
+            if (st == DB_LAVA_WALL) {
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+            } else if (st == DB_ENEMY) {
+                const float h = EF(c, F_HEALTH, si) - 1;
+                EF(c, F_HEALTH, si) = h;
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+                const int sf = EI(c, F_FLAGS, si);
+                if (h <= 0 && !(sf & EF_WILL_ERASE)) {
+                    EI(c, F_FLAGS, si) = sf | EF_WILL_ERASE;
+                    c.s.sd_reward += 2; // ENEMY_REWARD (const int 2.0f)
+                    // spawn_child(src, DUST_CLOUD, src->rx) (basic-abstract-game.cpp:233-239)
+                    const float sx = EF(c, F_X, si), sy = EF(c, F_Y, si), sr = EF(c, F_RX, si);
+                    wave_sync();
+                    const int k = append_entity(c, sx, sy, 0, 0, sr, sr, DB_DUST_CLOUD);
+                    if (k >= 0) {
+                        EF(c, F_VROT, k) = PI_F / 0.3f;
+                        EF(c, F_GROW_RATE, k) = 1.0f / 1.2f;
+                        EI(c, F_EXPIRE_TIME, k) = 4;
+                        EF(c, F_ALPHA_DECAY, k) = 0.9f;
+                        EI(c, F_IMAGE_THEME, k) = c.s.step_rand_int % c.d.num_themes[DB_DUST_CLOUD]; // choose_step_random_theme
+                    }
+                }
+            }
+        } else if (tt == DB_ENEMY_BALL) {
+            if (st == DB_LAVA_WALL) EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+        }
+    }
     if constexpr (G == PG_GAME_FRUITBOT) {
         if (EI(c, F_TYPE, si) == FB_PLAYER_BULLET) {
             const int tt = EI(c, F_TYPE, ti);
@@ -1580,6 +1624,110 @@ DEV void chaser_step_tail(Ctx &c) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ dodgeball (dodgeball.cpp:226-238, 371-444)
+DEV void db_choose_vel(Ctx &c, uint32_t *rg, int i) { // :226-238
+    const float vel = DB_ENEMY_VEL * (rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), 2) * 2 - 1);
+    if (rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), 2) == 0) {
+        EF(c, F_VX, i) = vel;
+        EF(c, F_VY, i) = 0;
+    } else {
+        EF(c, F_VY, i) = vel;
+        EF(c, F_VX, i) = 0;
+    }
+    EI(c, F_SPAWN_TIME, i) = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), 50) + 25;
+}
+
+DEV void db_fire_ball(Ctx &c, uint32_t *rg, int i, float vx, float vy) { // :371-376
+    const float ex = EF(c, F_X, i), ey = EF(c, F_Y, i);
+    wave_sync();
+    const int b = append_entity(c, ex, ey, vx * c.s.db_ball_vscale, vy * c.s.db_ball_vscale, c.s.db_ball_r, c.s.db_ball_r,
+                                DB_ENEMY_BALL);
+    const int ft = c.s.cur_time + rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), 4);
+    EI(c, F_FIRE_TIME, i) = ft;
+    if (b >= 0) {
+        EF(c, F_VROT, b) = PI_F * 0.23f; // BALL_V_ROT
+        EI(c, F_EXPIRE_TIME, b) = 50;
+    }
+    wave_sync();
+}
+
+DEV void dodgeball_step_tail(Ctx &c, uint32_t *rg) { // :378-444
+    const float vx = (float)(c.s.last_move_action / 3 - 1);
+    const float vy = (float)(c.s.last_move_action % 3 - 1);
+    const bool gh = c.s.agent_erased;
+    if (!gh) EF(c, F_ROTATION, 0) = face_rotation(vx, vy, EF(c, F_ROTATION, 0));
+    if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 7) {
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        wave_sync();
+        const int b = append_entity(c, ax, ay, vx * c.s.db_ball_vscale, vy * c.s.db_ball_vscale, c.s.db_ball_r,
+                                    c.s.db_ball_r, DB_PLAYER_BALL);
+        if (b >= 0) {
+            EI(c, F_FLAGS, b) = EF_AUTO_ERASE | EF_COLLIDES;
+            EI(c, F_EXPIRE_TIME, b) = 50;
+            EF(c, F_VROT, b) = PI_F * 0.23f;
+        }
+        c.s.last_fire_time = c.s.cur_time;
+    }
+    wave_sync();
+    const int n0 = c.s.num_ents;
+    // balls: each flags only itself (lane-parallel)
+    for (int base = 0; base < n0; base += 64) {
+        const int i = base + LANE;
+        if (i < n0) {
+            const int t = EI(c, F_TYPE, i);
+            if (t == DB_PLAYER_BALL || t == DB_ENEMY_BALL) {
+                const float x = EF(c, F_X, i), y = EF(c, F_Y, i), rx = EF(c, F_RX, i), ry = EF(c, F_RY, i);
+                if (x < rx || x > (c.s.main_width - rx) || y < ry || y > (c.s.main_height - ry))
+                    EI(c, F_FLAGS, i) = EI(c, F_FLAGS, i) | EF_WILL_ERASE;
+            }
+        }
+    }
+    wave_sync();
+    // enemies in the reference's descending order (random draws in order)
+    int num_enemies = 0;
+    int upper = n0;
+    while (upper > 0) {
+        int m = -1;
+        for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+            const int i = base + LANE;
+            const unsigned long long b = ballot(i < upper && EI(c, F_TYPE, i) == DB_ENEMY);
+            if (b) {
+                m = base + top_bit(b);
+                break;
+            }
+        }
+        if (m < 0) break;
+        upper = m;
+        num_enemies++;
+        const int st = EI(c, F_SPAWN_TIME, m);
+        wave_sync();
+        if (st == 0) db_choose_vel(c, rg, m);
+        else EI(c, F_SPAWN_TIME, m) = st - 1;
+        wave_sync();
+        if ((c.s.cur_time - EI(c, F_FIRE_TIME, m)) >= c.s.enemy_fire_delay) {
+            const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+            const float ex = EF(c, F_X, m), ey = EF(c, F_Y, m);
+            const float dx = ex - ax, dy = ey - ay;
+            const float bvelx = (float)(ex < ax ? 1 : -1);
+            const float bvely = (float)(ey < ay ? 1 : -1);
+            if (fabsf(dx) < 1) {
+                db_fire_ball(c, rg, m, 0, bvely);
+                EF(c, F_VX, m) = 0;
+                EF(c, F_VY, m) = bvely * DB_ENEMY_VEL;
+            } else if (fabsf(dy) < 1) {
+                db_fire_ball(c, rg, m, bvelx, 0);
+                EF(c, F_VX, m) = bvelx * DB_ENEMY_VEL;
+                EF(c, F_VY, m) = 0;
+            }
+        }
+        wave_sync();
+        EF(c, F_ROTATION, m) = face_rotation(EF(c, F_VX, m), EF(c, F_VY, m), EF(c, F_ROTATION, m));
+        wave_sync();
+    }
+    c.s.num_enemies = num_enemies;
+    erase_if_needed(c);
+}
+
 DEV void fruitbot_step_tail(Ctx &c) { // fruitbot.cpp:247-258
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= FB_KEY_DURATION) {
         const bool gh = c.s.agent_erased;
@@ -1658,6 +1806,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_LEAPER) leaper_step_tail(c, rg);
     if constexpr (G == PG_GAME_CHASER) chaser_step_tail(c);
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_step_tail(c);
+    if constexpr (G == PG_GAME_DODGEBALL) dodgeball_step_tail(c, rg);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1758,6 +1907,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_CLIMBER) { PG_W(has_support) PG_W(facing_right) PG_W(coins_collected) }
         if constexpr (G == PG_GAME_CHASER) { PG_W(eat_time) PG_W(orbs_collected) }
         if constexpr (G == PG_GAME_FRUITBOT) { PG_W(last_fire_time) }
+        if constexpr (G == PG_GAME_DODGEBALL) { PG_W(last_fire_time) PG_W(num_enemies) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1783,21 +1933,40 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_LEAPER)
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
+        PG_CASE(PG_GAME_DODGEBALL)
     default: break;
     }
 #undef PG_CASE
 }
 
 // Self-test of the libm-dependent device arithmetic (tests/test_gpu_libm.py): which = 0 ->
-// bigfish_fish_radius(in[i]).
-__global__ void pg_selftest_kernel(int which, const float *in, float *out, int64_t n) {
+// bigfish_fish_radius(in[i]) (float out); 1 -> qt_rotation_matrix(in[i]) before its fuzzy-null
+// clean-up (4 doubles out); 2 -> face_rotation(in[2i], in[2i+1]) (float out).
+__global__ void pg_selftest_kernel(int which, const float *in, void *out, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (which == 0) out[i] = bigfish_fish_radius(in[i]);
+    if (which == 0) {
+        reinterpret_cast<float *>(out)[i] = bigfish_fish_radius(in[i]);
+    } else if (which == 1) {
+        double m[4];
+        qt_rotation_matrix(in[i], m);
+        const double a = (double)(in[i] * 180 / PI_F);
+        if (a != 0 && a != 90. && a != -270. && a != 270. && a != -90. && a != 180.) { // undo the clean-up
+            const double b = 0.017453292519943295769 * a;
+            double sb, cb;
+            pg_sincos_cr(b, &sb, &cb);
+            m[1] = sb;
+            m[2] = -sb;
+        }
+        double *o = reinterpret_cast<double *>(out) + 4 * i;
+        o[0] = m[0]; o[1] = m[1]; o[2] = m[2]; o[3] = m[3];
+    } else if (which == 2) {
+        reinterpret_cast<float *>(out)[i] = face_rotation(in[2 * i], in[2 * i + 1], 0.0f);
+    }
 }
 
-extern "C" int procgen_selftest_libm(int which, const float *d_in, float *d_out, int64_t n, void *stream) {
-    if (which != 0 || n <= 0) return -1;
+extern "C" int procgen_selftest_libm(int which, const float *d_in, void *d_out, int64_t n, void *stream) {
+    if (which < 0 || which > 2 || n <= 0) return -1;
     int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(pg_selftest_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, which, d_in, d_out, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -67,6 +67,8 @@ class Atlas:
         for t, names in table.items():
             self.num_themes[t] = len(names)
             for theme, n in enumerate(names):
+                if theme >= catalog.MAX_IMAGE_THEMES:
+                    break  # never drawn: draw_image asserts theme < MAX_IMAGE_THEMES (basic-abstract-game.cpp:897)
                 img = sprites[n]
                 slot = t + catalog.MAX_ASSETS * theme
                 self.sprites[slot] = (place(img), img.shape[1], img.shape[0], 0)

@@ -215,6 +215,21 @@ FRUITBOT_SPRITES = {
     12: ["misc_assets/present%d.png" % i for i in range(1, 4)],
 }
 
+# ---------------------------------------------------------------- dodgeball
+# procgen/src/games/dodgeball.cpp:50-88 (LAVA_WALL 1, PLAYER_BALL 3, ENEMY 4, DOOR 5, ENEMY_BALL 6,
+# DOOR_OPEN 7, DUST_CLOUD 8, OOB_WALL 10)
+DODGEBALL_SPRITES = {
+    0: ["misc_assets/character12.png"],
+    3: ["misc_assets/ball_soccer1.png"],
+    4: ["misc_assets/character%d.png" % i for i in range(1, 12)],
+    5: ["misc_assets/blockRed.png"],
+    6: ["misc_assets/ball_soccer2.png"],
+    7: ["misc_assets/blockGreen.png"],
+    1: ["misc_assets/tileStone_slope2.png"],
+    10: ["misc_assets/tileStone_slope2.png"],
+    8: ["misc_assets/spaceEffect%d.png" % i for i in range(1, 10)],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -226,6 +241,7 @@ GAMES = {
     "leaper": (LEAPER_SPRITES, "topdown"),      # leaper.cpp:41-43
     "chaser": (CHASER_SPRITES, "topdown_simple"),  # chaser.cpp:50-52
     "fruitbot": (FRUITBOT_SPRITES, "topdown"),  # fruitbot.cpp:42-44
+    "dodgeball": (DODGEBALL_SPRITES, "topdown"),  # dodgeball.cpp:46-48
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -57,6 +57,8 @@ def load():
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_latent.argtypes = [ctypes.c_void_p] * 5
         lib.oracle_bigfish_radius.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        lib.oracle_qt_rotation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        lib.oracle_face_rotation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         _LIB = lib
     return _LIB
 

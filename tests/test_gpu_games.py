@@ -64,14 +64,16 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 
 
 LATENT = ("maze", "miner")
+# every game of this build except coinrun (tests/test_gpu_coinrun.py)
+GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball"]
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
+@pytest.mark.parametrize("game", GAMES)
 def test_parity_hard_unbounded(game):
     run_pair(game, 16, 300, seed=1, num_levels=0, rand_seed=0, latent=game in LATENT)
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
+@pytest.mark.parametrize("game", GAMES)
 def test_parity_200_levels_easy(game):
     run_pair(game, 8, 200, seed=2, num_levels=200, start_level=0, rand_seed=5, distribution_mode="easy",
              latent=game in LATENT)
@@ -90,7 +92,7 @@ def test_miner_long_run_deaths():
     assert episodes > 0
 
 
-@pytest.mark.parametrize("game", ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot"])
+@pytest.mark.parametrize("game", GAMES)
 def test_parity_options(game):
     run_pair(game, 8, 150, seed=4, num_levels=20, rand_seed=3, use_backgrounds=False, restrict_themes=True,
              use_sequential_levels=True)
@@ -122,6 +124,15 @@ def test_fruitbot_long_and_uncentered():
     run_pair("fruitbot", 8, 200, seed=17, num_levels=0, rand_seed=6, center_agent=False)
 
 
+def test_dodgeball_modes():
+    """dodgeball: recursive room split, enemies that reflect off lava walls and fire, player balls
+    (collides_with_entities) that kill enemies and leave rotating dust clouds, rotating balls drawn
+    through the device QTransform::rotate; extreme (8 splits) and memory (40x40, centred) modes."""
+    run_pair("dodgeball", 32, 500, seed=18, num_levels=0, rand_seed=7)
+    run_pair("dodgeball", 8, 200, seed=19, num_levels=0, rand_seed=8, distribution_mode="extreme")
+    run_pair("dodgeball", 8, 200, seed=20, num_levels=0, rand_seed=9, distribution_mode="memory")
+
+
 def test_bigfish_long_episodes():
     """bigfish episodes run up to 6,000 steps (bigfish.cpp:25): many fish spawn, grow, leave."""
     run_pair("bigfish", 8, 1200, seed=6, num_levels=0, rand_seed=12)
@@ -129,8 +140,8 @@ def test_bigfish_long_episodes():
 
 def test_mixed_batch_parity():
     """env n plays names[n % 4] (vecgame.cpp:357-358), level seeds from the global index."""
-    names = ["bigfish", "chaser", "climber", "coinrun", "fruitbot", "heist", "leaper", "maze", "miner"]
-    num = 36
+    names = sorted(GAMES + ["coinrun"])
+    num = 4 * len(names)
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=21)
     orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=21) for n in range(num)]
     g = gpu_obs(env)
@@ -167,7 +178,7 @@ def test_full_size_sampled_parity(game):
     env.close()
 
 
-@pytest.mark.parametrize("game", ["maze", "heist", "bigfish", "miner", "climber", "leaper", "chaser", "fruitbot"])
+@pytest.mark.parametrize("game", GAMES)
 def test_state_roundtrip(game):
     env = make_gpu(4, game, num_levels=20, rand_seed=11)
     rng = np.random.RandomState(1)
