@@ -57,7 +57,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
 enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
-       GAME_MINER = 12 };
+       GAME_MINER = 12, GAME_PLUNDER = 14 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -242,6 +242,12 @@ typedef struct {
     /* dodgeball (dodgeball.cpp:28-35) */
     float db_min_dim, db_hard_min_dim, db_ball_vscale, db_ball_r;
     int db_num_enemies, db_enemy_fire_delay;
+    /* plunder (plunder.cpp:19-31); lane_directions / target_bools / image_permutation / lane_vels */
+    bool pl_lane_dirs[5], pl_target_bools[6];
+    int pl_perm[6];
+    float pl_lane_vels[5];
+    int pl_num_lanes, pl_num_current_ship_types, pl_targets_hit, pl_target_quota;
+    float pl_juice_left, pl_r_scale, pl_spawn_prob, pl_legend_r, pl_min_agent_x;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -429,6 +435,29 @@ static int spawn_child(Game *g, int src_i, int type, float obj_r) { /* basic-abs
 }
 static void hook_handle_collision(Game *g, int si, int ti) {
     Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:87-108 */
+        if (src->type == 1) { /* PLAYER_BULLET */
+            if (target->type == 7) { /* SHIP */
+                target->will_erase = true;
+                src->will_erase = true;
+                if (g->pl_target_bools[target->image_theme]) {
+                    g->pl_targets_hit += 1;
+                    g->sd_reward += 1.0f; /* POSITIVE_REWARD */
+                    g->pl_juice_left += 0.1f;
+                } else {
+                    g->pl_juice_left -= 0.1f;
+                }
+            } else if (target->type == 6) { /* PANEL */
+                src->will_erase = true;
+            }
+            if (target->will_erase) {
+                float tx = target->x, ty = target->y, tvx = target->vx / 2, tvy = target->vy / 2;
+                float tr = (float)(.5 * target->rx);
+                add_entity(g, tx, ty, tvx, tvy, tr, EXPLOSION);
+            }
+        }
+        return;
+    }
     if (g->game_id == GAME_DODGEBALL) { /* dodgeball.cpp:120-151 */
         if (target->type == 3) { /* PLAYER_BALL */
             if (src->type == 1) { /* LAVA_WALL */
@@ -569,6 +598,7 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
 /* should_preserve_type_themes + mask_theme_if_necessary (basic-abstract-game.cpp:454-462, heist.cpp:42-44) */
 static int mask_theme(Game *g, int theme, int type) {
     bool preserve = (g->game_id == GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR)) ||
+                    (g->game_id == GAME_PLUNDER && type == 7) || /* plunder.cpp:83-85: SHIP */
                     (g->game_id == GAME_LEAPER && type == PLAYER); /* leaper.cpp:87-89 */
     if (g->options.restrict_themes && !preserve) return 0;
     return theme;
@@ -840,6 +870,12 @@ static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299
 }
 
 static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:110-114 */
+        g->action_vx = (float)(move_action / 3 - 1);
+        g->action_vy = 0;
+        g->action_vrot = 0;
+        return;
+    }
     if (g->game_id == GAME_FRUITBOT) { /* fruitbot.cpp:154-158 */
         g->action_vx = (float)(move_action / 3 - 1);
         g->action_vy = 0.2f;
@@ -2520,6 +2556,119 @@ static void dodgeball_game_step(Game *g) { /* :378-444 */
     erase_if_needed(g);
 }
 
+/* ================================================================== plunder (games/plunder.cpp) */
+#define PL_PLAYER_BULLET 1
+#define PL_TARGET_LEGEND 2
+#define PL_TARGET_BACKGROUND 3
+#define PL_PANEL 6
+#define PL_SHIP 7
+
+static void rg_choose_n(MT *r, const int *elems, int count, int n, int *out) { /* randgen.cpp:49-68 */
+    int rem[64];
+    fassert(count <= 64);
+    memcpy(rem, elems, sizeof(int) * (size_t)count);
+    int nrem = count;
+    if (n > count) {
+        memcpy(out, rem, sizeof(int) * (size_t)count);
+        return;
+    }
+    for (int k = 0; k < n; k++) {
+        int idx = rg_randn(r, nrem);
+        out[k] = rem[idx];
+        memmove(&rem[idx], &rem[idx + 1], sizeof(int) * (size_t)(nrem - idx - 1));
+        nrem--;
+    }
+}
+
+static void plunder_game_reset(Game *g, const or_atlas *at) { /* :116-192 */
+    MT *r = &g->rand_gen;
+    basic_game_reset(g, at);
+    Entity *agent = AG(g);
+    agent->image_type = PL_SHIP;
+    g->pl_juice_left = 1;
+    g->pl_targets_hit = 0;
+    g->pl_target_quota = 20;
+    g->pl_spawn_prob = 0.06f;
+    g->pl_r_scale = g->options.distribution_mode == EasyMode ? 1.5f : 1.0f;
+    int num_total_ship_types = 6;
+    g->pl_num_lanes = 5;
+    int image_idxs[6];
+    for (int i = 0; i < num_total_ship_types; i++) image_idxs[i] = i;
+    rg_choose_n(r, image_idxs, num_total_ship_types, num_total_ship_types, g->pl_perm);
+    g->pl_num_current_ship_types = 2;
+    for (int i = 0; i < num_total_ship_types; i++) g->pl_target_bools[i] = false;
+    for (int i = 0; i < g->pl_num_current_ship_types / 2; i++) g->pl_target_bools[g->pl_perm[i]] = true;
+    for (int i = 0; i < g->pl_num_lanes; i++) {
+        g->pl_lane_dirs[i] = rg_rand01(r) < .5;
+        g->pl_lane_vels[i] = (float)(.15 + .1 * rg_rand01(r));
+    }
+    int num_panels = g->options.distribution_mode == EasyMode ? 0 : rg_randn(r, 4);
+    float panel_width = 1.2f;
+    for (int i = 0; i < num_panels; i++)
+        spawn_entity_rxy(g, panel_width, .5, PL_PANEL, 0, (float)(.25 * g->main_height), (float)g->main_width,
+                         (float)(.25 * g->main_height));
+    float key_scale = 1.5;
+    g->pl_legend_r = 2;
+    add_entity(g, g->pl_legend_r, g->pl_legend_r, 0, 0, g->pl_legend_r, PL_TARGET_BACKGROUND);
+    int e = add_entity(g, g->pl_legend_r, g->pl_legend_r, 0, 0, g->pl_r_scale * key_scale, PL_TARGET_LEGEND);
+    g->ents[e].image_theme = g->pl_perm[0];
+    g->ents[e].image_type = PL_SHIP;
+    match_aspect_ratio(g, at, &g->ents[e]);
+    g->ents[e].rotation = PI_F / 2;
+    g->last_fire_time = 0;
+    g->options.center_agent = false;
+    agent = AG(g);
+    agent->rx = g->pl_r_scale;
+    agent->rotation = -1 * PI_F / 2;
+    agent->image_theme = g->pl_perm[rg_randn(r, g->pl_num_current_ship_types / 2) + g->pl_num_current_ship_types / 2];
+    match_aspect_ratio(g, at, agent);
+    reposition_agent(g);
+    agent->y = 1 + agent->ry;
+    g->pl_min_agent_x = 2 * g->pl_legend_r + agent->rx;
+    if (agent->x < g->pl_min_agent_x) agent->x = g->pl_min_agent_x;
+}
+
+static void plunder_game_step(Game *g, const or_atlas *at) { /* :194-241 */
+    MT *r = &g->rand_gen;
+    basic_game_step(g);
+    g->pl_juice_left -= 0.0015f;
+    if (rg_rand01(r) < g->pl_spawn_prob) {
+        float ent_r = g->pl_r_scale;
+        int lane = rg_randn(r, g->pl_num_lanes);
+        float ent_y = (float)((lane * .11 + .4) * (g->main_height / 2 - ent_r) + g->main_height / 2);
+        float moves_right = g->pl_lane_dirs[lane];
+        float ent_vx = g->pl_lane_vels[lane] * (moves_right != 0 ? 1 : -1);
+        Entity ent;
+        entity_init(&ent, 0, ent_y, ent_vx, 0, ent_r, ent_r, PL_SHIP);
+        ent.image_type = PL_SHIP;
+        ent.image_theme = g->pl_perm[rg_randn(r, g->pl_num_current_ship_types)];
+        match_aspect_ratio(g, at, &ent);
+        ent.x = moves_right != 0 ? -1 * ent_r : (g->main_width + ent_r);
+        ent.is_reflected = !(moves_right != 0);
+        if (!has_any_collision(g, &ent, 0)) {
+            fassert(g->num_ents < MAX_ENTS);
+            g->ents[g->num_ents++] = ent;
+        }
+    }
+    if (g->special_action == 1 && (g->cur_time - g->last_fire_time) >= 3) {
+        Entity *agent = AG(g);
+        int b = add_entity(g, agent->x, agent->y, 0, 1, .25, PL_PLAYER_BULLET);
+        g->ents[b].collides_with_entities = true;
+        g->ents[b].expire_time = 50;
+        g->last_fire_time = g->cur_time;
+        g->pl_juice_left -= 0.02f;
+    }
+    if (g->pl_juice_left <= 0) g->sd_done = true;
+    else if (g->pl_juice_left >= 1) g->pl_juice_left = 1;
+    if (g->pl_targets_hit >= g->pl_target_quota) {
+        g->sd_done = true;
+        g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+        g->sd_level_complete = true;
+    }
+    Entity *agent = AG(g);
+    if (agent->x < g->pl_min_agent_x) agent->x = g->pl_min_agent_x;
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -2669,6 +2818,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_CHASER) chaser_game_reset(g, at);
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_reset(g, at);
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_reset(g, at);
+    else if (g->game_id == GAME_PLUNDER) plunder_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -2682,6 +2832,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_CHASER) chaser_game_step(g);
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_step(g);
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_step(g);
+    else if (g->game_id == GAME_PLUNDER) plunder_game_step(g, at);
     else fatal_msg("game not restated");
 }
 
@@ -3279,6 +3430,14 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
 static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
     draw_background(g, at);
     draw_foreground(g, at);
+    if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:66-77: juice and progress bars, get_abs_rect (:812-814) */
+        float u = g->unit;
+        qt_fill_rectf(g->canvas, (double)(.25f * u), (double)(.25f * u), (double)(g->main_width * g->pl_juice_left * u),
+                      (double)(.5f * u), 0xff42f587u);
+        float prog = (float)(g->main_width * (g->pl_targets_hit * 1.0 / g->pl_target_quota));
+        qt_fill_rectf(g->canvas, (double)(.25f * u), (double)(.75f * u), (double)(prog * u), (double)(.5f * u),
+                      0xfff54290u);
+    }
 }
 
 /* ================================================================== construction (vecgame.cpp) */
@@ -3293,6 +3452,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "chaser") == 0) return GAME_CHASER;
     if (strcmp(name, "fruitbot") == 0) return GAME_FRUITBOT;
     if (strcmp(name, "dodgeball") == 0) return GAME_DODGEBALL;
+    if (strcmp(name, "plunder") == 0) return GAME_PLUNDER;
     return -1;
 }
 
@@ -3346,6 +3506,14 @@ static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
     g->maxspeed = 0.85f;
     g->bg_tile_ratio = -1;
     g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
+}
+static void plunder_ctor(Game *g) { /* plunder.cpp:33-43 */
+    g->timeout = 4000;
+    g->main_width = 20;
+    g->main_height = 20;
+    g->mixrate = .5;
+    g->maxspeed = 0.85f;
+    g->has_useful_vel_info = false;
 }
 static void dodgeball_ctor(Game *g) { /* dodgeball.cpp:37-44 */
     g->mixrate = .5;
@@ -3427,6 +3595,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_CHASER) chaser_ctor(g);
         else if (gid == GAME_FRUITBOT) fruitbot_ctor(g);
         else if (gid == GAME_DODGEBALL) dodgeball_ctor(g);
+        else if (gid == GAME_PLUNDER) plunder_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

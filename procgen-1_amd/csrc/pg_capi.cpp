@@ -117,9 +117,10 @@ int game_id(const std::string &name) {
     if (name == "chaser") return PG_GAME_CHASER;
     if (name == "fruitbot") return PG_GAME_FRUITBOT;
     if (name == "dodgeball") return PG_GAME_DODGEBALL;
+    if (name == "plunder") return PG_GAME_PLUNDER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner";
+const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -179,6 +180,13 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_PLUNDER) { // plunder.cpp:33-43
+        s.timeout = 4000;
+        s.main_width = 20;
+        s.main_height = 20;
+        s.mixrate = .5;
+        s.maxspeed = 0.85f;
+        s.has_useful_vel_info = 0;
     } else if (gid == PG_GAME_DODGEBALL) { // dodgeball.cpp:37-44
         s.mixrate = .5;
         s.enemy_fire_delay = 50;

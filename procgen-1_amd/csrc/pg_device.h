@@ -107,6 +107,12 @@ DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 #define DB_DUST_CLOUD 8
 #define DB_OOB_WALL 10
 #define DB_ENEMY_VEL 0.05f
+// plunder.cpp:11-15
+#define PL_PLAYER_BULLET 1
+#define PL_TARGET_LEGEND 2
+#define PL_TARGET_BACKGROUND 3
+#define PL_PANEL 6
+#define PL_SHIP 7
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3

@@ -23,7 +23,7 @@
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
     PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
-    PG_GAME_MINER = 12
+    PG_GAME_MINER = 12, PG_GAME_PLUNDER = 14
 };
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
@@ -175,7 +175,18 @@ struct PGEnv {
     float db_ball_r;
     int32_t num_enemies;
     int32_t enemy_fire_delay;
-    int32_t pad[128 - 107];
+    // ---- members of the games added later share one block (an env plays one game)
+    union {
+        struct { // plunder (plunder.cpp:19-31)
+            uint32_t lane_dirs;     // bit i = lane_directions[i]
+            uint32_t target_bools;  // bit i = target_bools[i]
+            uint32_t perm;          // image_permutation[i] in bits 4i..4i+3
+            float lane_vels[5];
+            int32_t num_lanes, num_current_ship_types, targets_hit, target_quota;
+            float juice_left, r_scale, spawn_prob, legend_r, min_agent_x;
+        } pl;
+        int32_t words[21];
+    } gs;
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

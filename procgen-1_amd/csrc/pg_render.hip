@@ -136,6 +136,7 @@ DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cp
 template <int G>
 DEV int mask_theme(const PGEnv &s, int theme, int img_type) { // mask_theme_if_necessary (:454-462, heist.cpp:42-44)
     bool preserve = (G == PG_GAME_HEIST && (img_type == HS_KEY || img_type == HS_LOCKED_DOOR)) ||
+                    (G == PG_GAME_PLUNDER && img_type == PL_SHIP) || // plunder.cpp:83-85
                     (G == PG_GAME_LEAPER && img_type == PLAYER); // leaper.cpp:91-93
     return (s.opt_restrict_themes && !preserve) ? 0 : theme;
 }
@@ -378,6 +379,28 @@ DEV bool grid_obj_fill(int img, double rx, double ry, double rw, double rh, Img 
         }
     }
     return false;
+}
+
+// fillRect(QRectF, opaque colour) straight into the frame, lane-parallel (same edges as fill_setup)
+DEV void fb_fill_rectf(uint32_t *fb, double x, double y, double w, double h, uint32_t argb) {
+    Img im;
+    im.draw = false;
+    if (!fill_setup(x, y, w, h, argb, im)) return;
+    const int nx = im.ex.n, ny = im.ey.n;
+    for (int p = LANE; p < nx * ny; p += 64) fb[(im.ey.t1 + p / nx) * PG_RES + im.ex.t1 + p % nx] = im.fill;
+}
+
+// game_draw additions drawn over the foreground (plunder.cpp:66-77)
+template <int G>
+DEV void game_overlay(uint32_t *fb, const PGEnv &s, const View &v) {
+    if constexpr (G == PG_GAME_PLUNDER) { // juice and progress bars, get_abs_rect (:812-814)
+        const float u = v.unit;
+        fb_fill_rectf(fb, (double)(.25f * u), (double)(.25f * u), (double)(s.main_width * s.gs.pl.juice_left * u),
+                      (double)(.5f * u), 0xff42f587u); // QColor(66, 245, 135)
+        const float prog = (float)(s.main_width * (s.gs.pl.targets_hit * 1.0 / s.gs.pl.target_quota));
+        fb_fill_rectf(fb, (double)(.25f * u), (double)(.75f * u), (double)(prog * u), (double)(.5f * u),
+                      0xfff54290u); // QColor(245, 66, 144)
+    }
 }
 
 DEV double readlane_d(double x, int j) {
@@ -1020,6 +1043,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     PG_DRAW_ENTITIES(1)
 #undef PG_DRAW_ENTITIES
     wave_sync();
+    game_overlay<G>(fb, s, v);
+    wave_sync();
 
 
     pt.mark(2);
@@ -1058,6 +1083,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
+        PG_CASE(PG_GAME_PLUNDER)
     default: break;
     }
 #undef PG_CASE

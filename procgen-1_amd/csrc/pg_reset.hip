@@ -114,7 +114,8 @@ DEV void choose_random_theme(RCtx &c, int i) {
 template <int G>
 DEV void match_aspect_ratio(RCtx &c, int i) {
     int type = EI(c, F_IMAGE_TYPE, i), theme = EI(c, F_IMAGE_THEME, i);
-    bool preserve = G == PG_GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR);
+    bool preserve = (G == PG_GAME_HEIST && (type == HS_KEY || type == HS_LOCKED_DOOR)) ||
+                    (G == PG_GAME_PLUNDER && type == PL_SHIP); // plunder.cpp:83-85
     if (c.s.opt_restrict_themes && !preserve) theme = 0;
     int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + theme * MAX_ASSETS];
     if (sp.y <= 0 || sp.z <= 0) {
@@ -1256,6 +1257,72 @@ DEV void dodgeball_game_reset(RCtx &c, float4 *rooms) { // :259-369
     wave_sync();
 }
 
+// ------------------------------------------------------------------ plunder (plunder.cpp:116-192)
+DEV int pl_perm_at(const PGEnv &s, int i) { return (int)((s.gs.pl.perm >> (4 * i)) & 15u); }
+
+DEV void plunder_game_reset(RCtx &c) {
+    base_game_reset<PG_GAME_PLUNDER>(c);
+    auto &P = c.s.gs.pl;
+    EI(c, F_IMAGE_TYPE, 0) = PL_SHIP;
+    P.juice_left = 1;
+    P.targets_hit = 0;
+    P.target_quota = 20;
+    P.spawn_prob = 0.06f;
+    P.r_scale = c.s.opt_distribution_mode == PG_EASY ? 1.5f : 1.0f;
+    const int num_total_ship_types = 6;
+    P.num_lanes = 5;
+    // RandGen::choose_n(0..5, 6) (randgen.cpp:49-68): draw from the remaining list, erase
+    uint32_t rem = 0x543210u, perm = 0;
+    for (int k = 0; k < num_total_ship_types; k++) {
+        const int idx = randn(c, num_total_ship_types - k);
+        const uint32_t v = (rem >> (4 * idx)) & 15u;
+        perm |= v << (4 * k);
+        const uint32_t low = rem & ((1u << (4 * idx)) - 1u);
+        rem = low | ((rem >> (4 * (idx + 1))) << (4 * idx));
+    }
+    P.perm = perm;
+    P.num_current_ship_types = 2;
+    P.target_bools = 0;
+    for (int i = 0; i < P.num_current_ship_types / 2; i++) P.target_bools |= 1u << pl_perm_at(c.s, i);
+    P.lane_dirs = 0;
+    for (int i = 0; i < P.num_lanes; i++) {
+        if (rand01(c) < .5) P.lane_dirs |= 1u << i;
+        const float v = (float)(.15 + .1 * rand01(c));
+        if (i == 0) P.lane_vels[0] = v;
+        else if (i == 1) P.lane_vels[1] = v;
+        else if (i == 2) P.lane_vels[2] = v;
+        else if (i == 3) P.lane_vels[3] = v;
+        else P.lane_vels[4] = v;
+    }
+    const int num_panels = c.s.opt_distribution_mode == PG_EASY ? 0 : randn(c, 4);
+    const float panel_width = 1.2f;
+    for (int i = 0; i < num_panels; i++) {
+        spawn_entity_rxy(c, panel_width, .5, PL_PANEL, 0, (float)(.25 * c.s.main_height), (float)c.s.main_width,
+                         (float)(.25 * c.s.main_height));
+        wave_sync();
+    }
+    const float key_scale = 1.5;
+    P.legend_r = 2;
+    add_entity(c, P.legend_r, P.legend_r, 0, 0, P.legend_r, PL_TARGET_BACKGROUND);
+    const int e = add_entity(c, P.legend_r, P.legend_r, 0, 0, P.r_scale * key_scale, PL_TARGET_LEGEND);
+    EI(c, F_IMAGE_THEME, e) = pl_perm_at(c.s, 0);
+    EI(c, F_IMAGE_TYPE, e) = PL_SHIP;
+    match_aspect_ratio<PG_GAME_PLUNDER>(c, e);
+    EF(c, F_ROTATION, e) = PI_F / 2;
+    c.s.last_fire_time = 0;
+    c.s.opt_center_agent = 0;
+    EF(c, F_RX, 0) = P.r_scale;
+    EF(c, F_ROTATION, 0) = -1 * PI_F / 2;
+    EI(c, F_IMAGE_THEME, 0) = pl_perm_at(c.s, randn(c, P.num_current_ship_types / 2) + P.num_current_ship_types / 2);
+    match_aspect_ratio<PG_GAME_PLUNDER>(c, 0);
+    wave_sync();
+    reposition_agent(c);
+    EF(c, F_Y, 0) = 1 + EF(c, F_RY, 0);
+    P.min_agent_x = 2 * P.legend_r + EF(c, F_RX, 0);
+    if (EF(c, F_X, 0) < P.min_agent_x) EF(c, F_X, 0) = P.min_agent_x;
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1582,6 +1649,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_CHASER) chaser_game_reset(c, &scratch->ch);
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_game_reset(c, scratch->part);
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_game_reset(c, scratch->rooms);
+    if constexpr (G == PG_GAME_PLUNDER) plunder_game_reset(c);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1686,6 +1754,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
+        PG_CASE(PG_GAME_PLUNDER)
     default: break;
     }
 #undef PG_CASE

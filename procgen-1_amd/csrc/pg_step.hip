@@ -619,6 +619,9 @@ DEV void set_action_xy(Ctx &c, int move_action) {
     } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:154-158
         c.s.action_vy = 0.2f;
         c.s.action_vrot = 0;
+    } else if constexpr (G == PG_GAME_PLUNDER) { // plunder.cpp:110-114
+        c.s.action_vy = 0;
+        c.s.action_vrot = 0;
     } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:299-318
         if (c.s.action_vy < 0) c.s.action_vy = 0;
         if (c.s.action_vx > 0) c.s.facing_right = 1;
@@ -713,6 +716,7 @@ DEV void update_agent_velocity(Ctx &c) {
 template <int G>
 DEV bool preserve_theme(int type) { // should_preserve_type_themes (heist.cpp:42-44)
     if constexpr (G == PG_GAME_HEIST) return type == HS_KEY || type == HS_LOCKED_DOOR;
+    if constexpr (G == PG_GAME_PLUNDER) return type == PL_SHIP; // plunder.cpp:83-85
     return false;
 }
 template <int G>
@@ -829,6 +833,33 @@ DEV void handle_agent_collision(Ctx &c, int m) {
 DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type);
 template <int G>
 DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_PLUNDER) { // plunder.cpp:87-108
+        if (EI(c, F_TYPE, si) == PL_PLAYER_BULLET) {
+            const int tt = EI(c, F_TYPE, ti);
+            bool target_erased = false;
+            if (tt == PL_SHIP) {
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+                EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+                target_erased = true;
+                if ((c.s.gs.pl.target_bools >> EI(c, F_IMAGE_THEME, ti)) & 1u) {
+                    c.s.gs.pl.targets_hit += 1;
+                    c.s.sd_reward += 1.0f; // POSITIVE_REWARD
+                    c.s.gs.pl.juice_left += 0.1f;
+                } else {
+                    c.s.gs.pl.juice_left -= 0.1f;
+                }
+            } else if (tt == PL_PANEL) {
+                EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+            }
+            if (target_erased) { // add_entity(x, y, vx / 2, vy / 2, .5 * rx, EXPLOSION)
+                const float tx = EF(c, F_X, ti), ty = EF(c, F_Y, ti);
+                const float tvx = EF(c, F_VX, ti) / 2, tvy = EF(c, F_VY, ti) / 2;
+                const float tr = (float)(.5 * EF(c, F_RX, ti));
+                wave_sync();
+                append_entity(c, tx, ty, tvx, tvy, tr, tr, EXPLOSION);
+            }
+        }
+    }
     if constexpr (G == PG_GAME_DODGEBALL) { // dodgeball.cpp:120-151
         const int tt = EI(c, F_TYPE, ti), st = EI(c, F_TYPE, si);
         if (tt == DB_PLAYER_BALL) {
@@ -1020,6 +1051,13 @@ DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, fl
     EI(c, F_TYPE, i) = type; EI(c, F_IMAGE_TYPE, i) = type; EI(c, F_IMAGE_THEME, i) = 0;
     EI(c, F_RENDER_Z, i) = 0; EI(c, F_LIFE_TIME, i) = 0; EI(c, F_EXPIRE_TIME, i) = -1;
     EI(c, F_FIRE_TIME, i) = -1; EI(c, F_SPAWN_TIME, i) = -1; EI(c, F_FLAGS, i) = EF_AUTO_ERASE;
+    if (type == EXPLOSION) { // entity.cpp:40-43
+        EF(c, F_GROW_RATE, i) = 1.4f;
+        EI(c, F_EXPIRE_TIME, i) = 4;
+    } else if (type == TRAIL) { // entity.cpp:44-46
+        EF(c, F_GROW_RATE, i) = 1.05f;
+        EF(c, F_ALPHA_DECAY, i) = 0.8f;
+    }
     return i;
 }
 
@@ -1728,6 +1766,72 @@ DEV void dodgeball_step_tail(Ctx &c, uint32_t *rg) { // :378-444
     erase_if_needed(c);
 }
 
+// ------------------------------------------------------------------ plunder (plunder.cpp:194-241)
+template <int G>
+DEV float aspect_ratio(Ctx &c, int type, int theme);
+
+DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
+    auto &P = c.s.gs.pl;
+    P.juice_left -= 0.0015f;
+    if (rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) < P.spawn_prob) {
+        const float ent_r = P.r_scale;
+        const int lane = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), P.num_lanes);
+        const float ent_y = (float)((lane * .11 + .4) * (c.s.main_height / 2 - ent_r) + c.s.main_height / 2);
+        const bool moves_right = (P.lane_dirs >> lane) & 1u;
+        const float lv = lane == 0 ? P.lane_vels[0] : lane == 1 ? P.lane_vels[1] : lane == 2 ? P.lane_vels[2]
+                       : lane == 3 ? P.lane_vels[3] : P.lane_vels[4];
+        const float ent_vx = lv * (moves_right ? 1 : -1);
+        const int k = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), P.num_current_ship_types);
+        const int theme = (int)((P.perm >> (4 * k)) & 15u);
+        const float ent_ry = ent_r / aspect_ratio<PG_GAME_PLUNDER>(c, PL_SHIP, theme); // match_aspect_ratio
+        const float ent_x = moves_right ? -1 * ent_r : (c.s.main_width + ent_r);
+        // has_any_collision(ent) (:1123-1133), margin 0
+        bool hit = false;
+        for (int base = 0; base < c.s.num_ents; base += 64) {
+            const int i = base + LANE;
+            if (i < c.s.num_ents && !(EI(c, F_FLAGS, i) & EF_AVOIDS)) {
+                const float tx = (ent_r + EF(c, F_RX, i)) + 0.0f, ty = (ent_ry + EF(c, F_RY, i)) + 0.0f;
+                if ((fabsf(ent_x - EF(c, F_X, i)) < tx) && (fabsf(ent_y - EF(c, F_Y, i)) < ty)) hit = true;
+            }
+        }
+        if (ballot(hit) == 0) {
+            wave_sync();
+            const int i = append_entity(c, ent_x, ent_y, ent_vx, 0, ent_r, ent_ry, PL_SHIP);
+            if (i >= 0) {
+                EI(c, F_IMAGE_THEME, i) = theme;
+                if (!moves_right) EI(c, F_FLAGS, i) = EF_AUTO_ERASE | EF_REFLECTED;
+            }
+        }
+        wave_sync();
+    }
+    const bool gh = c.s.agent_erased;
+    if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 3) {
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        wave_sync();
+        const int b = append_entity(c, ax, ay, 0, 1, .25f, .25f, PL_PLAYER_BULLET);
+        if (b >= 0) {
+            EI(c, F_FLAGS, b) = EF_AUTO_ERASE | EF_COLLIDES;
+            EI(c, F_EXPIRE_TIME, b) = 50;
+        }
+        c.s.last_fire_time = c.s.cur_time;
+        P.juice_left -= 0.02f;
+    }
+    if (P.juice_left <= 0) c.s.sd_done = 1;
+    else if (P.juice_left >= 1) P.juice_left = 1;
+    if (P.targets_hit >= P.target_quota) {
+        c.s.sd_done = 1;
+        c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+        c.s.sd_level_complete = 1;
+    }
+    wave_sync();
+    if (gh) {
+        if (c.s.ghost_x < P.min_agent_x) c.s.ghost_x = P.min_agent_x;
+    } else if (EF(c, F_X, 0) < P.min_agent_x) {
+        EF(c, F_X, 0) = P.min_agent_x;
+    }
+    wave_sync();
+}
+
 DEV void fruitbot_step_tail(Ctx &c) { // fruitbot.cpp:247-258
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= FB_KEY_DURATION) {
         const bool gh = c.s.agent_erased;
@@ -1807,6 +1911,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_CHASER) chaser_step_tail(c);
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_step_tail(c);
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_step_tail(c, rg);
+    if constexpr (G == PG_GAME_PLUNDER) plunder_step_tail(c, rg);
     wave_sync();
     c.pt.mark(5);
 }
@@ -1908,6 +2013,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_CHASER) { PG_W(eat_time) PG_W(orbs_collected) }
         if constexpr (G == PG_GAME_FRUITBOT) { PG_W(last_fire_time) }
         if constexpr (G == PG_GAME_DODGEBALL) { PG_W(last_fire_time) PG_W(num_enemies) }
+        if constexpr (G == PG_GAME_PLUNDER) { PG_W(last_fire_time) PG_W(gs) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -1934,6 +2040,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_CHASER)
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
+        PG_CASE(PG_GAME_PLUNDER)
     default: break;
     }
 #undef PG_CASE

@@ -47,7 +47,7 @@ class Atlas:
         table = catalog.sprite_table(game)
         group = catalog.GAMES[game][1]
         sprites = _load_pack("sprites_%s.npz" % game)
-        bgs = _load_pack("bg_%s.npz" % group)
+        bgs = _load_pack("bg_%s.npz" % catalog.BACKGROUND_PACK.get(group, group))
 
         chunks, offset = [], 0
         seen = {}

@@ -74,6 +74,10 @@ BACKGROUND_GROUPS = {
     "caves": CAVES,
 }
 
+# Groups whose images all live in another group's pack (no duplicate pack committed):
+# water_surface = water[0:4] (resources.cpp:952-961), space = platform[-13:] (:972-975).
+BACKGROUND_PACK = {"water_surface": "water", "space": "platform"}
+
 # ---------------------------------------------------------------- object ids
 # procgen/src/object-ids.h:9-27
 EXPLOSION, EXPLOSION2, EXPLOSION3, EXPLOSION4, EXPLOSION5, TRAIL = 54, 55, 56, 57, 58, 59
@@ -230,6 +234,16 @@ DODGEBALL_SPRITES = {
     8: ["misc_assets/spaceEffect%d.png" % i for i in range(1, 10)],
 }
 
+# ---------------------------------------------------------------- plunder
+# procgen/src/games/plunder.cpp:49-64 (PLAYER_BULLET 1, TARGET_LEGEND 2, TARGET_BACKGROUND 3, PANEL 6,
+# SHIP 7; the agent and the legend draw SHIP images)
+PLUNDER_SPRITES = {
+    7: ["misc_assets/ship_%d.png" % i for i in range(1, 7)],
+    1: ["misc_assets/cannonBall.png"],
+    6: ["misc_assets/panel_wood.png"],
+    3: ["misc_assets/target_red2.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -242,6 +256,7 @@ GAMES = {
     "chaser": (CHASER_SPRITES, "topdown_simple"),  # chaser.cpp:50-52
     "fruitbot": (FRUITBOT_SPRITES, "topdown"),  # fruitbot.cpp:42-44
     "dodgeball": (DODGEBALL_SPRITES, "topdown"),  # dodgeball.cpp:46-48
+    "plunder": (PLUNDER_SPRITES, "water_surface"),  # plunder.cpp:45-47
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -65,7 +65,7 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
-GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball"]
+GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -131,6 +131,13 @@ def test_dodgeball_modes():
     run_pair("dodgeball", 32, 500, seed=18, num_levels=0, rand_seed=7)
     run_pair("dodgeball", 8, 200, seed=19, num_levels=0, rand_seed=8, distribution_mode="extreme")
     run_pair("dodgeball", 8, 200, seed=20, num_levels=0, rand_seed=9, distribution_mode="memory")
+
+
+def test_plunder_long():
+    """plunder: lanes of ships, cannonballs (collides_with_entities) hit targets / non-targets and leave
+    explosions, juice runs out (~670 steps without hits), juice / progress bars (fillRect(QRectF))."""
+    episodes, _ = run_pair("plunder", 16, 900, seed=21, num_levels=0, rand_seed=10)
+    assert episodes > 0
 
 
 def test_bigfish_long_episodes():

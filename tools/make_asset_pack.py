@@ -71,6 +71,7 @@ def main():
             np.savez_compressed(os.path.join(OUT_DIR, "sprites_%s.npz" % game),
                                 **{key(k): v for k, v in imgs.items()})
             group = catalog.GAMES[game][1]
+            group = catalog.BACKGROUND_PACK.get(group, group)  # subset groups share a pack
             bgs = catalog.BACKGROUND_GROUPS[group]
             imgs = dump(tool, [("B", n) for n in dict.fromkeys(bgs)])
             np.savez_compressed(os.path.join(OUT_DIR, "bg_%s.npz" % group),
