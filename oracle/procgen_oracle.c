@@ -57,7 +57,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
 enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
-       GAME_MINER = 12, GAME_PLUNDER = 14 };
+       GAME_MINER = 12, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -248,6 +248,13 @@ typedef struct {
     float pl_lane_vels[5];
     int pl_num_lanes, pl_num_current_ship_types, pl_targets_hit, pl_target_quota;
     float pl_juice_left, pl_r_scale, pl_spawn_prob, pl_legend_r, pl_min_agent_x;
+    /* starpilot (starpilot.cpp:34-48): the spawner list (sorted by spawn time, popped from the back);
+     * the hp_* tables are init_hps() of the distribution mode */
+    Entity sp_spawners[512];
+    int sp_num_spawners;
+    float sp_hp_vs[9], sp_hp_healths[9], sp_hp_bullet_r[9], sp_hp_object_r[9], sp_hp_prob[9];
+    float sp_total_prob_weight, sp_hp_slow_v, sp_hp_weapon_bullet_dist, sp_hp_spawn_right_threshold;
+    int sp_hp_min_enemy_delta_t, sp_hp_max_group_size, sp_hp_max_enemy_delta_t;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -435,6 +442,17 @@ static int spawn_child(Game *g, int src_i, int type, float obj_r) { /* basic-abs
 }
 static void hook_handle_collision(Game *g, int si, int ti) {
     Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:138-145: BULLET_PLAYER 1 vs destructible non-CLOUD */
+        int tt = target->type;
+        bool destructible = tt == 4 || tt == 8 || tt == 7 || tt == 5; /* FLYER, FAST_FLYER, TURRET, METEOR */
+        if (src->type == 1 && tt != 6 && destructible) {
+            src->will_erase = true;
+            target->health -= 1;
+            float sx = src->x, sy = src->y, tvx = target->vx, tvy = target->vy, r = (float)(.5 * src->rx);
+            add_entity(g, sx, sy, tvx, tvy, r, EXPLOSION);
+        }
+        return;
+    }
     if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:87-108 */
         if (src->type == 1) { /* PLAYER_BULLET */
             if (target->type == 7) { /* SHIP */
@@ -517,6 +535,15 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
             }
+        }
+    } else if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:126-136 */
+        int t = obj->type;
+        if (t == 9) { /* FINISH_LINE */
+            g->sd_done = true;
+            g->sd_reward += 10.0f; /* COMPLETION_BONUS */
+            g->sd_level_complete = true;
+        } else if (t == 4 || t == 8 || t == 2 || t == 3 || t == 7 || t == 5) { /* is_lethal (:346-350) */
+            g->sd_done = true;
         }
     } else if (g->game_id == GAME_DODGEBALL) { /* dodgeball.cpp:102-118 */
         if (obj->type == 4 || obj->type == 6 || obj->type == 1) { /* ENEMY, ENEMY_BALL, LAVA_WALL */
@@ -2669,6 +2696,348 @@ static void plunder_game_step(Game *g, const or_atlas *at) { /* :194-241 */
     if (agent->x < g->pl_min_agent_x) agent->x = g->pl_min_agent_x;
 }
 
+/* ================================================================== starpilot (games/starpilot.cpp) */
+#define SP_BULLET_PLAYER 1
+#define SP_BULLET2 2
+#define SP_BULLET3 3
+#define SP_FLYER 4
+#define SP_METEOR 5
+#define SP_CLOUD 6
+#define SP_TURRET 7
+#define SP_FAST_FLYER 8
+#define SP_FINISH_LINE 9
+#define SP_SHOOTER_WIN_TIME 500
+#define SP_NUM_BASIC_OBJECTS 9
+static const float SP_V_SCALE = 2.0f / 5.0f;
+
+/* std::sort(first, last, comp) of libstdc++ (g++ 11, bits/stl_algo.h: introsort with median-of-3
+ * pivots, threshold 16, heapsort fallback, final insertion sort) over spawner indices with
+ * spawn_cmp (starpilot.cpp:28-30): a before b iff a.spawn_time > b.spawn_time.  Equal spawn times
+ * are common, so the reference's order among them is this algorithm's; pinned against the real
+ * std::sort in tests/test_oracle_pins.py. */
+typedef struct { const int *key; } SortCtx;
+static bool ls_cmp(const SortCtx *c, int a, int b) { return c->key[a] > c->key[b]; }
+static void ls_swap(int *x, int i, int j) { int t = x[i]; x[i] = x[j]; x[j] = t; }
+static void ls_push_heap(const SortCtx *c, int *f, int hole, int top, int value) {
+    int parent = (hole - 1) / 2;
+    while (hole > top && ls_cmp(c, f[parent], value)) {
+        f[hole] = f[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    f[hole] = value;
+}
+static void ls_adjust_heap(const SortCtx *c, int *f, int hole, int len, int value) {
+    int top = hole, second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (ls_cmp(c, f[second], f[second - 1])) second--;
+        f[hole] = f[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        f[hole] = f[second - 1];
+        hole = second - 1;
+    }
+    ls_push_heap(c, f, hole, top, value);
+}
+static void ls_make_heap(const SortCtx *c, int *f, int len) {
+    if (len < 2) return;
+    for (int parent = (len - 2) / 2;; parent--) {
+        ls_adjust_heap(c, f, parent, len, f[parent]);
+        if (parent == 0) return;
+    }
+}
+static void ls_heap_sort(const SortCtx *c, int *f, int len) { /* __partial_sort(first, last, last) */
+    ls_make_heap(c, f, len);
+    for (int last = len; last > 1;) {
+        last--;
+        int value = f[last];
+        f[last] = f[0];
+        ls_adjust_heap(c, f, 0, last, value);
+    }
+}
+static int ls_partition_pivot(const SortCtx *c, int *f, int first, int last) {
+    int mid = first + (last - first) / 2;
+    int a = first + 1, b = mid, cc = last - 1; /* __move_median_to_first(first, a, b, c) */
+    if (ls_cmp(c, f[a], f[b])) {
+        if (ls_cmp(c, f[b], f[cc])) ls_swap(f, first, b);
+        else if (ls_cmp(c, f[a], f[cc])) ls_swap(f, first, cc);
+        else ls_swap(f, first, a);
+    } else if (ls_cmp(c, f[a], f[cc])) ls_swap(f, first, a);
+    else if (ls_cmp(c, f[b], f[cc])) ls_swap(f, first, cc);
+    else ls_swap(f, first, b);
+    int lo = first + 1, hi = last, pivot = first; /* __unguarded_partition */
+    while (true) {
+        while (ls_cmp(c, f[lo], f[pivot])) lo++;
+        hi--;
+        while (ls_cmp(c, f[pivot], f[hi])) hi--;
+        if (!(lo < hi)) return lo;
+        ls_swap(f, lo, hi);
+        lo++;
+    }
+}
+static void ls_introsort_loop(const SortCtx *c, int *f, int first, int last, int depth) {
+    while (last - first > 16) {
+        if (depth == 0) {
+            ls_heap_sort(c, f + first, last - first);
+            return;
+        }
+        depth--;
+        int cut = ls_partition_pivot(c, f, first, last);
+        ls_introsort_loop(c, f, cut, last, depth);
+        last = cut;
+    }
+}
+static void ls_linear_insert(const SortCtx *c, int *f, int last) {
+    int val = f[last], next = last - 1;
+    while (ls_cmp(c, val, f[next])) {
+        f[last] = f[next];
+        last = next;
+        next--;
+    }
+    f[last] = val;
+}
+static void ls_insertion_sort(const SortCtx *c, int *f, int first, int last) {
+    if (first == last) return;
+    for (int i = first + 1; i != last; i++) {
+        if (ls_cmp(c, f[i], f[first])) {
+            int val = f[i];
+            memmove(&f[first + 1], &f[first], sizeof(int) * (size_t)(i - first));
+            f[first] = val;
+        } else {
+            ls_linear_insert(c, f, i);
+        }
+    }
+}
+static void libstdcxx_sort(const int *key, int *idx, int n) {
+    SortCtx c = {key};
+    if (n <= 1) return;
+    int lg = 0;
+    while ((1 << (lg + 1)) <= n) lg++; /* std::__lg */
+    ls_introsort_loop(&c, idx, 0, n, 2 * lg);
+    if (n > 16) {
+        ls_insertion_sort(&c, idx, 0, 16);
+        for (int i = 16; i < n; i++) ls_linear_insert(&c, idx, i);
+    } else {
+        ls_insertion_sort(&c, idx, 0, n);
+    }
+}
+
+/* test hook: the permutation std::sort(spawn_cmp) leaves */
+void oracle_spawn_sort(const int32_t *spawn_times, int32_t *idx, int n) {
+    for (int i = 0; i < n; i++) idx[i] = i;
+    libstdcxx_sort(spawn_times, idx, n);
+}
+
+static void sp_init_hps(Game *g) { /* :147-224 */
+    float scale = 1;
+    for (int i = 0; i < SP_NUM_BASIC_OBJECTS; i++) {
+        g->sp_hp_vs[i] = 1;
+        g->sp_hp_healths[i] = 0;
+        g->sp_hp_prob[i] = 1;
+        g->sp_hp_object_r[i] = scale / 2;
+    }
+    float default_bullet_r = (float)(scale / 2.5);
+    int dm = g->options.distribution_mode;
+    if (dm == EasyMode) {
+        g->sp_hp_prob[SP_METEOR] = 0; g->sp_hp_prob[SP_CLOUD] = 0; g->sp_hp_prob[SP_TURRET] = 0;
+        g->sp_hp_prob[SP_FAST_FLYER] = 0;
+        g->sp_hp_vs[SP_FLYER] = .75; g->sp_hp_vs[SP_BULLET2] = 1.25;
+        g->sp_hp_healths[SP_TURRET] = 5; g->sp_hp_healths[SP_FLYER] = 2; g->sp_hp_healths[SP_FAST_FLYER] = 1;
+        g->maxspeed = 0.75;
+    } else if (dm == HardMode) {
+        g->sp_hp_vs[SP_BULLET2] = 2;
+        g->sp_hp_healths[SP_TURRET] = 5; g->sp_hp_healths[SP_FLYER] = 2; g->sp_hp_healths[SP_FAST_FLYER] = 1;
+        g->maxspeed = 0.75;
+    } else if (dm == ExtremeMode) {
+        g->sp_hp_vs[SP_BULLET2] = 2;
+        g->sp_hp_healths[SP_TURRET] = 10; g->sp_hp_healths[SP_FLYER] = 5; g->sp_hp_healths[SP_FAST_FLYER] = 2;
+        g->maxspeed = 0.5;
+        default_bullet_r = scale / 5;
+    } else {
+        fatal_msg("starpilot: bad distribution mode");
+    }
+    for (int i = 0; i < SP_NUM_BASIC_OBJECTS; i++) g->sp_hp_bullet_r[i] = default_bullet_r;
+    g->sp_hp_healths[SP_METEOR] = 500;
+    g->sp_hp_vs[SP_FAST_FLYER] = 1.5;
+    g->sp_hp_vs[SP_BULLET_PLAYER] = 2;
+    g->sp_hp_vs[SP_BULLET3] = 2;
+    g->sp_hp_object_r[SP_TURRET] = scale * 2;
+    g->sp_hp_object_r[SP_METEOR] = scale * 2;
+    g->sp_hp_object_r[SP_CLOUD] = scale * 2;
+    g->sp_hp_prob[SP_FLYER] = 3;
+    g->sp_hp_slow_v = .5;
+    g->sp_hp_max_group_size = 5;
+    g->sp_hp_weapon_bullet_dist = 3;
+    g->sp_hp_min_enemy_delta_t = 10;
+    g->sp_hp_max_enemy_delta_t = g->sp_hp_min_enemy_delta_t + 20;
+    g->sp_hp_spawn_right_threshold = 0.9f;
+    g->sp_hp_prob[SP_BULLET_PLAYER] = 0; g->sp_hp_prob[SP_BULLET2] = 0; g->sp_hp_prob[SP_BULLET3] = 0;
+    g->sp_total_prob_weight = 0;
+    for (int i = 2; i < SP_NUM_BASIC_OBJECTS; i++) g->sp_total_prob_weight += g->sp_hp_prob[i];
+}
+
+static float rand_pos(Game *g, float r, float min, float max);
+
+static void sp_add_spawners(Game *g, const or_atlas *at, Entity *out, int *count) { /* :226-327 */
+    MT *r = &g->rand_gen;
+    int t = 1 + rg_randint(r, g->sp_hp_min_enemy_delta_t, g->sp_hp_max_enemy_delta_t);
+    bool can_spawn_left = g->options.distribution_mode != EasyMode;
+    *count = 0;
+    for (int i = 0; t <= SP_SHOOTER_WIN_TIME; i++) {
+        int group_size = 1;
+        float start_weight = rg_rand01(r) * g->sp_total_prob_weight;
+        float curr_weight = start_weight;
+        int type;
+        for (type = 2; type < SP_NUM_BASIC_OBJECTS; type++) {
+            curr_weight -= g->sp_hp_prob[type];
+            if (curr_weight <= 0) break;
+        }
+        if (type >= SP_NUM_BASIC_OBJECTS) type = SP_NUM_BASIC_OBJECTS - 1;
+        float rr = g->sp_hp_object_r[type];
+        int flyer_theme = 0;
+        if (type == SP_FLYER || type == SP_FAST_FLYER) {
+            group_size = rg_randint(r, 0, g->sp_hp_max_group_size) + 1;
+            flyer_theme = rg_randn(r, 7); /* NUM_SHIP_THEMES */
+        }
+        float y_pos = rand_pos(g, rr, 0, (float)g->main_height);
+        for (int j = 0; j < group_size; j++) {
+            int spawn_time = t + j * 5;
+            int fire_time = rg_randint(r, 10, 100);
+            float k = 2 * PI_F / 4;
+            float theta = (float)((rg_rand01(r) - .5) * k);
+            float v_scale = g->sp_hp_vs[type];
+            if (rg_randint(r, 0, 2) == 1) theta = 0;
+            float health = g->sp_hp_healths[type];
+            if (type == SP_METEOR || type == SP_CLOUD) {
+                theta = 0;
+                v_scale = g->sp_hp_slow_v;
+                fire_time = -1;
+            } else if (type == SP_TURRET) {
+                theta = 0;
+                v_scale = g->sp_hp_slow_v;
+                fire_time = rg_randint(r, 20, 30);
+            }
+            v_scale *= SP_V_SCALE;
+            float vx = (float)(-1 * cos((double)theta) * v_scale);
+            float vy = (float)(sin((double)theta) * v_scale);
+            bool spawn_right = true;
+            float x_pos;
+            if (type == SP_FLYER || type == SP_FAST_FLYER) {
+                if (rg_rand01(r) > g->sp_hp_spawn_right_threshold && can_spawn_left) spawn_right = false;
+            }
+            if (spawn_right) {
+                x_pos = g->main_width + rr;
+            } else {
+                x_pos = -rr;
+                vx *= -1;
+            }
+            fassert(*count < 512);
+            Entity *sp = &out[(*count)++];
+            entity_init(sp, x_pos, y_pos, vx, vy, rr, rr, type);
+            sp->fire_time = fire_time;
+            sp->spawn_time = spawn_time;
+            sp->health = health;
+            if (type == SP_CLOUD) {
+                sp->render_z = 1;
+                choose_random_theme(g, sp, at);
+            } else if (type == SP_METEOR) {
+                choose_random_theme(g, sp, at);
+            } else if (type == SP_FLYER || type == SP_FAST_FLYER) {
+                sp->image_theme = flyer_theme;
+                sp->rotation = ((vx > 0) ? -1 : 1) * PI_F / 2;
+            } else if (type == SP_TURRET) {
+                choose_random_theme(g, sp, at);
+                match_aspect_ratio(g, at, sp);
+            }
+        }
+        t += rg_randint(r, g->sp_hp_min_enemy_delta_t, g->sp_hp_max_enemy_delta_t);
+    }
+}
+
+static void starpilot_game_reset(Game *g, const or_atlas *at) { /* :329-344 */
+    basic_game_reset(g, at);
+    g->options.center_agent = false;
+    sp_init_hps(g);
+    static Entity gen[512];
+    int n = 0;
+    sp_add_spawners(g, at, gen, &n);
+    int key[512], idx[512];
+    for (int i = 0; i < n; i++) key[i] = gen[i].spawn_time;
+    for (int i = 0; i < n; i++) idx[i] = i;
+    libstdcxx_sort(key, idx, n);
+    for (int i = 0; i < n; i++) g->sp_spawners[i] = gen[idx[i]];
+    g->sp_num_spawners = n;
+    Entity *agent = AG(g);
+    agent->rotation = PI_F / 2;
+    choose_random_theme(g, agent, at);
+}
+
+static void starpilot_game_step(Game *g, const or_atlas *at) { /* :368-430 */
+    basic_game_step(g);
+    bool is_firing = g->special_action != 0;
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *m = &g->ents[i];
+        if (m->type == PLAYER) continue;
+        bool fire;
+        if (m->fire_time <= 0) fire = false; /* should_fire (:356-366) */
+        else if (m->type == SP_TURRET) fire = (g->cur_time - m->spawn_time) % m->fire_time == 0;
+        else fire = g->cur_time - m->spawn_time == m->fire_time;
+        if (fire) {
+            Entity *agent = AG(g);
+            int bullet_type = m->type == SP_TURRET ? SP_BULLET3 : SP_BULLET2;
+            float bullet_r = g->sp_hp_bullet_r[m->type];
+            float b_vx = agent->x - m->x;
+            float b_vy = agent->y - m->y;
+            float bv_scale = (float)(g->sp_hp_vs[bullet_type] * SP_V_SCALE / sqrt((double)(b_vx * b_vx + b_vy * b_vy)));
+            b_vx = b_vx * bv_scale;
+            b_vy = b_vy * bv_scale;
+            float mx = m->x, my = m->y;
+            int b = add_entity(g, mx, my, b_vx, b_vy, bullet_r, bullet_type);
+            if (b_vx != 0 || b_vy != 0) g->ents[b].rotation = -1 * atan2f(b_vy, b_vx) + -1 * PI_F / 2;
+            m = &g->ents[i];
+        }
+        bool destructible = m->type == SP_FLYER || m->type == SP_FAST_FLYER || m->type == SP_TURRET || m->type == SP_METEOR;
+        if (m->health <= 0 && destructible && !m->will_erase) {
+            float mx = m->x, my = m->y, mvx = m->vx, mvy = m->vy, cr = (float)(.5 * m->rx);
+            add_entity(g, mx, my, mvx, mvy, cr, EXPLOSION); /* spawn_child(m, EXPLOSION, .5 * rx, true) */
+            g->sd_reward += 1.0f; /* ENEMY_REWARD */
+            g->ents[i].will_erase = true;
+        }
+    }
+    while (g->sp_num_spawners > 0 && g->cur_time == g->sp_spawners[g->sp_num_spawners - 1].spawn_time) {
+        fassert(g->num_ents < MAX_ENTS);
+        g->ents[g->num_ents++] = g->sp_spawners[--g->sp_num_spawners];
+    }
+    float bullet_r = g->sp_hp_bullet_r[PLAYER];
+    if (is_firing) {
+        Entity *agent = AG(g);
+        float theta = g->special_action == 2 ? PI_F : 0;
+        float v_scale = g->sp_hp_vs[SP_BULLET_PLAYER] * SP_V_SCALE;
+        float vx = (float)(cos((double)theta) * v_scale);
+        float vy = (float)(sin((double)theta) * v_scale);
+        float x_off = (float)(agent->rx * cos((double)theta));
+        int b = add_entity(g, agent->x + x_off, agent->y, vx, vy, bullet_r, SP_BULLET_PLAYER);
+        Entity *bl = &g->ents[b];
+        bl->collides_with_entities = true;
+        if (vx != 0 || vy != 0) bl->rotation = -1 * atan2f(vy, vx) + 0.0f;
+        bl->rotation -= PI_F / 2;
+    }
+    if (g->cur_time == SP_SHOOTER_WIN_TIME) {
+        Entity fin;
+        entity_init(&fin, (float)g->main_width, (float)(g->main_height / 2), -1 * g->sp_hp_slow_v * SP_V_SCALE, 0, 2,
+                    (float)(g->main_height / 2), SP_FINISH_LINE);
+        choose_random_theme(g, &fin, at);
+        float ar = asset_aspect_ratio(g, at, fin.image_type + fin.image_theme * MAX_ASSETS); /* match_aspect_ratio(finish, false) */
+        fin.rx = fin.ry * ar;
+        fin.x = g->main_width + fin.rx;
+        fassert(g->num_ents < MAX_ENTS);
+        g->ents[g->num_ents++] = fin;
+    }
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -2819,6 +3188,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_reset(g, at);
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_reset(g, at);
     else if (g->game_id == GAME_PLUNDER) plunder_game_reset(g, at);
+    else if (g->game_id == GAME_STARPILOT) starpilot_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -2833,6 +3203,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_FRUITBOT) fruitbot_game_step(g);
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_step(g);
     else if (g->game_id == GAME_PLUNDER) plunder_game_step(g, at);
+    else if (g->game_id == GAME_STARPILOT) starpilot_game_step(g, at);
     else fatal_msg("game not restated");
 }
 
@@ -3428,6 +3799,22 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
 }
 
 static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
+    if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:107-124: scrolling tiled background */
+        float scale = (float)(RES_H / g->main_height); /* int / int */
+        qt_fill_rect_int(g->canvas, 0, 0, RES_W, RES_H, 0xff000000u);
+        if (g->options.use_backgrounds) {
+            float bg_k = 3;
+            float t = (float)g->cur_time;
+            float x_off = -t * scale * g->sp_hp_slow_v * 2 / g->char_dim;
+            const float BG_RATIO = 18;
+            RectD r_bg = {(double)x_off, (double)(-RES_H * (bg_k - 1) / 2), (double)(RES_H * bg_k * BG_RATIO),
+                          (double)(RES_H * bg_k)};
+            const or_image *bg = &at->backgrounds[g->background_index];
+            tile_image_fmt(g, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, r_bg, 1);
+        }
+        draw_foreground(g, at);
+        return;
+    }
     draw_background(g, at);
     draw_foreground(g, at);
     if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:66-77: juice and progress bars, get_abs_rect (:812-814) */
@@ -3453,6 +3840,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "fruitbot") == 0) return GAME_FRUITBOT;
     if (strcmp(name, "dodgeball") == 0) return GAME_DODGEBALL;
     if (strcmp(name, "plunder") == 0) return GAME_PLUNDER;
+    if (strcmp(name, "starpilot") == 0) return GAME_STARPILOT;
     return -1;
 }
 
@@ -3506,6 +3894,10 @@ static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
     g->maxspeed = 0.85f;
     g->bg_tile_ratio = -1;
     g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
+}
+static void starpilot_ctor(Game *g) { /* starpilot.cpp:50-54 */
+    g->main_width = 16;
+    g->main_height = 16;
 }
 static void plunder_ctor(Game *g) { /* plunder.cpp:33-43 */
     g->timeout = 4000;
@@ -3596,6 +3988,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_FRUITBOT) fruitbot_ctor(g);
         else if (gid == GAME_DODGEBALL) dodgeball_ctor(g);
         else if (gid == GAME_PLUNDER) plunder_ctor(g);
+        else if (gid == GAME_STARPILOT) starpilot_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

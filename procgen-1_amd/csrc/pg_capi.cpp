@@ -118,9 +118,10 @@ int game_id(const std::string &name) {
     if (name == "fruitbot") return PG_GAME_FRUITBOT;
     if (name == "dodgeball") return PG_GAME_DODGEBALL;
     if (name == "plunder") return PG_GAME_PLUNDER;
+    if (name == "starpilot") return PG_GAME_STARPILOT;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder";
+const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder, starpilot";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -180,6 +181,9 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_STARPILOT) { // starpilot.cpp:50-54
+        s.main_width = 16;
+        s.main_height = 16;
     } else if (gid == PG_GAME_PLUNDER) { // plunder.cpp:33-43
         s.timeout = 4000;
         s.main_width = 20;
@@ -875,7 +879,8 @@ LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int le
 }
 
 // ---- get_state / set_state (vecgame.cpp:485-505): this build's own snapshot format
-// [u32 magic][u32 version][PGEnv][num_ents x PG_NF words][grid cells int16][2 x 625 mt words][END]
+// [u32 magic][u32 version][PGEnv][num_ents x PG_NF words][num_tail x PG_NF words (the reserved top
+// slots, starpilot's spawners)][grid cells int16][2 x 625 mt words][END]
 static const uint32_t STATE_MAGIC = 0x50474d33u; // "PGM3"
 static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
 
@@ -885,18 +890,22 @@ LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
     if (hipStreamSynchronize(v->stream) != hipSuccess) return -1;
     PGEnv s;
     if (copy_sync(v, &s, v->dev.envs + env_idx, sizeof(s), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    size_t ents = (size_t)s.num_ents;
+    size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail;
     size_t cells = (size_t)s.main_width * s.main_height;
-    size_t need = 8 + sizeof(PGEnv) + ents * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
     if ((size_t)length < need) return -1;
     char *p = data;
     memcpy(p, &STATE_MAGIC, 4); p += 4;
-    uint32_t ver = 1; memcpy(p, &ver, 4); p += 4;
+    uint32_t ver = 2; memcpy(p, &ver, 4); p += 4;
     memcpy(p, &s, sizeof(s)); p += sizeof(s);
     size_t plane = (size_t)v->num_envs * PG_CAP;
     for (int f = 0; f < PG_NF; f++) {
         if (ents && copy_sync(v, p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
         p += ents * 4;
+    }
+    for (int f = 0; f < PG_NF; f++) {
+        if (tail && copy_sync(v, p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP + (PG_CAP - tail), tail * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        p += tail * 4;
     }
     if (cells && copy_sync(v, p, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, cells * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     p += cells * 2;
@@ -919,10 +928,10 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     memcpy(&ver, p, 4); p += 4;
     PGEnv s;
     memcpy(&s, p, sizeof(s)); p += sizeof(s);
-    size_t ents = (size_t)s.num_ents, cells = (size_t)s.main_width * s.main_height;
-    size_t need = 8 + sizeof(PGEnv) + ents * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail, cells = (size_t)s.main_width * s.main_height;
+    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
     int32_t end = 0;
-    if (magic != STATE_MAGIC || ver != 1 || (size_t)length < need || ents > PG_CAP || cells > PG_GRID_MAX) {
+    if (magic != STATE_MAGIC || ver != 2 || (size_t)length < need || ents + tail > PG_CAP || cells > PG_GRID_MAX) {
         fail(v, PG_ERR_BAD_OPTION, "set_state: not a state of this build");
         return;
     }
@@ -934,9 +943,14 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     size_t plane = (size_t)v->num_envs * PG_CAP;
     s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
     copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
+    const char *ent_base = p; // the live entity planes
     for (int f = 0; f < PG_NF; f++) {
         if (ents) copy_sync(v, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);
         p += ents * 4;
+    }
+    for (int f = 0; f < PG_NF; f++) {
+        if (tail) copy_sync(v, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP + (PG_CAP - tail), p, tail * 4, hipMemcpyHostToDevice);
+        p += tail * 4;
     }
     if (cells) copy_sync(v, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);
     if (v->has_latent && (s.game_id == PG_GAME_MAZE || s.game_id == PG_GAME_MINER)) { // latent mirrors the state
@@ -949,8 +963,8 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
             lat[2 + k] = cv;
         }
         float ax, ay;
-        memcpy(&ax, p - PG_NF * ents * 4 + (size_t)F_X * ents * 4, 4); // entity 0 = the agent
-        memcpy(&ay, p - PG_NF * ents * 4 + (size_t)F_Y * ents * 4, 4);
+        memcpy(&ax, ent_base + (size_t)F_X * ents * 4, 4); // entity 0 = the agent
+        memcpy(&ay, ent_base + (size_t)F_Y * ents * 4, 4);
         if (s.agent_erased) {
             ax = s.ghost_x;
             ay = s.ghost_y;
@@ -961,10 +975,10 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
             for (size_t e = 0; e < ents; e++) {
                 int32_t ty;
                 float ex, ey;
-                memcpy(&ty, p - PG_NF * ents * 4 + (size_t)F_TYPE * ents * 4 + e * 4, 4);
+                memcpy(&ty, ent_base + (size_t)F_TYPE * ents * 4 + e * 4, 4);
                 if (ty != 6) continue;
-                memcpy(&ex, p - PG_NF * ents * 4 + (size_t)F_X * ents * 4 + e * 4, 4);
-                memcpy(&ey, p - PG_NF * ents * 4 + (size_t)F_Y * ents * 4 + e * 4, 4);
+                memcpy(&ex, ent_base + (size_t)F_X * ents * 4 + e * 4, 4);
+                memcpy(&ey, ent_base + (size_t)F_Y * ents * 4 + e * 4, 4);
                 lat[4 + PG_LATENT_GRID] = (int)ex;
                 lat[5 + PG_LATENT_GRID] = (int)ey;
                 break;

@@ -15,7 +15,7 @@
 #include <stdint.h>
 
 #include "pg_engine.h"
-#include "pg_sincos.h"
+#include "pg_libm.h"
 
 #define DEV __device__ __forceinline__
 #define LANE ((int)threadIdx.x)
@@ -113,6 +113,46 @@ DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 #define PL_TARGET_BACKGROUND 3
 #define PL_PANEL 6
 #define PL_SHIP 7
+// starpilot.cpp:6-26
+#define SP_BULLET_PLAYER 1
+#define SP_BULLET2 2
+#define SP_BULLET3 3
+#define SP_FLYER 4
+#define SP_METEOR 5
+#define SP_CLOUD 6
+#define SP_TURRET 7
+#define SP_FAST_FLYER 8
+#define SP_FINISH_LINE 9
+#define SP_SHOOTER_WIN_TIME 500
+#define SP_V_SCALE (2.0f / 5.0f)
+// init_hps (starpilot.cpp:147-224) as functions of the distribution mode (the tables are constant
+// per mode; deserialize recomputes them the same way, :437-442)
+DEV float sp_hp_vs(int mode, int type) {
+    if (type == SP_FAST_FLYER) return 1.5f;
+    if (type == SP_BULLET_PLAYER || type == SP_BULLET3) return 2;
+    if (type == SP_BULLET2) return mode == PG_EASY ? 1.25f : 2.0f;
+    if (type == SP_FLYER && mode == PG_EASY) return .75f;
+    return 1;
+}
+DEV float sp_hp_health(int mode, int type) {
+    if (type == SP_METEOR) return 500;
+    const bool ex = mode == PG_EXTREME;
+    if (type == SP_TURRET) return ex ? 10 : 5;
+    if (type == SP_FLYER) return ex ? 5 : 2;
+    if (type == SP_FAST_FLYER) return ex ? 2 : 1;
+    return 0;
+}
+DEV float sp_hp_bullet_r(int mode) { return mode == PG_EXTREME ? (float)(1.0f / 5) : (float)(1.0f / 2.5); }
+DEV float sp_hp_object_r(int type) {
+    return (type == SP_TURRET || type == SP_METEOR || type == SP_CLOUD) ? 1.0f * 2 : 1.0f / 2;
+}
+DEV float sp_hp_prob(int mode, int type) {
+    if (type <= SP_BULLET3) return 0;
+    if (type == SP_FLYER) return 3;
+    if (mode == PG_EASY && (type == SP_METEOR || type == SP_CLOUD || type == SP_TURRET || type == SP_FAST_FLYER)) return 0;
+    return 1;
+}
+#define SP_HP_SLOW_V .5f
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3
@@ -139,25 +179,15 @@ DEV bool cl_is_wall(int t) { return t == CL_WALL_MID || t == CL_WALL_TOP; }
 #define PG_ROT_RING_KEY 9
 #define PI_F 3.14159265358979323846264338327950288f
 
-// atan2f as the C library returns it (entity.cpp:86 calls std::atan2(float, float)): the axis and
-// diagonal directions the games face are exact constants (the correctly rounded float of
-// 0, pi/4, pi/2, 3pi/4, pi with the sign of dy; checked against glibc in tests/test_gpu_libm.py);
-// any other direction uses the device atan2f (render-only rotation, pixel tolerance class).
-DEV float pg_atan2f(float dy, float dx) {
-    if (dy == 0) return dx >= 0 && !signbit(dx) ? dy : copysignf(PI_F, dy);
-    if (dx == 0) return copysignf(PI_F / 2, dy);
-    if (fabsf(dx) == fabsf(dy)) return copysignf(dx > 0 ? __uint_as_float(0x3f490fdbu) : __uint_as_float(0x4016cbe4u), dy);
-    return atan2f(dy, dx);
-}
-// Entity::face_direction(dx, dy, rotation_offset = 0) (entity.cpp:84-88)
-DEV float face_rotation(float dx, float dy, float rot) {
-    if (dx != 0 || dy != 0) rot = -1 * pg_atan2f(dy, dx) + 0.0f;
+// Entity::face_direction(dx, dy, rotation_offset) (entity.cpp:84-88; atan2 = glibc atan2f, pg_libm.h)
+DEV float face_rotation(float dx, float dy, float rot, float offset = 0.0f) {
+    if (dx != 0 || dy != 0) rot = -1 * pg_atan2f(dy, dx) + offset;
     return rot;
 }
 
 // QTransform::rotate(rotation * 180 / PI) of draw_image (basic-abstract-game.cpp:912-913; Qt5
 // qtransform.cpp): exact special cases for +-90 / 180 / 270, otherwise sin / cos of deg2rad * a in
-// double (correctly rounded here, pg_sincos.h); QTransform::type() then treats a qFuzzyIsNull sine
+// double (correctly rounded here, pg_libm.h); QTransform::type() then treats a qFuzzyIsNull sine
 // (|s| <= 1e-12) as no rotation.
 // m = {m11, m12, m21, m22}.  The host builds the same matrices with the C library for the
 // angles of the rotation table; this is the device path for every other angle.

@@ -23,7 +23,7 @@
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
     PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
-    PG_GAME_MINER = 12, PG_GAME_PLUNDER = 14
+    PG_GAME_MINER = 12, PG_GAME_PLUNDER = 14, PG_GAME_STARPILOT = 15
 };
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
@@ -185,8 +185,12 @@ struct PGEnv {
             int32_t num_lanes, num_current_ship_types, targets_hit, target_quota;
             float juice_left, r_scale, spawn_prob, legend_r, min_agent_x;
         } pl;
-        int32_t words[21];
+        int32_t words[20];
     } gs;
+    // entity slots reserved at the top of the planes, [PG_CAP - num_tail, PG_CAP): starpilot's
+    // spawner list (starpilot.cpp:34), vector index i at slot PG_CAP - 1 - i (pop_back frees the
+    // lowest slot)
+    int32_t num_tail;
 };
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");

@@ -1,8 +1,15 @@
-// pg_sincos.h -- correctly rounded double sin / cos for the rotation math (QTransform::rotate,
+// pg_libm.h -- the C-library math the reference's arithmetic depends on, restated for the device.
+//
+// (1) pg_atan2f: glibc 2.35's atan2f (sysdeps/ieee754/flt-32/e_atan2f.c + s_atanf.c, the fdlibm
+// algorithm with glibc's pi / pi_lo constants), operation by operation in float -- bit-identical to
+// the library on 40M+ random arguments and every special case (tests/test_libm_cpu.py).
+// Entity::face_direction calls it (entity.cpp:86: std::atan2(float, float) = atan2f).
+//
+// (2) pg_sincos_cr: correctly rounded double sin / cos for the rotation math (QTransform::rotate,
 // Qt5 qtransform.cpp, reached from draw_image, basic-abstract-game.cpp:912-913) and the games'
 // float-position steering (caveflyer / starpilot / bossfight / ninja call cos / sin on doubles).
 // The reference links glibc, whose sin / cos return the correctly rounded result for the
-// arguments these games produce (checked on 8M+ arguments in tests/test_sincos_cpu.py); the
+// arguments these games produce except ~0.15% (off by 1 ulp; tests/test_libm_cpu.py); the
 // device's own sin / cos are 1-ulp (3% of matrix entries differed), so the engine evaluates
 // both in double-double arithmetic (Cody-Waite reduction with a 4-part pi/2, Taylor series to
 // x^29) and rounds once.  Plain C so the same source is compiled for the host in the CPU test.
@@ -12,8 +19,80 @@
 #define PG_HD __host__ __device__ static inline
 #else
 #include <math.h>
+#include <stdint.h>
+#include <string.h>
 #define PG_HD static inline
 #endif
+
+PG_HD uint32_t pg_fbits(float f) {
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    return u;
+}
+PG_HD float pg_bitsf(uint32_t u) {
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+// s_atanf.c (fdlibm): atan(x) in float with a 4-interval argument reduction
+PG_HD float pg_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float aT[11] = {3.3333334327e-01f, -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                          9.0908870101e-02f, -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                          4.9768779427e-02f, -3.6531571299e-02f, 1.6285819933e-02f};
+    const int32_t hx = (int32_t)pg_fbits(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) { // |x| >= 2^25
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) { // |x| < 0.4375
+        if (ix < 0x31000000) return x; // |x| < 2^-29
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) { // |x| < 1.1875
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
+            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
+        } else {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
+            else { id = 3; x = -1.0f / x; }
+        }
+    }
+    const float z = x * x, w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+
+// e_atan2f.c (fdlibm, glibc constants pi = 0x40490fdb, pi_lo = -0x1.777a5cp-24)
+PG_HD float pg_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)pg_fbits(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)pg_fbits(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return pg_atanf(y); // x = 1
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        if (m <= 1) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000 || iy == 0x7f800000) return atan2f(y, x); // infinities: never drawn
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = pg_atanf(fabsf(y / x));
+    if (m == 0) return z;
+    if (m == 1) return pg_bitsf(pg_fbits(z) ^ 0x80000000u);
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
 
 typedef struct { double hi, lo; } pg_dd;
 

@@ -810,8 +810,47 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
         if (!bg_ok) bg_lane_row = -1;
     }
-    const bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
-    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
+    bool bg_col = bg_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
+    uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
+    if constexpr (G == PG_GAME_STARPILOT) {
+        // starpilot game_draw (starpilot.cpp:107-124): tile_image(r_bg, 1) of a background scrolled
+        // left by cur_time -- 3456 x 192 px, 18 square tiles side by side; a screen column shows the
+        // last tile covering it
+        bg_ok = false;
+        bg_col = false;
+        bg_lane_row = -1;
+        if (s.opt_use_backgrounds) {
+            const float scale = (float)(PG_RES / s.main_height); // int / int
+            const float bg_k = 3, t = (float)s.cur_time, BG_RATIO = 18;
+            const float x_off = -t * scale * SP_HP_SLOW_V * 2 / s.char_dim;
+            const double rx = (double)x_off, ry = (double)(-PG_RES * (bg_k - 1) / 2);
+            const double rw = (double)(PG_RES * bg_k * BG_RATIO), rh = (double)(PG_RES * bg_k);
+            int num_tiles = (int)(rw / (rh * 1.0f));
+            if (num_tiles < 1) num_tiles = 1;
+            const float tw = (float)(rw / num_tiles), th = (float)rh;
+            bg_ok = axis_setup(ry, (double)th, bgi.z, by);
+            bg_lane_row = (bg_ok && lane >= by.t1 && lane < by.t1 + by.n)
+                              ? (int)(((by.base + (uint32_t)((lane - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
+                              : -1;
+            for (int t0 = 0; t0 < num_tiles; t0 += 64) {
+                Axis tx;
+                const int k0 = t0 + lane;
+                const bool okt = k0 < num_tiles && axis_setup(rx + (double)(tw * (float)k0), (double)tw, bgi.y, tx);
+                const int tt1 = okt ? tx.t1 : 0, tn = okt ? tx.n : 0, tstep = okt ? tx.step : 0;
+                const uint32_t tbase = okt ? tx.base : 0u;
+                for (int k = 0; k < 64 && t0 + k < num_tiles; k++) {
+                    const int a1 = readlane(tt1, k), an = readlane(tn, k);
+                    if (lane >= a1 && lane < a1 + an) {
+                        const uint32_t bb = (uint32_t)readlane((int)tbase, k);
+                        const int st = readlane(tstep, k);
+                        bg_col = true;
+                        bg_col_base = (uint32_t)bgi.x + ((bb + (uint32_t)((lane - a1) * st)) >> 16);
+                    }
+                }
+            }
+            if (!bg_ok) bg_col = false;
+        }
+    }
 
     // fast path eligibility: square TILE_PX tiles only (uniform_tiles), no z = -1 entity
     // (drawn between background and grid), few tile rows per frame
@@ -1084,6 +1123,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
+        PG_CASE(PG_GAME_STARPILOT)
     default: break;
     }
 #undef PG_CASE

@@ -48,6 +48,18 @@ template <int G> struct Scratch { uint32_t dummy[1]; };
 template <> struct Scratch<PG_GAME_CHASER> { ChaserScratch ch; };
 template <> struct Scratch<PG_GAME_FRUITBOT> { int16_t part[16]; };
 template <> struct Scratch<PG_GAME_DODGEBALL> { float4 rooms[64]; }; // QRectF x, y, w, h
+// starpilot's spawners in generation order (at most 49 groups x 6, starpilot.cpp:226-327), then the
+// std::sort permutation and its explicit introsort stack
+#define SP_MAX_SPAWNERS 320
+struct SpawnerScratch {
+    float x[SP_MAX_SPAWNERS], y[SP_MAX_SPAWNERS], vx[SP_MAX_SPAWNERS], vy[SP_MAX_SPAWNERS];
+    float r[SP_MAX_SPAWNERS], ry[SP_MAX_SPAWNERS], rot[SP_MAX_SPAWNERS], health[SP_MAX_SPAWNERS];
+    int16_t type[SP_MAX_SPAWNERS], theme[SP_MAX_SPAWNERS], fire[SP_MAX_SPAWNERS], spawn[SP_MAX_SPAWNERS];
+    int8_t rz[SP_MAX_SPAWNERS];
+    int16_t idx[SP_MAX_SPAWNERS];
+    int16_t stack[3 * 64];
+};
+template <> struct Scratch<PG_GAME_STARPILOT> { SpawnerScratch sp; };
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -77,6 +89,10 @@ DEV int add_entity_rxy(RCtx &c, float x, float y, float vx, float vy, float rx, 
     if (i >= PG_CAP) {
         c.s.error = PG_ERR_ENTITY_OVERFLOW;
         return PG_CAP - 1;
+    }
+    if (i >= PG_CAP - c.s.num_tail) {
+        c.s.error = PG_ERR_ENTITY_OVERFLOW;
+        return PG_CAP - c.s.num_tail - 1;
     }
     c.s.num_ents = i + 1;
     float grow = 1.0f, decay = 1.0f;
@@ -212,6 +228,7 @@ DEV void base_game_reset(RCtx &c) { // basic-abstract-game.cpp:767-806
     fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, 0); // grid.resize -> zeros
     c.s.background_index = randn(c, c.d.num_backgrounds);
     c.s.num_ents = 0;
+    c.s.num_tail = 0;
     c.s.agent_erased = 0;
     float ax, ay;
     float a_r = 0.4f;
@@ -1323,6 +1340,238 @@ DEV void plunder_game_reset(RCtx &c) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ starpilot (starpilot.cpp:226-344)
+// std::sort(spawners, spawn_cmp) of libstdc++ (bits/stl_algo.h), run by lane 0 over the LDS index
+// array: introsort (median-of-3 pivot, unguarded partition, threshold 16, depth 2 * lg n with a
+// heapsort fallback) + final insertion sort -- the same steps as oracle/procgen_oracle.c
+// libstdcxx_sort, whose permutation is pinned against the real std::sort.  The recursion on the
+// right part becomes an explicit stack (the parts are disjoint, the order they are sorted in does
+// not change the result).
+struct SpSort {
+    const int16_t *key;
+    int16_t *f;
+    DEV bool cmp(int a, int b) const { return key[a] > key[b]; } // spawn_cmp (:28-30)
+    DEV void swp(int i, int j) { int16_t t = f[i]; f[i] = f[j]; f[j] = t; }
+    DEV void push_heap(int base, int hole, int top, int value) {
+        int parent = (hole - 1) / 2;
+        while (hole > top && cmp(f[base + parent], value)) {
+            f[base + hole] = f[base + parent];
+            hole = parent;
+            parent = (hole - 1) / 2;
+        }
+        f[base + hole] = (int16_t)value;
+    }
+    DEV void adjust_heap(int base, int hole, int len, int value) {
+        int top = hole, second = hole;
+        while (second < (len - 1) / 2) {
+            second = 2 * (second + 1);
+            if (cmp(f[base + second], f[base + second - 1])) second--;
+            f[base + hole] = f[base + second];
+            hole = second;
+        }
+        if ((len & 1) == 0 && second == (len - 2) / 2) {
+            second = 2 * (second + 1);
+            f[base + hole] = f[base + second - 1];
+            hole = second - 1;
+        }
+        push_heap(base, hole, top, value);
+    }
+    DEV void heap_sort(int base, int len) {
+        if (len >= 2)
+            for (int parent = (len - 2) / 2;; parent--) {
+                adjust_heap(base, parent, len, f[base + parent]);
+                if (parent == 0) break;
+            }
+        for (int last = len; last > 1;) {
+            last--;
+            int value = f[base + last];
+            f[base + last] = f[base];
+            adjust_heap(base, 0, last, value);
+        }
+    }
+    DEV int partition_pivot(int first, int last) {
+        int mid = first + (last - first) / 2, a = first + 1, b = mid, cc = last - 1;
+        if (cmp(f[a], f[b])) {
+            if (cmp(f[b], f[cc])) swp(first, b);
+            else if (cmp(f[a], f[cc])) swp(first, cc);
+            else swp(first, a);
+        } else if (cmp(f[a], f[cc])) swp(first, a);
+        else if (cmp(f[b], f[cc])) swp(first, cc);
+        else swp(first, b);
+        int lo = first + 1, hi = last;
+        while (true) {
+            while (cmp(f[lo], f[first])) lo++;
+            hi--;
+            while (cmp(f[first], f[hi])) hi--;
+            if (!(lo < hi)) return lo;
+            swp(lo, hi);
+            lo++;
+        }
+    }
+    DEV void linear_insert(int last) {
+        int val = f[last], next = last - 1;
+        while (cmp(val, f[next])) {
+            f[last] = f[next];
+            last = next;
+            next--;
+        }
+        f[last] = (int16_t)val;
+    }
+    DEV void sort(int n, int16_t *stack) {
+        if (n <= 1) return;
+        int lg = 0;
+        while ((1 << (lg + 1)) <= n) lg++;
+        int sp = 0;
+        int first = 0, last = n, depth = 2 * lg;
+        while (true) {
+            while (last - first > 16) {
+                if (depth == 0) {
+                    heap_sort(first, last - first);
+                    break;
+                }
+                depth--;
+                int cut = partition_pivot(first, last);
+                stack[3 * sp] = (int16_t)cut; stack[3 * sp + 1] = (int16_t)last; stack[3 * sp + 2] = (int16_t)depth;
+                sp++;
+                last = cut;
+            }
+            if (sp == 0) break;
+            sp--;
+            first = stack[3 * sp]; last = stack[3 * sp + 1]; depth = stack[3 * sp + 2];
+        }
+        // __final_insertion_sort
+        const int head = n > 16 ? 16 : n;
+        for (int i = 1; i < head; i++) {
+            if (cmp(f[i], f[0])) {
+                int16_t val = f[i];
+                for (int k = i; k > 0; k--) f[k] = f[k - 1];
+                f[0] = val;
+            } else {
+                linear_insert(i);
+            }
+        }
+        for (int i = head; i < n; i++) linear_insert(i);
+    }
+};
+
+DEV void starpilot_game_reset(RCtx &c, SpawnerScratch *S) {
+    base_game_reset<PG_GAME_STARPILOT>(c);
+    c.s.opt_center_agent = 0;
+    const int mode = c.s.opt_distribution_mode;
+    // init_hps (:147-224): maxspeed per mode; the tables are sp_hp_* (pg_device.h)
+    c.s.maxspeed = mode == PG_EXTREME ? 0.5f : 0.75f;
+    float total = 0;
+    for (int i = 2; i < 9; i++) total += sp_hp_prob(mode, i);
+    // add_spawners (:226-327)
+    const int dmin = 10, dmax = 10 + 20, max_group = 5;
+    int t = 1 + dmin + randn(c, dmax - dmin); // randint(lo, hi) = lo + x % (hi - lo)
+    const bool can_spawn_left = mode != PG_EASY;
+    int n = 0;
+    while (t <= SP_SHOOTER_WIN_TIME) {
+        int group_size = 1;
+        const float start_weight = rand01(c) * total;
+        float curr_weight = start_weight;
+        int type;
+        for (type = 2; type < 9; type++) {
+            curr_weight -= sp_hp_prob(mode, type);
+            if (curr_weight <= 0) break;
+        }
+        if (type >= 9) type = 8;
+        const float r = sp_hp_object_r(type);
+        int flyer_theme = 0;
+        if (type == SP_FLYER || type == SP_FAST_FLYER) {
+            group_size = randn(c, max_group) + 1; // randint(0, 5) + 1
+            flyer_theme = randn(c, 7);            // NUM_SHIP_THEMES
+        }
+        const float y_pos = rand_pos(c, r, 0, (float)c.s.main_height);
+        for (int j = 0; j < group_size; j++) {
+            const int spawn_time = t + j * 5;
+            int fire_time = 10 + randn(c, 90); // randint(10, 100)
+            const float k = 2 * PI_F / 4;
+            float theta = (float)((rand01(c) - .5) * k);
+            float v_scale = sp_hp_vs(mode, type);
+            if (randn(c, 2) == 1) theta = 0; // randint(0, 2)
+            const float health = sp_hp_health(mode, type);
+            if (type == SP_METEOR || type == SP_CLOUD) {
+                theta = 0;
+                v_scale = SP_HP_SLOW_V;
+                fire_time = -1;
+            } else if (type == SP_TURRET) {
+                theta = 0;
+                v_scale = SP_HP_SLOW_V;
+                fire_time = 20 + randn(c, 10); // randint(20, 30)
+            }
+            v_scale *= SP_V_SCALE;
+            double st, ct;
+            pg_sincos_cr((double)theta, &st, &ct); // ::cos / ::sin (double) of the float theta
+            float vx = (float)(-1 * ct * v_scale);
+            const float vy = (float)(st * v_scale);
+            bool spawn_right = true;
+            float x_pos;
+            if (type == SP_FLYER || type == SP_FAST_FLYER)
+                if (rand01(c) > 0.9f && can_spawn_left) spawn_right = false; // hp_spawn_right_threshold
+            if (spawn_right) {
+                x_pos = c.s.main_width + r;
+            } else {
+                x_pos = -r;
+                vx *= -1;
+            }
+            int theme = 0, rz = 0;
+            float ry = r, rot = 0;
+            if (type == SP_CLOUD) {
+                rz = 1;
+                theme = randn(c, c.d.num_themes[SP_CLOUD]);
+            } else if (type == SP_METEOR) {
+                theme = randn(c, c.d.num_themes[SP_METEOR]);
+            } else if (type == SP_FLYER || type == SP_FAST_FLYER) {
+                theme = flyer_theme;
+                rot = ((vx > 0) ? -1 : 1) * PI_F / 2;
+            } else if (type == SP_TURRET) {
+                theme = randn(c, c.d.num_themes[SP_TURRET]);
+                int th = c.s.opt_restrict_themes ? 0 : theme; // match_aspect_ratio
+                int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + th * MAX_ASSETS];
+                if (sp.y <= 0 || sp.z <= 0) c.s.error = PG_ERR_BAD_OPTION;
+                else ry = r / (float)(sp.y * 1.0 / sp.z);
+            }
+            if (n >= SP_MAX_SPAWNERS) {
+                c.s.error = PG_ERR_ENTITY_OVERFLOW;
+            } else if (LANE == 0) {
+                S->x[n] = x_pos; S->y[n] = y_pos; S->vx[n] = vx; S->vy[n] = vy; S->r[n] = r; S->ry[n] = ry;
+                S->rot[n] = rot; S->health[n] = health; S->type[n] = (int16_t)type; S->theme[n] = (int16_t)theme;
+                S->fire[n] = (int16_t)fire_time; S->spawn[n] = (int16_t)spawn_time; S->rz[n] = (int8_t)rz;
+                S->idx[n] = (int16_t)n;
+            }
+            if (n < SP_MAX_SPAWNERS) n++;
+        }
+        t += dmin + randn(c, dmax - dmin);
+    }
+    wave_sync();
+    if (LANE == 0) {
+        SpSort so;
+        so.key = S->spawn;
+        so.f = S->idx;
+        so.sort(n, S->stack);
+    }
+    wave_sync();
+    // spawners[i] -> slot PG_CAP - 1 - i
+    if (c.s.num_ents + n > PG_CAP) c.s.error = PG_ERR_ENTITY_OVERFLOW;
+    for (int i = LANE; i < n && c.s.num_ents + n <= PG_CAP; i += 64) {
+        const int g = S->idx[i], slot = PG_CAP - 1 - i;
+        EF(c, F_X, slot) = S->x[g]; EF(c, F_Y, slot) = S->y[g]; EF(c, F_VX, slot) = S->vx[g]; EF(c, F_VY, slot) = S->vy[g];
+        EF(c, F_RX, slot) = S->r[g]; EF(c, F_RY, slot) = S->ry[g]; EF(c, F_ROTATION, slot) = S->rot[g];
+        EF(c, F_VROT, slot) = 0; EF(c, F_ALPHA, slot) = 1.0f; EF(c, F_ALPHA_DECAY, slot) = 1.0f;
+        EF(c, F_GROW_RATE, slot) = 1.0f; EF(c, F_FRICTION, slot) = 1; EF(c, F_COLLISION_MARGIN, slot) = 0;
+        EF(c, F_HEALTH, slot) = S->health[g]; EF(c, F_THETA, slot) = -100; EF(c, F_CLIMBER_SPAWN_X, slot) = 0;
+        EI(c, F_TYPE, slot) = S->type[g]; EI(c, F_IMAGE_TYPE, slot) = S->type[g]; EI(c, F_IMAGE_THEME, slot) = S->theme[g];
+        EI(c, F_RENDER_Z, slot) = S->rz[g]; EI(c, F_LIFE_TIME, slot) = 0; EI(c, F_EXPIRE_TIME, slot) = -1;
+        EI(c, F_FIRE_TIME, slot) = S->fire[g]; EI(c, F_SPAWN_TIME, slot) = S->spawn[g]; EI(c, F_FLAGS, slot) = EF_AUTO_ERASE;
+    }
+    c.s.num_tail = n;
+    EF(c, F_ROTATION, 0) = PI_F / 2;
+    EI(c, F_IMAGE_THEME, 0) = randn(c, c.d.num_themes[PLAYER]); // choose_random_theme(agent)
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1650,6 +1899,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_game_reset(c, scratch->part);
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_game_reset(c, scratch->rooms);
     if constexpr (G == PG_GAME_PLUNDER) plunder_game_reset(c);
+    if constexpr (G == PG_GAME_STARPILOT) starpilot_game_reset(c, &scratch->sp);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -1755,6 +2005,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
+        PG_CASE(PG_GAME_STARPILOT)
     default: break;
     }
 #undef PG_CASE

@@ -750,6 +750,15 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 c.s.fish_eaten += 1;
             }
         }
+    } else if constexpr (G == PG_GAME_STARPILOT) { // starpilot.cpp:126-136
+        if (t == SP_FINISH_LINE) {
+            c.s.sd_done = 1;
+            c.s.sd_reward += 10.0f; // COMPLETION_BONUS
+            c.s.sd_level_complete = 1;
+        } else if (t == SP_FLYER || t == SP_FAST_FLYER || t == SP_BULLET2 || t == SP_BULLET3 || t == SP_TURRET ||
+                   t == SP_METEOR) { // is_lethal (:346-350)
+            c.s.sd_done = 1;
+        }
     } else if constexpr (G == PG_GAME_DODGEBALL) { // dodgeball.cpp:102-118
         if (t == DB_ENEMY || t == DB_ENEMY_BALL || t == DB_LAVA_WALL) {
             c.s.sd_done = 1;
@@ -831,8 +840,20 @@ DEV void handle_agent_collision(Ctx &c, int m) {
 //
 // handle_collision(src, target) (basic :383-385 empty; fruitbot.cpp:117-134)
 DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type);
+DEV bool sp_destructible(int t) { return t == SP_FLYER || t == SP_FAST_FLYER || t == SP_TURRET || t == SP_METEOR; }
 template <int G>
 DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_STARPILOT) { // starpilot.cpp:138-145
+        const int tt = EI(c, F_TYPE, ti);
+        if (EI(c, F_TYPE, si) == SP_BULLET_PLAYER && tt != SP_CLOUD && sp_destructible(tt)) {
+            EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+            EF(c, F_HEALTH, ti) = EF(c, F_HEALTH, ti) - 1;
+            const float sx = EF(c, F_X, si), sy = EF(c, F_Y, si), tvx = EF(c, F_VX, ti), tvy = EF(c, F_VY, ti);
+            const float r = (float)(.5 * EF(c, F_RX, si));
+            wave_sync();
+            append_entity(c, sx, sy, tvx, tvy, r, r, EXPLOSION);
+        }
+    }
     if constexpr (G == PG_GAME_PLUNDER) { // plunder.cpp:87-108
         if (EI(c, F_TYPE, si) == PL_PLAYER_BULLET) {
             const int tt = EI(c, F_TYPE, ti);
@@ -1038,7 +1059,7 @@ DEV void flag_reflected(Ctx &c, int slot, bool set) {
 // Entity(x, y, vx, vy, rx, ry, type) appended to `entities` (entity.cpp:8-47)
 DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type) {
     int i = c.s.num_ents;
-    if (i >= PG_CAP) {
+    if (i >= PG_CAP - c.s.num_tail) {
         c.s.error = PG_ERR_ENTITY_OVERFLOW;
         return -1;
     }
@@ -1832,6 +1853,111 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ starpilot (starpilot.cpp:356-430)
+DEV void sp_copy_slot(Ctx &c, int from, int to) {
+    for (int f = LANE; f < PG_NF; f += 64) EI(c, f, to) = EI(c, f, from);
+}
+
+DEV void starpilot_step_tail(Ctx &c, uint32_t *rg) {
+    const int mode = c.s.opt_distribution_mode;
+    const bool gh = c.s.agent_erased;
+    const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+    const bool is_firing = c.s.special_action != 0;
+    // entities that fire (should_fire, :356-366) or blow up, descending; each appends in order
+    const int n0 = c.s.num_ents;
+    int upper = n0;
+    while (upper > 0) {
+        int m = -1;
+        for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+            const int i = base + LANE;
+            bool act = false;
+            if (i < upper) {
+                const int t = EI(c, F_TYPE, i);
+                if (t != PLAYER) {
+                    const int ft = EI(c, F_FIRE_TIME, i), st = EI(c, F_SPAWN_TIME, i);
+                    bool fire = false;
+                    if (ft > 0) fire = t == SP_TURRET ? (c.s.cur_time - st) % ft == 0 : c.s.cur_time - st == ft;
+                    const bool boom = EF(c, F_HEALTH, i) <= 0 && sp_destructible(t) && !(EI(c, F_FLAGS, i) & EF_WILL_ERASE);
+                    act = fire || boom;
+                }
+            }
+            const unsigned long long b = ballot(act);
+            if (b) {
+                m = base + top_bit(b);
+                break;
+            }
+        }
+        if (m < 0) break;
+        upper = m;
+        const int t = EI(c, F_TYPE, m), ft = EI(c, F_FIRE_TIME, m), st = EI(c, F_SPAWN_TIME, m);
+        const float mx = EF(c, F_X, m), my = EF(c, F_Y, m);
+        bool fire = false;
+        if (ft > 0) fire = t == SP_TURRET ? (c.s.cur_time - st) % ft == 0 : c.s.cur_time - st == ft;
+        if (fire) {
+            const int bullet_type = t == SP_TURRET ? SP_BULLET3 : SP_BULLET2;
+            const float bullet_r = sp_hp_bullet_r(mode);
+            float b_vx = ax - mx, b_vy = ay - my;
+            const float bv_scale = (float)(sp_hp_vs(mode, bullet_type) * SP_V_SCALE / sqrt((double)(b_vx * b_vx + b_vy * b_vy)));
+            b_vx = b_vx * bv_scale;
+            b_vy = b_vy * bv_scale;
+            wave_sync();
+            const int b = append_entity(c, mx, my, b_vx, b_vy, bullet_r, bullet_r, bullet_type);
+            if (b >= 0) EF(c, F_ROTATION, b) = face_rotation(b_vx, b_vy, 0.0f, -1 * PI_F / 2);
+            wave_sync();
+        }
+        if (EF(c, F_HEALTH, m) <= 0 && sp_destructible(t) && !(EI(c, F_FLAGS, m) & EF_WILL_ERASE)) {
+            // spawn_child(m, EXPLOSION, .5 * rx, match_vel = true) (basic-abstract-game.cpp:233-239)
+            const float mvx = EF(c, F_VX, m), mvy = EF(c, F_VY, m), cr = (float)(.5 * EF(c, F_RX, m));
+            wave_sync();
+            append_entity(c, mx, my, mvx, mvy, cr, cr, EXPLOSION);
+            c.s.sd_reward += 1.0f; // ENEMY_REWARD
+            EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+            wave_sync();
+        }
+    }
+    // spawners due now move to `entities` (the back of the sorted list = slot PG_CAP - num_tail)
+    while (c.s.num_tail > 0 && c.s.cur_time == EI(c, F_SPAWN_TIME, PG_CAP - c.s.num_tail)) {
+        const int from = PG_CAP - c.s.num_tail;
+        if (c.s.num_ents >= from) {
+            c.s.error = PG_ERR_ENTITY_OVERFLOW;
+            break;
+        }
+        wave_sync();
+        sp_copy_slot(c, from, c.s.num_ents);
+        wave_sync();
+        c.s.num_ents += 1;
+        c.s.num_tail -= 1;
+    }
+    if (is_firing) {
+        const float theta = c.s.special_action == 2 ? PI_F : 0;
+        const float v_scale = sp_hp_vs(mode, SP_BULLET_PLAYER) * SP_V_SCALE;
+        double st, ct;
+        pg_sincos_cr((double)theta, &st, &ct);
+        const float vx = (float)(ct * v_scale), vy = (float)(st * v_scale);
+        const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0);
+        const float x_off = (float)(arx * ct);
+        wave_sync();
+        const int b = append_entity(c, ax + x_off, ay, vx, vy, sp_hp_bullet_r(mode), sp_hp_bullet_r(mode), SP_BULLET_PLAYER);
+        if (b >= 0) {
+            EI(c, F_FLAGS, b) = EF_AUTO_ERASE | EF_COLLIDES;
+            float rot = face_rotation(vx, vy, 0.0f);
+            rot -= PI_F / 2;
+            EF(c, F_ROTATION, b) = rot;
+        }
+        wave_sync();
+    }
+    if (c.s.cur_time == SP_SHOOTER_WIN_TIME) {
+        // Entity(main_width, main_height / 2, -slow_v * V_SCALE, 0, 2, main_height / 2, FINISH_LINE)
+        const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[SP_FINISH_LINE]);
+        const float fry = (float)(c.s.main_height / 2);
+        const float frx = fry * aspect_ratio<PG_GAME_STARPILOT>(c, SP_FINISH_LINE, theme); // match_aspect_ratio(, false)
+        wave_sync();
+        const int f = append_entity(c, c.s.main_width + frx, fry, -1 * SP_HP_SLOW_V * SP_V_SCALE, 0, frx, fry, SP_FINISH_LINE);
+        if (f >= 0) EI(c, F_IMAGE_THEME, f) = theme;
+        wave_sync();
+    }
+}
+
 DEV void fruitbot_step_tail(Ctx &c) { // fruitbot.cpp:247-258
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= FB_KEY_DURATION) {
         const bool gh = c.s.agent_erased;
@@ -1912,6 +2038,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_FRUITBOT) fruitbot_step_tail(c);
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_step_tail(c, rg);
     if constexpr (G == PG_GAME_PLUNDER) plunder_step_tail(c, rg);
+    if constexpr (G == PG_GAME_STARPILOT) starpilot_step_tail(c, rg);
     wave_sync();
     c.pt.mark(5);
 }
@@ -2014,6 +2141,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_FRUITBOT) { PG_W(last_fire_time) }
         if constexpr (G == PG_GAME_DODGEBALL) { PG_W(last_fire_time) PG_W(num_enemies) }
         if constexpr (G == PG_GAME_PLUNDER) { PG_W(last_fire_time) PG_W(gs) }
+        if constexpr (G == PG_GAME_STARPILOT) { PG_W(num_tail) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -2041,6 +2169,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_FRUITBOT)
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
+        PG_CASE(PG_GAME_STARPILOT)
     default: break;
     }
 #undef PG_CASE

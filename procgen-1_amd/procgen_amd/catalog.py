@@ -244,6 +244,24 @@ PLUNDER_SPRITES = {
     3: ["misc_assets/target_red2.png"],
 }
 
+# ---------------------------------------------------------------- starpilot
+# procgen/src/games/starpilot.cpp:60-104 (BULLET_PLAYER 1, BULLET2 2, BULLET3 3, FLYER 4, METEOR 5,
+# CLOUD 6, TURRET 7, FAST_FLYER 8, FINISH_LINE 9)
+_SP_SHIPS = ["misc_assets/spaceShips_%03d.png" % i for i in range(1, 8)]
+STARPILOT_SPRITES = {
+    0: ["misc_assets/playerShip2_blue.png"],
+    1: ["misc_assets/towerDefense_tile295.png"],
+    2: ["misc_assets/towerDefense_tile296.png"],
+    3: ["misc_assets/towerDefense_tile297.png"],
+    4: _SP_SHIPS,
+    8: _SP_SHIPS,
+    5: ["misc_assets/spaceMeteors_%03d.png" % i for i in range(1, 5)] +
+       ["misc_assets/meteorGrey_big%d.png" % i for i in range(1, 5)],
+    6: ["misc_assets/spaceEffect%d.png" % i for i in range(1, 10)],
+    7: ["misc_assets/spaceStation_018.png", "misc_assets/spaceStation_019.png"],
+    9: ["misc_assets/spaceRockets_%03d.png" % i for i in range(1, 5)],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -257,6 +275,7 @@ GAMES = {
     "fruitbot": (FRUITBOT_SPRITES, "topdown"),  # fruitbot.cpp:42-44
     "dodgeball": (DODGEBALL_SPRITES, "topdown"),  # dodgeball.cpp:46-48
     "plunder": (PLUNDER_SPRITES, "water_surface"),  # plunder.cpp:45-47
+    "starpilot": (STARPILOT_SPRITES, "space"),  # starpilot.cpp:56-58
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -58,6 +58,7 @@ def load():
         lib.oracle_latent.argtypes = [ctypes.c_void_p] * 5
         lib.oracle_bigfish_radius.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         lib.oracle_qt_rotation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        lib.oracle_spawn_sort.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.oracle_face_rotation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         _LIB = lib
     return _LIB

@@ -65,8 +65,8 @@ def test_missing_start_level_rejected():
 
 
 def test_unsupported_game_rejected():
-    h, msg = make(dict(BASE, env_name="starpilot"))
-    assert not h and "starpilot" in msg
+    h, msg = make(dict(BASE, env_name="notagame"))  # vecgame.cpp: unknown names fatal
+    assert not h and "notagame" in msg
 
 
 def test_invalid_distribution_mode_rejected():

@@ -65,7 +65,8 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
-GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder"]
+GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder",
+         "starpilot"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -138,6 +139,15 @@ def test_plunder_long():
     explosions, juice runs out (~670 steps without hits), juice / progress bars (fillRect(QRectF))."""
     episodes, _ = run_pair("plunder", 16, 900, seed=21, num_levels=0, rand_seed=10)
     assert episodes > 0
+
+
+def test_starpilot_long_and_extreme():
+    """starpilot: the spawner list (std::sort order among equal spawn times, popped as cur_time
+    reaches them), aimed enemy bullets (sqrt, face_direction through glibc's atan2f), player shots
+    both ways (sin / cos of PI), explosions, the finish line at t = 500, the scrolling tiled space
+    background; extreme mode (more health, smaller bullets)."""
+    run_pair("starpilot", 32, 650, seed=22, num_levels=0, rand_seed=11)
+    run_pair("starpilot", 8, 300, seed=23, num_levels=0, rand_seed=12, distribution_mode="extreme")
 
 
 def test_bigfish_long_episodes():

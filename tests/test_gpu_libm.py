@@ -90,15 +90,16 @@ def test_qt_rotation_matrix_matches_c_library():
 
 
 def test_face_rotation_matches_c_library():
-    """Entity::face_direction = -atan2f(dy, dx) (entity.cpp:84-88): exact for the axis and diagonal
-    directions the integer-action games face."""
+    """Entity::face_direction = -atan2f(dy, dx) (entity.cpp:84-88): the device runs the restated glibc
+    atan2f (pg_libm.h), bit-identical for any direction."""
     import torch
     vals = np.array([-1, 0, 1, -0.05, 0.05, -0.075, 0.075, 2.5, -3.0, -0.0], np.float32)
-    dxy = np.array([(a, b) for a in vals for b in vals if a != 0 or b != 0], np.float32).reshape(-1)
+    rng = np.random.RandomState(5)
+    dxy = np.concatenate([np.array([(a, b) for a in vals for b in vals if a != 0 or b != 0], np.float32).reshape(-1),
+                          rng.uniform(-20, 20, 2_000_000).astype(np.float32)])
     ref = np.empty(dxy.size // 2, np.float32)
     oracle_lib.load().oracle_face_rotation(dxy.ctypes.data, ref.ctypes.data, ref.size)
     got = _device(2, dxy, ref.size, torch.float32)
     pairs = dxy.reshape(-1, 2)
-    exact = (pairs[:, 0] == 0) | (pairs[:, 1] == 0) | (np.abs(pairs[:, 0]) == np.abs(pairs[:, 1]))
-    bad = np.nonzero((got.view(np.uint32) != ref.view(np.uint32)) & exact)[0]
+    bad = np.nonzero(got.view(np.uint32) != ref.view(np.uint32))[0]
     assert bad.size == 0, "face_direction differs for %r: %r vs %r" % (pairs[bad[:4]], got[bad[:4]], ref[bad[:4]])

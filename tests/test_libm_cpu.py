@@ -1,7 +1,7 @@
-"""CPU pin of the engine's double sin / cos (procgen-1_amd/csrc/pg_sincos.h, the same source the
-HIP kernels compile): correctly rounded against 200-bit mpmath, and within 1 ulp of glibc (what
-the reference links) with the disagreement rate bounded.  The .so built here is test
-infrastructure (gcc, host), never the product."""
+"""CPU pins of the engine's C-library math (procgen-1_amd/csrc/pg_libm.h, the same source the HIP
+kernels compile): atan2f bit-identical to glibc's (what the reference links); double sin / cos
+correctly rounded against 200-bit mpmath and within 1 ulp of glibc with the disagreement rate
+bounded.  The .so built here is test infrastructure (gcc, host), never the product."""
 import ctypes
 import os
 import subprocess
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDR = os.path.join(REPO, "procgen-1_amd", "csrc", "pg_sincos.h")
+HDR = os.path.join(REPO, "procgen-1_amd", "csrc", "pg_libm.h")
 
 
 @pytest.fixture(scope="module")
@@ -21,12 +21,16 @@ def lib(tmp_path_factory):
                    "void run(const double *x, double *s, double *c, int64_t n) {"
                    " for (int64_t i = 0; i < n; i++) pg_sincos_cr(x[i], &s[i], &c[i]); }\n"
                    "void glibc(const double *x, double *s, double *c, int64_t n) {"
-                   " for (int64_t i = 0; i < n; i++) { s[i] = sin(x[i]); c[i] = cos(x[i]); } }\n" % HDR)
+                   " for (int64_t i = 0; i < n; i++) { s[i] = sin(x[i]); c[i] = cos(x[i]); } }\n"
+                   "void a2(const float *y, const float *x, float *o, int64_t n) {"
+                   " for (int64_t i = 0; i < n; i++) o[i] = pg_atan2f(y[i], x[i]); }\n"
+                   "void a2g(const float *y, const float *x, float *o, int64_t n) {"
+                   " for (int64_t i = 0; i < n; i++) o[i] = atan2f(y[i], x[i]); }\n" % HDR)
     so = d / "s.so"
     subprocess.run(["gcc", "-O2", "-march=x86-64", "-ffp-contract=off", "-fPIC", "-shared", "-o", str(so), str(src),
                     "-lm"], check=True)
     L = ctypes.CDLL(str(so))
-    for f in (L.run, L.glibc):
+    for f in (L.run, L.glibc, L.a2, L.a2g):
         f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64]
     return L
 
@@ -62,3 +66,21 @@ def test_glibc_agreement(lib):
         ulps = np.abs(a.view(np.int64) - b.view(np.int64))
         assert ulps.max() <= 1
         assert np.count_nonzero(ulps) / ulps.size < 5e-3
+
+
+def test_atan2f_bit_identical_to_glibc(lib):
+    rng = np.random.RandomState(2)
+    n = 4_000_000
+    y = (rng.uniform(-30, 30, n) * np.where(rng.rand(n) < 0.3, 1e-3, 1)).astype(np.float32)
+    x = rng.uniform(-30, 30, n).astype(np.float32)
+    special = np.array([0.0, -0.0, 1.0, -1.0, 0.05, -0.05, 3.0, -2.5, 1e-30, -1e-30, 1e30, -1e30, 0.8, -0.8,
+                        -6.99e-8], np.float32)
+    yy, xx = np.meshgrid(special, special)
+    y = np.concatenate([y, yy.ravel()])
+    x = np.concatenate([x, xx.ravel(), ])
+    a = np.empty_like(y)
+    g = np.empty_like(y)
+    lib.a2(y.ctypes.data, x.ctypes.data, a.ctypes.data, y.size)
+    lib.a2g(y.ctypes.data, x.ctypes.data, g.ctypes.data, y.size)
+    bad = np.nonzero(a.view(np.uint32) != g.view(np.uint32))[0]
+    assert bad.size == 0, (y[bad[:4]], x[bad[:4]], a[bad[:4]], g[bad[:4]])

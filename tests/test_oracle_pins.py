@@ -272,3 +272,47 @@ def test_qt_raster_fill_goldens():
         if not np.array_equal(canvas, cout[i]):
             bad.append(i)
     assert not bad, "Qt fillRect mismatch in %d cases, first %s" % (len(bad), bad[:10])
+
+
+def test_spawner_sort_vs_libstdcxx(tmp_path):
+    """starpilot sorts its spawners with std::sort(spawn_cmp) (starpilot.cpp:28-30, 340); equal spawn
+    times are common, so the order among them is libstdc++'s introsort's.  The oracle's restatement
+    must leave the same permutation as the real std::sort of this toolchain (g++ / libstdc++, what
+    the reference builds with)."""
+    import subprocess
+    src = tmp_path / "s.cpp"
+    src.write_text(
+        "#include <algorithm>\n#include <vector>\n#include <cstdint>\n"
+        "struct E { int t, i; };\n"
+        "extern \"C\" void cxx_sort(const int32_t *key, int32_t *idx, int n) {\n"
+        "  std::vector<E> v; for (int i = 0; i < n; i++) v.push_back({key[i], i});\n"
+        "  std::sort(v.begin(), v.end(), [](const E &x, const E &y) { return x.t > y.t; });\n"
+        "  for (int i = 0; i < n; i++) idx[i] = v[i].i; }\n")
+    so = tmp_path / "s.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", str(so), str(src)], check=True)
+    cxx = ctypes.CDLL(str(so))
+    cxx.cxx_sort.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib = oracle_lib.load()
+    rng = np.random.RandomState(0)
+    for trial in range(3000):
+        n = int(rng.choice([0, 1, 2, 5, 16, 17, 33, 64, 100, 200, 300]))
+        kind = trial % 4
+        if kind == 0:
+            key = rng.randint(0, 20, n)
+        elif kind == 1:
+            key = np.sort(rng.randint(0, 500, n))
+        elif kind == 2:
+            key = np.sort(rng.randint(0, 500, n))[::-1]
+        else:  # starpilot-like: groups t + 5j with t increasing by 10..30
+            ts, t = [], 1 + rng.randint(10, 30)
+            while len(ts) < n:
+                for j in range(rng.randint(0, 5) + 1):
+                    ts.append(t + 5 * j)
+                t += rng.randint(10, 30)
+            key = np.array(ts[:n])
+        key = np.ascontiguousarray(key, dtype=np.int32)
+        a = np.zeros(n, np.int32)
+        b = np.zeros(n, np.int32)
+        lib.oracle_spawn_sort(key.ctypes.data, a.ctypes.data, n)
+        cxx.cxx_sort(key.ctypes.data, b.ctypes.data, n)
+        np.testing.assert_array_equal(a, b, err_msg="trial %d n %d kind %d" % (trial, n, kind))
