@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
 
 static void fatal_msg(const char *m) {
@@ -255,6 +255,15 @@ typedef struct {
     float sp_hp_vs[9], sp_hp_healths[9], sp_hp_bullet_r[9], sp_hp_object_r[9], sp_hp_prob[9];
     float sp_total_prob_weight, sp_hp_slow_v, sp_hp_weapon_bullet_dist, sp_hp_spawn_right_threshold;
     int sp_hp_min_enemy_delta_t, sp_hp_max_group_size, sp_hp_max_enemy_delta_t;
+    /* bossfight (bossfight.cpp:34-58); boss / shields are entities 1 and 2 of the list */
+    int bf_attack_modes[8], bf_num_attack_modes;
+    int bf_time_to_swap, bf_invulnerable_duration, bf_vulnerable_duration, bf_num_rounds, bf_round_num,
+        bf_round_health, bf_boss_vel_timeout, bf_curr_vel_timeout, bf_attack_mode, bf_player_laser_theme,
+        bf_boss_laser_theme, bf_damaged_until_time;
+    bool bf_shields_are_up, bf_barriers_moves_right;
+    float bf_base_fire_prob, bf_boss_bullet_vel, bf_barrier_vel, bf_barrier_spawn_prob, bf_rand_pct, bf_rand_fire_pct,
+        bf_rand_pct_x, bf_rand_pct_y;
+    Entity *bf_boss, *bf_shields;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -436,12 +445,72 @@ static bool hook_will_reflect(Game *g, int src, int target) {
 }
 
 /* handle_collision(src, target) (basic :383-385 is empty) */
+static void bf_prepare_boss(Game *g);
 static int spawn_child(Game *g, int src_i, int type, float obj_r) { /* basic-abstract-game.cpp:233-239, match_vel false */
     Entity *src = &g->ents[src_i];
     return add_entity(g, src->x, src->y, 0, 0, obj_r, type);
 }
 static void hook_handle_collision(Game *g, int si, int ti) {
     Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_BOSSFIGHT) { /* bossfight.cpp:140-190 */
+        if (src->type == 1) { /* PLAYER_BULLET */
+            bool will_erase = false;
+            if (target->type == 3) { /* SHIELDS */
+                if (g->bf_shields_are_up) {
+                    src->type = 6; /* REFLECTED_BULLET */
+                    float theta = (float)(PI_F * (1.25 + .5 * g->bf_rand_pct));
+                    src->vy = (float)(1 * sin((double)theta) * .5); /* PLAYER_BULLET_VEL (const int 1) */
+                    src->vx = (float)(1 * cos((double)theta) * .5);
+                    src->expire_time = 4;
+                    src->life_time = 0;
+                    src->alpha_decay = 0.8f;
+                }
+            } else if (target->type == 2) { /* BOSS */
+                if (!g->bf_shields_are_up) {
+                    target->health -= 1;
+                    will_erase = true;
+                    if ((int)target->health % g->bf_round_health == 0) {
+                        g->sd_reward += 1; /* POSITIVE_REWARD (const int) */
+                        if (target->health == 0) {
+                            g->sd_done = true;
+                            g->sd_reward += 10; /* COMPLETION_BONUS (const int) */
+                            g->sd_level_complete = true;
+                        } else {
+                            g->bf_round_num++;
+                            bf_prepare_boss(g);
+                            g->bf_curr_vel_timeout = 40; /* BOSS_DAMAGED_TIMEOUT */
+                            g->bf_damaged_until_time = g->cur_time + 40;
+                        }
+                    }
+                }
+            }
+            if (will_erase && !src->will_erase) {
+                src->will_erase = true;
+                float tvx = target->vx, tvy = target->vy;
+                int e = spawn_child(g, si, EXPLOSION, (float)(.5 * src->rx));
+                g->ents[e].vx = tvx;
+                g->ents[e].vy = tvy;
+            }
+        } else if (src->type == 7) { /* BARRIER */
+            if (target->type == 4 || target->type == 1) { /* ENEMY_BULLET, PLAYER_BULLET */
+                target->will_erase = true;
+                spawn_child(g, ti, EXPLOSION, (float)(.5 * target->rx));
+            } else if (target->type == 5) { /* LASER_TRAIL */
+                target->will_erase = true;
+            }
+            src = &g->ents[si];
+            if (src->health <= 0) {
+                if (!src->will_erase) {
+                    float svx = src->vx, svy = src->vy;
+                    int e = spawn_child(g, si, EXPLOSION, (float)(.5 * src->rx));
+                    g->ents[e].vx = svx;
+                    g->ents[e].vy = svy;
+                }
+                g->ents[si].will_erase = true;
+            }
+        }
+        return;
+    }
     if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:138-145: BULLET_PLAYER 1 vs destructible non-CLOUD */
         int tt = target->type;
         bool destructible = tt == 4 || tt == 8 || tt == 7 || tt == 5; /* FLYER, FAST_FLYER, TURRET, METEOR */
@@ -536,6 +605,8 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 g->fish_eaten += 1;
             }
         }
+    } else if (g->game_id == GAME_BOSSFIGHT) { /* bossfight.cpp:120-131: BOSS, BARRIER, ENEMY_BULLET */
+        if (obj->type == 2 || obj->type == 7 || obj->type == 4) g->sd_done = true;
     } else if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:126-136 */
         int t = obj->type;
         if (t == 9) { /* FINISH_LINE */
@@ -633,6 +704,7 @@ static int mask_theme(Game *g, int theme, int type) {
 
 /* should_draw_entity (basic-abstract-game.cpp:1052-1054, heist.cpp:73-78) */
 static bool hook_should_draw_entity(Game *g, const Entity *e) {
+    if (g->game_id == GAME_BOSSFIGHT && e->type == 3) return g->bf_shields_are_up; /* bossfight.cpp:133-138 */
     if (g->game_id == GAME_HEIST && e->type == HS_KEY_ON_RING) return g->has_keys[e->image_theme];
     return true;
 }
@@ -3038,6 +3110,189 @@ static void starpilot_game_step(Game *g, const or_atlas *at) { /* :368-430 */
     }
 }
 
+/* ================================================================== bossfight (games/bossfight.cpp) */
+#define BF_PLAYER_BULLET 1
+#define BF_BOSS 2
+#define BF_SHIELDS 3
+#define BF_ENEMY_BULLET 4
+#define BF_LASER_TRAIL 5
+#define BF_BARRIER 7
+static const float BF_BOSS_R = 3;
+#define BF_BOTTOM_MARGIN 6
+
+static void bf_prepare_boss(Game *g) { /* :192-199 */
+    g->bf_shields_are_up = true;
+    g->bf_curr_vel_timeout = g->bf_boss_vel_timeout;
+    g->bf_time_to_swap = g->bf_invulnerable_duration;
+    g->bf_attack_mode = g->bf_attack_modes[g->bf_round_num % g->bf_num_attack_modes];
+    g->bf_boss->vx = 0;
+    g->bf_boss->vy = 0;
+}
+
+static void bf_spawn_barriers(Game *g, const or_atlas *at) { /* :310-329 */
+    MT *r = &g->rand_gen;
+    int num_barriers = rg_randn(r, 3) + 1;
+    for (int i = 0; i < num_barriers; i++) {
+        float barrier_r = 0.6f;
+        float min_barrier_y = (float)(2 * AG(g)->ry + barrier_r + .5);
+        float ent_y = rg_rand01(r) * (BF_BOTTOM_MARGIN - min_barrier_y - barrier_r) + min_barrier_y;
+        float ent_x = rg_rand01(r) * (g->main_width - 2 * barrier_r) + barrier_r;
+        Entity ent;
+        entity_init(&ent, ent_x, ent_y, 0, 0, barrier_r, barrier_r, BF_BARRIER);
+        choose_random_theme(g, &ent, at);
+        match_aspect_ratio(g, at, &ent);
+        ent.health = 3;
+        ent.collides_with_entities = true;
+        if (!has_any_collision(g, &ent, 0)) {
+            fassert(g->num_ents < MAX_ENTS);
+            g->ents[g->num_ents++] = ent;
+        }
+    }
+}
+
+static void bossfight_game_reset(Game *g, const or_atlas *at) { /* :201-250 */
+    MT *r = &g->rand_gen;
+    basic_game_reset(g, at);
+    g->bf_damaged_until_time = 0;
+    g->last_fire_time = 0;
+    g->bf_boss_bullet_vel = (float)(g->options.distribution_mode == EasyMode ? .5 : .75);
+    int max_extra_invulnerable = g->options.distribution_mode == EasyMode ? 1 : 3;
+    g->options.center_agent = false;
+    int b = add_entity(g, (float)(g->main_width / 2), (float)(g->main_height / 2), 0, 0, BF_BOSS_R, BF_BOSS);
+    choose_random_theme(g, &g->ents[b], at);
+    match_aspect_ratio(g, at, &g->ents[b]);
+    Entity *boss = &g->ents[b];
+    add_entity_rxy(g, boss->x, boss->y, 0, 0, (float)(1.2 * boss->rx), (float)(1.2 * boss->ry), BF_SHIELDS);
+    fassert(b == 1);
+    g->bf_boss = &g->ents[1];
+    g->bf_shields = &g->ents[2];
+    g->bf_boss_vel_timeout = 20; /* BOSS_VEL_TIMEOUT */
+    g->bf_base_fire_prob = 0.1f;
+    g->bf_round_health = rg_randn(r, 9) + 1;
+    g->bf_num_rounds = 1 + rg_randn(r, 5);
+    g->bf_invulnerable_duration = 2 + rg_randn(r, max_extra_invulnerable + 1);
+    g->bf_vulnerable_duration = 500;
+    g->bf_boss->health = (float)(g->bf_round_health * g->bf_num_rounds);
+    choose_random_theme(g, AG(g), at);
+    g->bf_player_laser_theme = rg_randn(r, 3); /* NUM_LASER_THEMES */
+    g->bf_boss_laser_theme = rg_randn(r, 3);
+    g->bf_num_attack_modes = 0;
+    for (int i = 0; i < g->bf_num_rounds; i++) g->bf_attack_modes[g->bf_num_attack_modes++] = rg_randn(r, 4);
+    g->bf_round_num = 0;
+    bf_prepare_boss(g);
+    Entity *agent = AG(g);
+    agent->rx = .75;
+    match_aspect_ratio(g, at, agent);
+    reposition_agent(g);
+    agent->y = agent->ry;
+    g->bf_barrier_vel = 0.1f;
+    g->bf_barriers_moves_right = rg_randbool(r);
+    g->bf_barrier_spawn_prob = 0.025f;
+    bf_spawn_barriers(g, at);
+}
+
+static void bf_boss_fire(Game *g, float bullet_r, float vel, float theta) { /* :252-257 */
+    Entity *boss = g->bf_boss;
+    float bx = boss->x, by = boss->y;
+    int e = add_entity(g, bx, by, (float)(vel * cos((double)theta)), (float)(vel * sin((double)theta)), bullet_r,
+                       BF_ENEMY_BULLET);
+    g->ents[e].image_theme = g->bf_boss_laser_theme;
+    g->ents[e].expire_time = 50;
+    g->ents[e].vrot = PI_F / 8;
+}
+
+static void bossfight_game_step(Game *g) { /* :331-392 */
+    MT *r = &g->rand_gen;
+    basic_game_step(g);
+    /* erase_if_needed may have moved the boss / shields down one slot (only the agent can go) */
+    for (int i = 0; i < g->num_ents; i++) {
+        if (g->ents[i].type == BF_BOSS) g->bf_boss = &g->ents[i];
+        if (g->ents[i].type == BF_SHIELDS) g->bf_shields = &g->ents[i];
+    }
+    Entity *boss = g->bf_boss;
+    g->bf_shields->x = boss->x;
+    g->bf_shields->y = boss->y;
+    g->bf_rand_pct = rg_rand01(r);
+    g->bf_rand_fire_pct = rg_rand01(r);
+    g->bf_rand_pct_x = rg_rand01(r);
+    g->bf_rand_pct_y = rg_rand01(r);
+    if (g->bf_curr_vel_timeout <= 0) {
+        float dest_x = g->bf_rand_pct_x * (g->main_width - 2 * BF_BOSS_R) + BF_BOSS_R;
+        float dest_y = g->bf_rand_pct_y * (g->main_height - 2 * BF_BOSS_R - BF_BOTTOM_MARGIN) + BF_BOSS_R + BF_BOTTOM_MARGIN;
+        boss->vx = (dest_x - boss->x) / g->bf_boss_vel_timeout;
+        boss->vy = (dest_y - boss->y) / g->bf_boss_vel_timeout;
+        g->bf_curr_vel_timeout = g->bf_boss_vel_timeout;
+        if (g->bf_time_to_swap > 0) {
+            g->bf_time_to_swap -= 1;
+        } else {
+            g->bf_time_to_swap = g->bf_shields_are_up ? g->bf_vulnerable_duration : g->bf_invulnerable_duration;
+            g->bf_shields_are_up = !g->bf_shields_are_up;
+        }
+    } else {
+        g->bf_curr_vel_timeout -= 1;
+    }
+    if (g->special_action == 1 && (g->cur_time - g->last_fire_time) >= 3) {
+        Entity *agent = AG(g);
+        int e = add_entity(g, agent->x, agent->y, 0, 1, .25, BF_PLAYER_BULLET);
+        g->ents[e].image_theme = g->bf_player_laser_theme;
+        g->ents[e].collides_with_entities = true;
+        g->ents[e].expire_time = 25;
+        g->last_fire_time = g->cur_time;
+    }
+    int ct = g->cur_time;
+    float bv = g->bf_boss_bullet_vel, rp = g->bf_rand_pct;
+    if (g->bf_damaged_until_time >= ct) { /* damaged_mode (:299-305) */
+        if (ct % 3 == 0) {
+            boss = g->bf_boss;
+            float pos_x = boss->x + (2 * g->bf_rand_pct_x - 1) * boss->rx;
+            float pos_y = boss->y + (2 * g->bf_rand_pct_y - 1) * boss->ry;
+            add_entity(g, pos_x, pos_y, 0, 0, .75, EXPLOSION);
+        }
+    } else if (g->bf_shields_are_up) { /* active_attack (:307-317) */
+        int am = g->bf_attack_mode;
+        if (am == 0) { /* :265-271 */
+            if (ct % 8 == 0)
+                for (int i = 0; i < 5; i++) bf_boss_fire(g, .5, bv, (float)(PI_F * 1.5 + (i - 2) * PI_F / 8));
+        } else if (am == 1) { /* :273-282 */
+            int dt = 5;
+            if (ct % dt == 0) {
+                int k = ct / dt;
+                k = abs(8 - (k % 16));
+                for (int i = 0; i < 4; i++) bf_boss_fire(g, .5, bv, (float)(PI_F * (1.25 + .5 * k / 8.0) + i * PI_F / 2));
+            }
+        } else if (am == 2) { /* :284-293 */
+            if (ct % 10 == 0) {
+                int num_bullets = 8;
+                float offset = rp * 2 * PI_F;
+                for (int i = 0; i < num_bullets; i++) {
+                    float theta = 2 * PI_F / num_bullets * i + offset;
+                    bf_boss_fire(g, .5, bv, theta);
+                }
+            }
+        } else if (am == 3) { /* :295-299 */
+            if (ct % 4 == 0) bf_boss_fire(g, .5, bv, PI_F * (1 + rp));
+        }
+    } else { /* passive_attack_mode (:259-263) */
+        if (g->bf_rand_fire_pct < g->bf_base_fire_prob) bf_boss_fire(g, .5, bv, PI_F * (1 + rp));
+    }
+    for (int i = g->num_ents - 1; i >= 0; i--) {
+        Entity *ent = &g->ents[i];
+        if (ent->type == BF_ENEMY_BULLET) {
+            float v_trail = .5;
+            float ex = ent->x, ey = ent->y, evx = ent->vx * v_trail, evy = ent->vy * v_trail, erx = ent->rx, ery = ent->ry;
+            float evrot = ent->vrot, erot = ent->rotation;
+            int t = add_entity_rxy(g, ex, ey, evx, evy, erx, ery, BF_LASER_TRAIL);
+            Entity *tr = &g->ents[t];
+            tr->alpha_decay = 0.7f;
+            tr->image_type = BF_ENEMY_BULLET;
+            tr->image_theme = g->bf_boss_laser_theme;
+            tr->vrot = evrot;
+            tr->rotation = erot;
+            tr->expire_time = 8;
+        }
+    }
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -3189,6 +3444,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_reset(g, at);
     else if (g->game_id == GAME_PLUNDER) plunder_game_reset(g, at);
     else if (g->game_id == GAME_STARPILOT) starpilot_game_reset(g, at);
+    else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -3204,6 +3460,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_DODGEBALL) dodgeball_game_step(g);
     else if (g->game_id == GAME_PLUNDER) plunder_game_step(g, at);
     else if (g->game_id == GAME_STARPILOT) starpilot_game_step(g, at);
+    else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -3841,6 +4098,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "dodgeball") == 0) return GAME_DODGEBALL;
     if (strcmp(name, "plunder") == 0) return GAME_PLUNDER;
     if (strcmp(name, "starpilot") == 0) return GAME_STARPILOT;
+    if (strcmp(name, "bossfight") == 0) return GAME_BOSSFIGHT;
     return -1;
 }
 
@@ -3894,6 +4152,13 @@ static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
     g->maxspeed = 0.85f;
     g->bg_tile_ratio = -1;
     g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
+}
+static void bossfight_ctor(Game *g) { /* bossfight.cpp:60-68 */
+    g->timeout = 4000;
+    g->main_width = 20;
+    g->main_height = 20;
+    g->mixrate = .5;
+    g->maxspeed = 0.85f;
 }
 static void starpilot_ctor(Game *g) { /* starpilot.cpp:50-54 */
     g->main_width = 16;
@@ -3989,6 +4254,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_DODGEBALL) dodgeball_ctor(g);
         else if (gid == GAME_PLUNDER) plunder_ctor(g);
         else if (gid == GAME_STARPILOT) starpilot_ctor(g);
+        else if (gid == GAME_BOSSFIGHT) bossfight_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

@@ -119,9 +119,10 @@ int game_id(const std::string &name) {
     if (name == "dodgeball") return PG_GAME_DODGEBALL;
     if (name == "plunder") return PG_GAME_PLUNDER;
     if (name == "starpilot") return PG_GAME_STARPILOT;
+    if (name == "bossfight") return PG_GAME_BOSSFIGHT;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder, starpilot";
+const char *SUPPORTED_GAMES = "bigfish, bossfight, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder, starpilot";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -181,6 +182,12 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_BOSSFIGHT) { // bossfight.cpp:60-68
+        s.timeout = 4000;
+        s.main_width = 20;
+        s.main_height = 20;
+        s.mixrate = .5;
+        s.maxspeed = 0.85f;
     } else if (gid == PG_GAME_STARPILOT) { // starpilot.cpp:50-54
         s.main_width = 16;
         s.main_height = 16;

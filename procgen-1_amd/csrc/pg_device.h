@@ -153,6 +153,18 @@ DEV float sp_hp_prob(int mode, int type) {
     return 1;
 }
 #define SP_HP_SLOW_V .5f
+// bossfight.cpp:8-30
+#define BF_PLAYER_BULLET 1
+#define BF_BOSS 2
+#define BF_SHIELDS 3
+#define BF_ENEMY_BULLET 4
+#define BF_LASER_TRAIL 5
+#define BF_REFLECTED_BULLET 6
+#define BF_BARRIER 7
+#define BF_BOSS_R 3.0f
+#define BF_BOTTOM_MARGIN 6
+#define BF_BOSS_VEL_TIMEOUT 20
+#define BF_BOSS_DAMAGED_TIMEOUT 40
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3

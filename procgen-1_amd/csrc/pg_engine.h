@@ -22,7 +22,7 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_BIGFISH = 0, PG_GAME_BOSSFIGHT = 1, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
     PG_GAME_MINER = 12, PG_GAME_PLUNDER = 14, PG_GAME_STARPILOT = 15
 };
 #ifndef PG_NUM_GAMES
@@ -185,6 +185,13 @@ struct PGEnv {
             int32_t num_lanes, num_current_ship_types, targets_hit, target_quota;
             float juice_left, r_scale, spawn_prob, legend_r, min_agent_x;
         } pl;
+        struct { // bossfight (bossfight.cpp:34-58; the constant members are literals in the kernels)
+            uint32_t attack_modes;  // attack_modes[i] in bits 2i..2i+1 (num_rounds <= 5)
+            int32_t time_to_swap, invulnerable_duration, num_rounds, round_num, round_health, curr_vel_timeout;
+            int32_t attack_mode, player_laser_theme, boss_laser_theme, damaged_until_time, shields_are_up;
+            int32_t barriers_moves_right;
+            float boss_bullet_vel, rand_pct, rand_fire_pct, rand_pct_x, rand_pct_y;
+        } bf;
         int32_t words[20];
     } gs;
     // entity slots reserved at the top of the planes, [PG_CAP - num_tail, PG_CAP): starpilot's

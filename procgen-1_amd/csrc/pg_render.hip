@@ -142,6 +142,8 @@ DEV int mask_theme(const PGEnv &s, int theme, int img_type) { // mask_theme_if_n
 }
 template <int G>
 DEV bool should_draw(const PGEnv &s, int type, int theme) { // should_draw_entity (heist.cpp:73-78)
+    if constexpr (G == PG_GAME_BOSSFIGHT) // bossfight.cpp:133-138
+        if (type == BF_SHIELDS) return s.gs.bf.shields_are_up != 0;
     if constexpr (G == PG_GAME_HEIST)
         if (type == HS_KEY_ON_RING) return (s.has_keys >> theme) & 1;
     return true;
@@ -1124,6 +1126,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
+        PG_CASE(PG_GAME_BOSSFIGHT)
     default: break;
     }
 #undef PG_CASE

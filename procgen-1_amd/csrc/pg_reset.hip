@@ -1572,6 +1572,71 @@ DEV void starpilot_game_reset(RCtx &c, SpawnerScratch *S) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ bossfight (bossfight.cpp:192-250, 310-329)
+DEV void bf_prepare_boss(RCtx &c, int boss) { // :192-199
+    auto &B = c.s.gs.bf;
+    B.shields_are_up = 1;
+    B.curr_vel_timeout = BF_BOSS_VEL_TIMEOUT;
+    B.time_to_swap = B.invulnerable_duration;
+    B.attack_mode = (int)((B.attack_modes >> (2 * (B.round_num % B.num_rounds))) & 3u);
+    EF(c, F_VX, boss) = 0;
+    EF(c, F_VY, boss) = 0;
+}
+
+DEV void bossfight_game_reset(RCtx &c) {
+    base_game_reset<PG_GAME_BOSSFIGHT>(c);
+    auto &B = c.s.gs.bf;
+    B.damaged_until_time = 0;
+    c.s.last_fire_time = 0;
+    B.boss_bullet_vel = (float)(c.s.opt_distribution_mode == PG_EASY ? .5 : .75);
+    const int max_extra_invulnerable = c.s.opt_distribution_mode == PG_EASY ? 1 : 3;
+    c.s.opt_center_agent = 0;
+    const int boss = add_entity(c, (float)(c.s.main_width / 2), (float)(c.s.main_height / 2), 0, 0, BF_BOSS_R, BF_BOSS);
+    choose_random_theme(c, boss);
+    match_aspect_ratio<PG_GAME_BOSSFIGHT>(c, boss);
+    add_entity_rxy(c, EF(c, F_X, boss), EF(c, F_Y, boss), 0, 0, (float)(1.2 * EF(c, F_RX, boss)),
+                   (float)(1.2 * EF(c, F_RY, boss)), BF_SHIELDS);
+    B.round_health = randn(c, 9) + 1;
+    B.num_rounds = 1 + randn(c, 5);
+    B.invulnerable_duration = 2 + randn(c, max_extra_invulnerable + 1);
+    EF(c, F_HEALTH, boss) = (float)(B.round_health * B.num_rounds);
+    EI(c, F_IMAGE_THEME, 0) = randn(c, c.d.num_themes[PLAYER]); // choose_random_theme(agent)
+    B.player_laser_theme = randn(c, 3); // NUM_LASER_THEMES
+    B.boss_laser_theme = randn(c, 3);
+    B.attack_modes = 0;
+    for (int i = 0; i < B.num_rounds; i++) B.attack_modes |= (uint32_t)randn(c, 4) << (2 * i);
+    B.round_num = 0;
+    bf_prepare_boss(c, boss);
+    EF(c, F_RX, 0) = .75;
+    match_aspect_ratio<PG_GAME_BOSSFIGHT>(c, 0);
+    wave_sync();
+    reposition_agent(c);
+    EF(c, F_Y, 0) = EF(c, F_RY, 0);
+    B.barriers_moves_right = (double)rand01(c) > .5; // randbool (randgen.cpp:25-27)
+    wave_sync();
+    // spawn_barriers (:310-329)
+    const int num_barriers = randn(c, 3) + 1;
+    for (int i = 0; i < num_barriers; i++) {
+        const float barrier_r = 0.6f;
+        const float min_barrier_y = (float)(2 * EF(c, F_RY, 0) + barrier_r + .5);
+        const float ent_y = rand01(c) * (BF_BOTTOM_MARGIN - min_barrier_y - barrier_r) + min_barrier_y;
+        const float ent_x = rand01(c) * (c.s.main_width - 2 * barrier_r) + barrier_r;
+        const int theme = randn(c, c.d.num_themes[BF_BARRIER]); // choose_random_theme
+        const int th = c.s.opt_restrict_themes ? 0 : theme;    // match_aspect_ratio
+        const int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[BF_BARRIER + th * MAX_ASSETS];
+        float ry = barrier_r;
+        if (sp.y <= 0 || sp.z <= 0) c.s.error = PG_ERR_BAD_OPTION;
+        else ry = barrier_r / (float)(sp.y * 1.0 / sp.z);
+        if (!spawn_collides(c, ent_x, ent_y, barrier_r, ry)) { // has_any_collision
+            const int e = add_entity_rxy(c, ent_x, ent_y, 0, 0, barrier_r, ry, BF_BARRIER);
+            EI(c, F_IMAGE_THEME, e) = theme;
+            EF(c, F_HEALTH, e) = 3;
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES;
+        }
+        wave_sync();
+    }
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1900,6 +1965,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_game_reset(c, scratch->rooms);
     if constexpr (G == PG_GAME_PLUNDER) plunder_game_reset(c);
     if constexpr (G == PG_GAME_STARPILOT) starpilot_game_reset(c, &scratch->sp);
+    if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_game_reset(c);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -2006,6 +2072,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
+        PG_CASE(PG_GAME_BOSSFIGHT)
     default: break;
     }
 #undef PG_CASE

@@ -750,6 +750,8 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 c.s.fish_eaten += 1;
             }
         }
+    } else if constexpr (G == PG_GAME_BOSSFIGHT) { // bossfight.cpp:120-131
+        if (t == BF_BOSS || t == BF_BARRIER || t == BF_ENEMY_BULLET) c.s.sd_done = 1;
     } else if constexpr (G == PG_GAME_STARPILOT) { // starpilot.cpp:126-136
         if (t == SP_FINISH_LINE) {
             c.s.sd_done = 1;
@@ -840,9 +842,96 @@ DEV void handle_agent_collision(Ctx &c, int m) {
 //
 // handle_collision(src, target) (basic :383-385 empty; fruitbot.cpp:117-134)
 DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type);
+DEV int find_type(Ctx &c, int type) { // first entity of a type (bossfight's boss / shields pointers)
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        const int i = base + LANE;
+        const unsigned long long b = ballot(i < c.s.num_ents && EI(c, F_TYPE, i) == type);
+        if (b) return base + __ffsll((long long)b) - 1;
+    }
+    return -1;
+}
+DEV void bf_prepare_boss(Ctx &c, int boss) { // bossfight.cpp:192-199
+    auto &B = c.s.gs.bf;
+    B.shields_are_up = 1;
+    B.curr_vel_timeout = BF_BOSS_VEL_TIMEOUT;
+    B.time_to_swap = B.invulnerable_duration;
+    B.attack_mode = (int)((B.attack_modes >> (2 * (B.round_num % B.num_rounds))) & 3u);
+    if (boss >= 0) {
+        EF(c, F_VX, boss) = 0;
+        EF(c, F_VY, boss) = 0;
+    }
+}
 DEV bool sp_destructible(int t) { return t == SP_FLYER || t == SP_FAST_FLYER || t == SP_TURRET || t == SP_METEOR; }
 template <int G>
 DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_BOSSFIGHT) { // bossfight.cpp:140-190
+        auto &B = c.s.gs.bf;
+        const int st = EI(c, F_TYPE, si), tt = EI(c, F_TYPE, ti);
+        if (st == BF_PLAYER_BULLET) {
+            bool will_erase = false;
+            if (tt == BF_SHIELDS) {
+                if (B.shields_are_up) {
+                    EI(c, F_TYPE, si) = BF_REFLECTED_BULLET;
+                    const float theta = (float)(PI_F * (1.25 + .5 * B.rand_pct));
+                    double sn, cs;
+                    pg_sincos_cr((double)theta, &sn, &cs);
+                    EF(c, F_VY, si) = (float)(1 * sn * .5); // PLAYER_BULLET_VEL (const int 1)
+                    EF(c, F_VX, si) = (float)(1 * cs * .5);
+                    EI(c, F_EXPIRE_TIME, si) = 4;
+                    EI(c, F_LIFE_TIME, si) = 0;
+                    EF(c, F_ALPHA_DECAY, si) = 0.8f;
+                }
+            } else if (tt == BF_BOSS) {
+                if (!B.shields_are_up) {
+                    const float h = EF(c, F_HEALTH, ti) - 1;
+                    EF(c, F_HEALTH, ti) = h;
+                    will_erase = true;
+                    if ((int)h % B.round_health == 0) {
+                        c.s.sd_reward += 1; // POSITIVE_REWARD (const int)
+                        if (h == 0) {
+                            c.s.sd_done = 1;
+                            c.s.sd_reward += 10; // COMPLETION_BONUS (const int)
+                            c.s.sd_level_complete = 1;
+                        } else {
+                            B.round_num++;
+                            wave_sync();
+                            bf_prepare_boss(c, ti);
+                            B.curr_vel_timeout = BF_BOSS_DAMAGED_TIMEOUT;
+                            B.damaged_until_time = c.s.cur_time + BF_BOSS_DAMAGED_TIMEOUT;
+                        }
+                    }
+                }
+            }
+            const int sf = EI(c, F_FLAGS, si);
+            if (will_erase && !(sf & EF_WILL_ERASE)) {
+                EI(c, F_FLAGS, si) = sf | EF_WILL_ERASE;
+                const float sx = EF(c, F_X, si), sy = EF(c, F_Y, si), r = (float)(.5 * EF(c, F_RX, si));
+                const float tvx = EF(c, F_VX, ti), tvy = EF(c, F_VY, ti);
+                wave_sync();
+                append_entity(c, sx, sy, tvx, tvy, r, r, EXPLOSION); // spawn_child + target velocity
+            }
+        } else if (st == BF_BARRIER) {
+            if (tt == BF_ENEMY_BULLET || tt == BF_PLAYER_BULLET) {
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+                const float tx = EF(c, F_X, ti), ty = EF(c, F_Y, ti), r = (float)(.5 * EF(c, F_RX, ti));
+                wave_sync();
+                append_entity(c, tx, ty, 0, 0, r, r, EXPLOSION); // spawn_child(target, EXPLOSION, .5 * rx)
+            } else if (tt == BF_LASER_TRAIL) {
+                EI(c, F_FLAGS, ti) = EI(c, F_FLAGS, ti) | EF_WILL_ERASE;
+            }
+            wave_sync();
+            if (EF(c, F_HEALTH, si) <= 0) { // barriers keep health 3: never taken
+                const int sf = EI(c, F_FLAGS, si);
+                if (!(sf & EF_WILL_ERASE)) {
+                    const float sx = EF(c, F_X, si), sy = EF(c, F_Y, si), r = (float)(.5 * EF(c, F_RX, si));
+                    const float svx = EF(c, F_VX, si), svy = EF(c, F_VY, si);
+                    wave_sync();
+                    append_entity(c, sx, sy, svx, svy, r, r, EXPLOSION);
+                }
+                EI(c, F_FLAGS, si) = EI(c, F_FLAGS, si) | EF_WILL_ERASE;
+            }
+        }
+    }
     if constexpr (G == PG_GAME_STARPILOT) { // starpilot.cpp:138-145
         const int tt = EI(c, F_TYPE, ti);
         if (EI(c, F_TYPE, si) == SP_BULLET_PLAYER && tt != SP_CLOUD && sp_destructible(tt)) {
@@ -1853,6 +1942,137 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ bossfight (bossfight.cpp:252-392)
+DEV void bf_boss_fire(Ctx &c, int boss, float bullet_r, float vel, float theta) { // :252-257
+    double sn, cs;
+    pg_sincos_cr((double)theta, &sn, &cs);
+    const float bx = EF(c, F_X, boss), by = EF(c, F_Y, boss);
+    wave_sync();
+    const int e = append_entity(c, bx, by, (float)(vel * cs), (float)(vel * sn), bullet_r, bullet_r, BF_ENEMY_BULLET);
+    if (e >= 0) {
+        EI(c, F_IMAGE_THEME, e) = c.s.gs.bf.boss_laser_theme;
+        EI(c, F_EXPIRE_TIME, e) = 50;
+        EF(c, F_VROT, e) = PI_F / 8;
+    }
+    wave_sync();
+}
+
+DEV void bossfight_step_tail(Ctx &c, uint32_t *rg) {
+    auto &B = c.s.gs.bf;
+    const int boss = find_type(c, BF_BOSS), shields = find_type(c, BF_SHIELDS);
+    if (boss < 0 || shields < 0) {
+        c.s.error = PG_ERR_BAD_OPTION;
+        return;
+    }
+    const float bx0 = EF(c, F_X, boss), by0 = EF(c, F_Y, boss);
+    wave_sync();
+    EF(c, F_X, shields) = bx0;
+    EF(c, F_Y, shields) = by0;
+    B.rand_pct = rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds));
+    B.rand_fire_pct = rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds));
+    B.rand_pct_x = rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds));
+    B.rand_pct_y = rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds));
+    if (B.curr_vel_timeout <= 0) {
+        const float dest_x = B.rand_pct_x * (c.s.main_width - 2 * BF_BOSS_R) + BF_BOSS_R;
+        const float dest_y = B.rand_pct_y * (c.s.main_height - 2 * BF_BOSS_R - BF_BOTTOM_MARGIN) + BF_BOSS_R + BF_BOTTOM_MARGIN;
+        EF(c, F_VX, boss) = (dest_x - bx0) / BF_BOSS_VEL_TIMEOUT;
+        EF(c, F_VY, boss) = (dest_y - by0) / BF_BOSS_VEL_TIMEOUT;
+        B.curr_vel_timeout = BF_BOSS_VEL_TIMEOUT;
+        if (B.time_to_swap > 0) {
+            B.time_to_swap -= 1;
+        } else {
+            B.time_to_swap = B.shields_are_up ? 500 : B.invulnerable_duration; // vulnerable_duration = 500
+            B.shields_are_up = !B.shields_are_up;
+        }
+    } else {
+        B.curr_vel_timeout -= 1;
+    }
+    wave_sync();
+    const bool gh = c.s.agent_erased;
+    if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 3) {
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        wave_sync();
+        const int e = append_entity(c, ax, ay, 0, 1, .25f, .25f, BF_PLAYER_BULLET);
+        if (e >= 0) {
+            EI(c, F_IMAGE_THEME, e) = B.player_laser_theme;
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES;
+            EI(c, F_EXPIRE_TIME, e) = 25;
+        }
+        c.s.last_fire_time = c.s.cur_time;
+        wave_sync();
+    }
+    const int ct = c.s.cur_time;
+    const float bv = B.boss_bullet_vel, rp = B.rand_pct;
+    if (B.damaged_until_time >= ct) { // damaged_mode (:299-305)
+        if (ct % 3 == 0) {
+            const float pos_x = EF(c, F_X, boss) + (2 * B.rand_pct_x - 1) * EF(c, F_RX, boss);
+            const float pos_y = EF(c, F_Y, boss) + (2 * B.rand_pct_y - 1) * EF(c, F_RY, boss);
+            wave_sync();
+            append_entity(c, pos_x, pos_y, 0, 0, .75f, .75f, EXPLOSION);
+            wave_sync();
+        }
+    } else if (B.shields_are_up) { // active_attack (:307-317)
+        const int am = B.attack_mode;
+        if (am == 0) {
+            if (ct % 8 == 0)
+                for (int i = 0; i < 5; i++) bf_boss_fire(c, boss, .5f, bv, (float)(PI_F * 1.5 + (i - 2) * PI_F / 8));
+        } else if (am == 1) {
+            if (ct % 5 == 0) {
+                int k = ct / 5;
+                k = abs(8 - (k % 16));
+                for (int i = 0; i < 4; i++)
+                    bf_boss_fire(c, boss, .5f, bv, (float)(PI_F * (1.25 + .5 * k / 8.0) + i * PI_F / 2));
+            }
+        } else if (am == 2) {
+            if (ct % 10 == 0) {
+                const int num_bullets = 8;
+                const float offset = rp * 2 * PI_F;
+                for (int i = 0; i < num_bullets; i++) bf_boss_fire(c, boss, .5f, bv, 2 * PI_F / num_bullets * i + offset);
+            }
+        } else if (am == 3) {
+            if (ct % 4 == 0) bf_boss_fire(c, boss, .5f, bv, PI_F * (1 + rp));
+        }
+    } else { // passive_attack_mode (:259-263), base_fire_prob = 0.1f
+        if (B.rand_fire_pct < 0.1f) bf_boss_fire(c, boss, .5f, bv, PI_F * (1 + rp));
+    }
+    // each ENEMY_BULLET (descending) leaves a LASER_TRAIL (:375-391)
+    const int n0 = c.s.num_ents;
+    int cnt = 0;
+    for (int base = 0; base < n0; base += 64) {
+        const int i = base + LANE;
+        cnt += __popcll(ballot(i < n0 && EI(c, F_TYPE, i) == BF_ENEMY_BULLET));
+    }
+    if (n0 + cnt > PG_CAP - c.s.num_tail) {
+        c.s.error = PG_ERR_ENTITY_OVERFLOW;
+        return;
+    }
+    int done = 0;
+    for (int base = (n0 - 1) & ~63; base >= 0; base -= 64) {
+        const int i = base + LANE;
+        const bool eb = i < n0 && EI(c, F_TYPE, i) == BF_ENEMY_BULLET;
+        const unsigned long long b = ballot(eb);
+        if (eb) {
+            // rank from the top: bullets above i in this chunk
+            const int rank = done + __popcll(b & ~((2ull << LANE) - 1ull));
+            const int t = n0 + rank;
+            EF(c, F_X, t) = EF(c, F_X, i); EF(c, F_Y, t) = EF(c, F_Y, i);
+            EF(c, F_VX, t) = EF(c, F_VX, i) * .5f; EF(c, F_VY, t) = EF(c, F_VY, i) * .5f;
+            EF(c, F_RX, t) = EF(c, F_RX, i); EF(c, F_RY, t) = EF(c, F_RY, i);
+            EF(c, F_ROTATION, t) = EF(c, F_ROTATION, i); EF(c, F_VROT, t) = EF(c, F_VROT, i);
+            EF(c, F_ALPHA, t) = 1.0f; EF(c, F_ALPHA_DECAY, t) = 0.7f; EF(c, F_GROW_RATE, t) = 1.0f;
+            EF(c, F_FRICTION, t) = 1; EF(c, F_COLLISION_MARGIN, t) = 0; EF(c, F_HEALTH, t) = 1;
+            EF(c, F_THETA, t) = -100; EF(c, F_CLIMBER_SPAWN_X, t) = 0;
+            EI(c, F_TYPE, t) = BF_LASER_TRAIL; EI(c, F_IMAGE_TYPE, t) = BF_ENEMY_BULLET;
+            EI(c, F_IMAGE_THEME, t) = B.boss_laser_theme; EI(c, F_RENDER_Z, t) = 0; EI(c, F_LIFE_TIME, t) = 0;
+            EI(c, F_EXPIRE_TIME, t) = 8; EI(c, F_FIRE_TIME, t) = -1; EI(c, F_SPAWN_TIME, t) = -1;
+            EI(c, F_FLAGS, t) = EF_AUTO_ERASE;
+        }
+        done += __popcll(b);
+    }
+    c.s.num_ents = n0 + cnt;
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ starpilot (starpilot.cpp:356-430)
 DEV void sp_copy_slot(Ctx &c, int from, int to) {
     for (int f = LANE; f < PG_NF; f += 64) EI(c, f, to) = EI(c, f, from);
@@ -2039,6 +2259,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_DODGEBALL) dodgeball_step_tail(c, rg);
     if constexpr (G == PG_GAME_PLUNDER) plunder_step_tail(c, rg);
     if constexpr (G == PG_GAME_STARPILOT) starpilot_step_tail(c, rg);
+    if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_step_tail(c, rg);
     wave_sync();
     c.pt.mark(5);
 }
@@ -2142,6 +2363,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_DODGEBALL) { PG_W(last_fire_time) PG_W(num_enemies) }
         if constexpr (G == PG_GAME_PLUNDER) { PG_W(last_fire_time) PG_W(gs) }
         if constexpr (G == PG_GAME_STARPILOT) { PG_W(num_tail) }
+        if constexpr (G == PG_GAME_BOSSFIGHT) { PG_W(last_fire_time) PG_W(gs) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -2170,6 +2392,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_DODGEBALL)
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
+        PG_CASE(PG_GAME_BOSSFIGHT)
     default: break;
     }
 #undef PG_CASE

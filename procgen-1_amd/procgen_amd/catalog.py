@@ -262,6 +262,22 @@ STARPILOT_SPRITES = {
     9: ["misc_assets/spaceRockets_%03d.png" % i for i in range(1, 5)],
 }
 
+# ---------------------------------------------------------------- bossfight
+# procgen/src/games/bossfight.cpp:76-106 (PLAYER_BULLET 1, BOSS 2, SHIELDS 3, ENEMY_BULLET 4,
+# LASER_TRAIL 5 and REFLECTED_BULLET 6 draw other types' images, BARRIER 7)
+_BF_LASERS = ["misc_assets/laserGreen14.png", "misc_assets/laserRed11.png", "misc_assets/laserBlue09.png"]
+BOSSFIGHT_SPRITES = {
+    0: ["misc_assets/playerShip1_blue.png", "misc_assets/playerShip1_green.png",
+        "misc_assets/playerShip2_orange.png", "misc_assets/playerShip3_red.png"],
+    2: ["misc_assets/enemyShipBlack1.png", "misc_assets/enemyShipBlue2.png", "misc_assets/enemyShipGreen3.png",
+        "misc_assets/enemyShipRed4.png"],
+    4: _BF_LASERS,
+    1: _BF_LASERS,
+    3: ["misc_assets/shield2.png"],
+    7: ["misc_assets/spaceMeteors_%03d.png" % i for i in range(1, 5)] +
+       ["misc_assets/meteorGrey_big%d.png" % i for i in range(1, 5)],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -276,6 +292,7 @@ GAMES = {
     "dodgeball": (DODGEBALL_SPRITES, "topdown"),  # dodgeball.cpp:46-48
     "plunder": (PLUNDER_SPRITES, "water_surface"),  # plunder.cpp:45-47
     "starpilot": (STARPILOT_SPRITES, "space"),  # starpilot.cpp:56-58
+    "bossfight": (BOSSFIGHT_SPRITES, "space"),  # bossfight.cpp:72-74
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

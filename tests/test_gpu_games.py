@@ -66,7 +66,7 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
 GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder",
-         "starpilot"]
+         "starpilot", "bossfight"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -148,6 +148,12 @@ def test_starpilot_long_and_extreme():
     background; extreme mode (more health, smaller bullets)."""
     run_pair("starpilot", 32, 650, seed=22, num_levels=0, rand_seed=11)
     run_pair("starpilot", 8, 300, seed=23, num_levels=0, rand_seed=12, distribution_mode="extreme")
+
+
+def test_bossfight_long():
+    """bossfight: shields up / down cycles, reflected bullets (type change mid collision walk), boss
+    damage rounds with explosions, laser trails, attack modes 0-3 (sin / cos of the fire angles)."""
+    run_pair("bossfight", 32, 800, seed=24, num_levels=0, rand_seed=13)
 
 
 def test_bigfish_long_episodes():
