@@ -57,7 +57,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
 enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
-       GAME_MINER = 12, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
+       GAME_MINER = 12, GAME_NINJA = 13, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
 
 static void fatal_msg(const char *m) {
     fprintf(stderr, "oracle fatal: %s\n", m);
@@ -264,6 +264,8 @@ typedef struct {
     float bf_base_fire_prob, bf_boss_bullet_vel, bf_barrier_vel, bf_barrier_spawn_prob, bf_rand_pct, bf_rand_fire_pct,
         bf_rand_pct_x, bf_rand_pct_y;
     Entity *bf_boss, *bf_shields;
+    /* ninja (ninja.cpp:25-33; has_support / facing_right / wall_theme / gravity / air_control shared) */
+    float nj_jump_charge, nj_jump_charge_inc;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -372,6 +374,14 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
     (void)is_horizontal;
     /* basic-abstract-game.cpp:494-501 */
     bool base = (target == WALL_OBJ) || (target == g->out_of_bounds_object);
+    if (g->game_id == GAME_NINJA && target == 20) { /* ninja.cpp:128-141: WALL_MID */
+        if (src->type == PLAYER) return true;
+        if (src->type == 7) { /* THROWING_STAR: sticks to walls */
+            ((Entity *)src)->vx = 0;
+            ((Entity *)src)->vy = 0;
+            return true;
+        }
+    }
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:204-211 */
         if (base) return true;
         if (src->type == PLAYER && cr_is_wall(target)) return true;
@@ -605,6 +615,14 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 g->fish_eaten += 1;
             }
         }
+    } else if (g->game_id == GAME_NINJA) { /* ninja.cpp:77-87 */
+        if (obj->type == EXPLOSION) {
+            g->sd_done = true;
+        } else if (obj->type == 1) { /* GOAL */
+            g->sd_reward += 10.0f;
+            g->sd_level_complete = true;
+            g->sd_done = true;
+        }
     } else if (g->game_id == GAME_BOSSFIGHT) { /* bossfight.cpp:120-131: BOSS, BARRIER, ENEMY_BULLET */
         if (obj->type == 2 || obj->type == 7 || obj->type == 4) g->sd_done = true;
     } else if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:126-136 */
@@ -711,6 +729,19 @@ static bool hook_should_draw_entity(Game *g, const Entity *e) {
 
 static void hook_handle_grid_collision(Game *g, Entity *obj, int type, int i, int j) {
     (void)i; (void)j;
+    if (g->game_id == GAME_NINJA) { /* ninja.cpp:89-106 */
+        if (obj->type == PLAYER) {
+            if (type == 14 || type == 6) g->sd_done = true; /* FIRE, BOMB */
+        } else if (obj->type == 7) { /* THROWING_STAR */
+            if (type == 6) {
+                obj->will_erase = true;
+                set_obj(g, i, j, SPACE);
+                add_entity(g, (float)(i + .5), (float)(j + .5), 0, 0, .5, EXPLOSION);
+            }
+            if (type == 20) obj->will_erase = true;
+        }
+        return;
+    }
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:144-154 */
         if (obj->type == PLAYER) {
             if (type == CR_GOAL) {
@@ -755,6 +786,11 @@ static int hook_image_for_type(Game *g, int type) {
             return -1;
         }
     }
+    if (g->game_id == GAME_NINJA && type == PLAYER) { /* ninja.cpp:143-153 */
+        Entity *agent = AG(g);
+        if (fabs((double)agent->vx) < .01 && g->action_vx == 0 && g->has_support) return PLAYER;
+        return (g->cur_time / 5 % 2 == 0 || !g->has_support) ? 12 : 13; /* PLAYER_RIGHT1 / 2 */
+    }
     if (g->game_id == GAME_MINER) { /* miner.cpp:95-103: MOVING_BOULDER -> BOULDER, MOVING_DIAMOND -> DIAMOND */
         if (type == 3) return 1;
         if (type == 4) return 2;
@@ -763,6 +799,7 @@ static int hook_image_for_type(Game *g, int type) {
 }
 
 static int hook_theme_for_grid_obj(Game *g, int type) {
+    if (g->game_id == GAME_NINJA) return type == 20 ? g->wall_theme : 0; /* ninja.cpp:119-124 */
     if (g->game_id == GAME_COINRUN || g->game_id == GAME_CLIMBER) { /* coinrun.cpp:133-138, climber.cpp:106-111 */
         if (type == 15 || type == 16) return g->wall_theme;
         return 0;
@@ -969,6 +1006,26 @@ static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299
 }
 
 static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_NINJA) { /* ninja.cpp:387-418 */
+        g->action_vx = (float)(move_action / 3 - 1);
+        g->action_vy = (float)((move_action % 3) - 1);
+        if (g->action_vy < 0) g->action_vy = 0;
+        if (g->action_vx > 0) g->facing_right = true;
+        if (g->action_vx < 0) g->facing_right = false;
+        Entity *agent = AG(g);
+        int b1 = get_obj_from_floats(g, (float)(agent->x - (agent->rx - .01)), (float)(agent->y - (agent->ry + .01)));
+        int b2 = get_obj_from_floats(g, (float)(agent->x + (agent->rx - .01)), (float)(agent->y - (agent->ry + .01)));
+        g->has_support = (b1 == 20 || b1 == g->out_of_bounds_object) || (b2 == 20 || b2 == g->out_of_bounds_object);
+        if (g->has_support && g->action_vy == 1) {
+            g->action_vy = 1;
+            g->nj_jump_charge += g->nj_jump_charge_inc;
+            if (g->nj_jump_charge > 1) g->nj_jump_charge = 1;
+        } else {
+            g->action_vy = 0;
+        }
+        if (!g->has_support) g->nj_jump_charge = 0;
+        return;
+    }
     if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:110-114 */
         g->action_vx = (float)(move_action / 3 - 1);
         g->action_vy = 0;
@@ -1007,6 +1064,18 @@ static void lp_decay_vel(float *vel);
 static double cu_sign(double x);
 static void update_agent_velocity(Game *g) {
     Entity *agent = AG(g);
+    if (g->game_id == GAME_NINJA) { /* ninja.cpp:108-121 */
+        float mixrate_x = g->has_support ? g->mixrate : (g->mixrate * g->air_control);
+        agent->vx = (1 - mixrate_x) * agent->vx + mixrate_x * g->maxspeed * g->action_vx;
+        if (g->action_vy < 1 && g->nj_jump_charge > 0) {
+            agent->vy = g->nj_jump_charge * g->max_jump;
+            g->nj_jump_charge = 0;
+        }
+        if (!g->has_support) {
+            if (agent->vy > -2) agent->vy -= g->gravity;
+        }
+        return;
+    }
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:156-173 */
         float mixrate_x = g->has_support ? g->mixrate : (g->mixrate * g->air_control);
         agent->vx = (1 - mixrate_x) * agent->vx + mixrate_x * g->maxspeed * g->action_vx;
@@ -3293,6 +3362,137 @@ static void bossfight_game_step(Game *g) { /* :331-392 */
     }
 }
 
+/* ================================================================== ninja (games/ninja.cpp) */
+#define NJ_GOAL 1
+#define NJ_BOMB 6
+#define NJ_THROWING_STAR 7
+#define NJ_FIRE 14
+#define NJ_WALL_MID 20
+
+static void nj_fill_block_top(Game *g, int x, int y, int dx, int dy, int fill, int top) { /* :162-167 */
+    if (dy <= 0) return;
+    fill_elem(g, x, y, dx, dy - 1, fill);
+    fill_elem(g, x, y + dy - 1, dx, 1, top);
+}
+static void nj_fill_ground_block(Game *g, int x, int y, int dx, int dy) {
+    nj_fill_block_top(g, x, y, dx, dy, NJ_WALL_MID, NJ_WALL_MID);
+}
+
+static void nj_generate(Game *g, const or_atlas *at, int difficulty) { /* generate_coin_to_the_right :180-297 */
+    MT *r = &g->rand_gen;
+    int min_gap = difficulty - 1, min_plat_w = 1, inc_dy = 4;
+    if (g->options.distribution_mode == EasyMode) {
+        min_gap -= 1;
+        if (min_gap < 0) min_gap = 0;
+        min_plat_w = 3;
+        inc_dy = 2;
+    }
+    float bomb_prob = (float)(.25 * (difficulty - 1));
+    int max_gap_inc = difficulty == 1 ? 1 : 2;
+    int num_sections = rg_randn(r, difficulty) + difficulty;
+    int start_x = 5, curr_x = start_x, curr_y = g->main_height / 2, min_y = curr_y;
+    int w = g->main_width;
+    float _max_dy = g->max_jump * g->max_jump / (2 * g->gravity);
+    int max_dy = (int)(_max_dy - .5);
+    int prev_x, prev_y;
+    nj_fill_ground_block(g, 0, 0, start_x, curr_y);
+    fill_elem(g, 0, curr_y + 8, start_x, g->main_height - curr_y - 8, NJ_WALL_MID);
+    for (int i = 0; i < num_sections; i++) {
+        prev_x = curr_x;
+        prev_y = curr_y;
+        int num_edges = rg_randn(r, 2) + 1;
+        int max_y = -1, last_edge_y = -1;
+        for (int j = 0; j < num_edges; j++) {
+            curr_x = prev_x + j;
+            if (curr_x + 15 >= w) break;
+            curr_y = prev_y;
+            int dy = rg_randn(r, inc_dy) + 1 + (int)(difficulty / 3);
+            if (dy > max_dy) dy = max_dy;
+            if (curr_y >= g->main_height - 15) dy *= -1;
+            else if (curr_y >= 5 && rg_rand01(r) < .4) dy *= -1;
+            curr_y += dy;
+            if (curr_y < 3) curr_y = 3;
+            if (abs(curr_y - last_edge_y) <= 1) curr_y = last_edge_y + 2;
+            int dx = min_plat_w + rg_randn(r, 3);
+            nj_fill_ground_block(g, curr_x, curr_y - 1, dx, 1);
+            curr_x += dx;
+            curr_x += min_gap + rg_randn(r, max_gap_inc + 1);
+            if (curr_y > max_y) max_y = curr_y;
+            if (curr_y < min_y) min_y = curr_y;
+            last_edge_y = curr_y;
+        }
+        if (rg_rand01(r) < bomb_prob) {
+            int bx = rg_randn(r, curr_x - prev_x + 1) + prev_x;
+            set_obj(g, bx, max_y + 2, NJ_BOMB);
+        }
+        int ceiling_height = 11;
+        int ceiling_start = max_y - 1 + ceiling_height;
+        nj_fill_ground_block(g, prev_x, ceiling_start, curr_x - prev_x, g->main_height - ceiling_start);
+    }
+    int e = add_entity(g, (float)(curr_x + .5), (float)(curr_y + .5), 0, 0, .5, NJ_GOAL);
+    choose_random_theme(g, &g->ents[e], at);
+    nj_fill_ground_block(g, curr_x, curr_y - 1, 1, 1);
+    fill_elem(g, curr_x, curr_y + 6, 1, g->main_height - curr_y - 6, NJ_WALL_MID);
+    int fire_y = min_y - 2;
+    if (fire_y < 1) fire_y = 1;
+    nj_fill_ground_block(g, start_x, 0, g->main_width - start_x, fire_y);
+    fill_elem(g, start_x, fire_y, g->main_width - start_x, 1, NJ_FIRE);
+    fill_elem(g, curr_x + 1, 0, g->main_width - curr_x - 1, g->main_height, NJ_WALL_MID);
+}
+
+static void ninja_game_reset(Game *g, const or_atlas *at) { /* :299-331 */
+    basic_game_reset(g, at);
+    g->gravity = 0.2f;
+    g->max_jump = 1.5;
+    g->air_control = 0.15f;
+    g->maxspeed = .5;
+    g->has_support = false;
+    g->facing_right = true;
+    g->nj_jump_charge = 0;
+    g->nj_jump_charge_inc = .25;
+    g->visibility = 16;
+    Entity *agent = AG(g);
+    agent->rx = .5;
+    agent->ry = .5;
+    agent->x = 1 + agent->rx;
+    agent->y = g->main_height / 2 + agent->ry;
+    if (g->options.distribution_mode == EasyMode) {
+        g->max_jump = 1.25;
+        g->nj_jump_charge_inc = 1;
+        g->visibility = 10;
+    }
+    int difficulty = rg_randn(&g->rand_gen, 3) + 1;
+    g->last_fire_time = 0;
+    g->wall_theme = rg_randn(&g->rand_gen, 3); /* NUM_WALL_THEMES */
+    /* init_floor_and_walls (:169-174) */
+    fill_elem(g, 0, 0, g->main_width, 1, NJ_WALL_MID);
+    fill_elem(g, 0, 0, 1, g->main_height, NJ_WALL_MID);
+    fill_elem(g, g->main_width - 1, 0, 1, g->main_height, NJ_WALL_MID);
+    fill_elem(g, 0, g->main_height - 1, g->main_width, 1, NJ_WALL_MID);
+    nj_generate(g, at, difficulty);
+}
+
+static void ninja_game_step(Game *g) { /* :420-450 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+    if (g->special_action > 0 && (g->cur_time - g->last_fire_time) >= 3) {
+        float theta = 0, bullet_vel = 1;
+        if (g->special_action == 1) theta = 0;
+        else if (g->special_action == 2) theta = PI_F / 4;
+        else if (g->special_action == 3) theta = PI_F / 2;
+        else if (g->special_action == 4) theta = -1 * PI_F / 4;
+        if (agent->is_reflected) theta = PI_F - theta;
+        int b = add_entity(g, agent->x, agent->y, (float)(bullet_vel * cos((double)theta)),
+                           (float)(bullet_vel * sin((double)theta)), .25, NJ_THROWING_STAR);
+        g->ents[b].collides_with_entities = true;
+        g->ents[b].expire_time = 15;
+        g->ents[b].smart_step = true;
+        g->last_fire_time = g->cur_time;
+    }
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -3445,6 +3645,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_PLUNDER) plunder_game_reset(g, at);
     else if (g->game_id == GAME_STARPILOT) starpilot_game_reset(g, at);
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_reset(g, at);
+    else if (g->game_id == GAME_NINJA) ninja_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -3461,6 +3662,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_PLUNDER) plunder_game_step(g, at);
     else if (g->game_id == GAME_STARPILOT) starpilot_game_step(g, at);
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_step(g);
+    else if (g->game_id == GAME_NINJA) ninja_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -4074,6 +4276,13 @@ static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_dra
     }
     draw_background(g, at);
     draw_foreground(g, at);
+    if (g->game_id == GAME_NINJA) { /* ninja.cpp:155-164: jump charge bar, get_abs_rect (:812-814) */
+        float u = g->unit;
+        float bar_height = 3 * g->nj_jump_charge;
+        float vis = g->visibility;
+        qt_fill_rectf(g->canvas, (double)(.25f * u), (double)((float)(vis - .5 - bar_height) * u), (double)(.5f * u),
+                      (double)(bar_height * u), 0xff42f587u);
+    }
     if (g->game_id == GAME_PLUNDER) { /* plunder.cpp:66-77: juice and progress bars, get_abs_rect (:812-814) */
         float u = g->unit;
         qt_fill_rectf(g->canvas, (double)(.25f * u), (double)(.25f * u), (double)(g->main_width * g->pl_juice_left * u),
@@ -4099,6 +4308,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "plunder") == 0) return GAME_PLUNDER;
     if (strcmp(name, "starpilot") == 0) return GAME_STARPILOT;
     if (strcmp(name, "bossfight") == 0) return GAME_BOSSFIGHT;
+    if (strcmp(name, "ninja") == 0) return GAME_NINJA;
     return -1;
 }
 
@@ -4152,6 +4362,11 @@ static void fruitbot_ctor(Game *g) { /* fruitbot.cpp:30-40 */
     g->maxspeed = 0.85f;
     g->bg_tile_ratio = -1;
     g->out_of_bounds_object = 2; /* OUT_OF_BOUNDS_WALL */
+}
+static void ninja_ctor(Game *g) { /* ninja.cpp:35-41 */
+    g->main_width = 64;
+    g->main_height = 64;
+    g->out_of_bounds_object = 20; /* WALL_MID */
 }
 static void bossfight_ctor(Game *g) { /* bossfight.cpp:60-68 */
     g->timeout = 4000;
@@ -4255,6 +4470,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_PLUNDER) plunder_ctor(g);
         else if (gid == GAME_STARPILOT) starpilot_ctor(g);
         else if (gid == GAME_BOSSFIGHT) bossfight_ctor(g);
+        else if (gid == GAME_NINJA) ninja_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

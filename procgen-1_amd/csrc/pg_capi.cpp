@@ -120,9 +120,10 @@ int game_id(const std::string &name) {
     if (name == "plunder") return PG_GAME_PLUNDER;
     if (name == "starpilot") return PG_GAME_STARPILOT;
     if (name == "bossfight") return PG_GAME_BOSSFIGHT;
+    if (name == "ninja") return PG_GAME_NINJA;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, bossfight, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, plunder, starpilot";
+const char *SUPPORTED_GAMES = "bigfish, bossfight, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, ninja, plunder, starpilot";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -182,6 +183,10 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_NINJA) { // ninja.cpp:35-41
+        s.main_width = 64;
+        s.main_height = 64;
+        s.out_of_bounds_object = 20; // WALL_MID
     } else if (gid == PG_GAME_BOSSFIGHT) { // bossfight.cpp:60-68
         s.timeout = 4000;
         s.main_width = 20;

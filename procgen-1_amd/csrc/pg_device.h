@@ -165,6 +165,14 @@ DEV float sp_hp_prob(int mode, int type) {
 #define BF_BOTTOM_MARGIN 6
 #define BF_BOSS_VEL_TIMEOUT 20
 #define BF_BOSS_DAMAGED_TIMEOUT 40
+// ninja.cpp:11-21
+#define NJ_GOAL 1
+#define NJ_BOMB 6
+#define NJ_THROWING_STAR 7
+#define NJ_PLAYER_RIGHT1 12
+#define NJ_PLAYER_RIGHT2 13
+#define NJ_FIRE 14
+#define NJ_WALL_MID 20
 // chaser.cpp:10-23
 #define CH_LARGE_ORB 2
 #define CH_ENEMY_WEAK 3

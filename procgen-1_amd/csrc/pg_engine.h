@@ -23,7 +23,7 @@
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
     PG_GAME_BIGFISH = 0, PG_GAME_BOSSFIGHT = 1, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
-    PG_GAME_MINER = 12, PG_GAME_PLUNDER = 14, PG_GAME_STARPILOT = 15
+    PG_GAME_MINER = 12, PG_GAME_NINJA = 13, PG_GAME_PLUNDER = 14, PG_GAME_STARPILOT = 15
 };
 #ifndef PG_NUM_GAMES
 #define PG_NUM_GAMES 16
@@ -192,6 +192,10 @@ struct PGEnv {
             int32_t barriers_moves_right;
             float boss_bullet_vel, rand_pct, rand_fire_pct, rand_pct_x, rand_pct_y;
         } bf;
+        struct { // ninja (ninja.cpp:25-33; has_support, facing_right, wall_theme, gravity, air_control,
+                 // last_fire_time are the shared members above)
+            float jump_charge, jump_charge_inc;
+        } nj;
         int32_t words[20];
     } gs;
     // entity slots reserved at the top of the planes, [PG_CAP - num_tail, PG_CAP): starpilot's

@@ -99,6 +99,10 @@ DEV int player_image(const PGEnv &s, float agent_vx) {
         if (fabsf(agent_vx) < .01 && s.action_vx == 0 && s.has_support) return PLAYER;
         return (s.cur_time / 5 % 2 == 0 || !s.has_support) ? CL_PLAYER_RIGHT1 : CL_PLAYER_RIGHT2;
     }
+    if constexpr (G == PG_GAME_NINJA) // ninja.cpp:143-153
+        return (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
+                   ? PLAYER
+                   : ((s.cur_time / 5 % 2 == 0 || !s.has_support) ? NJ_PLAYER_RIGHT1 : NJ_PLAYER_RIGHT2);
     if constexpr (G == PG_GAME_COINRUN)
         return (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
                    ? PLAYER
@@ -115,6 +119,8 @@ DEV int image_for_type(const PGEnv &s, int type, int player_img) {
             return CH_ENEMY + rem;
         }
     }
+    if constexpr (G == PG_GAME_NINJA)
+        if (type == PLAYER) return player_img;
     if constexpr (G == PG_GAME_COINRUN || G == PG_GAME_CLIMBER) { // ENEMY_BARRIER is 19 in both
         if (type == PLAYER) return player_img;
         if (type == CR_ENEMY_BARRIER) return -1;
@@ -131,6 +137,7 @@ template <int G>
 DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cpp:133-138)
     if constexpr (G == PG_GAME_COINRUN) return cr_is_wall(type) ? s.wall_theme : 0;
     if constexpr (G == PG_GAME_CLIMBER) return cl_is_wall(type) ? s.wall_theme : 0; // climber.cpp:106-111
+    if constexpr (G == PG_GAME_NINJA) return type == NJ_WALL_MID ? s.wall_theme : 0; // ninja.cpp:119-124
     return 0;
 }
 template <int G>
@@ -395,6 +402,11 @@ DEV void fb_fill_rectf(uint32_t *fb, double x, double y, double w, double h, uin
 // game_draw additions drawn over the foreground (plunder.cpp:66-77)
 template <int G>
 DEV void game_overlay(uint32_t *fb, const PGEnv &s, const View &v) {
+    if constexpr (G == PG_GAME_NINJA) { // jump charge bar (ninja.cpp:155-164), get_abs_rect (:812-814)
+        const float u = v.unit, bar_height = 3 * s.gs.nj.jump_charge;
+        fb_fill_rectf(fb, (double)(.25f * u), (double)((float)(v.visibility - .5 - bar_height) * u), (double)(.5f * u),
+                      (double)(bar_height * u), 0xff42f587u); // QColor(66, 245, 135)
+    }
     if constexpr (G == PG_GAME_PLUNDER) { // juice and progress bars, get_abs_rect (:812-814)
         const float u = v.unit;
         fb_fill_rectf(fb, (double)(.25f * u), (double)(.25f * u), (double)(s.main_width * s.gs.pl.juice_left * u),
@@ -1127,6 +1139,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
+        PG_CASE(PG_GAME_NINJA)
     default: break;
     }
 #undef PG_CASE

@@ -157,7 +157,7 @@ DEV void set_obj(RCtx &c, int x, int y, int v) {
 }
 DEV void fill_elem(RCtx &c, int x, int y, int dx, int dy, int elem) {
     int16_t v = (int16_t)(signed char)elem; // `char elem` narrowing (basic-abstract-game.cpp:125)
-    int n = dx * dy;
+    int n = (dx > 0 && dy > 0) ? dx * dy : 0; // the reference loops run dx x dy times
     bool bad = false;
     for (int k = LANE; k < n; k += 64) {
         int j = k / dy, l = k % dy;
@@ -1637,6 +1637,101 @@ DEV void bossfight_game_reset(RCtx &c) {
     }
 }
 
+// ------------------------------------------------------------------ ninja (ninja.cpp:162-331)
+DEV void nj_fill_ground_block(RCtx &c, int x, int y, int dx, int dy) { // fill_block_top(.., WALL_MID, WALL_MID)
+    if (dy <= 0) return;
+    fill_elem(c, x, y, dx, dy - 1, NJ_WALL_MID);
+    fill_elem(c, x, y + dy - 1, dx, 1, NJ_WALL_MID);
+}
+
+DEV void ninja_game_reset(RCtx &c) {
+    base_game_reset<PG_GAME_NINJA>(c);
+    auto &N = c.s.gs.nj;
+    c.s.gravity = 0.2f;
+    c.s.max_jump = 1.5;
+    c.s.air_control = 0.15f;
+    c.s.maxspeed = .5;
+    c.s.has_support = 0;
+    c.s.facing_right = 1;
+    N.jump_charge = 0;
+    N.jump_charge_inc = .25;
+    c.s.visibility = 16;
+    EF(c, F_RX, 0) = .5;
+    EF(c, F_RY, 0) = .5;
+    EF(c, F_X, 0) = 1 + EF(c, F_RX, 0);
+    EF(c, F_Y, 0) = c.s.main_height / 2 + EF(c, F_RY, 0);
+    if (c.s.opt_distribution_mode == PG_EASY) {
+        c.s.max_jump = 1.25;
+        N.jump_charge_inc = 1;
+        c.s.visibility = 10;
+    }
+    const int difficulty = randn(c, 3) + 1;
+    c.s.last_fire_time = 0;
+    c.s.wall_theme = randn(c, 3); // NUM_WALL_THEMES
+    const int W = c.s.main_width, H = c.s.main_height;
+    fill_elem(c, 0, 0, W, 1, NJ_WALL_MID); // init_floor_and_walls (:169-174)
+    fill_elem(c, 0, 0, 1, H, NJ_WALL_MID);
+    fill_elem(c, W - 1, 0, 1, H, NJ_WALL_MID);
+    fill_elem(c, 0, H - 1, W, 1, NJ_WALL_MID);
+    // generate_coin_to_the_right (:180-297)
+    int min_gap = difficulty - 1, min_plat_w = 1, inc_dy = 4;
+    if (c.s.opt_distribution_mode == PG_EASY) {
+        min_gap -= 1;
+        if (min_gap < 0) min_gap = 0;
+        min_plat_w = 3;
+        inc_dy = 2;
+    }
+    const float bomb_prob = (float)(.25 * (difficulty - 1));
+    const int max_gap_inc = difficulty == 1 ? 1 : 2;
+    const int num_sections = randn(c, difficulty) + difficulty;
+    const int start_x = 5;
+    int curr_x = start_x, curr_y = H / 2, min_y = curr_y;
+    const float _max_dy = c.s.max_jump * c.s.max_jump / (2 * c.s.gravity);
+    const int max_dy = (int)(_max_dy - .5);
+    nj_fill_ground_block(c, 0, 0, start_x, curr_y);
+    fill_elem(c, 0, curr_y + 8, start_x, H - curr_y - 8, NJ_WALL_MID);
+    for (int i = 0; i < num_sections; i++) {
+        const int prev_x = curr_x, prev_y = curr_y;
+        const int num_edges = randn(c, 2) + 1;
+        int max_y = -1, last_edge_y = -1;
+        for (int j = 0; j < num_edges; j++) {
+            curr_x = prev_x + j;
+            if (curr_x + 15 >= W) break;
+            curr_y = prev_y;
+            int dy = randn(c, inc_dy) + 1 + (int)(difficulty / 3);
+            if (dy > max_dy) dy = max_dy;
+            if (curr_y >= H - 15) dy *= -1;
+            else if (curr_y >= 5 && rand01(c) < .4) dy *= -1;
+            curr_y += dy;
+            if (curr_y < 3) curr_y = 3;
+            if (abs(curr_y - last_edge_y) <= 1) curr_y = last_edge_y + 2;
+            const int dx = min_plat_w + randn(c, 3);
+            nj_fill_ground_block(c, curr_x, curr_y - 1, dx, 1);
+            curr_x += dx;
+            curr_x += min_gap + randn(c, max_gap_inc + 1);
+            if (curr_y > max_y) max_y = curr_y;
+            if (curr_y < min_y) min_y = curr_y;
+            last_edge_y = curr_y;
+        }
+        if (rand01(c) < bomb_prob) {
+            const int bx = randn(c, curr_x - prev_x + 1) + prev_x;
+            set_obj(c, bx, max_y + 2, NJ_BOMB);
+        }
+        const int ceiling_start = max_y - 1 + 11; // ceiling_height
+        nj_fill_ground_block(c, prev_x, ceiling_start, curr_x - prev_x, H - ceiling_start);
+    }
+    const int e = add_entity(c, (float)(curr_x + .5), (float)(curr_y + .5), 0, 0, .5, NJ_GOAL);
+    choose_random_theme(c, e);
+    nj_fill_ground_block(c, curr_x, curr_y - 1, 1, 1);
+    fill_elem(c, curr_x, curr_y + 6, 1, H - curr_y - 6, NJ_WALL_MID);
+    int fire_y = min_y - 2;
+    if (fire_y < 1) fire_y = 1;
+    nj_fill_ground_block(c, start_x, 0, W - start_x, fire_y);
+    fill_elem(c, start_x, fire_y, W - start_x, 1, NJ_FIRE);
+    fill_elem(c, curr_x + 1, 0, W - curr_x - 1, H, NJ_WALL_MID);
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -1966,6 +2061,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_PLUNDER) plunder_game_reset(c);
     if constexpr (G == PG_GAME_STARPILOT) starpilot_game_reset(c, &scratch->sp);
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_game_reset(c);
+    if constexpr (G == PG_GAME_NINJA) ninja_game_reset(c);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -2073,6 +2169,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
+        PG_CASE(PG_GAME_NINJA)
     default: break;
     }
 #undef PG_CASE

@@ -363,6 +363,8 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
 #pragma unroll
         for (int j = 0; j < 2; j++) {
             int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
+            if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
+                if (o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID) { o.vx = 0; o.vy = 0; }
             block = block || is_blocked<G>(c, o.type, type2);
             reflect = reflect || will_reflect<G>(o.type, type2);
         }
@@ -616,6 +618,24 @@ DEV void set_action_xy(Ctx &c, int move_action) {
         if (c.s.action_vy == 1) {
             if (!c.s.has_support) c.s.action_vy = 0;
         }
+    } else if constexpr (G == PG_GAME_NINJA) { // ninja.cpp:387-418
+        auto &N = c.s.gs.nj;
+        if (c.s.action_vy < 0) c.s.action_vy = 0;
+        if (c.s.action_vx > 0) c.s.facing_right = 1;
+        if (c.s.action_vx < 0) c.s.facing_right = 0;
+        float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+        int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        c.s.has_support = (b1 == NJ_WALL_MID || b1 == c.s.out_of_bounds_object) ||
+                          (b2 == NJ_WALL_MID || b2 == c.s.out_of_bounds_object); // can_support (:383-385)
+        if (c.s.has_support && c.s.action_vy == 1) {
+            c.s.action_vy = 1;
+            N.jump_charge += N.jump_charge_inc;
+            if (N.jump_charge > 1) N.jump_charge = 1;
+        } else {
+            c.s.action_vy = 0;
+        }
+        if (!c.s.has_support) N.jump_charge = 0;
     } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:154-158
         c.s.action_vy = 0.2f;
         c.s.action_vrot = 0;
@@ -671,6 +691,16 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!(c.s.has_support && c.s.action_vy > 0)) {
             vy -= c.s.gravity;
             vy = clip_abs(vy, c.s.max_jump);
+        }
+    } else if constexpr (G == PG_GAME_NINJA) { // ninja.cpp:108-121
+        float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
+        vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
+        if (c.s.action_vy < 1 && c.s.gs.nj.jump_charge > 0) {
+            vy = c.s.gs.nj.jump_charge * c.s.max_jump;
+            c.s.gs.nj.jump_charge = 0;
+        }
+        if (!c.s.has_support) {
+            if (vy > -2) vy -= c.s.gravity;
         }
     } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:117-128
         float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
@@ -749,6 +779,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_NINJA) { // ninja.cpp:77-87
+        if (t == EXPLOSION) {
+            c.s.sd_done = 1;
+        } else if (t == NJ_GOAL) {
+            c.s.sd_reward += 10.0f; // GOAL_REWARD
+            c.s.sd_level_complete = 1;
+            c.s.sd_done = 1;
         }
     } else if constexpr (G == PG_GAME_BOSSFIGHT) { // bossfight.cpp:120-131
         if (t == BF_BOSS || t == BF_BARRIER || t == BF_ENEMY_BULLET) c.s.sd_done = 1;
@@ -1056,8 +1094,80 @@ DEV void entity_collisions(Ctx &c, int i) {
     }
 }
 
+// ninja's check_grid_collisions (basic-abstract-game.cpp:145-165 -> ninja.cpp:89-106) of smart
+// entity m: the agent dies on FIRE / BOMB; a star that touches a BOMB clears the cell (HBM grid,
+// its int8 mirror, this step's LDS copy) and leaves an EXPLOSION, and a star on a wall goes away
+DEV void ninja_grid_collisions(Ctx &c, int m) {
+    const float ax = EF(c, F_X, m), ay = EF(c, F_Y, m), arx = EF(c, F_RX, m), ary = EF(c, F_RY, m);
+    const int t = EI(c, F_TYPE, m);
+    const int min_x = (int)(ax - (arx + POS_EPS)), max_x = (int)(ax + (arx + POS_EPS));
+    const int min_y = (int)(ay - (ary + POS_EPS)), max_y = (int)(ay + (ary + POS_EPS));
+    for (int x = min_x; x <= max_x; x++) {
+        for (int y = min_y; y <= max_y; y++) {
+            const int gt = get_obj_from_floats(c, (float)x, (float)y);
+            if (gt == SPACE) continue;
+            if (t == PLAYER) {
+                if (gt == NJ_FIRE || gt == NJ_BOMB) c.s.sd_done = 1;
+            } else if (t == NJ_THROWING_STAR) {
+                if (gt == NJ_BOMB) {
+                    EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+                    const int cell = y * c.s.main_width + x; // set_obj(x, y, SPACE): in the world (a BOMB was read)
+                    if (LANE == 0) {
+                        c.d.grid[(size_t)c.env * PG_GRID_MAX + cell] = SPACE;
+                        c.d.grid8[(size_t)c.env * PG_GRID_MAX + cell] = (int8_t)SPACE;
+                        c.grid8[cell] = (int8_t)SPACE;
+                    }
+                    wave_sync();
+                    append_entity(c, (float)(x + .5), (float)(y + .5), 0, 0, .5f, .5f, EXPLOSION);
+                    wave_sync();
+                }
+                if (gt == NJ_WALL_MID) EI(c, F_FLAGS, m) = EI(c, F_FLAGS, m) | EF_WILL_ERASE;
+            }
+        }
+    }
+    wave_sync();
+}
+
 template <int G>
 DEV void agent_collisions(Ctx &c) {
+    if constexpr (G == PG_GAME_NINJA) {
+        // descending walk (:727-751): entity m matters if it touches the agent (EXPLOSION / GOAL
+        // effects) or is smart (its grid check: the agent, throwing stars); the stars'
+        // collides_with_entities loop calls the empty base handle_collision
+        int upper = c.s.num_ents;
+        const bool gh = c.s.agent_erased;
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
+        while (upper > 0) {
+            int m = -1;
+            bool agent_hit = false;
+            for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
+                const int i = base + LANE;
+                bool hit = false, smart = false;
+                if (i < upper) {
+                    const int t = EI(c, F_TYPE, i);
+                    if ((t == EXPLOSION || t == NJ_GOAL) && (gh || i != 0)) {
+                        const float mrg = EF(c, F_COLLISION_MARGIN, i);
+                        const float tx = (EF(c, F_RX, i) + arx) + mrg, ty = (EF(c, F_RY, i) + ary) + mrg;
+                        hit = (fabsf(EF(c, F_X, i) - ax) < tx) && (fabsf(EF(c, F_Y, i) - ay) < ty);
+                    }
+                    smart = (EI(c, F_FLAGS, i) & EF_SMART_STEP) != 0;
+                }
+                const unsigned long long b = ballot(hit || smart);
+                if (b) {
+                    m = base + top_bit(b);
+                    agent_hit = ballot(hit && i == m) != 0;
+                    break;
+                }
+            }
+            if (m < 0) break;
+            if (agent_hit) handle_agent_collision<G>(c, m);
+            wave_sync();
+            if (EI(c, F_FLAGS, m) & EF_SMART_STEP) ninja_grid_collisions(c, m);
+            upper = m;
+        }
+        return;
+    }
     if constexpr (G == PG_GAME_COINRUN) {
         bool unsupported = false; // no coinrun entity has collides_with_entities
         for (int base = 0; base < c.s.num_ents; base += 64) {
@@ -1942,6 +2052,40 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ ninja (ninja.cpp:420-450)
+DEV void ninja_step_tail(Ctx &c) {
+    const bool gh = c.s.agent_erased;
+    int fl = EI(c, F_FLAGS, 0);
+    bool refl = (fl & EF_REFLECTED) != 0;
+    if (!gh) {
+        if (c.s.action_vx > 0) refl = false;
+        if (c.s.action_vx < 0) refl = true;
+        EI(c, F_FLAGS, 0) = refl ? (fl | EF_REFLECTED) : (fl & ~EF_REFLECTED);
+    }
+    wave_sync();
+    if (c.s.special_action > 0 && (c.s.cur_time - c.s.last_fire_time) >= 3) {
+        float theta = 0;
+        const float bullet_vel = 1;
+        if (c.s.special_action == 1) theta = 0;
+        else if (c.s.special_action == 2) theta = PI_F / 4;
+        else if (c.s.special_action == 3) theta = PI_F / 2;
+        else if (c.s.special_action == 4) theta = -1 * PI_F / 4;
+        if (refl) theta = PI_F - theta;
+        double sn, cs;
+        pg_sincos_cr((double)theta, &sn, &cs);
+        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        wave_sync();
+        const int b = append_entity(c, ax, ay, (float)(bullet_vel * cs), (float)(bullet_vel * sn), .25f, .25f,
+                                    NJ_THROWING_STAR);
+        if (b >= 0) {
+            EI(c, F_FLAGS, b) = EF_AUTO_ERASE | EF_COLLIDES | EF_SMART_STEP;
+            EI(c, F_EXPIRE_TIME, b) = 15;
+        }
+        c.s.last_fire_time = c.s.cur_time;
+        wave_sync();
+    }
+}
+
 // ------------------------------------------------------------------ bossfight (bossfight.cpp:252-392)
 DEV void bf_boss_fire(Ctx &c, int boss, float bullet_r, float vel, float theta) { // :252-257
     double sn, cs;
@@ -2260,6 +2404,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_PLUNDER) plunder_step_tail(c, rg);
     if constexpr (G == PG_GAME_STARPILOT) starpilot_step_tail(c, rg);
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_step_tail(c, rg);
+    if constexpr (G == PG_GAME_NINJA) ninja_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -2364,6 +2509,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_PLUNDER) { PG_W(last_fire_time) PG_W(gs) }
         if constexpr (G == PG_GAME_STARPILOT) { PG_W(num_tail) }
         if constexpr (G == PG_GAME_BOSSFIGHT) { PG_W(last_fire_time) PG_W(gs) }
+        if constexpr (G == PG_GAME_NINJA) { PG_W(last_fire_time) PG_W(gs) PG_W(has_support) PG_W(facing_right) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -2393,6 +2539,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_PLUNDER)
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
+        PG_CASE(PG_GAME_NINJA)
     default: break;
     }
 #undef PG_CASE

@@ -278,6 +278,21 @@ BOSSFIGHT_SPRITES = {
        ["misc_assets/meteorGrey_big%d.png" % i for i in range(1, 5)],
 }
 
+# ---------------------------------------------------------------- ninja
+# procgen/src/games/ninja.cpp:45-74 (GOAL 1, BOMB 6, THROWING_STAR 7, PLAYER_JUMP 9, PLAYER_RIGHT1 12,
+# PLAYER_RIGHT2 13, FIRE 14, WALL_MID 20)
+NINJA_SPRITES = {
+    20: ["misc_assets/tile_bricksGrey.png", "misc_assets/tile_bricksGrown.png", "misc_assets/tile_bricksRed.png"],
+    1: ["platformer/shroom%d.png" % i for i in range(1, 7)],
+    0: ["platformer/zombie_idle.png"],
+    9: ["platformer/zombie_jump.png"],
+    12: ["platformer/zombie_walk1.png"],
+    13: ["platformer/zombie_walk2.png"],
+    6: ["misc_assets/bomb.png"],
+    7: ["misc_assets/saw.png"],
+    14: ["misc_assets/bomb.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -293,6 +308,7 @@ GAMES = {
     "plunder": (PLUNDER_SPRITES, "water_surface"),  # plunder.cpp:45-47
     "starpilot": (STARPILOT_SPRITES, "space"),  # starpilot.cpp:56-58
     "bossfight": (BOSSFIGHT_SPRITES, "space"),  # bossfight.cpp:72-74
+    "ninja": (NINJA_SPRITES, "platform"),       # ninja.cpp:43-45
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -66,7 +66,7 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
 GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder",
-         "starpilot", "bossfight"]
+         "starpilot", "bossfight", "ninja"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -154,6 +154,13 @@ def test_bossfight_long():
     """bossfight: shields up / down cycles, reflected bullets (type change mid collision walk), boss
     damage rounds with explosions, laser trails, attack modes 0-3 (sin / cos of the fire angles)."""
     run_pair("bossfight", 32, 800, seed=24, num_levels=0, rand_seed=13)
+
+
+def test_ninja_long_and_easy():
+    """ninja: charged jumps, throwing stars (smart entities that stick to walls, blow up bombs: grid
+    write-through + explosions), fire / bomb deaths, the jump-charge bar; easy mode (visibility 10)."""
+    run_pair("ninja", 32, 600, seed=25, num_levels=0, rand_seed=14)
+    run_pair("ninja", 8, 300, seed=26, num_levels=0, rand_seed=15, distribution_mode="easy")
 
 
 def test_bigfish_long_episodes():
