@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CAVEFLYER = 2, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12, GAME_NINJA = 13, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
 
 static void fatal_msg(const char *m) {
@@ -441,6 +441,8 @@ static bool hook_is_blocked_ents(Game *g, const Entity *src, const Entity *targe
 }
 
 static bool hook_will_reflect(Game *g, int src, int target) {
+    if (g->game_id == GAME_CAVEFLYER) /* caveflyer.cpp:120-122: ENEMY 5 off CAVEWALL 8 / out of bounds */
+        return src == 5 && (target == 8 || target == g->out_of_bounds_object);
     if (g->game_id == GAME_COINRUN) /* coinrun.cpp:140-142 */
         return src == CR_ENEMY && (cr_is_wall(target) || target == CR_ENEMY_BARRIER);
     if (g->game_id == GAME_FRUITBOT) /* fruitbot.cpp:79-81: BAD_OBJ 4 off BARRIER 1 / WALL_OBJ */
@@ -462,6 +464,27 @@ static int spawn_child(Game *g, int src_i, int type, float obj_r) { /* basic-abs
 }
 static void hook_handle_collision(Game *g, int si, int ti) {
     Entity *src = &g->ents[si], *target = &g->ents[ti];
+    if (g->game_id == GAME_CAVEFLYER && target->type == 4) { /* caveflyer.cpp:92-118: PLAYER_BULLET */
+        bool erase_bullet = false;
+        if (src->type == 3) { /* TARGET */
+            src->health -= 1;
+            erase_bullet = true;
+            if (src->health <= 0 && !src->will_erase) {
+                spawn_child(g, si, EXPLOSION, (float)(.5 * src->rx));
+                src->will_erase = true;
+                g->sd_reward += 3.0f; /* TARGET_REWARD */
+            }
+        } else if (src->type == 2 || src->type == 5 || src->type == 1) { /* OBSTACLE, ENEMY, GOAL */
+            erase_bullet = true;
+        }
+        if (erase_bullet && !target->will_erase) {
+            target->will_erase = true;
+            int e = spawn_child(g, ti, EXPLOSION, (float)(.5 * target->rx));
+            g->ents[e].vx = src->vx;
+            g->ents[e].vy = src->vy;
+        }
+        return;
+    }
     if (g->game_id == GAME_BOSSFIGHT) { /* bossfight.cpp:140-190 */
         if (src->type == 1) { /* PLAYER_BULLET */
             bool will_erase = false;
@@ -614,6 +637,14 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 agent->ry += g->r_inc;
                 g->fish_eaten += 1;
             }
+        }
+    } else if (g->game_id == GAME_CAVEFLYER) { /* caveflyer.cpp:57-71 */
+        if (obj->type == 1) { /* GOAL */
+            g->sd_reward += 10.0f;
+            g->sd_level_complete = true;
+            g->sd_done = true;
+        } else if (obj->type == 2 || obj->type == 5 || obj->type == 3) { /* OBSTACLE, ENEMY, TARGET */
+            g->sd_done = true;
         }
     } else if (g->game_id == GAME_NINJA) { /* ninja.cpp:77-87 */
         if (obj->type == EXPLOSION) {
@@ -1005,7 +1036,12 @@ static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299
     else g->action_vy = 0;
 }
 
+static void caveflyer_set_action_xy(Game *g, int move_action);
 static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_CAVEFLYER) {
+        caveflyer_set_action_xy(g, move_action);
+        return;
+    }
     if (g->game_id == GAME_NINJA) { /* ninja.cpp:387-418 */
         g->action_vx = (float)(move_action / 3 - 1);
         g->action_vy = (float)((move_action % 3) - 1);
@@ -1064,6 +1100,14 @@ static void lp_decay_vel(float *vel);
 static double cu_sign(double x);
 static void update_agent_velocity(Game *g) {
     Entity *agent = AG(g);
+    if (g->game_id == GAME_CAVEFLYER) { /* caveflyer.cpp:73-81: no (1 - mixrate) decay */
+        float v_scale = 1.0f;
+        agent->vx = (float)((double)agent->vx + (double)(g->mixrate * g->maxspeed * g->action_vx * v_scale) * .2);
+        agent->vy = (float)((double)agent->vy + (double)(g->mixrate * g->maxspeed * g->action_vy * v_scale) * .2);
+        agent->vx = (float)(.9 * (double)agent->vx);
+        agent->vy = (float)(.9 * (double)agent->vy);
+        return;
+    }
     if (g->game_id == GAME_NINJA) { /* ninja.cpp:108-121 */
         float mixrate_x = g->has_support ? g->mixrate : (g->mixrate * g->air_control);
         agent->vx = (1 - mixrate_x) * agent->vx + mixrate_x * g->maxspeed * g->action_vx;
@@ -3493,6 +3537,272 @@ static void ninja_game_step(Game *g) { /* :420-450 */
     }
 }
 
+/* ================================================================== caveflyer (games/caveflyer.cpp) */
+#define CF_GOAL 1
+#define CF_OBSTACLE 2
+#define CF_TARGET 3
+#define CF_PLAYER_BULLET 4
+#define CF_ENEMY 5
+#define CF_CAVEWALL 8
+#define CF_EXHAUST 9
+#define CF_MARKER 1003
+
+/* RoomGenerator (roomgen.cpp) over the game grid; get_obj(idx) / to_grid_idx follow
+ * basic-abstract-game.cpp:187-203 (out-of-grid -> INVALID_IDX -> out_of_bounds_object) */
+static int rm_to_grid_idx(Game *g, int x, int y) { return grid_contains(g, x, y) ? y * g->grid_w + x : INVALID_IDX; }
+static int rm_get_obj_idx(Game *g, int idx) {
+    if (idx < 0 || idx >= g->grid_w * g->grid_h) return g->out_of_bounds_object;
+    return g->grid[idx];
+}
+static void rm_update(Game *g) { /* roomgen.cpp:3-37: count_neighbors(i, WALL_OBJ) >= 5 over the 3x3 block */
+    static int next_cells[MAX_GRID];
+    for (int i = 0; i < g->grid_size; i++) {
+        int x = i % g->grid_w, y = i / g->grid_w, n = 0;
+        for (int a = -1; a <= 1; a++)
+            for (int b = -1; b <= 1; b++)
+                if (get_obj(g, x + a, y + b) == WALL_OBJ) n++;
+        next_cells[i] = n >= 5 ? WALL_OBJ : SPACE;
+    }
+    for (int i = 0; i < g->grid_size; i++) g->grid[i] = next_cells[i];
+}
+/* build_room (roomgen.cpp:39-70): the start cell joins its own room only when a neighbour
+ * rediscovers it, so an isolated SPACE cell yields an empty room.  Fills `room` (bool per cell),
+ * returns its size. */
+static int rm_build_room(Game *g, int idx, bool *room) {
+    static int queue[MAX_GRID * 4 + 1];
+    int head = 0, tail = 0, size = 0;
+    if (rm_get_obj_idx(g, idx) != SPACE) return 0;
+    queue[tail++] = idx;
+    while (head < tail) {
+        int cur = queue[head++];
+        if (rm_get_obj_idx(g, cur) != SPACE) continue;
+        int x = cur % g->grid_w, y = cur / g->grid_w;
+        for (int i = -1; i <= 1; i++)
+            for (int j = -1; j <= 1; j++)
+                if ((i == 0 || j == 0) && (i + j != 0)) {
+                    int nx = rm_to_grid_idx(g, x + i, y + j);
+                    if (nx >= 0 && !room[nx] && rm_get_obj_idx(g, nx) == SPACE) {
+                        queue[tail++] = nx;
+                        room[nx] = true;
+                        size++;
+                    }
+                }
+    }
+    return size;
+}
+/* find_best_room (roomgen.cpp:116-136): first room (scan order) of strictly largest size */
+static int rm_find_best_room(Game *g, bool *best) {
+    static bool all_rooms[MAX_GRID], next_room[MAX_GRID];
+    int best_size = -1;
+    memset(all_rooms, 0, sizeof(all_rooms));
+    memset(best, 0, MAX_GRID);
+    for (int i = 0; i < g->grid_size; i++) {
+        if (rm_get_obj_idx(g, i) == SPACE && !all_rooms[i]) {
+            memset(next_room, 0, sizeof(next_room));
+            int sz = rm_build_room(g, i, next_room);
+            for (int k = 0; k < g->grid_size; k++) all_rooms[k] = all_rooms[k] || next_room[k];
+            if (sz > best_size) {
+                best_size = sz;
+                memcpy(best, next_room, MAX_GRID);
+            }
+        }
+    }
+    return best_size;
+}
+/* find_path (roomgen.cpp:72-114): BFS whose `covered` set never holds the source */
+static int rm_find_path(Game *g, int src, int dst, int *path) {
+    static int expanded[MAX_GRID + 2], parents[MAX_GRID + 2], tmp[MAX_GRID + 2];
+    static bool covered[MAX_GRID];
+    int n = 0, search_idx = 0;
+    if (rm_get_obj_idx(g, src) != SPACE) return 0;
+    memset(covered, 0, sizeof(covered));
+    expanded[n] = src;
+    parents[n++] = -1;
+    while (search_idx < n) {
+        int cur = expanded[search_idx];
+        if (cur == dst) break;
+        fassert(rm_get_obj_idx(g, cur) == SPACE);
+        int x = cur % g->grid_w, y = cur / g->grid_w;
+        for (int i = -1; i <= 1; i++)
+            for (int j = -1; j <= 1; j++)
+                if ((i == 0 || j == 0) && (i + j != 0)) {
+                    int nx = rm_to_grid_idx(g, x + i, y + j);
+                    if (nx >= 0 && !covered[nx] && rm_get_obj_idx(g, nx) == SPACE) {
+                        fassert(n < MAX_GRID + 2);
+                        expanded[n] = nx;
+                        parents[n++] = search_idx;
+                        covered[nx] = true;
+                    }
+                }
+        search_idx++;
+    }
+    fassert(search_idx < n && expanded[search_idx] == dst);
+    int t = 0;
+    while (search_idx >= 0) {
+        tmp[t++] = expanded[search_idx];
+        search_idx = parents[search_idx];
+    }
+    for (int j = t - 1; j >= 0; j--) path[t - 1 - j] = tmp[j];
+    return t;
+}
+/* expand_room (roomgen.cpp:138-177): n rounds of 8-neighbour growth through SPACE cells */
+static void rm_expand_room(Game *g, bool *set, int n) {
+    static bool curr[MAX_GRID], next[MAX_GRID];
+    memcpy(curr, set, MAX_GRID);
+    for (int loop = 0; loop < n; loop++) {
+        memset(next, 0, sizeof(next));
+        for (int cur = 0; cur < g->grid_size; cur++) {
+            if (!curr[cur] || rm_get_obj_idx(g, cur) != SPACE) continue;
+            int x = cur % g->grid_w, y = cur / g->grid_w;
+            for (int i = -1; i <= 1; i++)
+                for (int j = -1; j <= 1; j++)
+                    if (i != 0 || j != 0) {
+                        int nx = rm_to_grid_idx(g, x + i, y + j);
+                        if (nx >= 0 && !set[nx] && rm_get_obj_idx(g, nx) == SPACE) {
+                            set[nx] = true;
+                            next[nx] = true;
+                        }
+                    }
+        }
+        memcpy(curr, next, MAX_GRID);
+    }
+}
+
+static void caveflyer_ctor(Game *g) { g->mixrate = 0.9f; } /* caveflyer.cpp:25-29 */
+
+static void caveflyer_choose_world_dim(Game *g) { /* :128-143 */
+    int d = g->options.distribution_mode, world_dim = 20;
+    if (d == EasyMode) world_dim = 30;
+    else if (d == HardMode) world_dim = 40;
+    else if (d == MemoryMode) world_dim = 60;
+    g->main_width = world_dim;
+    g->main_height = world_dim;
+}
+
+static void caveflyer_game_reset(Game *g, const or_atlas *at) { /* :145-265 */
+    static bool best_room[MAX_GRID], wide_path[MAX_GRID];
+    static int free_cells[MAX_GRID], goal_path[MAX_GRID + 2], sel[MAX_GRID];
+    MT *r = &g->rand_gen;
+    caveflyer_choose_world_dim(g);
+    basic_game_reset(g, at);
+    g->out_of_bounds_object = WALL_OBJ;
+    for (int i = 0; i < g->grid_size; i++) g->grid[i] = rg_rand01(r) < .5 ? WALL_OBJ : SPACE;
+    for (int it = 0; it < 4; it++) rm_update(g);
+    int best = rm_find_best_room(g, best_room);
+    fassert(best > 0);
+    for (int i = 0; i < g->grid_size; i++) g->grid[i] = WALL_OBJ;
+    int nfree = 0;
+    for (int i = 0; i < g->grid_size; i++)
+        if (best_room[i]) {
+            g->grid[i] = SPACE;
+            free_cells[nfree++] = i;
+        }
+    rg_simple_choose(r, nfree, 2, sel);
+    int agent_cell = free_cells[sel[0]], goal_cell = free_cells[sel[1]];
+    Entity *agent = AG(g);
+    agent->x = (float)((agent_cell % g->main_width) + .5);
+    agent->y = (float)((agent_cell / g->main_width) + .5);
+    int ge = add_entity(g, (float)((goal_cell % g->main_width) + .5), (float)((goal_cell / g->main_width) + .5), 0, 0,
+                        .5, CF_GOAL); /* spawn_entity_at_idx (:587-594) */
+    g->ents[ge].collides_with_entities = true;
+    int npath = rm_find_path(g, agent_cell, goal_cell, goal_path);
+    if (g->options.distribution_mode != MemoryMode) { /* should_prune */
+        memset(wide_path, 0, sizeof(wide_path));
+        for (int k = 0; k < npath; k++) wide_path[goal_path[k]] = true;
+        rm_expand_room(g, wide_path, 4);
+        for (int i = 0; i < g->grid_size; i++) g->grid[i] = wide_path[i] ? SPACE : WALL_OBJ;
+    }
+    for (int it = 0; it < 4; it++) {
+        rm_update(g);
+        for (int k = 0; k < npath; k++) g->grid[goal_path[k]] = SPACE;
+    }
+    for (int k = 0; k < npath; k++) g->grid[goal_path[k]] = CF_MARKER;
+    nfree = 0;
+    for (int i = 0; i < g->grid_size; i++) {
+        if (g->grid[i] == SPACE) free_cells[nfree++] = i;
+        else if (g->grid[i] == WALL_OBJ) g->grid[i] = CF_CAVEWALL;
+    }
+    int chunk_size = nfree / 80, num_objs = 3 * chunk_size;
+    rg_simple_choose(r, nfree, num_objs, sel);
+    for (int i = 0; i < num_objs; i++) {
+        int val = free_cells[sel[i]];
+        float x = (float)((val % g->main_width) + .5), y = (float)((val / g->main_width) + .5);
+        if (i < chunk_size) {
+            int e = add_entity(g, x, y, 0, 0, .5, CF_OBSTACLE);
+            g->ents[e].collides_with_entities = true;
+        } else if (i < 2 * chunk_size) {
+            int e = add_entity(g, x, y, 0, 0, .5, CF_TARGET);
+            g->ents[e].health = 5;
+            g->ents[e].collides_with_entities = true;
+        } else {
+            int e = add_entity(g, x, y, 0, 0, .5, CF_ENEMY);
+            /* (.1 * rand01() + .1) * (randn(2) * 2 - 1): left operand drawn first (pinned,
+             * oracle/ref_harness.cpp ref_caveflyer_enemy_vel) */
+            double mag = .1 * (double)rg_rand01(r) + .1;
+            int sgn = rg_randn(r, 2) * 2 - 1;
+            float vel = (float)(mag * sgn);
+            if (rg_rand01(r) < .5) g->ents[e].vx = vel;
+            else g->ents[e].vy = vel;
+            g->ents[e].smart_step = true;
+            g->ents[e].collides_with_entities = true;
+        }
+    }
+    for (int i = 0; i < g->grid_size; i++)
+        if (g->grid[i] == CF_MARKER) g->grid[i] = SPACE;
+    g->out_of_bounds_object = CF_CAVEWALL;
+    g->visibility = g->options.distribution_mode == EasyMode ? 10 : 16;
+}
+
+static void caveflyer_set_action_xy(Game *g, int move_action) { /* :267-287 */
+    float acceleration = (float)(move_action % 3 - 1);
+    if (acceleration < 0) acceleration *= 0.33f;
+    Entity *agent = AG(g);
+    float theta = -1 * agent->rotation + PI_F / 2;
+    if (acceleration > 0) {
+        int e = add_entity(g, (float)(agent->x - agent->rx * cos((double)theta)),
+                           (float)(agent->y - agent->ry * sin((double)theta)), 0, 0, (float)(.5 * agent->rx), CF_EXHAUST);
+        agent = AG(g);
+        g->ents[e].expire_time = 4;
+        g->ents[e].rotation = -1 * theta - PI_F / 2;
+        g->ents[e].grow_rate = 1.25;
+        g->ents[e].alpha_decay = 0.8f;
+    }
+    g->action_vy = (float)(acceleration * sin((double)theta));
+    g->action_vx = (float)(acceleration * cos((double)theta));
+    g->action_vrot = (float)(move_action / 3 - 1);
+}
+
+static void caveflyer_game_step(Game *g) { /* :289-324 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->special_action == 1) {
+        float theta = -1 * agent->rotation + PI_F / 2;
+        float vx = (float)cos((double)theta), vy = (float)sin((double)theta);
+        float ax = agent->x, ay = agent->y, arot = agent->rotation;
+        int b = add_entity_rxy(g, ax, ay, vx, vy, 0.1f, 0.25f, CF_PLAYER_BULLET);
+        g->ents[b].expire_time = 10;
+        g->ents[b].rotation = arot;
+    }
+    for (int ei = g->num_ents - 1; ei >= 0; ei--) {
+        Entity *ent = &g->ents[ei];
+        if (ent->type == CF_ENEMY) { /* face_direction(vx, vy, -PI / 2) (entity.cpp:84-88) */
+            if (ent->vx != 0 || ent->vy != 0) ent->rotation = -1 * atan2f(ent->vy, ent->vx) + (-1 * PI_F / 2);
+        }
+        if (ent->type != CF_PLAYER_BULLET) continue;
+        bool found_wall = false;
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 2; j++) {
+                int t2 = get_obj_from_floats(g, ent->x + ent->rx * (float)(2 * i - 1), ent->y + ent->ry * (float)(2 * j - 1));
+                found_wall = found_wall || t2 == CF_CAVEWALL;
+            }
+        if (found_wall) {
+            ent->will_erase = true;
+            spawn_child(g, ei, EXPLOSION, (float)(.5 * ent->rx));
+        }
+    }
+    erase_if_needed(g);
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -3646,6 +3956,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_STARPILOT) starpilot_game_reset(g, at);
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_reset(g, at);
     else if (g->game_id == GAME_NINJA) ninja_game_reset(g, at);
+    else if (g->game_id == GAME_CAVEFLYER) caveflyer_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -3663,6 +3974,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_STARPILOT) starpilot_game_step(g, at);
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_step(g);
     else if (g->game_id == GAME_NINJA) ninja_game_step(g);
+    else if (g->game_id == GAME_CAVEFLYER) caveflyer_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -4309,6 +4621,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "starpilot") == 0) return GAME_STARPILOT;
     if (strcmp(name, "bossfight") == 0) return GAME_BOSSFIGHT;
     if (strcmp(name, "ninja") == 0) return GAME_NINJA;
+    if (strcmp(name, "caveflyer") == 0) return GAME_CAVEFLYER;
     return -1;
 }
 
@@ -4471,6 +4784,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         else if (gid == GAME_STARPILOT) starpilot_ctor(g);
         else if (gid == GAME_BOSSFIGHT) bossfight_ctor(g);
         else if (gid == GAME_NINJA) ninja_ctor(g);
+        else if (gid == GAME_CAVEFLYER) caveflyer_ctor(g);
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;

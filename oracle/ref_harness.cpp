@@ -135,3 +135,12 @@ void ref_leaper_lane_speed(int32_t seed, float lo, float hi, float *out) {
     out[0] = g.road_lane_speeds[0];
 }
 }
+
+// caveflyer.cpp:235: float vel = (.1 * rand_gen.rand01() + .1) * (rand_gen.randn(2) * 2 - 1) --
+// which operand of the `*` draws first, pinned with the reference's compiler and flags.
+extern "C" void ref_caveflyer_enemy_vel(int32_t seed, float *out) {
+    RandGen rand_gen;
+    rand_gen.seed(seed);
+    float vel = (.1 * rand_gen.rand01() + .1) * (rand_gen.randn(2) * 2 - 1);
+    out[0] = vel;
+}

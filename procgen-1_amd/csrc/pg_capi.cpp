@@ -121,9 +121,10 @@ int game_id(const std::string &name) {
     if (name == "starpilot") return PG_GAME_STARPILOT;
     if (name == "bossfight") return PG_GAME_BOSSFIGHT;
     if (name == "ninja") return PG_GAME_NINJA;
+    if (name == "caveflyer") return PG_GAME_CAVEFLYER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, bossfight, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, ninja, plunder, starpilot";
+const char *SUPPORTED_GAMES = "bigfish, bossfight, caveflyer, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, ninja, plunder, starpilot";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;
@@ -183,6 +184,8 @@ void construct_env(PGEnv &s, int gid) {
         s.maxspeed = 0.85f;
         s.bg_tile_ratio = -1;
         s.out_of_bounds_object = 2; // OUT_OF_BOUNDS_WALL
+    } else if (gid == PG_GAME_CAVEFLYER) { // caveflyer.cpp:25-29
+        s.mixrate = 0.9f;
     } else if (gid == PG_GAME_NINJA) { // ninja.cpp:35-41
         s.main_width = 64;
         s.main_height = 64;

@@ -165,6 +165,15 @@ DEV float sp_hp_prob(int mode, int type) {
 #define BF_BOTTOM_MARGIN 6
 #define BF_BOSS_VEL_TIMEOUT 20
 #define BF_BOSS_DAMAGED_TIMEOUT 40
+// caveflyer.cpp:12-21
+#define CF_GOAL 1
+#define CF_OBSTACLE 2
+#define CF_TARGET 3
+#define CF_PLAYER_BULLET 4
+#define CF_ENEMY 5
+#define CF_CAVEWALL 8
+#define CF_EXHAUST 9
+#define CF_MARKER 1003
 // ninja.cpp:11-21
 #define NJ_GOAL 1
 #define NJ_BOMB 6

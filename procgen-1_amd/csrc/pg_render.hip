@@ -1140,6 +1140,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
+        PG_CASE(PG_GAME_CAVEFLYER)
     default: break;
     }
 #undef PG_CASE

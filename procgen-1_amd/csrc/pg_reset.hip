@@ -60,6 +60,15 @@ struct SpawnerScratch {
     int16_t stack[3 * 64];
 };
 template <> struct Scratch<PG_GAME_STARPILOT> { SpawnerScratch sp; };
+// caveflyer's RoomGenerator (roomgen.cpp) over the LDS grid (world up to 60 x 60, memory mode)
+struct CaveScratch {
+    int16_t a[PG_GRID_MAX];         // CA next cells, then component labels, then BFS parent cells
+    int32_t b[PG_GRID_MAX];         // component sizes, then BFS discovery keys, then picks
+    int16_t list[PG_GRID_MAX + 1];  // BFS frontier, then free cells
+    int16_t list2[PG_GRID_MAX + 1]; // next frontier, then the goal path
+    uint8_t f[PG_GRID_MAX];         // CF_* bits per cell
+};
+template <> struct Scratch<PG_GAME_CAVEFLYER> { CaveScratch cf; };
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -205,6 +214,14 @@ DEV void choose_world_dim(RCtx &c) {
         int world_dim = 20;
         if (d == PG_EASY) world_dim = 9;
         else if (d == PG_HARD) world_dim = 15;
+        c.s.main_width = world_dim;
+        c.s.main_height = world_dim;
+    }
+    if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:128-143
+        int d = c.s.opt_distribution_mode, world_dim = 20;
+        if (d == PG_EASY) world_dim = 30;
+        else if (d == PG_HARD) world_dim = 40;
+        else if (d == PG_MEMORY) world_dim = 60;
         c.s.main_width = world_dim;
         c.s.main_height = world_dim;
     }
@@ -1732,6 +1749,334 @@ DEV void ninja_game_reset(RCtx &c) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ caveflyer (caveflyer.cpp:145-265)
+// RoomGenerator (roomgen.cpp) restated lane-parallel on the LDS grid:
+//  * update(): the cellular automaton reads the whole grid before writing (next_cells), so it is a
+//    pull over cells into a scratch copy;
+//  * find_best_room(): rooms are the 4-connected SPACE components, labelled with their smallest
+//    cell index by min-propagation + pointer jumping; build_room() leaves an isolated cell's room
+//    empty (the start cell only joins when a neighbour rediscovers it), so a room's size is its
+//    cell count when >= 2, else 0, and the first room in scan order of strictly largest size wins;
+//  * find_path(): a level-synchronous BFS that reproduces the FIFO's discovery order: a cell's
+//    parent is the frontier entry (frontier order, then neighbour order (-1,0), (0,-1), (0,1),
+//    (1,0)) with the smallest key p * 4 + k, and the next frontier is written in key order.  The
+//    source never enters `covered`, so it is rediscovered once at depth 2 and expands nothing;
+//    the path follows parents from the goal back to the source;
+//  * expand_room(set, 4): four pull rounds of 8-neighbour growth through SPACE cells.
+#define CF_ROOM 1
+#define CF_COVERED 2
+#define CF_SET 4
+#define CF_CURR 8
+#define CF_NEW 16
+#define CF_TAKEN 32
+
+DEV void cf_random_fill(RCtx &c) { // rand01() < .5 ? WALL_OBJ : SPACE per cell, draws in cell order
+    const int n = c.s.main_width * c.s.main_height;
+    for (int base = 0; base < n;) {
+        if (c.mti >= PG_MT_N) {
+            mt_twist_lds(c.mt);
+            c.mti = 0;
+        }
+        int m = PG_MT_N - c.mti;
+        if (m > 64) m = 64;
+        if (m > n - base) m = n - base;
+        if (LANE < m) c.grid[base + LANE] = rg_rand01_of(mt_temper(c.mt[c.mti + LANE])) < .5 ? WALL_OBJ : SPACE;
+        c.mti += m;
+        base += m;
+        wave_sync();
+    }
+}
+
+DEV void cf_update(RCtx &c, CaveScratch *S) { // roomgen.cpp:3-37 (count_neighbors(i, WALL_OBJ) >= 5)
+    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    for (int i = LANE; i < n; i += 64) {
+        const int x = i % W, y = i / W;
+        int cnt = 0;
+        for (int a = -1; a <= 1; a++)
+            for (int b = -1; b <= 1; b++) {
+                const int xx = x + a, yy = y + b;
+                const int v = (0 <= xx && xx < W && 0 <= yy && yy < H) ? c.grid[yy * W + xx] : c.s.out_of_bounds_object;
+                cnt += v == WALL_OBJ;
+            }
+        S->a[i] = cnt >= 5 ? WALL_OBJ : SPACE;
+    }
+    wave_sync();
+    for (int i = LANE; i < n; i += 64) c.grid[i] = S->a[i];
+    wave_sync();
+}
+
+// find_best_room (roomgen.cpp:116-136) -> label of the best room (cells with a[i] == label), or -1
+DEV int cf_find_best_room(RCtx &c, CaveScratch *S) {
+    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    for (int i = LANE; i < n; i += 64) {
+        S->a[i] = c.grid[i] == SPACE ? (int16_t)i : (int16_t)-1;
+        S->b[i] = 0;
+    }
+    wave_sync();
+    for (;;) {
+        bool changed = false;
+        for (int i = LANE; i < n; i += 64) {
+            int l = S->a[i];
+            if (l < 0) continue;
+            int m = l;
+            const int x = i % W, y = i / W;
+            if (x > 0 && S->a[i - 1] >= 0 && S->a[i - 1] < m) m = S->a[i - 1];
+            if (x < W - 1 && S->a[i + 1] >= 0 && S->a[i + 1] < m) m = S->a[i + 1];
+            if (y > 0 && S->a[i - W] >= 0 && S->a[i - W] < m) m = S->a[i - W];
+            if (y < H - 1 && S->a[i + W] >= 0 && S->a[i + W] < m) m = S->a[i + W];
+            m = S->a[m] < m ? S->a[m] : m; // pointer jump (labels are cells of the same component)
+            if (m < l) {
+                S->a[i] = (int16_t)m;
+                changed = true;
+            }
+        }
+        wave_sync();
+        if (!ballot(changed)) break;
+    }
+    for (int i = LANE; i < n; i += 64)
+        if (S->a[i] >= 0) atomicAdd(&S->b[S->a[i]], 1);
+    wave_sync();
+    int best = -1; // key = size * 4096 + (4095 - label): largest room, first in scan order
+    for (int i = LANE; i < n; i += 64) {
+        if (S->a[i] == i) {
+            const int sz = S->b[i] >= 2 ? S->b[i] : 0;
+            const int key = sz * 4096 + (4095 - i);
+            if (key > best) best = key;
+        }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int o = __shfl_xor(best, off);
+        if (o > best) best = o;
+    }
+    wave_sync();
+    if (best < 4096) return -1; // no room or only isolated cells: fassert(best_room.size() > 0)
+    return 4095 - (best & 4095);
+}
+
+// find_path (roomgen.cpp:72-114): writes the path's cells (any order) to S->list2, returns its length
+DEV int cf_find_path(RCtx &c, CaveScratch *S, int src, int dst) {
+    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    for (int i = LANE; i < n; i += 64) {
+        S->b[i] = 0x7fffffff;
+        S->f[i] &= (uint8_t)~CF_COVERED;
+    }
+    if (LANE == 0) S->list[0] = (int16_t)src;
+    wave_sync();
+    int16_t *fr = S->list, *nx = S->list2;
+    int nf = 1;
+    bool found = false;
+    while (nf > 0 && !found) {
+        for (int p = LANE; p < nf; p += 64) { // discovery keys
+            const int u = fr[p], x = u % W, y = u / W;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int xx = x + (k == 0 ? -1 : (k == 3 ? 1 : 0)), yy = y + (k == 1 ? -1 : (k == 2 ? 1 : 0));
+                if (0 <= xx && xx < W && 0 <= yy && yy < H) {
+                    const int v = yy * W + xx;
+                    if (c.grid[v] == SPACE && !(S->f[v] & CF_COVERED)) atomicMin(&S->b[v], p * 4 + k);
+                }
+            }
+        }
+        wave_sync();
+        int cnt = 0;
+        for (int base = 0; base < nf; base += 64) { // winners, written in key order
+            const int p = base + LANE;
+            int wm = 0, u = 0;
+            if (p < nf) {
+                u = fr[p];
+                const int x = u % W, y = u / W;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int xx = x + (k == 0 ? -1 : (k == 3 ? 1 : 0)), yy = y + (k == 1 ? -1 : (k == 2 ? 1 : 0));
+                    if (0 <= xx && xx < W && 0 <= yy && yy < H) {
+                        const int v = yy * W + xx;
+                        if (!(S->f[v] & CF_COVERED) && S->b[v] == p * 4 + k) wm |= 1 << k;
+                    }
+                }
+            }
+            const int nw = __popc(wm);
+            const unsigned long long lt = (1ull << LANE) - 1ull;
+            const unsigned long long b0 = ballot(nw & 1), b1 = ballot(nw & 2), b2 = ballot(nw & 4);
+            int o = cnt + __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+            const int x = u % W, y = u / W;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (wm & (1 << k)) {
+                    const int v = (y + (k == 1 ? -1 : (k == 2 ? 1 : 0))) * W + x + (k == 0 ? -1 : (k == 3 ? 1 : 0));
+                    nx[o++] = (int16_t)v;
+                    S->a[v] = (int16_t)u;
+                }
+            }
+            cnt += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        }
+        wave_sync();
+        bool hit = false;
+        for (int q = LANE; q < cnt; q += 64) {
+            const int v = nx[q];
+            S->f[v] |= CF_COVERED;
+            hit = hit || v == dst;
+        }
+        found = ballot(hit) != 0;
+        wave_sync();
+        int16_t *t = fr;
+        fr = nx;
+        nx = t;
+        nf = cnt;
+    }
+    if (!found) {
+        c.s.error = PG_ERR_GRID;
+        return 0;
+    }
+    // parent chain dst -> src (serial; the path is a set for every later use)
+    int len = 0;
+    if (LANE == 0) {
+        int v = dst;
+        for (;;) {
+            S->list2[len++] = (int16_t)v;
+            if (v == src || len > n) break;
+            v = S->a[v];
+        }
+    }
+    len = __shfl(len, 0);
+    wave_sync();
+    return len;
+}
+
+DEV void cf_expand_room(RCtx &c, CaveScratch *S, int rounds) { // expand_room (roomgen.cpp:138-177)
+    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    for (int r = 0; r < rounds; r++) {
+        for (int i = LANE; i < n; i += 64) {
+            const uint8_t fi = S->f[i];
+            bool add = false;
+            if (!(fi & CF_SET) && c.grid[i] == SPACE) {
+                const int x = i % W, y = i / W;
+                for (int a = -1; a <= 1; a++)
+                    for (int b = -1; b <= 1; b++) {
+                        const int xx = x + a, yy = y + b;
+                        if ((a != 0 || b != 0) && 0 <= xx && xx < W && 0 <= yy && yy < H) {
+                            const int v = yy * W + xx;
+                            if ((S->f[v] & CF_CURR) && c.grid[v] == SPACE) add = true;
+                        }
+                    }
+            }
+            if (add) S->f[i] = fi | CF_NEW;
+        }
+        wave_sync();
+        for (int i = LANE; i < n; i += 64) {
+            uint8_t fi = S->f[i] & (uint8_t)~CF_CURR;
+            if (fi & CF_NEW) fi = (uint8_t)((fi & ~CF_NEW) | CF_SET | CF_CURR);
+            S->f[i] = fi;
+        }
+        wave_sync();
+    }
+}
+
+DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
+    base_game_reset<PG_GAME_CAVEFLYER>(c);
+    const int W = c.s.main_width, n = W * c.s.main_height;
+    c.s.out_of_bounds_object = WALL_OBJ;
+    cf_random_fill(c);
+    for (int it = 0; it < 4; it++) cf_update(c, S);
+    const int best = cf_find_best_room(c, S);
+    if (best < 0) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    // the best room stays SPACE, its cells (ascending) are the free cells
+    int nfree = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + LANE;
+        const bool in = i < n && S->a[i] == best;
+        if (i < n) {
+            c.grid[i] = in ? SPACE : WALL_OBJ;
+            S->f[i] = 0;
+        }
+        const unsigned long long m = ballot(in);
+        if (in) S->list[nfree + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        nfree += __popcll(m);
+    }
+    wave_sync();
+    // simple_choose(free_cells.size(), 2) (fassert(k <= n), randgen.cpp:74)
+    if (nfree < 2) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    int pick0 = randn(c, nfree), pick1 = randn(c, nfree);
+    while (pick1 == pick0) pick1 = randn(c, nfree);
+    const int agent_cell = S->list[pick0], goal_cell = S->list[pick1];
+    EF(c, F_X, 0) = (float)((agent_cell % W) + .5);
+    EF(c, F_Y, 0) = (float)((agent_cell / W) + .5);
+    wave_sync();
+    int ge = add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, CF_GOAL);
+    EI(c, F_FLAGS, ge) = EF_AUTO_ERASE | EF_COLLIDES;
+    const int npath = cf_find_path(c, S, agent_cell, goal_cell);
+    if (c.s.opt_distribution_mode != PG_MEMORY) { // should_prune: wide path = path grown 4 times
+        for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
+        wave_sync();
+        cf_expand_room(c, S, 4);
+        for (int i = LANE; i < n; i += 64) c.grid[i] = (S->f[i] & CF_SET) ? SPACE : WALL_OBJ;
+        wave_sync();
+    }
+    for (int it = 0; it < 4; it++) {
+        cf_update(c, S);
+        for (int q = LANE; q < npath; q += 64) c.grid[S->list2[q]] = SPACE;
+        wave_sync();
+    }
+    for (int q = LANE; q < npath; q += 64) c.grid[S->list2[q]] = CF_MARKER;
+    wave_sync();
+    nfree = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + LANE;
+        int v = i < n ? c.grid[i] : -1;
+        const bool sp = v == SPACE;
+        if (v == WALL_OBJ) c.grid[i] = CF_CAVEWALL;
+        if (i < n) S->f[i] = 0;
+        const unsigned long long m = ballot(sp);
+        if (sp) S->list[nfree + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        nfree += __popcll(m);
+    }
+    wave_sync();
+    const int chunk_size = nfree / 80, num_objs = 3 * chunk_size;
+    // simple_choose(free_cells.size(), num_objs): rejection against the picks so far
+    for (int i = 0; i < num_objs; i++) {
+        int next = randn(c, nfree);
+        while (S->f[next] & CF_TAKEN) next = randn(c, nfree);
+        wave_sync();
+        if (LANE == 0) {
+            S->f[next] |= CF_TAKEN;
+            S->b[i] = next;
+        }
+        wave_sync();
+    }
+    for (int i = 0; i < num_objs; i++) {
+        const int val = S->list[S->b[i]];
+        const float x = (float)((val % W) + .5), y = (float)((val / W) + .5);
+        if (i < chunk_size) {
+            const int e = add_entity(c, x, y, 0, 0, .5f, CF_OBSTACLE);
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES;
+        } else if (i < 2 * chunk_size) {
+            const int e = add_entity(c, x, y, 0, 0, .5f, CF_TARGET);
+            EF(c, F_HEALTH, e) = 5;
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES;
+        } else {
+            const int e = add_entity(c, x, y, 0, 0, .5f, CF_ENEMY);
+            // (.1 * rand01() + .1) * (randn(2) * 2 - 1): left operand first (g++, pinned in
+            // tests/test_oracle_pins.py)
+            const double mag = .1 * (double)rand01(c) + .1;
+            const int sgn = randn(c, 2) * 2 - 1;
+            const float vel = (float)(mag * sgn);
+            if (rand01(c) < .5) EF(c, F_VX, e) = vel;
+            else EF(c, F_VY, e) = vel;
+            EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES | EF_SMART_STEP;
+        }
+    }
+    for (int i = LANE; i < n; i += 64)
+        if (c.grid[i] == CF_MARKER) c.grid[i] = SPACE;
+    wave_sync();
+    c.s.out_of_bounds_object = CF_CAVEWALL;
+    c.s.visibility = c.s.opt_distribution_mode == PG_EASY ? 10 : 16;
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -2062,6 +2407,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_STARPILOT) starpilot_game_reset(c, &scratch->sp);
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_game_reset(c);
     if constexpr (G == PG_GAME_NINJA) ninja_game_reset(c);
+    if constexpr (G == PG_GAME_CAVEFLYER) caveflyer_game_reset(c, &scratch->cf);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -2170,6 +2516,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
+        PG_CASE(PG_GAME_CAVEFLYER)
     default: break;
     }
 #undef PG_CASE

@@ -196,6 +196,8 @@ DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-5
         return src == CL_ENEMY && (cl_is_wall(target) || target == CL_ENEMY_BARRIER);
     if constexpr (G == PG_GAME_FRUITBOT) // fruitbot.cpp:79-81
         return src == FB_BAD_OBJ && (target == FB_BARRIER || target == WALL_OBJ);
+    if constexpr (G == PG_GAME_CAVEFLYER) // caveflyer.cpp:120-122 (out_of_bounds_object = CAVEWALL)
+        return src == CF_ENEMY && target == CF_CAVEWALL;
     if constexpr (G == PG_GAME_DODGEBALL) // dodgeball.cpp:98-100 (out_of_bounds_object = OOB_WALL)
         return src == DB_ENEMY && (target == DB_LAVA_WALL || target == DB_OOB_WALL);
     if constexpr (G == PG_GAME_MINER) // miner.cpp:77-79 (out_of_bounds_object = OOB_WALL)
@@ -601,8 +603,33 @@ DEV void erase_if_needed(Ctx &c) {
 }
 
 // ------------------------------------------------------------------ agent control
+DEV int append_entity(Ctx &c, float x, float y, float vx, float vy, float rx, float ry, int type);
 template <int G>
 DEV void set_action_xy(Ctx &c, int move_action) {
+    if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:267-287: thrust along the heading
+        float acceleration = (float)(move_action % 3 - 1);
+        if (acceleration < 0) acceleration *= 0.33f;
+        const float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+        const float theta = -1 * EF(c, F_ROTATION, 0) + PI_F / 2;
+        double sn, cs; // cos / sin of a float: the double C library functions (correctly rounded)
+        pg_sincos_cr((double)theta, &sn, &cs);
+        if (acceleration > 0) {
+            wave_sync();
+            const int e = append_entity(c, (float)((double)ax - (double)arx * cs), (float)((double)ay - (double)ary * sn), 0,
+                                        0, (float)(.5 * arx), (float)(.5 * arx), CF_EXHAUST);
+            if (e >= 0) {
+                EI(c, F_EXPIRE_TIME, e) = 4;
+                EF(c, F_ROTATION, e) = -1 * theta - PI_F / 2;
+                EF(c, F_GROW_RATE, e) = 1.25f;
+                EF(c, F_ALPHA_DECAY, e) = 0.8f;
+            }
+            wave_sync();
+        }
+        c.s.action_vy = (float)(acceleration * sn);
+        c.s.action_vx = (float)(acceleration * cs);
+        c.s.action_vrot = (float)(move_action / 3 - 1);
+        return;
+    }
     c.s.action_vx = (float)(move_action / 3 - 1); // basic :667-671
     c.s.action_vy = (float)((move_action % 3) - 1);
     if constexpr (G == PG_GAME_COINRUN) { // coinrun.cpp:451-472
@@ -702,6 +729,12 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!c.s.has_support) {
             if (vy > -2) vy -= c.s.gravity;
         }
+    } else if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:73-81: no (1 - mixrate) decay
+        const float v_scale = 1.0f;
+        vx = (float)((double)vx + (double)(c.s.mixrate * c.s.maxspeed * c.s.action_vx * v_scale) * .2);
+        vy = (float)((double)vy + (double)(c.s.mixrate * c.s.maxspeed * c.s.action_vy * v_scale) * .2);
+        vx = (float)(.9 * (double)vx);
+        vy = (float)(.9 * (double)vy);
     } else if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:117-128
         float mixrate_x = c.s.has_support ? c.s.mixrate : (c.s.mixrate * c.s.air_control);
         vx = (1 - mixrate_x) * vx + mixrate_x * c.s.maxspeed * c.s.action_vx;
@@ -779,6 +812,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:57-71
+        if (t == CF_GOAL) {
+            c.s.sd_reward += 10.0f; // GOAL_REWARD
+            c.s.sd_level_complete = 1;
+            c.s.sd_done = 1;
+        } else if (t == CF_OBSTACLE || t == CF_ENEMY || t == CF_TARGET) {
+            c.s.sd_done = 1;
         }
     } else if constexpr (G == PG_GAME_NINJA) { // ninja.cpp:77-87
         if (t == EXPLOSION) {
@@ -902,6 +943,35 @@ DEV void bf_prepare_boss(Ctx &c, int boss) { // bossfight.cpp:192-199
 DEV bool sp_destructible(int t) { return t == SP_FLYER || t == SP_FAST_FLYER || t == SP_TURRET || t == SP_METEOR; }
 template <int G>
 DEV void handle_collision(Ctx &c, int si, int ti) {
+    if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:92-118: only a PLAYER_BULLET target acts
+        if (EI(c, F_TYPE, ti) == CF_PLAYER_BULLET) {
+            const int st = EI(c, F_TYPE, si);
+            bool erase_bullet = false;
+            if (st == CF_TARGET) {
+                const float h = EF(c, F_HEALTH, si) - 1;
+                EF(c, F_HEALTH, si) = h;
+                erase_bullet = true;
+                const int sf = EI(c, F_FLAGS, si);
+                if (h <= 0 && !(sf & EF_WILL_ERASE)) {
+                    const float sx = EF(c, F_X, si), sy = EF(c, F_Y, si), r = (float)(.5 * EF(c, F_RX, si));
+                    wave_sync();
+                    append_entity(c, sx, sy, 0, 0, r, r, EXPLOSION); // spawn_child(src, EXPLOSION, .5 * rx)
+                    EI(c, F_FLAGS, si) = sf | EF_WILL_ERASE;
+                    c.s.sd_reward += 3.0f; // TARGET_REWARD
+                }
+            } else if (st == CF_OBSTACLE || st == CF_ENEMY || st == CF_GOAL) {
+                erase_bullet = true;
+            }
+            const int tf = EI(c, F_FLAGS, ti);
+            if (erase_bullet && !(tf & EF_WILL_ERASE)) {
+                EI(c, F_FLAGS, ti) = tf | EF_WILL_ERASE;
+                const float tx = EF(c, F_X, ti), ty = EF(c, F_Y, ti), r = (float)(.5 * EF(c, F_RX, ti));
+                const float svx = EF(c, F_VX, si), svy = EF(c, F_VY, si);
+                wave_sync();
+                append_entity(c, tx, ty, svx, svy, r, r, EXPLOSION); // explosion takes src's velocity
+            }
+        }
+    }
     if constexpr (G == PG_GAME_BOSSFIGHT) { // bossfight.cpp:140-190
         auto &B = c.s.gs.bf;
         const int st = EI(c, F_TYPE, si), tt = EI(c, F_TYPE, ti);
@@ -1078,7 +1148,9 @@ DEV void entity_collisions(Ctx &c, int i) {
         for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
             int j = base + LANE;
             bool hit = false;
-            if (j < upper && j != i && !(EI(c, F_FLAGS, j) & EF_WILL_ERASE)) {
+            bool relevant = true;
+            if constexpr (G == PG_GAME_CAVEFLYER) relevant = j < upper && EI(c, F_TYPE, j) == CF_PLAYER_BULLET;
+            if (relevant && j < upper && j != i && !(EI(c, F_FLAGS, j) & EF_WILL_ERASE)) {
                 float tx = (rx + EF(c, F_RX, j)) + mrg, ty = (ry + EF(c, F_RY, j)) + mrg;
                 hit = (fabsf(x - EF(c, F_X, j)) < tx) && (fabsf(y - EF(c, F_Y, j)) < ty);
             }
@@ -2052,6 +2124,63 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ caveflyer (caveflyer.cpp:289-324)
+DEV void caveflyer_step_tail(Ctx &c) {
+    if (c.s.special_action == 1) {
+        const float arot = EF(c, F_ROTATION, 0), ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0);
+        const float theta = -1 * arot + PI_F / 2;
+        double sn, cs;
+        pg_sincos_cr((double)theta, &sn, &cs);
+        wave_sync();
+        const int b = append_entity(c, ax, ay, (float)cs, (float)sn, 0.1f, 0.25f, CF_PLAYER_BULLET);
+        if (b >= 0) {
+            EI(c, F_EXPIRE_TIME, b) = 10;
+            EF(c, F_ROTATION, b) = arot;
+        }
+        wave_sync();
+    }
+    // descending walk: enemies face their velocity (face_direction(vx, vy, -PI / 2)); a bullet
+    // with a corner in a CAVEWALL goes away and leaves an explosion (appended in walk order)
+    const int n = c.s.num_ents;
+    for (int base = (n - 1) & ~63; base >= 0; base -= 64) {
+        const int i = base + LANE;
+        bool hit = false;
+        float bx = 0, by = 0, br = 0;
+        if (i < n) {
+            const int t = EI(c, F_TYPE, i);
+            if (t == CF_ENEMY) {
+                const float vx = EF(c, F_VX, i), vy = EF(c, F_VY, i);
+                if (vx != 0 || vy != 0) EF(c, F_ROTATION, i) = face_rotation(vx, vy, 0, -1 * PI_F / 2);
+            } else if (t == CF_PLAYER_BULLET) {
+                const float x = EF(c, F_X, i), y = EF(c, F_Y, i), rx = EF(c, F_RX, i), ry = EF(c, F_RY, i);
+                bool wall = false;
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+                        wall = wall || get_obj_from_floats(c, x + rx * (float)(2 * a - 1), y + ry * (float)(2 * b - 1)) == CF_CAVEWALL;
+                if (wall) {
+                    EI(c, F_FLAGS, i) = EI(c, F_FLAGS, i) | EF_WILL_ERASE;
+                    hit = true;
+                    bx = x;
+                    by = y;
+                    br = (float)(.5 * rx);
+                }
+            }
+        }
+        unsigned long long m = ballot(hit);
+        wave_sync();
+        while (m) {
+            const int l = top_bit(m);
+            m &= ~(1ull << l);
+            const float ex = rlf(bx, l), ey = rlf(by, l), er = rlf(br, l);
+            append_entity(c, ex, ey, 0, 0, er, er, EXPLOSION);
+            wave_sync();
+        }
+    }
+    erase_if_needed(c);
+}
+
 // ------------------------------------------------------------------ ninja (ninja.cpp:420-450)
 DEV void ninja_step_tail(Ctx &c) {
     const bool gh = c.s.agent_erased;
@@ -2405,6 +2534,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_STARPILOT) starpilot_step_tail(c, rg);
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_step_tail(c, rg);
     if constexpr (G == PG_GAME_NINJA) ninja_step_tail(c);
+    if constexpr (G == PG_GAME_CAVEFLYER) caveflyer_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -2540,6 +2670,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_STARPILOT)
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
+        PG_CASE(PG_GAME_CAVEFLYER)
     default: break;
     }
 #undef PG_CASE

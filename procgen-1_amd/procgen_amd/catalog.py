@@ -293,6 +293,20 @@ NINJA_SPRITES = {
     14: ["misc_assets/bomb.png"],
 }
 
+# ---------------------------------------------------------------- caveflyer
+# procgen/src/games/caveflyer.cpp:36-55 (PLAYER 0, GOAL 1, OBSTACLE 2, TARGET 3, PLAYER_BULLET 4,
+# ENEMY 5, CAVEWALL 8, EXHAUST 9)
+CAVEFLYER_SPRITES = {
+    1: ["misc_assets/ufoGreen2.png"],
+    2: ["misc_assets/meteorBrown_big1.png"],
+    3: ["misc_assets/ufoRed2.png"],
+    4: ["misc_assets/laserBlue02.png"],
+    5: ["misc_assets/enemyShipBlue4.png"],
+    0: ["misc_assets/playerShip1_red.png"],
+    8: ["misc_assets/groundA.png"],
+    9: ["misc_assets/towerDefense_tile295.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -309,6 +323,7 @@ GAMES = {
     "starpilot": (STARPILOT_SPRITES, "space"),  # starpilot.cpp:56-58
     "bossfight": (BOSSFIGHT_SPRITES, "space"),  # bossfight.cpp:72-74
     "ninja": (NINJA_SPRITES, "platform"),       # ninja.cpp:43-45
+    "caveflyer": (CAVEFLYER_SPRITES, "space"),  # caveflyer.cpp:31-33
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).

@@ -66,7 +66,7 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
 GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder",
-         "starpilot", "bossfight", "ninja"]
+         "starpilot", "bossfight", "ninja", "caveflyer"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -161,6 +161,16 @@ def test_ninja_long_and_easy():
     write-through + explosions), fire / bomb deaths, the jump-charge bar; easy mode (visibility 10)."""
     run_pair("ninja", 32, 600, seed=25, num_levels=0, rand_seed=14)
     run_pair("ninja", 8, 300, seed=26, num_levels=0, rand_seed=15, distribution_mode="easy")
+
+
+def test_caveflyer_modes():
+    """caveflyer: RoomGenerator levels (cellular automaton, best room, BFS goal path, 4x dilation),
+    thrust along the heading (sin / cos of the agent's rotation), exhaust, lasers that explode on
+    cave walls / targets (3 hits) / meteors, reflecting enemies facing their velocity (atan2f), the
+    agent drawn at arbitrary rotations; easy (30x30) and memory (60x60, unpruned) modes."""
+    run_pair("caveflyer", 32, 600, seed=27, num_levels=0, rand_seed=16)
+    run_pair("caveflyer", 8, 300, seed=28, num_levels=0, rand_seed=17, distribution_mode="easy")
+    run_pair("caveflyer", 8, 200, seed=29, num_levels=0, rand_seed=18, distribution_mode="memory")
 
 
 def test_bigfish_long_episodes():

@@ -254,6 +254,23 @@ def test_leaper_operand_order_pinned():
         assert out[0] == sign * spd, seed
 
 
+def test_caveflyer_operand_order_pinned():
+    """caveflyer.cpp:235 multiplies (.1 * rand01() + .1) by (randn(2) * 2 - 1): g++ draws the left
+    operand first; the oracle and engine follow that order."""
+    ref = ref_lib()
+    ref.ref_caveflyer_enemy_vel.argtypes = [ctypes.c_int32, ctypes.c_void_p]
+    lib = oracle_lib.load()
+    for seed in range(256):
+        out = np.zeros(1, np.float32)
+        ref.ref_caveflyer_enemy_vel(seed, out.ctypes.data)
+        ops = np.array([[2, 0, 0], [1, 2, 0]], np.int32)  # rand01, randn(2)
+        draws = np.zeros(2, np.int32)
+        lib.oracle_randgen_script(seed & 0xFFFFFFFF, ops.ctypes.data, 2, draws.ctypes.data)
+        u = float(draws[:1].view(np.float32)[0])
+        want = np.float32((.1 * u + .1) * (int(draws[1]) * 2 - 1))
+        assert out[0] == want, seed
+
+
 def test_qt_raster_fill_goldens():
     """fillRect(QRectF, opaque QColor) (chaser orbs, bars, draw_grid_obj) replayed through the
     oracle's restatement equals real Qt 5.9.7 (tests/golden/qt_raster_fill_goldens.npz,
