@@ -56,7 +56,7 @@ enum { EasyMode = 0, HardMode = 1, ExtremeMode = 2, MemoryMode = 10 };
 #define MAZE_MAX_CELLS (33 * 33)
 
 /* game ids: index in the reference's env list (procgen/env.py:15-32) */
-enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CAVEFLYER = 2, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_LEAPER = 10, GAME_MAZE = 11,
+enum { GAME_BIGFISH = 0, GAME_BOSSFIGHT = 1, GAME_CAVEFLYER = 2, GAME_CHASER = 3, GAME_CLIMBER = 4, GAME_COINRUN = 5, GAME_DODGEBALL = 6, GAME_FRUITBOT = 7, GAME_HEIST = 8, GAME_JUMPER = 9, GAME_LEAPER = 10, GAME_MAZE = 11,
        GAME_MINER = 12, GAME_NINJA = 13, GAME_PLUNDER = 14, GAME_STARPILOT = 15 };
 
 static void fatal_msg(const char *m) {
@@ -266,6 +266,9 @@ typedef struct {
     Entity *bf_boss, *bf_shields;
     /* ninja (ninja.cpp:25-33; has_support / facing_right / wall_theme / gravity / air_control shared) */
     float nj_jump_charge, nj_jump_charge_inc;
+    /* jumper (jumper.cpp:31-39; has_support / facing_right / wall_theme shared; goal = entity 1) */
+    int jp_jump_count, jp_jump_delta, jp_jump_time;
+    float jp_compass_dim;
     int free_list[MAX_GRID];
     bool is_space[MAX_GRID];
     /* leaper (leaper.cpp:27-32) */
@@ -382,6 +385,8 @@ static bool hook_is_blocked(Game *g, const Entity *src, int target, bool is_hori
             return true;
         }
     }
+    if (g->game_id == GAME_JUMPER) /* jumper.cpp:117-124: CAVEWALL 6, CAVEWALL_TOP 7 */
+        return base || (src->type == PLAYER && (target == 6 || target == 7));
     if (g->game_id == GAME_COINRUN) { /* coinrun.cpp:204-211 */
         if (base) return true;
         if (src->type == PLAYER && cr_is_wall(target)) return true;
@@ -638,6 +643,14 @@ static void hook_handle_agent_collision(Game *g, Entity *obj) {
                 g->fish_eaten += 1;
             }
         }
+    } else if (g->game_id == GAME_JUMPER) { /* jumper.cpp:86-96: GOAL 1, SPIKE 2 */
+        if (obj->type == 1) {
+            g->sd_reward += 10.0f; /* GOAL_REWARD */
+            g->sd_level_complete = true;
+            g->sd_done = true;
+        } else if (obj->type == 2) {
+            g->sd_done = true;
+        }
     } else if (g->game_id == GAME_CAVEFLYER) { /* caveflyer.cpp:57-71 */
         if (obj->type == 1) { /* GOAL */
             g->sd_reward += 10.0f;
@@ -817,6 +830,13 @@ static int hook_image_for_type(Game *g, int type) {
             return -1;
         }
     }
+    if (g->game_id == GAME_JUMPER && type == PLAYER) { /* jumper.cpp:126-135 */
+        Entity *agent = AG(g);
+        if (fabs((double)agent->vx) < .01 && g->action_vx == 0 && g->has_support) return PLAYER;
+        bool first = g->cur_time / 5 % 2 == 0 || !g->has_support;
+        if (g->facing_right) return first ? 12 : 13; /* PLAYER_RIGHT1 / 2 */
+        return first ? 10 : 11;                      /* PLAYER_LEFT1 / 2 */
+    }
     if (g->game_id == GAME_NINJA && type == PLAYER) { /* ninja.cpp:143-153 */
         Entity *agent = AG(g);
         if (fabs((double)agent->vx) < .01 && g->action_vx == 0 && g->has_support) return PLAYER;
@@ -830,6 +850,7 @@ static int hook_image_for_type(Game *g, int type) {
 }
 
 static int hook_theme_for_grid_obj(Game *g, int type) {
+    if (g->game_id == GAME_JUMPER) return (type == 6 || type == 7) ? g->wall_theme : 0; /* jumper.cpp:107-112 */
     if (g->game_id == GAME_NINJA) return type == 20 ? g->wall_theme : 0; /* ninja.cpp:119-124 */
     if (g->game_id == GAME_COINRUN || g->game_id == GAME_CLIMBER) { /* coinrun.cpp:133-138, climber.cpp:106-111 */
         if (type == 15 || type == 16) return g->wall_theme;
@@ -1037,7 +1058,12 @@ static void climber_set_action_xy(Game *g, int move_action) { /* climber.cpp:299
 }
 
 static void caveflyer_set_action_xy(Game *g, int move_action);
+static void jumper_set_action_xy(Game *g, int move_action);
 static void set_action_xy(Game *g, int move_action) {
+    if (g->game_id == GAME_JUMPER) {
+        jumper_set_action_xy(g, move_action);
+        return;
+    }
     if (g->game_id == GAME_CAVEFLYER) {
         caveflyer_set_action_xy(g, move_action);
         return;
@@ -1100,6 +1126,12 @@ static void lp_decay_vel(float *vel);
 static double cu_sign(double x);
 static void update_agent_velocity(Game *g) {
     Entity *agent = AG(g);
+    if (g->game_id == GAME_JUMPER) { /* jumper.cpp:98-105 */
+        float v_scale = 1.0f;
+        agent->vx = (1 - g->mixrate) * agent->vx + g->mixrate * g->maxspeed * g->action_vx * v_scale;
+        if (g->action_vy != 0) agent->vy = g->maxspeed * g->action_vy * 2;
+        return;
+    }
     if (g->game_id == GAME_CAVEFLYER) { /* caveflyer.cpp:73-81: no (1 - mixrate) decay */
         float v_scale = 1.0f;
         agent->vx = (float)((double)agent->vx + (double)(g->mixrate * g->maxspeed * g->action_vx * v_scale) * .2);
@@ -3803,6 +3835,161 @@ static void caveflyer_game_step(Game *g) { /* :289-324 */
     erase_if_needed(g);
 }
 
+/* ================================================================== jumper (games/jumper.cpp) */
+#define JP_GOAL 1
+#define JP_SPIKE 2
+#define JP_CAVEWALL 6
+#define JP_CAVEWALL_TOP 7
+#define JP_MAZE_SCALE 3
+#define JP_JUMP_COOLDOWN 3
+
+static bool jp_is_wall(int t) { return t == JP_CAVEWALL || t == JP_CAVEWALL_TOP; } /* :381-383 */
+static bool jp_is_space_on_ground(Game *g, int x, int y) { /* :182-189 */
+    if (get_obj(g, x, y) != SPACE) return false;
+    if (get_obj(g, x, y + 1) != SPACE) return false;
+    int below = get_obj(g, x, y - 1);
+    return below == JP_CAVEWALL || below == g->out_of_bounds_object;
+}
+static bool jp_is_top_wall(Game *g, int x, int y) { return get_obj(g, x, y) == JP_CAVEWALL && get_obj(g, x, y + 1) == SPACE; }
+static bool jp_is_left_wall(Game *g, int x, int y) { return get_obj(g, x, y) == JP_CAVEWALL && get_obj(g, x + 1, y) == SPACE; }
+static bool jp_is_right_wall(Game *g, int x, int y) { return get_obj(g, x, y) == JP_CAVEWALL && get_obj(g, x - 1, y) == SPACE; }
+
+static void jumper_game_reset(Game *g, const or_atlas *at) { /* :221-379 */
+    static bool best_room[MAX_GRID], wide_path[MAX_GRID];
+    static int free_cells[MAX_GRID], cands[MAX_GRID], goal_path[MAX_GRID + 2];
+    static MazeGen mg;
+    MT *r = &g->rand_gen;
+    int dm = g->options.distribution_mode;
+    if (dm == EasyMode) {
+        g->visibility = 12;
+        g->jp_compass_dim = 3;
+    } else {
+        g->visibility = 16;
+        g->jp_compass_dim = 2;
+    }
+    if (dm == MemoryMode) g->timeout = 2000;
+    int world_dim = 20; /* choose_world_dim (:204-219) */
+    if (dm == EasyMode) world_dim = 20;
+    else if (dm == HardMode) world_dim = 40;
+    else if (dm == MemoryMode) world_dim = 45;
+    g->main_width = world_dim;
+    g->main_height = world_dim;
+    basic_game_reset(g, at);
+    int W = g->main_width, H = g->main_height;
+    g->out_of_bounds_object = WALL_OBJ;
+    g->wall_theme = rg_randn(r, 4); /* NUM_WALL_THEMES */
+    g->jp_jump_count = 0;
+    g->jp_jump_delta = 0;
+    g->jp_jump_time = 0;
+    g->has_support = false;
+    g->facing_right = true;
+    int maze_dim = W / JP_MAZE_SCALE;
+    mg_init(&mg, r, maze_dim);
+    mg_generate_maze_no_dead_ends(&mg);
+    for (int i = 0; i < g->grid_size; i++) {
+        int obj = mg_gridget(&mg, (i % W) / JP_MAZE_SCALE + 1, (i / W) / JP_MAZE_SCALE + 1);
+        float prob = obj == WALL_OBJ ? .8f : .2f;
+        g->grid[i] = rg_rand01(r) < prob ? WALL_OBJ : SPACE;
+    }
+    for (int it = 0; it < 2; it++) rm_update(g);
+    for (int i = 0; i < W; i++) { /* border cells */
+        set_obj(g, i, 0, JP_CAVEWALL);
+        set_obj(g, i, H - 1, JP_CAVEWALL);
+    }
+    for (int i = 0; i < H; i++) {
+        set_obj(g, 0, i, JP_CAVEWALL);
+        set_obj(g, W - 1, i, JP_CAVEWALL);
+    }
+    int best = rm_find_best_room(g, best_room);
+    fassert(best > 0);
+    int nfree = 0;
+    for (int i = 0; i < g->grid_size; i++) {
+        g->grid[i] = best_room[i] ? SPACE : JP_CAVEWALL;
+        if (best_room[i]) free_cells[nfree++] = i;
+    }
+    int goal_cell = free_cells[rg_randn(r, nfree)]; /* choose_one (randgen.cpp:43-47) */
+    int ncand = 0;
+    for (int i = 0; i < g->grid_size; i++)
+        if (jp_is_space_on_ground(g, i % W, i / W)) cands[ncand++] = i;
+    fassert(ncand > 0);
+    int agent_cell = cands[rg_randn(r, ncand)];
+    int npath = rm_find_path(g, agent_cell, goal_cell, goal_path);
+    if (dm != MemoryMode) { /* should_prune */
+        memset(wide_path, 0, sizeof(wide_path));
+        for (int k = 0; k < npath; k++) wide_path[goal_path[k]] = true;
+        rm_expand_room(g, wide_path, 4);
+        for (int i = 0; i < g->grid_size; i++) g->grid[i] = wide_path[i] ? SPACE : JP_CAVEWALL;
+    }
+    int ge = add_entity(g, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5, JP_GOAL);
+    fassert(ge == 1);
+    float spike_prob = dm == MemoryMode ? 0 : .2f;
+    for (int i = 0; i < g->grid_size; i++) {
+        int x = i % W, y = i / W;
+        if (jp_is_space_on_ground(g, x, y) && (jp_is_space_on_ground(g, x - 1, y) && jp_is_space_on_ground(g, x + 1, y))) {
+            if (rg_rand01(r) < spike_prob) set_obj(g, x, y, JP_SPIKE);
+        }
+    }
+    for (int i = 0; i < g->grid_size; i++) { /* no long vertical walls (:325-337) */
+        int x = i % W, y = i / W;
+        if (jp_is_left_wall(g, x, y) && jp_is_left_wall(g, x, y + 1) && jp_is_left_wall(g, x, y + 2))
+            set_obj(g, x, y + rg_randn(r, 3), SPACE);
+        if (jp_is_right_wall(g, x, y) && jp_is_right_wall(g, x, y + 1) && jp_is_right_wall(g, x, y + 2))
+            set_obj(g, x, y + rg_randn(r, 3), SPACE);
+    }
+    Entity *agent = AG(g);
+    agent->x = (float)((agent_cell % W) + .5);
+    agent->y = (agent_cell / W) + agent->ry;
+    for (int i = 0; i < g->grid_size; i++) { /* get_cells_with_type(SPIKE), ascending */
+        if (g->grid[i] != JP_SPIKE) continue;
+        g->grid[i] = SPACE;
+        float spike_ry = 0.4f, spike_rx = 0.23f;
+        add_entity_rxy(g, (float)((i % W) + .5), (i / W) + spike_ry, 0, 0, spike_rx, spike_ry, JP_SPIKE);
+    }
+    for (int i = 0; i < g->grid_size; i++)
+        if (jp_is_top_wall(g, i % W, i / W)) g->grid[i] = JP_CAVEWALL_TOP;
+    agent = AG(g);
+    agent->rx = 0.254f;
+    agent->ry = 0.4f;
+    g->out_of_bounds_object = JP_CAVEWALL;
+}
+
+static void jumper_set_action_xy(Game *g, int move_action) { /* :389-422 */
+    g->action_vx = (float)(move_action / 3 - 1);
+    g->action_vy = (float)((move_action % 3) - 1);
+    if (g->action_vy < 0) g->action_vy = 0;
+    if (g->action_vx > 0) g->facing_right = true;
+    if (g->action_vx < 0) g->facing_right = false;
+    Entity *agent = AG(g);
+    int b1 = get_obj_from_floats(g, (float)(agent->x - (agent->rx - .01)), (float)(agent->y - (agent->ry + .01)));
+    int b2 = get_obj_from_floats(g, (float)(agent->x + (agent->rx - .01)), (float)(agent->y - (agent->ry + .01)));
+    g->jp_jump_delta = 0;
+    g->has_support = (jp_is_wall(b1) || b1 == g->out_of_bounds_object) || (jp_is_wall(b2) || b2 == g->out_of_bounds_object);
+    if (g->has_support) g->jp_jump_count = 2;
+    if (g->action_vy == 1 && g->jp_jump_count > 0 && (g->cur_time - g->jp_jump_time > JP_JUMP_COOLDOWN)) {
+        g->jp_jump_count -= 1;
+        g->jp_jump_delta = -1;
+    } else {
+        g->action_vy = 0;
+    }
+    if (g->action_vy > 0) g->jp_jump_time = g->cur_time;
+    g->action_vrot = 0;
+}
+
+static void jumper_game_step(Game *g) { /* :424-441 */
+    basic_game_step(g);
+    Entity *agent = AG(g);
+    if (g->action_vx > 0) agent->is_reflected = false;
+    if (g->action_vx < 0) agent->is_reflected = true;
+    if (fabs((double)agent->vx) + fabs((double)agent->vy) > .05) {
+        float ax = agent->x, ty = (float)(agent->y - agent->ry * .5);
+        int t = add_entity_rxy(g, ax, ty, 0, 0.01f, 0.3f, 0.2f, TRAIL);
+        g->ents[t].expire_time = 8;
+        g->ents[t].alpha = .5;
+    }
+    agent = AG(g);
+    if (agent->vy > -2) agent->vy -= 0.15f;
+}
+
 /* ================================================================== leaper (games/leaper.cpp) */
 #define LP_LOG 1
 #define LP_ROAD 2
@@ -3957,6 +4144,7 @@ static void game_reset_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_reset(g, at);
     else if (g->game_id == GAME_NINJA) ninja_game_reset(g, at);
     else if (g->game_id == GAME_CAVEFLYER) caveflyer_game_reset(g, at);
+    else if (g->game_id == GAME_JUMPER) jumper_game_reset(g, at);
     else fatal_msg("game not restated");
 }
 static void game_step_dispatch(Game *g, const or_atlas *at) {
@@ -3975,6 +4163,7 @@ static void game_step_dispatch(Game *g, const or_atlas *at) {
     else if (g->game_id == GAME_BOSSFIGHT) bossfight_game_step(g);
     else if (g->game_id == GAME_NINJA) ninja_game_step(g);
     else if (g->game_id == GAME_CAVEFLYER) caveflyer_game_step(g);
+    else if (g->game_id == GAME_JUMPER) jumper_game_step(g);
     else fatal_msg("game not restated");
 }
 
@@ -4569,6 +4758,64 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
     if (g->has_useful_vel_info && g->options.paint_vel_info) fatal_msg("paint_vel_info not restated yet");
 }
 
+/* jumper's draw_compass (jumper.cpp:137-177).  The dial ellipse, the cosmetic needle line and the
+ * translucent jump ellipse are the Qt 5.9.7 raster output tabulated by tools/qt_compass_tables.cpp
+ * (the atlas image slot JP_TABLE_SLOT carries the table, procgen_amd/assets.py); the distance bar
+ * is fillRect(QRectF) (qt_fill_rectf, pinned by qt_raster_fill_goldens). */
+#define JP_TABLE_SLOT 99
+static void jp_stamp(uint32_t *canvas, const uint32_t *rows64, int dx, int dy, uint32_t argb, bool blend) {
+    for (int y = 0; y < RES_H; y++) {
+        int sy = y - dy;
+        if (sy < 0 || sy >= RES_H) continue;
+        uint64_t m = (uint64_t)rows64[2 * sy] | ((uint64_t)rows64[2 * sy + 1] << 32);
+        for (int x = 0; x < RES_W; x++) {
+            int sx = x - dx;
+            if (sx < 0 || sx >= 64 || !((m >> sx) & 1)) continue;
+            uint32_t *d = &canvas[y * RES_W + x];
+            *d = blend ? argb + BYTE_MUL(*d, (~argb) >> 24) : argb;
+        }
+    }
+}
+static void jp_draw_compass(Game *g, const or_atlas *at) {
+    const or_image *ti = &at->sprites[JP_TABLE_SLOT];
+    fassert(ti->w > 0);
+    const uint32_t *t = at->pixels + ti->offset;
+    const int NY = (int)t[1], NX = (int)t[2], MAXW = (int)t[3], MAXH = (int)t[4];
+    const int cfg = (g->options.distribution_mode == EasyMode ? 0 : 1) + (g->options.center_agent ? 0 : 2);
+    const uint32_t *cg = t + 5 + 9 * cfg;
+    const int x1 = (int)cg[0], y1 = (int)cg[1], bx0 = (int)cg[2], by0 = (int)cg[3], bnx = (int)cg[4], bny = (int)cg[5];
+    float cx, cy, cr;
+    memcpy(&cx, &cg[6], 4);
+    memcpy(&cy, &cg[7], 4);
+    memcpy(&cr, &cg[8], 4);
+    const uint32_t *dial = t + 5 + 36;
+    const uint32_t *needle = dial + 4 * 128;
+    const uint32_t *jump = needle + (size_t)4 * NY * NX * 128;
+    float u = g->unit, vd = g->view_dim, cd = g->jp_compass_dim;
+    /* the table geometry must be the frame's: compass_rect = get_abs_rect(vd - cd - .25, .25, cd, cd) */
+    double rx = (double)((float)(vd - cd - .25) * u), rw = (double)(cd * u);
+    fassert((float)(rx + rw / 2) == cx);
+    jp_stamp(g->canvas, dial + 128 * cfg, 0, 0, 0xffa8a69eu, false); /* QColor(168, 166, 158) */
+    Entity *agent = AG(g), *goal = &g->ents[1];
+    float theta = (float)atan2((double)(goal->y - agent->y), (double)(goal->x - agent->x)); /* get_theta (:241-246) */
+    int x2 = (int)(cx + cr * cos((double)theta)), y2 = (int)(cy - cr * sin((double)theta));
+    (void)x1; (void)y1;
+    fassert(bx0 <= x2 && x2 < bx0 + bnx && by0 <= y2 && y2 < by0 + bny);
+    jp_stamp(g->canvas, needle + ((size_t)(cfg * NY + (y2 - by0)) * NX + (x2 - bx0)) * 128, 0, 0, 0xfffcba03u, false);
+    float ddx = agent->x - goal->x, ddy = agent->y - goal->y; /* get_distance (:133-143) */
+    float dist = (float)sqrt((double)(ddx * ddx + ddy * ddy));
+    float dist_pct = (float)(dist / (g->main_width * sqrt(2)));
+    float bar_thickness = cd / 8;
+    qt_fill_rectf(g->canvas, (double)((float)(vd - cd - .25) * u), (double)((float)(.25 + cd) * u),
+                  (double)(cd * dist_pct * u), (double)(bar_thickness * u), 0xfffcba03u);
+    if (g->jp_jump_delta < 0 && !g->has_support) { /* get_object_rect(agent) -> QRect(int, ...) */
+        RectD r1 = get_screen_rect(g, agent->x - agent->rx, agent->y + agent->ry, 2 * agent->rx, 2 * agent->ry, 0);
+        int qx = (int)r1.x, qy = (int)(r1.y + r1.h * (5.0 / 6)), qw = (int)r1.w, qh = (int)(r1.h / 3);
+        fassert(0 <= qw && qw <= MAXW && 0 <= qh && qh <= MAXH);
+        jp_stamp(g->canvas, jump + (size_t)(qw * (MAXH + 1) + qh) * 128, qx - 20, qy - 20, 0x78787878u, true);
+    }
+}
+
 static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
     if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:107-124: scrolling tiled background */
         float scale = (float)(RES_H / g->main_height); /* int / int */
@@ -4588,6 +4835,7 @@ static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_dra
     }
     draw_background(g, at);
     draw_foreground(g, at);
+    if (g->game_id == GAME_JUMPER && g->options.distribution_mode != MemoryMode) jp_draw_compass(g, at);
     if (g->game_id == GAME_NINJA) { /* ninja.cpp:155-164: jump charge bar, get_abs_rect (:812-814) */
         float u = g->unit;
         float bar_height = 3 * g->nj_jump_charge;
@@ -4622,6 +4870,7 @@ static int game_id_of(const char *name) {
     if (strcmp(name, "bossfight") == 0) return GAME_BOSSFIGHT;
     if (strcmp(name, "ninja") == 0) return GAME_NINJA;
     if (strcmp(name, "caveflyer") == 0) return GAME_CAVEFLYER;
+    if (strcmp(name, "jumper") == 0) return GAME_JUMPER;
     return -1;
 }
 

@@ -122,9 +122,10 @@ int game_id(const std::string &name) {
     if (name == "bossfight") return PG_GAME_BOSSFIGHT;
     if (name == "ninja") return PG_GAME_NINJA;
     if (name == "caveflyer") return PG_GAME_CAVEFLYER;
+    if (name == "jumper") return PG_GAME_JUMPER;
     return -1;
 }
-const char *SUPPORTED_GAMES = "bigfish, bossfight, caveflyer, chaser, climber, coinrun, dodgeball, fruitbot, heist, leaper, maze, miner, ninja, plunder, starpilot";
+const char *SUPPORTED_GAMES = "bigfish, bossfight, caveflyer, chaser, climber, coinrun, dodgeball, fruitbot, heist, jumper, leaper, maze, miner, ninja, plunder, starpilot";
 
 std::vector<std::string> split_names(const std::string &s) { // vecgame.cpp:20-28 split(",")
     std::vector<std::string> out;

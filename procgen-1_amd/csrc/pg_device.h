@@ -165,6 +165,17 @@ DEV float sp_hp_prob(int mode, int type) {
 #define BF_BOTTOM_MARGIN 6
 #define BF_BOSS_VEL_TIMEOUT 20
 #define BF_BOSS_DAMAGED_TIMEOUT 40
+// jumper.cpp:11-27
+#define JP_GOAL 1
+#define JP_SPIKE 2
+#define JP_CAVEWALL 6
+#define JP_CAVEWALL_TOP 7
+#define JP_PLAYER_JUMP 9
+#define JP_PLAYER_LEFT1 10
+#define JP_PLAYER_LEFT2 11
+#define JP_PLAYER_RIGHT1 12
+#define JP_PLAYER_RIGHT2 13
+DEV bool jp_is_wall(int t) { return t == JP_CAVEWALL || t == JP_CAVEWALL_TOP; }
 // caveflyer.cpp:12-21
 #define CF_GOAL 1
 #define CF_OBSTACLE 2

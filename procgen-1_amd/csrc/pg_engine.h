@@ -22,7 +22,7 @@
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
-    PG_GAME_BIGFISH = 0, PG_GAME_BOSSFIGHT = 1, PG_GAME_CAVEFLYER = 2, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
+    PG_GAME_BIGFISH = 0, PG_GAME_BOSSFIGHT = 1, PG_GAME_CAVEFLYER = 2, PG_GAME_CHASER = 3, PG_GAME_CLIMBER = 4, PG_GAME_COINRUN = 5, PG_GAME_DODGEBALL = 6, PG_GAME_FRUITBOT = 7, PG_GAME_HEIST = 8, PG_GAME_JUMPER = 9, PG_GAME_LEAPER = 10, PG_GAME_MAZE = 11,
     PG_GAME_MINER = 12, PG_GAME_NINJA = 13, PG_GAME_PLUNDER = 14, PG_GAME_STARPILOT = 15
 };
 #ifndef PG_NUM_GAMES
@@ -196,6 +196,11 @@ struct PGEnv {
                  // last_fire_time are the shared members above)
             float jump_charge, jump_charge_inc;
         } nj;
+        struct { // jumper (jumper.cpp:31-39; has_support, facing_right, wall_theme are shared; the goal
+                 // is entity 1 for the whole episode)
+            int32_t jump_count, jump_delta, jump_time;
+            float compass_dim;
+        } jp;
         int32_t words[20];
     } gs;
     // entity slots reserved at the top of the planes, [PG_CAP - num_tail, PG_CAP): starpilot's
@@ -242,6 +247,7 @@ struct PGDev {
     int32_t *latent;            // [num_envs][PG_LATENT_N] grid_size, grid, agent_pos, exit_pos (maze)
 };
 #define PG_ROT_N 16
+#define PG_TABLE_SLOT 99 // image slot of a game's Qt-tabulated overlay raster (jumper's compass)
 #define PG_LATENT_N (2 + PG_LATENT_GRID + 2 + 2)
 
 // The tables of game G (kernels are instantiated per game).

@@ -99,6 +99,12 @@ DEV int player_image(const PGEnv &s, float agent_vx) {
         if (fabsf(agent_vx) < .01 && s.action_vx == 0 && s.has_support) return PLAYER;
         return (s.cur_time / 5 % 2 == 0 || !s.has_support) ? CL_PLAYER_RIGHT1 : CL_PLAYER_RIGHT2;
     }
+    if constexpr (G == PG_GAME_JUMPER) { // jumper.cpp:126-135
+        if (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support) return PLAYER;
+        const bool first = s.cur_time / 5 % 2 == 0 || !s.has_support;
+        if (s.facing_right) return first ? JP_PLAYER_RIGHT1 : JP_PLAYER_RIGHT2;
+        return first ? JP_PLAYER_LEFT1 : JP_PLAYER_LEFT2;
+    }
     if constexpr (G == PG_GAME_NINJA) // ninja.cpp:143-153
         return (fabs((double)agent_vx) < .01 && s.action_vx == 0 && s.has_support)
                    ? PLAYER
@@ -119,7 +125,7 @@ DEV int image_for_type(const PGEnv &s, int type, int player_img) {
             return CH_ENEMY + rem;
         }
     }
-    if constexpr (G == PG_GAME_NINJA)
+    if constexpr (G == PG_GAME_NINJA || G == PG_GAME_JUMPER)
         if (type == PLAYER) return player_img;
     if constexpr (G == PG_GAME_COINRUN || G == PG_GAME_CLIMBER) { // ENEMY_BARRIER is 19 in both
         if (type == PLAYER) return player_img;
@@ -138,6 +144,7 @@ DEV int grid_theme(const PGEnv &s, int type) { // theme_for_grid_obj (coinrun.cp
     if constexpr (G == PG_GAME_COINRUN) return cr_is_wall(type) ? s.wall_theme : 0;
     if constexpr (G == PG_GAME_CLIMBER) return cl_is_wall(type) ? s.wall_theme : 0; // climber.cpp:106-111
     if constexpr (G == PG_GAME_NINJA) return type == NJ_WALL_MID ? s.wall_theme : 0; // ninja.cpp:119-124
+    if constexpr (G == PG_GAME_JUMPER) return jp_is_wall(type) ? s.wall_theme : 0;    // jumper.cpp:107-112
     return 0;
 }
 template <int G>
@@ -399,9 +406,71 @@ DEV void fb_fill_rectf(uint32_t *fb, double x, double y, double w, double h, uin
     for (int p = LANE; p < nx * ny; p += 64) fb[(im.ey.t1 + p / nx) * PG_RES + im.ex.t1 + p % nx] = im.fill;
 }
 
+// jumper's compass (jumper.cpp:137-177).  The dial ellipse, the cosmetic needle and the translucent
+// jump ellipse are Qt 5.9.7 raster output tabulated per configuration / endpoint / rect size by
+// tools/qt_compass_tables.cpp (atlas image slot PG_TABLE_SLOT, layout in procgen_amd/assets.py
+// compass_table_words); lane = canvas row, each lane stamps the set bits of its row mask.
+DEV void jp_stamp(uint32_t *fb, const uint32_t *rows, int dx, int dy, uint32_t argb, bool blend) {
+    const int y = LANE, sy = y - dy;
+    if (sy < 0 || sy >= PG_RES || dx <= -64 || dx >= 64) return;
+    uint64_t m = (uint64_t)rows[2 * sy] | ((uint64_t)rows[2 * sy + 1] << 32);
+    m = dx >= 0 ? (m << dx) : (m >> -dx);
+    while (m) {
+        const int x = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        uint32_t *p = &fb[y * PG_RES + x];
+        *p = blend ? argb + BYTE_MUL(*p, (~argb) >> 24) : argb;
+    }
+}
+DEV bool jp_draw_compass(uint32_t *fb, const PGEnv &s, const View &v, const PGDev &d, int env) {
+    const int4 ti = reinterpret_cast<const int4 *>(d.sprites)[PG_TABLE_SLOT];
+    if (ti.y <= 0) return false;
+    const uint32_t *t = d.pixels + (uint32_t)ti.x;
+    const int NY = (int)t[1], NX = (int)t[2], MAXW = (int)t[3], MAXH = (int)t[4];
+    const int cfg = (s.opt_distribution_mode == PG_EASY ? 0 : 1) + (s.opt_center_agent ? 0 : 2);
+    const uint32_t *cg = t + 5 + 9 * cfg;
+    const int bx0 = (int)cg[2], by0 = (int)cg[3], bnx = (int)cg[4], bny = (int)cg[5];
+    const float cx = __uint_as_float(cg[6]), cy = __uint_as_float(cg[7]), cr = __uint_as_float(cg[8]);
+    const uint32_t *dial = t + 5 + 36;
+    const uint32_t *needle = dial + 4 * 128;
+    const uint32_t *jump = needle + (size_t)4 * NY * NX * 128;
+    const float u = v.unit, vd = v.view_dim, cd = s.gs.jp.compass_dim;
+    const double rx = (double)((float)(vd - cd - .25) * u), rw = (double)(cd * u);
+    if ((float)(rx + rw / 2) != cx) return false; // the table was built for this frame geometry
+    jp_stamp(fb, dial + 128 * cfg, 0, 0, 0xffa8a69eu, false); // QColor(168, 166, 158)
+    wave_sync();
+    const float ax = EFr(d, F_X, env, 0), ay = EFr(d, F_Y, env, 0), arx = EFr(d, F_RX, env, 0), ary = EFr(d, F_RY, env, 0);
+    const float gx = EFr(d, F_X, env, 1), gy = EFr(d, F_Y, env, 1);
+    const float theta = (float)atan2((double)(gy - ay), (double)(gx - ax)); // get_theta (:241-246), double atan2
+    double sn, cs;
+    pg_sincos_cr((double)theta, &sn, &cs);
+    const int x2 = (int)((double)cx + (double)cr * cs), y2 = (int)((double)cy - (double)cr * sn);
+    if (x2 < bx0 || x2 >= bx0 + bnx || y2 < by0 || y2 >= by0 + bny) return false;
+    jp_stamp(fb, needle + ((size_t)(cfg * NY + (y2 - by0)) * NX + (x2 - bx0)) * 128, 0, 0, 0xfffcba03u, false);
+    wave_sync();
+    const float ddx = ax - gx, ddy = ay - gy; // get_distance (:133-143)
+    const float dist = (float)sqrt((double)(ddx * ddx + ddy * ddy));
+    const float dist_pct = (float)((double)dist / (s.main_width * 1.4142135623730951)); // main_width * sqrt(2)
+    const float bar_thickness = cd / 8;
+    fb_fill_rectf(fb, (double)((float)(vd - cd - .25) * u), (double)((float)(.25 + cd) * u), (double)(cd * dist_pct * u),
+                  (double)(bar_thickness * u), 0xfffcba03u);
+    wave_sync();
+    if (s.gs.jp.jump_delta < 0 && !s.has_support) { // drawEllipse(QRect(...)) of get_object_rect(agent)
+        double r1x, r1y, r1w, r1h;
+        screen_rect(v, ax - arx, ay + ary, 2 * arx, 2 * ary, 0, r1x, r1y, r1w, r1h);
+        const int qx = (int)r1x, qy = (int)(r1y + r1h * (5.0 / 6)), qw = (int)r1w, qh = (int)(r1h / 3);
+        if (qw < 0 || qw > MAXW || qh < 0 || qh > MAXH) return false;
+        jp_stamp(fb, jump + (size_t)(qw * (MAXH + 1) + qh) * 128, qx - 20, qy - 20, 0x78787878u, true);
+        wave_sync();
+    }
+    return true;
+}
+
 // game_draw additions drawn over the foreground (plunder.cpp:66-77)
 template <int G>
-DEV void game_overlay(uint32_t *fb, const PGEnv &s, const View &v) {
+DEV void game_overlay(uint32_t *fb, const PGEnv &s, const View &v, const PGDev &d, int env, bool &err) {
+    if constexpr (G == PG_GAME_JUMPER)
+        if (s.opt_distribution_mode != PG_MEMORY && !jp_draw_compass(fb, s, v, d, env)) err = true;
     if constexpr (G == PG_GAME_NINJA) { // jump charge bar (ninja.cpp:155-164), get_abs_rect (:812-814)
         const float u = v.unit, bar_height = 3 * s.gs.nj.jump_charge;
         fb_fill_rectf(fb, (double)(.25f * u), (double)((float)(v.visibility - .5 - bar_height) * u), (double)(.5f * u),
@@ -1096,7 +1165,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     PG_DRAW_ENTITIES(1)
 #undef PG_DRAW_ENTITIES
     wave_sync();
-    game_overlay<G>(fb, s, v);
+    game_overlay<G>(fb, s, v, d, env, err);
     wave_sync();
 
 
@@ -1141,6 +1210,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
         PG_CASE(PG_GAME_CAVEFLYER)
+        PG_CASE(PG_GAME_JUMPER)
     default: break;
     }
 #undef PG_CASE

@@ -69,6 +69,8 @@ struct CaveScratch {
     uint8_t f[PG_GRID_MAX];         // CF_* bits per cell
 };
 template <> struct Scratch<PG_GAME_CAVEFLYER> { CaveScratch cf; };
+// jumper: MazeGen first (its grid is read by the random fill), then the RoomGenerator
+template <> struct Scratch<PG_GAME_JUMPER> { union { MGScratch mg; CaveScratch cf; }; };
 template <> struct Scratch<PG_GAME_LEAPER> { LeaperScratch lp; };
 template <> struct Scratch<PG_GAME_MINER> { MinerScratch mn; };
 template <> struct Scratch<PG_GAME_MAZE> { MGScratch mg; };
@@ -505,10 +507,10 @@ DEV void mg_generate_maze(RCtx &c, MG &g) { // :112-188
     wave_sync();
     if (LANE == 0) m->grid[1 * ad + 1] = 0; // grid.set(MAZE_OFFSET, MAZE_OFFSET, 0)
     g.num_free = 0;
-    // wall list in push order (md odd): first i odd (x), j even (y); then i even, j odd
+    // wall list in push order: first i odd in [1, md - 2] (x), j even; then i even, j odd in [1, md - 2]
     const int A = (md - 1) / 2, B = (md + 1) / 2;
     const int nw1 = A * B, nw = 2 * A * B;
-    if ((md & 1) == 0 || nw > MG_MAX_WALLS) c.s.error = PG_ERR_GRID;
+    if (nw > MG_MAX_WALLS) c.s.error = PG_ERR_GRID; // also right for an even maze_dim (jumper easy: 6)
     for (int k = LANE; k < nw; k += 64) {
         int x1, y1, x2, y2;
         if (k < nw1) {
@@ -2077,6 +2079,187 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     c.s.visibility = c.s.opt_distribution_mode == PG_EASY ? 10 : 16;
 }
 
+// ------------------------------------------------------------------ jumper (jumper.cpp:182-379)
+DEV void mg_generate_maze_no_dead_ends(RCtx &c, MG &g);
+DEV int jp_get(RCtx &c, int x, int y) { return get_obj(c, x, y); }
+DEV bool jp_space_on_ground(RCtx &c, int x, int y) { // is_space_on_ground (:182-189)
+    if (jp_get(c, x, y) != SPACE) return false;
+    if (jp_get(c, x, y + 1) != SPACE) return false;
+    const int below = jp_get(c, x, y - 1);
+    return below == JP_CAVEWALL || below == c.s.out_of_bounds_object;
+}
+DEV bool jp_left_wall(RCtx &c, int x, int y) { return jp_get(c, x, y) == JP_CAVEWALL && jp_get(c, x + 1, y) == SPACE; }
+DEV bool jp_right_wall(RCtx &c, int x, int y) { return jp_get(c, x, y) == JP_CAVEWALL && jp_get(c, x - 1, y) == SPACE; }
+DEV bool jp_spike_site(RCtx &c, int x, int y) {
+    return jp_space_on_ground(c, x, y) && jp_space_on_ground(c, x - 1, y) && jp_space_on_ground(c, x + 1, y);
+}
+DEV bool jp_left_run(RCtx &c, int x, int y) { return jp_left_wall(c, x, y) && jp_left_wall(c, x, y + 1) && jp_left_wall(c, x, y + 2); }
+DEV bool jp_right_run(RCtx &c, int x, int y) {
+    return jp_right_wall(c, x, y) && jp_right_wall(c, x, y + 1) && jp_right_wall(c, x, y + 2);
+}
+
+// The reference's in-order scans whose actions change the predicate of later cells (spike
+// placement, long-wall breaking) run speculatively: 64 cells are tested at once against the
+// current grid, the first hit is acted on (uniformly, with its RNG draws), and the scan resumes
+// after it -- every cell is tested against exactly the grid the serial loop would show it.
+template <typename P, typename A>
+DEV void jp_ordered_scan(RCtx &c, int n, P pred, A act) {
+    const int W = c.s.main_width;
+    for (int start = 0; start < n;) {
+        const int i = start + LANE;
+        const unsigned long long m = ballot(i < n && pred(i % W, i / W));
+        if (!m) {
+            start += 64;
+            continue;
+        }
+        const int first = start + __ffsll((long long)m) - 1;
+        act(first % W, first / W);
+        start = first + 1;
+    }
+}
+
+DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
+    const int dm = c.s.opt_distribution_mode;
+    auto &J = c.s.gs.jp;
+    if (dm == PG_EASY) {
+        c.s.visibility = 12;
+        J.compass_dim = 3;
+    } else {
+        c.s.visibility = 16;
+        J.compass_dim = 2;
+    }
+    if (dm == PG_MEMORY) c.s.timeout = 2000;
+    int world_dim = 20; // choose_world_dim (:204-219)
+    if (dm == PG_HARD) world_dim = 40;
+    else if (dm == PG_MEMORY) world_dim = 45;
+    c.s.main_width = world_dim;
+    c.s.main_height = world_dim;
+    base_game_reset<PG_GAME_JUMPER>(c);
+    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    c.s.out_of_bounds_object = WALL_OBJ;
+    c.s.wall_theme = randn(c, 4); // NUM_WALL_THEMES
+    J.jump_count = 0;
+    J.jump_delta = 0;
+    J.jump_time = 0;
+    c.s.has_support = 0;
+    c.s.facing_right = 1;
+    // MazeGen(maze_dim = W / MAZE_SCALE).generate_maze_no_dead_ends(), then each cell draws against
+    // .8 (maze wall) or .2 (maze space) of its 3x3 maze block
+    MG g;
+    g.m = &X->mg;
+    g.md = W / 3;
+    g.ad = g.md + 2;
+    if (g.ad > MG_MAX_DIM) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    mg_generate_maze_no_dead_ends(c, g);
+    for (int base = 0; base < n;) {
+        if (c.mti >= PG_MT_N) {
+            mt_twist_lds(c.mt);
+            c.mti = 0;
+        }
+        int m = PG_MT_N - c.mti;
+        if (m > 64) m = 64;
+        if (m > n - base) m = n - base;
+        if (LANE < m) {
+            const int i = base + LANE;
+            const int obj = X->mg.grid[((i / W) / 3 + 1) * g.ad + (i % W) / 3 + 1];
+            const float prob = obj == WALL_OBJ ? .8f : .2f;
+            c.grid[i] = rg_rand01_of(mt_temper(c.mt[c.mti + LANE])) < prob ? WALL_OBJ : SPACE;
+        }
+        c.mti += m;
+        base += m;
+        wave_sync();
+    }
+    CaveScratch *S = &X->cf; // the maze is dead from here on
+    for (int it = 0; it < 2; it++) cf_update(c, S);
+    for (int i = LANE; i < n; i += 64) { // border cells
+        const int x = i % W, y = i / W;
+        if (x == 0 || y == 0 || x == W - 1 || y == H - 1) c.grid[i] = JP_CAVEWALL;
+    }
+    wave_sync();
+    const int best = cf_find_best_room(c, S);
+    if (best < 0) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    int nfree = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + LANE;
+        const bool in = i < n && S->a[i] == best;
+        if (i < n) {
+            c.grid[i] = in ? SPACE : JP_CAVEWALL;
+            S->f[i] = 0;
+        }
+        const unsigned long long m = ballot(in);
+        if (in) S->list[nfree + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        nfree += __popcll(m);
+    }
+    wave_sync();
+    const int goal_cell = S->list[randn(c, nfree)]; // choose_one (randgen.cpp:43-47)
+    int ncand = 0; // agent candidates: SPACE on ground, ascending
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + LANE;
+        const bool in = i < n && jp_space_on_ground(c, i % W, i / W);
+        const unsigned long long m = ballot(in);
+        if (in) S->list2[ncand + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+        ncand += __popcll(m);
+    }
+    wave_sync();
+    if (ncand == 0) {
+        c.s.error = PG_ERR_GRID;
+        return;
+    }
+    const int agent_cell = S->list2[randn(c, ncand)];
+    wave_sync();
+    const int npath = cf_find_path(c, S, agent_cell, goal_cell);
+    if (dm != PG_MEMORY) { // should_prune
+        for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
+        wave_sync();
+        cf_expand_room(c, S, 4);
+        for (int i = LANE; i < n; i += 64) c.grid[i] = (S->f[i] & CF_SET) ? SPACE : JP_CAVEWALL;
+        wave_sync();
+    }
+    add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, JP_GOAL); // entity 1
+    const float spike_prob = dm == PG_MEMORY ? 0 : .2f;
+    jp_ordered_scan(c, n, [&](int x, int y) { return jp_spike_site(c, x, y); }, [&](int x, int y) {
+        if (rand01(c) < spike_prob) set_obj(c, x, y, JP_SPIKE);
+    });
+    jp_ordered_scan(c, n, [&](int x, int y) { return jp_left_run(c, x, y) || jp_right_run(c, x, y); },
+                    [&](int x, int y) { // :325-337, left then right against the updated grid
+                        if (jp_left_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
+                        if (jp_right_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
+                    });
+    EF(c, F_X, 0) = (float)((agent_cell % W) + .5);
+    EF(c, F_Y, 0) = (float)(agent_cell / W) + EF(c, F_RY, 0);
+    wave_sync();
+    // spike cells (get_cells_with_type, ascending) become SPIKE entities
+    int nsp = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + LANE;
+        const bool in = i < n && c.grid[i] == JP_SPIKE;
+        const unsigned long long m = ballot(in);
+        if (in) {
+            S->list[nsp + __popcll(m & ((1ull << LANE) - 1ull))] = (int16_t)i;
+            c.grid[i] = SPACE;
+        }
+        nsp += __popcll(m);
+    }
+    wave_sync();
+    for (int k = 0; k < nsp; k++) {
+        const int cell = S->list[k];
+        const float spike_ry = 0.4f, spike_rx = 0.23f;
+        add_entity_rxy(c, (float)((cell % W) + .5), (float)(cell / W) + spike_ry, 0, 0, spike_rx, spike_ry, JP_SPIKE);
+    }
+    for (int i = LANE; i < n; i += 64) // is_top_wall -> CAVEWALL_TOP (order-independent)
+        if (c.grid[i] == JP_CAVEWALL && jp_get(c, i % W, i / W + 1) == SPACE) c.grid[i] = JP_CAVEWALL_TOP;
+    wave_sync();
+    EF(c, F_RX, 0) = 0.254f;
+    EF(c, F_RY, 0) = 0.4f;
+    c.s.out_of_bounds_object = JP_CAVEWALL;
+}
+
 // ------------------------------------------------------------------ chaser (chaser.cpp:146-252)
 // MazeGen::generate_maze_no_dead_ends (mazegen.cpp:190-211): the scan visits cells in index
 // order and may open a wall next to a later cell, so each step finds the first dead end at or
@@ -2408,6 +2591,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_game_reset(c);
     if constexpr (G == PG_GAME_NINJA) ninja_game_reset(c);
     if constexpr (G == PG_GAME_CAVEFLYER) caveflyer_game_reset(c, &scratch->cf);
+    if constexpr (G == PG_GAME_JUMPER) jumper_game_reset(c, scratch);
     c.s.cur_time = 0;
     c.s.total_reward = 0;
     c.s.episodes_remaining -= 1;
@@ -2517,6 +2701,7 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
         PG_CASE(PG_GAME_CAVEFLYER)
+        PG_CASE(PG_GAME_JUMPER)
     default: break;
     }
 #undef PG_CASE

@@ -180,6 +180,8 @@ DEV bool is_blocked(Ctx &c, int src_type, int target) { // basic :494-501 + coin
         if (src_type == PLAYER && cr_is_wall(target)) return true;
     if constexpr (G == PG_GAME_CLIMBER) // climber.cpp:147-154
         if (src_type == PLAYER && cl_is_wall(target)) return true;
+    if constexpr (G == PG_GAME_JUMPER) // jumper.cpp:117-124
+        if (src_type == PLAYER && jp_is_wall(target)) return true;
     if constexpr (G == PG_GAME_CHASER) // chaser.cpp:94-99
         if (target == CH_MAZE_WALL) return true;
     if constexpr (G == PG_GAME_FRUITBOT) // fruitbot.cpp:83-85
@@ -663,6 +665,26 @@ DEV void set_action_xy(Ctx &c, int move_action) {
             c.s.action_vy = 0;
         }
         if (!c.s.has_support) N.jump_charge = 0;
+    } else if constexpr (G == PG_GAME_JUMPER) { // jumper.cpp:389-422 (double jump with a cooldown)
+        auto &J = c.s.gs.jp;
+        if (c.s.action_vy < 0) c.s.action_vy = 0;
+        if (c.s.action_vx > 0) c.s.facing_right = 1;
+        if (c.s.action_vx < 0) c.s.facing_right = 0;
+        float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+        int b1 = get_obj_from_floats(c, (float)((double)ax - ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        int b2 = get_obj_from_floats(c, (float)((double)ax + ((double)arx - .01)), (float)((double)ay - ((double)ary + .01)));
+        J.jump_delta = 0;
+        c.s.has_support = (jp_is_wall(b1) || b1 == c.s.out_of_bounds_object) ||
+                          (jp_is_wall(b2) || b2 == c.s.out_of_bounds_object); // can_support (:385-387)
+        if (c.s.has_support) J.jump_count = 2;
+        if (c.s.action_vy == 1 && J.jump_count > 0 && (c.s.cur_time - J.jump_time > 3)) { // JUMP_COOLDOWN
+            J.jump_count -= 1;
+            J.jump_delta = -1;
+        } else {
+            c.s.action_vy = 0;
+        }
+        if (c.s.action_vy > 0) J.jump_time = c.s.cur_time;
+        c.s.action_vrot = 0;
     } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:154-158
         c.s.action_vy = 0.2f;
         c.s.action_vrot = 0;
@@ -729,6 +751,10 @@ DEV void update_agent_velocity(Ctx &c) {
         if (!c.s.has_support) {
             if (vy > -2) vy -= c.s.gravity;
         }
+    } else if constexpr (G == PG_GAME_JUMPER) { // jumper.cpp:98-105
+        const float v_scale = 1.0f;
+        vx = (1 - c.s.mixrate) * vx + c.s.mixrate * c.s.maxspeed * c.s.action_vx * v_scale;
+        if (c.s.action_vy != 0) vy = c.s.maxspeed * c.s.action_vy * 2;
     } else if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:73-81: no (1 - mixrate) decay
         const float v_scale = 1.0f;
         vx = (float)((double)vx + (double)(c.s.mixrate * c.s.maxspeed * c.s.action_vx * v_scale) * .2);
@@ -812,6 +838,14 @@ DEV void handle_agent_collision(Ctx &c, int m) {
                 EF(c, F_RY, 0) = ary + c.s.r_inc;
                 c.s.fish_eaten += 1;
             }
+        }
+    } else if constexpr (G == PG_GAME_JUMPER) { // jumper.cpp:86-96
+        if (t == JP_GOAL) {
+            c.s.sd_reward += 10.0f; // GOAL_REWARD
+            c.s.sd_level_complete = 1;
+            c.s.sd_done = 1;
+        } else if (t == JP_SPIKE) {
+            c.s.sd_done = 1;
         }
     } else if constexpr (G == PG_GAME_CAVEFLYER) { // caveflyer.cpp:57-71
         if (t == CF_GOAL) {
@@ -2124,6 +2158,31 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
 }
 
+// ------------------------------------------------------------------ jumper (jumper.cpp:424-441)
+DEV void jumper_step_tail(Ctx &c) {
+    int fl = EI(c, F_FLAGS, 0);
+    if (c.s.action_vx > 0) fl &= ~EF_REFLECTED;
+    if (c.s.action_vx < 0) fl |= EF_REFLECTED;
+    EI(c, F_FLAGS, 0) = fl;
+    const float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), ary = EF(c, F_RY, 0);
+    float vy = EF(c, F_VY, 0);
+    const float vx = EF(c, F_VX, 0);
+    wave_sync();
+    if (fabs((double)vx) + fabs((double)vy) > .05) { // fabs of a float: the double C function
+        const int t = append_entity(c, ax, (float)((double)ay - (double)ary * .5), 0, 0.01f, 0.3f, 0.2f, TRAIL);
+        if (t >= 0) {
+            EI(c, F_EXPIRE_TIME, t) = 8;
+            EF(c, F_ALPHA, t) = .5f;
+        }
+        wave_sync();
+    }
+    if (vy > -2) {
+        vy -= 0.15f;
+        EF(c, F_VY, 0) = vy;
+    }
+    wave_sync();
+}
+
 // ------------------------------------------------------------------ caveflyer (caveflyer.cpp:289-324)
 DEV void caveflyer_step_tail(Ctx &c) {
     if (c.s.special_action == 1) {
@@ -2535,6 +2594,7 @@ DEV void game_step(Ctx &c) {
     if constexpr (G == PG_GAME_BOSSFIGHT) bossfight_step_tail(c, rg);
     if constexpr (G == PG_GAME_NINJA) ninja_step_tail(c);
     if constexpr (G == PG_GAME_CAVEFLYER) caveflyer_step_tail(c);
+    if constexpr (G == PG_GAME_JUMPER) jumper_step_tail(c);
     wave_sync();
     c.pt.mark(5);
 }
@@ -2640,6 +2700,7 @@ __global__ __launch_bounds__(64) void pg_step_kernel(PGDev d, const int32_t *env
         if constexpr (G == PG_GAME_STARPILOT) { PG_W(num_tail) }
         if constexpr (G == PG_GAME_BOSSFIGHT) { PG_W(last_fire_time) PG_W(gs) }
         if constexpr (G == PG_GAME_NINJA) { PG_W(last_fire_time) PG_W(gs) PG_W(has_support) PG_W(facing_right) }
+        if constexpr (G == PG_GAME_JUMPER) { PG_W(gs) PG_W(has_support) PG_W(facing_right) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -2671,6 +2732,7 @@ extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list
         PG_CASE(PG_GAME_BOSSFIGHT)
         PG_CASE(PG_GAME_NINJA)
         PG_CASE(PG_GAME_CAVEFLYER)
+        PG_CASE(PG_GAME_JUMPER)
     default: break;
     }
 #undef PG_CASE

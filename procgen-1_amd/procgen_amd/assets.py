@@ -79,9 +79,30 @@ class Atlas:
             img = bgs[n]
             self.backgrounds[i] = (place(img), img.shape[1], img.shape[0], 0)
 
+        if game == "jumper":  # the compass overlay table rides in image slot TABLE_SLOT
+            table = compass_table_words()
+            self.sprites[catalog.TABLE_SLOT] = (place(table), table.size, 1, 0)
+
         self.pixels = np.ascontiguousarray(np.concatenate(chunks)).astype(np.uint32)
         assert self.pixels.size < 2 ** 31
         self.game = game
+
+
+@functools.lru_cache(maxsize=None)
+def compass_table_words():
+    """jumper_compass.npz flattened to the uint32 words the oracle and the engine read:
+    magic, NY, NX, MAXW, MAXH; per cfg (hard + 2 * uncentered) x1, y1, bx0, by0, bnx, bny, cx, cy, cr
+    (float bits); dial[4][64] u64; needle[4][NY][NX][64] u64; jump[MAXW + 1][MAXH + 1][64] u64."""
+    path = os.path.join(ASSET_DIR, "jumper_compass.npz")
+    if not os.path.exists(path):
+        raise FileNotFoundError("%s missing (run tools/make_compass_tables.py)" % path)
+    with np.load(path, allow_pickle=False) as z:
+        geom, cf, dial, needle, jump = z["cfg_geom"], z["cfg_cf"], z["dial"], z["needle"], z["jump"]
+    head = np.array([0x434D5053, needle.shape[1], needle.shape[2], jump.shape[0] - 1, jump.shape[1] - 1], np.uint32)
+    cfg = np.concatenate([geom.astype(np.int32).view(np.uint32), cf.astype(np.float32).view(np.uint32)], axis=1)
+    parts = [head, cfg.reshape(-1)] + [np.ascontiguousarray(a, dtype=np.uint64).view(np.uint32).reshape(-1)
+                                       for a in (dial, needle, jump)]
+    return np.ascontiguousarray(np.concatenate(parts), dtype=np.uint32)
 
 
 @functools.lru_cache(maxsize=None)

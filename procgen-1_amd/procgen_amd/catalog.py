@@ -307,6 +307,24 @@ CAVEFLYER_SPRITES = {
     9: ["misc_assets/towerDefense_tile295.png"],
 }
 
+# ---------------------------------------------------------------- jumper
+# procgen/src/games/jumper.cpp:52-83 (PLAYER 0, GOAL 1, SPIKE 2, CAVEWALL 6, CAVEWALL_TOP 7,
+# PLAYER_JUMP 9, PLAYER_LEFT1 10, PLAYER_LEFT2 11, PLAYER_RIGHT1 12, PLAYER_RIGHT2 13)
+JUMPER_SPRITES = {
+    0: ["misc_assets/bunny2_ready.png"],
+    2: ["misc_assets/spikeMan_stand.png"],
+    1: ["misc_assets/carrot.png"],
+    9: ["misc_assets/bunny2_jump.png"],
+    12: ["misc_assets/bunny2_walk1.png"],
+    13: ["misc_assets/bunny2_walk2.png"],
+    10: ["misc_assets/bunny2_walk1.png"],
+    11: ["misc_assets/bunny2_walk2.png"],
+    7: ["platformer/tileBlue_05.png", "platformer/tileGreen_05.png", "platformer/tileYellow_06.png",
+        "platformer/tileBrown_06.png"],
+    6: ["platformer/tileBlue_08.png", "platformer/tileGreen_08.png", "platformer/tileYellow_09.png",
+        "platformer/tileBrown_09.png"],
+}
+
 GAMES = {
     # game name -> (sprite table, background group)
     "coinrun": (COINRUN_SPRITES, "platform"),   # coinrun.cpp:60-62
@@ -324,6 +342,7 @@ GAMES = {
     "bossfight": (BOSSFIGHT_SPRITES, "space"),  # bossfight.cpp:72-74
     "ninja": (NINJA_SPRITES, "platform"),       # ninja.cpp:43-45
     "caveflyer": (CAVEFLYER_SPRITES, "space"),  # caveflyer.cpp:31-33
+    "jumper": (JUMPER_SPRITES, "platform"),     # jumper.cpp:48-50
 }
 
 # Game ids used across the C ABI (procgen/env.py:15-32 ordering).
@@ -348,3 +367,8 @@ def sprite_table(game):
 def num_themes(game):
     """asset_num_themes[type] for every type with a sprite (basic-abstract-game.cpp:113-119)."""
     return {t: len(v) for t, v in sprite_table(game).items()}
+
+
+# Image slot that carries a game's Qt-tabulated overlay raster instead of a sprite (never drawn as an
+# image): jumper's compass (jumper.cpp:137-177; tools/make_compass_tables.py -> jumper_compass.npz).
+TABLE_SLOT = 99

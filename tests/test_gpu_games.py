@@ -66,7 +66,7 @@ def run_pair(game, num, steps, seed=0, latent=False, **gpu_kw):
 LATENT = ("maze", "miner")
 # every game of this build except coinrun (tests/test_gpu_coinrun.py)
 GAMES = ["bigfish", "maze", "heist", "miner", "climber", "leaper", "chaser", "fruitbot", "dodgeball", "plunder",
-         "starpilot", "bossfight", "ninja", "caveflyer"]
+         "starpilot", "bossfight", "ninja", "caveflyer", "jumper"]
 
 
 @pytest.mark.parametrize("game", GAMES)
@@ -171,6 +171,17 @@ def test_caveflyer_modes():
     run_pair("caveflyer", 32, 600, seed=27, num_levels=0, rand_seed=16)
     run_pair("caveflyer", 8, 300, seed=28, num_levels=0, rand_seed=17, distribution_mode="easy")
     run_pair("caveflyer", 8, 200, seed=29, num_levels=0, rand_seed=18, distribution_mode="memory")
+
+
+def test_jumper_modes():
+    """jumper: MazeGen + RoomGenerator levels, spikes and long-wall breaking (in-order scans), double
+    jumps with a cooldown, trails, the compass overlay (Qt-tabulated dial / needle / jump ellipse,
+    double atan2 + sin / cos for the needle, the distance bar); easy, uncentered and memory (45x45,
+    no compass, timeout 2000) modes."""
+    run_pair("jumper", 32, 600, seed=30, num_levels=0, rand_seed=19)
+    run_pair("jumper", 8, 300, seed=31, num_levels=0, rand_seed=20, distribution_mode="easy")
+    run_pair("jumper", 8, 200, seed=32, num_levels=0, rand_seed=21, center_agent=False)
+    run_pair("jumper", 8, 200, seed=33, num_levels=0, rand_seed=22, distribution_mode="memory")
 
 
 def test_bigfish_long_episodes():

@@ -194,7 +194,7 @@ def test_oracle_trajectory_fixture():
         fi += 1
 
 
-MAZE_CASES = [(mode, dim, 0) for mode in (0, 1) for dim in (3, 5, 7, 11, 13, 15, 25)] + \
+MAZE_CASES = [(mode, dim, 0) for mode in (0, 1) for dim in (3, 5, 6, 7, 11, 13, 15, 25)] + \
              [(2, dim, doors) for dim in (5, 7, 9, 11, 13, 23) for doors in (0, 1, 2, 3)]
 
 
@@ -333,3 +333,32 @@ def test_spawner_sort_vs_libstdcxx(tmp_path):
         lib.oracle_spawn_sort(key.ctypes.data, a.ctypes.data, n)
         cxx.cxx_sort(key.ctypes.data, b.ctypes.data, n)
         np.testing.assert_array_equal(a, b, err_msg="trial %d n %d kind %d" % (trial, n, kind))
+
+
+def test_jumper_compass_table_pins():
+    """jumper's compass overlay is stamped from Qt 5.9.7 raster output (tools/qt_compass_tables.cpp):
+    the translucent jump ellipse's SourceOver blend equals premultiplied 0x78787878 + BYTE_MUL(dst, 135)
+    on every pixel Qt changed, and the packed table words carry the per-configuration geometry."""
+    from procgen_amd.assets import ASSET_DIR, compass_table_words
+    z = np.load(os.path.join(ASSET_DIR, "jumper_compass.npz"), allow_pickle=False)
+    bg, out = z["blend_bg"].astype(np.uint64), z["blend_out"].astype(np.uint64)
+
+    def byte_mul(x, a):
+        t = (x & 0xff00ff) * a
+        t = ((t + ((t >> 8) & 0xff00ff) + 0x800080) >> 8) & 0xff00ff
+        x = ((x >> 8) & 0xff00ff) * a
+        x = (x + ((x >> 8) & 0xff00ff) + 0x800080) & 0xff00ff00
+        return x | t
+
+    changed = out != bg
+    assert changed.sum() > 500
+    pred = (0x78787878 + byte_mul(bg, 135)) & 0xffffffff
+    np.testing.assert_array_equal(pred[changed], out[changed])
+    w = compass_table_words()
+    assert w[0] == 0x434D5053
+    geom = z["cfg_geom"]
+    for cfg in range(4):
+        np.testing.assert_array_equal(w[5 + 9 * cfg:5 + 9 * cfg + 6].view(np.int32), geom[cfg])
+    # hard mode, centred: the dial is Qt's midpoint ellipse of QRect(55, 1, 8, 8) with a 1-px pen
+    dial = z["dial"][1]
+    assert int(dial[1]) != 0 and int(dial[0]) == 0 and all(int(r) == 0 for r in dial[11:])
