@@ -14,6 +14,7 @@ measure exactly 65,536 x 12,288 B per launch (self-check below).
 """
 import csv
 import collections
+import re
 import json
 import os
 import shutil
@@ -22,10 +23,16 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def base_name(name):
+    """'void (anonymous namespace)::pg_step_kernel<5>(PGDev, ...)' -> 'pg_step_kernel'"""
+    m = re.search(r"(pg_\w+?_kernel)", name)
+    return m.group(1) if m else name
+
+
 def per_kernel(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        agg[base_name(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
@@ -33,7 +40,16 @@ def main(tag, prof=os.path.join(REPO, "gpurun_out", "prof")):
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
                 os.path.join(REPO, "profiles", "%s_kernel_stats.csv" % tag))
-    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv")))}
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))):
+        k = base_name(r["Name"])
+        if k in stats:  # several template instances (mixed batches): call-weighted average
+            a, b = stats[k], r
+            calls = int(a["Calls"]) + int(b["Calls"])
+            avg = (float(a["AverageNs"]) * int(a["Calls"]) + float(b["AverageNs"]) * int(b["Calls"])) / calls
+            stats[k] = {"Calls": calls, "AverageNs": avg}
+        else:
+            stats[k] = r
     fetch = per_kernel(os.path.join(prof, "fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(prof, "write", "run_counter_collection.csv"))
     out = {"tag": tag, "units": "bytes per launch", "kernels": {}}
