@@ -87,6 +87,9 @@ def main():
     ap.add_argument("--num-levels", type=int, default=None,
                     help="default: 200 for coinrun (configs[1]), 0 = unbounded otherwise (SURVEY 8d)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="after every step, RCCL all-gather of every rank's uint8[E,64,64,3] obs shard into a "
+                         "[N*E,64,64,3] tensor on each rank (north star's obs concatenation; SURVEY 8(e))")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,10 +112,36 @@ def main():
     env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
                          distribution_mode="hard", device_buffers=True, env_offset=rank * E)
     seed = 0x5EED
+    gather = None
+    if args.gather:
+        # the engine's HBM obs shard as a torch tensor (no copy), gathered on the engine's own stream so
+        # the collective is ordered after the render of the same step and before the next step's
+        dp = env.device_ptrs()
+
+        class _Shard:
+            __cuda_array_interface__ = {"shape": (E, 64, 64, 3), "typestr": "|u1", "data": (dp.rgb, False),
+                                        "version": 2}
+
+        local = torch.as_tensor(_Shard(), device="cuda")
+        gathered = torch.empty((world * E, 64, 64, 3), dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.ExternalStream(dp.stream)
+
+        def gather():
+            with torch.cuda.stream(stream):
+                if dist is not None:
+                    dist.all_gather_into_tensor(gathered, local)
+                else:
+                    gathered.copy_(local)
+
+    def step(t):
+        env.act_hashed(seed, t)
+        if gather is not None:
+            gather()
+
     t = 0
     for _ in range(args.warmup):
         t += 1
-        env.act_hashed(seed, t)
+        step(t)
     env.wait()
 
     def barrier():
@@ -126,7 +155,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         t += 1
-        env.act_hashed(seed, t)
+        step(t)
     env.wait()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -169,7 +198,9 @@ def main():
                                    "center_agent, backgrounds, random actions (device counter hash)"
                                    % (game, E, num_levels),
                        "env_name": game, "num_envs_per_gpu": E, "global_envs": world * E,
-                       "parallelism": "env-sharded x%d" % world},
+                       "parallelism": "env-sharded x%d" % world,
+                       "gather": ("rccl all_gather_into_tensor of obs, %d B per rank per step" % (E * OBS_BYTES))
+                       if args.gather else None},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

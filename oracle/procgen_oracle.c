@@ -5265,3 +5265,20 @@ int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas) {
     }
     return (int)(r.p - cmds);
 }
+
+/* diagnostic: type, image_type, rotation bits, rx bits, alpha bits of env i's entities (5 words each);
+ * returns the entity count */
+int oracle_entities(void *h, int i, int32_t *out, int max_ents) {
+    Vec *v = (Vec *)h;
+    Game *g = &v->games[i];
+    int n = g->num_ents < max_ents ? g->num_ents : max_ents;
+    for (int k = 0; k < n; k++) {
+        Entity *e = &g->ents[k];
+        out[5 * k] = e->type;
+        out[5 * k + 1] = e->image_type;
+        memcpy(&out[5 * k + 2], &e->rotation, 4);
+        memcpy(&out[5 * k + 3], &e->rx, 4);
+        memcpy(&out[5 * k + 4], &e->alpha, 4);
+    }
+    return g->num_ents;
+}

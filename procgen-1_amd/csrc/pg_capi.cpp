@@ -323,6 +323,11 @@ struct VecEnv {
     // games of the batch: env n plays games[n % games.size()]
     std::vector<int> games;
     int32_t *d_lists = nullptr;            // [games.size()][num_envs / games.size()] env ids (mixed only)
+    // mixed batches: each game's step -> reset -> render chain runs on its own stream (the games'
+    // envs are disjoint), forked from and joined back into `stream` every act
+    std::vector<hipStream_t> gstreams;
+    std::vector<hipEvent_t> gdone;
+    hipEvent_t fork = nullptr;
     bool has_latent = false;               // maze fills the fork's latent-state info
     const int32_t *list_of(size_t k) const {
         return games.size() > 1 ? d_lists + k * (size_t)(num_envs / games.size()) : nullptr;
@@ -387,34 +392,38 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
 int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
-    hipEvent_t *e = nullptr;
+    const size_t G = v->games.size();
+    hipEvent_t *e = nullptr; // 4 per game: before step, after step, after reset, after render
     if (v->timing) {
-        size_t need = (size_t)(v->t_used + 1) * 4;
+        size_t need = (size_t)(v->t_used + 1) * 4 * G;
         while (v->ev.size() < need) {
             hipEvent_t x;
             HIPCHECK(hipEventCreate(&x));
             v->ev.push_back(x);
         }
-        e = &v->ev[(size_t)v->t_used * 4];
+        e = &v->ev[(size_t)v->t_used * 4 * G];
         v->t_used++;
     }
     HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t) * PG_NUM_GAMES, v->stream));
-    if (e) HIPCHECK(hipEventRecord(e[0], v->stream));
-    for (size_t k = 0; k < v->games.size(); k++) {
-        PG_POISON(v->stream);
-        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, use_hash, seed, t);
+    if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
+    for (size_t k = 0; k < G; k++) {
+        hipStream_t s = G > 1 ? v->gstreams[k] : v->stream;
+        if (G > 1) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
+        if (e) HIPCHECK(hipEventRecord(e[4 * k], s));
+        PG_POISON(s);
+        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, use_hash, seed, t);
+        if (e) HIPCHECK(hipEventRecord(e[4 * k + 1], s));
+        PG_POISON(s);
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 0, 0);
+        if (e) HIPCHECK(hipEventRecord(e[4 * k + 2], s));
+        PG_POISON(s);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s);
+        if (e) HIPCHECK(hipEventRecord(e[4 * k + 3], s));
+        if (G > 1) {
+            HIPCHECK(hipEventRecord(v->gdone[k], s));
+            HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
+        }
     }
-    if (e) HIPCHECK(hipEventRecord(e[1], v->stream));
-    for (size_t k = 0; k < v->games.size(); k++) {
-        PG_POISON(v->stream);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, 0);
-    }
-    if (e) HIPCHECK(hipEventRecord(e[2], v->stream));
-    for (size_t k = 0; k < v->games.size(); k++) {
-        PG_POISON(v->stream);
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
-    }
-    if (e) HIPCHECK(hipEventRecord(e[3], v->stream));
     HIPCHECK(hipGetLastError());
     return 0;
 }
@@ -584,6 +593,21 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess) {
         delete v;
         return bad("hipStreamCreate failed");
+    }
+    if (gids.size() > 1) {
+        bool ok = hipEventCreateWithFlags(&v->fork, hipEventDisableTiming) == hipSuccess;
+        for (size_t k = 0; k < gids.size() && ok; k++) {
+            hipStream_t s = nullptr;
+            hipEvent_t d = nullptr;
+            ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&d, hipEventDisableTiming) == hipSuccess;
+            v->gstreams.push_back(s);
+            v->gdone.push_back(d);
+        }
+        if (!ok) {
+            libenv_close((libenv_env *)v);
+            return bad("hipStreamCreate failed");
+        }
     }
     (void)hipGetDevice(&v->device);
 
@@ -800,6 +824,11 @@ LIBENV_API void libenv_close(libenv_env *env) {
     if (v->h_actions) (void)hipHostFree(v->h_actions);
     for (auto &e : v->ev)
         if (e) hipEventDestroy(e);
+    for (auto &e : v->gdone)
+        if (e) hipEventDestroy(e);
+    if (v->fork) hipEventDestroy(v->fork);
+    for (auto &s : v->gstreams)
+        if (s) hipStreamDestroy(s);
     if (v->stream) hipStreamDestroy(v->stream);
     delete v;
 }
@@ -858,15 +887,20 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
     double sum[4] = {0, 0, 0, 0};
+    // per kernel: the sum over the batch's games of that kernel's duration (mixed batches run
+    // the games' chains concurrently, so the sum can exceed the wall time of a step)
+    const size_t G = v->games.size();
     if (v->t_used > 0) {
-        HIPCHECK(hipEventSynchronize(v->ev[(size_t)v->t_used * 4 - 1]));
+        HIPCHECK(hipStreamSynchronize(v->stream));
         for (int k = 0; k < v->t_used; k++) {
-            hipEvent_t *e = &v->ev[(size_t)k * 4];
-            float a = 0, b = 0, c = 0;
-            HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));
-            HIPCHECK(hipEventElapsedTime(&b, e[1], e[2]));
-            HIPCHECK(hipEventElapsedTime(&c, e[2], e[3]));
-            sum[0] += a; sum[1] += b; sum[2] += c; sum[3] += a + b + c;
+            for (size_t g = 0; g < G; g++) {
+                hipEvent_t *e = &v->ev[((size_t)k * G + g) * 4];
+                float a = 0, b = 0, c = 0;
+                HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));
+                HIPCHECK(hipEventElapsedTime(&b, e[1], e[2]));
+                HIPCHECK(hipEventElapsedTime(&c, e[2], e[3]));
+                sum[0] += a; sum[1] += b; sum[2] += c; sum[3] += a + b + c;
+            }
         }
     }
     for (int i = 0; i < n && i < 4; i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;

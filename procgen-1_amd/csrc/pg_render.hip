@@ -75,17 +75,18 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Size of the per-type grid sprite table (grid values 0..127 take the fast path).
 #define NTYPES 128
-// Most grid tile images have this size ("class 0"); one other size per game is handled by the
-// generic pass (maze's 27 px cheese), anything else is flagged, never drawn wrongly.
-#define TILE_PX 128
-// Most tile rows a frame may span on the fast path (centred coinrun views span 14-15).
-#define CROWS 16
+// Most tile rows a frame may span on the fast path (centred views of visibility 16 span 17-18).
+#define CROWS 18
 // Rows per batch of the pixel-centric pass, entities per stamping group.
 #ifndef RB
 #define RB 8
 #endif
 #ifndef EG
 #define EG 8
+#endif
+// Rows / chunks of one large image whose texel loads are issued together before the blends.
+#ifndef BB
+#define BB 1
 #endif
 
 
@@ -172,9 +173,22 @@ DEV float tile_aspect_ratio(int type, float rx, float ry) {
 }
 template <int G>
 DEV bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
-// every grid tile the game draws is a TILE_PX-square image (the fast path's assumption)
+// Side of the square grid-tile images of the pixel-centric fast path (0: the game always takes the
+// generic tile pass).  Coinrun and heist draw only such tiles; for the others a frame takes the fast
+// path when every tile in its window is one (a window scan decides, e.g. jumper's and climber's
+// 64x53 fourth wall theme or a visible ninja bomb send the frame to the generic pass).
 template <int G>
-DEV bool uniform_tiles() { return G == PG_GAME_COINRUN || G == PG_GAME_HEIST; }
+DEV constexpr int tile_px() {
+    if constexpr (G == PG_GAME_COINRUN || G == PG_GAME_HEIST || G == PG_GAME_CAVEFLYER) return 128;
+    if constexpr (G == PG_GAME_JUMPER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_LEAPER) return 64;
+    if constexpr (G == PG_GAME_DODGEBALL) return 12;
+    return 0;
+}
+template <int G>
+DEV constexpr bool uniform_tiles() { return tile_px<G>() > 0; }
+// every drawable grid type of the game has a tile_px() image: no window scan needed
+template <int G>
+DEV constexpr bool always_uniform() { return G == PG_GAME_COINRUN || G == PG_GAME_HEIST || G == PG_GAME_CAVEFLYER; }
 // the game has render_z = -1 entities (drawn between background and grid, :933)
 template <int G>
 DEV bool has_z_minus1() { return G == PG_GAME_MINER; } // miner's exit (miner.cpp:217)
@@ -247,18 +261,30 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
         Axis ex, ey;
         if (!axis_setup_signed(ax, bx - ax, iw, ex) || !axis_setup_signed(ay, by - ay, ih, ey)) return true;
         const int lane = LANE;
+        bool ok = true;
         if (lane >= ex.t1 && lane < ex.t1 + ex.n) {
             int scol = (int)((ex.base + (uint32_t)((lane - ex.t1) * ex.step)) >> 16);
             if (mir) scol = iw - 1 - scol;
-            for (int k = 0; k < ey.n; k++) {
-                const int srow = (int)((ey.base + (uint32_t)(k * ey.step)) >> 16);
-                const uint32_t idx = soff + (uint32_t)(srow * iw + scol);
-                if (idx >= npix) return false;
-                const int o = (ey.t1 + k) * PG_RES + lane;
-                fb[o] = blend_argb_pm(fb[o], pixels[idx], ca);
+            for (int k0 = 0; k0 < ey.n; k0 += BB) { // BB rows: every texel load issued before the blends
+                uint32_t tv[BB];
+#pragma unroll
+                for (int r = 0; r < BB; r++) {
+                    const int k = k0 + r;
+                    const uint32_t idx = soff + (uint32_t)(((int)((ey.base + (uint32_t)(k * ey.step)) >> 16)) * iw + scol);
+                    const bool in = k < ey.n && idx < npix;
+                    if (k < ey.n && !in) ok = false;
+                    tv[r] = pixels[in ? idx : 0u];
+                }
+#pragma unroll
+                for (int r = 0; r < BB; r++) {
+                    const int k = k0 + r;
+                    if (k >= ey.n) break;
+                    const int o = (ey.t1 + k) * PG_RES + lane;
+                    fb[o] = blend_argb_pm(fb[o], tv[r], ca);
+                }
             }
         }
-        return true;
+        return ok;
     }
     QV v[4]; // TopLeft, TopRight, BottomRight, BottomLeft
     auto map = [&](double px, double py, QV &o) {
@@ -315,25 +341,37 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
         trap_setup(v[1], v[2], v[3], v[2], v[1].y, v[2].y, tr[2]);
     }
     const int lane = LANE;
+    bool ok = true;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const Trap T = tr[k];
-        for (int yy = T.from_y; yy < T.to_y; yy++) {
-            const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
-            const int fromX = max(xl >> 16, 0), toX = min(xr >> 16, PG_RES);
-            if (lane >= fromX && lane < toX) {
+        for (int y0 = T.from_y; y0 < T.to_y; y0 += BB) { // BB scan lines: loads first, then blends
+            uint32_t tv[BB];
+            bool on[BB];
+#pragma unroll
+            for (int r = 0; r < BB; r++) {
+                const int yy = y0 + r;
+                const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
+                const int fromX = max(xl >> 16, 0), toX = min(xr >> 16, PG_RES);
+                on[r] = yy < T.to_y && lane >= fromX && lane < toX;
                 int uu = (lane * dudx + yy * dudy + u0) >> 16;
                 int vv = (lane * dvdx + yy * dvdy + v0) >> 16;
                 uu = min(max(uu, 0), iw - 1);
                 vv = min(max(vv, 0), ih - 1);
                 if (mir) uu = iw - 1 - uu;
                 const uint32_t idx = soff + (uint32_t)(vv * iw + uu);
-                if (idx >= npix) return false;
-                fb[yy * PG_RES + lane] = blend_argb_pm(fb[yy * PG_RES + lane], pixels[idx], ca);
+                if (on[r] && idx >= npix) {
+                    ok = false;
+                    on[r] = false;
+                }
+                tv[r] = pixels[on[r] ? idx : 0u];
             }
+#pragma unroll
+            for (int r = 0; r < BB; r++)
+                if (on[r]) fb[(y0 + r) * PG_RES + lane] = blend_argb_pm(fb[(y0 + r) * PG_RES + lane], tv[r], ca);
         }
     }
-    return true;
+    return ok;
 }
 
 
@@ -495,18 +533,30 @@ DEV double readlane_d(double x, int j) {
 // One scale blit, all lanes cooperating over its footprint (uniform arguments).
 DEV void blit_seq(uint32_t *fb, const PGDev &d, const Axis &ex, const Axis &ey, uint32_t soff, int sw, int mir, int ca,
                   bool &err) {
-    const int nx = ex.n, ny = ey.n;
+    const int nx = ex.n, ny = ey.n, total = nx * ny;
     const float inv = 1.0f / (float)nx;
-    for (int p = LANE; p < nx * ny; p += 64) {
-        int py = (int)(((float)p + 0.5f) * inv);
-        int pxx = p - py * nx;
-        int scol = (int)((ex.base + (uint32_t)(pxx * ex.step)) >> 16);
-        int srow = (int)((ey.base + (uint32_t)(py * ey.step)) >> 16);
-        if (mir) scol = sw - 1 - scol;
-        const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
-        const int o = (ey.t1 + py) * PG_RES + ex.t1 + pxx;
-        if (idx < d.num_pixels && o >= 0 && o < PG_RES * PG_RES) fb[o] = blend_argb_pm(fb[o], d.pixels[idx], ca);
-        else err = true;
+    // the footprint's pixels are distinct, so BB chunks of 64 load their texels before any blend
+    for (int p0 = LANE; p0 < total; p0 += 64 * BB) {
+        uint32_t tv[BB];
+        int oo[BB];
+#pragma unroll
+        for (int r = 0; r < BB; r++) {
+            const int p = p0 + 64 * r;
+            const int py = (int)(((float)p + 0.5f) * inv);
+            const int pxx = p - py * nx;
+            int scol = (int)((ex.base + (uint32_t)(pxx * ex.step)) >> 16);
+            const int srow = (int)((ey.base + (uint32_t)(py * ey.step)) >> 16);
+            if (mir) scol = sw - 1 - scol;
+            const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
+            const int o = (ey.t1 + py) * PG_RES + ex.t1 + pxx;
+            const bool in = p < total && idx < d.num_pixels && o >= 0 && o < PG_RES * PG_RES;
+            if (p < total && !in) err = true;
+            oo[r] = in ? o : -1;
+            tv[r] = d.pixels[in ? idx : 0u];
+        }
+#pragma unroll
+        for (int r = 0; r < BB; r++)
+            if (oo[r] >= 0) fb[oo[r]] = blend_argb_pm(fb[oo[r]], tv[r], ca);
     }
 }
 
@@ -789,7 +839,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
             } else {
                 int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
                 int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
-                if (sp.y == TILE_PX && sp.z == TILE_PX) off = sp.x;
+                if (sp.y == tile_px<G>() && sp.z == tile_px<G>()) off = sp.x;
                 else if (sp.y > 0) off = -2;
                 else off = -3; // generated assets: not in this build
             }
@@ -842,11 +892,11 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
             double rx, ry, rw, rh;
             if (lane < ww) {
                 screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
-                xr = rx; xw = rw; xiw = TILE_PX;
+                xr = rx; xw = rw; xiw = tile_px<G>();
             }
             if (lane < wh) {
                 screen_rect(v, 0.0f, (float)(low_y + lane + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
-                yr = ry; yh = rh; yih = TILE_PX;
+                yr = ry; yh = rh; yih = tile_px<G>();
             }
         }
         Axis a, b;
@@ -973,6 +1023,18 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         jy0 = jlo;
         nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
         fast = nrows <= CROWS;
+        if constexpr (!always_uniform<G>()) {
+            if (fast) { // every tile of the window must be a tile_px() square (or nothing)
+                bool other = false;
+                for (int k = lane; k < ww * wh; k += 64) {
+                    const int x = low_x + k % ww, y = low_y + k / ww;
+                    const int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                             : s.out_of_bounds_object;
+                    if (type != INVALID_OBJ && (type < 0 || type >= NTYPES || tile_off[type] <= -2)) other = true;
+                }
+                fast = ballot(other) == 0;
+            }
+        }
     }
     auto lookup_grid = [&](int x, int y) -> int {
         int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
@@ -1044,8 +1106,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 const int nr = info[k] >> 24;
                 ta[k] = 0;
                 tb[k] = 0;
-                if (nr > 0 && ca[k] >= 0) ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((info[k] & 127) * TILE_PX)];
-                if (nr > 1 && cbv[k] >= 0) tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((info[k] >> 7) & 127) * TILE_PX)];
+                if (nr > 0 && ca[k] >= 0) ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((info[k] & 127) * tile_px<G>())];
+                if (nr > 1 && cbv[k] >= 0) tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((info[k] >> 7) & 127) * tile_px<G>())];
             }
 #pragma unroll
             for (int k = 0; k < RB; k++) {
@@ -1072,7 +1134,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                     const int code = lookup_grid(x1, l ? ry1 : ry0);
                     if (code <= -2) err = true;
                     if (code >= 0) {
-                        const uint32_t t = d.pixels[(uint32_t)code + (uint32_t)((l ? srow1 : srow0) * TILE_PX + sc1)];
+                        const uint32_t t = d.pixels[(uint32_t)code + (uint32_t)((l ? srow1 : srow0) * tile_px<G>() + sc1)];
                         px = t + BYTE_MUL(px, (~t) >> 24);
                     }
                 }

@@ -20,12 +20,12 @@ STEP = ["rng+action", "set_action+velocity", "step_entities", "collisions", "era
 RENDER = ["setup tables", "bg+tiles", "entities", "output"]
 
 
-def main(num=65536, warm=20, steps=50):
+def main(game="coinrun", num=65536, warm=20, steps=50):
     torch.cuda.set_device(0)
     from procgen_amd import ProcgenGym3Env, _lib
     lib = _lib.load()
-    env = ProcgenGym3Env(num=num, env_name="coinrun", num_levels=200, start_level=0, rand_seed=0,
-                         device_buffers=True)
+    env = ProcgenGym3Env(num=num, env_name=game, num_levels=200 if game == "coinrun" else 0, start_level=0,
+                         rand_seed=0, device_buffers=True)
     for t in range(1, warm + 1):
         env.act_hashed(0x5EED, t)
     env.wait()
@@ -37,10 +37,11 @@ def main(num=65536, warm=20, steps=50):
     b = np.zeros(16, np.uint64)
     lib.procgen_profile_read(env._handle, b.ctypes.data)
     d = (b - a).astype(np.float64) / (num * steps)
-    out = {"cycles_per_env_step": {"step": {n: round(d[k], 1) for k, n in enumerate(STEP)},
+    out = {"game": game, "cycles_per_env_step": {"step": {n: round(d[k], 1) for k, n in enumerate(STEP)},
                                    "render": {n: round(d[8 + k], 1) for k, n in enumerate(RENDER)}}}
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    for g in (sys.argv[1:] or ["coinrun"]):
+        main(g)
