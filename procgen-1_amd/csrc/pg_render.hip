@@ -389,6 +389,7 @@ struct Img {
     int ntile;             // > 0: tile_image with this many tiles (seq path)
     float tw, th;          // tile size (float, as tile_image computes it)
     double rx, ry, rw, rh; // target rect of a rotated / tiled image
+    double m11, m12, m21;  // rotation matrix of a rotated image (m22 = m11), built lane-parallel
 };
 
 DEV void img_clear(Img &im) {
@@ -615,16 +616,10 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
             if (j < 0) continue;
             const int caj = readlane(im.ca, j);
             if (readlane(im.rot ? 1 : 0, j)) {
-                const int k = readlane(im.rslot, j);
-                double mt[4];
-                if (k >= 0) {
-                    const double *tm = d.rot_table + 4 * k;
-                    mt[0] = tm[0]; mt[1] = tm[1]; mt[2] = tm[2]; mt[3] = tm[3];
-                } else {
-                    qt_rotation_matrix(__builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j)), mt);
-                }
+                const double m11 = readlane_d(im.m11, j);
                 if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
-                                  readlane_d(im.rh, j), mt[0], mt[1], mt[2], mt[3], (uint32_t)readlane(im.soff, j),
+                                  readlane_d(im.rh, j), m11, readlane_d(im.m12, j), readlane_d(im.m21, j), m11,
+                                  (uint32_t)readlane(im.soff, j),
                                   readlane(im.sw, j), readlane(im.sh, j), readlane(im.mir, j) != 0, caj))
                     err = true;
                 continue;
@@ -732,8 +727,17 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         int rslot = -1;
         for (int k = 0; k < PG_ROT_N; k++)
             if (__float_as_uint(d.rot_angles[k]) == __float_as_uint(rotation)) rslot = k;
-        // rslot < 0: an angle outside the host table, its matrix is built on the device at blit
-        // time (qt_rotation_matrix; the rotation value rides in tw)
+        // rslot < 0: an angle outside the host table, its matrix is built on the device
+        // (qt_rotation_matrix), by this entity's lane, before the in-order stamping
+        double mt[4];
+        if (rslot >= 0) {
+            const double *tm = d.rot_table + 4 * rslot;
+            mt[0] = tm[0]; mt[1] = tm[1]; mt[2] = tm[2]; mt[3] = tm[3];
+        } else {
+            qt_rotation_matrix(rotation, mt);
+        }
+        if (mt[3] != mt[0]) err = true; // a rotation matrix has m22 == m11
+        im.m11 = mt[0]; im.m12 = mt[1]; im.m21 = mt[2];
         im.rslot = rslot;
         im.tw = rotation;
         im.draw = true;
