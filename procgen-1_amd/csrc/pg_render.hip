@@ -74,9 +74,12 @@ DEV bool is_player_image(int t) {
 DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Size of the per-type grid sprite table (grid values 0..127 take the fast path).
-#define NTYPES 128
-// Most tile rows a frame may span on the fast path (centred views of visibility 16 span 17-18).
-#define CROWS 18
+#define NTYPES 64 // grid values 0..63 (and SPACE) take the fast path; anything else falls back
+// Most tile rows a frame may span on the fast path: centred views of visibility 13 (coinrun) span
+// 14-15, of visibility 16 17-18.  The frame buffer (16 KB) + colb + tile_off of coinrun / heist fit
+// 20 KB, i.e. 8 workgroups per CU's 160 KB LDS.
+template <int G>
+DEV constexpr int crows() { return (G == PG_GAME_COINRUN || G == PG_GAME_HEIST) ? 15 : 18; }
 // Rows per batch of the pixel-centric pass, entities per stamping group.
 #ifndef RB
 #define RB 8
@@ -776,12 +779,13 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
     // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
     // <= -2 not drawable on the fast path
+    constexpr int CR = crows<G>();
     __shared__ int tile_off[NTYPES];
     // fast path: texel base of lane's first tile column per tile row.  Before it is built, the
     // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row
     // (class 0 at [0, 128), class 1 at [128, 256) in int4 units).
-    __shared__ __attribute__((aligned(16))) int colb[CROWS * 64];
-    static_assert(CROWS * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
+    __shared__ __attribute__((aligned(16))) int colb[CR * 64];
+    static_assert(CR * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
@@ -1026,7 +1030,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
         jy0 = jlo;
         nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
-        fast = nrows <= CROWS;
+        fast = nrows <= CR;
         if constexpr (!always_uniform<G>()) {
             if (fast) { // every tile of the window must be a tile_px() square (or nothing)
                 bool other = false;
@@ -1034,7 +1038,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                     const int x = low_x + k % ww, y = low_y + k / ww;
                     const int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
                                                                                              : s.out_of_bounds_object;
-                    if (type != INVALID_OBJ && (type < 0 || type >= NTYPES || tile_off[type] <= -2)) other = true;
+                    if (type != INVALID_OBJ && type != SPACE && (type < 0 || type >= NTYPES || tile_off[type] <= -2))
+                        other = true;
                 }
                 fast = ballot(other) == 0;
             }
@@ -1043,16 +1048,16 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     auto lookup_grid = [&](int x, int y) -> int {
         int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
                                                                                : s.out_of_bounds_object;
-        return type == INVALID_OBJ ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
+        return (type == INVALID_OBJ || type == SPACE) ? -1 : ((type >= 0 && type < NTYPES) ? tile_off[type] : -2);
     };
     wave_sync(); // tile table complete
     if (fast) {
         // ---- lookups for the fast path: every screen row's tile rows lie in [jy0, jy1]; for
         //      each of those rows the texel base of this lane's first tile column goes to LDS
         //      (colb), so a pixel costs one LDS read + one texel load + one blend.
-        int code[CROWS];
+        int code[CR];
 #pragma unroll
-        for (int j = 0; j < CROWS; j++) {
+        for (int j = 0; j < CR; j++) {
             code[j] = -1;
             if (j < nrows && ncx0 > 0) {
                 const int y = jy0 + j, x = cx0;
@@ -1062,10 +1067,10 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
         wave_sync(); // colb's axis-table contents are dead from here
 #pragma unroll
-        for (int j = 0; j < CROWS; j++) {
+        for (int j = 0; j < CR; j++) {
             if (j < nrows) {
                 int t = code[j];
-                int c = (ncx0 == 0 || t == INVALID_OBJ) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
+                int c = (ncx0 == 0 || t == INVALID_OBJ || t == SPACE) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
                 if (c <= -2) err = true;
                 colb[j * 64 + lane] = c >= 0 ? c + scol0 : -1;
             }
