@@ -4644,6 +4644,21 @@ static float hook_tile_aspect_ratio(Game *g, const Entity *e) {
     return 0;                                                            /* :417-419 */
 }
 
+/* color_for_type (basic-abstract-game.cpp:464-490): monochrome colour of (type, theme), k = 4 */
+static uint32_t color_for_type(Game *g, int type, int theme) {
+    theme = mask_theme(g, theme, type);
+    int new_type = (29 * (type + 1)) % 64;
+    new_type = (new_type + 19 * theme) % 64;
+    uint32_t r = 64 * (new_type / 16 + 1) - 1, gg = 64 * ((new_type / 4) % 4 + 1) - 1, b = 64 * (new_type % 4 + 1) - 1;
+    return 0xff000000u | (r << 16) | (gg << 8) | b;
+}
+
+/* to_shade (qt-utils.h:21-28) */
+static int to_shade(float f) {
+    int shade = (int)(f * 255);
+    return shade < 0 ? 0 : (shade > 255 ? 255 : shade);
+}
+
 static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, bool is_reflected, int base_type,
                        int theme, float alpha, float tile_ratio) { /* :886-922 */
     int img_type = hook_image_for_type(g, base_type);
@@ -4657,7 +4672,10 @@ static void draw_image(Game *g, const or_atlas *at, RectD base, float rotation, 
                           base.h * CH_ORB_DIM, 0xff00ff00u);
             return;
         }
-        fatal_msg("draw_grid_obj / monochrome not restated yet");
+        if (!g->options.use_monochrome_assets || img_type >= 64) /* color_for_type fasserts (:464-490) */
+            fatal_msg("draw_grid_obj: no colour for this type");
+        qt_fill_rectf(g->canvas, base.x, base.y, base.w, base.h, color_for_type(g, img_type, theme));
+        return;
     }
     fassert(theme < MAX_IMAGE_THEMES);
     theme = mask_theme(g, theme, img_type); /* the image initialize_asset_if_necessary loaded, :79-123 */
@@ -4755,7 +4773,14 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
     }
     draw_entities(g, at, 0);
     draw_entities(g, at, 1);
-    if (g->has_useful_vel_info && g->options.paint_vel_info) fatal_msg("paint_vel_info not restated yet");
+    if (g->has_useful_vel_info && g->options.paint_vel_info) { /* :969-977 */
+        Entity *agent = AG(g);
+        float infodim = (float)(RES_H * .2);
+        int s1 = to_shade((float)(.5 * (double)agent->vx / (double)g->maxspeed + .5));
+        int s2 = to_shade((float)(.5 * (double)agent->vy / (double)g->max_jump + .5));
+        qt_fill_rectf(g->canvas, 0, 0, infodim, infodim, 0xff000000u | (uint32_t)(s1 * 0x010101));
+        qt_fill_rectf(g->canvas, infodim, 0, infodim, infodim, 0xff000000u | (uint32_t)(s2 * 0x010101));
+    }
 }
 
 /* jumper's draw_compass (jumper.cpp:137-177).  The dial ellipse, the cosmetic needle line and the

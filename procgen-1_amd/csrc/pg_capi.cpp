@@ -579,8 +579,6 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     }
     if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
     if (use_generated_assets) return bad("use_generated_assets is not in this build yet");
-    if (use_monochrome_assets) return bad("use_monochrome_assets is not in this build yet");
-    if (paint_vel_info) return bad("paint_vel_info is not in this build yet");
     if (render_human) return bad("render_mode=rgb_array (render_human) is not in this build yet");
 
     VecEnv *v = new VecEnv();

@@ -439,6 +439,35 @@ DEV bool grid_obj_fill(int img, double rx, double ry, double rw, double rh, Img 
     return false;
 }
 
+// color_for_type (basic-abstract-game.cpp:464-490): the monochrome colour of (img_type, theme);
+// 0 when the reference would fassert (type >= k^3 = 64)
+template <int G>
+DEV uint32_t color_for_type(const PGEnv &s, int type, int theme) {
+    if (type < 0 || type >= 64) return 0;
+    theme = mask_theme<G>(s, theme, type);
+    int nt = (29 * (type + 1)) % 64;
+    nt = (nt + 19 * theme) % 64;
+    const uint32_t r = 64 * (nt / 16 + 1) - 1, g = 64 * ((nt / 4) % 4 + 1) - 1, b = 64 * (nt % 4 + 1) - 1;
+    return 0xff000000u | (r << 16) | (g << 8) | b;
+}
+
+// draw_grid_obj (basic-abstract-game.cpp:924-928) for monochrome assets, after the game's own
+// override (grid_obj_fill): fillRect(rect, color_for_type).  False when the reference fasserts.
+template <int G>
+DEV bool mono_fill(const PGEnv &s, int img, int theme, double rx, double ry, double rw, double rh, Img &im) {
+    if (grid_obj_fill<G>(img, rx, ry, rw, rh, im)) return true;
+    const uint32_t col = color_for_type<G>(s, img, theme);
+    if (col == 0) return false;
+    fill_setup(rx, ry, rw, rh, col, im);
+    return true;
+}
+
+// to_shade (qt-utils.h:21-28)
+DEV int to_shade(float f) {
+    int shade = (int)(f * 255);
+    return shade < 0 ? 0 : (shade > 255 ? 255 : shade);
+}
+
 // fillRect(QRectF, opaque colour) straight into the frame, lane-parallel (same edges as fill_setup)
 DEV void fb_fill_rectf(uint32_t *fb, double x, double y, double w, double h, uint32_t argb) {
     Img im;
@@ -684,7 +713,23 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
     int img = image_for_type<G>(s, itype, player_img);
     if (img < 0 || !should_draw<G>(s, etype, theme)) return;
     if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-        if (img != SPACE) err = true; // draw_grid_obj fills: not in this build
+        if (img == SPACE) return;
+        if (!s.opt_use_monochrome_assets) { // color_for_type fasserts without monochrome (:467-487)
+            err = true;
+            return;
+        }
+        // draw_grid_obj over the unadjusted object rect; rotation, reflection and alpha unused
+        double rx, ry, rw, rh;
+        if (flags & EF_ABS_COORDS) {
+            float vd = v.view_dim;
+            float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
+            rx = (double)(ax * v.unit); ry = (double)(ay * v.unit);
+            rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
+        } else {
+            screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+        }
+        if (!mono_fill<G>(s, img, theme, rx, ry, rw, rh, im)) err = true;
+        im.ez = EIr(d, F_RENDER_Z, env, i);
         return;
     }
     theme = mask_theme<G>(s, theme, img);
@@ -843,7 +888,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         int img = image_for_type<G>(s, t, player_img);
         if (img >= 0) {
             if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
-                off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: not in this build
+                off = (img == SPACE) ? -1 : -3; // draw_grid_obj fills: generic tile pass
             } else {
                 int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
                 int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
@@ -1043,6 +1088,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 }
                 fast = ballot(other) == 0;
             }
+        } else if (s.opt_use_monochrome_assets) {
+            fast = false; // every drawable tile is a draw_grid_obj fill: generic tile pass
         }
     }
     auto lookup_grid = [&](int x, int y) -> int {
@@ -1204,8 +1251,10 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                         if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
                             double rx, ry, rw, rh;
                             screen_rect(v, (float)x, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
-                            if (img != SPACE && (s.opt_use_monochrome_assets || !grid_obj_fill<G>(img, rx, ry, rw, rh, im)))
-                                err = true; // other draw_grid_obj fills: not in this build
+                            if (img != SPACE && !(s.opt_use_monochrome_assets
+                                                      ? mono_fill<G>(s, img, grid_theme<G>(s, type), rx, ry, rw, rh, im)
+                                                      : grid_obj_fill<G>(img, rx, ry, rw, rh, im)))
+                                err = true; // color_for_type fasserts (:464-490)
                         } else {
                             int theme = mask_theme<G>(s, grid_theme<G>(s, type), img);
                             int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
@@ -1236,6 +1285,16 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     PG_DRAW_ENTITIES(1)
 #undef PG_DRAW_ENTITIES
     wave_sync();
+    if (s.has_useful_vel_info && s.opt_paint_vel_info) { // paint_vel_info (basic-abstract-game.cpp:969-977)
+        const float vx = s.agent_erased ? s.ghost_vx : EFr(d, F_VX, env, 0);
+        const float vy = s.agent_erased ? s.ghost_vy : EFr(d, F_VY, env, 0);
+        const float infodim = (float)(PG_RES * .2);
+        const uint32_t s1 = (uint32_t)to_shade((float)(.5 * (double)vx / (double)s.maxspeed + .5));
+        const uint32_t s2 = (uint32_t)to_shade((float)(.5 * (double)vy / (double)s.max_jump + .5));
+        fb_fill_rectf(fb, 0, 0, infodim, infodim, 0xff000000u | (s1 * 0x010101u));
+        fb_fill_rectf(fb, infodim, 0, infodim, infodim, 0xff000000u | (s2 * 0x010101u));
+        wave_sync();
+    }
     game_overlay<G>(fb, s, v, d, env, err);
     wave_sync();
 

@@ -27,7 +27,8 @@ def oracle_kw(gpu_kw):
     kw = dict(gpu_kw)
     dm = kw.pop("distribution_mode", "hard")
     kw["distribution_mode"] = {"easy": 0, "hard": 1, "extreme": 2, "memory": 10}[dm]
-    for k in ("center_agent", "use_backgrounds", "restrict_themes", "use_sequential_levels"):
+    for k in ("center_agent", "use_backgrounds", "restrict_themes", "use_sequential_levels", "use_monochrome_assets",
+              "paint_vel_info"):
         if k in kw:
             kw[k] = int(kw[k])
     return kw
@@ -91,6 +92,21 @@ def test_miner_long_run_deaths():
     later, miner.cpp:326-330, 256-259), diamonds, exits -- 32 envs x 600 steps."""
     episodes, rewards = run_pair("miner", 32, 600, seed=8, num_levels=0, rand_seed=4, latent=True)
     assert episodes > 0
+
+
+@pytest.mark.parametrize("game", GAMES + ["coinrun"])
+def test_parity_monochrome_assets(game):
+    """use_monochrome_assets: every sprite becomes fillRect(color_for_type) (basic-abstract-game.cpp:
+    464-490, 886-928); with and without restrict_themes (mask_theme_if_necessary, :458-462)."""
+    run_pair(game, 8, 120, seed=11, num_levels=0, rand_seed=2, use_monochrome_assets=True, latent=game in LATENT)
+    run_pair(game, 4, 60, seed=12, num_levels=0, rand_seed=6, use_monochrome_assets=True, restrict_themes=True)
+
+
+@pytest.mark.parametrize("game", GAMES + ["coinrun"])
+def test_parity_paint_vel_info(game):
+    """paint_vel_info: two grey velocity squares in the top-left corner (basic-abstract-game.cpp:
+    969-977); games with has_useful_vel_info = false draw nothing extra."""
+    run_pair(game, 8, 150, seed=13, num_levels=0, rand_seed=7, paint_vel_info=True)
 
 
 @pytest.mark.parametrize("game", GAMES)
