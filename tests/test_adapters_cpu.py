@@ -1,0 +1,85 @@
+"""Host logic of the baselines-VecEnv / gym adapters (procgen/env.py:276-290,
+procgen/gym_registration.py:6-34) over a scripted gym3-style env -- CPU only."""
+import numpy as np
+import pytest
+
+from procgen_amd.adapters import ENV_IDS, ToBaselinesVecEnv, ToGymEnv, register_environments
+from procgen_amd.env import ENV_NAMES, Discrete, TensorType
+
+
+class ScriptedEnv:
+    """gym3-style env whose observation encodes (step, env) and whose env 1 ends every 3 steps."""
+
+    def __init__(self, num):
+        self.num = num
+        self.t = 0
+        self.acts = []
+        self.closed = False
+        self.ob_space = {"rgb": TensorType((64, 64, 3), Discrete(256))}
+        self.ac_space = TensorType((), Discrete(15))
+
+    def act(self, ac):
+        self.acts.append(np.asarray(ac).copy())
+        self.t += 1
+
+    def observe(self):
+        rgb = np.zeros((self.num, 64, 64, 3), np.uint8)
+        rgb[:, 0, 0, 0] = self.t
+        rgb[:, 0, 0, 1] = np.arange(self.num)
+        first = np.zeros(self.num, bool)
+        first[:] = self.t == 0
+        if self.num > 1 and self.t and self.t % 3 == 0:
+            first[1] = True
+        rew = np.arange(self.num, dtype=np.float32) + self.t
+        return rew, {"rgb": rgb}, first
+
+    def get_info(self):
+        return [{"level_seed": np.int32(100 + i + self.t)} for i in range(self.num)]
+
+    def close(self):
+        self.closed = True
+
+
+def test_vecenv_reset_step_semantics():
+    env = ScriptedEnv(4)
+    ve = ToBaselinesVecEnv(env)
+    assert ve.num_envs == 4 and ve.action_space.eltype.n == 15
+    ob = ve.reset()
+    assert ob["rgb"].shape == (4, 64, 64, 3) and (ob["rgb"][:, 0, 0, 0] == 0).all()
+    for t in range(1, 7):
+        ob, rew, done, infos = ve.step(np.full(4, t % 15))
+        assert (ob["rgb"][:, 0, 0, 0] == t).all()
+        np.testing.assert_array_equal(rew, np.arange(4) + t)
+        assert done.tolist() == [False, t % 3 == 0, False, False]  # done = first of the new frame
+        assert len(infos) == 4 and int(infos[2]["level_seed"]) == 102 + t
+    assert len(env.acts) == 6
+    assert (ve.render("rgb_array") == ob["rgb"][0]).all()
+    ve.close()
+    assert env.closed
+
+
+def test_vecenv_reset_mid_episode_warns(capsys):
+    env = ScriptedEnv(2)
+    ve = ToBaselinesVecEnv(env)
+    ve.step(np.zeros(2))
+    ve.reset()
+    assert "will not reset the env" in capsys.readouterr().out
+
+
+def test_gym_env_single():
+    env = ScriptedEnv(1)
+    ge = ToGymEnv(env)
+    assert ge.observation_space.shape == (64, 64, 3)
+    ob = ge.reset()
+    assert ob.shape == (64, 64, 3)
+    ob, rew, done, info = ge.step(3)
+    assert int(ob[0, 0, 0]) == 1 and rew == 1.0 and done is False and int(info["level_seed"]) == 101
+    assert env.acts[-1].dtype == np.int32 and env.acts[-1].tolist() == [3]
+    with pytest.raises(ValueError):
+        ToGymEnv(ScriptedEnv(2))
+
+
+def test_env_ids():
+    ids = register_environments()
+    assert ids == ENV_IDS and len(ids) == 16
+    assert sorted(ids.values()) == sorted(ENV_NAMES) and ids["procgen-coinrun-v0"] == "coinrun"
