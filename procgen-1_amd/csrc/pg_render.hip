@@ -712,30 +712,21 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
     int theme = EIr(d, F_IMAGE_THEME, env, i);
     int img = image_for_type<G>(s, itype, player_img);
     if (img < 0 || !should_draw<G>(s, etype, theme)) return;
-    if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+    // draw_grid_obj (monochrome / >= USE_ASSET_THRESHOLD) fills the unadjusted object rect;
+    // rotation, reflection and alpha are unused there
+    const bool grid_obj = s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD;
+    if (grid_obj) {
         if (img == SPACE) return;
         if (!s.opt_use_monochrome_assets) { // color_for_type fasserts without monochrome (:467-487)
             err = true;
             return;
         }
-        // draw_grid_obj over the unadjusted object rect; rotation, reflection and alpha unused
-        double rx, ry, rw, rh;
-        if (flags & EF_ABS_COORDS) {
-            float vd = v.view_dim;
-            float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
-            rx = (double)(ax * v.unit); ry = (double)(ay * v.unit);
-            rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
-        } else {
-            screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+    } else {
+        theme = mask_theme<G>(s, theme, img);
+        if (theme < 0 || theme >= 10) {
+            err = true;
+            return;
         }
-        if (!mono_fill<G>(s, img, theme, rx, ry, rw, rh, im)) err = true;
-        im.ez = EIr(d, F_RENDER_Z, env, i);
-        return;
-    }
-    theme = mask_theme<G>(s, theme, img);
-    if (theme < 0 || theme >= 10) {
-        err = true;
-        return;
     }
     double rx, ry, rw, rh;
     if (flags & EF_ABS_COORDS) { // get_abs_rect (:812-814) via get_object_rect (:820-826)
@@ -745,6 +736,10 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
     } else {
         screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+    }
+    if (grid_obj) {
+        if (!mono_fill<G>(s, img, theme, rx, ry, rw, rh, im)) err = true;
+        return;
     }
     if constexpr (G == PG_GAME_COINRUN) {
         if (is_player_image(img)) { // coinrun get_adjusted_image_rect (coinrun.cpp:64-70)
@@ -1285,7 +1280,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     PG_DRAW_ENTITIES(1)
 #undef PG_DRAW_ENTITIES
     wave_sync();
-    if (s.has_useful_vel_info && s.opt_paint_vel_info) { // paint_vel_info (basic-abstract-game.cpp:969-977)
+    if (__builtin_expect(s.has_useful_vel_info && s.opt_paint_vel_info, 0)) { // paint_vel_info (basic-abstract-game.cpp:969-977)
         const float vx = s.agent_erased ? s.ghost_vx : EFr(d, F_VX, env, 0);
         const float vy = s.agent_erased ? s.ghost_vy : EFr(d, F_VY, env, 0);
         const float infodim = (float)(PG_RES * .2);
