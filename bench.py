@@ -63,17 +63,45 @@ def cpu_baseline(game, num_levels, max_workers=16, steps=12000):
                       "(%.1f s wall, slowest worker %.1f s)" % (game, envs, steps, cores, wall, max(times))}
 
 
-def pmc_traffic():
-    """HBM bytes per render launch from the committed rocprofv3 PMC summary (profiles/), or None."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            d = json.load(f)
-        return d.get("render_hbm_bytes_per_launch")
-    except Exception:
-        return None
+def pmc_traffic(game):
+    """HBM bytes per render launch of `game` from the newest committed rocprofv3 PMC summary
+    (profiles/*pmc*.json, written by scripts/gpu_profile.sh from separate FETCH_SIZE / WRITE_SIZE
+    passes over this same bench command), or (None, None)."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("game", "coinrun") == game and d.get("render_hbm_bytes_per_launch"):
+            return d["render_hbm_bytes_per_launch"], os.path.basename(path)
+    return None, None
+
+
+def host_path_rate(game, num_levels, E, steps):
+    """The reference's own contract: host buffers (libenv_act reads numpy actions, libenv_observe
+    fills numpy obs / rew / first / info after a device->host copy), PCIe included.  Reported
+    beside `value` (device-resident obs), never as it."""
+    import numpy as np
+    from procgen_amd import ProcgenGym3Env
+    env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
+                         distribution_mode="hard")
+    rng = np.random.RandomState(0)
+    acts = rng.randint(0, 15, size=(steps + 2, E)).astype(np.int32)
+    for k in range(2):
+        env.act(acts[k])
+        env.observe()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.act(acts[2 + k])
+        rew, ob, first = env.observe()
+        info = env.get_info_arrays()
+    dt = time.perf_counter() - t0
+    env.close()
+    return {"value": round(E * steps / dt, 1), "unit": "env-steps/s", "steps": steps, "num_envs": E,
+            "what": "ProcgenGym3Env host mode: act(numpy) + observe() -> numpy rgb/rew/first + info arrays "
+                    "(libenv_observe device->host copy included)"}
 
 
 def main():
@@ -87,6 +115,11 @@ def main():
     ap.add_argument("--num-levels", type=int, default=None,
                     help="default: 200 for coinrun (configs[1]), 0 = unbounded otherwise (SURVEY 8d)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle", type=int, default=300,
+                    help="untimed steps after the warmup so that episodes, resets and entity lists reach "
+                         "steady state before the timed window (reported as settle_steps)")
+    ap.add_argument("--host-steps", type=int, default=8,
+                    help="steps of the host-buffer (libenv observe -> numpy) path reported as host_path; 0 = skip")
     ap.add_argument("--gather", action="store_true",
                     help="after every step, RCCL all-gather of every rank's uint8[E,64,64,3] obs shard into a "
                          "[N*E,64,64,3] tensor on each rank (north star's obs concatenation; SURVEY 8(e))")
@@ -139,7 +172,7 @@ def main():
             gather()
 
     t = 0
-    for _ in range(args.warmup):
+    for _ in range(args.warmup + args.settle):
         t += 1
         step(t)
     env.wait()
@@ -159,7 +192,7 @@ def main():
     env.wait()
     barrier()
     elapsed = time.perf_counter() - t0
-    n_timed, kt = env.kernel_times()  # ms: step, reset, render, total per step
+    n_timed, kt, kt_games = env.kernel_times()  # ms: step, reset, render (sums over games), wall span
     env.set_timing(False)
 
     if dist is not None:
@@ -173,16 +206,40 @@ def main():
 
     if rank == 0:
         names = ["pg_step_kernel", "pg_reset_kernel", "pg_render_kernel"]
-        dom = max(range(3), key=lambda i: kt[i])
-        render_ms = kt[2]
-        algo_bytes = E * OBS_BYTES  # per render launch: every env's 64x64x3 obs write
-        achieved = algo_bytes / (render_ms * 1e-3) if render_ms > 0 else 0.0
-        traffic = pmc_traffic()
-        roof = {"bound": "hbm", "kernel": names[2], "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5), "traffic": traffic,
-                "algorithmic_bytes_per_launch": algo_bytes,
-                "kernel_ms": {"step": round(kt[0], 4), "reset": round(kt[1], 4), "render": round(kt[2], 4)},
-                "dominant_kernel": names[dom], "timed_launches": n_timed}
+        mixed = len(game.split(",")) > 1
+        algo_bytes = E * OBS_BYTES  # every env's 64x64x3 obs write per step
+        if not mixed:
+            dom = max(range(3), key=lambda i: kt[i])
+            render_ms = kt[2]
+            achieved = algo_bytes / (render_ms * 1e-3) if render_ms > 0 else 0.0
+            traffic, traffic_src = pmc_traffic(game)
+            roof = {"bound": "hbm", "kernel": names[2], "achieved": round(achieved / 1e9, 2),
+                    "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
+                    "traffic": traffic, "traffic_source": traffic_src,
+                    "algorithmic_bytes_per_launch": algo_bytes,
+                    "kernel_ms": {"step": round(kt[0], 4), "reset": round(kt[1], 4), "render": round(kt[2], 4),
+                                  "step_wall": round(kt[3], 4)},
+                    "dominant_kernel": names[dom], "timed_launches": n_timed}
+        else:
+            # a mixed batch runs every game's step -> reset -> render chain concurrently on its own
+            # stream: no single kernel's duration is attributable, so the roofline is taken over
+            # the step's wall span (fork -> join on the env's stream), i.e. all 16 chains together
+            achieved = algo_bytes / (kt[3] * 1e-3) if kt[3] > 0 else 0.0
+            roof = {"bound": "hbm", "kernel": "all games' step+reset+render chains (concurrent streams)",
+                    "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK, 5), "traffic": None,
+                    "algorithmic_bytes_per_launch": algo_bytes,
+                    "kernel_ms": {"step_wall": round(kt[3], 4),
+                                  "sum_over_games": {"step": round(kt[0], 4), "reset": round(kt[1], 4),
+                                                     "render": round(kt[2], 4)},
+                                  "per_game": {g: [round(x, 4) for x in v] for g, v in kt_games.items()}},
+                    "timed_launches": n_timed}
+        host = None
+        if args.host_steps > 0 and world == 1:
+            try:
+                host = host_path_rate(game, num_levels, E, args.host_steps)
+            except Exception as e:
+                host = {"error": repr(e)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -192,7 +249,8 @@ def main():
         line = {
             "metric": "env-steps/sec at num_envs=65536 (1/2/4/8 GPU) + obs/reward parity vs CPU ref",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "settle_steps": args.settle, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
             "config": {"workload": "%s num_envs=%d per GPU, start_level=0 num_levels=%d, hard, "
                                    "center_agent, backgrounds, random actions (device counter hash)"
@@ -202,6 +260,7 @@ def main():
                        "gather": ("rccl all_gather_into_tensor of obs, %d B per rank per step" % (E * OBS_BYTES))
                        if args.gather else None},
             "roofline": roof,
+            "host_path": host,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

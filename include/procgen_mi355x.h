@@ -1,16 +1,17 @@
 /*
  * procgen_mi355x.h -- extensions of libprocgen_mi355x.so beyond the libenv ABI.
  *
- * The reference loads its sprite atlas from PNG files inside libenv_make
- * (vecgame.cpp:144-153 global_init -> images_load, resources.cpp:20-30); this
- * build receives the decoded atlas from the host instead (procgen_upload_atlas),
- * keeps every env's state resident in HBM, and can hand out device pointers so a
- * consumer on the same GPU never copies observations to the host.
+ * Like the reference (vecgame.cpp:144-153 global_init -> images_load, resources.cpp:20-30),
+ * libenv_make loads the sprite atlas itself: from the `resource_root` option when given, else
+ * from the package's assets directory (Qt-decoded .npz packs + manifest.txt, see
+ * csrc/pg_assets.cpp).  The library keeps every env's state resident in HBM and can hand out
+ * device pointers so a consumer on the same GPU never copies observations to the host.
  *
- * Call order for a libenv host:  libenv_make -> procgen_upload_atlas ->
- *   libenv_get_tensortypes -> libenv_set_buffers -> (libenv_act, libenv_observe)* -> libenv_close.
- * Device-resident order:          libenv_make -> procgen_upload_atlas ->
- *   procgen_start -> (procgen_act_device | procgen_act_hashed, procgen_wait)* -> libenv_close.
+ * Call order for a libenv host (gym3 CEnv, unchanged):  libenv_make ->
+ *   libenv_get_tensortypes x3 -> libenv_set_buffers -> (libenv_act, libenv_observe)* -> libenv_close.
+ * Device-resident order:  libenv_make -> procgen_start ->
+ *   (procgen_act_device | procgen_act_hashed, procgen_wait)* -> libenv_close.
+ * procgen_upload_atlas optionally replaces the loaded atlas before the first reset.
  */
 #pragma once
 #include <stdint.h>
@@ -43,7 +44,7 @@ struct pg_device_buffers {
 #define PG_NUM_SLOTS 1000 /* image slot = type + 100 * theme (basic-abstract-game.cpp:896) */
 #define PG_MAX_BG 64
 
-/* Upload the decoded sprite atlas (reference: images_load + each game's asset_for_type and
+/* Replace the decoded sprite atlas (reference: images_load + each game's asset_for_type and
  * background group, resources.cpp:20-30, 837-979).  One pixel array for all games; per-game
  * tables indexed by game id: sprites [PG_NUM_GAMES][PG_NUM_SLOTS], backgrounds
  * [PG_NUM_GAMES][PG_MAX_BG], num_backgrounds [PG_NUM_GAMES], num_themes [PG_NUM_GAMES][100].
@@ -60,6 +61,19 @@ LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t);
 /* Block until every enqueued step finished (the device half of libenv_observe). */
 LIBENV_API int procgen_wait(libenv_env *env);
 LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers *out);
+/* Copy the outputs of `count` envs (ids env_ids[k]) to host arrays of `count` rows after the
+ * enqueued steps finish; any pointer may be NULL.  For consumers (and tests) that sample a few
+ * envs of a device-resident batch without copying the whole observation tensor. */
+LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int count, uint8_t *rgb, float *rew,
+                                 uint8_t *first, int32_t *prev_level_seed, uint8_t *prev_level_complete,
+                                 int32_t *level_seed);
+/* Build the atlas libenv_make would load for `env_name` (comma list) from `resource_root` (NULL or
+ * "" = the package's assets directory) on the host only: returns the pixel count (copied into
+ * `pixels` when capacity allows) and fills the tables (layouts as procgen_upload_atlas); < 0 on
+ * error (message via procgen_error_string(NULL)).  Lets a CPU test check the loader. */
+LIBENV_API int64_t procgen_atlas_host(const char *env_name, const char *resource_root, uint32_t *pixels,
+                                      int64_t capacity, struct pg_image *sprites, struct pg_image *backgrounds,
+                                      int32_t *num_backgrounds, int32_t *num_themes);
 /* Sticky error: 0 ok; otherwise a code (see PG_ERR_*), message via procgen_error_string. */
 LIBENV_API int procgen_last_error(libenv_env *env);
 LIBENV_API const char *procgen_error_string(libenv_env *env);

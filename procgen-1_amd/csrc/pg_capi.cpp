@@ -18,6 +18,7 @@
 
 #include "../../include/libenv.h"
 #include "../../include/procgen_mi355x.h"
+#include "pg_assets.h"
 #include "pg_engine.h"
 
 extern "C" {
@@ -310,12 +311,15 @@ struct VecEnv {
     uint32_t *d_pixels = nullptr;
     int32_t *d_sprites = nullptr, *d_bgs = nullptr, *d_themes = nullptr;
     int32_t *h_actions = nullptr; // page-locked staging of libenv_act's actions
+    hipEvent_t act_copied = nullptr; // the last action upload has read h_actions
+    bool act_pending = false;
     std::vector<uint8_t> h_staging;
     uint8_t *pinned = nullptr;  // page-locked landing zone of copy_out (all output planes)
     size_t pinned_bytes = 0;
     // timing
     bool timing = false;
-    std::vector<hipEvent_t> ev; // 4 per timed step: before step, after step, after reset, after render
+    std::vector<hipEvent_t> ev; // per timed step: 4 per game (before step, after step, after reset,
+                                // after render) + 2 on the main stream (before the fork, after the join)
     int t_used = 0;             // timed steps recorded since procgen_set_timing
     int device = 0;
     int error = 0;
@@ -329,6 +333,9 @@ struct VecEnv {
     std::vector<hipEvent_t> gdone;
     hipEvent_t fork = nullptr;
     bool has_latent = false;               // maze fills the fork's latent-state info
+    // game of env e: the global index decides (vecgame.cpp:357-358), so a shard at env_offset
+    // plays exactly the games of the same envs of one unsharded vec env
+    int game_of(int e) const { return games[(size_t)(env_offset + e) % games.size()]; }
     const int32_t *list_of(size_t k) const {
         return games.size() > 1 ? d_lists + k * (size_t)(num_envs / games.size()) : nullptr;
     }
@@ -352,6 +359,9 @@ static hipError_t copy_sync(VecEnv *v, void *dst, const void *src, size_t bytes,
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(v->stream);
 }
+
+int upload_atlas(VecEnv *v, const uint32_t *pixels, int64_t num_pixels, const pg_image *sprites,
+                 const pg_image *backgrounds, const int32_t *num_backgrounds, const int32_t *num_themes);
 
 int fail(VecEnv *v, int code, const char *msg) {
     if (v && !v->error) {
@@ -393,17 +403,19 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
     const size_t G = v->games.size();
-    hipEvent_t *e = nullptr; // 4 per game: before step, after step, after reset, after render
+    hipEvent_t *e = nullptr; // 4 per game: before step, after step, after reset, after render; then 2 wall
+    const size_t per = 4 * G + 2;
     if (v->timing) {
-        size_t need = (size_t)(v->t_used + 1) * 4 * G;
+        size_t need = (size_t)(v->t_used + 1) * per;
         while (v->ev.size() < need) {
             hipEvent_t x;
             HIPCHECK(hipEventCreate(&x));
             v->ev.push_back(x);
         }
-        e = &v->ev[(size_t)v->t_used * 4 * G];
+        e = &v->ev[(size_t)v->t_used * per];
         v->t_used++;
     }
+    if (e) HIPCHECK(hipEventRecord(e[4 * G], v->stream));
     HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t) * PG_NUM_GAMES, v->stream));
     if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     for (size_t k = 0; k < G; k++) {
@@ -424,6 +436,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
         }
     }
+    if (e) HIPCHECK(hipEventRecord(e[4 * G + 1], v->stream));
     HIPCHECK(hipGetLastError());
     return 0;
 }
@@ -578,6 +591,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         gids.push_back(gid);
     }
     if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
+    if (env_offset < 0) return bad("env_offset must be >= 0");
     if (use_generated_assets) return bad("use_generated_assets is not in this build yet");
     if (render_human) return bad("render_mode=rgb_array (render_human) is not in this build yet");
 
@@ -675,7 +689,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     for (int k = 0; k < env_offset; k++) (void)seed_gen.next();
     for (size_t e = 0; e < n; e++) {
         PGEnv &s = h[e];
-        construct_env(s, gids[e % gids.size()]);
+        construct_env(s, v->game_of((int)e));
         s.level_seed_low = level_seed_low;
         s.level_seed_high = level_seed_high;
         s.game_n = env_offset + (int)e;
@@ -693,13 +707,16 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         memcpy(&hmt[(e * 2 + 1) * PG_MT_WORDS], lsg.mt, sizeof(lsg.mt));
         s.lsg_mti = lsg.mti;
     }
-    // env lists of a mixed batch: game k owns envs k, k + G, k + 2G, ...
+    // env lists of a mixed batch: game k owns the envs whose global index is k mod G, i.e.
+    // local envs r, r + G, r + 2G, ... with r = (k - env_offset) mod G
     std::vector<int32_t> lists;
     const size_t ng = gids.size();
     if (ng > 1) {
         lists.resize(n);
-        for (size_t k = 0; k < ng; k++)
-            for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + k);
+        for (size_t k = 0; k < ng; k++) {
+            size_t r = (size_t)((((int64_t)k - env_offset) % (int64_t)ng + (int64_t)ng) % (int64_t)ng);
+            for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + r);
+        }
     }
     float rot_angles[PG_ROT_N];
     double rot_table[PG_ROT_N * 4];
@@ -713,10 +730,27 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         libenv_close(v);
         return bad("device upload failed");
     }
-    if (hipHostMalloc((void **)&v->h_actions, (size_t)n * 4 + 4, hipHostMallocDefault) != hipSuccess) {
-        v->h_actions = nullptr;
+    if (hipHostMalloc((void **)&v->h_actions, (size_t)n * 4 + 4, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&v->act_copied, hipEventDisableTiming) != hipSuccess) {
+        if (!v->h_actions) v->h_actions = nullptr;
         libenv_close(v);
         return bad("pinned host allocation failed");
+    }
+    // images: global_init -> images_load from resource_root (vecgame.cpp:144-153, 189-193), here
+    // the committed Qt-decoded packs (pg_assets.cpp); procgen_upload_atlas may replace them later
+    {
+        PGAtlasHost at;
+        std::string err, root = resource_root.empty() ? pg_default_asset_root() : resource_root;
+        if (!pg_atlas_load(root, gids, &at, &err)) {
+            libenv_close(v);
+            return bad("asset load failed: " + err);
+        }
+        if (upload_atlas(v, at.pixels.data(), (int64_t)at.pixels.size(), (const pg_image *)at.sprites.data(),
+                         (const pg_image *)at.backgrounds.data(), at.num_backgrounds.data(), at.num_themes.data()) != 0) {
+            std::string m = "atlas upload failed: " + v->error_msg;
+            libenv_close(v);
+            return bad(m);
+        }
     }
     return (libenv_env *)v;
 }
@@ -736,10 +770,55 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
                                     const struct pg_image *sprites, const struct pg_image *backgrounds,
                                     const int32_t *num_backgrounds, const int32_t *num_themes) {
     VecEnv *v = (VecEnv *)env;
+    if (v->started) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas after the first reset");
+    return upload_atlas(v, pixels, num_pixels, sprites, backgrounds, num_backgrounds, num_themes);
+}
+
+LIBENV_API int64_t procgen_atlas_host(const char *env_name, const char *resource_root, uint32_t *pixels,
+                                      int64_t capacity, struct pg_image *sprites, struct pg_image *backgrounds,
+                                      int32_t *num_backgrounds, int32_t *num_themes) {
+    std::vector<int> gids;
+    for (const std::string &nm : split_names(env_name ? env_name : "")) {
+        int g = game_id(nm);
+        if (g < 0) return -PG_ERR_BAD_OPTION;
+        gids.push_back(g);
+    }
+    PGAtlasHost at;
+    std::string err, root = resource_root && resource_root[0] ? resource_root : pg_default_asset_root();
+    if (!pg_atlas_load(root, gids, &at, &err)) {
+        g_last_make_error = err;
+        return -PG_ERR_NO_ATLAS;
+    }
+    if (pixels && capacity >= (int64_t)at.pixels.size()) memcpy(pixels, at.pixels.data(), at.pixels.size() * 4);
+    if (sprites) memcpy(sprites, at.sprites.data(), at.sprites.size() * 4);
+    if (backgrounds) memcpy(backgrounds, at.backgrounds.data(), at.backgrounds.size() * 4);
+    if (num_backgrounds) memcpy(num_backgrounds, at.num_backgrounds.data(), at.num_backgrounds.size() * 4);
+    if (num_themes) memcpy(num_themes, at.num_themes.data(), at.num_themes.size() * 4);
+    return (int64_t)at.pixels.size();
+}
+
+}  // extern "C"
+
+namespace {
+int upload_atlas(VecEnv *v, const uint32_t *pixels, int64_t num_pixels, const pg_image *sprites,
+                 const pg_image *backgrounds, const int32_t *num_backgrounds, const int32_t *num_themes) {
     for (int g : v->games)
         if (num_backgrounds[g] <= 0 || num_backgrounds[g] > PG_MAX_BG)
             return fail(v, PG_ERR_NO_ATLAS, "bad background count for a game of the batch");
+    if (num_pixels <= 0 || num_pixels >= 0xffffffffLL) return fail(v, PG_ERR_NO_ATLAS, "bad atlas pixel count");
     const size_t slots = (size_t)PG_NUM_GAMES * PG_NUM_SLOTS, bgs = (size_t)PG_NUM_GAMES * PG_MAX_BG;
+    for (void *old : {(void *)v->d_pixels, (void *)v->d_sprites, (void *)v->d_bgs, (void *)v->d_themes}) {
+        if (!old) continue;
+        for (size_t i = 0; i < v->allocs.size(); i++)
+            if (v->allocs[i] == old) {
+                (void)hipFree(old);
+                v->allocs.erase(v->allocs.begin() + i);
+                break;
+            }
+    }
+    v->d_pixels = nullptr;
+    v->d_sprites = v->d_bgs = v->d_themes = nullptr;
+    v->atlas = false;
     if (dalloc(v, &v->d_pixels, (size_t)num_pixels) || dalloc(v, &v->d_sprites, slots * 4) ||
         dalloc(v, &v->d_bgs, bgs * 4) || dalloc(v, &v->d_themes, (size_t)PG_NUM_GAMES * 100))
         return -PG_ERR_HIP;
@@ -748,7 +827,7 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
     HIPCHECK(copy_sync(v, v->d_bgs, backgrounds, bgs * sizeof(pg_image), hipMemcpyHostToDevice));
     HIPCHECK(copy_sync(v, v->d_themes, num_themes, (size_t)PG_NUM_GAMES * 100 * 4, hipMemcpyHostToDevice));
     v->dev.pixels = v->d_pixels;
-    v->dev.num_pixels = num_pixels < 0xffffffffLL ? (uint32_t)num_pixels : 0xffffffffu;
+    v->dev.num_pixels = (uint32_t)num_pixels;
     v->dev.sprites = v->d_sprites;
     v->dev.backgrounds = v->d_bgs;
     v->dev.num_themes = v->d_themes;
@@ -756,6 +835,9 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
     v->atlas = true;
     return 0;
 }
+} // namespace
+
+extern "C" {
 
 LIBENV_API int procgen_start(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
@@ -797,11 +879,19 @@ LIBENV_API void libenv_set_buffers(libenv_env *env, struct libenv_buffers *bufs)
 LIBENV_API void libenv_act(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     size_t n = (size_t)v->num_envs;
+    // each act keeps its own actions (the reference waits for the stepping threads before
+    // reading them, vecgame.cpp:426-444): the previous upload must have read the staging buffer
+    if (v->act_pending && hipEventSynchronize(v->act_copied) != hipSuccess) {
+        fail(v, PG_ERR_HIP, "action upload wait failed");
+        return;
+    }
     for (size_t e = 0; e < n; e++) v->h_actions[e] = *(const int32_t *)v->ac_ptrs[e];
-    if (hipMemcpyAsync(v->dev.actions, v->h_actions, n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess) {
+    if (hipMemcpyAsync(v->dev.actions, v->h_actions, n * 4, hipMemcpyHostToDevice, v->stream) != hipSuccess ||
+        hipEventRecord(v->act_copied, v->stream) != hipSuccess) {
         fail(v, PG_ERR_HIP, "action upload failed");
         return;
     }
+    v->act_pending = true;
     launch_step(v, 0, 0, 0);
 }
 
@@ -820,6 +910,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     for (void *p : v->allocs) hipFree(p);
     if (v->pinned) (void)hipHostFree(v->pinned);
     if (v->h_actions) (void)hipHostFree(v->h_actions);
+    if (v->act_copied) hipEventDestroy(v->act_copied);
     for (auto &e : v->ev)
         if (e) hipEventDestroy(e);
     for (auto &e : v->gdone)
@@ -863,6 +954,29 @@ LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers 
     return 0;
 }
 
+LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int count, uint8_t *rgb, float *rew,
+                                 uint8_t *first, int32_t *prev_level_seed, uint8_t *prev_level_complete,
+                                 int32_t *level_seed) {
+    VecEnv *v = (VecEnv *)env;
+    HIPCHECK(hipSetDevice(v->device));
+    for (int k = 0; k < count; k++) {
+        size_t e = (size_t)env_ids[k];
+        if (env_ids[k] < 0 || e >= (size_t)v->num_envs) return fail(v, PG_ERR_BAD_OPTION, "procgen_read_envs: bad env id");
+        if (rgb) HIPCHECK(hipMemcpyAsync(rgb + (size_t)k * PG_OBS_BYTES, v->dev.rgb + e * PG_OBS_BYTES, PG_OBS_BYTES,
+                                         hipMemcpyDeviceToHost, v->stream));
+        if (rew) HIPCHECK(hipMemcpyAsync(rew + k, v->dev.rew + e, 4, hipMemcpyDeviceToHost, v->stream));
+        if (first) HIPCHECK(hipMemcpyAsync(first + k, v->dev.first + e, 1, hipMemcpyDeviceToHost, v->stream));
+        if (prev_level_seed)
+            HIPCHECK(hipMemcpyAsync(prev_level_seed + k, v->dev.prev_level_seed + e, 4, hipMemcpyDeviceToHost, v->stream));
+        if (prev_level_complete)
+            HIPCHECK(hipMemcpyAsync(prev_level_complete + k, v->dev.prev_level_complete + e, 1, hipMemcpyDeviceToHost,
+                                    v->stream));
+        if (level_seed) HIPCHECK(hipMemcpyAsync(level_seed + k, v->dev.level_seed + e, 4, hipMemcpyDeviceToHost, v->stream));
+    }
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    return 0;
+}
+
 LIBENV_API int procgen_last_error(libenv_env *env) {
     if (!env) return g_last_make_error.empty() ? 0 : PG_ERR_BAD_OPTION;
     return ((VecEnv *)env)->error;
@@ -880,28 +994,35 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
     return 0;
 }
 
-// Averages over the steps timed since procgen_set_timing(env, 1): out[0] step kernel,
-// out[1] reset kernel, out[2] render kernel, out[3] whole step (ms).
+// Averages over the steps timed since procgen_set_timing(env, 1), ms:
+//   out[0] step kernel, out[1] reset kernel, out[2] render kernel -- each the SUM over the
+//          batch's games (a mixed batch runs the games' chains concurrently on their own streams,
+//          so these sums can exceed the step's wall time);
+//   out[3] wall span of the whole step on the env's stream (before the fork -> after the join);
+//   out[4 + 3g .. 6 + 3g] step / reset / render of game slot g (v->games order).
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
-    double sum[4] = {0, 0, 0, 0};
-    // per kernel: the sum over the batch's games of that kernel's duration (mixed batches run
-    // the games' chains concurrently, so the sum can exceed the wall time of a step)
-    const size_t G = v->games.size();
+    const size_t G = v->games.size(), per = 4 * G + 2;
+    std::vector<double> sum(4 + 3 * G, 0.0);
     if (v->t_used > 0) {
         HIPCHECK(hipStreamSynchronize(v->stream));
         for (int k = 0; k < v->t_used; k++) {
+            hipEvent_t *base = &v->ev[(size_t)k * per];
             for (size_t g = 0; g < G; g++) {
-                hipEvent_t *e = &v->ev[((size_t)k * G + g) * 4];
+                hipEvent_t *e = base + 4 * g;
                 float a = 0, b = 0, c = 0;
                 HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));
                 HIPCHECK(hipEventElapsedTime(&b, e[1], e[2]));
                 HIPCHECK(hipEventElapsedTime(&c, e[2], e[3]));
-                sum[0] += a; sum[1] += b; sum[2] += c; sum[3] += a + b + c;
+                sum[0] += a; sum[1] += b; sum[2] += c;
+                sum[4 + 3 * g] += a; sum[5 + 3 * g] += b; sum[6 + 3 * g] += c;
             }
+            float w = 0;
+            HIPCHECK(hipEventElapsedTime(&w, base[4 * G], base[4 * G + 1]));
+            sum[3] += w;
         }
     }
-    for (int i = 0; i < n && i < 4; i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;
+    for (int i = 0; i < n && i < (int)sum.size(); i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;
     return v->t_used;
 }
 
@@ -930,6 +1051,13 @@ LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int le
 // [u32 magic][u32 version][PGEnv][num_ents x PG_NF words][num_tail x PG_NF words (the reserved top
 // slots, starpilot's spawners)][grid cells int16][2 x 625 mt words][END]
 static const uint32_t STATE_MAGIC = 0x50474d33u; // "PGM3"
+// largest main_width x main_height of each game over its distribution modes (choose_world_dim of
+// bigfish.cpp:27, bossfight.cpp:65, caveflyer.cpp:128-142, chaser.cpp:135-152, climber.cpp:230-232,
+// coinrun.cpp:54, dodgeball.cpp:248-256, fruitbot.cpp:147-154, heist.cpp:98-112, jumper.cpp:204-218,
+// leaper.cpp:103-115, maze.cpp:44-56, miner.cpp:127-138, ninja.cpp:36, plunder.cpp:37, starpilot.cpp:52)
+static const int GAME_MAX_DIM[PG_NUM_GAMES][2] = {
+    {20, 20}, {20, 20}, {60, 60}, {19, 19}, {20, 64}, {64, 64}, {40, 40}, {20, 60},
+    {23, 23}, {45, 45}, {20, 20}, {31, 31}, {35, 35}, {64, 64}, {20, 20}, {16, 16}};
 static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
 
 LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
@@ -976,11 +1104,26 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     memcpy(&ver, p, 4); p += 4;
     PGEnv s;
     memcpy(&s, p, sizeof(s)); p += sizeof(s);
+    if (magic != STATE_MAGIC || ver != 2) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: not a state of this build");
+        return;
+    }
+    // the slot's game must match (the reference: fassert(game_name == b->read_string()),
+    // game.cpp:259), and every size must be one that game's kernels are built for
+    if (s.game_id != v->game_of(env_idx)) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: the state belongs to another game than this env slot");
+        return;
+    }
+    if (s.num_ents < 0 || s.num_tail < 0 || s.num_ents + s.num_tail > PG_CAP || s.main_width < 0 ||
+        s.main_height < 0 || s.main_width > GAME_MAX_DIM[s.game_id][0] || s.main_height > GAME_MAX_DIM[s.game_id][1]) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: entity count or world size out of range for the game");
+        return;
+    }
     size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail, cells = (size_t)s.main_width * s.main_height;
     size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
     int32_t end = 0;
-    if (magic != STATE_MAGIC || ver != 2 || (size_t)length < need || ents + tail > PG_CAP || cells > PG_GRID_MAX) {
-        fail(v, PG_ERR_BAD_OPTION, "set_state: not a state of this build");
+    if ((size_t)length < need || cells > PG_GRID_MAX) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: truncated state");
         return;
     }
     memcpy(&end, data + need - 4, 4);

@@ -15,7 +15,6 @@ import random
 import numpy as np
 
 from . import _lib
-from .assets import engine_atlas_for
 
 MAX_STATE_SIZE = 2 ** 20  # procgen/env.py:13
 
@@ -69,7 +68,7 @@ class BaseProcgenEnv:
 
     def __init__(self, num, env_name, options, debug=False, rand_seed=None, num_levels=0, start_level=0,
                  use_sequential_levels=False, debug_mode=0, resource_root=None, num_threads=4, render_mode=None,
-                 device_buffers=False, env_offset=0):
+                 device_buffers=False, env_offset=0, upload_atlas=False):
         lib = _lib.load()
         self._lib = lib
         if render_mode is None:
@@ -105,12 +104,16 @@ class BaseProcgenEnv:
         if not self._handle:
             msg = lib.procgen_error_string(None)
             raise ProcgenError("libenv_make failed: %s" % (msg.decode() if msg else "unknown"))
-        atlas = engine_atlas_for(tuple(env_name.split(",")))
-        self._atlas = atlas
-        rc = lib.procgen_upload_atlas(self._handle, atlas.pixels.ctypes.data, atlas.pixels.size,
-                                      atlas.sprites.ctypes.data, atlas.backgrounds.ctypes.data,
-                                      atlas.num_backgrounds.ctypes.data, atlas.num_themes.ctypes.data)
-        _check(lib, self._handle, rc)
+        # libenv_make loaded the images itself (the reference's images_load); a host-built atlas
+        # can still replace them before the first reset (procgen_upload_atlas, tests only)
+        if upload_atlas:
+            from .assets import engine_atlas_for
+            atlas = engine_atlas_for(tuple(env_name.split(",")))
+            self._atlas = atlas
+            rc = lib.procgen_upload_atlas(self._handle, atlas.pixels.ctypes.data, atlas.pixels.size,
+                                          atlas.sprites.ctypes.data, atlas.backgrounds.ctypes.data,
+                                          atlas.num_backgrounds.ctypes.data, atlas.num_themes.ctypes.data)
+            _check(lib, self._handle, rc)
 
         self.ob_types = self._types(_lib.SPACE_OBSERVATION)
         self.ac_types = self._types(_lib.SPACE_ACTION)
@@ -199,9 +202,17 @@ class BaseProcgenEnv:
         return self._rew.copy(), {k: v.copy() for k, v in self._ob.items()}, self._first.astype(bool)
 
     def get_info(self):
+        """gym3 contract: one dict per env (procgen/env.py via gym3 CEnv.get_info)."""
         if self.device_buffers:
             raise ProcgenError("device-buffer env: read device_ptrs() instead")
-        return [{k: v[i].copy() for k, v in self._info.items()} for i in range(self.num)]
+        items = list(self._info.items())
+        return [{k: (v[i] if v.ndim == 1 else v[i].copy()) for k, v in items} for i in range(self.num)]
+
+    def get_info_arrays(self):
+        """The info tensors of the last observe() as arrays [num, ...] (no per-env dicts)."""
+        if self.device_buffers:
+            raise ProcgenError("device-buffer env: read device_ptrs() instead")
+        return {k: v.copy() for k, v in self._info.items()}
 
     def callmethod(self, method, *args, **kwargs):
         return getattr(self, method)(*args, **kwargs)
@@ -237,6 +248,19 @@ class BaseProcgenEnv:
         rc = self._lib.procgen_wait(self._handle)
         _check(self._lib, self._handle, rc)
 
+    def read_envs(self, env_ids):
+        """Outputs of a few envs (after the enqueued steps finish) without copying the batch:
+        dict of rgb [k,64,64,3], rew, first, prev_level_seed, prev_level_complete, level_seed."""
+        ids = np.ascontiguousarray(env_ids, dtype=np.int32).reshape(-1)
+        k = ids.size
+        out = dict(rgb=np.zeros((k, 64, 64, 3), np.uint8), rew=np.zeros(k, np.float32), first=np.zeros(k, np.uint8),
+                   prev_level_seed=np.zeros(k, np.int32), prev_level_complete=np.zeros(k, np.uint8),
+                   level_seed=np.zeros(k, np.int32))
+        rc = self._lib.procgen_read_envs(self._handle, ids.ctypes.data, k, *[out[n].ctypes.data for n in (
+            "rgb", "rew", "first", "prev_level_seed", "prev_level_complete", "level_seed")])
+        _check(self._lib, self._handle, rc)
+        return out
+
     def device_ptrs(self):
         d = _lib.pg_device_buffers()
         self._lib.procgen_device_buffers(self._handle, ctypes.byref(d))
@@ -246,9 +270,15 @@ class BaseProcgenEnv:
         self._lib.procgen_set_timing(self._handle, int(on))
 
     def kernel_times(self):
-        out = (ctypes.c_float * 3)()
-        n = self._lib.procgen_kernel_times(self._handle, out, 3)
-        return n, list(out)
+        """(timed steps, [step, reset, render, wall] ms, {game: [step, reset, render] ms}): the first
+        three are sums over a mixed batch's games (concurrent streams), wall is the step's span."""
+        names = self.env_name.split(",")
+        k = 4 + 3 * len(names)
+        out = (ctypes.c_float * k)()
+        n = self._lib.procgen_kernel_times(self._handle, out, k)
+        vals = list(out)
+        per_game = {nm: vals[4 + 3 * g:7 + 3 * g] for g, nm in enumerate(names)}
+        return n, vals[:4], per_game
 
     def debug_env(self, i):
         buf = np.zeros(128, dtype=np.int32)

@@ -100,3 +100,31 @@ def test_mixed_batch_size_must_divide():
 def test_memory_mode_only_for_memory_games():
     h, msg = make(dict(BASE, env_name="bigfish", distribution_mode=10))  # game.cpp:83-84
     assert not h and "distribution_mode" in msg
+
+
+def test_gym3_sequence_uses_only_libenv_symbols():
+    """gym3's CEnv sequence (tests/gym3_cenv.py) needs no extension call: the driver resolves only
+    the libenv symbols, and libenv_make loads the atlas itself (no procgen_upload_atlas step).
+    Without a GPU the make stops at the first HIP call, never at a missing atlas."""
+    from procgen_amd import _lib
+    from gym3_cenv import LIBENV_SYMBOLS, CEnv, RecordingLib
+    from conftest import has_gpu
+    lib = RecordingLib(_lib.LIB_PATH)
+    opts = dict(BASE, num_levels=200, use_backgrounds=True, center_agent=True, distribution_mode=1)
+    if has_gpu():
+        env = CEnv(lib, 2, opts)
+        env.observe()
+        env.act([1, 2])
+        env.observe()
+        env.close()
+    else:
+        with pytest.raises(RuntimeError):
+            CEnv(lib, 2, opts)
+        msg = _lib.load().procgen_error_string(None).decode()
+        assert "asset" not in msg and "atlas" not in msg, msg
+    assert set(lib.looked_up) <= set(LIBENV_SYMBOLS), lib.looked_up
+
+
+def test_env_offset_must_be_nonnegative():
+    h, msg = make(dict(BASE, env_offset=-3))
+    assert not h and "env_offset" in msg
