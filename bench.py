@@ -82,26 +82,31 @@ def pmc_traffic(game):
 def host_path_rate(game, num_levels, E, steps):
     """The reference's own contract: host buffers (libenv_act reads numpy actions, libenv_observe
     fills numpy obs / rew / first / info after a device->host copy), PCIe included.  Reported
-    beside `value` (device-resident obs), never as it."""
+    beside `value` (device-resident obs), never as it.  `value`: gym3 CEnv default semantics
+    (observe() returns fresh copies); `reuse_arrays`: CEnv(reuse_arrays=True), the live buffers."""
     import numpy as np
     from procgen_amd import ProcgenGym3Env
-    env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
-                         distribution_mode="hard")
-    rng = np.random.RandomState(0)
-    acts = rng.randint(0, 15, size=(steps + 2, E)).astype(np.int32)
-    for k in range(2):
-        env.act(acts[k])
-        env.observe()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        env.act(acts[2 + k])
-        rew, ob, first = env.observe()
-        info = env.get_info_arrays()
-    dt = time.perf_counter() - t0
-    env.close()
-    return {"value": round(E * steps / dt, 1), "unit": "env-steps/s", "steps": steps, "num_envs": E,
+    out = {}
+    for reuse in (False, True):
+        env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
+                             distribution_mode="hard", reuse_arrays=reuse)
+        rng = np.random.RandomState(0)
+        acts = rng.randint(0, 15, size=(steps + 2, E)).astype(np.int32)
+        for k in range(2):
+            env.act(acts[k])
+            env.observe()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            env.act(acts[2 + k])
+            rew, ob, first = env.observe()
+            info = env.get_info_arrays()
+        dt = time.perf_counter() - t0
+        env.close()
+        out[reuse] = E * steps / dt
+    return {"value": round(out[False], 1), "reuse_arrays": round(out[True], 1), "unit": "env-steps/s",
+            "steps": steps, "num_envs": E,
             "what": "ProcgenGym3Env host mode: act(numpy) + observe() -> numpy rgb/rew/first + info arrays "
-                    "(libenv_observe device->host copy included)"}
+                    "(libenv_observe: DMA straight into the page-locked caller buffers)"}
 
 
 def main():
@@ -147,29 +152,18 @@ def main():
     seed = 0x5EED
     gather = None
     if args.gather:
-        # the engine's HBM obs shard as a torch tensor (no copy), gathered on the engine's own stream so
-        # the collective is ordered after the render of the same step and before the next step's
+        # double-buffered obs all-gather (procgen_amd/gather.py): step t renders into local[t % 2]
+        # and its RCCL all-gather runs on a communication stream while step t+1 computes
+        from procgen_amd.gather import ObsGather
         dp = env.device_ptrs()
-
-        class _Shard:
-            __cuda_array_interface__ = {"shape": (E, 64, 64, 3), "typestr": "|u1", "data": (dp.rgb, False),
-                                        "version": 2}
-
-        local = torch.as_tensor(_Shard(), device="cuda")
-        gathered = torch.empty((world * E, 64, 64, 3), dtype=torch.uint8, device="cuda")
-        stream = torch.cuda.ExternalStream(dp.stream)
-
-        def gather():
-            with torch.cuda.stream(stream):
-                if dist is not None:
-                    dist.all_gather_into_tensor(gathered, local)
-                else:
-                    gathered.copy_(local)
+        gather = ObsGather(E, world=world, dist=dist, engine_stream=torch.cuda.ExternalStream(dp.stream),
+                           bind=lambda buf: env.set_obs_buffer(buf.data_ptr()))
 
     def step(t):
-        env.act_hashed(seed, t)
         if gather is not None:
-            gather()
+            gather.step(lambda: env.act_hashed(seed, t))
+        else:
+            env.act_hashed(seed, t)
 
     t = 0
     for _ in range(args.warmup + args.settle):
@@ -257,8 +251,8 @@ def main():
                                    % (game, E, num_levels),
                        "env_name": game, "num_envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": "env-sharded x%d" % world,
-                       "gather": ("rccl all_gather_into_tensor of obs, %d B per rank per step" % (E * OBS_BYTES))
-                       if args.gather else None},
+                       "gather": ("double-buffered rccl all_gather_into_tensor of obs on a comm stream, "
+                                  "%d B per rank per step" % (E * OBS_BYTES)) if args.gather else None},
             "roofline": roof,
             "host_path": host,
             "cpu_baseline": cpu,

@@ -61,6 +61,12 @@ LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t);
 /* Block until every enqueued step finished (the device half of libenv_observe). */
 LIBENV_API int procgen_wait(libenv_env *env);
 LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers *out);
+/* Render the following steps into d_rgb (device memory of the env's GPU, uint8
+ * [num_envs][64][64][3], owned by the caller) instead of the library's observation tensor; NULL
+ * switches back.  Takes effect for steps enqueued after the call (the target is captured at
+ * launch), so a consumer can alternate two buffers and read / all-gather step t's observations
+ * while step t+1 renders (procgen_amd/gather.py).  Every step rewrites every env's frame. */
+LIBENV_API int procgen_set_obs_buffer(libenv_env *env, void *d_rgb);
 /* Copy the outputs of `count` envs (ids env_ids[k]) to host arrays of `count` rows after the
  * enqueued steps finish; any pointer may be NULL.  For consumers (and tests) that sample a few
  * envs of a device-resident batch without copying the whole observation tensor. */

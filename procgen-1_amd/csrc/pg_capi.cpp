@@ -310,12 +310,18 @@ struct VecEnv {
     std::vector<void *> allocs;
     uint32_t *d_pixels = nullptr;
     int32_t *d_sprites = nullptr, *d_bgs = nullptr, *d_themes = nullptr;
+    uint8_t *own_rgb = nullptr;   // the library's observation tensor (dev.rgb may point elsewhere,
+                                  // procgen_set_obs_buffer)
     int32_t *h_actions = nullptr; // page-locked staging of libenv_act's actions
     hipEvent_t act_copied = nullptr; // the last action upload has read h_actions
     bool act_pending = false;
     std::vector<uint8_t> h_staging;
     uint8_t *pinned = nullptr;  // page-locked landing zone of copy_out (all output planes)
     size_t pinned_bytes = 0;
+    // caller buffers that are one contiguous array per output plane (what gym3 allocates) are
+    // page-locked in place with hipHostRegister and written by DMA directly (no staging copy)
+    std::vector<void *> registered;
+    bool direct = false;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev; // per timed step: 4 per game (before step, after step, after reset,
@@ -362,6 +368,7 @@ static hipError_t copy_sync(VecEnv *v, void *dst, const void *src, size_t bytes,
 
 int upload_atlas(VecEnv *v, const uint32_t *pixels, int64_t num_pixels, const pg_image *sprites,
                  const pg_image *backgrounds, const int32_t *num_backgrounds, const int32_t *num_themes);
+int copy_latent(VecEnv *v);
 
 int fail(VecEnv *v, int code, const char *msg) {
     if (v && !v->error) {
@@ -460,11 +467,56 @@ static void host_copy(void *dst, const void *src, size_t bytes) {
     for (auto &x : th) x.join();
 }
 
-int copy_out(VecEnv *v) {
-    // device planes -> one page-locked landing zone (DMA, ordered on the env's stream) ->
-    // the caller's per-env host pointers (contiguous runs become one memcpy).  Landing in
-    // pinned memory first keeps the caller's pageable buffers out of the async copy path.
+// The caller's buffers of one output plane, if they form one contiguous array (stride = element
+// size): its base, else nullptr.
+static void *contiguous(void **ptrs, size_t n, size_t elem) {
+    for (size_t e = 1; e < n; e++)
+        if ((char *)ptrs[e] != (char *)ptrs[0] + e * elem) return nullptr;
+    return ptrs[0];
+}
+
+static void unregister_buffers(VecEnv *v) {
+    for (void *p : v->registered) (void)hipHostUnregister(p);
+    v->registered.clear();
+    v->direct = false;
+}
+
+// libenv_set_buffers: page-lock the caller's planes when every one is a contiguous array
+static void register_buffers(VecEnv *v) {
+    unregister_buffers(v);
     const size_t n = (size_t)v->num_envs;
+    void *planes[6] = {contiguous(&v->ob_ptrs[0], n, PG_OBS_BYTES), v->rew_host, v->first_host,
+                       contiguous(&v->info_ptrs[0], n, 4), contiguous(&v->info_ptrs[n], n, 1),
+                       contiguous(&v->info_ptrs[2 * n], n, 4)};
+    const size_t sizes[6] = {PG_OBS_BYTES, 4, 1, 4, 1, 4};
+    for (int k = 0; k < 6; k++)
+        if (!planes[k]) return;
+    for (int k = 0; k < 6; k++) {
+        if (hipHostRegister(planes[k], sizes[k] * n, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            unregister_buffers(v);
+            return;
+        }
+        v->registered.push_back(planes[k]);
+    }
+    v->direct = true;
+}
+
+int copy_out(VecEnv *v) {
+    // device planes -> the caller's buffers: straight DMA into page-locked contiguous planes
+    // (register_buffers), otherwise one page-locked landing zone (DMA, ordered on the env's
+    // stream) -> the caller's per-env host pointers (contiguous runs become one memcpy).
+    const size_t n = (size_t)v->num_envs;
+    if (v->direct) {
+        HIPCHECK(hipMemcpyAsync(v->registered[0], v->dev.rgb, PG_OBS_BYTES * n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipMemcpyAsync(v->registered[1], v->dev.rew, 4 * n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipMemcpyAsync(v->registered[2], v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipMemcpyAsync(v->registered[3], v->dev.prev_level_seed, 4 * n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipMemcpyAsync(v->registered[4], v->dev.prev_level_complete, n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipMemcpyAsync(v->registered[5], v->dev.level_seed, 4 * n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(hipStreamSynchronize(v->stream));
+        return copy_latent(v);
+    }
     const size_t sizes[6] = {PG_OBS_BYTES, 4, 1, 4, 1, 4};
     const void *dsrc[6] = {v->dev.rgb, v->dev.rew, v->dev.first, v->dev.prev_level_seed,
                            v->dev.prev_level_complete, v->dev.level_seed};
@@ -496,6 +548,11 @@ int copy_out(VecEnv *v) {
     scatter(v->pinned + off[3], 4, &v->info_ptrs[0 * n]);
     scatter(v->pinned + off[4], 1, &v->info_ptrs[1 * n]);
     scatter(v->pinned + off[5], 4, &v->info_ptrs[2 * n]);
+    return copy_latent(v);
+}
+
+int copy_latent(VecEnv *v) {
+    const size_t n = (size_t)v->num_envs;
     if (v->has_latent) { // grid_size, grid, agent_pos, exit_pos (vecgame.cpp:270-316)
         const size_t row = (size_t)PG_LATENT_N * 4;
         std::vector<int32_t> lat((size_t)PG_LATENT_N * n);
@@ -657,6 +714,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.mt, n * 2 * PG_MT_WORDS);
     rc |= dalloc(v, &d.actions, n);
     rc |= dalloc(v, &d.rgb, n * PG_OBS_BYTES);
+    v->own_rgb = d.rgb;
     rc |= dalloc(v, &d.rew, n);
     rc |= dalloc(v, &d.first, n);
     rc |= dalloc(v, &d.prev_level_seed, n);
@@ -865,6 +923,8 @@ LIBENV_API void libenv_set_buffers(libenv_env *env, struct libenv_buffers *bufs)
     v->rew_host = bufs->rew;
     v->first_host = bufs->first;
     v->buffers_set = true;
+    (void)hipSetDevice(v->device);
+    register_buffers(v);
     // latent-state info tensors (grid_size, grid, agent_pos, exit_pos) are only filled by
     // maze/miner (maze.cpp:152-165, miner.cpp:378-396); zero them for the other games (copy_out
     // overwrites them every observe when a game of the batch has a latent state)
@@ -907,6 +967,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     if (!v) return;
     if (v->stream) hipStreamSynchronize(v->stream);
+    unregister_buffers(v);
     for (void *p : v->allocs) hipFree(p);
     if (v->pinned) (void)hipHostFree(v->pinned);
     if (v->h_actions) (void)hipHostFree(v->h_actions);
@@ -951,6 +1012,12 @@ LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers 
     out->level_seed = v->dev.level_seed;
     out->actions = v->dev.actions;
     out->stream = (void *)v->stream;
+    return 0;
+}
+
+LIBENV_API int procgen_set_obs_buffer(libenv_env *env, void *d_rgb) {
+    VecEnv *v = (VecEnv *)env;
+    v->dev.rgb = d_rgb ? (uint8_t *)d_rgb : v->own_rgb;
     return 0;
 }
 

@@ -1220,8 +1220,10 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     bool ent_setup_valid = false;
 #define PG_DRAW_ENTITIES(Z)                                                                   \
     for (int base = 0; base < n; base += 64) {                                                \
+        pt.mark(4);                                                                           \
         if (!one_chunk || !ent_setup_valid) entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err); \
         ent_setup_valid = true;                                                               \
+        pt.mark(3);                                                                           \
         stamp_images(fb, d, im, ballot(im.draw && im.ez == (Z)), err);                        \
     }
 
@@ -1274,6 +1276,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     } else if (has_z_minus1<G>()) {
         err = true; // unreachable: the fast path is never taken with z = -1 entities
     }
+    pt.mark(2);
     // ---- entities, render_z 0 then 1 (basic-abstract-game.cpp:966-967)
     ent_setup_valid = false;
     PG_DRAW_ENTITIES(0)
@@ -1290,11 +1293,10 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         fb_fill_rectf(fb, infodim, 0, infodim, infodim, 0xff000000u | (s2 * 0x010101u));
         wave_sync();
     }
+    pt.mark(4);
     game_overlay<G>(fb, s, v, d, env, err);
     wave_sync();
-
-
-    pt.mark(2);
+    pt.mark(5);
     // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
     uint8_t *out = d.rgb + (size_t)env * PG_OBS_BYTES;
     for (int q = lane; q < PG_RES * PG_RES / 4; q += 64) {
@@ -1309,7 +1311,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         o[2] = w2;
     }
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
-    pt.mark(3);
+    pt.mark(6);
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 

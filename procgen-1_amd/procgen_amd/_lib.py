@@ -74,6 +74,7 @@ SIGNATURES = {
     "procgen_atlas_host": (ctypes.c_int64, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_read_envs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
+    "procgen_set_obs_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_start": (ctypes.c_int, [ctypes.c_void_p]),
     "procgen_act_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_act_hashed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32]),

@@ -37,6 +37,25 @@ COMBOS = [("LEFT", "DOWN"), ("LEFT",), ("LEFT", "UP"), ("DOWN",), (), ("UP",), (
           ("RIGHT", "UP"), ("D",), ("A",), ("W",), ("S",), ("Q",), ("E",)]
 
 
+_POOL = None
+
+
+def _copy(a, chunk=64 << 20):
+    """np.copy, split over threads when large (numpy releases the GIL while copying)."""
+    if a.nbytes <= chunk or a.shape[0] < 2:
+        return a.copy()
+    global _POOL
+    if _POOL is None:
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max(1, min(8, len(os.sched_getaffinity(0)))))
+    out = np.empty_like(a)
+    n = a.shape[0]
+    k = min(n, max(2, a.nbytes // chunk))
+    list(_POOL.map(lambda i: np.copyto(out[i * n // k:(i + 1) * n // k], a[i * n // k:(i + 1) * n // k]), range(k)))
+    return out
+
+
 def create_random_seed():  # procgen/env.py:73-82 (no mpi4py here)
     return random.SystemRandom().randint(0, 2 ** 31 - 1)
 
@@ -68,7 +87,7 @@ class BaseProcgenEnv:
 
     def __init__(self, num, env_name, options, debug=False, rand_seed=None, num_levels=0, start_level=0,
                  use_sequential_levels=False, debug_mode=0, resource_root=None, num_threads=4, render_mode=None,
-                 device_buffers=False, env_offset=0, upload_atlas=False):
+                 device_buffers=False, env_offset=0, upload_atlas=False, reuse_arrays=False):
         lib = _lib.load()
         self._lib = lib
         if render_mode is None:
@@ -122,6 +141,7 @@ class BaseProcgenEnv:
         self.ac_space = TensorType((), Discrete(act[3] + 1))
         self.ob_space = {"rgb": TensorType(self.ob_types[0][2], Discrete(256))}
         self.device_buffers = device_buffers
+        self.reuse_arrays = reuse_arrays  # gym3 CEnv(reuse_arrays=...): observe() returns the live buffers
         if device_buffers:
             rc = lib.procgen_start(self._handle)
             _check(lib, self._handle, rc)
@@ -199,7 +219,10 @@ class BaseProcgenEnv:
             return None
         self._lib.libenv_observe(self._handle)
         _check(self._lib, self._handle)
-        return self._rew.copy(), {k: v.copy() for k, v in self._ob.items()}, self._first.astype(bool)
+        if self.reuse_arrays:
+            return self._rew, self._ob, self._first.view(bool)
+        # gym3 CEnv._maybe_copy: fresh arrays every observe (a threaded copy for large batches)
+        return self._rew.copy(), {k: _copy(v) for k, v in self._ob.items()}, self._first.astype(bool)
 
     def get_info(self):
         """gym3 contract: one dict per env (procgen/env.py via gym3 CEnv.get_info)."""
@@ -260,6 +283,11 @@ class BaseProcgenEnv:
             "rgb", "rew", "first", "prev_level_seed", "prev_level_complete", "level_seed")])
         _check(self._lib, self._handle, rc)
         return out
+
+    def set_obs_buffer(self, ptr):
+        """Render later steps into the device buffer at `ptr` (uint8 [num,64,64,3]); None = own tensor."""
+        rc = self._lib.procgen_set_obs_buffer(self._handle, ptr)
+        _check(self._lib, self._handle, rc)
 
     def device_ptrs(self):
         d = _lib.pg_device_buffers()

@@ -64,3 +64,36 @@ def test_c4_maze_heist_combined():
     sample = [0, 1, 2, 3, 4095, 4096, 32767, 32768, 50001, 50002, num - 2, num - 1]
     eps = run_sampled(["maze", "heist"], num, 0, sample, 520, seed=0xC4)  # maze times out at 500 (maze.cpp:22)
     assert eps > 0
+
+
+def test_double_buffered_gather_on_device():
+    """procgen_amd.gather.ObsGather with the HIP engine (world 1: the gather is a device copy on
+    the communication stream): step t's gathered frames, read after step t+1 was issued, are step
+    t's frames (sampled envs vs the oracle), and the engine keeps alternating its render target."""
+    import torch
+    from procgen_amd import ProcgenGym3Env
+    from procgen_amd.gather import ObsGather
+    torch.cuda.set_device(0)
+    num = 4096
+    names = ENV_NAMES
+    env = ProcgenGym3Env(num=num, env_name=",".join(names), num_levels=0, rand_seed=5, device_buffers=True)
+    dp = env.device_ptrs()
+    g = ObsGather(num, engine_stream=torch.cuda.ExternalStream(dp.stream),
+                  bind=lambda t: env.set_obs_buffer(t.data_ptr()))
+    sample = np.array([0, 1, 2, 3, 17, 33, 1000, 2047, 4095], np.int32)
+    orcs = [OracleEnv(names[int(n) % 16], 1, env_offset=int(n), num_levels=0, rand_seed=5) for n in sample]
+    seed = 0xD8
+    pending = None
+    for t in range(1, 82):
+        k = g.step(lambda: env.act_hashed(seed, t)) if t <= 80 else None
+        if pending is not None:
+            tp, kp = pending
+            got = g.result(kp)[torch.from_numpy(sample).long().cuda()].cpu().numpy()
+            g.release(kp)
+            act = hashed_actions(seed, sample, tp)
+            for j, o in enumerate(orcs):
+                o.step(act[j:j + 1])
+                np.testing.assert_array_equal(got[j], o.observe()["rgb"][0], err_msg="step %d env %d" % (tp, sample[j]))
+        pending = (t, k) if k is not None else None
+    torch.cuda.synchronize()
+    env.close()
