@@ -64,18 +64,26 @@ def cpu_baseline(game, num_levels, max_workers=16, steps=12000):
 
 
 def pmc_traffic(game):
-    """HBM bytes per render launch of `game` from the newest committed rocprofv3 PMC summary
-    (profiles/*pmc*.json, written by scripts/gpu_profile.sh from separate FETCH_SIZE / WRITE_SIZE
-    passes over this same bench command), or (None, None)."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), key=os.path.getmtime)
-    for path in reversed(files):
+    """HBM bytes (FETCH_SIZE + WRITE_SIZE) per render launch of `game` from the newest committed
+    rocprofv3 PMC summary under profiles/ (separate FETCH_SIZE / WRITE_SIZE passes over this same
+    bench command: scripts/gpu_counters.sh -> *counters_summary.json, or the older
+    scripts/gpu_profile.sh -> *pmc*.json), or (None, None).  "Newest" = last by path name
+    (profiles/r01_v1 ... profiles/r02/r02_x ...), not by file time, which a checkout resets."""
+    files = glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True)
+    files += glob.glob(os.path.join(REPO, "profiles", "**", "*counters_summary.json"), recursive=True)
+    for path in sorted(files, key=lambda p: os.path.relpath(p, REPO), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except Exception:
             continue
         if d.get("game", "coinrun") == game and d.get("render_hbm_bytes_per_launch"):
-            return d["render_hbm_bytes_per_launch"], os.path.basename(path)
+            return d["render_hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
+        g = d.get(game)
+        if isinstance(g, dict):
+            for kname, k in g.items():
+                if kname.startswith("pg_render_kernel") and isinstance(k, dict) and k.get("hbm_bytes_per_launch"):
+                    return k["hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
     return None, None
 
 

@@ -387,6 +387,13 @@ DEV uint32_t blend_argb_pm(uint32_t dst, uint32_t src, int const_alpha) {
     return s + BYTE_MUL(dst, (~s) >> 24);
 }
 
+// SourceOver shortcut for a texel whose alpha is 0 or 255 at full opacity: BYTE_MUL(dst, 255) ==
+// dst and BYTE_MUL(dst, 0) == 0 exactly, so blend_argb_pm(dst, src, 256) == over_binary(dst, src).
+// Callers take it only when no lane of the wave holds a partial-alpha texel (alpha_partial),
+// a wave-uniform branch, so the result is bit-identical to the full blend.
+DEV uint32_t alpha_partial(uint32_t t) { return (t - 0x01000000u) < 0xfe000000u ? 1u : 0u; }
+DEV uint32_t over_binary(uint32_t dst, uint32_t src) { return src + (src < 0x01000000u ? dst : 0u); }
+
 DEV int qt_int_opacity(double o) {
     if (o < 0) o = 0;
     if (o > 1) o = 1;

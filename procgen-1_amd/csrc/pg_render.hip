@@ -175,7 +175,7 @@ DEV float tile_aspect_ratio(int type, float rx, float ry) {
     return 0.0f;
 }
 template <int G>
-DEV bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
+DEV constexpr bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
 // Side of the square grid-tile images of the pixel-centric fast path (0: the game always takes the
 // generic tile pass).  Coinrun and heist draw only such tiles; for the others a frame takes the fast
 // path when every tile in its window is one (a window scan decides, e.g. jumper's and climber's
@@ -194,7 +194,7 @@ template <int G>
 DEV constexpr bool always_uniform() { return G == PG_GAME_COINRUN || G == PG_GAME_HEIST || G == PG_GAME_CAVEFLYER; }
 // the game has render_z = -1 entities (drawn between background and grid, :933)
 template <int G>
-DEV bool has_z_minus1() { return G == PG_GAME_MINER; } // miner's exit (miner.cpp:217)
+DEV constexpr bool has_z_minus1() { return G == PG_GAME_MINER; } // miner's exit (miner.cpp:217)
 // an image the reference lists but the asset tree lacks (miner's mud.png, resources.cpp:511):
 // drawn as nothing (the reference cannot load it; parity unpinned for MUD tiles)
 template <int G>
@@ -250,10 +250,17 @@ DEV bool axis_setup_signed(double r, double rw, int iw, Axis &a) {
     return true;
 }
 
-// returns false when the transform is not a rotation this path reproduces
-DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
-                      double m11, double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
-    if (!(w > 0) || !(h > 0) || iw <= 0 || ih <= 0) return true; // QRectF::isEmpty: nothing drawn
+// The integer state of qt_transform_image for one rotated image: 3 trapezoids + texture stepping.
+struct RotGeo {
+    Trap tr[3];
+    int dudx, dvdx, dudy, dvdy, u0, v0;
+};
+
+// Setup of save(); translate; rotate; drawImage(QRectF(-w/2, -h/2, w, h)): 0 = nothing drawn,
+// 1 = TxScale (qt_scale_image_32bit with the signed axes ex / ey), 2 = a transform blit (g).
+DEV int rot_prepare(double x, double y, double w, double h, double m11, double m12, double m21, double m22, int iw,
+                    int ih, Axis &ex, Axis &ey, RotGeo &g) {
+    if (!(w > 0) || !(h > 0) || iw <= 0 || ih <= 0) return 0; // QRectF::isEmpty: nothing drawn
     const double dx = x + w / 2, dy = y + h / 2;
     const double rx = -w / 2, ry = -h / 2, right = rx + w, bottom = ry + h;
     if (m12 == 0 && m21 == 0) {
@@ -261,33 +268,8 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
         // qt_scale_image_32bit on qt_mapRect_non_normalizing(r, matrix) -- the TxScale map
         const double ax = m11 * rx + dx, ay = m22 * ry + dy;
         const double bx = m11 * right + dx, by = m22 * bottom + dy;
-        Axis ex, ey;
-        if (!axis_setup_signed(ax, bx - ax, iw, ex) || !axis_setup_signed(ay, by - ay, ih, ey)) return true;
-        const int lane = LANE;
-        bool ok = true;
-        if (lane >= ex.t1 && lane < ex.t1 + ex.n) {
-            int scol = (int)((ex.base + (uint32_t)((lane - ex.t1) * ex.step)) >> 16);
-            if (mir) scol = iw - 1 - scol;
-            for (int k0 = 0; k0 < ey.n; k0 += BB) { // BB rows: every texel load issued before the blends
-                uint32_t tv[BB];
-#pragma unroll
-                for (int r = 0; r < BB; r++) {
-                    const int k = k0 + r;
-                    const uint32_t idx = soff + (uint32_t)(((int)((ey.base + (uint32_t)(k * ey.step)) >> 16)) * iw + scol);
-                    const bool in = k < ey.n && idx < npix;
-                    if (k < ey.n && !in) ok = false;
-                    tv[r] = pixels[in ? idx : 0u];
-                }
-#pragma unroll
-                for (int r = 0; r < BB; r++) {
-                    const int k = k0 + r;
-                    if (k >= ey.n) break;
-                    const int o = (ey.t1 + k) * PG_RES + lane;
-                    fb[o] = blend_argb_pm(fb[o], tv[r], ca);
-                }
-            }
-        }
-        return ok;
+        if (!axis_setup_signed(ax, bx - ax, iw, ex) || !axis_setup_signed(ay, by - ay, ih, ey)) return 0;
+        return 1;
     }
     QV v[4]; // TopLeft, TopRight, BottomRight, BottomLeft
     auto map = [&](double px, double py, QV &o) {
@@ -321,7 +303,7 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
     QV u = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].u - v[0].u, v[1].v - v[0].v};
     QV ww = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].u - v[0].u, v[2].v - v[0].v};
     double det = u.x * ww.y - u.y * ww.x;
-    if (det == 0) return true;
+    if (det == 0) return 0;
     double invDet = 1.0 / det;
     double n11 = (u.u * ww.y - u.y * ww.u) * invDet;
     double n12 = (u.x * ww.u - u.u * ww.x) * invDet;
@@ -329,25 +311,61 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
     double n22 = (u.x * ww.v - u.v * ww.x) * invDet;
     double mdx = v[0].u - n11 * v[0].x - n12 * v[0].y;
     double mdy = v[0].v - n21 * v[0].x - n22 * v[0].y;
-    const int dudx = (int)(n11 * 0x10000), dvdx = (int)(n21 * 0x10000);
-    const int dudy = (int)(n12 * 0x10000), dvdy = (int)(n22 * 0x10000);
-    const int u0 = (int)ceil((0.5 * n11 + 0.5 * n12 + mdx) * 0x10000) - 1;
-    const int v0 = (int)ceil((0.5 * n21 + 0.5 * n22 + mdy) * 0x10000) - 1;
-    Trap tr[3];
+    g.dudx = (int)(n11 * 0x10000); g.dvdx = (int)(n21 * 0x10000);
+    g.dudy = (int)(n12 * 0x10000); g.dvdy = (int)(n22 * 0x10000);
+    g.u0 = (int)ceil((0.5 * n11 + 0.5 * n12 + mdx) * 0x10000) - 1;
+    g.v0 = (int)ceil((0.5 * n21 + 0.5 * n22 + mdy) * 0x10000) - 1;
     if (v[1].y < v[3].y) {
-        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[1].y, tr[0]);
-        trap_setup(v[1], v[2], v[0], v[3], v[1].y, v[3].y, tr[1]);
-        trap_setup(v[1], v[2], v[3], v[2], v[3].y, v[2].y, tr[2]);
+        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[1].y, g.tr[0]);
+        trap_setup(v[1], v[2], v[0], v[3], v[1].y, v[3].y, g.tr[1]);
+        trap_setup(v[1], v[2], v[3], v[2], v[3].y, v[2].y, g.tr[2]);
     } else {
-        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[3].y, tr[0]);
-        trap_setup(v[0], v[1], v[3], v[2], v[3].y, v[1].y, tr[1]);
-        trap_setup(v[1], v[2], v[3], v[2], v[1].y, v[2].y, tr[2]);
+        trap_setup(v[0], v[1], v[0], v[3], v[0].y, v[3].y, g.tr[0]);
+        trap_setup(v[0], v[1], v[3], v[2], v[3].y, v[1].y, g.tr[1]);
+        trap_setup(v[1], v[2], v[3], v[2], v[1].y, v[2].y, g.tr[2]);
+    }
+    return 2;
+}
+
+// returns false when the transform is not a rotation this path reproduces
+DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
+                      double m11, double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
+    Axis ex, ey;
+    RotGeo g;
+    const int kind = rot_prepare(x, y, w, h, m11, m12, m21, m22, iw, ih, ex, ey, g);
+    if (kind == 0) return true;
+    if (kind == 1) {
+        const int lane = LANE;
+        bool ok = true;
+        if (lane >= ex.t1 && lane < ex.t1 + ex.n) {
+            int scol = (int)((ex.base + (uint32_t)((lane - ex.t1) * ex.step)) >> 16);
+            if (mir) scol = iw - 1 - scol;
+            for (int k0 = 0; k0 < ey.n; k0 += BB) { // BB rows: every texel load issued before the blends
+                uint32_t tv[BB];
+#pragma unroll
+                for (int r = 0; r < BB; r++) {
+                    const int k = k0 + r;
+                    const uint32_t idx = soff + (uint32_t)(((int)((ey.base + (uint32_t)(k * ey.step)) >> 16)) * iw + scol);
+                    const bool in = k < ey.n && idx < npix;
+                    if (k < ey.n && !in) ok = false;
+                    tv[r] = pixels[in ? idx : 0u];
+                }
+#pragma unroll
+                for (int r = 0; r < BB; r++) {
+                    const int k = k0 + r;
+                    if (k >= ey.n) break;
+                    const int o = (ey.t1 + k) * PG_RES + lane;
+                    fb[o] = blend_argb_pm(fb[o], tv[r], ca);
+                }
+            }
+        }
+        return ok;
     }
     const int lane = LANE;
     bool ok = true;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        const Trap T = tr[k];
+        const Trap T = g.tr[k];
         for (int y0 = T.from_y; y0 < T.to_y; y0 += BB) { // BB scan lines: loads first, then blends
             uint32_t tv[BB];
             bool on[BB];
@@ -357,8 +375,8 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
                 const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
                 const int fromX = max(xl >> 16, 0), toX = min(xr >> 16, PG_RES);
                 on[r] = yy < T.to_y && lane >= fromX && lane < toX;
-                int uu = (lane * dudx + yy * dudy + u0) >> 16;
-                int vv = (lane * dvdx + yy * dvdy + v0) >> 16;
+                int uu = (lane * g.dudx + yy * g.dudy + g.u0) >> 16;
+                int vv = (lane * g.dvdx + yy * g.dvdy + g.v0) >> 16;
                 uu = min(max(uu, 0), iw - 1);
                 vv = min(max(vv, 0), ih - 1);
                 if (mir) uu = iw - 1 - uu;
@@ -385,7 +403,9 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
 // is blended strictly in order.  Footprints wider than one wave (> 64 px) fall back to an
 // in-order loop with inline loads; rotated images run the transform blit in place.
 struct Img {
-    bool draw, rot;
+    bool draw;
+    int rot;               // 0 scale blit, 1 transform blit (set up when stamped), 2 transform blit, descriptor rdi in LDS
+    int rdi;
     uint32_t fill;         // != 0: an opaque fillRect of this colour over the ex / ey footprint
     Axis ex, ey;
     int soff, sw, sh, ca, mir, rslot, ez;
@@ -397,7 +417,8 @@ struct Img {
 
 DEV void img_clear(Img &im) {
     im.draw = false;
-    im.rot = false;
+    im.rot = 0;
+    im.rdi = 0;
     im.ntile = 0;
     im.tw = im.th = 0;
     im.fill = 0;
@@ -593,7 +614,48 @@ DEV void blit_seq(uint32_t *fb, const PGDev &d, const Axis &ex, const Axis &ey, 
     }
 }
 
-DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long long m, bool &err) {
+// Transform blit of image descriptor `rd` (rot_stage): lanes = pixels of its bounding box, each
+// finds its scan line's trapezoid -- the pixels qt_transform_image's row loop would touch, in any
+// order, since one image's pixels are distinct.
+DEV void rot_stamp_lds(uint32_t *fb, const PGDev &d, const uint8_t *aux, int rd, bool &err) {
+    const int4 *D = reinterpret_cast<const int4 *>(aux) + 8 * rd;
+    const int4 a0 = D[0], a1 = D[1], a2 = D[2], a3 = D[3], a4 = D[4], a5 = D[5], a6 = D[6], a7 = D[7];
+    // a0 = tr0 (from, to, x_l, dx_l), a1 = (tr0 x_r, dx_r, tr1 from, to), a2 = tr1 (x_l, dx_l, x_r, dx_r),
+    // a3 = tr2 (from, to, x_l, dx_l), a4 = (tr2 x_r, dx_r, dudx, dvdx), a5 = (dudy, dvdy, u0, v0),
+    // a6 = (soff, iw, ih, mir), a7 = (ca, xmin, nx, ymin | ny << 16)
+    const int xmin = a7.y, nx = a7.z, ymin = a7.w & 0xffff, ny = a7.w >> 16;
+    const int total = nx * ny;
+    if (total <= 0) return;
+    const float inv = 1.0f / (float)nx;
+    const uint32_t npix = d.num_pixels;
+    for (int p = LANE; p < total; p += 64) {
+        const int yy = ymin + (int)(((float)(p - 0) + 0.5f) * inv);
+        const int x = xmin + (p - (yy - ymin) * nx);
+        int from, xl, dxl, xr, dxr;
+        bool in;
+        if (yy >= a0.x && yy < a0.y) { from = a0.x; xl = a0.z; dxl = a0.w; xr = a1.x; dxr = a1.y; in = true; }
+        else if (yy >= a1.z && yy < a1.w) { from = a1.z; xl = a2.x; dxl = a2.y; xr = a2.z; dxr = a2.w; in = true; }
+        else if (yy >= a3.x && yy < a3.y) { from = a3.x; xl = a3.z; dxl = a3.w; xr = a4.x; dxr = a4.y; in = true; }
+        else { from = 0; xl = dxl = xr = dxr = 0; in = false; }
+        const int xlv = xl + (yy - from) * dxl, xrv = xr + (yy - from) * dxr;
+        const int fromX = max(xlv >> 16, 0), toX = min(xrv >> 16, PG_RES);
+        bool on = in && x >= fromX && x < toX;
+        int uu = (x * a4.z + yy * a5.x + a5.z) >> 16;
+        int vv = (x * a4.w + yy * a5.y + a5.w) >> 16;
+        uu = min(max(uu, 0), a6.y - 1);
+        vv = min(max(vv, 0), a6.z - 1);
+        if (a6.w) uu = a6.y - 1 - uu;
+        const uint32_t idx = (uint32_t)a6.x + (uint32_t)(vv * a6.y + uu);
+        if (on && idx >= npix) {
+            err = true;
+            on = false;
+        }
+        const uint32_t tv = d.pixels[on ? idx : 0u];
+        if (on) fb[yy * PG_RES + x] = blend_argb_pm(fb[yy * PG_RES + x], tv, a7.x);
+    }
+}
+
+DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
     const int lane = LANE;
     const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
     const uint32_t npix = d.num_pixels;
@@ -647,7 +709,12 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
             const int j = js[g];
             if (j < 0) continue;
             const int caj = readlane(im.ca, j);
-            if (readlane(im.rot ? 1 : 0, j)) {
+            const int rk = readlane(im.rot, j);
+            if (rk == 2) {
+                rot_stamp_lds(fb, d, aux, readlane(im.rdi, j), err);
+                continue;
+            }
+            if (rk) {
                 const double m11 = readlane_d(im.m11, j);
                 if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
                                   readlane_d(im.rh, j), m11, readlane_d(im.m12, j), readlane_d(im.m21, j), m11,
@@ -664,7 +731,14 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const Img &im, unsigned long
                 const int vert = readlane(im.rslot, j); // 1: vertical tiling (negative ratio)
                 const uint32_t offj = (uint32_t)readlane(im.soff, j);
                 const int swj = readlane(im.sw, j), shj = readlane(im.sh, j), mirj = readlane(im.mir, j);
-                for (int t = 0; t < ntile; t++) {
+                // tiles that can reach the frame (2 px margin; axis_setup culls exactly)
+                const double tsz = vert ? (double)th : (double)tw, org = vert ? ry : rx;
+                int tlo = 0, thi = ntile;
+                if (tsz > 0) {
+                    tlo = max(0, (int)floor((-2.0 - org) / tsz) - 1);
+                    thi = min(ntile, (int)ceil((PG_RES + 2.0 - org) / tsz) + 1);
+                }
+                for (int t = tlo; t < thi; t++) {
                     const double x = vert ? rx : rx + (double)(tw * (float)t);
                     const double y = vert ? ry + (double)(th * (float)t) : ry;
                     Axis ex, ey;
@@ -784,7 +858,7 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         im.rslot = rslot;
         im.tw = rotation;
         im.draw = true;
-        im.rot = true;
+        im.rot = 1;
         im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
     } else if (tile_aspect_ratio<G>(etype, prx, pry) != 0) {
         float tile_ratio = tile_aspect_ratio<G>(etype, prx, pry);
@@ -805,9 +879,369 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         }
         im.ntile = num_tiles;
         im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
-        im.draw = true;
+        // the tiles lie inside the rect (up to float rounding of the tile size): a rect 2 px clear
+        // of the frame draws nothing (fruitbot's walls off screen)
+        im.draw = rx + rw > -2 && rx < PG_RES + 2 && ry + rh > -2 && ry < PG_RES + 2;
     } else if (axis_setup(rx, rw, sp.y, im.ex) && axis_setup(ry, rh, sp.z, im.ey)) {
         im.draw = true;
+    }
+}
+
+// Transform blits of a chunk's rotated images, set up lane-parallel: a TxScale map becomes a plain
+// scale blit, a rotation's trapezoids and texture stepping go to descriptor slot `rank` in the aux
+// LDS (dead once the tiles are drawn); past `cap` descriptors an image keeps the in-order setup.
+#define ROT_DESC_CAP 32
+DEV void rot_stage(Img &im, uint8_t *aux) {
+    const int lane = LANE;
+    Axis ex, ey;
+    RotGeo g;
+    int kind = 0;
+    const bool cand = im.draw && im.rot == 1;
+    if (cand) kind = rot_prepare(im.rx, im.ry, im.rw, im.rh, im.m11, im.m12, im.m21, im.m11, im.sw, im.sh, ex, ey, g);
+    if (cand && kind == 0) im.draw = false;
+    if (cand && kind == 1) { im.rot = 0; im.ex = ex; im.ey = ey; }
+    const bool gen = cand && kind == 2;
+    const int rank = __popcll(ballot(gen) & ((1ull << lane) - 1));
+    if (gen && rank < ROT_DESC_CAP) {
+        int ymin = PG_RES, ymax = 0, xmin = PG_RES, xmax = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const Trap T = g.tr[k];
+            if (T.from_y >= T.to_y) continue;
+            ymin = min(ymin, T.from_y);
+            ymax = max(ymax, T.to_y);
+#pragma unroll
+            for (int e = 0; e < 2; e++) { // fromX / toX are monotone in y: extremes at the end rows
+                const int yy = e ? T.to_y - 1 : T.from_y;
+                const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
+                xmin = min(xmin, max(xl >> 16, 0));
+                xmax = max(xmax, min(xr >> 16, PG_RES));
+            }
+        }
+        const int nx = xmax > xmin ? xmax - xmin : 0, ny = ymax > ymin ? ymax - ymin : 0;
+        int4 *D = reinterpret_cast<int4 *>(aux) + 8 * rank;
+        D[0] = make_int4(g.tr[0].from_y, g.tr[0].to_y, g.tr[0].x_l, g.tr[0].dx_l);
+        D[1] = make_int4(g.tr[0].x_r, g.tr[0].dx_r, g.tr[1].from_y, g.tr[1].to_y);
+        D[2] = make_int4(g.tr[1].x_l, g.tr[1].dx_l, g.tr[1].x_r, g.tr[1].dx_r);
+        D[3] = make_int4(g.tr[2].from_y, g.tr[2].to_y, g.tr[2].x_l, g.tr[2].dx_l);
+        D[4] = make_int4(g.tr[2].x_r, g.tr[2].dx_r, g.dudx, g.dvdx);
+        D[5] = make_int4(g.dudy, g.dvdy, g.u0, g.v0);
+        D[6] = make_int4(im.soff, im.sw, im.sh, im.mir);
+        D[7] = make_int4(im.ca, xmin, nx, (ymin & 0xffff) | (ny << 16));
+        im.rot = 2;
+        im.rdi = rank;
+    }
+}
+
+// ------------------------------------------------------------------ general pixel-centric tile pass
+// draw_foreground's grid loop (basic-abstract-game.cpp:930-964) for any mix of tile image sizes and
+// draw_grid_obj fills, lane = screen column like the fast path.  Every drawable grid value of the game
+// gets a typeinfo slot; tile images of one (w, h) -- or one fill geometry -- form a class, and the Qt
+// blit setup (axis_setup / fillRect edges) of every window column and row is computed once per class.
+// A pixel then blends the <= 2 x 2 tiles covering it in x-major / y-minor order: first tile column in
+// the row pass (the background fused in when no z = -1 entity has to go between them), the second
+// tile column of the few screen columns two tiles overlap in a lane = row pass.  Frames this cannot
+// express (more classes than GEN_K, a window wider than 63 or larger than GEN_GW cells, a grid value
+// outside the table, 3 tiles covering one pixel) take the stamped generic pass instead.
+#define GEN_K 6       // tile classes per frame
+#define GEN_GW 1024   // window cells (u8 slot per cell)
+#define GEN_NOTHING 64
+#define GEN_BAD 15
+template <int G>
+DEV constexpr bool has_general() { return has_grid_tiles<G>() && !always_uniform<G>(); }
+// aux LDS: typeinfo (65 int2) | window slots (GEN_GW u8) | xs0, xs1, ys0, ys1 (GEN_K x 64 int16 each)
+#define GEN_TI_BYTES (65 * 8)
+#define GEN_AUX_BYTES (GEN_TI_BYTES + GEN_GW + 4 * GEN_K * 64 * 2)
+// typeinfo slot <-> grid value: values 0..62 map to themselves; chaser's ORB (1002) takes slot 63
+template <int G>
+DEV int gen_slot_type(int slot) {
+    if constexpr (G == PG_GAME_CHASER) if (slot == 63) return CH_ORB;
+    return slot;
+}
+template <int G>
+DEV int gen_slot(int type) { // GEN_NOTHING: not drawn; -1: not on this path
+    if (type == INVALID_OBJ || type == SPACE) return GEN_NOTHING;
+    if constexpr (G == PG_GAME_CHASER) {
+        if (type == CH_ORB) return 63;
+        if (type == 63) return -1;
+    }
+    return (type >= 0 && type < 64) ? type : -1;
+}
+
+// fillRect(QRectF) edges of one axis (fill_setup), clipped to the frame
+DEV bool fill_axis(double x, double w, Axis &a) {
+    int x1 = qRound(x), x2 = qRound(x + w);
+    if (x2 < x1) { int t = x1; x1 = x2; x2 = t; }
+    x1 = max(x1, 0); x2 = min(x2, PG_RES);
+    a.t1 = x1; a.n = x2 - x1; a.base = 0; a.step = 0;
+    return x1 < x2;
+}
+// one axis of a class: kind 1 = Qt scale blit of an image of `isz` px, 2 = fillRect of the tile rect
+// (monochrome draw_grid_obj), 3 = chaser's orb fillRect (chaser.cpp:111-117 via grid_obj_fill)
+DEV bool class_axis(int kind, int isz, double r, double rw, Axis &a) {
+    a.t1 = a.n = 0; a.base = 0; a.step = 0;
+    if (kind == 1) return axis_setup(r, rw, isz, a);
+    if (kind == 2) return fill_axis(r, rw, a);
+    if (kind == 3) {
+        const float dim = 0.3f, k = 1 - dim;
+        return fill_axis(r + rw * k / 2, rw * dim, a);
+    }
+    return false;
+}
+
+struct GenLane {
+    int cx0, cx1, ncx; // lane = screen column: covering window columns (relative to low_x)
+    int ry0, ry1, ncy; // lane = screen row: covering window rows (relative to low_y)
+};
+
+// Builds the class tables (scratch in `tmp`, >= 2 * GEN_K * 64 int4, dead afterwards) and the
+// per-lane coverage (wave-uniform result): 0 = the frame is not expressible, 1 = draw it with
+// gen_draw, 2 = the window holds no drawn tile (nothing to draw).
+template <int G>
+DEV int gen_setup(const PGDev &d, const PGEnv &s, const View &v, const int16_t *Gd, int player_img, int low_x,
+                   int low_y, int ww, int wh, int xg, int yg, uint8_t *aux, int4 *tmp, GenLane &gl) {
+    const int lane = LANE;
+    int2 *ti = reinterpret_cast<int2 *>(aux);
+    uint8_t *gw = aux + GEN_TI_BYTES;
+    int16_t *xs0 = reinterpret_cast<int16_t *>(aux + GEN_TI_BYTES + GEN_GW);
+    int16_t *xs1 = xs0 + GEN_K * 64, *ys0 = xs1 + GEN_K * 64, *ys1 = ys0 + GEN_K * 64;
+    int4 *xt = tmp, *yt = tmp + GEN_K * 64;
+    if (ww > 63 || wh > 63 || ww * wh > GEN_GW) return 0;
+    // ---- typeinfo (lane = slot): what draw_foreground does with this grid value
+    int kind = 0, off = 0, iw = 0, ih = 0;
+    {
+        const int t = gen_slot_type<G>(lane);
+        const int img = image_for_type<G>(s, t, player_img);
+        if (img >= 0) {
+            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) { // draw_grid_obj (:924-928)
+                if (img != SPACE) {
+                    if (G == PG_GAME_CHASER && img == CH_ORB) {
+                        kind = 3; off = (int)0xff00ff00u;
+                    } else if (s.opt_use_monochrome_assets) {
+                        const uint32_t col = color_for_type<G>(s, img, grid_theme<G>(s, t));
+                        if (col == 0) kind = GEN_BAD;
+                        else { kind = 2; off = (int)(col | 0xff000000u); }
+                    } else {
+                        kind = GEN_BAD;
+                    }
+                }
+            } else {
+                const int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
+                const int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                if (sp.y > 0) { kind = 1; off = sp.x; iw = sp.y; ih = sp.z; }
+                else if (!missing_image_ok<G>(img)) kind = GEN_BAD;
+            }
+        }
+    }
+    // ---- window grid -> slot (u8), and which slots the window holds; a cell this path cannot
+    //      draw sends the frame to the generic pass
+    bool bad = false;
+    unsigned long long present = 0;
+    for (int c = lane; c < ww * wh; c += 64) {
+        const int x = low_x + c % ww, y = low_y + c / ww;
+        const int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                   : s.out_of_bounds_object;
+        int sl = gen_slot<G>(type);
+        if (sl < 0) { bad = true; sl = GEN_NOTHING; }
+        if (sl < 64) present |= 1ull << sl;
+        gw[c] = (uint8_t)sl;
+    }
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const uint32_t lo = (uint32_t)present, hi = (uint32_t)(present >> 32);
+        present |= (unsigned long long)(uint32_t)__shfl_xor((int)lo, sh) | ((unsigned long long)(uint32_t)__shfl_xor((int)hi, sh) << 32);
+    }
+    const bool here = (present >> lane) & 1;
+    if (here && kind == GEN_BAD) bad = true;
+    if (ballot(bad)) return 0;
+    // ---- classes: one per distinct (kind, w, h) among the slots the window holds
+    const bool drawn = here && kind >= 1 && kind <= 3;
+    const int key = kind == 1 ? (iw | (ih << 12) | (1 << 24)) : (kind << 24);
+    unsigned long long pend = ballot(drawn);
+    int cls = 0, K = 0;
+    int ck[GEN_K], cw[GEN_K], chh[GEN_K];
+#pragma unroll
+    for (int k = 0; k < GEN_K; k++) ck[k] = cw[k] = chh[k] = 0;
+    while (pend) {
+        const int f = __ffsll((long long)pend) - 1;
+        const int kf = readlane(key, f);
+        const unsigned long long mem = ballot(drawn && key == kf);
+        if (K < GEN_K) {
+            if (drawn && key == kf) cls = K;
+#pragma unroll
+            for (int k = 0; k < GEN_K; k++)
+                if (k == K) { ck[k] = readlane(kind, f); cw[k] = readlane(iw, f); chh[k] = readlane(ih, f); }
+        }
+        K++;
+        pend &= ~mem;
+    }
+    if (K > GEN_K) return 0;
+    if (K == 0) return 2;
+    ti[lane] = drawn ? make_int2(off, iw | (cls << 16) | (kind << 24)) : make_int2(0, 0);
+    if (lane == 0) ti[GEN_NOTHING] = make_int2(0, 0);
+    // ---- per class: the blit / fill setup of window column `lane` and window row `lane`
+    {
+        double rx = 0, rw = 0, ry = 0, rh = 0, t0, t1;
+        if (lane < ww) screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, t0, rw, t1);
+        if (lane < wh) screen_rect(v, 0.0f, (float)(low_y + lane + 1), 1, 1, RENDER_EPS, t0, ry, t1, rh);
+#pragma unroll
+        for (int k = 0; k < GEN_K; k++) {
+            if (k >= K) break;
+            Axis a, b;
+            const bool okx = lane < ww && class_axis(ck[k], cw[k], rx, rw, a);
+            const bool oky = lane < wh && class_axis(ck[k], chh[k], ry, rh, b);
+            xt[k * 64 + lane] = make_int4(a.t1, okx ? a.n : 0, (int)a.base, a.step);
+            yt[k * 64 + lane] = make_int4(b.t1, oky ? b.n : 0, (int)b.base, b.step);
+        }
+    }
+    wave_sync();
+    // ---- coverage: lane = screen column (columns), lane = screen row (rows); <= 2 each
+    gl.cx0 = gl.cx1 = gl.ry0 = gl.ry1 = -1;
+    gl.ncx = gl.ncy = 0;
+    for (int x = xg - 2; x <= xg + 2; x++) {
+        const int i = x - low_x;
+        if (i < 0 || i >= ww) continue;
+        bool cov = false;
+        for (int k = 0; k < K; k++) {
+            const int4 t = xt[k * 64 + i];
+            cov |= t.y > 0 && lane >= t.x && lane < t.x + t.y;
+        }
+        if (cov) {
+            if (gl.ncx == 0) gl.cx0 = i; else if (gl.ncx == 1) gl.cx1 = i; else bad = true;
+            gl.ncx++;
+        }
+    }
+    for (int y = yg - 2; y <= yg + 2; y++) {
+        const int j = y - low_y;
+        if (j < 0 || j >= wh) continue;
+        bool cov = false;
+        for (int k = 0; k < K; k++) {
+            const int4 t = yt[k * 64 + j];
+            cov |= t.y > 0 && lane >= t.x && lane < t.x + t.y;
+        }
+        if (cov) {
+            if (gl.ncy == 0) gl.ry0 = j; else if (gl.ncy == 1) gl.ry1 = j; else bad = true;
+            gl.ncy++;
+        }
+    }
+    if (ballot(bad)) return 0;
+    // ---- per class: source column of this lane's covering columns, source row of this row's
+    for (int k = 0; k < K; k++) {
+        int v0 = -1, v1 = -1, w0 = -1, w1 = -1;
+        if (gl.ncx > 0) {
+            const int4 t = xt[k * 64 + gl.cx0];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) v0 = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+        }
+        if (gl.ncx > 1) {
+            const int4 t = xt[k * 64 + gl.cx1];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) v1 = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+        }
+        if (gl.ncy > 0) {
+            const int4 t = yt[k * 64 + gl.ry0];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) w0 = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+        }
+        if (gl.ncy > 1) {
+            const int4 t = yt[k * 64 + gl.ry1];
+            if (t.y > 0 && lane >= t.x && lane < t.x + t.y) w1 = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
+        }
+        xs0[k * 64 + lane] = (int16_t)v0; xs1[k * 64 + lane] = (int16_t)v1;
+        ys0[k * 64 + lane] = (int16_t)w0; ys1[k * 64 + lane] = (int16_t)w1;
+    }
+    wave_sync();
+    return 1;
+}
+
+// texel of window cell `cell` at source column table `xs` (per class, this lane) / row `sr` table
+DEV uint32_t gen_texel(const PGDev &d, const int2 t, int sc, int sr, bool &err) {
+    const int kind = t.y >> 24;
+    if (kind == 0 || sc < 0 || sr < 0) return 0u;
+    if (kind != 1) return (uint32_t)t.x;
+    const uint32_t idx = (uint32_t)t.x + (uint32_t)(sr * (t.y & 0xffff) + sc);
+    if (idx >= d.num_pixels) { err = true; return 0u; }
+    return d.pixels[idx];
+}
+
+// Row pass (first covering tile column) + second-column pass.  FUSE: the background texel of the
+// pixel (bg_col / bg_base / bgrow as in the fast path) is the destination; else the frame buffer.
+template <bool FUSE>
+DEV void gen_draw(uint32_t *fb, const PGDev &d, const uint8_t *aux, const GenLane &gl, int ww, bool bg_col,
+                  uint32_t bg_base, int bgrow, bool &err) {
+    const int lane = LANE;
+    const int2 *ti = reinterpret_cast<const int2 *>(aux);
+    const uint8_t *gw = aux + GEN_TI_BYTES;
+    const int16_t *xs0 = reinterpret_cast<const int16_t *>(aux + GEN_TI_BYTES + GEN_GW);
+    const int16_t *xs1 = xs0 + GEN_K * 64, *ys0 = xs1 + GEN_K * 64, *ys1 = ys0 + GEN_K * 64;
+    // per screen row (lane = row): its covering window rows, packed for one readlane per row
+    const int rinfo = gl.ncy == 0 ? 0 : (gl.ry0 | ((gl.ncy > 1 ? gl.ry1 : 0) << 8) | (gl.ncy << 16));
+    const int cxo = gl.ncx > 0 ? gl.cx0 : -1;
+    for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+        int info[RB], s0[RB], s1[RB];
+        int2 t0[RB], t1[RB];
+        uint32_t dst[RB], ta[RB], tb[RB];
+#pragma unroll
+        for (int k = 0; k < RB; k++) {
+            info[k] = readlane(rinfo, r0 + k);
+            const int ny = info[k] >> 16;
+            s0[k] = (ny > 0 && cxo >= 0) ? gw[(info[k] & 255) * ww + cxo] : GEN_NOTHING;
+            s1[k] = (ny > 1 && cxo >= 0) ? gw[((info[k] >> 8) & 255) * ww + cxo] : GEN_NOTHING;
+        }
+#pragma unroll
+        for (int k = 0; k < RB; k++) {
+            t0[k] = ti[s0[k]];
+            t1[k] = ti[s1[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < RB; k++) {
+            const int c0 = (t0[k].y >> 16) & 255, c1 = (t1[k].y >> 16) & 255;
+            ta[k] = gen_texel(d, t0[k], xs0[c0 * 64 + lane], ys0[c0 * 64 + r0 + k], err);
+            tb[k] = gen_texel(d, t1[k], xs0[c1 * 64 + lane], ys1[c1 * 64 + r0 + k], err);
+        }
+        if constexpr (FUSE) {
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int br = readlane(bgrow, r0 + k);
+                const bool inb = bg_col && br >= 0;
+                const uint32_t px = d.pixels[inb ? bg_base + (uint32_t)br : 0u];
+                dst[k] = inb ? px : 0xff000000u;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < RB; k++) dst[k] = fb[(r0 + k) * PG_RES + lane];
+        }
+        uint32_t part = 0;
+#pragma unroll
+        for (int k = 0; k < RB; k++) part |= alpha_partial(ta[k]) | alpha_partial(tb[k]);
+        if (!ballot(part != 0)) {
+#pragma unroll
+            for (int k = 0; k < RB; k++) fb[(r0 + k) * PG_RES + lane] = over_binary(over_binary(dst[k], ta[k]), tb[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                uint32_t px = dst[k];
+                px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
+                px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
+                fb[(r0 + k) * PG_RES + lane] = px;
+            }
+        }
+    }
+    wave_sync();
+    // second covering tile column of the screen columns two tiles overlap; lane = screen row
+    unsigned long long m2 = ballot(gl.ncx > 1);
+    while (m2) {
+        const int c = __ffsll((long long)m2) - 1;
+        m2 &= m2 - 1;
+        const int x1 = readlane(gl.cx1, c);
+        const int row = lane;
+        if (gl.ncy > 0) {
+            uint32_t px = fb[row * PG_RES + c];
+            for (int l = 0; l < gl.ncy; l++) {
+                const int2 t = ti[gw[(l ? gl.ry1 : gl.ry0) * ww + x1]];
+                const int cl = (t.y >> 16) & 255;
+                const uint32_t tv = gen_texel(d, t, xs1[cl * 64 + c], (l ? ys1 : ys0)[cl * 64 + row], err);
+                px = tv + BYTE_MUL(px, (~tv) >> 24);
+            }
+            fb[row * PG_RES + c] = px;
+        }
     }
 }
 
@@ -820,12 +1254,17 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
     // <= -2 not drawable on the fast path
     constexpr int CR = crows<G>();
-    __shared__ int tile_off[NTYPES];
-    // fast path: texel base of lane's first tile column per tile row.  Before it is built, the
-    // same LDS holds the Qt blit setup (t1, n, base, step) of every window tile column / row
-    // (class 0 at [0, 128), class 1 at [128, 256) in int4 units).
-    __shared__ __attribute__((aligned(16))) int colb[CR * 64];
+    // aux LDS, fast path: tile_off[NTYPES] | colb[CR * 64] -- colb: texel base of lane's first tile
+    // column per tile row; before it is built, the same LDS holds the Qt blit setup (t1, n, base,
+    // step) of every window tile column / row (class 0 at [0, 128), class 1 at [128, 256) in int4
+    // units).  General tile pass (decided after the fast path): GEN_AUX_BYTES of tables.
+    constexpr int FAST_BYTES = (NTYPES + CR * 64) * 4;
+    constexpr int AUX_BYTES = has_general<G>() && GEN_AUX_BYTES > FAST_BYTES ? GEN_AUX_BYTES : FAST_BYTES;
+    __shared__ __attribute__((aligned(16))) uint8_t aux[AUX_BYTES];
+    int *const tile_off = reinterpret_cast<int *>(aux);
+    int *const colb = tile_off + NTYPES;
     static_assert(CR * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
+    static_assert(AUX_BYTES >= ROT_DESC_CAP * 128, "aux holds the rotated-image descriptors");
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
@@ -1119,6 +1558,18 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
     }
     wave_sync();
+    // general tile pass for the frames the fast path does not take (class tables built in fb's LDS,
+    // which is dead until the background pass)
+    GenLane gl;
+    gl.cx0 = gl.cx1 = gl.ry0 = gl.ry1 = -1;
+    gl.ncx = gl.ncy = 0;
+    bool gen = false, notiles = false;
+    if constexpr (has_general<G>())
+        if (!fast && tab) {
+            const int gs = gen_setup<G>(d, s, v, Gd, player_img, low_x, low_y, ww, wh, xg, yg, aux, reinterpret_cast<int4 *>(fb), gl);
+            gen = gs == 1;
+            notiles = gs == 2;
+        }
 
     pt.mark(0);
     if (fast) {
@@ -1160,13 +1611,22 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 if (nr > 0 && ca[k] >= 0) ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((info[k] & 127) * tile_px<G>())];
                 if (nr > 1 && cbv[k] >= 0) tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((info[k] >> 7) & 127) * tile_px<G>())];
             }
+            // a missing tile texel is 0, which blends to the unchanged pixel on either path
+            uint32_t part = 0;
 #pragma unroll
-            for (int k = 0; k < RB; k++) {
-                const int nr = info[k] >> 24;
-                uint32_t px = bgv[k];
-                if (nr > 0) px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
-                if (nr > 1) px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
-                fb[(r0 + k) * PG_RES + lane] = px;
+            for (int k = 0; k < RB; k++) part |= alpha_partial(ta[k]) | alpha_partial(tb[k]);
+            if (!ballot(part != 0)) {
+#pragma unroll
+                for (int k = 0; k < RB; k++) fb[(r0 + k) * PG_RES + lane] = over_binary(over_binary(bgv[k], ta[k]), tb[k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < RB; k++) {
+                    const int nr = info[k] >> 24;
+                    uint32_t px = bgv[k];
+                    if (nr > 0) px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
+                    if (nr > 1) px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
+                    fb[(r0 + k) * PG_RES + lane] = px;
+                }
             }
         }
         wave_sync();
@@ -1192,6 +1652,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 fb[row * PG_RES + c] = px;
             }
         }
+    } else if (gen && !has_z_minus1<G>()) {
+        gen_draw<true>(fb, d, aux, gl, ww, bg_col, bg_col_base, bg_lane_row, err);
     } else {
         // ---- background alone (lane = column), RB rows per batch
         const int bgrow = bg_lane_row;
@@ -1221,10 +1683,13 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
 #define PG_DRAW_ENTITIES(Z)                                                                   \
     for (int base = 0; base < n; base += 64) {                                                \
         pt.mark(4);                                                                           \
-        if (!one_chunk || !ent_setup_valid) entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err); \
+        if (!one_chunk || !ent_setup_valid) {                                                 \
+            entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);               \
+            if (!has_z_minus1<G>()) rot_stage(im, aux);                                       \
+        }                                                                                     \
         ent_setup_valid = true;                                                               \
         pt.mark(3);                                                                           \
-        stamp_images(fb, d, im, ballot(im.draw && im.ez == (Z)), err);                        \
+        stamp_images(fb, d, aux, im, ballot(im.draw && im.ez == (Z)), err);                   \
     }
 
     if (!fast) {
@@ -1234,7 +1699,13 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         if (has_z_minus1<G>()) {
             PG_DRAW_ENTITIES(-1)
         }
-        if (has_grid_tiles<G>()) {
+        if (notiles) {
+        } else if (gen) {
+            if constexpr (has_z_minus1<G>()) {
+                wave_sync();
+                gen_draw<false>(fb, d, aux, gl, ww, false, 0u, -1, err);
+            }
+        } else if (has_grid_tiles<G>()) {
             const int ntiles = ww * wh;
             for (int base = 0; base < ntiles; base += 64) {
                 const int k = base + lane;
@@ -1270,7 +1741,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                         }
                     }
                 }
-                stamp_images(fb, d, im, ballot(im.draw), err);
+                stamp_images(fb, d, aux, im, ballot(im.draw), err);
             }
         }
     } else if (has_z_minus1<G>()) {

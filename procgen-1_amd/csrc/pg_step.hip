@@ -20,6 +20,8 @@ struct Ctx {
     int16_t *ilist; // LDS: ascending indices of entities that can interact in sub_step
     int nlist;
     int16_t *slist; // LDS: smart entity indices (fast step_entities path)
+    float4 *ibox;   // LDS: static interactors' (x, y, rx, ry) for the lane-parallel smart steps
+    int *iinfo;     // LDS: static interactors' index | will_erase << 31
     int8_t *grid8;  // LDS copy of the grid
     uint8_t *moved; // LDS has_moved map (miner)
     bool grid8_ok;
@@ -84,8 +86,9 @@ DEV void entity_step(Ent &e) {
 
 // Entity::step of one slot in place (lane-parallel form): reads the fields the update
 // depends on and writes back only the words whose bits changed.
-DEV void entity_step_slot(Ctx &c, int i) {
+DEV void entity_step_slot(Ctx &c, int i, bool skip_smart = false) {
     int flags = EI(c, F_FLAGS, i);
+    if (skip_smart && (flags & EF_SMART_STEP)) return; // stepped from registers by the caller
     float x = EF(c, F_X, i), y = EF(c, F_Y, i), vx = EF(c, F_VX, i), vy = EF(c, F_VY, i);
     float rx = EF(c, F_RX, i), ry = EF(c, F_RY, i), rot = EF(c, F_ROTATION, i), vrot = EF(c, F_VROT, i);
     float fr = EF(c, F_FRICTION, i), alpha = EF(c, F_ALPHA, i), decay = EF(c, F_ALPHA_DECAY, i);
@@ -298,6 +301,22 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
     return -1;
 }
 
+// next_collider for a lane stepping its own entity (lane-parallel smart steps): the static
+// interactors are read from LDS, the ascending list's last hit is the largest index.
+DEV int next_collider_pl(Ctx &c, int oi, int upper, const Ent &o) {
+    int best = -1;
+    for (int k = 0; k < c.nlist; k++) {
+        const int inf = c.iinfo[k];
+        const int i = inf & 0x7fffffff;
+        if (inf < 0 || i >= upper || i == oi) continue;
+        const float4 b = c.ibox[k];
+        float tx = (o.rx + b.z) + POS_EPS;
+        float ty = (o.ry + b.w) + POS_EPS;
+        if ((fabsf(o.x - b.x) < tx) && (fabsf(o.y - b.y) < ty)) best = i;
+    }
+    return best;
+}
+
 template <int G>
 DEV void build_interactor_list(Ctx &c) {
     int cnt = 0;
@@ -330,16 +349,21 @@ DEV void build_interactor_list(Ctx &c) {
                    EF(c, F_GROW_RATE, i) == 1 && EI(c, F_EXPIRE_TIME, i) <= 0;
         }
         c.ireg = ballot(!stat) == 0;
+        if (LANE < cnt) {
+            c.ibox[LANE] = make_float4(c.i_x, c.i_y, c.i_rx, c.i_ry);
+            c.iinfo[LANE] = c.i_idx | (c.i_erase ? (int)0x80000000u : 0);
+        }
+        wave_sync();
     }
 }
 
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
 
-template <int G, int D>
+template <int G, int D, bool PL>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy);
 
 // basic-abstract-game.cpp:248-276 (target is always the stepped object)
-template <int G, int D>
+template <int G, int D, bool PL>
 DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
     float sx = EF(c, F_X, src), sy = EF(c, F_Y, src);
     float rsum = is_h ? (EF(c, F_RX, src) + o.rx) : (EF(c, F_RY, src) + o.ry);
@@ -348,13 +372,13 @@ DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
     float t_vx = 0, t_vy = 0;
     if (is_h) t_vx = (float)((double)sx + dsign(delx) * (double)rsum - (double)o.x);
     else t_vy = (float)((double)sy + dsign(dely) * (double)rsum - (double)o.y);
-    if constexpr (D < 5) (void)sub_step<G, D + 1>(c, oi, o, t_vx, t_vy);
+    if constexpr (D < 5) (void)sub_step<G, D + 1, PL>(c, oi, o, t_vx, t_vy);
     if (is_h) o.vx = 0;
     else o.vy = 0;
 }
 
-// basic-abstract-game.cpp:278-380
-template <int G, int D>
+// basic-abstract-game.cpp:278-380.  PL: every lane steps its own entity (no cross-lane operation).
+template <int G, int D, bool PL>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
     if (o.flags & EF_WILL_ERASE) return false;
     float ny = o.y + _vy;
@@ -401,7 +425,7 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
     bool block2 = false;
     int upper = c.s.num_ents;
     while (scan_needed<G>(is_h)) {
-        int m = next_collider(c, oi, upper, o);
+        int m = PL ? next_collider_pl(c, oi, upper, o) : next_collider(c, oi, upper, o);
         if (m < 0) break;
         upper = m;
         int mtype = EI(c, F_TYPE, m);
@@ -422,14 +446,14 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 o.vy = -1 * o.vy;
             }
         }
-        if (curr_block) push_obj<G, D>(c, m, oi, o, is_h);
+        if (curr_block) push_obj<G, D, PL>(c, m, oi, o, is_h);
         block2 = block2 || curr_block;
     }
     return block || block2;
 }
 
 // basic-abstract-game.cpp:602-665
-template <int G>
+template <int G, bool PL = false>
 DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     if (o.flags & EF_WILL_ERASE) return;
     int num_sub_steps;
@@ -450,11 +474,11 @@ DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     for (int s = 0; s < num_sub_steps; s++) {
         bool block_x, block_y;
         if (step_x_first) {
-            block_x = sub_step<G, 0>(c, oi, o, o.vx * pct, 0);
-            block_y = sub_step<G, 0>(c, oi, o, 0, o.vy * pct);
+            block_x = sub_step<G, 0, PL>(c, oi, o, o.vx * pct, 0);
+            block_y = sub_step<G, 0, PL>(c, oi, o, 0, o.vy * pct);
         } else {
-            block_y = sub_step<G, 0>(c, oi, o, 0, o.vy * pct);
-            block_x = sub_step<G, 0>(c, oi, o, o.vx * pct, 0);
+            block_y = sub_step<G, 0, PL>(c, oi, o, 0, o.vy * pct);
+            block_x = sub_step<G, 0, PL>(c, oi, o, o.vx * pct, 0);
         }
         if (!block_x) vx_pct += 1;
         if (!block_y) vy_pct += 1;
@@ -489,6 +513,11 @@ DEV void ent_readlane(const Ent &m, int l, Ent &o) {
 // be loaded lane-parallel up front (lane k <-> k-th smart entity), stepped from registers
 // in the reference's reverse order, and stored lane-parallel at the end.
 template <int G>
+DEV constexpr bool pl_smart() {
+    return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER;
+}
+
+template <int G>
 DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
     int n = c.s.num_ents;
     int nsm = 0;
@@ -505,23 +534,45 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
     Ent mine;
     int my_i = LANE < nsm ? slist[LANE] : 0;
     if (LANE < nsm) load_ent(c, my_i, mine);
-    int hi = n - 1;
-    for (int j = nsm - 1; j >= 0; j--) {
-        int sm = rli(my_i, j);
-        for (int base = (sm + 1) & ~63; base <= hi; base += 64) {
-            int i = base + LANE;
-            if (i > sm && i <= hi) entity_step_slot(c, i);
-        }
-        Ent o;
-        ent_readlane(mine, j, o);
-        basic_step_object<G>(c, sm, o);
-        entity_step(o);
-        if (LANE == j) mine = o;
-        hi = sm - 1;
-    }
-    for (int base = 0; base <= hi; base += 64) {
+    // The non-smart entities' Entity::step touches only their own slots and no smart step reads
+    // them (the only entities a smart step reads are the static interactors, whose Entity::step
+    // leaves x, y, rx, ry and will_erase as they are, and the agent, itself smart), so they are
+    // stepped in one lane-parallel pass -- one round of loads for the whole list instead of one
+    // per run between two smart entities of the reverse loop.
+    for (int base = 0; base < n; base += 64) {
         int i = base + LANE;
-        if (i <= hi) entity_step_slot(c, i);
+        if (i < n) entity_step_slot(c, i, true);
+    }
+    // The smart entities' steps are independent of each other as well: a smart step writes only
+    // its own entity and reads the grid, the static interactors and the agent (slot 0, stepped
+    // last by the reverse loop, so every other smart step sees its pre-step state, which is what
+    // HBM holds until the store below).  All but the agent step at once, lane k <-> smart entity k;
+    // the one shared write, coinrun's is_on_crate = 1 (is_blocked_ents), is OR-ed back.
+    // Measured per game (profiles/r02): a win where several smart entities take many sub-steps
+    // (chaser, climber, ninja, caveflyer); coinrun's step ran 2x slower this way, so the others
+    // keep the in-order loop.
+    if constexpr (pl_smart<G>()) {
+        if (LANE < nsm && my_i != 0) {
+            basic_step_object<G, true>(c, my_i, mine);
+            entity_step(mine);
+        }
+        if constexpr (G == PG_GAME_COINRUN) c.s.is_on_crate = ballot(c.s.is_on_crate != 0) ? 1 : 0;
+    } else {
+        const int jlo = (nsm > 0 && rli(my_i, 0) == 0) ? 1 : 0; // the agent goes last, below
+        for (int j = nsm - 1; j >= jlo; j--) {
+            Ent o;
+            ent_readlane(mine, j, o);
+            basic_step_object<G>(c, rli(my_i, j), o);
+            entity_step(o);
+            if (LANE == j) mine = o;
+        }
+    }
+    if (nsm > 0 && rli(my_i, 0) == 0) { // slist is ascending: the agent is smart entity 0
+        Ent o;
+        ent_readlane(mine, 0, o);
+        basic_step_object<G>(c, 0, o);
+        entity_step(o);
+        if (LANE == 0) mine = o;
     }
     if (LANE < nsm) store_ent(c, my_i, mine);
     wave_sync();
@@ -2618,6 +2669,8 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
+    __shared__ float4 lds_ibox[64];
+    __shared__ int lds_iinfo[64];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
     Ctx c;
@@ -2632,6 +2685,8 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     c.lds = lds_mt;
     c.ilist = lds_list;
     c.slist = lds_slist;
+    c.ibox = lds_ibox;
+    c.iinfo = lds_iinfo;
     c.nlist = 0;
     c.grid8 = lds_grid;
     c.grid8_ok = false;
