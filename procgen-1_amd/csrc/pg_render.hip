@@ -617,44 +617,105 @@ DEV void blit_seq(uint32_t *fb, const PGDev &d, const Axis &ex, const Axis &ey, 
 // Transform blit of image descriptor `rd` (rot_stage): lanes = pixels of its bounding box, each
 // finds its scan line's trapezoid -- the pixels qt_transform_image's row loop would touch, in any
 // order, since one image's pixels are distinct.
+// Descriptor (6 int4 = 96 B): a0..a2 = trapezoid k's (x_l, dx_l, x_r, dx_r), a3 = (dudx, dvdx, dudy,
+// dvdy), a4 = (u0, v0, soff, iw | ih << 16), a5 = (from0 | to0 << 8 | from1 << 16 | to1 << 24,
+// from2 | to2 << 8 | mir << 16, ca | xmin << 16, nx | ymin << 8 | ny << 16)
+#define ROT_DESC_BYTES 96
+struct RotD { int4 a0, a1, a2, a3, a4, a5; };
+DEV RotD rot_desc(const uint8_t *aux, int rd) {
+    const int4 *D = reinterpret_cast<const int4 *>(aux) + 6 * rd;
+    RotD r;
+    r.a0 = D[0]; r.a1 = D[1]; r.a2 = D[2]; r.a3 = D[3]; r.a4 = D[4]; r.a5 = D[5];
+    return r;
+}
+DEV int rot_nx(const RotD &r) { return r.a5.w & 255; }
+DEV int rot_total(const RotD &r) { return (r.a5.w & 255) * ((r.a5.w >> 16) & 255); }
+// pixel p of the bounding box (inv = 1 / nx): frame offset `o`, texel index, drawn or not
+DEV bool rot_pixel(const RotD &r, int p, float inv, int &o, uint32_t &idx) {
+    const int xmin = r.a5.z >> 16, nx = r.a5.w & 255, ymin = (r.a5.w >> 8) & 255;
+    const int py = (int)(((float)p + 0.5f) * inv);
+    const int yy = ymin + py;
+    const int x = xmin + (p - py * nx);
+    const int f0 = r.a5.x & 255, t0 = (r.a5.x >> 8) & 255, f1 = (r.a5.x >> 16) & 255, t1 = (r.a5.x >> 24) & 255;
+    const int f2 = r.a5.y & 255, t2 = (r.a5.y >> 8) & 255;
+    int from;
+    int4 e;
+    bool in = true;
+    if (yy >= f0 && yy < t0) { from = f0; e = r.a0; }
+    else if (yy >= f1 && yy < t1) { from = f1; e = r.a1; }
+    else if (yy >= f2 && yy < t2) { from = f2; e = r.a2; }
+    else { from = 0; e = make_int4(0, 0, 0, 0); in = false; }
+    const int xlv = e.x + (yy - from) * e.y, xrv = e.z + (yy - from) * e.w;
+    const int fromX = max(xlv >> 16, 0), toX = min(xrv >> 16, PG_RES);
+    const int iw = r.a4.w & 0xffff, ih = r.a4.w >> 16;
+    int uu = (x * r.a3.x + yy * r.a3.z + r.a4.x) >> 16;
+    int vv = (x * r.a3.y + yy * r.a3.w + r.a4.y) >> 16;
+    uu = min(max(uu, 0), iw - 1);
+    vv = min(max(vv, 0), ih - 1);
+    if ((r.a5.y >> 16) & 1) uu = iw - 1 - uu;
+    idx = (uint32_t)r.a4.z + (uint32_t)(vv * iw + uu);
+    o = yy * PG_RES + x;
+    return in && x >= fromX && x < toX;
+}
 DEV void rot_stamp_lds(uint32_t *fb, const PGDev &d, const uint8_t *aux, int rd, bool &err) {
-    const int4 *D = reinterpret_cast<const int4 *>(aux) + 8 * rd;
-    const int4 a0 = D[0], a1 = D[1], a2 = D[2], a3 = D[3], a4 = D[4], a5 = D[5], a6 = D[6], a7 = D[7];
-    // a0 = tr0 (from, to, x_l, dx_l), a1 = (tr0 x_r, dx_r, tr1 from, to), a2 = tr1 (x_l, dx_l, x_r, dx_r),
-    // a3 = tr2 (from, to, x_l, dx_l), a4 = (tr2 x_r, dx_r, dudx, dvdx), a5 = (dudy, dvdy, u0, v0),
-    // a6 = (soff, iw, ih, mir), a7 = (ca, xmin, nx, ymin | ny << 16)
-    const int xmin = a7.y, nx = a7.z, ymin = a7.w & 0xffff, ny = a7.w >> 16;
-    const int total = nx * ny;
+    const RotD r = rot_desc(aux, rd);
+    const int total = rot_total(r);
     if (total <= 0) return;
-    const float inv = 1.0f / (float)nx;
-    const uint32_t npix = d.num_pixels;
+    const float inv = 1.0f / (float)rot_nx(r);
     for (int p = LANE; p < total; p += 64) {
-        const int yy = ymin + (int)(((float)(p - 0) + 0.5f) * inv);
-        const int x = xmin + (p - (yy - ymin) * nx);
-        int from, xl, dxl, xr, dxr;
-        bool in;
-        if (yy >= a0.x && yy < a0.y) { from = a0.x; xl = a0.z; dxl = a0.w; xr = a1.x; dxr = a1.y; in = true; }
-        else if (yy >= a1.z && yy < a1.w) { from = a1.z; xl = a2.x; dxl = a2.y; xr = a2.z; dxr = a2.w; in = true; }
-        else if (yy >= a3.x && yy < a3.y) { from = a3.x; xl = a3.z; dxl = a3.w; xr = a4.x; dxr = a4.y; in = true; }
-        else { from = 0; xl = dxl = xr = dxr = 0; in = false; }
-        const int xlv = xl + (yy - from) * dxl, xrv = xr + (yy - from) * dxr;
-        const int fromX = max(xlv >> 16, 0), toX = min(xrv >> 16, PG_RES);
-        bool on = in && x >= fromX && x < toX;
-        int uu = (x * a4.z + yy * a5.x + a5.z) >> 16;
-        int vv = (x * a4.w + yy * a5.y + a5.w) >> 16;
-        uu = min(max(uu, 0), a6.y - 1);
-        vv = min(max(vv, 0), a6.z - 1);
-        if (a6.w) uu = a6.y - 1 - uu;
-        const uint32_t idx = (uint32_t)a6.x + (uint32_t)(vv * a6.y + uu);
-        if (on && idx >= npix) {
+        int o;
+        uint32_t idx;
+        bool on = rot_pixel(r, p, inv, o, idx);
+        if (on && idx >= d.num_pixels) {
             err = true;
             on = false;
         }
         const uint32_t tv = d.pixels[on ? idx : 0u];
-        if (on) fb[yy * PG_RES + x] = blend_argb_pm(fb[yy * PG_RES + x], tv, a7.x);
+        if (on) fb[o] = blend_argb_pm(fb[o], tv, r.a5.z & 0xffff);
     }
 }
 
+template <bool TILES>
+DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
+
+// tile_image (basic-abstract-game.cpp:849-877) of image j: the tiles (left to right / top to
+// bottom) become lanes of a plain-image list, set up lane-parallel and stamped in order.
+DEV void stamp_tiles(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, int caj, bool &err) {
+    const int ntile = readlane(im.ntile, j);
+    const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
+    const float tw = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j));
+    const float th = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.th), j));
+    const int vert = readlane(im.rslot, j); // 1: vertical tiling (negative ratio)
+    const int offj = readlane(im.soff, j);
+    const int swj = readlane(im.sw, j), shj = readlane(im.sh, j), mirj = readlane(im.mir, j);
+    // tiles that can reach the frame (2 px margin; axis_setup culls exactly)
+    const double tsz = vert ? (double)th : (double)tw, org = vert ? ry : rx;
+    int tlo = 0, thi = ntile;
+    if (tsz > 0) {
+        tlo = max(0, (int)floor((-2.0 - org) / tsz) - 1);
+        thi = min(ntile, (int)ceil((PG_RES + 2.0 - org) / tsz) + 1);
+    }
+    for (int t0 = tlo; t0 < thi; t0 += 64) {
+        Img ti;
+        img_clear(ti);
+        const int t = t0 + LANE;
+        if (t < thi) {
+            const double x = vert ? rx : rx + (double)(tw * (float)t);
+            const double y = vert ? ry + (double)(th * (float)t) : ry;
+            if (axis_setup(x, (double)tw, swj, ti.ex) && axis_setup(y, (double)th, shj, ti.ey)) {
+                ti.draw = true;
+                ti.soff = offj; ti.sw = swj; ti.sh = shj; ti.mir = mirj; ti.ca = caj;
+            }
+        }
+        stamp_images<false>(fb, d, aux, ti, ballot(ti.draw), err);
+    }
+}
+
+// Images of `m` in ascending lane order.  Per group of EG images, the texel of this lane's pixel of
+// every small one (<= 64 px: plain blits, fills, transform blits with a descriptor) is loaded first
+// (loads are order-free), then the group is blended strictly in order; larger, tiled and
+// set-up-in-order images run their own loops at their turn.
+template <bool TILES>
 DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
     const int lane = LANE;
     const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
@@ -668,16 +729,41 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
         }
         uint32_t tv[EG];
         int fo[EG];
-        bool on[EG];
+        bool on[EG], pre[EG];
+        uint32_t part = 0;
 #pragma unroll
         for (int g = 0; g < EG; g++) {
             on[g] = false;
+            pre[g] = false;
             tv[g] = 0;
             fo[g] = 0;
             const int j = js[g];
-            if (j < 0 || readlane(im.rot || im.ntile > 0 ? 1 : 0, j)) continue;
+            if (j < 0) continue;
+            const int rk = readlane(im.rot, j);
+            if (rk == 1 || readlane(im.ntile, j) > 0) continue;
+            if (rk == 2) {
+                const RotD r = rot_desc(aux, readlane(im.rdi, j));
+                const int total = rot_total(r);
+                if (total > 64) continue;
+                pre[g] = true;
+                if (lane < total) {
+                    int o;
+                    uint32_t idx;
+                    if (rot_pixel(r, lane, 1.0f / (float)rot_nx(r), o, idx)) {
+                        if (idx < npix) {
+                            tv[g] = d.pixels[idx];
+                            fo[g] = o;
+                            on[g] = true;
+                        } else {
+                            err = true;
+                        }
+                    }
+                }
+                continue;
+            }
             const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
             if (nx * ny > 64) continue;
+            pre[g] = true;
             if (lane < nx * ny) {
                 const float inv = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, inv_l), j));
                 const int py = (int)(((float)lane + 0.5f) * inv);
@@ -705,10 +791,17 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
             }
         }
 #pragma unroll
+        for (int g = 0; g < EG; g++) part |= on[g] ? alpha_partial(tv[g]) : 0u;
+        const bool binary = ballot(part != 0) == 0; // every prefetched texel has alpha 0 or 255
+#pragma unroll
         for (int g = 0; g < EG; g++) {
             const int j = js[g];
             if (j < 0) continue;
             const int caj = readlane(im.ca, j);
+            if (pre[g]) {
+                if (on[g]) fb[fo[g]] = (binary && caj == 256) ? over_binary(fb[fo[g]], tv[g]) : blend_argb_pm(fb[fo[g]], tv[g], caj);
+                continue;
+            }
             const int rk = readlane(im.rot, j);
             if (rk == 2) {
                 rot_stamp_lds(fb, d, aux, readlane(im.rdi, j), err);
@@ -723,34 +816,13 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
                     err = true;
                 continue;
             }
-            const int ntile = readlane(im.ntile, j);
-            if (ntile > 0) { // tile_image (basic-abstract-game.cpp:849-877): tiles left to right / top to bottom
-                const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
-                const float tw = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j));
-                const float th = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.th), j));
-                const int vert = readlane(im.rslot, j); // 1: vertical tiling (negative ratio)
-                const uint32_t offj = (uint32_t)readlane(im.soff, j);
-                const int swj = readlane(im.sw, j), shj = readlane(im.sh, j), mirj = readlane(im.mir, j);
-                // tiles that can reach the frame (2 px margin; axis_setup culls exactly)
-                const double tsz = vert ? (double)th : (double)tw, org = vert ? ry : rx;
-                int tlo = 0, thi = ntile;
-                if (tsz > 0) {
-                    tlo = max(0, (int)floor((-2.0 - org) / tsz) - 1);
-                    thi = min(ntile, (int)ceil((PG_RES + 2.0 - org) / tsz) + 1);
-                }
-                for (int t = tlo; t < thi; t++) {
-                    const double x = vert ? rx : rx + (double)(tw * (float)t);
-                    const double y = vert ? ry + (double)(th * (float)t) : ry;
-                    Axis ex, ey;
-                    if (axis_setup(x, (double)tw, swj, ex) && axis_setup(y, (double)th, shj, ey))
-                        blit_seq(fb, d, ex, ey, offj, swj, mirj, caj, err);
-                }
+            if (readlane(im.ntile, j) > 0) {
+                if constexpr (TILES) stamp_tiles(fb, d, aux, im, j, caj, err);
+                else err = true; // unreachable: tile lists hold plain images only
                 continue;
             }
             const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
-            if (nx * ny <= 64) {
-                if (on[g]) fb[fo[g]] = blend_argb_pm(fb[fo[g]], tv[g], caj);
-            } else if (readlane((int)im.fill, j) != 0) {
+            if (readlane((int)im.fill, j) != 0) {
                 const uint32_t col = (uint32_t)readlane((int)im.fill, j);
                 const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
                 for (int p = lane; p < nx * ny; p += 64) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
@@ -890,8 +962,7 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
 // Transform blits of a chunk's rotated images, set up lane-parallel: a TxScale map becomes a plain
 // scale blit, a rotation's trapezoids and texture stepping go to descriptor slot `rank` in the aux
 // LDS (dead once the tiles are drawn); past `cap` descriptors an image keeps the in-order setup.
-#define ROT_DESC_CAP 32
-DEV void rot_stage(Img &im, uint8_t *aux) {
+DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
     const int lane = LANE;
     Axis ex, ey;
     RotGeo g;
@@ -902,7 +973,7 @@ DEV void rot_stage(Img &im, uint8_t *aux) {
     if (cand && kind == 1) { im.rot = 0; im.ex = ex; im.ey = ey; }
     const bool gen = cand && kind == 2;
     const int rank = __popcll(ballot(gen) & ((1ull << lane) - 1));
-    if (gen && rank < ROT_DESC_CAP) {
+    if (gen && rank < cap) {
         int ymin = PG_RES, ymax = 0, xmin = PG_RES, xmax = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
@@ -919,15 +990,19 @@ DEV void rot_stage(Img &im, uint8_t *aux) {
             }
         }
         const int nx = xmax > xmin ? xmax - xmin : 0, ny = ymax > ymin ? ymax - ymin : 0;
-        int4 *D = reinterpret_cast<int4 *>(aux) + 8 * rank;
-        D[0] = make_int4(g.tr[0].from_y, g.tr[0].to_y, g.tr[0].x_l, g.tr[0].dx_l);
-        D[1] = make_int4(g.tr[0].x_r, g.tr[0].dx_r, g.tr[1].from_y, g.tr[1].to_y);
-        D[2] = make_int4(g.tr[1].x_l, g.tr[1].dx_l, g.tr[1].x_r, g.tr[1].dx_r);
-        D[3] = make_int4(g.tr[2].from_y, g.tr[2].to_y, g.tr[2].x_l, g.tr[2].dx_l);
-        D[4] = make_int4(g.tr[2].x_r, g.tr[2].dx_r, g.dudx, g.dvdx);
-        D[5] = make_int4(g.dudy, g.dvdy, g.u0, g.v0);
-        D[6] = make_int4(im.soff, im.sw, im.sh, im.mir);
-        D[7] = make_int4(im.ca, xmin, nx, (ymin & 0xffff) | (ny << 16));
+        // trap_setup clamps from / to to [0, 64]; an empty trapezoid is stored as 0..0
+        int ft[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            ft[k] = g.tr[k].from_y < g.tr[k].to_y ? (g.tr[k].from_y | (g.tr[k].to_y << 8)) : 0;
+        int4 *D = reinterpret_cast<int4 *>(aux) + 6 * rank;
+        D[0] = make_int4(g.tr[0].x_l, g.tr[0].dx_l, g.tr[0].x_r, g.tr[0].dx_r);
+        D[1] = make_int4(g.tr[1].x_l, g.tr[1].dx_l, g.tr[1].x_r, g.tr[1].dx_r);
+        D[2] = make_int4(g.tr[2].x_l, g.tr[2].dx_l, g.tr[2].x_r, g.tr[2].dx_r);
+        D[3] = make_int4(g.dudx, g.dvdx, g.dudy, g.dvdy);
+        D[4] = make_int4(g.u0, g.v0, im.soff, (im.sw & 0xffff) | (im.sh << 16));
+        D[5] = make_int4(ft[0] | (ft[1] << 16), ft[2] | ((im.mir ? 1 : 0) << 16), (im.ca & 0xffff) | (xmin << 16),
+                         (nx & 255) | ((ymin & 255) << 8) | ((ny & 255) << 16));
         im.rot = 2;
         im.rdi = rank;
     }
@@ -1264,7 +1339,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     int *const tile_off = reinterpret_cast<int *>(aux);
     int *const colb = tile_off + NTYPES;
     static_assert(CR * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
-    static_assert(AUX_BYTES >= ROT_DESC_CAP * 128, "aux holds the rotated-image descriptors");
+    constexpr int ROT_CAP = AUX_BYTES / ROT_DESC_BYTES; // rotated-image descriptors per chunk in aux
+    static_assert(ROT_CAP >= 32, "aux holds the rotated-image descriptors");
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
@@ -1685,11 +1761,11 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         pt.mark(4);                                                                           \
         if (!one_chunk || !ent_setup_valid) {                                                 \
             entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);               \
-            if (!has_z_minus1<G>()) rot_stage(im, aux);                                       \
+            if (!has_z_minus1<G>()) rot_stage(im, aux, ROT_CAP);                              \
         }                                                                                     \
         ent_setup_valid = true;                                                               \
         pt.mark(3);                                                                           \
-        stamp_images(fb, d, aux, im, ballot(im.draw && im.ez == (Z)), err);                   \
+        stamp_images<true>(fb, d, aux, im, ballot(im.draw && im.ez == (Z)), err);                \
     }
 
     if (!fast) {
@@ -1741,7 +1817,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                         }
                     }
                 }
-                stamp_images(fb, d, aux, im, ballot(im.draw), err);
+                stamp_images<true>(fb, d, aux, im, ballot(im.draw), err);
             }
         }
     } else if (has_z_minus1<G>()) {

@@ -543,6 +543,7 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         int i = base + LANE;
         if (i < n) entity_step_slot(c, i, true);
     }
+    c.pt.mark(7); // diagnostic build: interactor list + smart loads + the non-smart pass
     // The smart entities' steps are independent of each other as well: a smart step writes only
     // its own entity and reads the grid, the static interactors and the agent (slot 0, stepped
     // last by the reverse loop, so every other smart step sees its pre-step state, which is what

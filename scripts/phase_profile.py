@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(REPO, "procgen-1_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-STEP = ["rng+action", "set_action+velocity", "step_entities", "collisions", "erase", "trails", "finish"]
+STEP = ["rng+action", "set_action+velocity", "step_entities", "collisions", "erase", "trails", "finish", "ilist+nonsmart"]
 RENDER = ["setup tables", "bg+fast tiles", "generic tiles", "entity setup", "entity stamping", "overlays", "output"]
 
 
