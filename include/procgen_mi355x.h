@@ -80,6 +80,21 @@ LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int co
 LIBENV_API int64_t procgen_atlas_host(const char *env_name, const char *resource_root, uint32_t *pixels,
                                       int64_t capacity, struct pg_image *sprites, struct pg_image *backgrounds,
                                       int32_t *num_backgrounds, int32_t *num_themes);
+/* This build's own per-env snapshot (PGEnv + entity planes + grid + both generators): exact for
+ * every state the engine can hold, including ones the upstream format cannot carry (an erased
+ * agent).  libenv's get_state / set_state use the upstream byte format (pg_state.cpp). */
+LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, int length);
+LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *data, int length);
+
+/* Pinning helper: RandGen::serialize's text (randgen.cpp:100-106) of 624 MT words + position. */
+LIBENV_API int procgen_mt_text(const uint32_t *words, int pos, char *out, int length);
+
+/* MinerGame::game_set_state (reference games/miner.cpp:423-449, exposed by the fork's JS binding as
+ * setState, cheerpgame.cpp:54-56): grid values (grid_width x grid_height, row-major, a DEAD_PLAYER
+ * cell sets `died`), agent and exit cell positions (+ .5); the frame is re-rendered.  0 ok, < 0 error. */
+LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int32_t *grid, int grid_width,
+                                        int grid_height, int agent_x, int agent_y, int exit_x, int exit_y);
+
 /* Sticky error: 0 ok; otherwise a code (see PG_ERR_*), message via procgen_error_string. */
 LIBENV_API int procgen_last_error(libenv_env *env);
 LIBENV_API const char *procgen_error_string(libenv_env *env);

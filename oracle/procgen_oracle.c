@@ -5154,6 +5154,51 @@ void oracle_latent(void *h, int32_t *grid_size, int32_t *grid, int32_t *agent_po
     }
 }
 
+/* MinerGame::game_set_state (miner.cpp:423-449): write the grid (a DEAD_PLAYER cell sets `died`),
+ * then erase the PLAYER entity if died, else put the agent at (agent_x + .5, agent_y + .5); the
+ * first EXIT entity goes to (exit_x + .5, exit_y + .5).  Re-renders the frame, as libenv's
+ * set_state re-observes (vecgame.cpp:503).  Returns 0, or -1 when the reference would crash
+ * (not miner, grid larger than the world, no EXIT entity). */
+int oracle_miner_set_state(void *h, int i, const int32_t *grid, int grid_width, int grid_height, int agent_x,
+                           int agent_y, int exit_x, int exit_y) {
+    Vec *v = (Vec *)h;
+    if (i < 0 || i >= v->count) return -1;
+    Game *g = &v->games[i];
+    if (g->game_id != GAME_MINER || grid_width < 0 || grid_height < 0 ||
+        grid_width * grid_height > g->grid_w * g->grid_h)
+        return -1;
+    int exit_i = -1;
+    for (int k = 0; k < g->num_ents; k++)
+        if (g->ents[k].type == MN_EXIT) { exit_i = k; break; }
+    if (exit_i < 0) return -1;
+    for (int idx = 0; idx < grid_width * grid_height; ++idx) {
+        int obj = grid[idx];
+        set_obj_idx(g, idx, obj);
+        if (obj == MN_DEAD_PLAYER) g->died = true;
+    }
+    if (g->died) {
+        /* std::find_if(PLAYER) + entities.erase: entities[0] is the agent while it is listed */
+        if (!g->agent_erased && g->num_ents > 0 && g->ents[0].type == PLAYER) {
+            g->agent_ghost = g->ents[0];
+            g->agent_erased = true;
+            memmove(&g->ents[0], &g->ents[1], sizeof(Entity) * (size_t)(g->num_ents - 1));
+            g->num_ents--;
+        }
+    } else {
+        Entity *a = AG(g);
+        a->x = agent_x + 0.5f;
+        a->y = agent_y + 0.5f;
+    }
+    for (int k = 0; k < g->num_ents; k++)
+        if (g->ents[k].type == MN_EXIT) {
+            g->ents[k].x = exit_x + 0.5f;
+            g->ents[k].y = exit_y + 0.5f;
+            break;
+        }
+    render(g, v->atlas);
+    return 0;
+}
+
 int oracle_debug(void *h, int i, int32_t *out, int n) {
     Vec *v = (Vec *)h;
     Game *g = &v->games[i];

@@ -63,6 +63,9 @@ void oracle_observe(void *h, uint8_t *rgb, float *rew, uint8_t *first,
                     int32_t *prev_level_seed, uint8_t *prev_level_complete, int32_t *level_seed);
 /* fork latent-state info per env: grid_size[2], grid[35*35], agent_pos[2], exit_pos[2] */
 void oracle_latent(void *h, int32_t *grid_size, int32_t *grid, int32_t *agent_pos, int32_t *exit_pos);
+/* miner.cpp:423-449 game_set_state on env i, then re-render; 0 ok, -1 where the reference crashes */
+int oracle_miner_set_state(void *h, int i, const int32_t *grid, int grid_width, int grid_height, int agent_x,
+                           int agent_y, int exit_x, int exit_y);
 /* debug: a few scalars of env i: [num_entities, cur_time, agent_x_bits, agent_y_bits,
  * background_index, wall_theme, episodes... ] (see .c) */
 int oracle_debug(void *h, int i, int32_t *out, int n);

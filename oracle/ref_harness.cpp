@@ -11,11 +11,24 @@
 #include <cstring>
 #include <memory>
 #include <vector>
+#include "buffer.h"
 #include "randgen.h"
 #include "entity.h"
 #include "mazegen.h"
 
 extern "C" {
+
+// RandGen::serialize (randgen.cpp:100-106) through the reference's own WriteBuffer (buffer.h): in
+// the fork write_int is a no-op and write_string copies the characters, so the bytes are exactly
+// the std::mt19937 text after seed(seed) and `draws` randint() calls.  Returns the byte count.
+int ref_randgen_text(int32_t seed, int draws, char *out, int length) {
+    RandGen r;
+    r.seed(seed);
+    for (int i = 0; i < draws; i++) r.randint();
+    WriteBuffer b(out, (size_t)length);
+    r.serialize(&b);
+    return (int)b.offset;
+}
 
 // successive raw 32-bit draws of the reference RandGen::randint() after seed(seed)
 void ref_mt_stream(int32_t seed, uint32_t *out, int n) {

@@ -19,6 +19,7 @@
 #include "../../include/libenv.h"
 #include "../../include/procgen_mi355x.h"
 #include "pg_assets.h"
+#include "pg_state.h"
 #include "pg_engine.h"
 
 extern "C" {
@@ -1114,7 +1115,7 @@ LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int le
     return (int)sizeof(PGEnv);
 }
 
-// ---- get_state / set_state (vecgame.cpp:485-505): this build's own snapshot format
+// ---- snapshots: this build's own per-env format (PGEnv + entity planes + grid + generators)
 // [u32 magic][u32 version][PGEnv][num_ents x PG_NF words][num_tail x PG_NF words (the reserved top
 // slots, starpilot's spawners)][grid cells int16][2 x 625 mt words][END]
 static const uint32_t STATE_MAGIC = 0x50474d33u; // "PGM3"
@@ -1127,7 +1128,7 @@ static const int GAME_MAX_DIM[PG_NUM_GAMES][2] = {
     {23, 23}, {45, 45}, {20, 20}, {31, 31}, {35, 35}, {64, 64}, {20, 20}, {16, 16}};
 static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
 
-LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
+LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, int length) {
     VecEnv *v = (VecEnv *)env;
     if (env_idx < 0 || env_idx >= v->num_envs) return -1;
     if (hipStreamSynchronize(v->stream) != hipSuccess) return -1;
@@ -1158,7 +1159,7 @@ LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
     return (int)(p - data);
 }
 
-LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) {
+LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *data, int length) {
     VecEnv *v = (VecEnv *)env;
     if (env_idx < 0 || env_idx >= v->num_envs || length < (int)(8 + sizeof(PGEnv) + 4)) {
         fail(v, PG_ERR_BAD_OPTION, "set_state: bad arguments");
@@ -1251,6 +1252,174 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     for (size_t k = 0; k < v->games.size(); k++)
         pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
     hipStreamSynchronize(v->stream);
+}
+
+// MinerGame::game_set_state (miner.cpp:423-449; the fork's JS binding's setState,
+// cheerpgame.cpp:54-56) on one env, through this build's own snapshot: the grid values are
+// written cell by cell (a DEAD_PLAYER cell sets `died`); if `died`, the PLAYER entity leaves the
+// list (the agent's state stays addressable, as the reference's `agent` shared_ptr); else the agent
+// goes to (agent_x + .5, agent_y + .5); the first EXIT entity to (exit_x + .5, exit_y + .5).  The
+// frame is re-rendered, as after set_state.  Where the reference would crash (another game, a grid
+// larger than the world, no EXIT entity) this fails with a sticky error instead.
+LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int32_t *grid, int grid_width,
+                                        int grid_height, int agent_x, int agent_y, int exit_x, int exit_y) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v || env_idx < 0 || env_idx >= v->num_envs || (!grid && grid_width * grid_height > 0))
+        return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: bad arguments");
+    if (v->game_of(env_idx) != PG_GAME_MINER)
+        return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: only miner has a game_set_state (miner.cpp:423-449)");
+    const size_t cap = 8 + sizeof(PGEnv) + (size_t)PG_CAP * PG_NF * 4 + (size_t)PG_GRID_MAX * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    std::vector<char> buf(cap);
+    if (procgen_get_snapshot(env, env_idx, buf.data(), (int)cap) < 0)
+        return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: could not read the env's state");
+    PGEnv s;
+    memcpy(&s, buf.data() + 8, sizeof(s));
+    size_t ents = (size_t)s.num_ents;
+    const size_t tail = (size_t)s.num_tail, cells = (size_t)s.main_width * s.main_height;
+    if (grid_width < 0 || grid_height < 0 || (size_t)grid_width * grid_height > cells)
+        return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: grid larger than the world");
+    const char *P = buf.data() + 8 + sizeof(PGEnv);
+    std::vector<std::vector<int32_t>> planes(PG_NF, std::vector<int32_t>(ents));
+    for (int f = 0; f < PG_NF; f++)
+        if (ents) memcpy(planes[f].data(), P + (size_t)f * ents * 4, ents * 4);
+    const char *T = P + (size_t)PG_NF * ents * 4; // tail planes, then grid, then generators
+    std::vector<int16_t> cellv(cells);
+    if (cells) memcpy(cellv.data(), T + (size_t)PG_NF * tail * 4, cells * 2);
+    const char *MT = T + (size_t)PG_NF * tail * 4 + cells * 2;
+    auto find_type = [&](int ty) {
+        for (size_t e = 0; e < ents; e++)
+            if (planes[F_TYPE][e] == ty) return (long)e;
+        return -1L;
+    };
+    if (find_type(6) < 0) return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: the env has no EXIT entity");
+    for (int idx = 0; idx < grid_width * grid_height; idx++) {
+        const int obj = grid[idx];
+        if (obj < -32768 || obj > 32767) return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: grid value out of range");
+        cellv[idx] = (int16_t)obj;
+        if (obj == 12) s.died = 1; // DEAD_PLAYER
+    }
+    auto fbits = [](float x) { int32_t b; memcpy(&b, &x, 4); return b; };
+    auto bitsf = [](int32_t b) { float x; memcpy(&x, &b, 4); return x; };
+    if (s.died) {
+        const long a = find_type(0); // PLAYER: entity 0 while the agent is listed
+        if (a == 0 && !s.agent_erased) {
+            s.agent_erased = 1;
+            s.ghost_x = bitsf(planes[F_X][0]); s.ghost_y = bitsf(planes[F_Y][0]);
+            s.ghost_vx = bitsf(planes[F_VX][0]); s.ghost_vy = bitsf(planes[F_VY][0]);
+            s.ghost_rx = bitsf(planes[F_RX][0]); s.ghost_ry = bitsf(planes[F_RY][0]);
+            for (int f = 0; f < PG_NF; f++) planes[f].erase(planes[f].begin());
+            ents--;
+        }
+    } else if (s.agent_erased) {
+        s.ghost_x = agent_x + 0.5f;
+        s.ghost_y = agent_y + 0.5f;
+    } else if (ents > 0) {
+        planes[F_X][0] = fbits(agent_x + 0.5f);
+        planes[F_Y][0] = fbits(agent_y + 0.5f);
+    }
+    const long ex = find_type(6);
+    planes[F_X][ex] = fbits(exit_x + 0.5f);
+    planes[F_Y][ex] = fbits(exit_y + 0.5f);
+    s.num_ents = (int32_t)ents;
+    std::vector<char> out(cap);
+    char *q = out.data();
+    memcpy(q, buf.data(), 8); q += 8;
+    memcpy(q, &s, sizeof(s)); q += sizeof(s);
+    for (int f = 0; f < PG_NF; f++) {
+        if (ents) memcpy(q, planes[f].data(), ents * 4);
+        q += ents * 4;
+    }
+    memcpy(q, T, (size_t)PG_NF * tail * 4); q += (size_t)PG_NF * tail * 4;
+    if (cells) memcpy(q, cellv.data(), cells * 2);
+    q += cells * 2;
+    memcpy(q, MT, 2 * PG_MT_WORDS * 4); q += 2 * PG_MT_WORDS * 4;
+    memcpy(q, &END_OF_BUFFER, 4); q += 4;
+    procgen_set_snapshot(env, env_idx, out.data(), (int)(q - out.data()));
+    return v->error ? -v->error : 0;
+}
+
+// Pinning helper (tests/test_state_cpu.py): RandGen::serialize's text of 624 MT words + position,
+// as get_state writes it.  Returns the length, or -1 when `out` is too small.
+LIBENV_API int procgen_mt_text(const uint32_t *words, int pos, char *out, int length) {
+    const std::string t = pg_mt_text(words, pos);
+    if ((int)t.size() > length) return -1;
+    memcpy(out, t.data(), t.size());
+    return (int)t.size();
+}
+
+// ---- get_state / set_state (vecgame.cpp:485-505) in the upstream byte format (pg_state.cpp)
+static const size_t SNAP_CAP = 8 + sizeof(PGEnv) + (size_t)PG_CAP * PG_NF * 4 + (size_t)PG_GRID_MAX * 2 +
+                               2 * PG_MT_WORDS * 4 + 4;
+
+static int read_host_env(VecEnv *v, int env_idx, HostEnv &h) {
+    std::vector<char> buf(SNAP_CAP);
+    if (procgen_get_snapshot(v, env_idx, buf.data(), (int)SNAP_CAP) < 0) return -1;
+    const char *p = buf.data() + 8;
+    memcpy(&h.s, p, sizeof(PGEnv)); p += sizeof(PGEnv);
+    const size_t ents = (size_t)h.s.num_ents, tail = (size_t)h.s.num_tail;
+    const size_t cells = (size_t)h.s.main_width * h.s.main_height;
+    for (int f = 0; f < PG_NF; f++) {
+        h.ent[f].resize(ents);
+        if (ents) memcpy(h.ent[f].data(), p, ents * 4);
+        p += ents * 4;
+    }
+    for (int f = 0; f < PG_NF; f++) {
+        h.tail[f].resize(tail);
+        if (tail) memcpy(h.tail[f].data(), p, tail * 4);
+        p += tail * 4;
+    }
+    h.cells.resize(cells);
+    if (cells) memcpy(h.cells.data(), p, cells * 2);
+    p += cells * 2;
+    memcpy(h.mt, p, sizeof(h.mt));
+    return 0;
+}
+
+static void write_host_env(VecEnv *v, int env_idx, const HostEnv &h) {
+    std::vector<char> buf;
+    buf.reserve(SNAP_CAP);
+    auto put = [&](const void *d, size_t n) { buf.insert(buf.end(), (const char *)d, (const char *)d + n); };
+    const uint32_t ver = 2;
+    put(&STATE_MAGIC, 4);
+    put(&ver, 4);
+    put(&h.s, sizeof(PGEnv));
+    for (int f = 0; f < PG_NF; f++) put(h.ent[f].data(), (size_t)h.s.num_ents * 4);
+    for (int f = 0; f < PG_NF; f++) put(h.tail[f].data(), (size_t)h.s.num_tail * 4);
+    put(h.cells.data(), h.cells.size() * 2);
+    put(h.mt, sizeof(h.mt));
+    put(&END_OF_BUFFER, 4);
+    procgen_set_snapshot(v, env_idx, buf.data(), (int)buf.size());
+}
+
+LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v || env_idx < 0 || env_idx >= v->num_envs || !data) return -1;
+    HostEnv h;
+    if (read_host_env(v, env_idx, h) < 0) return -1;
+    std::vector<char> out;
+    pg_state_write(h, out);
+    if (out.size() > (size_t)length) return -1; // the reference fasserts (buffer.h:96)
+    memcpy(data, out.data(), out.size());
+    return (int)out.size();
+}
+
+LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v || env_idx < 0 || env_idx >= v->num_envs || !data || length < 0) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: bad arguments");
+        return;
+    }
+    HostEnv h;
+    if (read_host_env(v, env_idx, h) < 0) {
+        fail(v, PG_ERR_BAD_OPTION, "set_state: could not read the env's state");
+        return;
+    }
+    std::string err;
+    if (!pg_state_read(data, (size_t)length, h, err)) { // the reference fasserts
+        fail(v, PG_ERR_BAD_OPTION, err.c_str()); // copied into the env's error message
+        return;
+    }
+    write_host_env(v, env_idx, h);
 }
 
 } // extern "C"

@@ -1655,7 +1655,6 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         // per screen row (lane = row), packed for one readlane per row: source rows of its
         // tile rows (7 bits each), their colb rows (5 bits each), tile-row count (2 bits);
         // and the background source row offset (-1: outside the background blit)
-        const int prow = lane;
         const int rinfo = ncy0 == 0 ? 0
                         : (srow0 | ((ncy0 > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
                            ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));

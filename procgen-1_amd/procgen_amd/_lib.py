@@ -75,6 +75,7 @@ SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_read_envs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "procgen_set_obs_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "procgen_set_latent_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 6),
     "procgen_start": (ctypes.c_int, [ctypes.c_void_p]),
     "procgen_act_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_act_hashed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32]),

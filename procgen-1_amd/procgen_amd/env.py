@@ -284,6 +284,16 @@ class BaseProcgenEnv:
         _check(self._lib, self._handle, rc)
         return out
 
+    def set_latent_state(self, env_idx, grid, agent_pos, exit_pos):
+        """MinerGame::game_set_state (procgen/src/games/miner.cpp:423-449, the fork's JS setState):
+        `grid` [h, w] (or flat with an explicit shape) of cell values, agent and exit cell positions.
+        A DEAD_PLAYER (12) cell kills the agent.  The env's frame is re-rendered."""
+        g = np.ascontiguousarray(grid, dtype=np.int32)
+        h, w = (g.shape if g.ndim == 2 else (1, g.size))
+        rc = self._lib.procgen_set_latent_state(self._handle, int(env_idx), g.ctypes.data, int(w), int(h),
+                                                int(agent_pos[0]), int(agent_pos[1]), int(exit_pos[0]), int(exit_pos[1]))
+        _check(self._lib, self._handle, rc)
+
     def set_obs_buffer(self, ptr):
         """Render later steps into the device buffer at `ptr` (uint8 [num,64,64,3]); None = own tensor."""
         rc = self._lib.procgen_set_obs_buffer(self._handle, ptr)

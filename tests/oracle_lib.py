@@ -56,6 +56,8 @@ def load():
         lib.oracle_mazegen.argtypes = [ctypes.c_int32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_latent.argtypes = [ctypes.c_void_p] * 5
+        lib.oracle_miner_set_state.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 6
+        lib.oracle_miner_set_state.restype = ctypes.c_int
         lib.oracle_bigfish_radius.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         lib.oracle_qt_rotation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         lib.oracle_spawn_sort.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -131,6 +133,15 @@ class OracleEnv:
         ep = np.zeros((n, 2), np.int32)
         self.lib.oracle_latent(self.h, gs.ctypes.data, grid.ctypes.data, ap.ctypes.data, ep.ctypes.data)
         return dict(grid_size=gs, grid=grid, agent_pos=ap, exit_pos=ep)
+
+    def miner_set_state(self, i, grid, agent_pos, exit_pos):
+        """miner.cpp:423-449 game_set_state on env i (grid [h, w]), then re-render."""
+        g = np.ascontiguousarray(grid, dtype=np.int32)
+        h, w = g.shape
+        rc = self.lib.oracle_miner_set_state(self.h, i, g.ctypes.data, w, h, int(agent_pos[0]), int(agent_pos[1]),
+                                             int(exit_pos[0]), int(exit_pos[1]))
+        if rc != 0:
+            raise ValueError("oracle_miner_set_state rejected the state")
 
     def debug(self, i):
         out = np.zeros(16, np.int32)
