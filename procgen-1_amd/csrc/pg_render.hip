@@ -1548,6 +1548,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         }
     }
 
+    pt.mark(7); // diagnostic build: env / tile-table / window / background setup
     // fast path eligibility: square TILE_PX tiles only (uniform_tiles), no z = -1 entity
     // (drawn between background and grid), few tile rows per frame
     const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);

@@ -34,7 +34,7 @@ const char *NAMES[PG_NUM_GAMES] = {"bigfish", "bossfight", "caveflyer", "chaser"
 // entity flags (pg_engine.h)
 bool flag(int32_t f, int bit) { return (f & bit) != 0; }
 
-struct WB {
+struct StateWriter {
     std::vector<char> &o;
     void raw(const void *p, size_t n) { o.insert(o.end(), (const char *)p, (const char *)p + n); }
     void i(int32_t v) { raw(&v, 4); }
@@ -46,7 +46,7 @@ struct WB {
     }
 };
 
-struct RB {
+struct StateReader {
     const char *p;
     size_t n, off;
     bool ok;
@@ -139,7 +139,7 @@ ViewM view_members(const HostEnv &h) {
     return m;
 }
 
-void write_entity(WB &w, const std::vector<int32_t> *pl, size_t k) { // Entity::serialize (entity.cpp:90-134)
+void write_entity(StateWriter &w, const std::vector<int32_t> *pl, size_t k) { // Entity::serialize (entity.cpp:90-134)
     auto F = [&](int f) { return fbits(pl[f][k]); };
     auto I = [&](int f) { return pl[f][k]; };
     const int32_t fl = I(F_FLAGS);
@@ -154,7 +154,7 @@ void write_entity(WB &w, const std::vector<int32_t> *pl, size_t k) { // Entity::
     w.f(F(F_CLIMBER_SPAWN_X));
 }
 
-void read_entity(RB &r, std::vector<int32_t> *pl, size_t k) { // Entity::deserialize (entity.cpp:136-179)
+void read_entity(StateReader &r, std::vector<int32_t> *pl, size_t k) { // Entity::deserialize (entity.cpp:136-179)
     auto F = [&](int f) { pl[f][k] = bitsf(r.f()); };
     auto I = [&](int f) { pl[f][k] = r.i(); };
     int32_t fl = 0;
@@ -169,12 +169,12 @@ void read_entity(RB &r, std::vector<int32_t> *pl, size_t k) { // Entity::deseria
     pl[F_FLAGS][k] = fl;
 }
 
-void write_randgen(WB &w, const uint32_t *words, int pos) { // RandGen::serialize (randgen.cpp:100-106)
+void write_randgen(StateWriter &w, const uint32_t *words, int pos) { // RandGen::serialize (randgen.cpp:100-106)
     w.i(1); // is_seeded: both generators are seeded before any state exists
     w.s(pg_mt_text(words, pos));
 }
 
-bool read_randgen(RB &r, uint32_t *words, int32_t &pos) {
+bool read_randgen(StateReader &r, uint32_t *words, int32_t &pos) {
     r.i(); // is_seeded
     int p = 0;
     const std::string t = r.s();
@@ -215,7 +215,7 @@ void pg_state_write(const HostEnv &h, std::vector<char> &out) {
     const PGEnv &s = h.s;
     const int gid = s.game_id;
     const std::string name = pg_game_name(gid);
-    WB w{out};
+    StateWriter w{out};
     // ---- Game::serialize (game.cpp:196-242)
     w.i(SERIALIZE_VERSION);
     w.s(name);
@@ -347,7 +347,7 @@ void pg_state_write(const HostEnv &h, std::vector<char> &out) {
 }
 
 bool pg_state_read(const char *data, size_t length, HostEnv &h, std::string &err) {
-    RB r{data, length, 0, true};
+    StateReader r{data, length, 0, true};
     PGEnv s = h.s;
     const int gid = s.game_id;
     auto bad = [&](const char *msg) {

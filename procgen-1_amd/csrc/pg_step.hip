@@ -514,7 +514,11 @@ DEV void ent_readlane(const Ent &m, int l, Ent &o) {
 // in the reference's reverse order, and stored lane-parallel at the end.
 template <int G>
 DEV constexpr bool pl_smart() {
+#ifdef PG_PL_ALL
+    return true;
+#else
     return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER;
+#endif
 }
 
 template <int G>

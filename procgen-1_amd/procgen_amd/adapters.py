@@ -24,7 +24,9 @@ from .env import ENV_NAMES, ProcgenGym3Env
 class ToBaselinesVecEnv:
     """gym3.ToBaselinesVecEnv + procgen's render() (procgen/env.py:276-286)."""
 
-    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 15}
+    # "human" needs gym3's viewer window and render_mode="rgb_array"'s 512x512 frame, neither built;
+    # render("rgb_array") returns the 64x64 observation of env 0
+    metadata = {"render.modes": ["rgb_array"], "video.frames_per_second": 15}
 
     def __init__(self, env):
         self.env = env
@@ -111,8 +113,10 @@ def make_env(render_mode=None, render=False, **kwargs):  # procgen/gym_registrat
     if render:
         render_mode = "human"
     if render_mode is not None:
-        # the reference routes both modes through render_mode="rgb_array" (512x512 info["rgb"])
-        kwargs["render_mode"] = "rgb_array"
+        # the reference routes both modes through render_mode="rgb_array" (the 512x512 antialiased
+        # info["rgb"], vecgame.cpp:318-330), which this build does not draw
+        raise NotImplementedError("make_env(render_mode=%r): the 512x512 render_mode='rgb_array' frame is "
+                                  "not built; use the 64x64 observation" % render_mode)
     return ToGymEnv(ProcgenGym3Env(num=1, num_threads=0, **kwargs))
 
 

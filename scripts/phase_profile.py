@@ -17,7 +17,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 STEP = ["rng+action", "set_action+velocity", "step_entities", "collisions", "erase", "trails", "finish", "ilist+nonsmart"]
-RENDER = ["setup tables", "bg+fast tiles", "generic tiles", "entity setup", "entity stamping", "overlays", "output"]
+RENDER = ["setup tables", "bg+fast tiles", "generic tiles", "entity setup", "entity stamping", "overlays", "output",
+          "setup env+window"]
 
 
 def main(game="coinrun", num=65536, warm=20, steps=50):

@@ -83,3 +83,14 @@ def test_env_ids():
     ids = register_environments()
     assert ids == ENV_IDS and len(ids) == 16
     assert sorted(ids.values()) == sorted(ENV_NAMES) and ids["procgen-coinrun-v0"] == "coinrun"
+
+
+def test_make_env_render_modes_not_built():
+    """make_env(render_mode=...) / render=True need the 512x512 rgb_array frame (vecgame.cpp:318-330),
+    which this build does not draw: a clear NotImplementedError before any env is created."""
+    import pytest
+    from procgen_amd.adapters import ToBaselinesVecEnv, make_env
+    for kw in ({"render_mode": "rgb_array"}, {"render_mode": "human"}, {"render": True}):
+        with pytest.raises(NotImplementedError):
+            make_env(env_name="coinrun", **kw)
+    assert ToBaselinesVecEnv.metadata["render.modes"] == ["rgb_array"]
