@@ -73,6 +73,18 @@ DEV bool is_player_image(int t) {
 
 DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// The frame may be drawn in passes of h rows: the LDS frame buffer holds rows [y0, y0 + h) of the
+// current pass, and every write is clipped to them.  Two 32-row passes halve the 16 KB frame and
+// raise the workgroups an MI355X CU holds (LDS-bound at 8 with a full frame) -- for the games
+// whose register budget allows 3 waves per SIMD (frame_rows below).
+struct FB {
+    uint32_t *p; // LDS rows of the pass
+    int y0, h;
+    DEV bool row_in(int row) const { return (unsigned)(row - y0) < (unsigned)h; }
+    DEV bool o_in(int o) const { return (unsigned)(o - y0 * PG_RES) < (unsigned)(h * PG_RES); }
+    DEV uint32_t &operator[](int o) const { return p[o - y0 * PG_RES]; }
+};
+
 // Size of the per-type grid sprite table (grid values 0..127 take the fast path).
 #define NTYPES 64 // grid values 0..63 (and SPACE) take the fast path; anything else falls back
 // Most tile rows a frame may span on the fast path: centred views of visibility 13 (coinrun) span
@@ -85,7 +97,7 @@ DEV constexpr int crows() { return (G == PG_GAME_COINRUN || G == PG_GAME_HEIST) 
 #define RB 8
 #endif
 #ifndef EG
-#define EG 8
+#define EG 4
 #endif
 // Rows / chunks of one large image whose texel loads are issued together before the blends.
 #ifndef BB
@@ -176,6 +188,20 @@ DEV float tile_aspect_ratio(int type, float rx, float ry) {
 }
 template <int G>
 DEV constexpr bool has_grid_tiles() { return G != PG_GAME_BIGFISH; } // bigfish: every cell is SPACE (never drawn)
+// games whose entities can rotate (face_direction / rotation / vrot in games/*.cpp; the agent's
+// action_vrot is 0 in every other game): elsewhere a rotation sets the error flag instead of
+// keeping the transform-blit state live in registers
+template <int G>
+DEV constexpr bool has_rotation() {
+    return G == PG_GAME_BOSSFIGHT || G == PG_GAME_CAVEFLYER || G == PG_GAME_DODGEBALL || G == PG_GAME_FRUITBOT ||
+           G == PG_GAME_HEIST || G == PG_GAME_JUMPER || G == PG_GAME_LEAPER || G == PG_GAME_PLUNDER ||
+           G == PG_GAME_STARPILOT;
+}
+// games with tile_image entities (get_tile_aspect_ratio != 0)
+template <int G>
+DEV constexpr bool has_tiled_entities() {
+    return G == PG_GAME_LEAPER || G == PG_GAME_DODGEBALL || G == PG_GAME_FRUITBOT;
+}
 // Side of the square grid-tile images of the pixel-centric fast path (0: the game always takes the
 // generic tile pass).  Coinrun and heist draw only such tiles; for the others a frame takes the fast
 // path when every tile in its window is one (a window scan decides, e.g. jumper's and climber's
@@ -328,7 +354,7 @@ DEV int rot_prepare(double x, double y, double w, double h, double m11, double m
 }
 
 // returns false when the transform is not a rotation this path reproduces
-DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
+DEV bool rotated_blit(const FB &fb, const uint32_t *pixels, uint32_t npix, double x, double y, double w, double h,
                       double m11, double m12, double m21, double m22, uint32_t soff, int iw, int ih, bool mir, int ca) {
     Axis ex, ey;
     RotGeo g;
@@ -340,20 +366,21 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
         if (lane >= ex.t1 && lane < ex.t1 + ex.n) {
             int scol = (int)((ex.base + (uint32_t)((lane - ex.t1) * ex.step)) >> 16);
             if (mir) scol = iw - 1 - scol;
-            for (int k0 = 0; k0 < ey.n; k0 += BB) { // BB rows: every texel load issued before the blends
+            const int klo = max(0, fb.y0 - ey.t1), khi = min(ey.n, fb.y0 + fb.h - ey.t1); // the pass's rows
+            for (int k0 = klo; k0 < khi; k0 += BB) { // BB rows: every texel load issued before the blends
                 uint32_t tv[BB];
 #pragma unroll
                 for (int r = 0; r < BB; r++) {
                     const int k = k0 + r;
                     const uint32_t idx = soff + (uint32_t)(((int)((ey.base + (uint32_t)(k * ey.step)) >> 16)) * iw + scol);
-                    const bool in = k < ey.n && idx < npix;
-                    if (k < ey.n && !in) ok = false;
+                    const bool in = k < khi && idx < npix;
+                    if (k < khi && !in) ok = false;
                     tv[r] = pixels[in ? idx : 0u];
                 }
 #pragma unroll
                 for (int r = 0; r < BB; r++) {
                     const int k = k0 + r;
-                    if (k >= ey.n) break;
+                    if (k >= khi) break;
                     const int o = (ey.t1 + k) * PG_RES + lane;
                     fb[o] = blend_argb_pm(fb[o], tv[r], ca);
                 }
@@ -366,15 +393,16 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const Trap T = g.tr[k];
-        for (int y0 = T.from_y; y0 < T.to_y; y0 += BB) { // BB scan lines: loads first, then blends
+        const int ylo = max(T.from_y, fb.y0), yhi = min(T.to_y, fb.y0 + fb.h); // the pass's scan lines
+        for (int yb = ylo; yb < yhi; yb += BB) { // BB scan lines: loads first, then blends
             uint32_t tv[BB];
             bool on[BB];
 #pragma unroll
             for (int r = 0; r < BB; r++) {
-                const int yy = y0 + r;
+                const int yy = yb + r;
                 const int xl = T.x_l + (yy - T.from_y) * T.dx_l, xr = T.x_r + (yy - T.from_y) * T.dx_r;
                 const int fromX = max(xl >> 16, 0), toX = min(xr >> 16, PG_RES);
-                on[r] = yy < T.to_y && lane >= fromX && lane < toX;
+                on[r] = yy < yhi && lane >= fromX && lane < toX;
                 int uu = (lane * g.dudx + yy * g.dudy + g.u0) >> 16;
                 int vv = (lane * g.dvdx + yy * g.dvdy + g.v0) >> 16;
                 uu = min(max(uu, 0), iw - 1);
@@ -389,7 +417,7 @@ DEV bool rotated_blit(uint32_t *fb, const uint32_t *pixels, uint32_t npix, doubl
             }
 #pragma unroll
             for (int r = 0; r < BB; r++)
-                if (on[r]) fb[(y0 + r) * PG_RES + lane] = blend_argb_pm(fb[(y0 + r) * PG_RES + lane], tv[r], ca);
+                if (on[r]) fb[(yb + r) * PG_RES + lane] = blend_argb_pm(fb[(yb + r) * PG_RES + lane], tv[r], ca);
         }
     }
     return ok;
@@ -490,21 +518,22 @@ DEV int to_shade(float f) {
 }
 
 // fillRect(QRectF, opaque colour) straight into the frame, lane-parallel (same edges as fill_setup)
-DEV void fb_fill_rectf(uint32_t *fb, double x, double y, double w, double h, uint32_t argb) {
+DEV void fb_fill_rectf(const FB &fb, double x, double y, double w, double h, uint32_t argb) {
     Img im;
     im.draw = false;
     if (!fill_setup(x, y, w, h, argb, im)) return;
     const int nx = im.ex.n, ny = im.ey.n;
-    for (int p = LANE; p < nx * ny; p += 64) fb[(im.ey.t1 + p / nx) * PG_RES + im.ex.t1 + p % nx] = im.fill;
+    for (int p = LANE; p < nx * ny; p += 64)
+        if (fb.row_in(im.ey.t1 + p / nx)) fb[(im.ey.t1 + p / nx) * PG_RES + im.ex.t1 + p % nx] = im.fill;
 }
 
 // jumper's compass (jumper.cpp:137-177).  The dial ellipse, the cosmetic needle and the translucent
 // jump ellipse are Qt 5.9.7 raster output tabulated per configuration / endpoint / rect size by
 // tools/qt_compass_tables.cpp (atlas image slot PG_TABLE_SLOT, layout in procgen_amd/assets.py
 // compass_table_words); lane = canvas row, each lane stamps the set bits of its row mask.
-DEV void jp_stamp(uint32_t *fb, const uint32_t *rows, int dx, int dy, uint32_t argb, bool blend) {
+DEV void jp_stamp(const FB &fb, const uint32_t *rows, int dx, int dy, uint32_t argb, bool blend) {
     const int y = LANE, sy = y - dy;
-    if (sy < 0 || sy >= PG_RES || dx <= -64 || dx >= 64) return;
+    if (sy < 0 || sy >= PG_RES || dx <= -64 || dx >= 64 || !fb.row_in(y)) return;
     uint64_t m = (uint64_t)rows[2 * sy] | ((uint64_t)rows[2 * sy + 1] << 32);
     m = dx >= 0 ? (m << dx) : (m >> -dx);
     while (m) {
@@ -514,7 +543,7 @@ DEV void jp_stamp(uint32_t *fb, const uint32_t *rows, int dx, int dy, uint32_t a
         *p = blend ? argb + BYTE_MUL(*p, (~argb) >> 24) : argb;
     }
 }
-DEV bool jp_draw_compass(uint32_t *fb, const PGEnv &s, const View &v, const PGDev &d, int env) {
+DEV bool jp_draw_compass(const FB &fb, const PGEnv &s, const View &v, const PGDev &d, int env) {
     const int4 ti = reinterpret_cast<const int4 *>(d.sprites)[PG_TABLE_SLOT];
     if (ti.y <= 0) return false;
     const uint32_t *t = d.pixels + (uint32_t)ti.x;
@@ -560,7 +589,7 @@ DEV bool jp_draw_compass(uint32_t *fb, const PGEnv &s, const View &v, const PGDe
 
 // game_draw additions drawn over the foreground (plunder.cpp:66-77)
 template <int G>
-DEV void game_overlay(uint32_t *fb, const PGEnv &s, const View &v, const PGDev &d, int env, bool &err) {
+DEV void game_overlay(const FB &fb, const PGEnv &s, const View &v, const PGDev &d, int env, bool &err) {
     if constexpr (G == PG_GAME_JUMPER)
         if (s.opt_distribution_mode != PG_MEMORY && !jp_draw_compass(fb, s, v, d, env)) err = true;
     if constexpr (G == PG_GAME_NINJA) { // jump charge bar (ninja.cpp:155-164), get_abs_rect (:812-814)
@@ -585,12 +614,14 @@ DEV double readlane_d(double x, int j) {
 }
 
 // One scale blit, all lanes cooperating over its footprint (uniform arguments).
-DEV void blit_seq(uint32_t *fb, const PGDev &d, const Axis &ex, const Axis &ey, uint32_t soff, int sw, int mir, int ca,
+DEV void blit_seq(const FB &fb, const PGDev &d, const Axis &ex, const Axis &ey, uint32_t soff, int sw, int mir, int ca,
                   bool &err) {
-    const int nx = ex.n, ny = ey.n, total = nx * ny;
+    const int nx = ex.n, ny = ey.n;
     const float inv = 1.0f / (float)nx;
-    // the footprint's pixels are distinct, so BB chunks of 64 load their texels before any blend
-    for (int p0 = LANE; p0 < total; p0 += 64 * BB) {
+    // the footprint's rows inside the pass; its pixels are distinct, so BB chunks of 64 load their
+    // texels before any blend
+    const int pstart = max(0, fb.y0 - ey.t1) * nx, total = min(ny, fb.y0 + fb.h - ey.t1) * nx;
+    for (int p0 = pstart + LANE; p0 < total; p0 += 64 * BB) {
         uint32_t tv[BB];
         int oo[BB];
 #pragma unroll
@@ -657,7 +688,7 @@ DEV bool rot_pixel(const RotD &r, int p, float inv, int &o, uint32_t &idx) {
     o = yy * PG_RES + x;
     return in && x >= fromX && x < toX;
 }
-DEV void rot_stamp_lds(uint32_t *fb, const PGDev &d, const uint8_t *aux, int rd, bool &err) {
+DEV void rot_stamp_lds(const FB &fb, const PGDev &d, const uint8_t *aux, int rd, bool &err) {
     const RotD r = rot_desc(aux, rd);
     const int total = rot_total(r);
     if (total <= 0) return;
@@ -665,7 +696,7 @@ DEV void rot_stamp_lds(uint32_t *fb, const PGDev &d, const uint8_t *aux, int rd,
     for (int p = LANE; p < total; p += 64) {
         int o;
         uint32_t idx;
-        bool on = rot_pixel(r, p, inv, o, idx);
+        bool on = rot_pixel(r, p, inv, o, idx) && fb.o_in(o);
         if (on && idx >= d.num_pixels) {
             err = true;
             on = false;
@@ -676,11 +707,11 @@ DEV void rot_stamp_lds(uint32_t *fb, const PGDev &d, const uint8_t *aux, int rd,
 }
 
 template <bool TILES>
-DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
+DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
 
 // tile_image (basic-abstract-game.cpp:849-877) of image j: the tiles (left to right / top to
 // bottom) become lanes of a plain-image list, set up lane-parallel and stamped in order.
-DEV void stamp_tiles(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, int caj, bool &err) {
+DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, int caj, bool &err) {
     const int ntile = readlane(im.ntile, j);
     const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
     const float tw = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), j));
@@ -716,7 +747,7 @@ DEV void stamp_tiles(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img
 // (loads are order-free), then the group is blended strictly in order; larger, tiled and
 // set-up-in-order images run their own loops at their turn.
 template <bool TILES>
-DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
+DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
     const int lane = LANE;
     const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
     const uint32_t npix = d.num_pixels;
@@ -749,7 +780,7 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
                 if (lane < total) {
                     int o;
                     uint32_t idx;
-                    if (rot_pixel(r, lane, 1.0f / (float)rot_nx(r), o, idx)) {
+                    if (rot_pixel(r, lane, 1.0f / (float)rot_nx(r), o, idx) && fb.o_in(o)) {
                         if (idx < npix) {
                             tv[g] = d.pixels[idx];
                             fo[g] = o;
@@ -777,11 +808,13 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
                 const uint32_t idx = (uint32_t)readlane(im.soff, j) + (uint32_t)(srow * swj + scol);
                 const int o = (readlane(im.ey.t1, j) + py) * PG_RES + readlane(im.ex.t1, j) + pxx;
                 const uint32_t fillj = (uint32_t)readlane((int)im.fill, j);
-                if (fillj != 0 && o >= 0 && o < PG_RES * PG_RES) {
+                if (!fb.o_in(o)) {
+                    // another pass's row
+                } else if (fillj != 0) {
                     tv[g] = fillj;
                     fo[g] = o;
                     on[g] = true;
-                } else if (idx < npix && o >= 0 && o < PG_RES * PG_RES) {
+                } else if (idx < npix) {
                     tv[g] = d.pixels[idx];
                     fo[g] = o;
                     on[g] = true;
@@ -825,7 +858,8 @@ DEV void stamp_images(uint32_t *fb, const PGDev &d, const uint8_t *aux, const Im
             if (readlane((int)im.fill, j) != 0) {
                 const uint32_t col = (uint32_t)readlane((int)im.fill, j);
                 const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
-                for (int p = lane; p < nx * ny; p += 64) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
+                for (int p = lane; p < nx * ny; p += 64)
+                    if (fb.row_in(ty + p / nx)) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
             } else {
                 Axis ex, ey;
                 ex.t1 = readlane(im.ex.t1, j); ex.n = nx; ex.base = (uint32_t)readlane((int)im.ex.base, j);
@@ -911,7 +945,9 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
     im.sh = sp.z;
     if (sp.y <= 0) {
         err = true; // missing image
-    } else if (rotation != 0) {
+    } else if (!has_rotation<G>() && rotation != 0) {
+        err = true; // not reachable in this game (has_rotation)
+    } else if (has_rotation<G>() && rotation != 0) {
         // rotated: the Qt transform blit runs in order when this entity is stamped
         int rslot = -1;
         for (int k = 0; k < PG_ROT_N; k++)
@@ -932,7 +968,7 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
         im.draw = true;
         im.rot = 1;
         im.rx = rx; im.ry = ry; im.rw = rw; im.rh = rh;
-    } else if (tile_aspect_ratio<G>(etype, prx, pry) != 0) {
+    } else if (has_tiled_entities<G>() && tile_aspect_ratio<G>(etype, prx, pry) != 0) {
         float tile_ratio = tile_aspect_ratio<G>(etype, prx, pry);
         int num_tiles;
         if (tile_ratio < 0) {
@@ -1018,7 +1054,7 @@ DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
 // tile column of the few screen columns two tiles overlap in a lane = row pass.  Frames this cannot
 // express (more classes than GEN_K, a window wider than 63 or larger than GEN_GW cells, a grid value
 // outside the table, 3 tiles covering one pixel) take the stamped generic pass instead.
-#define GEN_K 6       // tile classes per frame
+#define GEN_K 4       // tile classes per frame (their setup tables fill the 8 KB pass frame)
 #define GEN_GW 1024   // window cells (u8 slot per cell)
 #define GEN_NOTHING 64
 #define GEN_BAD 15
@@ -1239,7 +1275,7 @@ DEV uint32_t gen_texel(const PGDev &d, const int2 t, int sc, int sr, bool &err) 
 // Row pass (first covering tile column) + second-column pass.  FUSE: the background texel of the
 // pixel (bg_col / bg_base / bgrow as in the fast path) is the destination; else the frame buffer.
 template <bool FUSE>
-DEV void gen_draw(uint32_t *fb, const PGDev &d, const uint8_t *aux, const GenLane &gl, int ww, bool bg_col,
+DEV void gen_draw(const FB &fb, const PGDev &d, const uint8_t *aux, const GenLane &gl, int ww, bool bg_col,
                   uint32_t bg_base, int bgrow, bool &err) {
     const int lane = LANE;
     const int2 *ti = reinterpret_cast<const int2 *>(aux);
@@ -1249,7 +1285,7 @@ DEV void gen_draw(uint32_t *fb, const PGDev &d, const uint8_t *aux, const GenLan
     // per screen row (lane = row): its covering window rows, packed for one readlane per row
     const int rinfo = gl.ncy == 0 ? 0 : (gl.ry0 | ((gl.ncy > 1 ? gl.ry1 : 0) << 8) | (gl.ncy << 16));
     const int cxo = gl.ncx > 0 ? gl.cx0 : -1;
-    for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+    for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
         int info[RB], s0[RB], s1[RB];
         int2 t0[RB], t1[RB];
         uint32_t dst[RB], ta[RB], tb[RB];
@@ -1307,7 +1343,7 @@ DEV void gen_draw(uint32_t *fb, const PGDev &d, const uint8_t *aux, const GenLan
         m2 &= m2 - 1;
         const int x1 = readlane(gl.cx1, c);
         const int row = lane;
-        if (gl.ncy > 0) {
+        if (gl.ncy > 0 && fb.row_in(row)) {
             uint32_t px = fb[row * PG_RES + c];
             for (int l = 0; l < gl.ncy; l++) {
                 const int2 t = ti[gw[(l ? gl.ry1 : gl.ry0) * ww + x1]];
@@ -1322,10 +1358,25 @@ DEV void gen_draw(uint32_t *fb, const PGDev &d, const uint8_t *aux, const GenLan
 
 } // namespace
 
+// Frame rows per pass and waves per SIMD: the games without rotated / tiled entities fit 168 VGPRs
+// (77-114 measured) and render in two 32-row passes at 3 waves per SIMD (12-15 KB of LDS); the
+// others keep the transform-blit state in registers (171-206 VGPRs) and render the whole frame in
+// one pass at 2 waves per SIMD.
 template <int G>
-__global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *env_list) {
+DEV constexpr int frame_rows() { return (has_rotation<G>() || has_tiled_entities<G>()) ? 64 : 32; }
+template <int G>
+DEV constexpr int render_waves() { return frame_rows<G>() == 32 ? 3 : 2; }
+// rotated-image descriptors per 64-entity chunk (beyond them an image takes the in-order setup)
+template <int G>
+DEV constexpr int rot_cap() {
+    return G == PG_GAME_COINRUN ? 0 : ((G == PG_GAME_BOSSFIGHT || G == PG_GAME_STARPILOT) ? 48 : 16);
+}
+
+template <int G>
+__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list) {
     const PGDev d = game_view(dg, G);
-    __shared__ __attribute__((aligned(16))) uint32_t fb[PG_RES * PG_RES];
+    constexpr int HR = frame_rows<G>();
+    __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES]; // the rows of one pass
     // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
     // <= -2 not drawable on the fast path
     constexpr int CR = crows<G>();
@@ -1339,8 +1390,12 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     int *const tile_off = reinterpret_cast<int *>(aux);
     int *const colb = tile_off + NTYPES;
     static_assert(CR * 64 >= 2 * 64 * 4, "colb doubles as the axis tables");
-    constexpr int ROT_CAP = AUX_BYTES / ROT_DESC_BYTES; // rotated-image descriptors per chunk in aux
-    static_assert(ROT_CAP >= 32, "aux holds the rotated-image descriptors");
+    // rotated-image descriptors: in one full-frame pass they reuse aux, whose tile tables are dead
+    // once the tiles are drawn; with two passes the second pass still needs the tables
+    constexpr bool ONE_PASS = HR == PG_RES;
+    constexpr int ROT_CAP = ONE_PASS ? AUX_BYTES / ROT_DESC_BYTES : rot_cap<G>();
+    __shared__ __attribute__((aligned(16))) uint8_t rdesc_own[ONE_PASS ? 16 : (ROT_CAP > 0 ? ROT_CAP : 1) * ROT_DESC_BYTES];
+    uint8_t *const rdesc = ONE_PASS ? aux : rdesc_own;
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
@@ -1643,12 +1698,35 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     bool gen = false, notiles = false;
     if constexpr (has_general<G>())
         if (!fast && tab) {
-            const int gs = gen_setup<G>(d, s, v, Gd, player_img, low_x, low_y, ww, wh, xg, yg, aux, reinterpret_cast<int4 *>(fb), gl);
+            static_assert(2 * GEN_K * 64 * 16 <= 32 * PG_RES * 4, "the class tables fit the pass frame");
+            const int gs = gen_setup<G>(d, s, v, Gd, player_img, low_x, low_y, ww, wh, xg, yg, aux, reinterpret_cast<int4 *>(fb_lds), gl);
             gen = gs == 1;
             notiles = gs == 2;
         }
 
     pt.mark(0);
+    Img im;
+    img_clear(im);
+    // ---- entities of one render_z, in list order (basic-abstract-game.cpp:1061-1075); one
+    //      setup per 64-entity chunk, reused by every z pass and both frame passes when the list
+    //      fits one chunk (and nothing else used `im` in between)
+    const int n = s.num_ents;
+    const bool one_chunk = n <= 64;
+    bool ent_setup_valid = false;
+#define PG_DRAW_ENTITIES(Z)                                                                   \
+    for (int base = 0; base < n; base += 64) {                                                \
+        pt.mark(4);                                                                           \
+        if (!one_chunk || !ent_setup_valid) {                                                 \
+            entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);               \
+            if (!has_z_minus1<G>()) rot_stage(im, rdesc, ROT_CAP);                            \
+        }                                                                                     \
+        ent_setup_valid = true;                                                               \
+        pt.mark(3);                                                                           \
+        stamp_images<true>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z)), err);           \
+    }
+
+    for (int pass = 0; pass < PG_RES / HR; pass++) {
+    const FB fb{fb_lds, pass * HR, HR};
     if (fast) {
         // ---- background + first tile column, pixel-centric, RB rows per batch (all loads of
         //      a batch are issued before the first blend).  A transparent texel (0) blends to
@@ -1660,7 +1738,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                         : (srow0 | ((ncy0 > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
                            ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));
         const int bgrow = bg_lane_row;
-        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+        for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
             uint32_t bgv[RB], ta[RB], tb[RB];
             int info[RB], bgr[RB], ca[RB], cbv[RB];
 #pragma unroll
@@ -1715,7 +1793,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
             m2 &= m2 - 1;
             const int x1 = readlane(cx1, c), sc1 = readlane(scol1, c);
             const int row = lane;
-            if (ncy0 > 0) {
+            if (ncy0 > 0 && fb.row_in(row)) {
                 uint32_t px = fb[row * PG_RES + c];
                 for (int l = 0; l < ncy0; l++) {
                     const int code = lookup_grid(x1, l ? ry1 : ry0);
@@ -1733,7 +1811,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     } else {
         // ---- background alone (lane = column), RB rows per batch
         const int bgrow = bg_lane_row;
-        for (int r0 = 0; r0 < PG_RES; r0 += RB) {
+        for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
             uint32_t bgv[RB];
 #pragma unroll
             for (int k = 0; k < RB; k++) {
@@ -1749,25 +1827,6 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     wave_sync();
 
     pt.mark(1);
-    Img im;
-    img_clear(im);
-    // ---- entities of one render_z, in list order (basic-abstract-game.cpp:1061-1075); one
-    //      setup per 64-entity chunk, reused by every z pass when the list fits one chunk
-    const int n = s.num_ents;
-    const bool one_chunk = n <= 64;
-    bool ent_setup_valid = false;
-#define PG_DRAW_ENTITIES(Z)                                                                   \
-    for (int base = 0; base < n; base += 64) {                                                \
-        pt.mark(4);                                                                           \
-        if (!one_chunk || !ent_setup_valid) {                                                 \
-            entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);               \
-            if (!has_z_minus1<G>()) rot_stage(im, aux, ROT_CAP);                              \
-        }                                                                                     \
-        ent_setup_valid = true;                                                               \
-        pt.mark(3);                                                                           \
-        stamp_images<true>(fb, d, aux, im, ballot(im.draw && im.ez == (Z)), err);                \
-    }
-
     if (!fast) {
         // ---- z = -1 entities, then the grid tiles in the reference's x-major / y-minor order
         //      (draw_foreground :930-964), stamped like entities: lane k <-> the k-th tile of
@@ -1782,6 +1841,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                 gen_draw<false>(fb, d, aux, gl, ww, false, 0u, -1, err);
             }
         } else if (has_grid_tiles<G>()) {
+            ent_setup_valid = false; // the tile chunks reuse `im`
             const int ntiles = ww * wh;
             for (int base = 0; base < ntiles; base += 64) {
                 const int k = base + lane;
@@ -1817,7 +1877,7 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
                         }
                     }
                 }
-                stamp_images<true>(fb, d, aux, im, ballot(im.draw), err);
+                stamp_images<true>(fb, d, rdesc, im, ballot(im.draw), err);
             }
         }
     } else if (has_z_minus1<G>()) {
@@ -1825,10 +1885,8 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     }
     pt.mark(2);
     // ---- entities, render_z 0 then 1 (basic-abstract-game.cpp:966-967)
-    ent_setup_valid = false;
     PG_DRAW_ENTITIES(0)
     PG_DRAW_ENTITIES(1)
-#undef PG_DRAW_ENTITIES
     wave_sync();
     if (__builtin_expect(s.has_useful_vel_info && s.opt_paint_vel_info, 0)) { // paint_vel_info (basic-abstract-game.cpp:969-977)
         const float vx = s.agent_erased ? s.ghost_vx : EFr(d, F_VX, env, 0);
@@ -1844,10 +1902,10 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
     game_overlay<G>(fb, s, v, d, env, err);
     wave_sync();
     pt.mark(5);
-    // ---- bgr32_to_rgb888 (game.cpp:8-23): lane writes 4 pixels = 12 bytes per iteration
+    // ---- bgr32_to_rgb888 (game.cpp:8-23) of the pass's rows: lane writes 4 pixels = 12 bytes
     uint8_t *out = d.rgb + (size_t)env * PG_OBS_BYTES;
-    for (int q = lane; q < PG_RES * PG_RES / 4; q += 64) {
-        uint4 p4 = reinterpret_cast<const uint4 *>(fb)[q];
+    for (int q = fb.y0 * (PG_RES / 4) + lane; q < (fb.y0 + fb.h) * (PG_RES / 4); q += 64) {
+        uint4 p4 = reinterpret_cast<const uint4 *>(fb_lds)[q - fb.y0 * (PG_RES / 4)];
         // bytes r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
         uint32_t w0 = ((p4.x >> 16) & 0xff) | (p4.x & 0xff00) | ((p4.x & 0xff) << 16) | (((p4.y >> 16) & 0xff) << 24);
         uint32_t w1 = ((p4.y >> 8) & 0xff) | ((p4.y & 0xff) << 8) | (((p4.z >> 16) & 0xff) << 16) | (((p4.z >> 8) & 0xff) << 24);
@@ -1857,6 +1915,9 @@ __global__ __launch_bounds__(64) void pg_render_kernel(PGDev dg, const int32_t *
         o[1] = w1;
         o[2] = w2;
     }
+    wave_sync(); // the next pass overwrites the frame rows
+    } // pass
+#undef PG_DRAW_ENTITIES
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
     pt.mark(6);
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
