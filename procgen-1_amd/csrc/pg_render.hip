@@ -96,9 +96,6 @@ DEV constexpr int crows() { return (G == PG_GAME_COINRUN || G == PG_GAME_HEIST) 
 #ifndef RB
 #define RB 8
 #endif
-#ifndef EG
-#define EG 4
-#endif
 // Rows / chunks of one large image whose texel loads are issued together before the blends.
 #ifndef BB
 #define BB 1
@@ -706,11 +703,24 @@ DEV void rot_stamp_lds(const FB &fb, const PGDev &d, const uint8_t *aux, int rd,
     }
 }
 
-template <bool TILES>
+template <bool TILES, int EGN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
+
+// Rows an image can touch, for skipping it in a pass that holds none of them: plain blits, fills
+// and descriptor transform blits keep their row range in ey (rot_stage sets it); the others
+// (in-order transform setup, tile lists) count as the whole frame.
+DEV bool img_in_pass(const Img &im, const FB &fb) {
+    int lo = 0, hi = PG_RES;
+    if (im.rot != 1 && im.ntile == 0) {
+        lo = im.ey.t1;
+        hi = im.ey.t1 + im.ey.n;
+    }
+    return hi > fb.y0 && lo < fb.y0 + fb.h;
+}
 
 // tile_image (basic-abstract-game.cpp:849-877) of image j: the tiles (left to right / top to
 // bottom) become lanes of a plain-image list, set up lane-parallel and stamped in order.
+template <int EGN>
 DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, int caj, bool &err) {
     const int ntile = readlane(im.ntile, j);
     const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
@@ -738,7 +748,7 @@ DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img
                 ti.soff = offj; ti.sw = swj; ti.sh = shj; ti.mir = mirj; ti.ca = caj;
             }
         }
-        stamp_images<false>(fb, d, aux, ti, ballot(ti.draw), err);
+        stamp_images<false, EGN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
     }
 }
 
@@ -746,24 +756,24 @@ DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img
 // every small one (<= 64 px: plain blits, fills, transform blits with a descriptor) is loaded first
 // (loads are order-free), then the group is blended strictly in order; larger, tiled and
 // set-up-in-order images run their own loops at their turn.
-template <bool TILES>
+template <bool TILES, int EGN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
     const int lane = LANE;
     const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
     const uint32_t npix = d.num_pixels;
     while (m) {
-        int js[EG];
+        int js[EGN];
 #pragma unroll
-        for (int g = 0; g < EG; g++) {
+        for (int g = 0; g < EGN; g++) {
             js[g] = m ? __ffsll((long long)m) - 1 : -1;
             if (m) m &= m - 1;
         }
-        uint32_t tv[EG];
-        int fo[EG];
-        bool on[EG], pre[EG];
+        uint32_t tv[EGN];
+        int fo[EGN];
+        bool on[EGN], pre[EGN];
         uint32_t part = 0;
 #pragma unroll
-        for (int g = 0; g < EG; g++) {
+        for (int g = 0; g < EGN; g++) {
             on[g] = false;
             pre[g] = false;
             tv[g] = 0;
@@ -824,10 +834,10 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
             }
         }
 #pragma unroll
-        for (int g = 0; g < EG; g++) part |= on[g] ? alpha_partial(tv[g]) : 0u;
+        for (int g = 0; g < EGN; g++) part |= on[g] ? alpha_partial(tv[g]) : 0u;
         const bool binary = ballot(part != 0) == 0; // every prefetched texel has alpha 0 or 255
 #pragma unroll
-        for (int g = 0; g < EG; g++) {
+        for (int g = 0; g < EGN; g++) {
             const int j = js[g];
             if (j < 0) continue;
             const int caj = readlane(im.ca, j);
@@ -850,7 +860,7 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
                 continue;
             }
             if (readlane(im.ntile, j) > 0) {
-                if constexpr (TILES) stamp_tiles(fb, d, aux, im, j, caj, err);
+                if constexpr (TILES) stamp_tiles<EGN>(fb, d, aux, im, j, caj, err);
                 else err = true; // unreachable: tile lists hold plain images only
                 continue;
             }
@@ -1041,6 +1051,8 @@ DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
                          (nx & 255) | ((ymin & 255) << 8) | ((ny & 255) << 16));
         im.rot = 2;
         im.rdi = rank;
+        im.ey.t1 = ymin; // the rows it covers, for the pass filter (ey is otherwise unused here)
+        im.ey.n = ny;
     }
 }
 
@@ -1396,6 +1408,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     constexpr int ROT_CAP = ONE_PASS ? AUX_BYTES / ROT_DESC_BYTES : rot_cap<G>();
     __shared__ __attribute__((aligned(16))) uint8_t rdesc_own[ONE_PASS ? 16 : (ROT_CAP > 0 ? ROT_CAP : 1) * ROT_DESC_BYTES];
     uint8_t *const rdesc = ONE_PASS ? aux : rdesc_own;
+    constexpr int EGK = 4; // images per texel-prefetch group (8 measured slower for every game)
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
@@ -1722,7 +1735,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
         }                                                                                     \
         ent_setup_valid = true;                                                               \
         pt.mark(3);                                                                           \
-        stamp_images<true>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z)), err);           \
+        stamp_images<true, EGK>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z) && img_in_pass(im, fb)), err); \
     }
 
     for (int pass = 0; pass < PG_RES / HR; pass++) {
@@ -1877,7 +1890,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                         }
                     }
                 }
-                stamp_images<true>(fb, d, rdesc, im, ballot(im.draw), err);
+                stamp_images<true, EGK>(fb, d, rdesc, im, ballot(im.draw && img_in_pass(im, fb)), err);
             }
         }
     } else if (has_z_minus1<G>()) {
