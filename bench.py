@@ -63,7 +63,7 @@ def cpu_baseline(game, num_levels, max_workers=16, steps=12000):
                       "(%.1f s wall, slowest worker %.1f s)" % (game, envs, steps, cores, wall, max(times))}
 
 
-def pmc_traffic(game):
+def pmc_traffic(game, kernel="pg_render_kernel"):
     """HBM bytes (FETCH_SIZE + WRITE_SIZE) per render launch of `game` from the newest committed
     rocprofv3 PMC summary under profiles/ (separate FETCH_SIZE / WRITE_SIZE passes over this same
     bench command: scripts/gpu_counters.sh -> *counters_summary.json, or the older
@@ -77,12 +77,12 @@ def pmc_traffic(game):
                 d = json.load(f)
         except Exception:
             continue
-        if d.get("game", "coinrun") == game and d.get("render_hbm_bytes_per_launch"):
+        if kernel == "pg_render_kernel" and d.get("game", "coinrun") == game and d.get("render_hbm_bytes_per_launch"):
             return d["render_hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
         g = d.get(game)
         if isinstance(g, dict):
             for kname, k in g.items():
-                if kname.startswith("pg_render_kernel") and isinstance(k, dict) and k.get("hbm_bytes_per_launch"):
+                if kname.startswith(kernel) and isinstance(k, dict) and k.get("hbm_bytes_per_launch"):
                     return k["hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
     return None, None
 
@@ -222,6 +222,11 @@ def main():
                     "kernel_ms": {"step": round(kt[0], 4), "reset": round(kt[1], 4), "render": round(kt[2], 4),
                                   "step_wall": round(kt[3], 4)},
                     "dominant_kernel": names[dom], "timed_launches": n_timed}
+            # the step kernel (game logic, latency-bound: no algorithmic byte count in SURVEY 8(d)):
+            # its counter traffic per launch and the bandwidth that is over its in-bench duration
+            st_traffic, st_src = pmc_traffic(game, "pg_step_kernel")
+            roof["step_kernel"] = {"ms": round(kt[0], 4), "traffic": st_traffic, "traffic_source": st_src,
+                                   "traffic_GBps": round(st_traffic / (kt[0] * 1e-3) / 1e9, 2) if st_traffic and kt[0] > 0 else None}
         else:
             # a mixed batch runs every game's step -> reset -> render chain concurrently on its own
             # stream: no single kernel's duration is attributable, so the roofline is taken over
