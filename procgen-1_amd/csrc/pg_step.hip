@@ -301,6 +301,17 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
     return -1;
 }
 
+// Games whose smart entities step lane-parallel (step_entities_fast; measured per game,
+// profiles/r02: a win where several smart entities take many sub-steps, a 2x loss for coinrun)
+template <int G>
+DEV constexpr bool pl_smart() {
+#ifdef PG_PL_ALL
+    return true;
+#else
+    return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER;
+#endif
+}
+
 // next_collider for a lane stepping its own entity (lane-parallel smart steps): the static
 // interactors are read from LDS, the ascending list's last hit is the largest index.
 DEV int next_collider_pl(Ctx &c, int oi, int upper, const Ent &o) {
@@ -349,11 +360,13 @@ DEV void build_interactor_list(Ctx &c) {
                    EF(c, F_GROW_RATE, i) == 1 && EI(c, F_EXPIRE_TIME, i) <= 0;
         }
         c.ireg = ballot(!stat) == 0;
-        if (LANE < cnt) {
-            c.ibox[LANE] = make_float4(c.i_x, c.i_y, c.i_rx, c.i_ry);
-            c.iinfo[LANE] = c.i_idx | (c.i_erase ? (int)0x80000000u : 0);
+        if constexpr (pl_smart<G>()) {
+            if (LANE < cnt) {
+                c.ibox[LANE] = make_float4(c.i_x, c.i_y, c.i_rx, c.i_ry);
+                c.iinfo[LANE] = c.i_idx | (c.i_erase ? (int)0x80000000u : 0);
+            }
+            wave_sync();
         }
-        wave_sync();
     }
 }
 
@@ -512,14 +525,6 @@ DEV void ent_readlane(const Ent &m, int l, Ent &o) {
 // the scans read only the register-cached static interactors), so every smart entity can
 // be loaded lane-parallel up front (lane k <-> k-th smart entity), stepped from registers
 // in the reference's reverse order, and stored lane-parallel at the end.
-template <int G>
-DEV constexpr bool pl_smart() {
-#ifdef PG_PL_ALL
-    return true;
-#else
-    return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER;
-#endif
-}
 
 template <int G>
 DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
@@ -2674,8 +2679,10 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
-    __shared__ float4 lds_ibox[64];
-    __shared__ int lds_iinfo[64];
+    // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the
+    // workgroups per CU here)
+    __shared__ float4 lds_ibox[pl_smart<G>() ? 64 : 1];
+    __shared__ int lds_iinfo[pl_smart<G>() ? 64 : 1];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
     Ctx c;
