@@ -1371,11 +1371,16 @@ DEV void gen_draw(const FB &fb, const PGDev &d, const uint8_t *aux, const GenLan
 } // namespace
 
 // Frame rows per pass and waves per SIMD: the games without rotated / tiled entities fit 168 VGPRs
-// (77-114 measured) and render in two 32-row passes at 3 waves per SIMD (12-15 KB of LDS); the
-// others keep the transform-blit state in registers (171-206 VGPRs) and render the whole frame in
-// one pass at 2 waves per SIMD.
+// (77-114 measured) and render in two 32-row passes at 3 waves per SIMD (12-15 KB of LDS), as do
+// four rotating games; the others keep one full-frame pass at 2 waves per SIMD.
 template <int G>
-DEV constexpr int frame_rows() { return (has_rotation<G>() || has_tiled_entities<G>()) ? 64 : 32; }
+DEV constexpr int frame_rows() {
+    // measured per game (profiles/r02/r02_k_variants.txt): two passes win for every game whose
+    // registers fit 168 (the rotating heist, caveflyer, plunder and starpilot with a few spills too);
+    // bossfight (48 rotated-image descriptors of LDS) and the games with tile_image entities or
+    // jumper's compass (170-176 VGPRs) keep one pass at 2 waves per SIMD
+    return (has_tiled_entities<G>() || G == PG_GAME_JUMPER || G == PG_GAME_BOSSFIGHT) ? 64 : 32;
+}
 template <int G>
 DEV constexpr int render_waves() { return frame_rows<G>() == 32 ? 3 : 2; }
 // rotated-image descriptors per 64-entity chunk (beyond them an image takes the in-order setup)
