@@ -1372,14 +1372,13 @@ DEV void gen_draw(const FB &fb, const PGDev &d, const uint8_t *aux, const GenLan
 
 // Frame rows per pass and waves per SIMD: the games without rotated / tiled entities fit 168 VGPRs
 // (77-114 measured) and render in two 32-row passes at 3 waves per SIMD (12-15 KB of LDS), as do
-// four rotating games; the others keep one full-frame pass at 2 waves per SIMD.
+// six rotating / tiling games; three keep one full-frame pass at 2 waves per SIMD.
 template <int G>
 DEV constexpr int frame_rows() {
-    // measured per game (profiles/r02/r02_k_variants.txt): two passes win for every game whose
-    // registers fit 168 (the rotating heist, caveflyer, plunder and starpilot with a few spills too);
-    // bossfight (48 rotated-image descriptors of LDS) and the games with tile_image entities or
-    // jumper's compass (170-176 VGPRs) keep one pass at 2 waves per SIMD
-    return (has_tiled_entities<G>() || G == PG_GAME_JUMPER || G == PG_GAME_BOSSFIGHT) ? 64 : 32;
+    // measured per game (profiles/r02/r02_k_variants.txt): two passes win for every game but
+    // bossfight (48 rotated-image descriptors of LDS), jumper (compass overlay; 170 VGPRs spill) and
+    // fruitbot (tile lists), which keep one full-frame pass at 2 waves per SIMD
+    return (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT) ? 64 : 32;
 }
 template <int G>
 DEV constexpr int render_waves() { return frame_rows<G>() == 32 ? 3 : 2; }
