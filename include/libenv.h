@@ -102,8 +102,12 @@ LIBENV_API void libenv_observe(libenv_env *env);
 LIBENV_API void libenv_act(libenv_env *env);
 /* vecgame.cpp:95-98 */
 LIBENV_API void libenv_close(libenv_env *env);
-/* vecgame.cpp:485-505: per-env state snapshot (this build's own byte format, see
- * procgen_mi355x.h); returns bytes written, -1 if length is too small */
+/* vecgame.cpp:485-505: per-env state in upstream procgen's serialize format (game.cpp:196-255,
+ * basic-abstract-game.cpp:1178-1225, games/*.cpp, END_OF_BUFFER; pg_state.cpp) -- the fork's own
+ * buffer writes are stubs, so the byte layout is parity unpinned beyond the RandGen text.
+ * get_state returns bytes written, -1 if length is too small; set_state of a malformed or
+ * out-of-range state sets a sticky error (procgen_last_error) instead of the reference's fassert.
+ * This build's exact own format is procgen_get/set_snapshot (procgen_mi355x.h). */
 LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length);
 LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length);
 

@@ -65,7 +65,11 @@ LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers 
  * [num_envs][64][64][3], owned by the caller) instead of the library's observation tensor; NULL
  * switches back.  Takes effect for steps enqueued after the call (the target is captured at
  * launch), so a consumer can alternate two buffers and read / all-gather step t's observations
- * while step t+1 renders (procgen_amd/gather.py).  Every step rewrites every env's frame. */
+ * while step t+1 renders (procgen_amd/gather.py).  Every step rewrites every env's frame.
+ * The library keeps the raw pointer: the caller must switch back (NULL) before freeing d_rgb.
+ * set_state / procgen_set_snapshot / procgen_set_latent_state re-render every env into the bound
+ * buffer on the env's stream: a caller still reading it on another stream orders that first
+ * (ObsGather.sync_engine). */
 LIBENV_API int procgen_set_obs_buffer(libenv_env *env, void *d_rgb);
 /* Copy the outputs of `count` envs (ids env_ids[k]) to host arrays of `count` rows after the
  * enqueued steps finish; any pointer may be NULL.  For consumers (and tests) that sample a few
@@ -104,6 +108,10 @@ LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n);
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
 /* Diagnostic builds only (libprocgen_mi355x_prof.so): per-phase cycle sums, out[16]. */
 LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out);
+/* Diagnostic builds: the raw per-env buffer behind procgen_profile_read, uint64 [num_envs][16]
+ * (PG_CENSUS builds: per launch, words 0-2 / 8-10 = the step / render wave's start and end on the
+ * 100 MHz clock and its HW_ID | XCC_ID << 32). */
+LIBENV_API int procgen_profile_raw(libenv_env *env, uint64_t *out);
 /* Self-test of libm-dependent device arithmetic on device buffers (tests/test_gpu_libm.py):
  * which = 0: bigfish fish radius 1.75 * pow(u, 1.4) + .25 (bigfish.cpp:84) for n floats u (float out);
  * 1: QTransform::rotate matrix of an entity rotation (4 doubles out); 2: face_direction rotation of

@@ -4555,8 +4555,716 @@ static void qt_fill_rectf(uint32_t *canvas, double x, double y, double w, double
     qt_fill_rect_int(canvas, x1, y1, x2 - x1, y2 - y1, argb);
 }
 
-/* ================================================================== render (basic-abstract-game.cpp) */
 typedef struct { double x, y, w, h; } RectD;
+
+/* ================================================================== AssetGen (assetgen.cpp) and the
+ * Qt 5.9 raster paths it paints with, on a canvas of any size: fillRect(QRectF, QColor) (opaque,
+ * alpha 200 SourceOver, transparent Source), drawEllipse(QRectF) with a solid brush (the
+ * non-antialiased path filler: QBezier flattening -> QOutlineMapper 26.6 outline -> QRasterizer's
+ * scan converter) and a 1-px pen (QCosmeticStroker, aliased).  Pinned against the reference's own
+ * assetgen.cpp compiled with the real Qt 5.9.7 of this image (oracle/_ref/libref_qt.so,
+ * tests/test_assetgen_pins.py). */
+typedef struct {
+    uint32_t *px;
+    int w, h;
+    int fmt;    /* QFMT_RGB32 (backgrounds) or QFMT_ARGB32 (generated sprites, not premultiplied) */
+    int source; /* CompositionMode_Source (paint_shape_resource) instead of SourceOver */
+} AgCanvas;
+enum { QFMT_ARGB32 = 5 };
+
+static uint32_t qt_div_65535(uint32_t x) { return (x + (x >> 16) + 0x8000u) >> 16; }
+static uint32_t qt_div_257(uint32_t x) { x += 128u; return (x - (x >> 8)) >> 8; } /* QRgba64::div_257 */
+/* qPremultiply(QColor::rgba64()).toArgb32(): the raster engine's solid colour (QSpanData::setup) */
+static uint32_t qt_solid_premul(uint32_t argb) {
+    const uint32_t a = (argb >> 24) * 257u;
+    uint32_t out = qt_div_257(a) << 24;
+    for (int s = 16; s >= 0; s -= 8) out |= qt_div_257(qt_div_65535(((argb >> s) & 255u) * 257u * a)) << s;
+    return out;
+}
+/* qUnpremultiply (qrgb.h / qdrawhelper: ARGB32PM -> ARGB32 store) */
+static uint32_t qt_unpremultiply(uint32_t p) {
+    const uint32_t a = p >> 24;
+    if (a == 255) return p;
+    if (a == 0) return 0;
+    const uint32_t inv = (255u * 0x10000u + a / 2) / a; /* qt_inv_premul_factor */
+    uint32_t r = (((p >> 16) & 255u) * inv + 0x8000u) >> 16;
+    uint32_t g = (((p >> 8) & 255u) * inv + 0x8000u) >> 16;
+    uint32_t b = ((p & 255u) * inv + 0x8000u) >> 16;
+    return (a << 24) | (r << 16) | (g << 8) | b;
+}
+
+/* one coverage-255 span [x0, x1) of row y in the solid colour `pm` (premultiplied) */
+static void ag_span(AgCanvas *c, int y, int x0, int x1, uint32_t pm) {
+    if (y < 0 || y >= c->h) return;
+    if (x0 < 0) x0 = 0;
+    if (x1 > c->w) x1 = c->w;
+    uint32_t *row = c->px + (size_t)y * c->w;
+    const uint32_t a = pm >> 24;
+    for (int x = x0; x < x1; x++) {
+        if (c->source || a == 255) {
+            row[x] = c->fmt == QFMT_ARGB32 ? qt_unpremultiply(pm) : (pm | 0xff000000u);
+        } else {
+            /* comp_func_solid_SourceOver on the premultiplied destination (ARGB32 is fetched
+             * premultiplied and stored back unpremultiplied) */
+            uint32_t d = row[x];
+            if (c->fmt == QFMT_ARGB32) {
+                const uint32_t da = d >> 24;
+                d = da == 255 ? d : (da == 0 ? 0 : BYTE_MUL(d | 0xff000000u, da) & 0x00ffffffu) | (da << 24);
+            }
+            d = pm + BYTE_MUL(d, 255u - a);
+            row[x] = c->fmt == QFMT_ARGB32 ? qt_unpremultiply(d) : d;
+        }
+    }
+}
+
+/* QPainter::fillRect(QRectF, QColor): QRasterPaintEngine::fillRect -> fillRect_normalized of
+ * toNormalizedFillRect (qRound of the edges); a fully transparent colour under SourceOver paints
+ * nothing */
+static void ag_fill_rectf(AgCanvas *c, double x, double y, double w, double h, uint32_t argb) {
+    const uint32_t pm = qt_solid_premul(argb);
+    if ((pm >> 24) == 0 && !c->source) return;
+    int x1 = qRound(x), y1 = qRound(y), x2 = qRound(x + w), y2 = qRound(y + h);
+    if (x2 < x1) { int t = x1; x1 = x2; x2 = t; }
+    if (y2 < y1) { int t = y1; y1 = y2; y2 = t; }
+    if (y1 < 0) y1 = 0;
+    if (y2 > c->h) y2 = c->h;
+    if (c->fmt == QFMT_ARGB32 && (c->source || (pm >> 24) == 255)) {
+        /* qt_rectfill_nonpremul_argb32: the premultiplied QRgba64 unpremultiplied at 16 bits */
+        const uint32_t a16 = (argb >> 24) * 257u;
+        uint32_t v = argb;
+        if (a16 != 0 && a16 != 65535) {
+            v = (argb >> 24) << 24;
+            for (int sh = 16; sh >= 0; sh -= 8) {
+                const uint32_t p16 = qt_div_65535(((argb >> sh) & 255u) * 257u * a16);
+                v |= qt_div_257((p16 * 65535u + a16 / 2) / a16) << sh;
+            }
+        } else if (a16 == 0) {
+            v = 0;
+        }
+        if (x1 < 0) x1 = 0;
+        if (x2 > c->w) x2 = c->w;
+        for (int yy = y1; yy < y2; yy++)
+            for (int xx = x1; xx < x2; xx++) c->px[(size_t)yy * c->w + xx] = v;
+        return;
+    }
+    for (int yy = y1; yy < y2; yy++) ag_span(c, yy, x1, x2, pm);
+}
+
+/* ---- drawEllipse(QRectF): QPaintEngineEx::drawEllipse -> qt_curves_for_arc(rect, 0, -360) */
+#define QT_PATH_KAPPA 0.5522847498
+typedef struct { double x, y; } PtD;
+static void qt_ellipse_points(double x, double y, double w, double h, PtD pts[13]) {
+    const double w2 = w / 2, w2k = w2 * QT_PATH_KAPPA, h2 = h / 2, h2k = h2 * QT_PATH_KAPPA;
+    const PtD p[13] = {{x + w, y + h2},
+                       {x + w, y + h2 + h2k}, {x + w2 + w2k, y + h}, {x + w2, y + h},
+                       {x + w2 - w2k, y + h}, {x, y + h2 + h2k}, {x, y + h2},
+                       {x, y + h2 - h2k}, {x + w2 - w2k, y}, {x + w2, y},
+                       {x + w2 + w2k, y}, {x + w, y + h2 - h2k}, {x + w, y + h2}};
+    memcpy(pts, p, sizeof(p));
+}
+
+/* QBezier::split (qbezier_p.h), alias-safe in the order Qt writes */
+typedef struct { double x1, y1, x2, y2, x3, y3, x4, y4; } QBez;
+static void qbez_split(const QBez *b, QBez *first, QBez *second) {
+    const QBez s = *b;
+    double c = (s.x2 + s.x3) * .5;
+    first->x2 = (s.x1 + s.x2) * .5;
+    second->x3 = (s.x3 + s.x4) * .5;
+    first->x1 = s.x1;
+    second->x4 = s.x4;
+    first->x3 = (first->x2 + c) * .5;
+    second->x2 = (second->x3 + c) * .5;
+    first->x4 = second->x1 = (first->x3 + second->x2) * .5;
+    c = (s.y2 + s.y3) * .5;
+    first->y2 = (s.y1 + s.y2) * .5;
+    second->y3 = (s.y3 + s.y4) * .5;
+    first->y1 = s.y1;
+    second->y4 = s.y4;
+    first->y3 = (first->y2 + c) * .5;
+    second->y2 = (second->y3 + c) * .5;
+    first->y4 = second->y1 = (first->y3 + second->y2) * .5;
+}
+/* QBezier::addToPolygon(threshold): appends the end points of the flattened pieces */
+static int qbez_flatten(QBez b0, double threshold, PtD *out, int n) {
+    QBez st[10];
+    int lv[10];
+    st[0] = b0;
+    lv[0] = 9;
+    int top = 0;
+    while (top >= 0) {
+        QBez *b = &st[top];
+        double y4y1 = b->y4 - b->y1, x4x1 = b->x4 - b->x1;
+        double l = fabs(x4x1) + fabs(y4y1), d;
+        if (l > 1.) {
+            d = fabs((x4x1) * (b->y1 - b->y2) - (y4y1) * (b->x1 - b->x2)) +
+                fabs((x4x1) * (b->y1 - b->y3) - (y4y1) * (b->x1 - b->x3));
+        } else {
+            d = fabs(b->x1 - b->x2) + fabs(b->y1 - b->y2) + fabs(b->x1 - b->x3) + fabs(b->y1 - b->y3);
+            l = 1.;
+        }
+        if (d < threshold * l || lv[top] == 0) {
+            out[n].x = b->x4;
+            out[n].y = b->y4;
+            n++;
+            top--;
+        } else {
+            QBez first, second;
+            qbez_split(b, &first, &second);
+            st[top] = second;
+            st[top + 1] = first;
+            lv[top + 1] = --lv[top];
+            top++;
+        }
+    }
+    return n;
+}
+
+/* QRasterizer / QScanConverter (non-antialiased fill of a 26.6 outline, no legacy rounding) */
+typedef struct { int x, delta, top, bottom, winding; } ScanLine;
+static int64_t q16mul(int64_t a, int64_t b) { return (a * b) >> 16; }
+#define AG_MAX_LINES 512
+typedef struct {
+    int top, bottom, leftFP, rightFP;
+    ScanLine lines[AG_MAX_LINES];
+    int n;
+} ScanConv;
+static void sc_add(ScanConv *s, int x, int delta, int top, int bottom, int winding) {
+    if (s->n < AG_MAX_LINES) {
+        ScanLine l = {x, delta, top, bottom, winding};
+        s->lines[s->n++] = l;
+    }
+}
+/* QScanConverter::clip: true when the whole line was replaced by edge lines */
+static bool sc_clip(ScanConv *s, int *xFP, int *iTop, int *iBottom, int slopeFP, int edgeFP, int winding) {
+    const bool right = edgeFP == s->rightFP;
+    if (*xFP == edgeFP) {
+        if ((slopeFP > 0) ^ right) return false;
+        sc_add(s, edgeFP, 0, *iTop, *iBottom, winding);
+        return true;
+    }
+    const int lastFP = *xFP + slopeFP * (*iBottom - *iTop);
+    if (lastFP == edgeFP) {
+        if ((slopeFP < 0) ^ right) return false;
+        sc_add(s, edgeFP, 0, *iTop, *iBottom, winding);
+        return true;
+    }
+    if ((lastFP < edgeFP) ^ (*xFP < edgeFP)) {
+        const int deltaY = (int)((edgeFP - *xFP) / (slopeFP / 65536.));
+        if ((*xFP < edgeFP) ^ right) {
+            const int iHeight = (deltaY + 1) >> 16;
+            const int iMiddle = *iTop + iHeight;
+            sc_add(s, edgeFP, 0, *iTop, iMiddle, winding);
+            if (iMiddle != *iBottom) {
+                *xFP += slopeFP * (iHeight + 1);
+                *iTop = iMiddle + 1;
+            } else {
+                return true;
+            }
+        } else {
+            const int iHeight = deltaY >> 16;
+            const int iMiddle = *iTop + iHeight;
+            if (iMiddle != *iBottom) {
+                sc_add(s, edgeFP, 0, iMiddle + 1, *iBottom, winding);
+                *iBottom = iMiddle;
+            }
+        }
+        return false;
+    } else if ((*xFP < edgeFP) ^ right) {
+        sc_add(s, edgeFP, 0, *iTop, *iBottom, winding);
+        return true;
+    }
+    return false;
+}
+static void sc_merge_line(ScanConv *s, int ax, int ay, int bx, int by) {
+    int winding = 1;
+    if (ay > by) {
+        int t = ax; ax = bx; bx = t;
+        t = ay; ay = by; by = t;
+        winding = -1;
+    }
+    int iTop = (ay + 32) >> 6, iBottom = (by - 32) >> 6;
+    if (iTop < s->top) iTop = s->top;
+    if (iBottom > s->bottom) iBottom = s->bottom;
+    if (iTop > iBottom) return;
+    const int aFP = 65536 / 2 + ax * 1024;
+    if (bx == ax) {
+        int x = aFP < s->leftFP ? s->leftFP : (aFP > s->rightFP ? s->rightFP : aFP);
+        sc_add(s, x, 0, iTop, iBottom, winding);
+        return;
+    }
+    const double slope = (double)(bx - ax) / (double)(by - ay);
+    const int slopeFP = (int)(slope * 65536.);
+    int xFP = aFP + (int)q16mul(slopeFP, (int64_t)iTop * 65536 + 65536 / 2 - (int64_t)ay * 1024);
+    if (sc_clip(s, &xFP, &iTop, &iBottom, slopeFP, s->leftFP, winding)) return;
+    if (sc_clip(s, &xFP, &iTop, &iBottom, slopeFP, s->rightFP, winding)) return;
+    sc_add(s, xFP, slopeFP, iTop, iBottom, winding);
+}
+/* emit the spans of every row (winding fill of the ellipse's single convex contour: the rows'
+ * crossings sorted by x, spans where the winding is non-zero) */
+static void sc_end(ScanConv *s, AgCanvas *c, uint32_t pm) {
+    for (int y = s->top; y <= s->bottom; y++) {
+        int xs[AG_MAX_LINES], ws[AG_MAX_LINES], k = 0;
+        for (int i = 0; i < s->n; i++) {
+            const ScanLine *l = &s->lines[i];
+            if (y < l->top || y > l->bottom) continue;
+            const int x = (int)(((int64_t)l->x + (int64_t)l->delta * (y - l->top)) >> 16);
+            int j = k++;
+            while (j > 0 && xs[j - 1] > x) { xs[j] = xs[j - 1]; ws[j] = ws[j - 1]; j--; }
+            xs[j] = x;
+            ws[j] = l->winding;
+        }
+        int x = 0, wind = 0;
+        for (int i = 0; i < k; i++) {
+            if (wind != 0 && xs[i] > x) ag_span(c, y, x, xs[i], pm);
+            x = xs[i];
+            wind += ws[i];
+        }
+    }
+}
+/* QOutlineMapper's qreal_to_fixed_26_6 rounds (pinned: truncating here mismatches Qt) */
+static int qt_fixed_26_6(double v) { return qRound(v * 64); }
+
+static void ag_fill_ellipse(AgCanvas *c, const PtD pts[13], uint32_t pm) {
+    PtD poly[4 * 1100];
+    int n = 0;
+    poly[n++] = pts[0];
+    for (int k = 0; k < 4; k++) {
+        QBez b = {poly[n - 1].x, poly[n - 1].y, pts[3 * k + 1].x, pts[3 * k + 1].y, pts[3 * k + 2].x, pts[3 * k + 2].y,
+                  pts[3 * k + 3].x, pts[3 * k + 3].y};
+        n = qbez_flatten(b, 0.25, poly, n);
+    }
+    /* closeSubpath: the end point equals the start, nothing added */
+    int fx[4 * 1100], fy[4 * 1100];
+    int miny = 0x7fffffff, maxy = -0x7fffffff;
+    for (int i = 0; i < n; i++) {
+        fx[i] = qt_fixed_26_6(poly[i].x);
+        fy[i] = qt_fixed_26_6(poly[i].y);
+        if (fy[i] < miny) miny = fy[i];
+        if (fy[i] > maxy) maxy = fy[i];
+    }
+    ScanConv *s = (ScanConv *)malloc(sizeof(ScanConv));
+    s->top = (miny + 32) >> 6;
+    if (s->top < 0) s->top = 0;
+    s->bottom = (maxy - 32) >> 6;
+    if (s->bottom > c->h - 1) s->bottom = c->h - 1;
+    s->leftFP = 0;
+    s->rightFP = c->w * 65536; /* IntToQ16Dot16(clip right + 1) */
+    s->n = 0;
+    if (s->top <= s->bottom) {
+        for (int i = 0; i + 1 < n; i++) sc_merge_line(s, fx[i], fy[i], fx[i + 1], fy[i + 1]);
+        sc_end(s, c, pm);
+    }
+    free(s);
+}
+
+/* ---- QCosmeticStroker (aliased, solid, no dash) for a 1-px pen (qcosmeticstroker.cpp) */
+enum { CS_T2B = 1, CS_B2T = 2, CS_L2R = 4, CS_R2L = 8, CS_VMASK = 3, CS_HMASK = 12 };
+enum { CS_NOCAPS = 0, CS_CAPBEGIN = 1, CS_CAPEND = 2 };
+#define CS_MAXSUB 6 /* renderCubic's maxSubDivisions */
+typedef struct {
+    AgCanvas *c;
+    uint32_t pm;
+    double xmin, xmax, ymin, ymax;
+    int lastx, lasty, lastDir;
+    bool lastAxisAligned;
+} CStroker;
+#define CS_INT_MIN (-2147483647 - 1)
+static int toF26Dot6(double v) { return (int)(v * 64.); } /* the stroker truncates */
+static int F16Dot16FixedDiv(int x, int y) {
+    if (abs(x) > 0x7fff) return (int)(((int64_t)x * 65536) / y);
+    return x * 65536 / y;
+}
+static int swapCaps(int caps) { return ((caps & 1) << 1) | ((caps & 2) >> 1); }
+static void capAdjust(int caps, int *x1, int *x2, int *y, int yinc) {
+    if (caps & CS_CAPBEGIN) {
+        *x1 -= 32;
+        *y -= yinc >> 1;
+    }
+    if (caps & CS_CAPEND) *x2 += 32;
+}
+static void cs_pixel(CStroker *s, int x, int y) {
+    if (x < 0 || x >= s->c->w || y < 0 || y >= s->c->h) return;
+    ag_span(s->c, y, x, x + 1, s->pm);
+}
+/* QCosmeticStroker::clipLine: true = completely outside */
+static bool cs_clip(CStroker *s, double *x1, double *y1, double *x2, double *y2) {
+    if (*x1 < s->xmin) {
+        if (*x2 <= s->xmin) goto clipped;
+        *y1 += (*y2 - *y1) / (*x2 - *x1) * (s->xmin - *x1);
+        *x1 = s->xmin;
+    } else if (*x1 > s->xmax) {
+        if (*x2 >= s->xmax) goto clipped;
+        *y1 += (*y2 - *y1) / (*x2 - *x1) * (s->xmax - *x1);
+        *x1 = s->xmax;
+    }
+    if (*x2 < s->xmin) {
+        s->lastx = CS_INT_MIN;
+        *y2 += (*y2 - *y1) / (*x2 - *x1) * (s->xmin - *x2);
+        *x2 = s->xmin;
+    } else if (*x2 > s->xmax) {
+        s->lastx = CS_INT_MIN;
+        *y2 += (*y2 - *y1) / (*x2 - *x1) * (s->xmax - *x2);
+        *x2 = s->xmax;
+    }
+    if (*y1 < s->ymin) {
+        if (*y2 <= s->ymin) goto clipped;
+        *x1 += (*x2 - *x1) / (*y2 - *y1) * (s->ymin - *y1);
+        *y1 = s->ymin;
+    } else if (*y1 > s->ymax) {
+        if (*y2 >= s->ymax) goto clipped;
+        *x1 += (*x2 - *x1) / (*y2 - *y1) * (s->ymax - *y1);
+        *y1 = s->ymax;
+    }
+    if (*y2 < s->ymin) {
+        s->lastx = CS_INT_MIN;
+        *x2 += (*x2 - *x1) / (*y2 - *y1) * (s->ymin - *y2);
+        *y2 = s->ymin;
+    } else if (*y2 > s->ymax) {
+        s->lastx = CS_INT_MIN;
+        *x2 += (*x2 - *x1) / (*y2 - *y1) * (s->ymax - *y2);
+        *y2 = s->ymax;
+    }
+    return false;
+clipped:
+    s->lastx = CS_INT_MIN;
+    return true;
+}
+/* drawLine<drawPixel, NoDasher>, both branches in one routine: `vert` = major axis y.  a1 / a2 are
+ * the major coordinates (26.6), b1 / b2 the minor ones.  What the black-box probes against Qt 5.9.7
+ * established (tests/test_assetgen_pins.py): a direction reversal (lastDir ^ mask == dir) caps the
+ * path-start end of the new segment -- CapEnd when it is drawn swapped, CapBegin otherwise, but the
+ * duplicate-pixel test still compares the pixel the uncapped segment would start with; the
+ * same-direction dropout test reads |dx| <= 1 && |dy| > 1 in both branches. */
+static void cs_run(CStroker *s, bool vert, int a1, int b1, int a2, int b2, int caps) {
+    int dir = vert ? CS_T2B : CS_L2R;
+    bool swapped = false;
+    if (a1 > a2) {
+        swapped = true;
+        int t = a1; a1 = a2; a2 = t;
+        t = b1; b1 = b2; b2 = t;
+        caps = swapCaps(caps);
+        dir = vert ? CS_B2T : CS_R2L;
+    }
+    const int binc = F16Dot16FixedDiv(b2 - b1, a2 - a1);
+    int b = b1 * 1024;
+    const int mask = vert ? CS_VMASK : CS_HMASK;
+    int rev = 0;
+    if ((s->lastDir ^ mask) == dir && swapped) rev = CS_CAPEND; /* a non-swapped reversal gets no CapBegin */
+    const int round = (binc > 0) ? 32 : 0;
+    capAdjust(caps | rev, &a1, &a2, &b, binc);
+    int a = (a1 + 32) >> 6;
+    int as = (a2 + 32) >> 6;
+    int lasta = s->lastx, lastb = s->lasty; /* in (x, y) terms below */
+    if (a != as) {
+        b += ((a * 64) + round - a1) * binc >> 6;
+        int fa = a, fb = b >> 16;
+        int la = as - 1, lb = (b + (as - a - 1) * binc) >> 16;
+        if (swapped) {
+            int t = fa; fa = la; la = t;
+            t = fb; fb = lb; lb = t;
+        }
+        (void)fa;
+        /* pixels in (x, y) */
+        const int fx = vert ? fb : fa, fy = vert ? fa : fb;
+        int lx = vert ? lb : la, ly = vert ? la : lb;
+        const bool axisAligned = abs(binc) < (1 << 14);
+        if (s->lastx > -1) {
+            if (fx == s->lastx && fy == s->lasty) { /* remove duplicated pixel */
+                if (swapped) {
+                    --as;
+                } else {
+                    ++a;
+                    b += binc;
+                }
+            } else if (s->lastDir != dir &&
+                       (((axisAligned && s->lastAxisAligned) && s->lastx != fx && s->lasty != fy) ||
+                        (abs(s->lastx - fx) > 1 || abs(s->lasty - fy) > 1))) { /* missing pixel: insert */
+                if (swapped) {
+                    ++as;
+                } else {
+                    --a;
+                    b -= binc;
+                }
+            } else if (s->lastDir == dir && abs(s->lastx - fx) <= 1 && abs(s->lasty - fy) > 1) {
+                b += binc >> 1;
+                const int nl = swapped ? (b >> 16) : ((b + (as - a - 1) * binc) >> 16);
+                if (vert) lx = nl;
+                else ly = nl;
+            }
+        }
+        s->lastDir = dir;
+        s->lastAxisAligned = axisAligned;
+        do {
+            if (vert) cs_pixel(s, b >> 16, a);
+            else cs_pixel(s, a, b >> 16);
+            b += binc;
+        } while (++a < as);
+        lasta = lx;
+        lastb = ly;
+    }
+    s->lastx = lasta;
+    s->lasty = lastb;
+}
+static void cs_line(CStroker *s, double rx1, double ry1, double rx2, double ry2, int caps) {
+    if (cs_clip(s, &rx1, &ry1, &rx2, &ry2)) return;
+    const int x1 = toF26Dot6(rx1), y1 = toF26Dot6(ry1), x2 = toF26Dot6(rx2), y2 = toF26Dot6(ry2);
+    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
+    if (dx < dy) cs_run(s, true, y1, x1, y2, x2, caps);
+    else if (dx) cs_run(s, false, x1, y1, x2, y2, caps);
+}
+/* QCosmeticStroker::calculateLastPoint: the closing segment's last pixel and direction */
+static void cs_last_point(CStroker *s, double rx1, double ry1, double rx2, double ry2) {
+    /* Qt 5.9 has no NoDirection: lastDir keeps its value when the closing segment has no pixel */
+    s->lastx = CS_INT_MIN;
+    s->lasty = CS_INT_MIN;
+    if (cs_clip(s, &rx1, &ry1, &rx2, &ry2)) return;
+    int x1 = toF26Dot6(rx1), y1 = toF26Dot6(ry1), x2 = toF26Dot6(rx2), y2 = toF26Dot6(ry2);
+    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
+    if (dx < dy) {
+        bool swapped = false;
+        if (y1 > y2) {
+            swapped = true;
+            int t = y1; y1 = y2; y2 = t;
+            t = x1; x1 = x2; x2 = t;
+        }
+        const int xinc = F16Dot16FixedDiv(x2 - x1, y2 - y1);
+        int x = x1 * 1024;
+        const int y = (y1 + 32) >> 6, ys = (y2 + 32) >> 6;
+        const int round = (xinc > 0) ? 32 : 0;
+        if (y != ys) {
+            x += ((y * 64) + round - y1) * xinc >> 6;
+            if (swapped) {
+                s->lastx = x >> 16;
+                s->lasty = y;
+                s->lastDir = CS_B2T;
+            } else {
+                s->lastx = (x + (ys - y - 1) * xinc) >> 16;
+                s->lasty = ys - 1;
+                s->lastDir = CS_T2B;
+            }
+            s->lastAxisAligned = abs(xinc) < (1 << 14);
+        }
+    } else {
+        if (!dx) return;
+        bool swapped = false;
+        if (x1 > x2) {
+            swapped = true;
+            int t = x1; x1 = x2; x2 = t;
+            t = y1; y1 = y2; y2 = t;
+        }
+        const int yinc = F16Dot16FixedDiv(y2 - y1, x2 - x1);
+        int y = y1 * 1024;
+        const int x = (x1 + 32) >> 6, xs = (x2 + 32) >> 6;
+        const int round = (yinc > 0) ? 32 : 0;
+        if (x != xs) {
+            y += ((x * 64) + round - x1) * yinc >> 6;
+            if (swapped) {
+                s->lastx = x;
+                s->lasty = y >> 16;
+                s->lastDir = CS_R2L;
+            } else {
+                s->lastx = xs - 1;
+                s->lasty = (y + (xs - x - 1) * yinc) >> 16;
+                s->lastDir = CS_L2R;
+            }
+            s->lastAxisAligned = abs(yinc) < (1 << 14);
+        }
+    }
+}
+/* renderCubic / renderCubicSubdivision / splitCubic; points[3] is the start, points[0] the end */
+static void cs_split_cubic(PtD *p) {
+    const double half = .5;
+    double a, b, c, d;
+    p[6].x = p[3].x;
+    c = p[1].x;
+    d = p[2].x;
+    p[1].x = a = (p[0].x + c) * half;
+    p[5].x = b = (p[3].x + d) * half;
+    c = (c + d) * half;
+    p[2].x = a = (a + c) * half;
+    p[4].x = b = (b + c) * half;
+    p[3].x = (a + b) * half;
+    p[6].y = p[3].y;
+    c = p[1].y;
+    d = p[2].y;
+    p[1].y = a = (p[0].y + c) * half;
+    p[5].y = b = (p[3].y + d) * half;
+    c = (c + d) * half;
+    p[2].y = a = (a + c) * half;
+    p[4].y = b = (b + c) * half;
+    p[3].y = (a + b) * half;
+}
+static void cs_cubic_sub(CStroker *s, PtD *p, int level, int caps) {
+    if (level) {
+        const double dx = p[3].x - p[0].x, dy = p[3].y - p[0].y;
+        const double len = ((double).25) * (fabs(dx) + fabs(dy));
+        if (fabs(dx * (p[0].y - p[2].y) - dy * (p[0].x - p[2].x)) >= len ||
+            fabs(dx * (p[0].y - p[1].y) - dy * (p[0].x - p[1].x)) >= len) {
+            cs_split_cubic(p);
+            --level;
+            cs_cubic_sub(s, p + 3, level, caps);
+            cs_cubic_sub(s, p, level, caps);
+            return;
+        }
+    }
+    cs_line(s, p[3].x, p[3].y, p[0].x, p[0].y, caps);
+}
+/* QCosmeticStroker::drawPath of the ellipse's closed subpath: caps off (closed), the last point of
+ * the closing segment (cp2 -> end of the last curve) primes the duplicate / dropout checks */
+static void ag_stroke_ellipse(AgCanvas *c, const PtD pts[13], uint32_t pm) {
+    CStroker s;
+    s.c = c;
+    s.pm = pm;
+    s.xmin = -1;
+    s.xmax = c->w + 1; /* deviceRect.right() + 2 */
+    s.ymin = -1;
+    s.ymax = c->h + 1;
+    s.lastAxisAligned = false;
+    s.lastDir = CS_L2R; /* QCosmeticStroker ctor */
+    s.lastx = CS_INT_MIN;
+    s.lasty = CS_INT_MIN;
+    cs_last_point(&s, pts[11].x, pts[11].y, pts[12].x, pts[12].y);
+    for (int k = 0; k < 4; k++) {
+        PtD p[3 * CS_MAXSUB + 4];
+        p[3] = pts[3 * k];
+        p[2] = pts[3 * k + 1];
+        p[1] = pts[3 * k + 2];
+        p[0] = pts[3 * k + 3];
+        cs_cubic_sub(&s, p, CS_MAXSUB, CS_NOCAPS);
+    }
+}
+
+/* QPainter::drawEllipse(QRectF) with setBrush(QBrush(c1)), setPen(QPen(c2)) (assetgen.cpp:95-99):
+ * the brush fill, then the pen.  Returns -1 for an integral rect, which Qt draws with its own
+ * midpoint-ellipse path instead (QRasterPaintEngine::drawEllipse; not restated: a random float
+ * rect is integral with probability ~1e-10) */
+static int ag_draw_ellipse(AgCanvas *c, double x, double y, double w, double h, uint32_t brush, uint32_t pen, int parts) {
+    if (w <= 0 || h <= 0) return 0; /* QRectF::isNull / empty: qt_curves_for_arc returns nothing */
+    if (x == (int)x && y == (int)y && w == (int)w && h == (int)h) return -1;
+    PtD pts[13];
+    qt_ellipse_points(x, y, w, h, pts);
+    if (parts & 1) ag_fill_ellipse(c, pts, qt_solid_premul(brush));
+    if (parts & 2) ag_stroke_ellipse(c, pts, qt_solid_premul(pen));
+    return 0;
+}
+
+/* ---- AssetGen (assetgen.cpp:3-195); float / double promotion as the C++ source has it */
+typedef struct {
+    MT *rg;
+    float rgb_start[3], rgb_len[3];
+    int rgb_choice[3];
+    float p_rect;
+} ColorGen;
+static void cg_roll(ColorGen *g) { /* :10-20 */
+    for (int i = 0; i < 3; i++) g->rgb_len[i] = rg_rand01(g->rg);
+    for (int i = 0; i < 3; i++) g->rgb_start[i] = rg_rand01(g->rg) * (1 - g->rgb_len[i]);
+    g->p_rect = rg_rand01(g->rg);
+}
+static uint32_t cg_rand_color(ColorGen *g) { /* :22-28, QColor(r, g, b) */
+    for (int i = 0; i < 3; i++) g->rgb_choice[i] = (int)(255 * (rg_rand01(g->rg) * g->rgb_len[i] + g->rgb_start[i]));
+    return 0xff000000u | ((uint32_t)g->rgb_choice[0] << 16) | ((uint32_t)g->rgb_choice[1] << 8) | (uint32_t)g->rgb_choice[2];
+}
+typedef struct {
+    MT *rg;
+    AgCanvas *c;
+    int err; /* an integral ellipse rect (Qt's midpoint path, not restated) */
+} AssetGen;
+static RectD ag_choose_sub_rect(AssetGen *a, RectD rect, float min_dim, float max_dim) { /* :35-51 */
+    const int w = (int)rect.w, h = (int)rect.h;
+    const int smaller = (w > h) ? h : w;
+    const float del_dim = max_dim - min_dim;
+    const float rdx = (rg_rand01(a->rg) * del_dim + min_dim) * smaller;
+    const float rdy = (rg_rand01(a->rg) * del_dim + min_dim) * smaller;
+    const float rx_off = rg_rand01(a->rg) * (w - rdx);
+    const float ry_off = rg_rand01(a->rg) * (h - rdy);
+    RectD r = {rx_off + rect.x, ry_off + rect.y, rdx, rdy};
+    return r;
+}
+static void ag_paint_shape(AssetGen *a, RectD main_rect, ColorGen *cg) { /* :75-102 (split_rect :53-73) */
+    const int k = rg_randn(a->rg, 10);
+    const int num_splits = (k * k) / 50 + 1;
+    const bool is_horizontal = rg_randbool(a->rg);
+    const float x = (float)main_rect.x, y = (float)main_rect.y, w = (float)main_rect.w, h = (float)main_rect.h;
+    const float dw = w / num_splits, dh = h / num_splits;
+    const bool use_rect = rg_randbool(a->rg);
+    const bool regen_colors = rg_randbool(a->rg);
+    uint32_t c1 = cg_rand_color(cg);
+    uint32_t c2 = cg_rand_color(cg);
+    for (int i = 0; i < num_splits; i++) {
+        RectD r;
+        if (is_horizontal) {
+            r.x = x + i * dw; r.y = y; r.w = dw; r.h = h;
+        } else {
+            r.x = x; r.y = y + i * dh; r.w = w; r.h = dh;
+        }
+        if (regen_colors) {
+            c1 = cg_rand_color(cg);
+            c2 = cg_rand_color(cg);
+        }
+        if (use_rect) {
+            ag_fill_rectf(a->c, r.x, r.y, r.w, r.h, c1);
+        } else if (ag_draw_ellipse(a->c, r.x, r.y, r.w, r.h, c1, c2, 3) < 0) {
+            a->err = 1;
+        }
+    }
+}
+static void ag_paint_rect_resource(AssetGen *a, RectD rect, int num_recurse, int blotch_scale) { /* :104-132 */
+    ColorGen cg = {a->rg, {0}, {0}, {0}, 0};
+    cg_roll(&cg);
+    const uint32_t bgcolor = cg_rand_color(&cg);
+    ag_fill_rectf(a->c, rect.x, rect.y, rect.w, rect.h, bgcolor);
+    const float scale = (float)(.3 + .7 * (double)rg_rand01(a->rg));
+    const float max_rand_dim = (float)(.5 * (double)scale);
+    const float min_rand_dim = (float)(.05 * (double)scale);
+    const int num_blotches = rg_randint(a->rg, blotch_scale, 2 * blotch_scale);
+    const float p_recurse = (float)((double)rg_rand01(a->rg) * .75);
+    for (int j = 0; j < num_blotches; j++) {
+        const RectD dst3 = ag_choose_sub_rect(a, rect, min_rand_dim, max_rand_dim);
+        if ((num_recurse > 0) && (rg_rand01(a->rg) < p_recurse)) ag_paint_rect_resource(a, dst3, num_recurse - 1, 10);
+        else ag_paint_shape(a, dst3, &cg);
+    }
+    ag_fill_rectf(a->c, rect.x, rect.y, rect.w, rect.h, (bgcolor & 0x00ffffffu) | (200u << 24)); /* setAlpha(200) */
+}
+static RectD ag_create_bar(AssetGen *a, RectD rect, bool is_horizontal) { /* :134-149 */
+    const float k1 = (float)(.45 + (double)rg_rand01(a->rg) * .4);
+    const float k2 = (float)(.45 + (double)rg_rand01(a->rg) * .4);
+    const float w = (float)(rect.w * k1 * k1);
+    const float h = (float)(rect.h * k2 * k2);
+    const float pct = rg_rand01(a->rg);
+    RectD r;
+    if (is_horizontal == 0) {
+        r.x = 0; r.y = (rect.h - h) * pct; r.w = rect.w; r.h = h;
+    } else {
+        r.x = (rect.h - w) * pct; r.y = 0; r.w = w; r.h = rect.h; /* the reference uses height() for x */
+    }
+    return r;
+}
+static void ag_paint_shape_resource(AssetGen *a, RectD rect) { /* :151-184 */
+    ColorGen cg = {a->rg, {0}, {0}, {0}, 0};
+    cg_roll(&cg);
+    const bool horizontal_first = rg_randbool(a->rg);
+    const int nbar1 = rg_randn(a->rg, 3) / 2 + 1;
+    const int nbar2 = rg_randn(a->rg, 3) / 2 + 1;
+    const int saved = a->c->source;
+    a->c->source = 1; /* save(); setCompositionMode(CompositionMode_Source) */
+    ag_fill_rectf(a->c, rect.x, rect.y, rect.w, rect.h, 0x00000000u);
+    for (int i = 0; i < nbar1; i++) ag_paint_shape(a, ag_create_bar(a, rect, horizontal_first), &cg);
+    for (int i = 0; i < nbar2; i++) ag_paint_shape(a, ag_create_bar(a, rect, !horizontal_first), &cg);
+    const int num_blotches = rg_randint(a->rg, 1, 5);
+    for (int j = 0; j < num_blotches; j++) ag_paint_shape(a, ag_choose_sub_rect(a, rect, 0.1f, 0.6f), &cg);
+    a->c->source = saved; /* restore() */
+}
+/* AssetGen::generate_resource (:186-195) on the canvas; returns 0, or -1 when an integral ellipse rect
+ * was met */
+static int ag_generate_resource(MT *rg, AgCanvas *c, int num_recurse, int blotch_scale, bool is_rect) {
+    AssetGen a = {rg, c, 0};
+    RectD rect = {0, 0, (double)c->w, (double)c->h};
+    if (is_rect) ag_paint_rect_resource(&a, rect, num_recurse, blotch_scale);
+    else ag_paint_shape_resource(&a, rect);
+    return a.err ? -1 : 0;
+}
+
+/* ================================================================== render (basic-abstract-game.cpp) */
 
 static void prepare_for_drawing(Game *g, float rect_height) { /* :828-847 */
     g->center_x = (float)(g->main_width * .5);
@@ -5223,6 +5931,31 @@ int oracle_debug(void *h, int i, int32_t *out, int n) {
     return 16;
 }
 
+/* env i's entity list, 31 words per entity in Entity::serialize's order (entity.cpp:90-134: the
+ * struct's member order above), floats as their bits, bools as 0 / 1; returns the entity count
+ * (the caller's buffer holds cap entities) */
+int oracle_entity_words(void *h, int i, int32_t *out, int cap) {
+    Vec *v = (Vec *)h;
+    Game *g = &v->games[i];
+    for (int k = 0; k < g->num_ents && k < cap; k++) {
+        const Entity *e = &g->ents[k];
+        int32_t *o = out + (size_t)k * 31;
+        float f6[6] = {e->x, e->y, e->vx, e->vy, e->rx, e->ry};
+        memcpy(o, f6, sizeof(f6));
+        o[6] = e->type; o[7] = e->image_type; o[8] = e->image_theme; o[9] = e->render_z;
+        o[10] = e->will_erase; o[11] = e->collides_with_entities;
+        float f3[3] = {e->collision_margin, e->rotation, e->vrot};
+        memcpy(o + 12, f3, sizeof(f3));
+        o[15] = e->is_reflected; o[16] = e->fire_time; o[17] = e->spawn_time; o[18] = e->life_time;
+        o[19] = e->expire_time; o[20] = e->use_abs_coords;
+        memcpy(o + 21, &e->friction, 4);
+        o[22] = e->smart_step; o[23] = e->avoids_collisions; o[24] = e->auto_erase;
+        float f7[6] = {e->alpha, e->health, e->theta, e->grow_rate, e->alpha_decay, e->climber_spawn_x};
+        memcpy(o + 25, f7, sizeof(f7));
+    }
+    return g->num_ents;
+}
+
 /* ================================================================== pinning helpers */
 void oracle_mt_stream(uint32_t seed, uint32_t *out, int n) {
     MT m;
@@ -5351,4 +6084,49 @@ int oracle_entities(void *h, int i, int32_t *out, int max_ents) {
         memcpy(&out[5 * k + 4], &e->alpha, 4);
     }
     return g->num_ents;
+}
+
+/* ---- AssetGen pins (tests/test_assetgen_pins.py) */
+/* mirror of ref_qt_shape (oracle/ref_qt_harness.cpp): kind 0 fillRect, 1 ellipse brush + pen,
+ * 2 brush only, 3 pen only */
+int oracle_qt_shape(int w, int h, int fmt, int kind, double x, double y, double rw, double rh, uint32_t c1, uint32_t c2,
+                    int source, uint32_t *inout) {
+    AgCanvas c = {inout, w, h, fmt, source};
+    if (kind == 0) {
+        ag_fill_rectf(&c, x, y, rw, rh, c1);
+        return 0;
+    }
+    return ag_draw_ellipse(&c, x, y, rw, rh, c1, c2, kind == 1 ? 3 : (kind == 2 ? 1 : 2));
+}
+/* mirror of ref_qt_polyline: QCosmeticStroker::drawPath of a polyline (caps on an open path's ends) */
+void oracle_qt_polyline(int w, int h, const double *pts, int n, uint32_t color, uint32_t *inout) {
+    AgCanvas c = {inout, w, h, QFMT_RGB32, 0};
+    CStroker s;
+    s.c = &c;
+    s.pm = qt_solid_premul(color);
+    s.xmin = -1; s.xmax = w + 1; s.ymin = -1; s.ymax = h + 1;
+    s.lastAxisAligned = false;
+    s.lastDir = CS_L2R;
+    s.lastx = CS_INT_MIN;
+    s.lasty = CS_INT_MIN;
+    const bool closed = pts[0] == pts[2 * (n - 1)] && pts[1] == pts[2 * (n - 1) + 1];
+    if (closed) cs_last_point(&s, pts[2 * (n - 2)], pts[2 * (n - 2) + 1], pts[2 * (n - 1)], pts[2 * (n - 1) + 1]);
+    int caps = closed ? CS_NOCAPS : CS_CAPBEGIN;
+    for (int i = 1; i < n; i++) {
+        if (!closed && i == n - 1) caps |= CS_CAPEND;
+        cs_line(&s, pts[2 * (i - 1)], pts[2 * (i - 1) + 1], pts[2 * i], pts[2 * i + 1], caps);
+        caps = CS_NOCAPS;
+    }
+}
+/* mirror of ref_generate_resource: returns the generator's next randint() after painting, via *next */
+int oracle_generate_resource(int32_t seed, int pre_draws, int w, int h, int fmt, int num_recurse, int blotch_scale,
+                             int is_rect, uint32_t init, uint32_t *out, int32_t *next) {
+    MT m;
+    rg_seed(&m, seed);
+    for (int i = 0; i < pre_draws; i++) rg_randint0(&m);
+    for (size_t i = 0; i < (size_t)w * h; i++) out[i] = init;
+    AgCanvas c = {out, w, h, fmt, 0};
+    int rc = ag_generate_resource(&m, &c, num_recurse, blotch_scale, is_rect != 0);
+    *next = rg_randint0(&m);
+    return rc;
 }

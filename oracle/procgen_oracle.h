@@ -69,6 +69,14 @@ int oracle_miner_set_state(void *h, int i, const int32_t *grid, int grid_width, 
 /* debug: a few scalars of env i: [num_entities, cur_time, agent_x_bits, agent_y_bits,
  * background_index, wall_theme, episodes... ] (see .c) */
 int oracle_debug(void *h, int i, int32_t *out, int n);
+/* env i's entity list, 31 words per entity in Entity::serialize order; returns the count */
+int oracle_entity_words(void *h, int i, int32_t *out, int cap);
+/* AssetGen pins (assetgen.cpp + the Qt raster paths it uses) */
+int oracle_qt_shape(int w, int h, int fmt, int kind, double x, double y, double rw, double rh, uint32_t c1, uint32_t c2,
+                    int source, uint32_t *inout);
+void oracle_qt_polyline(int w, int h, const double *pts, int n, uint32_t color, uint32_t *inout);
+int oracle_generate_resource(int32_t seed, int pre_draws, int w, int h, int fmt, int num_recurse, int blotch_scale,
+                             int is_rect, uint32_t init, uint32_t *out, int32_t *next);
 
 /* ------------ pinning helpers (compared against oracle/_ref and Qt goldens) ------------ */
 /* fill out[n] with successive 32-bit outputs of an MT19937 seeded with `seed` */

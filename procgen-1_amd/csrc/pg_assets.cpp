@@ -109,9 +109,23 @@ bool zip_open(const std::string &path, ZipFile *z, std::string *err) {
             uint16_t id = rd16(&b[x]), len = rd16(&b[x + 2]);
             if (id == 1) {
                 size_t q = x + 4;
-                if (e.usize == 0xFFFFFFFFu) { e.usize = rd64(&b[q]); q += 8; }
-                if (e.csize == 0xFFFFFFFFu) { e.csize = rd64(&b[q]); q += 8; }
-                if (e.local_offset == 0xFFFFFFFFu) e.local_offset = rd64(&b[q]);
+                const size_t qend = x + 4 + len; // every 8-byte field must lie inside this record
+                if (qend > p + 46 + nl + xl) {
+                    *err = path + ": truncated zip64 extra field";
+                    return false;
+                }
+                if (e.usize == 0xFFFFFFFFu) {
+                    if (q + 8 > qend) { *err = path + ": short zip64 extra field"; return false; }
+                    e.usize = rd64(&b[q]); q += 8;
+                }
+                if (e.csize == 0xFFFFFFFFu) {
+                    if (q + 8 > qend) { *err = path + ": short zip64 extra field"; return false; }
+                    e.csize = rd64(&b[q]); q += 8;
+                }
+                if (e.local_offset == 0xFFFFFFFFu) {
+                    if (q + 8 > qend) { *err = path + ": short zip64 extra field"; return false; }
+                    e.local_offset = rd64(&b[q]);
+                }
             }
             x += 4 + len;
         }
@@ -195,13 +209,22 @@ bool npy_parse(const std::vector<uint8_t> &raw, const std::string &what, NpyArra
         *err = what + ": malformed .npy header";
         return false;
     }
-    size_t q0 = h.find('\'', d + 8), q1 = h.find('\'', q0 + 1);
+    size_t q0 = h.find('\'', d + 8), q1 = q0 == std::string::npos ? q0 : h.find('\'', q0 + 1);
+    const size_t fo = h.find_first_not_of(' ', f + 16);
+    if (q1 == std::string::npos || fo == std::string::npos) {
+        *err = what + ": malformed .npy header";
+        return false;
+    }
     a->descr = h.substr(q0 + 1, q1 - q0 - 1);
-    if (h.compare(h.find_first_not_of(' ', f + 16), 5, "False") != 0) {
+    if (h.compare(fo, 5, "False") != 0) {
         *err = what + ": fortran-order arrays are not supported";
         return false;
     }
-    size_t p0 = h.find('(', s), p1 = h.find(')', p0);
+    size_t p0 = h.find('(', s), p1 = p0 == std::string::npos ? p0 : h.find(')', p0);
+    if (p1 == std::string::npos) {
+        *err = what + ": malformed .npy shape";
+        return false;
+    }
     std::string dims = h.substr(p0 + 1, p1 - p0 - 1);
     a->shape.clear();
     std::stringstream ss(dims);
@@ -304,7 +327,22 @@ std::string pg_default_asset_root() {
     return "assets";
 }
 
+static bool atlas_load(const std::string &root, const std::vector<int> &games, PGAtlasHost *out, std::string *err);
+
+// The C ABI callers (libenv_make, procgen_atlas_host) must never see a C++ exception: a corrupt
+// pack (a malformed number in an .npy header, an allocation failure) becomes an error message.
 bool pg_atlas_load(const std::string &root, const std::vector<int> &games, PGAtlasHost *out, std::string *err) {
+    try {
+        return atlas_load(root, games, out, err);
+    } catch (const std::exception &e) {
+        *err = std::string("asset load failed: ") + e.what();
+    } catch (...) {
+        *err = "asset load failed";
+    }
+    return false;
+}
+
+static bool atlas_load(const std::string &root, const std::vector<int> &games, PGAtlasHost *out, std::string *err) {
     const int NG = 16, SLOTS = 1000, MAXBG = 64;
     out->pixels.clear();
     out->sprites.assign((size_t)NG * SLOTS * 4, 0);

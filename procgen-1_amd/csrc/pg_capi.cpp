@@ -1107,6 +1107,15 @@ LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out) {
     return 0;
 }
 
+// the whole per-env diagnostic buffer, [num_envs][16] words (PG_PROFILE phase sums or PG_CENSUS
+// wave records: words 0-2 step, 8-10 render)
+LIBENV_API int procgen_profile_raw(libenv_env *env, uint64_t *out) {
+    VecEnv *v = (VecEnv *)env;
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    HIPCHECK(copy_sync(v, out, v->dev.prof, (size_t)v->num_envs * 16 * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length) {
     VecEnv *v = (VecEnv *)env;
     if (env_idx < 0 || env_idx >= v->num_envs || length < (int)sizeof(PGEnv)) return -1;
@@ -1127,6 +1136,37 @@ static const int GAME_MAX_DIM[PG_NUM_GAMES][2] = {
     {20, 20}, {20, 20}, {60, 60}, {19, 19}, {20, 64}, {64, 64}, {40, 40}, {20, 60},
     {23, 23}, {45, 45}, {20, 20}, {31, 31}, {35, 35}, {64, 64}, {20, 20}, {16, 16}};
 static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
+
+// Bounds of every PGEnv member a kernel uses as an array / LDS / table index (shared by the own
+// format and the upstream format, which reaches the device through procgen_set_snapshot too).
+// Returns the reason a state is rejected, or null.
+static const char *validate_env(const VecEnv *v, const PGEnv &s) {
+    if (s.num_ents < 0 || s.num_tail < 0 || s.num_ents + s.num_tail > PG_CAP || s.main_width < 0 ||
+        s.main_height < 0 || s.main_width > GAME_MAX_DIM[s.game_id][0] || s.main_height > GAME_MAX_DIM[s.game_id][1])
+        return "set_state: entity count or world size out of range for the game";
+    if (s.rg_mti < 0 || s.rg_mti > PG_MT_N || s.lsg_mti < 0 || s.lsg_mti > PG_MT_N)
+        return "set_state: RandGen position out of range";
+    const int nbg = v->dev.num_bg[s.game_id];
+    if (s.background_index < 0 || s.background_index >= PG_MAX_BG || (nbg > 0 && s.background_index >= nbg))
+        return "set_state: background_index out of range for the game's backgrounds";
+    if (s.game_id == PG_GAME_LEAPER && (s.num_road_lanes < 0 || s.num_road_lanes > 5 || s.num_water_lanes < 0 ||
+                                        s.num_water_lanes > 5))
+        return "set_state: leaper lane count out of range";
+    if (s.game_id == PG_GAME_BOSSFIGHT &&
+        (s.gs.bf.num_rounds < 1 || s.gs.bf.num_rounds > 5 || s.gs.bf.round_num < 0 || s.gs.bf.attack_mode < 0 ||
+         s.gs.bf.attack_mode > 3))
+        return "set_state: bossfight round counts out of range";
+    if (s.game_id == PG_GAME_HEIST && (s.num_keys < 0 || s.num_keys > 31))
+        return "set_state: heist key count out of range";
+    if (s.game_id == PG_GAME_PLUNDER) {
+        const auto &p = s.gs.pl;
+        if (p.num_lanes < 0 || p.num_lanes > 5 || p.num_current_ship_types < 1 || p.num_current_ship_types > 6)
+            return "set_state: plunder lane / ship-type count out of range";
+        for (int i = 0; i < 6; i++)
+            if (((p.perm >> (4 * i)) & 15u) > 5) return "set_state: plunder image permutation out of range";
+    }
+    return nullptr;
+}
 
 LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, int length) {
     VecEnv *v = (VecEnv *)env;
@@ -1182,9 +1222,8 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
         fail(v, PG_ERR_BAD_OPTION, "set_state: the state belongs to another game than this env slot");
         return;
     }
-    if (s.num_ents < 0 || s.num_tail < 0 || s.num_ents + s.num_tail > PG_CAP || s.main_width < 0 ||
-        s.main_height < 0 || s.main_width > GAME_MAX_DIM[s.game_id][0] || s.main_height > GAME_MAX_DIM[s.game_id][1]) {
-        fail(v, PG_ERR_BAD_OPTION, "set_state: entity count or world size out of range for the game");
+    if (const char *why = validate_env(v, s)) {
+        fail(v, PG_ERR_BAD_OPTION, why);
         return;
     }
     size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail, cells = (size_t)s.main_width * s.main_height;

@@ -282,6 +282,29 @@ struct PTimer {
 #endif
 };
 
+// Occupancy census (diagnostic PG_CENSUS builds only): a wave's start / end on the 100 MHz
+// constant clock and where it ran (HW_ID: wave, SIMD, CU, SE; XCC_ID), so the host can rebuild how
+// many waves of a launch were resident at once (scripts/census.py).
+struct Census {
+#ifdef PG_CENSUS
+    uint64_t t0;
+    DEV void start() { t0 = __builtin_amdgcn_s_memrealtime(); }
+    DEV void flush(uint64_t *p) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // HW_REG_XCC_ID
+        if (threadIdx.x == 0 && p) {
+            p[0] = t0;
+            p[1] = t1;
+            p[2] = (uint64_t)hw | ((uint64_t)xcc << 32);
+        }
+    }
+#else
+    DEV void start() {}
+    DEV void flush(uint64_t *) {}
+#endif
+};
+
 DEV unsigned long long ballot(bool p) { return __ballot(p); }
 DEV int top_bit(unsigned long long m) { return 63 - __clzll(m); }
 

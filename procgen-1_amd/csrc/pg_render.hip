@@ -1460,6 +1460,8 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 
     const int lane = LANE;
     PTimer pt;
+    Census census;
+    census.start();
     pt.start();
 
     // ---- grid type -> sprite table for the fast path (theme_for_grid_obj, image_for_type,
@@ -1938,6 +1940,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
     pt.mark(6);
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
+    census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 
 extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s) {

@@ -79,7 +79,8 @@ template <> struct Scratch<PG_GAME_HEIST> { MGScratch mg; };
 struct RCtx {
     PGDev d;
     int env;
-    PGEnv s;
+    PGEnv &s;        // the env's scalars, staged in LDS for the whole reset (wave-uniform: keeping
+                     // the 512-B struct in VGPRs cost ~128 registers and scratch spills)
     float *E;
     size_t plane, eb;
     uint32_t *mt;    // LDS rand_gen words
@@ -2545,11 +2546,14 @@ DEV void leaper_game_reset(RCtx &c, LeaperScratch *L) {
 
 // ------------------------------------------------------------------ Game::reset
 template <int G>
-DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial) {
-    RCtx c;
-    c.d = d;
-    c.env = env;
-    c.s = d.envs[env];
+DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial,
+                   PGEnv *lds_env) {
+    {
+        const uint2 *src = reinterpret_cast<const uint2 *>(d.envs + env);
+        reinterpret_cast<uint2 *>(lds_env)[LANE] = src[LANE]; // 64 lanes x 8 B = the 512-B PGEnv
+    }
+    wave_sync();
+    RCtx c{d, env, *lds_env};
     c.E = d.ents;
     c.plane = (size_t)d.num_envs * PG_CAP;
     c.eb = (size_t)env * PG_CAP;
@@ -2654,8 +2658,9 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
             d.prev_level_complete[env] = (uint8_t)c.s.sd_level_complete;
         }
         if (c.s.error) atomicOr(d.error_any, 1 << c.s.error);
-        d.envs[env] = c.s;
     }
+    wave_sync();
+    reinterpret_cast<uint2 *>(d.envs + env)[LANE] = reinterpret_cast<const uint2 *>(lds_env)[LANE];
     wave_sync();
 }
 
@@ -2666,12 +2671,13 @@ __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *en
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ __attribute__((aligned(16))) int16_t lds_grid[PG_GRID_MAX];
     __shared__ Scratch<G> scratch;
+    __shared__ __attribute__((aligned(16))) PGEnv lds_env;
     int n = all_envs ? count : d.reset_count[G];
     const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
     PGDev dv = game_view(d, G);
     for (int q = blockIdx.x; q < n; q += gridDim.x) {
         int env = all_envs ? (env_list ? env_list[q] : q) : queue[q];
-        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0);
+        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0, &lds_env);
     }
 }
 

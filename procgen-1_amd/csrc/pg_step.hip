@@ -2702,6 +2702,8 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     c.nlist = 0;
     c.grid8 = lds_grid;
     c.grid8_ok = false;
+    Census census;
+    census.start();
     c.pt.start();
     load_grid_lds(c);
 
@@ -2775,6 +2777,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     }
     c.pt.mark(6);
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
+    census.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 }
 
 } // namespace

@@ -87,6 +87,7 @@ SIGNATURES = {
     "procgen_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "procgen_debug_env": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "procgen_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "procgen_profile_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_selftest_libm": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p]),
 }

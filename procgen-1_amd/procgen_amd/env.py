@@ -295,7 +295,8 @@ class BaseProcgenEnv:
         _check(self._lib, self._handle, rc)
 
     def set_obs_buffer(self, ptr):
-        """Render later steps into the device buffer at `ptr` (uint8 [num,64,64,3]); None = own tensor."""
+        """Render later steps into the device buffer at `ptr` (uint8 [num,64,64,3]); None = own tensor.
+        The engine keeps the raw pointer: unbind (None) before the buffer is freed."""
         rc = self._lib.procgen_set_obs_buffer(self._handle, ptr)
         _check(self._lib, self._handle, rc)
 

@@ -99,3 +99,32 @@ class ObsGather:
 
     def local_obs(self, k):
         return self.local[k]
+
+    def sync_engine(self):
+        """Make the engine stream wait until both outstanding gathers have read their local buffer.
+        Call before anything that renders outside ``step`` (``set_state``, ``set_latent_state``
+        re-render every env into the bound buffer, which a gather may still be reading)."""
+        for ev in self.gathered:
+            if ev is not None:
+                self.engine.wait_event(ev)
+
+    def close(self):
+        """Unbind: the engine renders into its own tensor again, after every gather has read the
+        local buffers, which may then be freed (the engine keeps a raw pointer while bound)."""
+        if self.bind is None:
+            return
+        self.sync_engine()
+        if self.cuda:
+            for ev in self.gathered:
+                if ev is not None:
+                    ev.synchronize()
+        try:
+            self.bind(None)
+        finally:
+            self.bind = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

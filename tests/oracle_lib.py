@@ -49,6 +49,8 @@ def load():
         lib.oracle_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         lib.oracle_observe.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
         lib.oracle_debug.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        lib.oracle_entity_words.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        lib.oracle_entity_words.restype = ctypes.c_int
         lib.oracle_mt_stream.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
         lib.oracle_randgen_script.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         lib.oracle_qt_replay.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p]
@@ -147,6 +149,12 @@ class OracleEnv:
         out = np.zeros(16, np.int32)
         self.lib.oracle_debug(self.h, i, out.ctypes.data, 16)
         return out
+
+    def entities(self, i, cap=1024):
+        """env i's entity list: int32 [n, 31] in Entity::serialize order (floats as their bits)."""
+        out = np.zeros((cap, 31), np.int32)
+        n = self.lib.oracle_entity_words(self.h, i, out.ctypes.data, cap)
+        return out[:min(n, cap)]
 
     def close(self):
         if self.h:

@@ -79,7 +79,7 @@ def test_double_buffered_gather_on_device():
     env = ProcgenGym3Env(num=num, env_name=",".join(names), num_levels=0, rand_seed=5, device_buffers=True)
     dp = env.device_ptrs()
     g = ObsGather(num, engine_stream=torch.cuda.ExternalStream(dp.stream),
-                  bind=lambda t: env.set_obs_buffer(t.data_ptr()))
+                  bind=lambda t: env.set_obs_buffer(None if t is None else t.data_ptr()))
     sample = np.array([0, 1, 2, 3, 17, 33, 1000, 2047, 4095], np.int32)
     orcs = [OracleEnv(names[int(n) % 16], 1, env_offset=int(n), num_levels=0, rand_seed=5) for n in sample]
     seed = 0xD8
@@ -96,4 +96,7 @@ def test_double_buffered_gather_on_device():
                 np.testing.assert_array_equal(got[j], o.observe()["rgb"][0], err_msg="step %d env %d" % (tp, sample[j]))
         pending = (t, k) if k is not None else None
     torch.cuda.synchronize()
+    g.close()  # unbinds: the engine renders into its own tensor again
+    env.act_hashed(seed, 82)
+    env.wait()
     env.close()

@@ -93,7 +93,7 @@ def test_upstream_state_fields(game):
     """get_state bytes walked field by field (tests/upstream_state.py) and checked against the
     oracle's own objects after the same steps."""
     import struct
-    from upstream_state import END_OF_BUFFER, parse
+    from upstream_state import END_OF_BUFFER, entity_words, parse
     num = 3
     env = make_gpu(num, game, num_levels=0, start_level=0, rand_seed=9)
     orc = OracleEnv(game, num, rand_seed=9)
@@ -120,6 +120,12 @@ def test_upstream_state_fields(game):
         if game in ("maze", "miner"):
             w, h = lat["grid_size"][i]
             assert d["grid"]["data"] == list(lat["grid"][i][: w * h])
+        # every field of every listed entity, bit for bit, against the oracle's entity list
+        oe = orc.entities(i)
+        got = np.array([entity_words(e) for e in d["entities"]], np.int32).reshape(-1, 31)
+        assert got.shape == oe.shape, "entity count"
+        for k in range(len(oe)):
+            np.testing.assert_array_equal(got[k], oe[k], err_msg="entity %d of env %d" % (k, i))
     env.close()
 
 

@@ -78,6 +78,15 @@ class _R:
         return [self.ent() for _ in range(self.i())]
 
 
+def entity_words(e):
+    """One parsed entity as the 31 int32 words it was written as (floats as their bits)."""
+    out = []
+    for names, fl in zip(ENTITY, (True, False, True, False, True, False, True)):
+        for n in names:
+            out.append(struct.unpack("<i", struct.pack("<f", e[n]))[0] if fl else int(e[n]))
+    return out
+
+
 def randgen(r):
     seeded = r.i()
     words = r.s().split()
