@@ -126,6 +126,8 @@ LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int le
 #define PG_ERR_NO_ATLAS 3
 #define PG_ERR_HIP 4
 #define PG_ERR_GRID 5
+#define PG_ERR_ASSETGEN 6 /* use_generated_assets: the device painter met a path it does not restate */
+#define PG_ERR_RENDER 7   /* a draw referenced pixels outside the atlas or a case the renderer lacks */
 
 #ifdef __cplusplus
 }

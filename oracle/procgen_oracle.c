@@ -276,12 +276,21 @@ typedef struct {
     float road_lane_speeds[8], water_lane_speeds[8];
     /* observation of the last step */
     uint32_t canvas[RES_W * RES_H];
+    /* use_generated_assets: the env's 500 x 500 RGB32 background, repainted by AssetGen at every
+     * reset (basic-abstract-game.cpp:60-63, 778-782) */
+    uint32_t *gen_bg;
 } Game;
 
 typedef struct {
     int count, offset;
     Game *games;
     const or_atlas *atlas;
+    /* use_generated_assets: the atlas the games draw from (generated sprites, one 500 x 500
+     * background slot whose pixels are each env's gen_bg) */
+    or_atlas gen_atlas;
+    uint32_t *gen_pixels;
+    or_image *gen_sprites, *gen_backgrounds;
+    int32_t *gen_num_themes;
 } Vec;
 
 static Entity *AG(Game *g) { return g->agent_erased ? &g->agent_ghost : &g->ents[0]; }
@@ -1383,6 +1392,7 @@ static void cr_generate_coin_to_the_right(Game *g, const or_atlas *at) { /* coin
     fill_elem(g, curr_x + 1, 0, g->main_width - curr_x - 1, g->main_height, CR_WALL_MID);
 }
 
+static void gen_paint_background(Game *g);
 static void basic_game_reset(Game *g, const or_atlas *at) { /* basic-abstract-game.cpp:767-806 */
     fassert(g->main_width > 0 && g->main_height > 0);
     g->bg_pct_x = rg_rand01(&g->rand_gen);
@@ -1392,6 +1402,7 @@ static void basic_game_reset(Game *g, const or_atlas *at) { /* basic-abstract-ga
     g->grid_h = g->main_height;
     memset(g->grid, 0, sizeof(g->grid));
     g->background_index = rg_randn(&g->rand_gen, at->num_backgrounds);
+    if (g->gen_bg) gen_paint_background(g); /* AssetGen bggen(&rand_gen); generate_resource (:778-782) */
     g->num_ents = 0;
     g->agent_erased = false;
     float ax, ay;
@@ -5264,6 +5275,76 @@ static int ag_generate_resource(MT *rg, AgCanvas *c, int num_recurse, int blotch
     return a.err ? -1 : 0;
 }
 
+#define GEN_BG_DIM 500   /* QImage(500, 500, Format_RGB32) (basic-abstract-game.cpp:61) */
+#define GEN_SPRITE_DIM 64 /* QImage(64, 64, Format_ARGB32) (:105) */
+static void gen_paint_background(Game *g) {
+    AgCanvas c = {g->gen_bg, GEN_BG_DIM, GEN_BG_DIM, QFMT_RGB32, 0};
+    fassert(ag_generate_resource(&g->rand_gen, &c, 1, 50, true) == 0);
+}
+/* use_block_asset(type) of each game (basic-abstract-game.cpp:412-414 and the overrides: caveflyer.cpp:81,
+ * chaser.cpp:74, climber.cpp:128, coinrun.cpp:183, dodgeball.cpp:153, fruitbot.cpp:137, heist.cpp:62,
+ * jumper.cpp:107, leaper.cpp:87, ninja.cpp:135) */
+static bool gen_use_block_asset(int gid, int t) {
+    switch (gid) {
+    case GAME_CAVEFLYER: return t == 8;                      /* CAVEWALL */
+    case GAME_CHASER: return t == 5;                         /* MAZE_WALL */
+    case GAME_CLIMBER: case GAME_COINRUN: return t == 15 || t == 16; /* WALL_MID, WALL_TOP */
+    case GAME_DODGEBALL: return t == 1 || t == 5 || t == 7;  /* LAVA_WALL, DOOR, DOOR_OPEN */
+    case GAME_FRUITBOT: return t == 1 || t == 10 || t == 12; /* BARRIER, LOCKED_DOOR, PRESENT */
+    case GAME_HEIST: return t == WALL_OBJ || t == 1;         /* WALL_OBJ, LOCKED_DOOR */
+    case 9 /* jumper */: return t == 6 || t == 7;            /* CAVEWALL, CAVEWALL_TOP */
+    case GAME_LEAPER: return t == 3 || t == 2;               /* WATER, ROAD */
+    case GAME_NINJA: return t == 20;                         /* WALL_MID */
+    default: return false;
+    }
+}
+static uint32_t fnv1a(const char *s) { /* hash_str_uint32 (vecgame.cpp:156-167) */
+    uint32_t h = 0x811c9dc5u;
+    for (; *s; s++) h = (h ^ (uint8_t)*s) * 0x1000193u;
+    return h;
+}
+#define GEN_TYPES 99 /* image types 0..98 (slot 99 holds jumper's Qt-tabulated compass raster) */
+/* The atlas of a use_generated_assets vec (initialize_asset_if_necessary, :79-123): every type's image
+ * is generate_resource(64 x 64 ARGB32, 0, 5, use_block_asset(type)) with asset_rand_gen seeded
+ * fixed_asset_seed + type, fixed_asset_seed = int(FNV-1a(env name)) (vecgame.cpp:370-375); one theme,
+ * aspect ratio 1, the same image for every theme index (the seed ignores the theme); one background
+ * slot, 500 x 500, whose pixels are each env's gen_bg.  Drawn premultiplied (Qt converts an ARGB32
+ * source when blitting; its pixels are opaque or fully transparent, so that is the pixel or 0). */
+static void gen_build_atlas(Vec *v, const char *env_name, int gid, const or_atlas *src) {
+    const or_image *tab = &src->sprites[99];
+    const size_t tab_px = (size_t)(tab->w > 0 ? tab->w * tab->h : 0);
+    v->gen_pixels = (uint32_t *)calloc((size_t)GEN_TYPES * 4096 + tab_px + 1, sizeof(uint32_t));
+    v->gen_sprites = (or_image *)calloc(1000, sizeof(or_image));
+    v->gen_backgrounds = (or_image *)calloc(1, sizeof(or_image));
+    v->gen_num_themes = (int32_t *)calloc(100, sizeof(int32_t));
+    const uint32_t seed0 = fnv1a(env_name);
+    uint32_t img[64 * 64];
+    for (int t = 0; t < GEN_TYPES; t++) {
+        MT m;
+        rg_seed(&m, (int)(seed0 + (uint32_t)t));
+        AgCanvas c = {img, GEN_SPRITE_DIM, GEN_SPRITE_DIM, QFMT_ARGB32, 0};
+        fassert(ag_generate_resource(&m, &c, 0, 5, gen_use_block_asset(gid, t)) == 0);
+        uint32_t *dst = v->gen_pixels + (size_t)t * 4096;
+        for (int k = 0; k < 4096; k++) dst[k] = (img[k] >> 24) == 255 ? img[k] : 0u;
+        for (int th = 0; th < 10; th++) {
+            or_image im = {(uint32_t)(t * 4096), GEN_SPRITE_DIM, GEN_SPRITE_DIM, 0};
+            v->gen_sprites[t + 100 * th] = im;
+        }
+        v->gen_num_themes[t] = 1;
+    }
+    if (tab_px) {
+        memcpy(v->gen_pixels + (size_t)GEN_TYPES * 4096, src->pixels + tab->offset, tab_px * 4);
+        or_image im = {(uint32_t)(GEN_TYPES * 4096), tab->w, tab->h, 0};
+        v->gen_sprites[99] = im;
+        v->gen_num_themes[99] = src->num_themes[99];
+    }
+    or_image bg = {0, GEN_BG_DIM, GEN_BG_DIM, 0};
+    v->gen_backgrounds[0] = bg;
+    or_atlas a = {v->gen_pixels, v->gen_sprites, v->gen_backgrounds, 1, v->gen_num_themes};
+    v->gen_atlas = a;
+    v->atlas = &v->gen_atlas;
+}
+
 /* ================================================================== render (basic-abstract-game.cpp) */
 
 static void prepare_for_drawing(Game *g, float rect_height) { /* :828-847 */
@@ -5439,8 +5520,9 @@ static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
     if (!g->options.use_backgrounds) return;
     RectD main_rect = get_screen_rect(g, 0, (float)g->main_height, (float)g->main_width, (float)g->main_height, 0);
     const or_image *bg = &at->backgrounds[g->background_index];
+    const uint32_t *bgpx = g->gen_bg ? g->gen_bg : at->pixels + bg->offset; /* procedurally generated */
     if (g->bg_tile_ratio < 0) { /* :1003-1004 */
-        tile_image_fmt(g, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, main_rect, g->bg_tile_ratio);
+        tile_image_fmt(g, bgpx, bg->w, bg->h, QFMT_RGB32, false, 1.0, main_rect, g->bg_tile_ratio);
         return;
     }
     float bgw = (float)bg->w;
@@ -5451,7 +5533,7 @@ static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
     float offset_x = g->bg_pct_x * extra_w;
     RectD adj = {(double)(-offset_x), 0, (double)(bg_ar / world_ar), 1};
     RectD r = adjust_rect(main_rect, adj);
-    qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0);
+    qt_draw_image(g->canvas, r.x, r.y, r.w, r.h, bgpx, bg->w, bg->h, QFMT_RGB32, false, 1.0);
 }
 
 static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
@@ -5561,7 +5643,7 @@ static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_dra
             RectD r_bg = {(double)x_off, (double)(-RES_H * (bg_k - 1) / 2), (double)(RES_H * bg_k * BG_RATIO),
                           (double)(RES_H * bg_k)};
             const or_image *bg = &at->backgrounds[g->background_index];
-            tile_image_fmt(g, at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, r_bg, 1);
+            tile_image_fmt(g, g->gen_bg ? g->gen_bg : at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, r_bg, 1);
         }
         draw_foreground(g, at);
         return;
@@ -5736,6 +5818,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     v->offset = env_offset;
     v->atlas = atlas;
     v->games = (Game *)calloc((size_t)count, sizeof(Game));
+    if (opt->use_generated_assets) gen_build_atlas(v, env_name, gid, atlas);
     int level_seed_low = 0, level_seed_high = 0; /* vecgame.cpp:332-341 */
     if (opt->num_levels == 0) {
         level_seed_low = 0;
@@ -5773,7 +5856,8 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         g->game_n = env_offset + n;
         /* parse_options, game.cpp:62-95 */
         g->options.paint_vel_info = opt->paint_vel_info;
-        g->options.use_generated_assets = false;
+        g->options.use_generated_assets = opt->use_generated_assets != 0;
+        if (g->options.use_generated_assets) g->gen_bg = (uint32_t *)calloc((size_t)GEN_BG_DIM * GEN_BG_DIM, 4);
         g->options.use_monochrome_assets = opt->use_monochrome_assets;
         g->options.restrict_themes = opt->restrict_themes;
         g->options.use_backgrounds = opt->use_backgrounds;
@@ -5788,8 +5872,15 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
 void oracle_close(void *h) {
     Vec *v = (Vec *)h;
     if (!v) return;
-    for (int n = 0; n < v->count; n++) free(v->games[n].ents);
+    for (int n = 0; n < v->count; n++) {
+        free(v->games[n].ents);
+        free(v->games[n].gen_bg);
+    }
     free(v->games);
+    free(v->gen_pixels);
+    free(v->gen_sprites);
+    free(v->gen_backgrounds);
+    free(v->gen_num_themes);
     free(v);
 }
 
@@ -6000,6 +6091,45 @@ static double rd_f64(Rd *r) {
 }
 
 /* replays ONE case body (after the canvas words) of tools/qt_raster_golden.cpp's format */
+/* qt-utils.h / grid.h pins (tests/test_oracle_pins.py, against the reference headers compiled in
+ * oracle/_ref): adjust_rect over (x, y, w, h) quadruples, to_shade of floats, and the Grid
+ * operations the oracle's Game grid restates (contains, get_obj's in-range read / out-of-bounds
+ * object, y * w + x indexing and its inverse) */
+void oracle_adjust_rect(const double *base, const double *adj, double *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) {
+        RectD b = {base[4 * i], base[4 * i + 1], base[4 * i + 2], base[4 * i + 3]};
+        RectD a = {adj[4 * i], adj[4 * i + 1], adj[4 * i + 2], adj[4 * i + 3]};
+        RectD r = adjust_rect(b, a);
+        out[4 * i] = r.x; out[4 * i + 1] = r.y; out[4 * i + 2] = r.w; out[4 * i + 3] = r.h;
+    }
+}
+void oracle_to_shade(const float *f, int32_t *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = to_shade(f[i]);
+}
+int oracle_grid_ops(int w, int h, const int32_t *xy, int n, int32_t *out) {
+    if (w <= 0 || h <= 0 || w * h > MAX_GRID) return -1;
+    Game *g = (Game *)calloc(1, sizeof(Game));
+    g->grid_w = w;
+    g->grid_h = h;
+    g->out_of_bounds_object = -7;
+    for (int i = 0; i < w * h; i++) g->grid[i] = 0; /* Grid::resize: value-initialised */
+    int zeros = 0;
+    for (int i = 0; i < w * h; i++) zeros += g->grid[i] == 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) set_obj(g, x, y, 3 * (y * w + x) + 1);
+    for (int k = 0; k < n; k++) {
+        const int x = xy[2 * k], y = xy[2 * k + 1];
+        const int idx = y * w + x;
+        out[5 * k + 0] = grid_contains(g, x, y);
+        out[5 * k + 1] = get_obj(g, x, y);
+        out[5 * k + 2] = idx;
+        out[5 * k + 3] = idx % w; /* to_xy */
+        out[5 * k + 4] = idx / w;
+    }
+    free(g);
+    return zeros;
+}
+
 /* bigfish.cpp:84 fish radius through the C library's pow (the checker of the device pow) */
 void oracle_bigfish_radius(const float *u, float *out, int64_t n) {
     for (int64_t i = 0; i < n; i++)

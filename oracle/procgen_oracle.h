@@ -45,6 +45,7 @@ typedef struct {
     int32_t distribution_mode;
     int32_t center_agent, use_backgrounds, restrict_themes, use_sequential_levels;
     int32_t use_monochrome_assets, paint_vel_info, debug_mode;
+    int32_t use_generated_assets; /* AssetGen sprites + per-env procedural backgrounds */
 } or_options;
 
 /* Create `count` envs of game `env_name` whose GLOBAL indices are
@@ -88,6 +89,10 @@ void oracle_randgen_script(uint32_t seed, const int32_t *ops, int nops, int32_t 
 int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int start_obj, int num_objs, int32_t *out,
                    uint32_t *next_draw);
 /* bigfish.cpp:84 fish radius 1.75 * pow(u, 1.4) + .25 with the C library's pow */
+/* qt-utils.h adjust_rect / to_shade and grid.h Grid pins */
+void oracle_adjust_rect(const double *base, const double *adj, double *out, int64_t n);
+void oracle_to_shade(const float *f, int32_t *out, int64_t n);
+int oracle_grid_ops(int w, int h, const int32_t *xy, int n, int32_t *out);
 void oracle_bigfish_radius(const float *u, float *out, int64_t n);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);

@@ -15,6 +15,7 @@
 #include "randgen.h"
 #include "entity.h"
 #include "mazegen.h"
+#include "grid.h"
 
 extern "C" {
 
@@ -156,4 +157,33 @@ extern "C" void ref_caveflyer_enemy_vel(int32_t seed, float *out) {
     rand_gen.seed(seed);
     float vel = (.1 * rand_gen.rand01() + .1) * (rand_gen.randn(2) * 2 - 1);
     out[0] = vel;
+}
+
+// grid.h: Grid<int> resized to w x h (value-initialised: returns how many cells read 0), every cell
+// set to 3 * index + 1 through set(), then per probe point: contains, get() (or -7 outside, the
+// out-of-bounds object get_obj substitutes, basic-abstract-game.cpp:180-185), to_index, to_xy.
+// Also pins that Grid::serialize through the fork's WriteBuffer writes no bytes.
+extern "C" int ref_grid_ops(int w, int h, const int32_t *xy, int n, int32_t *out, int32_t *serialized_bytes) {
+    Grid<int> g;
+    g.resize(w, h);
+    int zeros = 0;
+    for (int i = 0; i < w * h; i++) zeros += g.get_index(i) == 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) g.set(x, y, 3 * g.to_index(x, y) + 1);
+    for (int k = 0; k < n; k++) {
+        const int x = xy[2 * k], y = xy[2 * k + 1];
+        out[5 * k + 0] = g.contains(x, y);
+        out[5 * k + 1] = g.contains(x, y) ? g.get(x, y) : -7;
+        const int idx = g.to_index(x, y);
+        out[5 * k + 2] = idx;
+        int tx, ty;
+        g.to_xy(idx, &tx, &ty);
+        out[5 * k + 3] = tx;
+        out[5 * k + 4] = ty;
+    }
+    std::vector<char> buf(1 << 16);
+    WriteBuffer b(buf.data(), buf.size());
+    g.serialize(&b);
+    *serialized_bytes = (int32_t)b.offset;
+    return zeros;
 }

@@ -15,6 +15,7 @@
 #include <memory>
 
 #include "assetgen.h"
+#include "qt-utils.h"
 #include "randgen.h"
 
 static void copy_out(const QImage &img, uint32_t *out) {
@@ -84,11 +85,40 @@ void ref_qt_polyline(int w, int h, const double *pts, int n, uint32_t color, uin
     copy_out(img, inout);
 }
 
+// drawImage(QRectF(x, y, w, h), img) of an iw x ih image of `fmt` (optionally mirrored first, as the
+// reference's reflections) onto a 64x64 RGB32 canvas `inout`: how generated ARGB32 sprites are drawn
+void ref_qt_draw_image(const uint32_t *img, int iw, int ih, int fmt, int mirrored, double x, double y, double w,
+                       double h, uint32_t *inout) {
+    QImage src(iw, ih, (QImage::Format)fmt);
+    for (int r = 0; r < ih; r++) memcpy(src.scanLine(r), img + (size_t)r * iw, (size_t)iw * 4);
+    QImage canvas(64, 64, QImage::Format_RGB32);
+    for (int r = 0; r < 64; r++) memcpy(canvas.scanLine(r), inout + (size_t)r * 64, 64 * 4);
+    {
+        QPainter p(&canvas);
+        p.drawImage(QRectF(x, y, w, h), mirrored ? src.mirrored(true, false) : src);
+    }
+    copy_out(canvas, inout);
+}
+
 // QImage::mirrored(true, false) of a w x h image (basic-abstract-game.cpp:121-122)
 void ref_qt_mirrored(int w, int h, int fmt, const uint32_t *in, uint32_t *out) {
     QImage img(w, h, (QImage::Format)fmt);
     for (int r = 0; r < h; r++) memcpy(img.scanLine(r), in + (size_t)r * w, (size_t)w * 4);
     copy_out(img.mirrored(true, false), out);
+}
+
+// qt-utils.h:12-19 adjust_rect over (x, y, w, h) quadruples (QRectF arithmetic in qreal = double)
+void ref_adjust_rect(const double *base, const double *adj, double *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) {
+        QRectF r = adjust_rect(QRectF(base[4 * i], base[4 * i + 1], base[4 * i + 2], base[4 * i + 3]),
+                               QRectF(adj[4 * i], adj[4 * i + 1], adj[4 * i + 2], adj[4 * i + 3]));
+        out[4 * i] = r.x(); out[4 * i + 1] = r.y(); out[4 * i + 2] = r.width(); out[4 * i + 3] = r.height();
+    }
+}
+
+// qt-utils.h:21-28 to_shade
+void ref_to_shade(const float *f, int32_t *out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = to_shade(f[i]);
 }
 
 } // extern "C"

@@ -28,6 +28,7 @@ void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
                      int grid);
 void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s);
+int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s);
 void pg_launch_poison(hipStream_t s, uint32_t pattern);
 
 // PROCGEN_MI355X_POISON_LDS=1: scribble over LDS before every engine kernel (debug aid, see
@@ -306,6 +307,7 @@ struct VecEnv {
     uint8_t *first_host = nullptr;
     bool buffers_set = false;
     bool atlas = false;
+    bool gen_assets = false; // use_generated_assets: AssetGen sprites + per-env procedural backgrounds
     bool started = false;
     // device allocations
     std::vector<void *> allocs;
@@ -571,10 +573,13 @@ int check_device_errors(VecEnv *v) {
     HIPCHECK(copy_sync(v, &flags, v->dev.error_any, 4, hipMemcpyDeviceToHost));
     if (flags && !v->error) {
         int code = __builtin_ctz((unsigned)flags);
-        const char *msg = code == PG_ERR_ENTITY_OVERFLOW ? "entity capacity exceeded"
+        std::string msg = code == PG_ERR_ENTITY_OVERFLOW ? "entity capacity exceeded"
                           : code == PG_ERR_GRID        ? "grid write out of range"
+                          : code == PG_ERR_ASSETGEN    ? "AssetGen background painter met a path it does not restate (reason bits " +
+                                                          std::to_string((unsigned)flags >> 16) + ")"
+                          : code == PG_ERR_RENDER      ? "render met an atlas reference or a case it does not have"
                                                        : "unsupported feature reached on device";
-        fail(v, code, msg);
+        fail(v, code, msg.c_str());
     }
     return 0;
 }
@@ -584,6 +589,63 @@ int check_device_errors(VecEnv *v) {
 extern "C" {
 
 LIBENV_API int libenv_version(void) { return LIBENV_VERSION; }
+
+// use_generated_assets (basic-abstract-game.cpp:54-123): every image type of every game present is
+// AssetGen'd on the device (pg_assetgen_sprites_kernel) -- asset_rand_gen seeded fixed_asset_seed +
+// type with fixed_asset_seed = int(FNV-1a(env name)) (vecgame.cpp:156-167, 370-375) -- one theme,
+// aspect ratio 1 and the same image for every theme index (the seed ignores the theme); one
+// background slot (offset 0, 500 x 500) whose pixels are each env's gen_bg.  Slot 99 keeps jumper's
+// tabulated compass raster.
+static const int GEN_TYPES = 99;
+static int generated_atlas(VecEnv *v, const std::vector<int> &gids, PGAtlasHost &at, std::string &err) {
+    uint32_t *d_img = nullptr;
+    if (hipMalloc((void **)&d_img, (size_t)GEN_TYPES * 4096 * 4) != hipSuccess) {
+        err = "device allocation failed";
+        return -1;
+    }
+    std::vector<uint32_t> img((size_t)GEN_TYPES * 4096);
+    int rc = 0;
+    for (int g : gids) {
+        const char *name = pg_game_name(g);
+        uint32_t h = 0x811c9dc5u;
+        for (const char *c = name; *c; c++) h = (h ^ (uint8_t)*c) * 0x1000193u;
+        if (pg_launch_assetgen_sprites(g, h, d_img, GEN_TYPES, v->stream) != 0 ||
+            hipMemcpyAsync(img.data(), d_img, img.size() * 4, hipMemcpyDeviceToHost, v->stream) != hipSuccess ||
+            hipStreamSynchronize(v->stream) != hipSuccess) {
+            err = "sprite generation failed";
+            rc = -1;
+            break;
+        }
+        const uint32_t base = (uint32_t)at.pixels.size();
+        for (int t = 0; t < GEN_TYPES; t++)
+            if (img[(size_t)t * 4096] == 0xdeadbeefu) {
+                err = std::string("AssetGen met a path it does not restate (") + name + " type " + std::to_string(t) + ")";
+                rc = -1;
+            }
+        if (rc) break;
+        at.pixels.insert(at.pixels.end(), img.begin(), img.end());
+        int32_t *spr = at.sprites.data() + (size_t)g * PG_NUM_SLOTS * 4;
+        int32_t *thm = at.num_themes.data() + (size_t)g * 100;
+        for (int t = 0; t < GEN_TYPES; t++) {
+            for (int th = 0; th < PG_NUM_SLOTS / 100; th++) {
+                int32_t *e = spr + (size_t)(t + 100 * th) * 4;
+                e[0] = (int32_t)(base + (uint32_t)t * 4096);
+                e[1] = 64;
+                e[2] = 64;
+                e[3] = 0;
+            }
+            thm[t] = 1;
+        }
+        int32_t *bg = at.backgrounds.data() + (size_t)g * PG_MAX_BG * 4;
+        bg[0] = 0;
+        bg[1] = 500;
+        bg[2] = 500;
+        bg[3] = 0;
+        at.num_backgrounds[g] = 1;
+    }
+    (void)hipFree(d_img);
+    return rc;
+}
 
 LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options options) {
     g_last_make_error.clear();
@@ -650,7 +712,6 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     }
     if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
     if (env_offset < 0) return bad("env_offset must be >= 0");
-    if (use_generated_assets) return bad("use_generated_assets is not in this build yet");
     if (render_human) return bad("render_mode=rgb_array (render_human) is not in this build yet");
 
     VecEnv *v = new VecEnv();
@@ -660,6 +721,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     v->env_offset = env_offset;
     v->num_actions = num_actions;
     v->render_human = render_human;
+    v->gen_assets = use_generated_assets;
     if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess) {
         delete v;
         return bad("hipStreamCreate failed");
@@ -733,6 +795,9 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     d.rot_table = d_rot_table;
     rc |= dalloc(v, &d.error_any, 1);
     rc |= dalloc(v, &d.prof, n * 16); // written only by PG_PROFILE (diagnostic) builds
+    // use_generated_assets: each env owns a 500 x 500 RGB32 background (main_bg_images_ptr of one
+    // QImage, basic-abstract-game.cpp:58-63), 1 MB per env
+    if (use_generated_assets) rc |= dalloc(v, &d.gen_bg, n * PG_GEN_BG_PX);
     if (rc) {
         libenv_close(v);
         return bad("device allocation failed");
@@ -803,6 +868,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (!pg_atlas_load(root, gids, &at, &err)) {
             libenv_close(v);
             return bad("asset load failed: " + err);
+        }
+        if (use_generated_assets && generated_atlas(v, gids, at, err) != 0) {
+            libenv_close(v);
+            return bad("generated assets: " + err);
         }
         if (upload_atlas(v, at.pixels.data(), (int64_t)at.pixels.size(), (const pg_image *)at.sprites.data(),
                          (const pg_image *)at.backgrounds.data(), at.num_backgrounds.data(), at.num_themes.data()) != 0) {
@@ -1176,7 +1245,8 @@ LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, in
     if (copy_sync(v, &s, v->dev.envs + env_idx, sizeof(s), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail;
     size_t cells = (size_t)s.main_width * s.main_height;
-    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    const size_t bgb = v->dev.gen_bg ? (size_t)PG_GEN_BG_PX * 4 : 0; // the env's generated background
+    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + bgb + 4;
     if ((size_t)length < need) return -1;
     char *p = data;
     memcpy(p, &STATE_MAGIC, 4); p += 4;
@@ -1195,6 +1265,8 @@ LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, in
     p += cells * 2;
     if (copy_sync(v, p, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, 2 * PG_MT_WORDS * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     p += 2 * PG_MT_WORDS * 4;
+    if (bgb && copy_sync(v, p, v->dev.gen_bg + (size_t)env_idx * PG_GEN_BG_PX, bgb, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    p += bgb;
     memcpy(p, &END_OF_BUFFER, 4); p += 4;
     return (int)(p - data);
 }
@@ -1227,7 +1299,8 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
         return;
     }
     size_t ents = (size_t)s.num_ents, tail = (size_t)s.num_tail, cells = (size_t)s.main_width * s.main_height;
-    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    const size_t bgb = v->dev.gen_bg ? (size_t)PG_GEN_BG_PX * 4 : 0;
+    size_t need = 8 + sizeof(PGEnv) + (ents + tail) * PG_NF * 4 + cells * 2 + 2 * PG_MT_WORDS * 4 + bgb + 4;
     int32_t end = 0;
     if ((size_t)length < need || cells > PG_GRID_MAX) {
         fail(v, PG_ERR_BAD_OPTION, "set_state: truncated state");
@@ -1286,6 +1359,8 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     }
     p += cells * 2;
     copy_sync(v, v->dev.mt + (size_t)env_idx * 2 * PG_MT_WORDS, p, 2 * PG_MT_WORDS * 4, hipMemcpyHostToDevice);
+    p += 2 * PG_MT_WORDS * 4;
+    if (bgb) copy_sync(v, v->dev.gen_bg + (size_t)env_idx * PG_GEN_BG_PX, p, bgb, hipMemcpyHostToDevice);
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
     for (size_t k = 0; k < v->games.size(); k++)
@@ -1307,7 +1382,9 @@ LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int3
         return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: bad arguments");
     if (v->game_of(env_idx) != PG_GAME_MINER)
         return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: only miner has a game_set_state (miner.cpp:423-449)");
-    const size_t cap = 8 + sizeof(PGEnv) + (size_t)PG_CAP * PG_NF * 4 + (size_t)PG_GRID_MAX * 2 + 2 * PG_MT_WORDS * 4 + 4;
+    const size_t bgb = v->dev.gen_bg ? (size_t)PG_GEN_BG_PX * 4 : 0;
+    const size_t cap = 8 + sizeof(PGEnv) + (size_t)PG_CAP * PG_NF * 4 + (size_t)PG_GRID_MAX * 2 + 2 * PG_MT_WORDS * 4 +
+                       bgb + 4;
     std::vector<char> buf(cap);
     if (procgen_get_snapshot(env, env_idx, buf.data(), (int)cap) < 0)
         return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: could not read the env's state");
@@ -1372,6 +1449,8 @@ LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int3
     if (cells) memcpy(q, cellv.data(), cells * 2);
     q += cells * 2;
     memcpy(q, MT, 2 * PG_MT_WORDS * 4); q += 2 * PG_MT_WORDS * 4;
+    if (bgb) memcpy(q, MT + 2 * PG_MT_WORDS * 4, bgb); // the generated background, unchanged
+    q += bgb;
     memcpy(q, &END_OF_BUFFER, 4); q += 4;
     procgen_set_snapshot(env, env_idx, out.data(), (int)(q - out.data()));
     return v->error ? -v->error : 0;
@@ -1388,7 +1467,7 @@ LIBENV_API int procgen_mt_text(const uint32_t *words, int pos, char *out, int le
 
 // ---- get_state / set_state (vecgame.cpp:485-505) in the upstream byte format (pg_state.cpp)
 static const size_t SNAP_CAP = 8 + sizeof(PGEnv) + (size_t)PG_CAP * PG_NF * 4 + (size_t)PG_GRID_MAX * 2 +
-                               2 * PG_MT_WORDS * 4 + 4;
+                               2 * PG_MT_WORDS * 4 + (size_t)PG_GEN_BG_PX * 4 + 4;
 
 static int read_host_env(VecEnv *v, int env_idx, HostEnv &h) {
     std::vector<char> buf(SNAP_CAP);
@@ -1433,6 +1512,8 @@ static void write_host_env(VecEnv *v, int env_idx, const HostEnv &h) {
 LIBENV_API int get_state(libenv_env *env, int env_idx, char *data, int length) {
     VecEnv *v = (VecEnv *)env;
     if (!v || env_idx < 0 || env_idx >= v->num_envs || !data) return -1;
+    if (v->gen_assets) // BasicAbstractGame::serialize fasserts !use_generated_assets (basic-abstract-game.cpp:1185)
+        return fail(v, PG_ERR_BAD_OPTION, "get_state: states of use_generated_assets envs are not serializable");
     HostEnv h;
     if (read_host_env(v, env_idx, h) < 0) return -1;
     std::vector<char> out;
@@ -1446,6 +1527,10 @@ LIBENV_API void set_state(libenv_env *env, int env_idx, char *data, int length) 
     VecEnv *v = (VecEnv *)env;
     if (!v || env_idx < 0 || env_idx >= v->num_envs || !data || length < 0) {
         fail(v, PG_ERR_BAD_OPTION, "set_state: bad arguments");
+        return;
+    }
+    if (v->gen_assets) { // BasicAbstractGame::deserialize fasserts !use_generated_assets (:1240)
+        fail(v, PG_ERR_BAD_OPTION, "set_state: use_generated_assets envs have no serialized state");
         return;
     }
     HostEnv h;

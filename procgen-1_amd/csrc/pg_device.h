@@ -287,8 +287,12 @@ struct PTimer {
 // many waves of a launch were resident at once (scripts/census.py).
 struct Census {
 #ifdef PG_CENSUS
-    uint64_t t0;
-    DEV void start() { t0 = __builtin_amdgcn_s_memrealtime(); }
+    uint64_t t0, tm[5];
+    DEV void start() {
+        t0 = __builtin_amdgcn_s_memrealtime();
+        for (int k = 0; k < 5; k++) tm[k] = 0;
+    }
+    DEV void mark(int k) { tm[k] = __builtin_amdgcn_s_memrealtime(); }
     DEV void flush(uint64_t *p) {
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
@@ -297,9 +301,11 @@ struct Census {
             p[0] = t0;
             p[1] = t1;
             p[2] = (uint64_t)hw | ((uint64_t)xcc << 32);
+            for (int k = 0; k < 5; k++) p[3 + k] = tm[k];
         }
     }
 #else
+    DEV void mark(int) {}
     DEV void start() {}
     DEV void flush(uint64_t *) {}
 #endif

@@ -19,6 +19,7 @@
 #define PG_MT_WORDS 625       // 624 state words + index
 #define PG_NUM_SLOTS 1000     // image slots: type + 100 * theme
 #define PG_MAX_BG 64
+#define PG_GEN_BG_PX (500 * 500) // use_generated_assets: one env's background (QImage 500 x 500 RGB32)
 
 // game ids = index in the reference's env list (procgen/env.py:15-32)
 enum PGGame {
@@ -38,6 +39,8 @@ enum PGGame {
 #define PG_ERR_NO_ATLAS 3
 #define PG_ERR_HIP 4
 #define PG_ERR_GRID 5
+#define PG_ERR_ASSETGEN 6 // the AssetGen painter met a path it does not restate (reason bits << 16 in error_any)
+#define PG_ERR_RENDER 7   // a draw referenced atlas pixels / a case the renderer does not have
 #endif
 
 // reference DistributionMode (game.h:34-39)
@@ -245,6 +248,9 @@ struct PGDev {
     const double *rot_table;    // [PG_ROT_N][4] = m11, m12, m21, m22
     const float *rot_angles;    // [PG_ROT_N] entity rotation values (radians, float) of the table
     int32_t *latent;            // [num_envs][PG_LATENT_N] grid_size, grid, agent_pos, exit_pos (maze)
+    // use_generated_assets: each env's 500 x 500 RGB32 background, repainted by AssetGen at every
+    // reset (basic-abstract-game.cpp:60-63, 778-782); null otherwise
+    uint32_t *gen_bg;
 };
 #define PG_ROT_N 16
 #define PG_TABLE_SLOT 99 // image slot of a game's Qt-tabulated overlay raster (jumper's compass)

@@ -1287,7 +1287,7 @@ DEV uint32_t gen_texel(const PGDev &d, const int2 t, int sc, int sr, bool &err) 
 // Row pass (first covering tile column) + second-column pass.  FUSE: the background texel of the
 // pixel (bg_col / bg_base / bgrow as in the fast path) is the destination; else the frame buffer.
 template <bool FUSE>
-DEV void gen_draw(const FB &fb, const PGDev &d, const uint8_t *aux, const GenLane &gl, int ww, bool bg_col,
+DEV void gen_draw(const FB &fb, const PGDev &d, const uint32_t *bgpix, const uint8_t *aux, const GenLane &gl, int ww, bool bg_col,
                   uint32_t bg_base, int bgrow, bool &err) {
     const int lane = LANE;
     const int2 *ti = reinterpret_cast<const int2 *>(aux);
@@ -1324,7 +1324,7 @@ DEV void gen_draw(const FB &fb, const PGDev &d, const uint8_t *aux, const GenLan
             for (int k = 0; k < RB; k++) {
                 const int br = readlane(bgrow, r0 + k);
                 const bool inb = bg_col && br >= 0;
-                const uint32_t px = d.pixels[inb ? bg_base + (uint32_t)br : 0u];
+                const uint32_t px = bgpix[inb ? bg_base + (uint32_t)br : 0u];
                 dst[k] = inb ? px : 0xff000000u;
             }
         } else {
@@ -1478,7 +1478,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                 int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
                 if (sp.y == tile_px<G>() && sp.z == tile_px<G>()) off = sp.x;
                 else if (sp.y > 0) off = -2;
-                else off = -3; // generated assets: not in this build
+                else off = -3; // no image (missing_image_ok decides in the generic pass)
             }
         }
         tile_off[t] = off;
@@ -1504,6 +1504,9 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     Axis bx, by;
     bool bg_ok = false;
     int4 bgi = make_int4(0, 0, 0, 0);
+    // the background's pixels: the atlas, or (use_generated_assets) this env's AssetGen image, whose
+    // table entry is (offset 0, 500, 500)
+    const uint32_t *bgpix = d.gen_bg ? d.gen_bg + (size_t)env * (500 * 500) : d.pixels;
     double bg_rx = 0, bg_ry = 0, bg_rw = 0, bg_rh = 0;
     if (s.opt_use_backgrounds) {
         double mx, my, mw, mh;
@@ -1673,8 +1676,10 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                 }
                 fast = ballot(other) == 0;
             }
-        } else if (s.opt_use_monochrome_assets) {
-            fast = false; // every drawable tile is a draw_grid_obj fill: generic tile pass
+        } else if (s.opt_use_monochrome_assets || d.gen_bg) {
+            // monochrome: every drawable tile is a draw_grid_obj fill; use_generated_assets: the
+            // tiles are 64 x 64 AssetGen images, not tile_px() squares -- generic tile pass
+            fast = false;
         }
     }
     auto lookup_grid = [&](int x, int y) -> int {
@@ -1773,7 +1778,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #pragma unroll
             for (int k = 0; k < RB; k++) { // branch-free: an out-of-blit pixel loads pixels[0] and discards it
                 const bool inb = bg_col && bgr[k] >= 0;
-                uint32_t px = d.pixels[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
+                uint32_t px = bgpix[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
                 bgv[k] = inb ? px : 0xff000000u;
             }
 #pragma unroll
@@ -1826,7 +1831,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
             }
         }
     } else if (gen && !has_z_minus1<G>()) {
-        gen_draw<true>(fb, d, aux, gl, ww, bg_col, bg_col_base, bg_lane_row, err);
+        gen_draw<true>(fb, d, bgpix, aux, gl, ww, bg_col, bg_col_base, bg_lane_row, err);
     } else {
         // ---- background alone (lane = column), RB rows per batch
         const int bgrow = bg_lane_row;
@@ -1836,7 +1841,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
             for (int k = 0; k < RB; k++) {
                 const int br = readlane(bgrow, r0 + k);
                 const bool inb = bg_col && br >= 0;
-                uint32_t px = d.pixels[inb ? bg_col_base + (uint32_t)br : 0u];
+                uint32_t px = bgpix[inb ? bg_col_base + (uint32_t)br : 0u];
                 bgv[k] = inb ? px : 0xff000000u;
             }
 #pragma unroll
@@ -1857,7 +1862,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
         } else if (gen) {
             if constexpr (has_z_minus1<G>()) {
                 wave_sync();
-                gen_draw<false>(fb, d, aux, gl, ww, false, 0u, -1, err);
+                gen_draw<false>(fb, d, bgpix, aux, gl, ww, false, 0u, -1, err);
             }
         } else if (has_grid_tiles<G>()) {
             ent_setup_valid = false; // the tile chunks reuse `im`
@@ -1937,7 +1942,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     wave_sync(); // the next pass overwrites the frame rows
     } // pass
 #undef PG_DRAW_ENTITIES
-    if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_BAD_OPTION);
+    if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
     pt.mark(6);
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
     census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);

@@ -10,6 +10,7 @@
 // std::set BFS of expand_to_type a lane-parallel frontier over cell bytes that honours the
 // reference's ascending visiting order and early return.
 #include "pg_device.h"
+#include "pg_assetgen.h"
 
 namespace {
 
@@ -86,12 +87,17 @@ struct RCtx {
     uint32_t *mt;    // LDS rand_gen words
     int32_t mti;
     int16_t *grid;   // LDS grid
+    AgLds *ag;       // AssetGen scratch (use_generated_assets kernels only, else null)
 };
 
 DEV float &EF(RCtx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
 DEV int &EI(RCtx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
 
 DEV uint32_t draw(RCtx &c) { return mt_next_lds(c.mt, c.mti); }
+struct RCtxRng { // the env's rand_gen as AssetGen's generator (AssetGen bggen(&rand_gen))
+    RCtx *c;
+    DEV uint32_t next() { return draw(*c); }
+};
 DEV int randn(RCtx &c, int n) { return rg_randn_of(draw(c), n); }
 DEV float rand01(RCtx &c) { return rg_rand01_of(draw(c)); }
 
@@ -247,6 +253,17 @@ DEV void base_game_reset(RCtx &c) { // basic-abstract-game.cpp:767-806
         c.s.error = PG_ERR_GRID;
     fill_elem(c, 0, 0, c.s.main_width, c.s.main_height, 0); // grid.resize -> zeros
     c.s.background_index = randn(c, c.d.num_backgrounds);
+    if (c.ag) { // use_procgen_background: bggen.generate_resource(bg) with rand_gen (:778-782)
+        wave_sync();
+        AgPainter<RCtxRng> p{c.d.gen_bg + (size_t)c.env * AG_BG_DIM * AG_BG_DIM, AG_BG_DIM, AG_BG_DIM, AG_FMT_RGB32, 0,
+                             c.ag, RCtxRng{&c}, 0};
+        ag_generate_resource(p, 1, 50, true);
+        if (p.err) {
+            c.s.error = PG_ERR_ASSETGEN;
+            if (LANE == 0) atomicOr(c.d.error_any, p.err << 16);
+        }
+        wave_sync();
+    }
     c.s.num_ents = 0;
     c.s.num_tail = 0;
     c.s.agent_erased = 0;
@@ -2547,7 +2564,7 @@ DEV void leaper_game_reset(RCtx &c, LeaperScratch *L) {
 // ------------------------------------------------------------------ Game::reset
 template <int G>
 DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scratch<G> *scratch, bool initial,
-                   PGEnv *lds_env) {
+                   PGEnv *lds_env, AgLds *ag) {
     {
         const uint2 *src = reinterpret_cast<const uint2 *>(d.envs + env);
         reinterpret_cast<uint2 *>(lds_env)[LANE] = src[LANE]; // 64 lanes x 8 B = the 512-B PGEnv
@@ -2555,6 +2572,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     wave_sync();
     RCtx c{d, env, *lds_env};
     c.E = d.ents;
+    c.ag = ag;
     c.plane = (size_t)d.num_envs * PG_CAP;
     c.eb = (size_t)env * PG_CAP;
     c.mt = lds_mt;
@@ -2665,20 +2683,51 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
 }
 
 // all_envs != 0: reset every env in env_list / 0..count-1 (initial reset of set_buffers);
-// else drain this game's queue filled by the step kernel.
-template <int G>
+// else drain this game's queue filled by the step kernel.  GEN: use_generated_assets (the AssetGen
+// scratch is allocated only in these instances).
+template <int G, bool GEN>
 __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int all_envs) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ __attribute__((aligned(16))) int16_t lds_grid[PG_GRID_MAX];
     __shared__ Scratch<G> scratch;
     __shared__ __attribute__((aligned(16))) PGEnv lds_env;
+    AgLds *ag = nullptr;
+    if constexpr (GEN) {
+        __shared__ AgLds ag_lds;
+        ag = &ag_lds;
+    }
     int n = all_envs ? count : d.reset_count[G];
     const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
     PGDev dv = game_view(d, G);
     for (int q = blockIdx.x; q < n; q += gridDim.x) {
         int env = all_envs ? (env_list ? env_list[q] : q) : queue[q];
-        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0, &lds_env);
+        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0, &lds_env, ag);
     }
+}
+
+// The use_generated_assets sprites of one game (initialize_asset_if_necessary,
+// basic-abstract-game.cpp:79-123): workgroup t paints image type t -- asset_rand_gen.seed(
+// fixed_asset_seed + t); generate_resource(QImage(64, 64, ARGB32), 0, 5, use_block_asset(t)) -- into
+// out[t][64][64], stored premultiplied as the compositor reads it (the pixels are opaque or clear).
+__global__ __launch_bounds__(64) void pg_assetgen_sprites_kernel(int game, uint32_t seed0, uint32_t *out) {
+    __shared__ uint32_t lds_mt[PG_MT_N];
+    __shared__ AgLds ag_lds;
+    const int t = blockIdx.x;
+    mt_seed_lds(lds_mt, seed0 + (uint32_t)t);
+    struct LdsRng {
+        uint32_t *mt;
+        int32_t mti;
+        DEV uint32_t next() { return mt_next_lds(mt, mti); }
+    };
+    uint32_t *img = out + (size_t)t * AG_SPRITE_DIM * AG_SPRITE_DIM;
+    AgPainter<LdsRng> p{img, AG_SPRITE_DIM, AG_SPRITE_DIM, AG_FMT_ARGB32, 0, &ag_lds, LdsRng{lds_mt, PG_MT_N}, 0};
+    ag_generate_resource(p, 0, 5, ag_use_block_asset(game, t));
+    wave_sync();
+    for (int i = LANE; i < AG_SPRITE_DIM * AG_SPRITE_DIM; i += 64) {
+        const uint32_t v = img[i];
+        img[i] = (v >> 24) == 255 ? v : 0u;
+    }
+    if (p.err && LANE == 0) img[0] = 0xdeadbeefu; // flagged to the host (never a valid premultiplied texel)
 }
 
 } // namespace
@@ -2687,9 +2736,10 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
                                 int all_envs, int grid) {
     if (count <= 0) return;
     int g = grid > 0 ? grid : (count < 4096 ? count : 4096);
-#define PG_CASE(G)                                                                                      \
-    case G:                                                                                             \
-        hipLaunchKernelGGL(pg_reset_kernel<G>, dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
+#define PG_CASE(G)                                                                                              \
+    case G:                                                                                                     \
+        if (d->gen_bg) hipLaunchKernelGGL((pg_reset_kernel<G, true>), dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
+        else hipLaunchKernelGGL((pg_reset_kernel<G, false>), dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)
@@ -2711,4 +2761,10 @@ extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_lis
     default: break;
     }
 #undef PG_CASE
+}
+
+extern "C" int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s) {
+    if (types <= 0) return 0;
+    hipLaunchKernelGGL(pg_assetgen_sprites_kernel, dim3(types), dim3(64), 0, s, game, seed0, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -31,6 +31,7 @@ struct Ctx {
     bool i_erase;
     int i_theme;
     PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
+    Census cs;      // diagnostic wave census (PG_CENSUS builds only)
 };
 
 DEV float &EF(Ctx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
@@ -372,97 +373,130 @@ DEV void build_interactor_list(Ctx &c) {
 
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
 
-template <int G, int D, bool PL>
-DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy);
-
-// basic-abstract-game.cpp:248-276 (target is always the stepped object)
-template <int G, int D, bool PL>
-DEV void push_obj(Ctx &c, int src, int oi, Ent &o, bool is_h) {
+// push_obj's target offset (basic-abstract-game.cpp:248-270; the target is always the stepped object)
+DEV void push_offset(Ctx &c, int src, const Ent &o, bool is_h, float &t_vx, float &t_vy) {
     float sx = EF(c, F_X, src), sy = EF(c, F_Y, src);
     float rsum = is_h ? (EF(c, F_RX, src) + o.rx) : (EF(c, F_RY, src) + o.ry);
     float delx = o.x - sx;
     float dely = o.y - sy;
-    float t_vx = 0, t_vy = 0;
+    t_vx = 0;
+    t_vy = 0;
     if (is_h) t_vx = (float)((double)sx + dsign(delx) * (double)rsum - (double)o.x);
     else t_vy = (float)((double)sy + dsign(dely) * (double)rsum - (double)o.y);
-    if constexpr (D < 5) (void)sub_step<G, D + 1, PL>(c, oi, o, t_vx, t_vy);
-    if (is_h) o.vx = 0;
-    else o.vy = 0;
 }
 
-// basic-abstract-game.cpp:278-380.  PL: every lane steps its own entity (no cross-lane operation).
-template <int G, int D, bool PL>
+// basic-abstract-game.cpp:278-380 with push_obj (:247-276) folded in.  The reference recurses
+// sub_step -> push_obj -> sub_step(depth + 1) while depth < 5; here the recursion is an explicit
+// stack of at most 5 suspended frames (each: its move, the scan position, block || block2 so far),
+// so the body exists once in the kernel instead of once per depth per call site (a 6-deep inlined
+// chain per call site made the coinrun kernel 177 KB, far past the instruction cache).
+// A child's return value is ignored by push_obj; after it returns the parent zeroes the pushed
+// velocity component and resumes its reverse entity loop.
+// PL: every lane steps its own entity (no cross-lane operation).
+template <int G, bool PL>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
-    if (o.flags & EF_WILL_ERASE) return false;
-    float ny = o.y + _vy;
-    float nx = o.x + _vx;
-    const float margin = 0.98f;
-    bool is_h = _vx != 0;
-    bool block = false, reflect = false;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
-            if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
-                if (o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID) { o.vx = 0; o.vy = 0; }
-            block = block || is_blocked<G>(c, o.type, type2);
-            reflect = reflect || will_reflect<G>(o.type, type2);
-        }
-    }
-    if (reflect) {
-        if (is_h) {
-            float delta;
-            if (_vx < 0) delta = ceilf(nx - o.rx) - (nx - o.rx);
-            else delta = floorf(nx + o.rx) - (nx + o.rx);
-            o.vx = -1 * o.vx;
-            nx = nx + 2 * delta;
-        } else {
-            float delta;
-            if (_vy < 0) delta = ceilf(ny - o.ry) - (ny - o.ry);
-            else delta = floorf(ny + o.ry) - (ny + o.ry);
-            o.vy = -1 * o.vy;
-            ny = ny + 2 * delta;
-        }
-    } else if (block) {
-        if (is_h) {
-            if (c.s.grid_step) nx = o.x;
-            else nx = _vx > 0 ? (floorf(nx + o.rx) - o.rx) : (ceilf(nx - o.rx) + o.rx);
-        } else {
-            if (c.s.grid_step) ny = o.y;
-            else ny = _vy > 0 ? (floorf(ny + o.ry) - o.ry) : (ceilf(ny - o.ry) + o.ry);
-        }
-    }
-    o.x = nx;
-    o.y = ny;
-    bool block2 = false;
-    int upper = c.s.num_ents;
-    while (scan_needed<G>(is_h)) {
-        int m = PL ? next_collider_pl(c, oi, upper, o) : next_collider(c, oi, upper, o);
-        if (m < 0) break;
-        upper = m;
-        int mtype = EI(c, F_TYPE, m);
-        bool curr_block = false;
-        AgentView av = agent_view(c, oi, o);
-        if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, av)) {
-            curr_block = true;
-        } else if (will_reflect<G>(o.type, mtype)) {
-            if (is_h) {
-                float delx = EF(c, F_X, m) - o.x;
-                float rsum = EF(c, F_RX, m) + o.rx;
-                o.x += _vx > 0 ? -2 * (rsum - delx) : 2 * (rsum + delx);
-                o.vx = -1 * o.vx;
+    constexpr int MAXD = 5;
+    float svx[MAXD], svy[MAXD];
+    int sup[MAXD];
+    bool sacc[MAXD];
+    int d = 0;
+    bool fresh = true, acc = false;
+    int upper = 0;
+    for (;;) {
+        bool is_h = _vx != 0;
+        if (fresh) {
+            if (o.flags & EF_WILL_ERASE) {
+                acc = false;
+                upper = -1; // return false without scanning
             } else {
-                float dely = EF(c, F_Y, m) - o.y;
-                float rsum = EF(c, F_RY, m) + o.ry;
-                o.y += _vy > 0 ? -2 * (rsum - dely) : 2 * (rsum + dely);
-                o.vy = -1 * o.vy;
+                float ny = o.y + _vy;
+                float nx = o.x + _vx;
+                const float margin = 0.98f;
+                bool block = false, reflect = false;
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+#pragma unroll
+                    for (int j = 0; j < 2; j++) {
+                        int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
+                        if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
+                            if (o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID) { o.vx = 0; o.vy = 0; }
+                        block = block || is_blocked<G>(c, o.type, type2);
+                        reflect = reflect || will_reflect<G>(o.type, type2);
+                    }
+                }
+                if (reflect) {
+                    if (is_h) {
+                        float delta;
+                        if (_vx < 0) delta = ceilf(nx - o.rx) - (nx - o.rx);
+                        else delta = floorf(nx + o.rx) - (nx + o.rx);
+                        o.vx = -1 * o.vx;
+                        nx = nx + 2 * delta;
+                    } else {
+                        float delta;
+                        if (_vy < 0) delta = ceilf(ny - o.ry) - (ny - o.ry);
+                        else delta = floorf(ny + o.ry) - (ny + o.ry);
+                        o.vy = -1 * o.vy;
+                        ny = ny + 2 * delta;
+                    }
+                } else if (block) {
+                    if (is_h) {
+                        if (c.s.grid_step) nx = o.x;
+                        else nx = _vx > 0 ? (floorf(nx + o.rx) - o.rx) : (ceilf(nx - o.rx) + o.rx);
+                    } else {
+                        if (c.s.grid_step) ny = o.y;
+                        else ny = _vy > 0 ? (floorf(ny + o.ry) - o.ry) : (ceilf(ny - o.ry) + o.ry);
+                    }
+                }
+                o.x = nx;
+                o.y = ny;
+                acc = block;
+                upper = c.s.num_ents;
+            }
+        } else {
+            // a child frame returned: the rest of push_obj (:271-275)
+            if (is_h) o.vx = 0;
+            else o.vy = 0;
+        }
+        fresh = false;
+        while (upper >= 0 && scan_needed<G>(is_h)) {
+            int m = PL ? next_collider_pl(c, oi, upper, o) : next_collider(c, oi, upper, o);
+            if (m < 0) break;
+            upper = m;
+            int mtype = EI(c, F_TYPE, m);
+            AgentView av = agent_view(c, oi, o);
+            if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, av)) {
+                acc = true; // block2 = block2 || curr_block
+                float t_vx, t_vy;
+                push_offset(c, m, o, is_h, t_vx, t_vy);
+                if (d < MAXD) { // suspend this frame, run sub_step(t_vx, t_vy, depth + 1)
+                    svx[d] = _vx; svy[d] = _vy; sup[d] = upper; sacc[d] = acc;
+                    d++;
+                    _vx = t_vx;
+                    _vy = t_vy;
+                    fresh = true;
+                    break;
+                }
+                if (is_h) o.vx = 0;
+                else o.vy = 0;
+            } else if (will_reflect<G>(o.type, mtype)) {
+                if (is_h) {
+                    float delx = EF(c, F_X, m) - o.x;
+                    float rsum = EF(c, F_RX, m) + o.rx;
+                    o.x += _vx > 0 ? -2 * (rsum - delx) : 2 * (rsum + delx);
+                    o.vx = -1 * o.vx;
+                } else {
+                    float dely = EF(c, F_Y, m) - o.y;
+                    float rsum = EF(c, F_RY, m) + o.ry;
+                    o.y += _vy > 0 ? -2 * (rsum - dely) : 2 * (rsum + dely);
+                    o.vy = -1 * o.vy;
+                }
             }
         }
-        if (curr_block) push_obj<G, D, PL>(c, m, oi, o, is_h);
-        block2 = block2 || curr_block;
+        if (fresh) continue;
+        if (d == 0) return acc;
+        d--;
+        _vx = svx[d]; _vy = svy[d]; upper = sup[d]; acc = sacc[d];
     }
-    return block || block2;
 }
 
 // basic-abstract-game.cpp:602-665
@@ -485,13 +519,15 @@ DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     }
     float vx_pct = 0, vy_pct = 0;
     for (int s = 0; s < num_sub_steps; s++) {
-        bool block_x, block_y;
-        if (step_x_first) {
-            block_x = sub_step<G, 0, PL>(c, oi, o, o.vx * pct, 0);
-            block_y = sub_step<G, 0, PL>(c, oi, o, 0, o.vy * pct);
-        } else {
-            block_y = sub_step<G, 0, PL>(c, oi, o, 0, o.vy * pct);
-            block_x = sub_step<G, 0, PL>(c, oi, o, o.vx * pct, 0);
+        // one sub_step call site for both half steps (the second reads the velocity the first
+        // may have changed)
+        bool block_x = false, block_y = false;
+#pragma unroll 1
+        for (int h = 0; h < 2; h++) {
+            const bool xmove = (h == 0) == step_x_first;
+            const bool b = sub_step<G, PL>(c, oi, o, xmove ? o.vx * pct : 0, xmove ? 0 : o.vy * pct);
+            if (xmove) block_x = b;
+            else block_y = b;
         }
         if (!block_x) vx_pct += 1;
         if (!block_y) vy_pct += 1;
@@ -553,6 +589,7 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         if (i < n) entity_step_slot(c, i, true);
     }
     c.pt.mark(7); // diagnostic build: interactor list + smart loads + the non-smart pass
+    c.cs.mark(3);
     // The smart entities' steps are independent of each other as well: a smart step writes only
     // its own entity and reads the grid, the static interactors and the agent (slot 0, stepped
     // last by the reverse loop, so every other smart step sees its pre-step state, which is what
@@ -2625,9 +2662,12 @@ DEV void game_step(Ctx &c) {
     }
     wave_sync();
     c.pt.mark(1);
+    c.cs.mark(1);
     build_interactor_list<G>(c);
+    c.cs.mark(2);
     step_entities<G>(c, c.slist);
     c.pt.mark(2);
+    c.cs.mark(4);
     agent_collisions<G>(c);
     c.pt.mark(3);
     erase_if_needed(c);
@@ -2702,10 +2742,10 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     c.nlist = 0;
     c.grid8 = lds_grid;
     c.grid8_ok = false;
-    Census census;
-    census.start();
+    c.cs.start();
     c.pt.start();
     load_grid_lds(c);
+    c.cs.mark(0);
 
     int action;
     if (use_hash) {
@@ -2777,7 +2817,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     }
     c.pt.mark(6);
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
-    census.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
+    c.cs.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 }
 
 } // namespace

@@ -80,10 +80,18 @@ def main(game="coinrun", num=65536, warm=60):
     slow = []
     for e in np.argsort(-life)[:16]:
         w = env.debug_env(int(e))
-        slow.append({"env": int(e), "us": round(float(life[e]), 1), "num_ents": int(w[27]), "cur_time": int(w[2]),
-                     "action": int(w[1]), "rg_mti": int(w[64]), "done": int(w[14]), "agent_erased": int(w[28])})
-    ne = np.array([env.debug_env(int(e))[27] for e in range(0, num, 64)])
+        marks = [round((int(raw[e, 3 + k]) - int(raw[e, 0])) * 10.0 / 1e3, 1) for k in range(5)]
+        slow.append({"env": int(e), "us": round(float(life[e]), 1), "marks_us": marks, "num_ents": int(w[27]), "cur_time": int(w[2]),
+                     "action": int(w[1]), "rg_mti": int(w[64]), "done": int(w[14]), "agent_erased": int(w[28]), "grid8_ok": int(w[67])})
+    dbg = [env.debug_env(int(e)) for e in range(0, num, 16)]
+    ne = np.array([w[27] for w in dbg])
+    g8 = np.array([w[67] for w in dbg])
+    out["grid8_ok_frac"] = {"all": float(g8.mean()), "first4096": float(g8[:256].mean()), "rest": float(g8[256:].mean())}
     out["step_slowest"] = slow
+    # phase split of a typical wave (median of the mark offsets over all waves)
+    offs = (raw[:, 3:8].astype(np.int64) - raw[:, 0:1].astype(np.int64)) * 10.0 / 1e3
+    out["marks_median_us"] = [round(float(np.median(offs[:, k])), 2) for k in range(5)]
+    out["start_us_of_slowest"] = [round((int(raw[e, 0]) - int(raw[:, 0].min())) * 10.0 / 1e3, 1) for e in np.argsort(-life)[:16]]
     out["num_ents_sample"] = {"mean": float(ne.mean()), "p99": float(np.percentile(ne, 99)), "max": int(ne.max())}
     out["lifetime_hist_us"] = np.histogram(life, bins=[0, 20, 40, 60, 80, 120, 200, 400, 800, 2000])[0].tolist()
     env.close()

@@ -24,7 +24,8 @@ class or_atlas(ctypes.Structure):
 
 
 OPTION_FIELDS = ["num_levels", "start_level", "rand_seed", "distribution_mode", "center_agent", "use_backgrounds",
-                 "restrict_themes", "use_sequential_levels", "use_monochrome_assets", "paint_vel_info", "debug_mode"]
+                 "restrict_themes", "use_sequential_levels", "use_monochrome_assets", "paint_vel_info", "debug_mode",
+                 "use_generated_assets"]
 
 
 class or_options(ctypes.Structure):
@@ -101,7 +102,7 @@ class OracleEnv:
                             a.backgrounds.shape[0], a.num_themes.ctypes.data)
         opts = dict(num_levels=0, start_level=0, rand_seed=0, distribution_mode=1, center_agent=1, use_backgrounds=1,
                     restrict_themes=0, use_sequential_levels=0, use_monochrome_assets=0, paint_vel_info=0,
-                    debug_mode=0)
+                    debug_mode=0, use_generated_assets=0)
         opts.update(kw)
         self._opt = or_options(*[int(opts[n]) for n in OPTION_FIELDS])
         self.count = count

@@ -28,7 +28,7 @@ def oracle_kw(gpu_kw):
     dm = kw.pop("distribution_mode", "hard")
     kw["distribution_mode"] = {"easy": 0, "hard": 1, "extreme": 2, "memory": 10}[dm]
     for k in ("center_agent", "use_backgrounds", "restrict_themes", "use_sequential_levels", "use_monochrome_assets",
-              "paint_vel_info"):
+              "paint_vel_info", "use_generated_assets"):
         if k in kw:
             kw[k] = int(kw[k])
     return kw

@@ -362,3 +362,61 @@ def test_jumper_compass_table_pins():
     # hard mode, centred: the dial is Qt's midpoint ellipse of QRect(55, 1, 8, 8) with a 1-px pen
     dial = z["dial"][1]
     assert int(dial[1]) != 0 and int(dial[0]) == 0 and all(int(r) == 0 for r in dial[11:])
+
+
+def test_grid_vs_reference():
+    """grid.h: Grid<int>::resize value-initialises, contains / get / to_index / to_xy, and (fork
+    buffer.h) serialize writes no bytes -- the oracle's Game grid (grid_contains, get_obj with the
+    out-of-bounds object, y * w + x) against the reference's Grid compiled in oracle/_ref."""
+    ref = ref_lib()
+    orc = oracle_lib.load()
+    P = ctypes.c_void_p
+    ref.ref_grid_ops.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, P]
+    orc.oracle_grid_ops.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P]
+    rng = np.random.RandomState(5)
+    for w, h in ((1, 1), (13, 13), (64, 64), (20, 35), (35, 20), (100, 7)):
+        xy = np.stack([rng.randint(-3, w + 3, 400), rng.randint(-3, h + 3, 400)], 1).astype(np.int32)
+        xy = np.ascontiguousarray(np.concatenate([xy, [[0, 0], [w - 1, h - 1], [w, 0], [0, h], [-1, 0]]]).astype(np.int32))
+        a = np.zeros((len(xy), 5), np.int32)
+        b = a.copy()
+        nbytes = np.zeros(1, np.int32)
+        za = ref.ref_grid_ops(w, h, xy.ctypes.data, len(xy), a.ctypes.data, nbytes.ctypes.data)
+        zb = orc.oracle_grid_ops(w, h, xy.ctypes.data, len(xy), b.ctypes.data)
+        assert za == zb == w * h
+        assert int(nbytes[0]) == 0
+        inside = a[:, 0] == 1
+        np.testing.assert_array_equal(b[:, :2], a[:, :2])
+        np.testing.assert_array_equal(b[:, 2], a[:, 2])
+        # to_xy round trip: defined (and used by the games) for in-grid indices
+        np.testing.assert_array_equal(b[inside, 3:], a[inside, 3:])
+
+
+def test_qt_utils_vs_reference():
+    """qt-utils.h: adjust_rect (QRectF arithmetic; coinrun.cpp:66, leaper.cpp:244 and the background
+    rect, basic-abstract-game.cpp:1013) and to_shade (the velocity squares, :972-973), against the
+    reference header compiled with the real Qt 5.9.7 (oracle/_ref/libref_qt.so)."""
+    qt_so = os.path.join(os.path.dirname(oracle_lib.REF_SO), "libref_qt.so")
+    if not os.path.exists(qt_so):
+        pytest.skip("oracle/_ref/libref_qt.so not built")
+    ref = ctypes.CDLL(qt_so)
+    orc = oracle_lib.load()
+    P, L = ctypes.c_void_p, ctypes.c_int64
+    for lib, pre in ((ref, "ref"), (orc, "oracle")):
+        getattr(lib, pre + "_adjust_rect").argtypes = [P, P, P, L]
+        getattr(lib, pre + "_to_shade").argtypes = [P, P, L]
+    rng = np.random.RandomState(9)
+    n = 20000
+    base = np.ascontiguousarray(rng.uniform(-100, 600, (n, 4)))
+    adj = np.ascontiguousarray(rng.uniform(-2, 2, (n, 4)))
+    adj[:4] = [[0, -.7415, 1, 1.7415], [0, -.275, 1, 1.55], [-0.3, 0, 1.7, 1], [0, 0, 1, 1]]
+    a, b = np.zeros((n, 4)), np.zeros((n, 4))
+    ref.ref_adjust_rect(base.ctypes.data, adj.ctypes.data, a.ctypes.data, n)
+    orc.oracle_adjust_rect(base.ctypes.data, adj.ctypes.data, b.ctypes.data, n)
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+    f = np.concatenate([rng.uniform(-0.5, 1.5, 200000), np.linspace(-0.01, 1.01, 100001),
+                        [0.0, -0.0, 1.0, 1 / 255, 254.5 / 255, 255.5 / 255]]).astype(np.float32)
+    f = np.ascontiguousarray(np.concatenate([f, np.nextafter(f, np.float32(2)), np.nextafter(f, np.float32(-2))]))
+    sa, sb = np.zeros(len(f), np.int32), np.zeros(len(f), np.int32)
+    ref.ref_to_shade(f.ctypes.data, sa.ctypes.data, len(f))
+    orc.oracle_to_shade(f.ctypes.data, sb.ctypes.data, len(f))
+    np.testing.assert_array_equal(sa, sb)
