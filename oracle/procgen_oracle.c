@@ -896,7 +896,17 @@ static bool push_obj(Game *g, int src_i, int target_i, bool is_horizontal, int d
     return block;
 }
 
+/* diagnostic counters of the physics work (scripts only: how many sub_steps / collision-scan
+ * iterations one step costs an env) */
+static long long g_diag_substeps, g_diag_scans;
+void oracle_diag_counters(long long *out, int reset) {
+    out[0] = g_diag_substeps;
+    out[1] = g_diag_scans;
+    if (reset) g_diag_substeps = g_diag_scans = 0;
+}
+
 static bool sub_step(Game *g, int obj_i, float _vx, float _vy, int depth) { /* :278-380 */
+    g_diag_substeps++;
     Entity *obj = &g->ents[obj_i];
     if (obj->will_erase) return false;
     float ny = obj->y + _vy;
@@ -944,6 +954,7 @@ static bool sub_step(Game *g, int obj_i, float _vx, float _vy, int depth) { /* :
         if (i == obj_i || m->will_erase) continue;
         bool curr_block = false;
         if (has_collision(obj, m, POS_EPS)) {
+            g_diag_scans++;
             if (hook_is_blocked_ents(g, obj, m, is_horizontal)) {
                 curr_block = true;
             } else if (hook_will_reflect(g, obj->type, m->type)) {

@@ -93,6 +93,7 @@ int oracle_mazegen(int32_t seed, int maze_dim, int mode, int num_doors, int star
 void oracle_adjust_rect(const double *base, const double *adj, double *out, int64_t n);
 void oracle_to_shade(const float *f, int32_t *out, int64_t n);
 int oracle_grid_ops(int w, int h, const int32_t *xy, int n, int32_t *out);
+void oracle_diag_counters(long long *out, int reset);
 void oracle_bigfish_radius(const float *u, float *out, int64_t n);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);

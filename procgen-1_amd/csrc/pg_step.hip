@@ -30,6 +30,8 @@ struct Ctx {
     float i_x, i_y, i_rx, i_ry;
     bool i_erase;
     int i_theme;
+    float av_vy, av_ry; // the agent's vy / ry as other objects' steps see it (coinrun's crate rule)
+    float *pstk;        // LDS: sub_step's suspended push frames (5 x {vx, vy, upper, acc})
     PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
     Census cs;      // diagnostic wave census (PG_CENSUS builds only)
 };
@@ -212,36 +214,33 @@ DEV bool will_reflect(int src, int target) { // coinrun.cpp:140-142; base :507-5
     return false;
 }
 
-struct AgentView { float x, y, vx, vy, rx, ry; };
+// The scanned entity m of sub_step's loop: its index and the fields the loop body reads.  Interactors
+// are static during step_entities (see build_interactor_list), so these come from the lane that
+// caches m (ireg) or one set of loads -- never re-read per use inside the push chain.
+struct IView {
+    int m;
+    float x, y, rx, ry;
+    int theme;
+};
 
-// is_blocked_ents (basic :503-505; coinrun.cpp:187-202; heist.cpp:66-71).  `agent` is the
-// current agent state (registers if it is the stepped object).
+// is_blocked_ents (basic :503-505; coinrun.cpp:187-202; heist.cpp:66-71).  The agent's vy / ry are
+// the stepped object's own when it is the agent (slot 0), else the agent's pre-step state (c.av_*).
 template <int G>
-DEV bool is_blocked_ents(Ctx &c, int src_type, int m, int t_type, bool is_h, const AgentView &agent) {
+DEV bool is_blocked_ents(Ctx &c, int src_type, const IView &m, int t_type, bool is_h, int oi, const Ent &o) {
     if constexpr (G == PG_GAME_COINRUN) {
         if (t_type == CR_CRATE && !is_h) {
-            if (agent.vy >= 0) return false;
+            const float avy = oi == 0 ? o.vy : c.av_vy, ary = oi == 0 ? o.ry : c.av_ry;
+            if (avy >= 0) return false;
             if (c.s.action_vy < 0) return false;
-            if (c.s.last_agent_y < (EF(c, F_Y, m) + EF(c, F_RY, m) + agent.ry)) return false;
+            if (c.s.last_agent_y < (m.y + m.ry + ary)) return false;
             c.s.is_on_crate = 1;
             return true;
         }
     }
     if constexpr (G == PG_GAME_HEIST) {
-        if (t_type == HS_LOCKED_DOOR) return !((c.s.has_keys >> EI(c, F_IMAGE_THEME, m)) & 1);
+        if (t_type == HS_LOCKED_DOOR) return !((c.s.has_keys >> m.theme) & 1);
     }
     return is_blocked<G>(c, src_type, t_type);
-}
-
-DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
-    AgentView a;
-    if (oi == 0) {
-        a.x = o.x; a.y = o.y; a.vx = o.vx; a.vy = o.vy; a.rx = o.rx; a.ry = o.ry;
-    } else {
-        a.x = EF(c, F_X, 0); a.y = EF(c, F_Y, 0); a.vx = EF(c, F_VX, 0); a.vy = EF(c, F_VY, 0);
-        a.rx = EF(c, F_RX, 0); a.ry = EF(c, F_RY, 0);
-    }
-    return a;
 }
 
 // ------------------------------------------------------------------ collision scan
@@ -256,23 +255,36 @@ DEV AgentView agent_view(Ctx &c, int oi, const Ent &o) {
 // step_entities (no insertion or erase there).
 // dodgeball: LAVA_WALL reflects ENEMY (dodgeball.cpp:98-100); no entity type blocks.
 template <int G>
-DEV bool scan_needed(bool is_h) {
+DEV constexpr bool scan_needed(bool is_h) {
     if constexpr (G == PG_GAME_COINRUN) return !is_h;
     if constexpr (G == PG_GAME_HEIST) return true;
     if constexpr (G == PG_GAME_DODGEBALL) return true;
     return false;
 }
+// the one entity type that interacts in each scanning game (-1: none)
 template <int G>
-DEV bool is_interactor(int type) {
-    if constexpr (G == PG_GAME_COINRUN) return type == CR_CRATE;
-    if constexpr (G == PG_GAME_HEIST) return type == HS_LOCKED_DOOR;
-    if constexpr (G == PG_GAME_DODGEBALL) return type == DB_LAVA_WALL;
-    return false;
+DEV constexpr int interactor_type() {
+    if constexpr (G == PG_GAME_COINRUN) return CR_CRATE;
+    if constexpr (G == PG_GAME_HEIST) return HS_LOCKED_DOOR;
+    if constexpr (G == PG_GAME_DODGEBALL) return DB_LAVA_WALL;
+    return -1;
 }
+template <int G>
+DEV bool is_interactor(int type) { return interactor_type<G>() >= 0 && type == interactor_type<G>(); }
 
 // Largest interactor index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
 // i.e. the next entity the reference's reverse loop would act on; lane-parallel over the list.
-DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
+DEV float rlf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+DEV int rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+DEV void iview_load(Ctx &c, int m, IView &v) {
+    v.m = m;
+    v.x = EF(c, F_X, m); v.y = EF(c, F_Y, m); v.rx = EF(c, F_RX, m); v.ry = EF(c, F_RY, m);
+    v.theme = EI(c, F_IMAGE_THEME, m);
+}
+
+// Fills `v` and returns true when there is a next collider.
+DEV bool next_collider(Ctx &c, int oi, int upper, const Ent &o, IView &v) {
     if (c.ireg) { // <= 64 static interactors: lane k holds interactor k in registers
         int i = LANE < c.nlist ? c.i_idx : PG_CAP;
         bool hit = false;
@@ -282,7 +294,12 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
             hit = (fabsf(o.x - c.i_x) < tx) && (fabsf(o.y - c.i_y) < ty);
         }
         unsigned long long m = ballot(hit);
-        return m ? __builtin_amdgcn_readlane(i, top_bit(m)) : -1;
+        if (!m) return false;
+        const int l = top_bit(m);
+        v.m = rli(i, l);
+        v.x = rlf(c.i_x, l); v.y = rlf(c.i_y, l); v.rx = rlf(c.i_rx, l); v.ry = rlf(c.i_ry, l);
+        v.theme = rli(c.i_theme, l);
+        return true;
     }
     for (int base = (c.nlist - 1) & ~63; base >= 0; base -= 64) {
         int k = base + LANE;
@@ -297,9 +314,12 @@ DEV int next_collider(Ctx &c, int oi, int upper, const Ent &o) {
             }
         }
         unsigned long long m = ballot(hit);
-        if (m) return __builtin_amdgcn_readlane(i, top_bit(m)); // list is ascending by index
+        if (m) { // list is ascending by index
+            iview_load(c, rli(i, top_bit(m)), v);
+            return true;
+        }
     }
-    return -1;
+    return false;
 }
 
 // Games whose smart entities step lane-parallel (step_entities_fast; measured per game,
@@ -315,7 +335,7 @@ DEV constexpr bool pl_smart() {
 
 // next_collider for a lane stepping its own entity (lane-parallel smart steps): the static
 // interactors are read from LDS, the ascending list's last hit is the largest index.
-DEV int next_collider_pl(Ctx &c, int oi, int upper, const Ent &o) {
+DEV bool next_collider_pl(Ctx &c, int oi, int upper, const Ent &o, IView &v) {
     int best = -1;
     for (int k = 0; k < c.nlist; k++) {
         const int inf = c.iinfo[k];
@@ -326,7 +346,9 @@ DEV int next_collider_pl(Ctx &c, int oi, int upper, const Ent &o) {
         float ty = (o.ry + b.w) + POS_EPS;
         if ((fabsf(o.x - b.x) < tx) && (fabsf(o.y - b.y) < ty)) best = i;
     }
-    return best;
+    if (best < 0) return false;
+    iview_load(c, best, v);
+    return true;
 }
 
 template <int G>
@@ -374,9 +396,9 @@ DEV void build_interactor_list(Ctx &c) {
 DEV double dsign(double x) { return x > 0 ? +1 : (x == 0 ? 0 : -1); }
 
 // push_obj's target offset (basic-abstract-game.cpp:248-270; the target is always the stepped object)
-DEV void push_offset(Ctx &c, int src, const Ent &o, bool is_h, float &t_vx, float &t_vy) {
-    float sx = EF(c, F_X, src), sy = EF(c, F_Y, src);
-    float rsum = is_h ? (EF(c, F_RX, src) + o.rx) : (EF(c, F_RY, src) + o.ry);
+DEV void push_offset(const IView &src, const Ent &o, bool is_h, float &t_vx, float &t_vy) {
+    float sx = src.x, sy = src.y;
+    float rsum = is_h ? (src.rx + o.rx) : (src.ry + o.ry);
     float delx = o.x - sx;
     float dely = o.y - sy;
     t_vx = 0;
@@ -395,10 +417,9 @@ DEV void push_offset(Ctx &c, int src, const Ent &o, bool is_h, float &t_vx, floa
 // PL: every lane steps its own entity (no cross-lane operation).
 template <int G, bool PL>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
+    // the frame stack is wave-uniform LDS: the lane-parallel (PL) games never scan
+    static_assert(!PL || (!scan_needed<G>(true) && !scan_needed<G>(false)), "PL games have no push chain");
     constexpr int MAXD = 5;
-    float svx[MAXD], svy[MAXD];
-    int sup[MAXD];
-    bool sacc[MAXD];
     int d = 0;
     bool fresh = true, acc = false;
     int upper = 0;
@@ -459,17 +480,17 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
         }
         fresh = false;
         while (upper >= 0 && scan_needed<G>(is_h)) {
-            int m = PL ? next_collider_pl(c, oi, upper, o) : next_collider(c, oi, upper, o);
-            if (m < 0) break;
-            upper = m;
-            int mtype = EI(c, F_TYPE, m);
-            AgentView av = agent_view(c, oi, o);
-            if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, av)) {
+            IView m;
+            if (!(PL ? next_collider_pl(c, oi, upper, o, m) : next_collider(c, oi, upper, o, m))) break;
+            upper = m.m;
+            constexpr int mtype = interactor_type<G>(); // the scan lists hold only this type
+            if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, oi, o)) {
                 acc = true; // block2 = block2 || curr_block
                 float t_vx, t_vy;
-                push_offset(c, m, o, is_h, t_vx, t_vy);
+                push_offset(m, o, is_h, t_vx, t_vy);
                 if (d < MAXD) { // suspend this frame, run sub_step(t_vx, t_vy, depth + 1)
-                    svx[d] = _vx; svy[d] = _vy; sup[d] = upper; sacc[d] = acc;
+                    float *f = c.pstk + 4 * d;
+                    f[0] = _vx; f[1] = _vy; f[2] = __int_as_float(upper); f[3] = acc ? 1.f : 0.f;
                     d++;
                     _vx = t_vx;
                     _vy = t_vy;
@@ -480,13 +501,13 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 else o.vy = 0;
             } else if (will_reflect<G>(o.type, mtype)) {
                 if (is_h) {
-                    float delx = EF(c, F_X, m) - o.x;
-                    float rsum = EF(c, F_RX, m) + o.rx;
+                    float delx = m.x - o.x;
+                    float rsum = m.rx + o.rx;
                     o.x += _vx > 0 ? -2 * (rsum - delx) : 2 * (rsum + delx);
                     o.vx = -1 * o.vx;
                 } else {
-                    float dely = EF(c, F_Y, m) - o.y;
-                    float rsum = EF(c, F_RY, m) + o.ry;
+                    float dely = m.y - o.y;
+                    float rsum = m.ry + o.ry;
                     o.y += _vy > 0 ? -2 * (rsum - dely) : 2 * (rsum + dely);
                     o.vy = -1 * o.vy;
                 }
@@ -495,7 +516,8 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
         if (fresh) continue;
         if (d == 0) return acc;
         d--;
-        _vx = svx[d]; _vy = svy[d]; upper = sup[d]; acc = sacc[d];
+        const float *f = c.pstk + 4 * d;
+        _vx = f[0]; _vy = f[1]; upper = __float_as_int(f[2]); acc = f[3] != 0.f;
     }
 }
 
@@ -503,6 +525,10 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
 template <int G, bool PL = false>
 DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     if (o.flags & EF_WILL_ERASE) return;
+    if constexpr (G == PG_GAME_COINRUN) {
+        // the agent as this object's crate checks see it: slot 0 is written only by its own step
+        if (oi != 0) { c.av_vy = EF(c, F_VY, 0); c.av_ry = EF(c, F_RY, 0); }
+    }
     int num_sub_steps;
     if (c.s.grid_step) {
         num_sub_steps = 1;
@@ -542,9 +568,6 @@ DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
 // basic-abstract-game.cpp:1095-1107: reverse order; runs of non-smart entities are
 // independent (Entity::step touches only its own entity) and are stepped lane-parallel
 // with slot i always owned by lane i % 64.
-DEV float rlf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-DEV int rli(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
 DEV void ent_readlane(const Ent &m, int l, Ent &o) {
     o.x = rlf(m.x, l); o.y = rlf(m.y, l); o.vx = rlf(m.vx, l); o.vy = rlf(m.vy, l);
     o.rx = rlf(m.rx, l); o.ry = rlf(m.ry, l); o.rotation = rlf(m.rotation, l); o.vrot = rlf(m.vrot, l);
@@ -2722,6 +2745,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the
     // workgroups per CU here)
     __shared__ float4 lds_ibox[pl_smart<G>() ? 64 : 1];
+    __shared__ float lds_pstk[(scan_needed<G>(true) || scan_needed<G>(false)) ? 4 * 5 : 1];
     __shared__ int lds_iinfo[pl_smart<G>() ? 64 : 1];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
@@ -2738,6 +2762,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     c.ilist = lds_list;
     c.slist = lds_slist;
     c.ibox = lds_ibox;
+    c.pstk = lds_pstk;
     c.iinfo = lds_iinfo;
     c.nlist = 0;
     c.grid8 = lds_grid;
