@@ -24,7 +24,7 @@
 
 extern "C" {
 void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int use_hash,
-                    uint64_t seed, int32_t t);
+                    uint64_t seed, int32_t t, int parity);
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
                      int grid);
 void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s);
@@ -308,6 +308,7 @@ struct VecEnv {
     bool buffers_set = false;
     bool atlas = false;
     bool gen_assets = false; // use_generated_assets: AssetGen sprites + per-env procedural backgrounds
+    int parity = 0;          // alternates per act: which slow-env list the step launches write
     bool started = false;
     // device allocations
     std::vector<void *> allocs;
@@ -426,14 +427,16 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         v->t_used++;
     }
     if (e) HIPCHECK(hipEventRecord(e[4 * G], v->stream));
-    HIPCHECK(hipMemsetAsync(v->dev.reset_count, 0, sizeof(int32_t) * PG_NUM_GAMES, v->stream));
+    // reset counts and the slow-list length of this act's step order (PGDev::sched)
+    v->parity ^= 1;
+    HIPCHECK(hipMemsetAsync(v->dev.sched + PG_SCHED_CLEAR(v->parity), 0, sizeof(int32_t) * 32, v->stream));
     if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     for (size_t k = 0; k < G; k++) {
         hipStream_t s = G > 1 ? v->gstreams[k] : v->stream;
         if (G > 1) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
         if (e) HIPCHECK(hipEventRecord(e[4 * k], s));
         PG_POISON(s);
-        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, use_hash, seed, t);
+        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, use_hash, seed, t, v->parity);
         if (e) HIPCHECK(hipEventRecord(e[4 * k + 1], s));
         PG_POISON(s);
         pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 0, 0);
@@ -784,7 +787,11 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.prev_level_complete, n);
     rc |= dalloc(v, &d.level_seed, n);
     rc |= dalloc(v, &d.reset_queue, n * PG_NUM_GAMES);
-    rc |= dalloc(v, &d.reset_count, PG_NUM_GAMES);
+    rc |= dalloc(v, &d.sched, 48);
+    d.reset_count = d.sched + PG_SCHED_RC;
+    rc |= dalloc(v, &d.heavy, 2 * (size_t)PG_NUM_GAMES * PG_HEAVY_CAP);
+    rc |= dalloc(v, &d.heavy_flag, 2 * n);
+    d.heavy_ticks = 10000; // 100 us: ~3x the median coinrun step wave
     if (v->has_latent) rc |= dalloc(v, &d.latent, n * PG_LATENT_N);
     if (gids.size() > 1) rc |= dalloc(v, &v->d_lists, n);
     float *d_rot_angles = nullptr;

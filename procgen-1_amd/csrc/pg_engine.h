@@ -251,7 +251,18 @@ struct PGDev {
     // use_generated_assets: each env's 500 x 500 RGB32 background, repainted by AssetGen at every
     // reset (basic-abstract-game.cpp:60-63, 778-782); null otherwise
     uint32_t *gen_bg;
+    // step launch order (pg_step_kernel): sched = [slow-list length of parity 1 | reset counts
+    // (reset_count points here) | slow-list length of parity 0], 16 ints each (one per game), so one
+    // 32-int memset clears the reset counts with the length of the parity being written.
+    int32_t *sched;
+    int32_t *heavy;             // [2][PG_NUM_GAMES][PG_HEAVY_CAP] each game's slow envs of a step
+    uint8_t *heavy_flag;        // [2][num_envs] env is on its game's slow list
+    int64_t heavy_ticks;        // wall-clock ticks (100 MHz) above which a step counts as slow
 };
+#define PG_HEAVY_CAP 2048
+#define PG_SCHED_RC 16
+#define PG_SCHED_HC(p) ((p) ? 0 : 32)
+#define PG_SCHED_CLEAR(p) ((p) ? 0 : 16) // first of the 32 ints to zero before a launch of parity p
 #define PG_ROT_N 16
 #define PG_TABLE_SLOT 99 // image slot of a game's Qt-tabulated overlay raster (jumper's compass)
 #define PG_LATENT_N (2 + PG_LATENT_GRID + 2 + 2)

@@ -2731,28 +2731,33 @@ DEV uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// Game::step (game.cpp:136-171) minus reset (queued) and observe (pg_render).
-// env_list: the envs of this game (mixed batches), or null = envs 0..gridDim.x-1.
-template <int G>
 #ifndef STEP_WAVES
 #define STEP_WAVES 5 // <= 96 VGPRs: 5 waves per SIMD (measured +4% on the coinrun step)
 #endif
-__global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const int32_t *env_list, int use_hash,
-                                                      uint64_t hash_seed, int32_t hash_t) {
-    __shared__ uint32_t lds_mt[PG_MT_N];
-    __shared__ int16_t lds_list[PG_CAP];
-    __shared__ int16_t lds_slist[64];
-    // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the
-    // workgroups per CU here)
-    __shared__ float4 lds_ibox[pl_smart<G>() ? 64 : 1];
-    __shared__ float lds_pstk[(scan_needed<G>(true) || scan_needed<G>(false)) ? 4 * 5 : 1];
-    __shared__ int lds_iinfo[pl_smart<G>() ? 64 : 1];
-    __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
-    __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
+struct StepLds {
+    uint32_t *mt;
+    int16_t *list, *slist;
+    float4 *ibox;
+    float *pstk;
+    int *iinfo;
+    int8_t *grid;
+    uint8_t *moved;
+};
+
+// Game::step (game.cpp:136-171) of one env by the calling wave, minus reset (queued) and observe
+// (pg_render)
+template <int G>
+DEV void step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t) {
+    uint32_t *lds_mt = L.mt;
+    int16_t *lds_list = L.list, *lds_slist = L.slist;
+    float4 *lds_ibox = L.ibox;
+    float *lds_pstk = L.pstk;
+    int *lds_iinfo = L.iinfo;
+    int8_t *lds_grid = L.grid;
     Ctx c;
     c.d = game_view(d, G);
-    c.moved = lds_moved;
-    c.env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
+    c.moved = L.moved;
+    c.env = env;
     c.s = d.envs[c.env];
     c.E = d.ents;
     c.plane = (size_t)d.num_envs * PG_CAP;
@@ -2845,14 +2850,67 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     c.cs.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 }
 
+
+// Launch order: the previous step's slow envs first, then the game's env list in order.  An env is
+// slow when its step took > d.heavy_ticks of wall clock (e.g. coinrun's crate-pile push chains,
+// ~10x the median step); such envs tend to stay slow for several steps, and dispatching them first
+// lets them overlap the bulk instead of forming the launch's tail (longest first).  The grid is
+// n + PG_HEAVY_CAP workgroups: b < nh steps the b-th slow env; b >= nh the (b - nh)-th env of the
+// list unless it was slow (already taken) or past the end -- those workgroups exit at once.  Each
+// stepped env writes its flag and, when slow, appends itself to this step's list (one atomic per
+// slow env only).  The order only affects scheduling: every env is stepped exactly once and envs
+// are independent.  `parity` alternates per act: the previous step's list / flags are read, this
+// step's are written.  env_list: the envs of this game (mixed batches), or null = envs 0..n-1.
+template <int G>
+__global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const int32_t *env_list, int n, int parity,
+                                                                int use_hash, uint64_t hash_seed, int32_t hash_t) {
+    __shared__ uint32_t lds_mt[PG_MT_N];
+    __shared__ int16_t lds_list[PG_CAP];
+    __shared__ int16_t lds_slist[64];
+    // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the
+    // workgroups per CU here)
+    __shared__ float4 lds_ibox[pl_smart<G>() ? 64 : 1];
+    __shared__ float lds_pstk[(scan_needed<G>(true) || scan_needed<G>(false)) ? 4 * 5 : 1];
+    __shared__ int lds_iinfo[pl_smart<G>() ? 64 : 1];
+    __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
+    __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
+    const int prev = parity ^ 1, b = (int)blockIdx.x;
+    const int nh = min(d.sched[PG_SCHED_HC(prev) + G], PG_HEAVY_CAP);
+    int env;
+    if (b < nh) {
+        env = d.heavy[((size_t)prev * PG_NUM_GAMES + G) * PG_HEAVY_CAP + b];
+    } else {
+        const int p = b - nh;
+        if (p >= n) return;
+        env = env_list ? env_list[p] : p;
+        if (d.heavy_flag[(size_t)prev * d.num_envs + env]) return; // stepped as a slow item
+    }
+    const StepLds L{lds_mt, lds_list, lds_slist, lds_ibox, lds_pstk, lds_iinfo, lds_grid, lds_moved};
+    const uint64_t t0 = wall_clock64();
+    step_env<G>(d, env, L, use_hash, hash_seed, hash_t);
+    const bool heavy = (int64_t)(wall_clock64() - t0) > d.heavy_ticks;
+    if (LANE == 0) {
+        bool listed = false;
+        if (heavy) {
+            const int q = atomicAdd(d.sched + PG_SCHED_HC(parity) + G, 1);
+            listed = q < PG_HEAVY_CAP;
+            if (listed) d.heavy[((size_t)parity * PG_NUM_GAMES + G) * PG_HEAVY_CAP + q] = env;
+        }
+        d.heavy_flag[(size_t)parity * d.num_envs + env] = listed ? 1 : 0;
+    }
+}
+
 } // namespace
 
+// parity: alternates per act (the host zeroes this parity's slow-list length and the reset counts)
 extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
-                               int use_hash, uint64_t seed, int32_t t) {
+                               int use_hash, uint64_t seed, int32_t t, int parity) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                                   \
     case G:                                                                                          \
-        hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, use_hash, seed, t); \
+        hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count + (count < PG_HEAVY_CAP ? count : PG_HEAVY_CAP)), dim3(64), 0, \
+                           s, *d, env_list, count, parity, use_hash,                                 \
+                           seed, t);                                                                 \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)
