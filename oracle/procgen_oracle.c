@@ -4296,6 +4296,21 @@ static inline void qt_blend(uint32_t *dst, uint32_t src, int fmt, int const_alph
     }
 }
 
+/* Render target of the painter calls: the 64x64 observation (aliased, the canvas argument the
+ * primitives get), or -- render_mode="rgb_array" -- a w x h frame painted with Antialiasing +
+ * SmoothPixmapTransform (game.cpp:97-107), where the primitives below switch to qt_smooth_*. */
+typedef struct {
+    uint32_t *px;
+    int w, h;
+    bool smooth;
+    double *log; /* optional command log (tests replay it through the real Qt) */
+    int log_n, log_cap;
+} QtTarget;
+static QtTarget RT = {NULL, 64, 64, false, NULL, 0, 0};
+static void qt_smooth_draw_image(double x, double y, double w, double h, const uint32_t *px, int iw, int ih, int fmt,
+                                 bool mirrored, double opacity);
+static void qt_smooth_fill_rectf(double x, double y, double w, double h, uint32_t argb);
+
 /* QPainter::drawImage(QRectF target, QImage img) with identity transform
  * (qpaintengine_raster.cpp drawImage -> qt_scale_image_32bit). */
 static void qt_scale_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
@@ -4303,6 +4318,10 @@ static void qt_scale_image(uint32_t *canvas, double rx, double ry, double rw, do
 static void qt_draw_image(uint32_t *canvas, double rx, double ry, double rw, double rh, const uint32_t *px, int iw,
                           int ih, int fmt, bool mirrored, double opacity) {
     if (rw <= 0 || rh <= 0) return; /* QRectF::isEmpty */
+    if (RT.smooth) {
+        qt_smooth_draw_image(rx, ry, rw, rh, px, iw, ih, fmt, mirrored, opacity);
+        return;
+    }
     qt_scale_image(canvas, rx, ry, rw, rh, px, iw, ih, fmt, mirrored, opacity);
 }
 /* qt_scale_image_32bit on the already-mapped target rect (width/height may be negative) */
@@ -4546,6 +4565,7 @@ static bool qt_fuzzy_null(double d) { return fabs(d) <= 0.000000000001; }
  * qt_scale_image_32bit on qt_mapRect_non_normalizing(r, matrix), whose TxScale map ignores m12/m21. */
 static void qt_draw_image_rotated(uint32_t *canvas, double x, double y, double w, double h, double deg,
                                   const uint32_t *px, int iw, int ih, bool mirrored, double opacity) {
+    if (RT.smooth) fatal_msg("render_mode=rgb_array: rotated sprites are not restated");
     QtXform t = qt_translate_rotate(x + w / 2, y + h / 2, deg);
     double rx = -w / 2, ry = -h / 2;
     if (w <= 0 || h <= 0) return; /* QRectF::isEmpty */
@@ -4560,6 +4580,10 @@ static void qt_draw_image_rotated(uint32_t *canvas, double x, double y, double w
 
 /* QPainter::fillRect(QRect, QColor) with an opaque color on RGB32 */
 static void qt_fill_rect_int(uint32_t *canvas, int x, int y, int w, int h, uint32_t argb) {
+    if (RT.smooth) { /* QPainter::fillRect(QRect) goes through the QRectF overload */
+        qt_smooth_fill_rectf(x, y, w, h, argb);
+        return;
+    }
     int x1 = x < 0 ? 0 : x, y1 = y < 0 ? 0 : y;
     int x2 = x + w > RES_W ? RES_W : x + w, y2 = y + h > RES_H ? RES_H : y + h;
     for (int yy = y1; yy < y2; yy++)
@@ -4570,6 +4594,10 @@ static void qt_fill_rect_int(uint32_t *canvas, int x, int y, int w, int h, uint3
  * the raster engine fills toNormalizedFillRect(r) = qRound of the four edges, normalised
  * (qpaintengine_raster.cpp).  Pinned against Qt 5.9.7 (tests/golden/qt_raster_fill_goldens.npz). */
 static void qt_fill_rectf(uint32_t *canvas, double x, double y, double w, double h, uint32_t argb) {
+    if (RT.smooth) {
+        qt_smooth_fill_rectf(x, y, w, h, argb);
+        return;
+    }
     int x1 = qRound(x), y1 = qRound(y);
     int x2 = qRound(x + w), y2 = qRound(y + h);
     if (x2 < x1) { int t = x1; x1 = x2; x2 = t; }
@@ -4578,6 +4606,288 @@ static void qt_fill_rectf(uint32_t *canvas, double x, double y, double w, double
 }
 
 typedef struct { double x, y, w, h; } RectD;
+
+/* ------------------------------------------------------------------ Antialiasing + SmoothPixmapTransform
+ * (render_mode="rgb_array": the 512x512 frame, game.cpp:97-107).  Pinned against the real Qt 5.9.7
+ * (tests/test_smooth_pins.py).
+ *
+ * drawImage(QRectF r, img) and fillRect(QRectF r, colour) both rasterise r as a thick line through
+ * QRasterizer::rasterizeLine(mid-left, mid-right, h / w) with antialiasing: the line is clipped
+ * to the device grown by half its width, turned into a vertical line, and emitted as <= 3 spans
+ * per row (left partial column, full columns, right partial column) with 8-bit coverage
+ * (rowHeight x columnCoverage x 255 in 16.16, truncated to a byte -- Qt 5.9 does not subtract a
+ * pixel when both edges fall in one column, so such coverages wrap).  Spans go through a
+ * 256-span buffer; each flush is one blend call whose adjacent spans share one texture fetch.
+ * The fetch is fetchTransformedBilinearARGB32PM for the inverse of translate(1/65536) x scale x
+ * translate(r.topLeft): simple / > 8x vertical upscale -> 8-bit bilinear (top/bottom first);
+ * downscale -> groups of 4 pixels with 4-bit weights (the SSE2 helper), the rest 8-bit. */
+#define QT_SPANBUF 256
+typedef struct { int x, len, y, cov; } QtSpan;
+static int qt_c_int(double v) { return (int)v; }
+
+/* QRasterizer::rasterizeLine(a, b, width) for the rect's mid line, antialiased; clip = [0, cw) x [0, ch) */
+static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int ch, QtSpan *out, int cap) {
+    const double ax = (x + x) * 0.5, ay = (y + (y + h)) * 0.5;
+    const double bx = ((x + w) + (x + w)) * 0.5, by = ay;
+    double width = h / w;
+    double pax = ax, pay = ay, pbx = bx, pby = by;
+    if (ax == bx && ay == by) return 0;
+    {
+        const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
+        const double cl = 0 - offx, ct = 0 - offy;
+        const double cr = cl + ((cw - 1 + 1 + offx) - cl), cb = ct + ((ch - 1 + 1 + offy) - ct);
+        const bool in_a = cl <= pax && pax <= cr && ct <= pay && pay <= cb;
+        const bool in_b = cl <= pbx && pbx <= cr && ct <= pby && pby <= cb;
+        if (!in_a || !in_b) {
+            double t1 = 0, t2 = 1;
+            const double o[2] = {pax, pay}, d[2] = {pbx - pax, pby - pay};
+            const double low[2] = {cl, ct}, high[2] = {cr, cb};
+            for (int i = 0; i < 2; i++) {
+                if (d[i] == 0) {
+                    if (o[i] <= low[i] || o[i] >= high[i]) return 0;
+                    continue;
+                }
+                const double dinv = 1 / d[i];
+                double tl = (low[i] - o[i]) * dinv, th = (high[i] - o[i]) * dinv;
+                if (tl > th) { const double t = tl; tl = th; th = t; }
+                if (t1 < tl) t1 = tl;
+                if (t2 > th) t2 = th;
+                if (t1 >= t2) return 0;
+            }
+            const double nax = pax + (pbx - pax) * t1, nay = pay + (pby - pay) * t1;
+            const double nbx = pax + (pbx - pax) * t2, nby = pay + (pby - pay) * t2;
+            pax = nax; pay = nay; pbx = nbx; pby = nby;
+        }
+    }
+    {
+        const double d0x = ax - bx, d0y = ay - by, w0 = d0x * d0x + d0y * d0y;
+        const double dx = pax - pbx, dy = pay - pby, ww = dx * dx + dy * dy;
+        if (ww == 0) return 0;
+        width *= sqrt(w0 / ww);
+    }
+    { /* horizontal -> vertical (qFuzzyCompare(pa.y, pb.y) holds for the mid line) */
+        const double xm = (pax + pbx) * 0.5f, dx = fabs(pbx - pax) * 0.5f, yy = pay, dy = width * dx;
+        pax = xm; pay = yy - dy;
+        pbx = xm; pby = yy + dy;
+        width = 1 / width;
+    }
+    if (pay > pby) { const double t = pay; pay = pby; pby = t; }
+    const double dy = pby - pay, half = 0.5f * width * dy;
+    double left = pax - half, right = pax + half;
+    left = left < 0 ? 0 : (left > cw ? cw : left);
+    right = right < 0 ? 0 : (right > cw ? cw : right);
+    pay = pay < 0 ? 0 : (pay > ch ? ch : pay);
+    pby = pby < 0 ? 0 : (pby > ch ? ch : pby);
+    if (qt_c_int(left * 64) == qt_c_int(right * 64) || qt_c_int(pay * 64) == qt_c_int(pby * 64)) return 0;
+    const int iL = qt_c_int(left), iR = qt_c_int(right);
+    const int lw = ((iL + 1) << 16) - qt_c_int(left * 65536.), rw = qt_c_int(right * 65536.) - (iR << 16);
+    int cov[3], xs[3], lens[3], n = 1;
+    if (iL == iR) {
+        cov[0] = lw + rw; /* (sic) */
+        xs[0] = iL;
+        lens[0] = 1;
+    } else {
+        cov[0] = lw; xs[0] = iL; lens[0] = 1;
+        if (lw == 65536) {
+            lens[0] = iR - iL;
+        } else if (iR - iL > 1) {
+            cov[1] = 65536; xs[1] = iL + 1; lens[1] = iR - iL - 1;
+            n++;
+        }
+        if (rw) {
+            cov[n] = rw; xs[n] = iR; lens[n] = 1;
+            n++;
+        }
+    }
+    const int iTop = qt_c_int(pay) << 16, iBot = qt_c_int(pby) << 16;
+    const int yPa = qt_c_int(pay * 65536.), yPb = qt_c_int(pby * 65536.);
+    int k = 0;
+    for (int yFP = iTop; yFP <= iBot; yFP += 65536) {
+        const int rh = (yFP + 65536 < yPb ? yFP + 65536 : yPb) - (yFP > yPa ? yFP : yPa);
+        const int yi = yFP >> 16;
+        if (yi > ch - 1) break;
+        for (int i = 0; i < n; i++) {
+            const int c = (int)((((int64_t)rh * (int64_t)(255 * cov[i])) >> 16) >> 16) & 0xff;
+            if (c && lens[i] && k < cap) {
+                QtSpan sp = {xs[i], lens[i], yi, c};
+                out[k++] = sp;
+            }
+        }
+    }
+    return k;
+}
+
+static uint32_t qt_interp_256(uint32_t x, uint32_t a, uint32_t y, uint32_t b) { /* INTERPOLATE_PIXEL_256 */
+    uint32_t t = (x & 0xff00ffu) * a + (y & 0xff00ffu) * b;
+    t = (t >> 8) & 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a + ((y >> 8) & 0xff00ffu) * b;
+    return (x & 0xff00ff00u) | t;
+}
+/* interpolate_4_pixels (SSE2 form): top/bottom with disty first, then left/right with distx */
+static uint32_t qt_interp4_8(uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br, uint32_t dx, uint32_t dy) {
+    const uint32_t l = qt_interp_256(tl, 256 - dy, bl, dy), r = qt_interp_256(tr, 256 - dy, br, dy);
+    return qt_interp_256(l, 256 - dx, r, dx);
+}
+/* interpolate_4_pixels_16: 4-bit weights, one rounding */
+static uint32_t qt_interp4_4(uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br, uint32_t dx, uint32_t dy) {
+    const uint32_t dxy = dx * dy;
+    const uint32_t wtl = 16 * 16 - 16 * dx - 16 * dy + dxy, wtr = dx * 16 - dxy, wbl = dy * 16 - dxy, wbr = dxy;
+    const uint32_t rb = (tl & 0xff00ffu) * wtl + (tr & 0xff00ffu) * wtr + (bl & 0xff00ffu) * wbl + (br & 0xff00ffu) * wbr;
+    const uint32_t ag = ((tl >> 8) & 0xff00ffu) * wtl + ((tr >> 8) & 0xff00ffu) * wtr + ((bl >> 8) & 0xff00ffu) * wbl +
+                        ((br >> 8) & 0xff00ffu) * wbr;
+    return ((rb >> 8) & 0xff00ffu) | (ag & 0xff00ff00u);
+}
+
+/* fetchTransformedBilinearARGB32PM (not tiled) of `len` device pixels from (x, y) for a TxScale
+ * inverse (m11, m22, mdx, mdy); `mirrored` reads the horizontally mirrored image */
+static void qt_fetch_bilinear(uint32_t *out, int x, int y, int len, const uint32_t *px, int iw, int ih, bool mirrored,
+                              double m11, double m22, double mdx, double mdy) {
+#define QT_TEX(r, c) px[(size_t)(r) * iw + (mirrored ? iw - 1 - (c) : (c))]
+    const double cx = x + 0.5, cy = y + 0.5;
+    const int fdx = (int)(m11 * 65536);
+    int fx = (int)((0.0 * cy + m11 * cx + mdx) * 65536) - 32768;
+    const int fy = (int)((m22 * cy + 0.0 * cx + mdy) * 65536) - 32768;
+    int y1 = fy >> 16, y2;
+    if (y1 < 0) y1 = y2 = 0;
+    else if (y1 >= ih - 1) y1 = y2 = ih - 1;
+    else y2 = y1 + 1;
+    const uint32_t dy8 = (uint32_t)(fy & 0xffff) >> 8, dy4 = (dy8 + 8) >> 4;
+    /* helper choice: |fdx| <= 1 -> simple upscale; |m22| < 1/8 -> upscale; else downscale */
+    const bool down = !(abs(fdx) <= 65536) && !(fabs(m22) < 1. / 8.);
+    int n = 0;
+    while (n < len) { /* leading pixels on a clamped column: vertical interpolation only */
+        const int c = fx >> 16;
+        if (!(c < 0 || c >= iw - 1)) break;
+        const int cc = c < 0 ? 0 : iw - 1;
+        out[n++] = qt_interp_256(QT_TEX(y1, cc), 256 - dy8, QT_TEX(y2, cc), dy8);
+        fx += fdx;
+    }
+    int bend = len; /* end of the part that needs no column clamp */
+    const int64_t max_fx = (int64_t)(iw - 1) * 65536;
+    if (fdx > 0) {
+        const int64_t b = n + (max_fx - fx) / fdx;
+        if (b < bend) bend = (int)b;
+    } else if (fdx < 0) {
+        const int64_t b = n + (0 - (int64_t)fx) / fdx;
+        if (b < bend) bend = (int)b;
+    }
+    if (down) { /* the SSE2 loop: 4 pixels at a time, 4-bit weights */
+        while (n < bend - 3) {
+            for (int q = 0; q < 4; q++, n++) {
+                const int c = fx >> 16;
+                const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4;
+                out[n] = qt_interp4_4(QT_TEX(y1, c), QT_TEX(y1, c + 1), QT_TEX(y2, c), QT_TEX(y2, c + 1), dx4, dy4);
+                fx += fdx;
+            }
+        }
+    }
+    for (; n < len; n++) { /* 8-bit weights; columns clamped past `bend` */
+        int c1 = fx >> 16, c2;
+        if (c1 < 0) c1 = c2 = 0;
+        else if (c1 >= iw - 1) c1 = c2 = iw - 1;
+        else c2 = c1 + 1;
+        const uint32_t dx8 = (uint32_t)(fx & 0xffff) >> 8;
+        out[n] = qt_interp4_8(QT_TEX(y1, c1), QT_TEX(y1, c2), QT_TEX(y2, c1), QT_TEX(y2, c2), dx8, dy8);
+        fx += fdx;
+    }
+#undef QT_TEX
+}
+
+static void qt_log(double kind, double a, double b, double c, double d, double e, double f, double g, double h) {
+    if (!RT.log || RT.log_n + 9 > RT.log_cap) return;
+    double *q = RT.log + RT.log_n;
+    q[0] = kind; q[1] = a; q[2] = b; q[3] = c; q[4] = d; q[5] = e; q[6] = f; q[7] = g; q[8] = h;
+    RT.log_n += 9;
+}
+
+/* QPainter::drawImage(QRectF(x, y, w, h), img) under Antialiasing + SmoothPixmapTransform on RT */
+static void qt_smooth_draw_image(double x, double y, double w, double h, const uint32_t *px, int iw, int ih, int fmt,
+                                 bool mirrored, double opacity) {
+    if (iw <= 0 || ih <= 0) return;
+    qt_log(0, x, y, w, h, (double)(uintptr_t)px, iw * 65536.0 + ih, fmt * 2 + (mirrored ? 1 : 0), opacity);
+    const int ca = qt_int_opacity(opacity);
+    if (fmt == QFMT_RGB32 && ca != 256) fatal_msg("rgb_array: translucent RGB32 image");
+    if (w == (double)iw && h == (double)ih) {
+        /* not stretched (and no transform): the untransformed texture fill of the qRound'ed rect,
+         * aliased (QRasterPaintEngine::drawImage -> fillRect_normalized -> blend_untransformed_argb) */
+        int x1 = qRound(x), y1 = qRound(y), x2 = qRound(x + w), y2 = qRound(y + h);
+        const int xoff = -x1, yoff = -y1; /* -qRound(-dx) with dx = -x */
+        const int cov = (255 * ca) >> 8;
+        if (x1 < 0) x1 = 0;
+        if (y1 < 0) y1 = 0;
+        if (x2 > RT.w) x2 = RT.w;
+        if (y2 > RT.h) y2 = RT.h;
+        if (cov == 0) return;
+        for (int yy = y1; yy < y2; yy++) {
+            const int sy = yoff + yy;
+            if (sy < 0 || sy >= ih) continue;
+            for (int xx = x1; xx < x2; xx++) {
+                const int sx = xoff + xx;
+                if (sx < 0 || sx >= iw) continue;
+                uint32_t s = px[(size_t)sy * iw + (mirrored ? iw - 1 - sx : sx)], *dp = RT.px + (size_t)yy * RT.w + xx;
+                if (fmt == QFMT_RGB32) {
+                    *dp = cov == 255 ? s : INTERPOLATE_PIXEL_255(s, (uint32_t)cov, *dp, 255 - (uint32_t)cov);
+                } else if (cov == 255) {
+                    if (s >= 0xff000000u) *dp = s;
+                    else if (s != 0) *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                } else {
+                    s = BYTE_MUL(s, (uint32_t)cov);
+                    *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                }
+            }
+        }
+        return;
+    }
+    /* inverse of (translate(1/65536) * QTransform(sx, 0, 0, sy, x, y)) (QSpanData::setupMatrix) */
+    const double sx = w / iw, sy = h / ih;
+    const double tdx = (1.0 / 65536) * sx + x, tdy = (1.0 / 65536) * sy + y;
+    const double m11 = 1. / sx, m22 = 1. / sy, mdx = -tdx * m11, mdy = -tdy * m22;
+    static QtSpan spans[4096];
+    static uint32_t src[4096];
+    const int ns = qt_aa_rect_spans(x, y, w, h, RT.w, RT.h, spans, 4096);
+    for (int i = 0; i < ns;) {
+        const int x0 = spans[i].x, yy = spans[i].y;
+        int j = i, right = x0 + spans[i].len;
+        while (j + 1 < ns && (j + 1) % QT_SPANBUF != 0 && spans[j + 1].y == yy && spans[j + 1].x == right) right += spans[++j].len;
+        qt_fetch_bilinear(src, x0, yy, right - x0, px, iw, ih, mirrored, m11, m22, mdx, mdy);
+        for (int k = i; k <= j; k++) {
+            const int cov = (spans[k].cov * ca) >> 8;
+            uint32_t *row = RT.px + (size_t)yy * RT.w;
+            for (int xx = spans[k].x; xx < spans[k].x + spans[k].len; xx++) {
+                uint32_t s = src[xx - x0], *dp = &row[xx];
+                if (fmt == QFMT_RGB32) { /* SourceOver of an opaque image = Source (comp_func_Source) */
+                    *dp = cov == 255 ? s : INTERPOLATE_PIXEL_255(s, (uint32_t)cov, *dp, 255 - (uint32_t)cov);
+                } else if (cov == 255) { /* comp_func_SourceOver */
+                    if (s >= 0xff000000u) *dp = s;
+                    else if (s != 0) *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                } else {
+                    s = BYTE_MUL(s, (uint32_t)cov);
+                    *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                }
+            }
+        }
+        i = j + 1;
+    }
+}
+
+/* QPainter::fillRect(QRectF, QColor) with an opaque colour under Antialiasing on RT (blend_color_argb,
+ * SourceOver of an opaque colour = Source) */
+static void qt_smooth_fill_rectf(double x, double y, double w, double h, uint32_t argb) {
+    if ((argb >> 24) != 255) fatal_msg("rgb_array: translucent fill");
+    if (w < 0) { x += w; w = -w; } /* QRectF::normalized */
+    if (h < 0) { y += h; h = -h; }
+    if (w <= 0 || h <= 0) return;
+    qt_log(1, x, y, w, h, (double)argb, 0, 0, 1);
+    static QtSpan spans[4096];
+    const int ns = qt_aa_rect_spans(x, y, w, h, RT.w, RT.h, spans, 4096);
+    for (int k = 0; k < ns; k++) {
+        uint32_t *row = RT.px + (size_t)spans[k].y * RT.w;
+        const uint32_t cov = (uint32_t)spans[k].cov;
+        const uint32_t c = cov == 255 ? argb : BYTE_MUL(argb, cov);
+        for (int xx = spans[k].x; xx < spans[k].x + spans[k].len; xx++)
+            row[xx] = cov == 255 ? c : c + BYTE_MUL(row[xx], 255 - cov);
+    }
+}
 
 /* ================================================================== AssetGen (assetgen.cpp) and the
  * Qt 5.9 raster paths it paints with, on a canvas of any size: fillRect(QRectF, QColor) (opaque,
@@ -5526,8 +5836,8 @@ static void draw_entities(Game *g, const or_atlas *at, int render_z) { /* :1061-
 }
 
 static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
-    qt_fill_rect_int(g->canvas, 0, 0, RES_W, RES_H, 0xff000000u);
-    prepare_for_drawing(g, 64);
+    qt_fill_rect_int(g->canvas, 0, 0, RT.w, RT.h, 0xff000000u);
+    prepare_for_drawing(g, (float)RT.h);
     if (!g->options.use_backgrounds) return;
     RectD main_rect = get_screen_rect(g, 0, (float)g->main_height, (float)g->main_width, (float)g->main_height, 0);
     const or_image *bg = &at->backgrounds[g->background_index];
@@ -5548,7 +5858,7 @@ static void draw_background(Game *g, const or_atlas *at) { /* :988-1016 */
 }
 
 static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
-    prepare_for_drawing(g, 64);
+    prepare_for_drawing(g, (float)RT.h);
     draw_entities(g, at, -1);
     int low_x, high_x, low_y, high_y;
     if (g->options.center_agent) {
@@ -5576,7 +5886,7 @@ static void draw_foreground(Game *g, const or_atlas *at) { /* :930-979 */
     draw_entities(g, at, 1);
     if (g->has_useful_vel_info && g->options.paint_vel_info) { /* :969-977 */
         Entity *agent = AG(g);
-        float infodim = (float)(RES_H * .2);
+        float infodim = (float)(RT.h * .2);
         int s1 = to_shade((float)(.5 * (double)agent->vx / (double)g->maxspeed + .5));
         int s2 = to_shade((float)(.5 * (double)agent->vy / (double)g->max_jump + .5));
         qt_fill_rectf(g->canvas, 0, 0, infodim, infodim, 0xff000000u | (uint32_t)(s1 * 0x010101));
@@ -5603,6 +5913,7 @@ static void jp_stamp(uint32_t *canvas, const uint32_t *rows64, int dx, int dy, u
     }
 }
 static void jp_draw_compass(Game *g, const or_atlas *at) {
+    if (RT.smooth) fatal_msg("render_mode=rgb_array: jumper's compass is not restated");
     const or_image *ti = &at->sprites[JP_TABLE_SLOT];
     fassert(ti->w > 0);
     const uint32_t *t = at->pixels + ti->offset;
@@ -5644,6 +5955,7 @@ static void jp_draw_compass(Game *g, const or_atlas *at) {
 
 static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
     if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:107-124: scrolling tiled background */
+        if (RT.smooth) fatal_msg("render_mode=rgb_array: starpilot is not restated");
         float scale = (float)(RES_H / g->main_height); /* int / int */
         qt_fill_rect_int(g->canvas, 0, 0, RES_W, RES_H, 0xff000000u);
         if (g->options.use_backgrounds) {
@@ -5911,6 +6223,42 @@ void oracle_step(void *h, const int32_t *actions) {
     }
 }
 
+/* render_mode="rgb_array": info["rgb"] of every env, its current state painted at res x res with
+ * Antialiasing + SmoothPixmapTransform (vecgame.cpp:415-423, Game::render_to_buf(buf, RENDER_RES,
+ * RENDER_RES, true), game.cpp:97-107) and converted by bgr32_to_rgb888.  The games whose draws are
+ * all axis-aligned images and fills are restated (bigfish, chaser, climber, coinrun, maze, miner,
+ * ninja); the others return -1.  `log` (optional, `cap` doubles) receives env 0's painter
+ * commands for replay through the real Qt (tests).  Render-time members (unit, view_dim, offsets)
+ * are left as the 64-px observe sets them, as the step path reads them from there. */
+int oracle_render_rgb_array(void *h, uint8_t *rgb, int res, double *log, int cap) {
+    Vec *v = (Vec *)h;
+    uint32_t *frame = (uint32_t *)malloc((size_t)res * res * 4);
+    int rc = 0;
+    for (int n = 0; n < v->count && rc == 0; n++) {
+        Game *g = &v->games[n];
+        switch (g->game_id) {
+        case GAME_BIGFISH: case GAME_CHASER: case GAME_CLIMBER: case GAME_COINRUN: case GAME_MAZE: case GAME_MINER:
+        case GAME_NINJA: break;
+        default: rc = -1; continue;
+        }
+        Game saved = *g;
+        RT.px = frame; RT.w = res; RT.h = res; RT.smooth = true;
+        RT.log = n == 0 ? log : NULL; RT.log_n = 0; RT.log_cap = cap;
+        render(g, v->atlas);
+        RT.px = NULL; RT.w = RES_W; RT.h = RES_H; RT.smooth = false; RT.log = NULL;
+        *g = saved; /* the 64-px render-time members */
+        uint8_t *d = rgb + (size_t)n * res * res * 3;
+        for (size_t p = 0; p < (size_t)res * res; p++) {
+            const uint32_t c = frame[p];
+            d[3 * p + 0] = (uint8_t)(c >> 16);
+            d[3 * p + 1] = (uint8_t)(c >> 8);
+            d[3 * p + 2] = (uint8_t)c;
+        }
+    }
+    free(frame);
+    return rc;
+}
+
 void oracle_observe(void *h, uint8_t *rgb, float *rew, uint8_t *first, int32_t *prev_level_seed,
                     uint8_t *prev_level_complete, int32_t *level_seed) {
     Vec *v = (Vec *)h;
@@ -6102,6 +6450,18 @@ static double rd_f64(Rd *r) {
 }
 
 /* replays ONE case body (after the canvas words) of tools/qt_raster_golden.cpp's format */
+/* one Antialiasing + SmoothPixmapTransform primitive on a cw x ch RGB32 canvas (tests/test_smooth_pins.py,
+ * against tools/qt_smooth_probe.cpp on the real Qt): kind 0 drawImage(QRectF, img [mirrored]) with
+ * opacity, kind 1 fillRect(QRectF, opaque colour) */
+void oracle_qt_smooth(int cw, int ch, uint32_t *inout, int kind, const uint32_t *img, int iw, int ih, int fmt,
+                      int mirrored, double x, double y, double w, double h, double opacity, uint32_t argb) {
+    QtTarget saved = RT;
+    RT.px = inout; RT.w = cw; RT.h = ch; RT.smooth = true; RT.log = NULL;
+    if (kind == 0) qt_draw_image(inout, x, y, w, h, img, iw, ih, fmt, mirrored != 0, opacity);
+    else qt_fill_rectf(inout, x, y, w, h, argb);
+    RT = saved;
+}
+
 /* qt-utils.h / grid.h pins (tests/test_oracle_pins.py, against the reference headers compiled in
  * oracle/_ref): adjust_rect over (x, y, w, h) quadruples, to_shade of floats, and the Grid
  * operations the oracle's Game grid restates (contains, get_obj's in-range read / out-of-bounds

@@ -94,6 +94,9 @@ void oracle_adjust_rect(const double *base, const double *adj, double *out, int6
 void oracle_to_shade(const float *f, int32_t *out, int64_t n);
 int oracle_grid_ops(int w, int h, const int32_t *xy, int n, int32_t *out);
 void oracle_diag_counters(long long *out, int reset);
+int oracle_render_rgb_array(void *h, uint8_t *rgb, int res, double *log, int cap);
+void oracle_qt_smooth(int cw, int ch, uint32_t *inout, int kind, const uint32_t *img, int iw, int ih, int fmt,
+                      int mirrored, double x, double y, double w, double h, double opacity, uint32_t argb);
 void oracle_bigfish_radius(const float *u, float *out, int64_t n);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);

@@ -1,0 +1,137 @@
+"""Pins of the oracle's render_mode="rgb_array" primitives -- CPU only.
+
+The 512x512 frame (vecgame.cpp:318-330, 415-423 -> Game::render_to_buf with antialias = true,
+game.cpp:97-107) is painted with QPainter::Antialiasing + SmoothPixmapTransform.  The oracle
+restates the two primitives the supported games paint with (oracle/procgen_oracle.c qt_smooth_*):
+drawImage(QRectF, QImage) -- antialiased rect coverage + bilinear fetch -- and fillRect(QRectF, QColor).
+Both are checked here against the REAL Qt 5.9.7 raster engine of this image through
+tools/qt_smooth_probe.cpp (oracle/_ref/libqt_probe.so, built by `make -C oracle ref`; absent on the
+GPU box, where these tests skip): random rects on 64- and 512-px canvases, up- and downscaling,
+clipped at every border, premultiplied sprites with transparent texels, mirrored images, opacity,
+RGB32 backgrounds -- bit-exact.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+PROBE = os.path.join(os.path.dirname(oracle_lib.REF_SO), "libqt_probe.so")
+D, I, P, U = ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32
+
+
+def libs():
+    if not os.path.exists(PROBE):
+        pytest.skip("oracle/_ref/libqt_probe.so not built (needs Qt at build time)")
+    q = ctypes.CDLL(PROBE)
+    q.qtp_draw.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, D, U, I, I]
+    o = oracle_lib.load()
+    o.oracle_qt_smooth.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, U]
+    return q, o
+
+
+def both(q, o, canvas, kind, img, fmt, mir, x, y, w, h, op=1.0, argb=0):
+    a = np.ascontiguousarray(canvas.copy())
+    b = np.ascontiguousarray(canvas.copy())
+    im = np.ascontiguousarray(img if img is not None else np.zeros((1, 1), np.uint32))
+    q.qtp_draw(a.shape[1], a.shape[0], a.ctypes.data, kind, im.ctypes.data, im.shape[1], im.shape[0], fmt, mir,
+               x, y, w, h, 0.0, op, argb, 1, 1)
+    o.oracle_qt_smooth(b.shape[1], b.shape[0], b.ctypes.data, kind, im.ctypes.data, im.shape[1], im.shape[0], fmt,
+                       mir, x, y, w, h, op, argb)
+    return a, b
+
+
+def _canvas(rng, W):
+    return rng.randint(0, 1 << 24, (W, W)).astype(np.uint32) | np.uint32(0xff000000)
+
+
+@pytest.mark.parametrize("W", [64, 512])
+def test_smooth_fill_rect(W):
+    """fillRect(QRectF, opaque colour) under Antialiasing: thin, sub-pixel, clipped and large rects."""
+    q, o = libs()
+    rng = np.random.RandomState(W)
+    for k in range(600 if W == 64 else 150):
+        x, y = rng.uniform(-W * 0.3, W * 0.95, 2)
+        w, h = rng.uniform(0.05, W * 0.6, 2)
+        if k % 3 == 0:
+            w, h = rng.uniform(0.02, 2.5, 2)
+        if k % 11 == 0:
+            x, y, w, h = 0.0, 0.0, float(W), float(W)  # the black background fill
+        col = 0xff000000 | int(rng.randint(0, 1 << 24))
+        a, b = both(q, o, _canvas(rng, W), 1, None, 6, 0, x, y, w, h, argb=col)
+        np.testing.assert_array_equal(b, a, err_msg="fill (%r, %r, %r, %r) on %d px" % (x, y, w, h, W))
+
+
+@pytest.mark.parametrize("W", [64, 512])
+def test_smooth_draw_image(W):
+    """drawImage(QRectF, QImage) with SmoothPixmapTransform + Antialiasing: every fetch helper
+    (simple upscale, > 8x vertical upscale, 4-bit SSE2 downscale groups + 8-bit tail), the 256-span
+    buffer flushes, clamped edges, transparent texels, mirrored images, opacity, RGB32 sources."""
+    q, o = libs()
+    rng = np.random.RandomState(100 + W)
+    for k in range(160 if W == 64 else 60):
+        iw, ih = rng.randint(2, 150, 2)
+        img = rng.randint(0, 1 << 24, (ih, iw)).astype(np.uint32) | np.uint32(0xff000000)
+        fmt = 6
+        if k % 3 == 0:
+            img[rng.rand(ih, iw) < 0.4] = 0  # premultiplied sprite with transparent texels
+        op = 1.0
+        if k % 5 == 0:
+            fmt = 4  # RGB32 background
+        elif k % 7 == 0:
+            op = float(rng.choice([0.5, 0.25, 0.7, 0.3]))
+        mir = int(k % 4 == 1)
+        x, y = rng.uniform(-W * 0.2, W * 0.95, 2)
+        w, h = rng.uniform(1, W * 0.5, 2)
+        if k % 9 == 0:
+            h = w * rng.uniform(9, 14)  # > 8x vertical upscale helper
+        if k % 13 == 0:
+            w, h = float(iw), float(ih)  # not stretched: the untransformed texture fill
+        a, b = both(q, o, _canvas(rng, W), 0, img, fmt, mir, x, y, w, h, op=op)
+        np.testing.assert_array_equal(b, a, err_msg="image %dx%d fmt %d mir %d op %r at (%r, %r, %r, %r) on %d px"
+                                      % (iw, ih, fmt, mir, op, x, y, w, h, W))
+
+
+def replay(q, log, res):
+    """The oracle's logged painter commands of one frame through the real Qt, on one canvas."""
+    canvas = np.zeros((res, res), np.uint32) | np.uint32(0xff000000)
+    for row in log:
+        kind = int(row[0])
+        x, y, w, h = (float(v) for v in row[1:5])
+        if kind == 1:
+            canvas = _draw(q, canvas, 1, None, 6, 0, x, y, w, h, 1.0, int(row[5]))
+        else:
+            ptr, dims, fm, op = int(row[5]), int(row[6]), int(row[7]), float(row[8])
+            iw, ih = dims >> 16, dims & 0xffff
+            img = np.ctypeslib.as_array((ctypes.c_uint32 * (iw * ih)).from_address(ptr)).reshape(ih, iw).copy()
+            canvas = _draw(q, canvas, 0, img, fm >> 1, fm & 1, x, y, w, h, op, 0)
+    return canvas
+
+
+def _draw(q, canvas, kind, img, fmt, mir, x, y, w, h, op, argb):
+    a = np.ascontiguousarray(canvas)
+    im = np.ascontiguousarray(img if img is not None else np.zeros((1, 1), np.uint32))
+    q.qtp_draw(a.shape[1], a.shape[0], a.ctypes.data, kind, im.ctypes.data, im.shape[1], im.shape[0], fmt, mir,
+               x, y, w, h, 0.0, op, argb, 1, 1)
+    return a
+
+
+@pytest.mark.parametrize("game", ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja"])
+def test_rgb_array_frames_replayed_through_qt(game):
+    """Whole 512x512 rgb_array frames: the oracle paints the frame of a running env and logs every
+    painter call (background fill + image, grid tiles, entities, overlays); the same calls replayed
+    through the real Qt with Antialiasing + SmoothPixmapTransform give the same pixels."""
+    q, _ = libs()
+    orc = oracle_lib.OracleEnv(game, 1, num_levels=0, rand_seed=3, paint_vel_info=1)
+    rng = np.random.RandomState(4)
+    for t in range(40):
+        orc.step(rng.randint(0, 15, 1).astype(np.int32))
+        if t % 13 != 12:
+            continue
+        rgb, log = orc.render_rgb_array(512, log_cap=4000)
+        assert len(log) > 3
+        qt_frame = replay(q, log, 512)
+        ref = np.stack([(qt_frame >> 16) & 255, (qt_frame >> 8) & 255, qt_frame & 255], -1).astype(np.uint8)
+        np.testing.assert_array_equal(rgb[0], ref, err_msg="%s step %d" % (game, t))
