@@ -28,6 +28,8 @@ void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
                      int grid);
 void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s);
+int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames, uint8_t *rgb,
+                           hipStream_t s);
 int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s);
 void pg_launch_poison(hipStream_t s, uint32_t pattern);
 
@@ -297,7 +299,10 @@ struct VecEnv {
     int num_envs = 0;
     int env_offset = 0;
     int num_actions = 15;
-    bool render_human = false;
+    bool render_human = false; // render_mode="rgb_array": info["rgb"] at RENDER_RES (vecgame.cpp:318-330, 415-423)
+    uint32_t *hr_frames = nullptr; // [num_envs][512 * 512] RGB32 frames of the antialiased render
+    uint8_t *hr_rgb = nullptr;     // [num_envs][512 * 512 * 3] their bgr32_to_rgb888
+    size_t hr_info = 0;            // index of the "rgb" info tensor
     PGDev dev{};
     hipStream_t stream = nullptr;
     std::vector<libenv_tensortype> ob_types, ac_types, info_types;
@@ -337,6 +342,7 @@ struct VecEnv {
     // games of the batch: env n plays games[n % games.size()]
     std::vector<int> games;
     int32_t *d_lists = nullptr;            // [games.size()][num_envs / games.size()] env ids (mixed only)
+    std::vector<int32_t> h_lists;          // host copy of d_lists
     // mixed batches: each game's step -> reset -> render chain runs on its own stream (the games'
     // envs are disjoint), forked from and joined back into `stream` every act
     std::vector<hipStream_t> gstreams;
@@ -559,6 +565,22 @@ int copy_out(VecEnv *v) {
 
 int copy_latent(VecEnv *v) {
     const size_t n = (size_t)v->num_envs;
+    if (v->render_human) { // VecGame::observe: every env's frame at RENDER_RES (vecgame.cpp:415-423)
+        const size_t per = (size_t)512 * 512, cnt = (size_t)v->count_of();
+        for (size_t k = 0; k < v->games.size(); k++)
+            if (pg_launch_render_hires(&v->dev, v->games[k], v->list_of(k), (int)cnt, v->hr_frames + k * cnt * per,
+                                       v->hr_rgb + k * cnt * per * 3, v->stream) != 0)
+                return fail(v, PG_ERR_BAD_OPTION, "render_mode=rgb_array: game not built");
+        HIPCHECK(hipGetLastError());
+        std::vector<uint8_t> host(cnt * per * 3);
+        for (size_t k = 0; k < v->games.size(); k++) {
+            HIPCHECK(copy_sync(v, host.data(), v->hr_rgb + k * cnt * per * 3, host.size(), hipMemcpyDeviceToHost));
+            for (size_t q = 0; q < cnt; q++) {
+                const size_t e = v->games.size() > 1 ? (size_t)v->h_lists[k * cnt + q] : q; // list_of(k) order
+                memcpy(v->info_ptrs[v->hr_info * n + e], host.data() + q * per * 3, per * 3);
+            }
+        }
+    }
     if (v->has_latent) { // grid_size, grid, agent_pos, exit_pos (vecgame.cpp:270-316)
         const size_t row = (size_t)PG_LATENT_N * 4;
         std::vector<int32_t> lat((size_t)PG_LATENT_N * n);
@@ -715,7 +737,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     }
     if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
     if (env_offset < 0) return bad("env_offset must be >= 0");
-    if (render_human) return bad("render_mode=rgb_array (render_human) is not in this build yet");
+    if (render_human) // the antialiased primitives are restated for the games that draw only axis-aligned images / fills
+        for (int g : gids)
+            if (g != PG_GAME_BIGFISH && g != PG_GAME_CHASER && g != PG_GAME_CLIMBER && g != PG_GAME_COINRUN &&
+                g != PG_GAME_MAZE && g != PG_GAME_MINER && g != PG_GAME_NINJA)
+                return bad("render_mode=rgb_array is built for bigfish, chaser, climber, coinrun, maze, miner and ninja "
+                           "(the games whose frames are axis-aligned images and fills)");
 
     VecEnv *v = new VecEnv();
     v->num_envs = num_envs;
@@ -756,6 +783,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     v->info_types.push_back(make_type("grid", LIBENV_DTYPE_INT32, {35 * 35}, 0, INT32_MAX));
     v->info_types.push_back(make_type("agent_pos", LIBENV_DTYPE_INT32, {2}, 0, 35));
     v->info_types.push_back(make_type("exit_pos", LIBENV_DTYPE_INT32, {2}, 0, 35));
+    if (render_human) { // vecgame.cpp:318-330
+        v->hr_info = v->info_types.size();
+        v->info_types.push_back(make_type("rgb", LIBENV_DTYPE_UINT8, {512, 512, 3}, 0, 255));
+    }
 
     // level seed bounds (vecgame.cpp:332-341)
     int level_seed_low = 0, level_seed_high = 0;
@@ -793,6 +824,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
     d.heavy_ticks = 10000; // 100 us: ~3x the median coinrun step wave
     if (v->has_latent) rc |= dalloc(v, &d.latent, n * PG_LATENT_N);
+    if (render_human) {
+        rc |= dalloc(v, &v->hr_frames, n * 512 * 512);
+        rc |= dalloc(v, &v->hr_rgb, n * 512 * 512 * 3);
+    }
     if (gids.size() > 1) rc |= dalloc(v, &v->d_lists, n);
     float *d_rot_angles = nullptr;
     double *d_rot_table = nullptr;
@@ -848,6 +883,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             size_t r = (size_t)((((int64_t)k - env_offset) % (int64_t)ng + (int64_t)ng) % (int64_t)ng);
             for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + r);
         }
+        v->h_lists = lists;
     }
     float rot_angles[PG_ROT_N];
     double rot_table[PG_ROT_N * 4];
@@ -1006,7 +1042,7 @@ LIBENV_API void libenv_set_buffers(libenv_env *env, struct libenv_buffers *bufs)
     // maze/miner (maze.cpp:152-165, miner.cpp:378-396); zero them for the other games (copy_out
     // overwrites them every observe when a game of the batch has a latent state)
     for (size_t k = 3; k < v->info_types.size(); k++) {
-        size_t bytes = 4;
+        size_t bytes = v->info_types[k].dtype == LIBENV_DTYPE_UINT8 ? 1 : 4;
         for (int dd = 0; dd < v->info_types[k].ndim; dd++) bytes *= (size_t)v->info_types[k].shape[dd];
         for (size_t e = 0; e < n; e++) memset(v->info_ptrs[k * n + e], 0, bytes);
     }

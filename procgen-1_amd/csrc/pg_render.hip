@@ -1948,6 +1948,495 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 
+// ================================================================== render_mode="rgb_array"
+// The RENDER_RES x RENDER_RES frame of info["rgb"] (vecgame.cpp:318-330, 415-423: Game::render_to_buf
+// with antialias = true, game.cpp:97-107): the same game_draw as the observation, painted with
+// QPainter::Antialiasing + SmoothPixmapTransform.  The primitives are the oracle's pinned restatement
+// (oracle/procgen_oracle.c qt_smooth_*, tests/test_smooth_pins.py against the real Qt 5.9.7):
+//   * a rect -> QRasterizer::rasterizeLine spans (<= 3 per row, 8-bit coverage, 256-span buffer
+//     flushes), computed per pixel in closed form;
+//   * drawImage -> fetchTransformedBilinearARGB32PM of each span run (a pixel's weights -- 4-bit in
+//     the downscale helper's groups of 4, else 8-bit -- follow from its offset in the run), then
+//     SourceOver (premultiplied sprites) / Source (opaque RGB32 backgrounds) with the coverage;
+//   * fillRect(opaque colour) -> Source with the coverage.
+// One 256-thread workgroup per env; the frame lives in HBM (1 MB per env), every primitive is
+// painted by all threads over its footprint and a barrier orders it before the next.  The games
+// whose draws are all axis-aligned images and fills are built (bigfish, chaser, climber, coinrun,
+// maze, miner, ninja); libenv_make rejects render_mode="rgb_array" for the others.
+#define HR_RES 512
+#define HR_THREADS 256
+
+struct HRect { // QRasterizer::rasterizeLine of one axis-aligned rect (uniform)
+    int n;                 // spans per row (0: nothing drawn)
+    int xs[3], lens[3], cov[3];
+    int r0, r1;            // first / last row
+    int yPa, yPb;          // 16.16 top / bottom
+    int k1;                // nonzero spans of the first row
+    int kM;                // nonzero spans of a full row
+};
+
+DEV int hr_span_cov(const HRect &R, int r, int i) {
+    const int yFP = r << 16;
+    const int rh = min(yFP + 65536, R.yPb) - max(yFP, R.yPa);
+    return (int)((((int64_t)rh * (int64_t)(255 * R.cov[i])) >> 16) >> 16) & 0xff;
+}
+DEV int hr_row_count(const HRect &R, int r) {
+    int c = 0;
+    for (int i = 0; i < R.n; i++) c += hr_span_cov(R, r, i) != 0;
+    return c;
+}
+DEV void hr_rect(double x, double y, double w, double h, HRect &R) {
+    R.n = 0;
+    const double ax = (x + x) * 0.5, ay = (y + (y + h)) * 0.5;
+    const double bx = ((x + w) + (x + w)) * 0.5, by = ay;
+    double width = h / w;
+    double pax = ax, pay = ay, pbx = bx, pby = by;
+    if (ax == bx && ay == by) return;
+    {
+        const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
+        const double cl = 0 - offx, ct = 0 - offy;
+        const double cr = cl + ((HR_RES - 1 + 1 + offx) - cl), cb = ct + ((HR_RES - 1 + 1 + offy) - ct);
+        const bool in_a = cl <= pax && pax <= cr && ct <= pay && pay <= cb;
+        const bool in_b = cl <= pbx && pbx <= cr && ct <= pby && pby <= cb;
+        if (!in_a || !in_b) {
+            double t1 = 0, t2 = 1;
+            const double o[2] = {pax, pay}, dd[2] = {pbx - pax, pby - pay};
+            const double low[2] = {cl, ct}, high[2] = {cr, cb};
+            for (int i = 0; i < 2; i++) {
+                if (dd[i] == 0) {
+                    if (o[i] <= low[i] || o[i] >= high[i]) return;
+                    continue;
+                }
+                const double dinv = 1 / dd[i];
+                double tl = (low[i] - o[i]) * dinv, th = (high[i] - o[i]) * dinv;
+                if (tl > th) { const double t = tl; tl = th; th = t; }
+                if (t1 < tl) t1 = tl;
+                if (t2 > th) t2 = th;
+                if (t1 >= t2) return;
+            }
+            const double nax = pax + (pbx - pax) * t1, nay = pay + (pby - pay) * t1;
+            const double nbx = pax + (pbx - pax) * t2, nby = pay + (pby - pay) * t2;
+            pax = nax; pay = nay; pbx = nbx; pby = nby;
+        }
+    }
+    {
+        const double d0x = ax - bx, d0y = ay - by, w0 = d0x * d0x + d0y * d0y;
+        const double dx = pax - pbx, dy = pay - pby, ww = dx * dx + dy * dy;
+        if (ww == 0) return;
+        width *= sqrt(w0 / ww);
+    }
+    {
+        const double xm = (pax + pbx) * 0.5f, dx = fabs(pbx - pax) * 0.5f, yy = pay, dy = width * dx;
+        pax = xm; pay = yy - dy;
+        pbx = xm; pby = yy + dy;
+        width = 1 / width;
+    }
+    if (pay > pby) { const double t = pay; pay = pby; pby = t; }
+    const double dy = pby - pay, half = 0.5f * width * dy;
+    double left = pax - half, right = pax + half;
+    left = left < 0 ? 0 : (left > HR_RES ? HR_RES : left);
+    right = right < 0 ? 0 : (right > HR_RES ? HR_RES : right);
+    pay = pay < 0 ? 0 : (pay > HR_RES ? HR_RES : pay);
+    pby = pby < 0 ? 0 : (pby > HR_RES ? HR_RES : pby);
+    if ((int)(left * 64) == (int)(right * 64) || (int)(pay * 64) == (int)(pby * 64)) return;
+    const int iL = (int)left, iR = (int)right;
+    const int lw = ((iL + 1) << 16) - (int)(left * 65536.), rw = (int)(right * 65536.) - (iR << 16);
+    int n = 1;
+    if (iL == iR) {
+        R.cov[0] = lw + rw; // (sic, Qt 5.9)
+        R.xs[0] = iL;
+        R.lens[0] = 1;
+    } else {
+        R.cov[0] = lw; R.xs[0] = iL; R.lens[0] = 1;
+        if (lw == 65536) {
+            R.lens[0] = iR - iL;
+        } else if (iR - iL > 1) {
+            R.cov[1] = 65536; R.xs[1] = iL + 1; R.lens[1] = iR - iL - 1;
+            n++;
+        }
+        if (rw) {
+            R.cov[n] = rw; R.xs[n] = iR; R.lens[n] = 1;
+            n++;
+        }
+    }
+    R.n = n;
+    R.r0 = (int)pay;
+    R.r1 = min((int)pby, HR_RES - 1);
+    R.yPa = (int)(pay * 65536.);
+    R.yPb = (int)(pby * 65536.);
+    R.k1 = hr_row_count(R, R.r0);
+    R.kM = R.r0 + 1 < R.r1 ? hr_row_count(R, R.r0 + 1) : 0;
+}
+// global index (in the rasterizer's emission order) of row r's first span
+DEV int hr_row_base(const HRect &R, int r) {
+    if (r == R.r0) return 0;
+    return R.k1 + (r - R.r0 - 1) * R.kM;
+}
+
+DEV uint32_t hr_interp_256(uint32_t x, uint32_t a, uint32_t y, uint32_t b) {
+    uint32_t t = (x & 0xff00ffu) * a + (y & 0xff00ffu) * b;
+    t = (t >> 8) & 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a + ((y >> 8) & 0xff00ffu) * b;
+    return (x & 0xff00ff00u) | t;
+}
+DEV uint32_t hr_interp4_8(uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br, uint32_t dx, uint32_t dy) {
+    const uint32_t l = hr_interp_256(tl, 256 - dy, bl, dy), r = hr_interp_256(tr, 256 - dy, br, dy);
+    return hr_interp_256(l, 256 - dx, r, dx);
+}
+DEV uint32_t hr_interp4_4(uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br, uint32_t dx, uint32_t dy) {
+    const uint32_t dxy = dx * dy;
+    const uint32_t wtl = 16 * 16 - 16 * dx - 16 * dy + dxy, wtr = dx * 16 - dxy, wbl = dy * 16 - dxy, wbr = dxy;
+    const uint32_t rb = (tl & 0xff00ffu) * wtl + (tr & 0xff00ffu) * wtr + (bl & 0xff00ffu) * wbl + (br & 0xff00ffu) * wbr;
+    const uint32_t ag = ((tl >> 8) & 0xff00ffu) * wtl + ((tr >> 8) & 0xff00ffu) * wtr + ((bl >> 8) & 0xff00ffu) * wbl +
+                        ((br >> 8) & 0xff00ffu) * wbr;
+    return ((rb >> 8) & 0xff00ffu) | (ag & 0xff00ff00u);
+}
+DEV uint32_t hr_interp_255(uint32_t x, uint32_t a, uint32_t y, uint32_t b) {
+    uint32_t t = (x & 0xff00ffu) * a + (y & 0xff00ffu) * b;
+    t = (t + ((t >> 8) & 0xff00ffu) + 0x800080u) >> 8;
+    t &= 0xff00ffu;
+    x = ((x >> 8) & 0xff00ffu) * a + ((y >> 8) & 0xff00ffu) * b;
+    x = (x + ((x >> 8) & 0xff00ffu) + 0x800080u);
+    x &= 0xff00ff00u;
+    return x | t;
+}
+
+// one primitive (uniform arguments); all threads of the workgroup
+struct HOp {
+    int kind;              // 0 image, 1 opaque fill
+    double x, y, w, h;
+    const uint32_t *px;    // image pixels (row-major iw x ih)
+    int iw, ih, rgb32, mir, ca;
+    uint32_t argb;
+};
+
+DEV void hr_blend(uint32_t *dp, uint32_t s, int cov, bool rgb32) {
+    if (rgb32) { // SourceOver of an opaque image = Source (comp_func_Source)
+        *dp = cov == 255 ? s : hr_interp_255(s, (uint32_t)cov, *dp, 255 - (uint32_t)cov);
+    } else if (cov == 255) { // comp_func_SourceOver
+        if (s >= 0xff000000u) *dp = s;
+        else if (s != 0) *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+    } else {
+        s = BYTE_MUL(s, (uint32_t)cov);
+        *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+    }
+}
+
+DEV void hr_paint(uint32_t *frame, const HOp &op) {
+    const int tid = threadIdx.x;
+    if (op.kind == 0 && op.w == (double)op.iw && op.h == (double)op.ih) {
+        // not stretched: untransformed texture fill of the qRound'ed rect (aliased)
+        const int x1 = qRound(op.x), y1 = qRound(op.y), x2 = qRound(op.x + op.w), y2 = qRound(op.y + op.h);
+        const int cx1 = max(x1, 0), cy1 = max(y1, 0), cx2 = min(x2, HR_RES), cy2 = min(y2, HR_RES);
+        const int cov = (255 * op.ca) >> 8;
+        if (cov == 0 || cx1 >= cx2 || cy1 >= cy2) return;
+        const int cw = cx2 - cx1, tot = cw * (cy2 - cy1);
+        for (int p = tid; p < tot; p += HR_THREADS) {
+            const int yy = cy1 + p / cw, xx = cx1 + p % cw;
+            const int sy = yy - y1, sx = xx - x1;
+            if (sy < 0 || sy >= op.ih || sx < 0 || sx >= op.iw) continue;
+            hr_blend(frame + (size_t)yy * HR_RES + xx, op.px[(size_t)sy * op.iw + (op.mir ? op.iw - 1 - sx : sx)], cov,
+                     op.rgb32 != 0);
+        }
+        return;
+    }
+    double x = op.x, y = op.y, w = op.w, h = op.h;
+    if (op.kind == 1) {
+        if (w < 0) { x += w; w = -w; }
+        if (h < 0) { y += h; h = -h; }
+        if (w <= 0 || h <= 0) return;
+    }
+    HRect R;
+    hr_rect(x, y, w, h, R);
+    if (R.n == 0 || R.r1 < R.r0) return;
+    const int x0 = R.xs[0], x1 = R.xs[R.n - 1] + R.lens[R.n - 1];
+    const int cw = x1 - x0, tot = cw * (R.r1 - R.r0 + 1);
+    // drawImage: inverse of (translate(1/65536) * QTransform(sx, 0, 0, sy, x, y)) (QSpanData::setupMatrix)
+    double m11 = 0, m22 = 0, mdx = 0, mdy = 0;
+    int fdx = 0;
+    bool down = false;
+    if (op.kind == 0) {
+        const double sxs = w / op.iw, sys = h / op.ih;
+        const double tdx = (1.0 / 65536) * sxs + x, tdy = (1.0 / 65536) * sys + y;
+        m11 = 1. / sxs; m22 = 1. / sys; mdx = -tdx * m11; mdy = -tdy * m22;
+        fdx = (int)(m11 * 65536);
+        down = !(abs(fdx) <= 65536) && !(fabs(m22) < 1. / 8.);
+    }
+    for (int p = tid; p < tot; p += HR_THREADS) {
+        const int r = R.r0 + p / cw, xx = x0 + p % cw;
+        int j = 0; // the span of this pixel
+        while (j + 1 < R.n && xx >= R.xs[j] + R.lens[j]) j++;
+        const int cov0 = hr_span_cov(R, r, j);
+        if (cov0 == 0) continue;
+        uint32_t *dp = frame + (size_t)r * HR_RES + xx;
+        if (op.kind == 1) {
+            const uint32_t c = cov0 == 255 ? op.argb : BYTE_MUL(op.argb, (uint32_t)cov0);
+            *dp = cov0 == 255 ? c : c + BYTE_MUL(*dp, 255 - (uint32_t)cov0);
+            continue;
+        }
+        // the fetch run of this pixel: this row's emitted spans, restarting at every 256-span flush
+        const int base = hr_row_base(R, r);
+        int e = 0, seg_s = -1, seg_e = -1;
+        for (int i = 0; i < R.n; i++) {
+            if (hr_span_cov(R, r, i) == 0) continue;
+            const bool restart = seg_s < 0 || ((base + e) % 256) == 0;
+            if (restart) {
+                if (i > j) break;
+                seg_s = R.xs[i];
+            }
+            seg_e = R.xs[i] + R.lens[i];
+            e++;
+            if (i >= j) {
+                // extend over the following emitted spans of the same run
+                int k = e;
+                for (int i2 = i + 1; i2 < R.n; i2++) {
+                    if (hr_span_cov(R, r, i2) == 0) continue;
+                    if (((base + k) % 256) == 0) break;
+                    seg_e = R.xs[i2] + R.lens[i2];
+                    k++;
+                }
+                break;
+            }
+        }
+        const int n = xx - seg_s, len = seg_e - seg_s;
+        const double cy = r + 0.5;
+        const int fx0 = (int)((0.0 * cy + m11 * (seg_s + 0.5) + mdx) * 65536) - 32768;
+        const int fy = (int)((m22 * cy + 0.0 * (seg_s + 0.5) + mdy) * 65536) - 32768;
+        int y1 = fy >> 16, y2;
+        if (y1 < 0) y1 = y2 = 0;
+        else if (y1 >= op.ih - 1) y1 = y2 = op.ih - 1;
+        else y2 = y1 + 1;
+        const uint32_t dy8 = (uint32_t)(fy & 0xffff) >> 8, dy4 = (dy8 + 8) >> 4;
+        // leading clamped pixels, bounded end, 4-bit groups (fetchTransformedBilinearARGB32PM helpers)
+        int n0 = 0;
+        {
+            const int c0 = fx0 >> 16;
+            if (c0 >= op.iw - 1) {
+                n0 = len;
+            } else if (c0 < 0) {
+                n0 = (int)((-(int64_t)fx0 + fdx - 1) / fdx); // first n with fx >= 0
+                if (n0 > len) n0 = len;
+                if (n0 < len && ((fx0 + n0 * fdx) >> 16) >= op.iw - 1) n0 = len;
+            }
+        }
+        const int fxn0 = fx0 + n0 * fdx;
+        int bend = len;
+        {
+            const int64_t b = n0 + ((int64_t)(op.iw - 1) * 65536 - fxn0) / fdx;
+            if (b < bend) bend = (int)b;
+        }
+        int groups = 0;
+        if (down && bend - 3 > n0) groups = (bend - 4 - n0) / 4 + 1;
+        const int fx = fx0 + n * fdx;
+        const uint32_t *row1 = op.px + (size_t)y1 * op.iw, *row2 = op.px + (size_t)y2 * op.iw;
+#define HR_TEX(rowp, c) (rowp)[op.mir ? op.iw - 1 - (c) : (c)]
+        uint32_t src;
+        if (n < n0) {
+            const int c = (fx >> 16) < 0 ? 0 : op.iw - 1;
+            src = hr_interp_256(HR_TEX(row1, c), 256 - dy8, HR_TEX(row2, c), dy8);
+        } else if (n < n0 + 4 * groups) {
+            const int c = fx >> 16;
+            const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4;
+            src = hr_interp4_4(HR_TEX(row1, c), HR_TEX(row1, c + 1), HR_TEX(row2, c), HR_TEX(row2, c + 1), dx4, dy4);
+        } else {
+            int c1 = fx >> 16, c2;
+            if (c1 < 0) c1 = c2 = 0;
+            else if (c1 >= op.iw - 1) c1 = c2 = op.iw - 1;
+            else c2 = c1 + 1;
+            const uint32_t dx8 = (uint32_t)(fx & 0xffff) >> 8;
+            src = hr_interp4_8(HR_TEX(row1, c1), HR_TEX(row1, c2), HR_TEX(row2, c1), HR_TEX(row2, c2), dx8, dy8);
+        }
+#undef HR_TEX
+        hr_blend(dp, src, (cov0 * op.ca) >> 8, op.rgb32 != 0);
+    }
+}
+
+DEV void hr_run(uint32_t *frame, const HOp &op) {
+    hr_paint(frame, op);
+    __syncthreads();
+}
+
+// draw_image (basic-abstract-game.cpp:886-922) for the rgb_array games: no rotation, no tiling
+template <int G>
+DEV bool hr_draw_image(uint32_t *frame, const PGDev &d, const PGEnv &s, double bx, double by, double bw, double bh,
+                       bool refl, int base_type, int theme, float alpha, int player_img) {
+    const int img = image_for_type<G>(s, base_type, player_img);
+    if (img < 0) return true;
+    HOp op;
+    op.kind = 1; op.px = nullptr; op.iw = op.ih = 0; op.rgb32 = 0; op.mir = 0; op.ca = 256; op.argb = 0;
+    if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) { // draw_grid_obj (:924-928)
+        if (img == SPACE) return true;
+        if (G == PG_GAME_CHASER && img == CH_ORB) { // chaser.cpp:111-117
+            const float dim = 0.3f, k = 1 - dim;
+            op.x = bx + bw * k / 2; op.y = by + bh * k / 2; op.w = bw * dim; op.h = bh * dim; op.argb = 0xff00ff00u;
+            hr_run(frame, op);
+            return true;
+        }
+        const uint32_t col = color_for_type<G>(s, img, theme);
+        if (col == 0) return false;
+        op.x = bx; op.y = by; op.w = bw; op.h = bh; op.argb = col;
+        hr_run(frame, op);
+        return true;
+    }
+    theme = mask_theme<G>(s, theme, img);
+    if (theme < 0 || theme >= 10) return false;
+    if constexpr (G == PG_GAME_COINRUN) {
+        if (is_player_image(img)) { // coinrun.cpp:64-70
+            by = by + bh * -.7415;
+            bh = bh * 1.7415;
+            bx = bx + bw * 0.0;
+            bw = bw * 1.0;
+        }
+    }
+    const int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+    if (sp.y <= 0) return missing_image_ok<G>(img);
+    if (!(bw > 0) || !(bh > 0)) return true; // QRectF::isEmpty
+    if ((size_t)sp.x + (size_t)sp.y * sp.z > d.num_pixels) return false;
+    op.kind = 0; op.x = bx; op.y = by; op.w = bw; op.h = bh;
+    op.px = d.pixels + sp.x; op.iw = sp.y; op.ih = sp.z; op.mir = refl ? 1 : 0;
+    op.ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
+    hr_run(frame, op);
+    return true;
+}
+
+template <int G>
+DEV bool hr_entities(uint32_t *frame, const PGDev &d, const PGEnv &s, const View &v, int env, int z, int player_img) {
+    bool ok = true;
+    for (int i = 0; i < s.num_ents; i++) {
+        if (EIr(d, F_RENDER_Z, env, i) != z) continue;
+        const int itype = EIr(d, F_IMAGE_TYPE, env, i), theme = EIr(d, F_IMAGE_THEME, env, i);
+        if (!should_draw<G>(s, EIr(d, F_TYPE, env, i), theme)) continue;
+        if (EFr(d, F_ROTATION, env, i) != 0) { ok = false; continue; }
+        const float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
+        const float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
+        const int flags = EIr(d, F_FLAGS, env, i);
+        double rx, ry, rw, rh;
+        if (flags & EF_ABS_COORDS) { // get_abs_rect (:812-814)
+            const float vd = v.view_dim;
+            const float ax = vd * (px_ - prx), ay = vd * (py_ + pry), aw = 2 * vd * prx, ah = 2 * vd * pry;
+            rx = (double)(ax * v.unit); ry = (double)(ay * v.unit); rw = (double)(aw * v.unit); rh = (double)(ah * v.unit);
+        } else {
+            screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
+        }
+        ok = hr_draw_image<G>(frame, d, s, rx, ry, rw, rh, (flags & EF_REFLECTED) != 0, itype, theme,
+                              EFr(d, F_ALPHA, env, i), player_img) && ok;
+    }
+    return ok;
+}
+
+template <int G>
+__global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, const int32_t *env_list, uint32_t *frames,
+                                                                     uint8_t *rgb) {
+    const PGDev d = game_view(dg, G);
+    const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
+    const int slot = blockIdx.x; // frame / rgb rows of this launch
+    uint32_t *frame = frames + (size_t)slot * HR_RES * HR_RES;
+    const PGEnv s = d.envs[env];
+    const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
+    bool ok = true;
+    float agent_x, agent_y, agent_vx, agent_vy;
+    if (s.agent_erased) {
+        agent_x = s.ghost_x; agent_y = s.ghost_y; agent_vx = s.ghost_vx; agent_vy = s.ghost_vy;
+    } else {
+        agent_x = EFr(d, F_X, env, 0); agent_y = EFr(d, F_Y, env, 0);
+        agent_vx = EFr(d, F_VX, env, 0); agent_vy = EFr(d, F_VY, env, 0);
+    }
+    const int player_img = player_image<G>(s, agent_vx);
+    // prepare_for_drawing(rect_height = RENDER_RES) (basic-abstract-game.cpp:828-847)
+    View v;
+    v.center_x = (float)(s.main_width * .5);
+    v.center_y = (float)(s.main_height * .5);
+    v.visibility = s.visibility;
+    if (s.opt_center_agent) {
+        if constexpr (G == PG_GAME_CLIMBER) { // climber.cpp:291-295
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
+            v.visibility = (float)s.main_width;
+        } else {
+            v.center_x = agent_x;
+            v.center_y = agent_y;
+        }
+    } else {
+        v.visibility = (float)(s.main_width > s.main_height ? s.main_width : s.main_height);
+        if (v.visibility < s.min_visibility) v.visibility = s.min_visibility;
+    }
+    const float raw_unit = 64 / v.visibility;
+    v.unit = (float)((double)raw_unit * ((double)(float)HR_RES / 64.0));
+    v.view_dim = (float)(64.0 / (double)raw_unit);
+    v.x_off = v.unit * (v.center_x - v.view_dim / 2);
+    v.y_off = v.unit * (v.center_y - v.view_dim / 2);
+
+    // draw_background (:988-1016): fillRect(rect, black) + the background image
+    HOp op;
+    op.kind = 1; op.x = 0; op.y = 0; op.w = HR_RES; op.h = HR_RES; op.argb = 0xff000000u;
+    op.px = nullptr; op.iw = op.ih = 0; op.rgb32 = 0; op.mir = 0; op.ca = 256;
+    hr_run(frame, op);
+    if (s.opt_use_backgrounds) {
+        if (s.bg_tile_ratio < 0) ok = false; // tiled backgrounds: not in the rgb_array games
+        double mx, my, mw, mh;
+        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
+        const int4 bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
+        const float bgw = (float)bgi.y, bgh = (float)bgi.z;
+        const float bg_ar = bgw / bgh;
+        const float world_ar = (float)(s.main_width * 1.0 / s.main_height);
+        const float offset_x = s.bg_pct_x * (bg_ar - world_ar);
+        const double ax = (double)(-offset_x), aw = (double)(bg_ar / world_ar);
+        op.kind = 0; op.x = mx + mw * ax; op.y = my + mh * 0.0; op.w = mw * aw; op.h = mh * 1.0;
+        op.px = (d.gen_bg ? d.gen_bg + (size_t)env * (500 * 500) : d.pixels + bgi.x);
+        op.iw = bgi.y; op.ih = bgi.z; op.rgb32 = 1; op.mir = 0; op.ca = 256;
+        if (op.w > 0 && op.h > 0 && op.iw > 0 && op.ih > 0) hr_run(frame, op);
+    }
+    // draw_foreground (:930-979)
+    if constexpr (has_z_minus1<G>()) ok = hr_entities<G>(frame, d, s, v, env, -1, player_img) && ok;
+    int low_x, high_x, low_y, high_y;
+    if (s.opt_center_agent) {
+        const double margin = (double)v.visibility / 2.0 + 1;
+        low_x = (int)((double)v.center_x - margin);
+        high_x = (int)((double)v.center_x + margin);
+        low_y = (int)((double)v.center_y - margin);
+        high_y = (int)((double)v.center_y + margin);
+    } else {
+        low_x = 0; high_x = s.main_width - 1; low_y = 0; high_y = s.main_height - 1;
+    }
+    for (int x = low_x; x <= high_x; x++) {
+        for (int y = low_y; y <= high_y; y++) {
+            const int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                       : s.out_of_bounds_object;
+            if (type == INVALID_OBJ) continue;
+            double rx, ry, rw, rh;
+            screen_rect(v, (float)x, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+            ok = hr_draw_image<G>(frame, d, s, rx, ry, rw, rh, false, type, grid_theme<G>(s, type), 1.0f, player_img) && ok;
+        }
+    }
+    ok = hr_entities<G>(frame, d, s, v, env, 0, player_img) && ok;
+    ok = hr_entities<G>(frame, d, s, v, env, 1, player_img) && ok;
+    if (s.has_useful_vel_info && s.opt_paint_vel_info) { // :969-977
+        const float infodim = (float)(HR_RES * .2);
+        const int s1 = to_shade((float)(.5 * (double)agent_vx / (double)s.maxspeed + .5));
+        const int s2 = to_shade((float)(.5 * (double)agent_vy / (double)s.max_jump + .5));
+        op.kind = 1; op.x = 0; op.y = 0; op.w = infodim; op.h = infodim; op.argb = 0xff000000u | (uint32_t)(s1 * 0x010101);
+        hr_run(frame, op);
+        op.x = infodim; op.argb = 0xff000000u | (uint32_t)(s2 * 0x010101);
+        hr_run(frame, op);
+    }
+    if constexpr (G == PG_GAME_NINJA) { // ninja.cpp:155-164: jump charge bar, get_abs_rect (:812-814)
+        const float u = v.unit, bar_height = 3 * s.gs.nj.jump_charge;
+        op.kind = 1; op.x = (double)(.25f * u); op.y = (double)((float)(v.visibility - .5 - bar_height) * u);
+        op.w = (double)(.5f * u); op.h = (double)(bar_height * u); op.argb = 0xff42f587u;
+        hr_run(frame, op);
+    }
+    // bgr32_to_rgb888 (game.cpp:8-23) into info["rgb"]
+    uint8_t *out = rgb + (size_t)slot * HR_RES * HR_RES * 3;
+    for (int p = threadIdx.x; p < HR_RES * HR_RES; p += HR_THREADS) {
+        const uint32_t c = frame[p];
+        out[3 * p + 0] = (uint8_t)(c >> 16);
+        out[3 * p + 1] = (uint8_t)(c >> 8);
+        out[3 * p + 2] = (uint8_t)c;
+    }
+    if (!ok && threadIdx.x == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
+}
+
 extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                              \
@@ -1986,4 +2475,25 @@ extern "C" __global__ __launch_bounds__(256) void pg_poison_lds_kernel(uint32_t 
 
 extern "C" void pg_launch_poison(hipStream_t s, uint32_t pattern) {
     hipLaunchKernelGGL(pg_poison_lds_kernel, dim3(2048), dim3(256), 0, s, pattern);
+}
+
+// render_mode="rgb_array": frames / rgb hold `count` RENDER_RES^2 slots (the game's envs in list order)
+extern "C" int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames,
+                                      uint8_t *rgb, hipStream_t s) {
+    if (count <= 0) return 0;
+    switch (game) {
+#define PG_CASE(G)                                                                                               \
+    case G:                                                                                                      \
+        hipLaunchKernelGGL(pg_render_hires_kernel<G>, dim3(count), dim3(HR_THREADS), 0, s, *d, env_list, frames, rgb); \
+        return 0;
+        PG_CASE(PG_GAME_BIGFISH)
+        PG_CASE(PG_GAME_CHASER)
+        PG_CASE(PG_GAME_CLIMBER)
+        PG_CASE(PG_GAME_COINRUN)
+        PG_CASE(PG_GAME_MAZE)
+        PG_CASE(PG_GAME_MINER)
+        PG_CASE(PG_GAME_NINJA)
+#undef PG_CASE
+    default: return -1;
+    }
 }

@@ -13,8 +13,9 @@ published semantics (gym3 0.3.3 ``interop.py``):
   already the next episode's first frame.
 * infos are ``env.get_info()``, one dict per env.
 
-``render_mode="human"`` (gym3's ViewerWrapper window) and ``"rgb_array"`` (512x512
-``info["rgb"]``) are not in this build: ``ProcgenGym3Env`` rejects them at ``libenv_make``.
+``render_mode="rgb_array"`` (the 512x512 antialiased ``info["rgb"]``) is built for the games whose
+frames are axis-aligned images and fills (``ProcgenGym3Env`` rejects it at ``libenv_make`` for the
+others); ``render_mode="human"`` needs gym3's ViewerWrapper window, which this build has not.
 """
 import numpy as np
 
@@ -24,8 +25,8 @@ from .env import ENV_NAMES, ProcgenGym3Env
 class ToBaselinesVecEnv:
     """gym3.ToBaselinesVecEnv + procgen's render() (procgen/env.py:276-286)."""
 
-    # "human" needs gym3's viewer window and render_mode="rgb_array"'s 512x512 frame, neither built;
-    # render("rgb_array") returns the 64x64 observation of env 0
+    # "human" needs gym3's viewer window; render("rgb_array") returns env 0's info["rgb"] (the 512x512
+    # frame of render_mode="rgb_array") or else its 64x64 observation
     metadata = {"render.modes": ["rgb_array"], "video.frames_per_second": 15}
 
     def __init__(self, env):
@@ -99,9 +100,12 @@ class ToGymEnv:
         rew, ob, first = self.env.observe()
         return ob[self.key][0], float(rew[0]), bool(first[0]), self.env.get_info()[0]
 
-    def render(self, mode="rgb_array"):
+    def render(self, mode="rgb_array"):  # gym3 ToGymEnv.render: the info dict's "rgb" entry
         if mode != "rgb_array":
             raise NotImplementedError("render(mode=%r): no viewer window in this build" % mode)
+        info = self.env.get_info()[0]
+        if "rgb" in info:
+            return info["rgb"]
         _, ob, _ = self.env.observe()
         return ob[self.key][0]
 
@@ -112,12 +116,11 @@ class ToGymEnv:
 def make_env(render_mode=None, render=False, **kwargs):  # procgen/gym_registration.py:6-26
     if render:
         render_mode = "human"
-    if render_mode is not None:
-        # the reference routes both modes through render_mode="rgb_array" (the 512x512 antialiased
-        # info["rgb"], vecgame.cpp:318-330), which this build does not draw
-        raise NotImplementedError("make_env(render_mode=%r): the 512x512 render_mode='rgb_array' frame is "
-                                  "not built; use the 64x64 observation" % render_mode)
-    return ToGymEnv(ProcgenGym3Env(num=1, num_threads=0, **kwargs))
+    if render_mode == "human":
+        # the reference wraps the env in gym3's ViewerWrapper (a window fed by info["rgb"])
+        raise NotImplementedError("make_env(render_mode='human'): no viewer window in this build; use "
+                                  "render_mode='rgb_array' and env.render()")
+    return ToGymEnv(ProcgenGym3Env(num=1, num_threads=0, render_mode=render_mode, **kwargs))
 
 
 ENV_IDS = {"procgen-%s-v0" % name: name for name in ENV_NAMES}

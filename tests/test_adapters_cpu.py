@@ -85,12 +85,18 @@ def test_env_ids():
     assert sorted(ids.values()) == sorted(ENV_NAMES) and ids["procgen-coinrun-v0"] == "coinrun"
 
 
-def test_make_env_render_modes_not_built():
-    """make_env(render_mode=...) / render=True need the 512x512 rgb_array frame (vecgame.cpp:318-330),
-    which this build does not draw: a clear NotImplementedError before any env is created."""
+def test_make_env_render_modes():
+    """make_env(render_mode="human") / render=True need gym3's viewer window: a clear
+    NotImplementedError before any env is created; render_mode="rgb_array" is passed through to
+    ProcgenGym3Env (libenv's render_human), whose unsupported games are rejected at libenv_make."""
     import pytest
     from procgen_amd.adapters import ToBaselinesVecEnv, make_env
-    for kw in ({"render_mode": "rgb_array"}, {"render_mode": "human"}, {"render": True}):
+    from procgen_amd.env import ProcgenError
+    for kw in ({"render_mode": "human"}, {"render": True}):
         with pytest.raises(NotImplementedError):
             make_env(env_name="coinrun", **kw)
+    with pytest.raises((ProcgenError, ValueError, RuntimeError)):
+        make_env(env_name="starpilot", render_mode="rgb_array")  # rotated sprites: not built
+    with pytest.raises(Exception):
+        make_env(env_name="coinrun", render_mode="bogus")
     assert ToBaselinesVecEnv.metadata["render.modes"] == ["rgb_array"]
