@@ -18,6 +18,9 @@
 
 #include "../../include/libenv.h"
 #include "../../include/procgen_mi355x.h"
+
+#define PG_EV_G 7 // timing events per game and act: step start / end, reset start / end (side stream),
+                  // render of the unfinished envs end, render of the finished envs start / end
 #include "pg_assets.h"
 #include "pg_state.h"
 #include "pg_engine.h"
@@ -27,7 +30,7 @@ void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count
                     uint64_t seed, int32_t t, int parity);
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
                      int grid);
-void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s);
+void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode);
 int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames, uint8_t *rgb,
                            hipStream_t s);
 int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s);
@@ -347,6 +350,10 @@ struct VecEnv {
     // envs are disjoint), forked from and joined back into `stream` every act
     std::vector<hipStream_t> gstreams;
     std::vector<hipEvent_t> gdone;
+    // per game: the stream the reset kernel runs on while the envs that did not finish render, and
+    // the events ordering step -> reset -> render of the finished envs
+    std::vector<hipStream_t> rstreams;
+    std::vector<hipEvent_t> ev_stepped, ev_reset;
     hipEvent_t fork = nullptr;
     bool has_latent = false;               // maze fills the fork's latent-state info
     // game of env e: the global index decides (vecgame.cpp:357-358), so a shard at env_offset
@@ -420,8 +427,8 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
     const size_t G = v->games.size();
-    hipEvent_t *e = nullptr; // 4 per game: before step, after step, after reset, after render; then 2 wall
-    const size_t per = 4 * G + 2;
+    hipEvent_t *e = nullptr; // PG_EV_G per game (see procgen_kernel_times); then 2 wall
+    const size_t per = PG_EV_G * G + 2;
     if (v->timing) {
         size_t need = (size_t)(v->t_used + 1) * per;
         while (v->ev.size() < need) {
@@ -432,30 +439,51 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         e = &v->ev[(size_t)v->t_used * per];
         v->t_used++;
     }
-    if (e) HIPCHECK(hipEventRecord(e[4 * G], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * G], v->stream));
     // reset counts and the slow-list length of this act's step order (PGDev::sched)
     v->parity ^= 1;
     HIPCHECK(hipMemsetAsync(v->dev.sched + PG_SCHED_CLEAR(v->parity), 0, sizeof(int32_t) * 32, v->stream));
     if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     for (size_t k = 0; k < G; k++) {
-        hipStream_t s = G > 1 ? v->gstreams[k] : v->stream;
+        // single game: the finished envs' resets (level generation: long single-wave chains) run on
+        // a side stream while the envs that did not finish render; a mixed batch keeps each game's
+        // step -> reset -> render chain on its stream (its 16 chains already overlap, and twice as
+        // many streams over the GPU_MAX_HW_QUEUES queues measured slower: 14.5 vs 17.4 M env-steps/s)
+        const bool split = G == 1;
+        hipStream_t s = G > 1 ? v->gstreams[k] : v->stream, r = split ? v->rstreams[k] : s;
         if (G > 1) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
-        if (e) HIPCHECK(hipEventRecord(e[4 * k], s));
+        if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
         pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, use_hash, seed, t, v->parity);
-        if (e) HIPCHECK(hipEventRecord(e[4 * k + 1], s));
+        if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 1], s));
+        if (split) {
+            HIPCHECK(hipEventRecord(v->ev_stepped[k], s));
+            HIPCHECK(hipStreamWaitEvent(r, v->ev_stepped[k], 0));
+        }
+        if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 2], r));
+        PG_POISON(r);
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), r, 0, 0);
+        if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 3], r));
         PG_POISON(s);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 0, 0);
-        if (e) HIPCHECK(hipEventRecord(e[4 * k + 2], s));
-        PG_POISON(s);
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s);
-        if (e) HIPCHECK(hipEventRecord(e[4 * k + 3], s));
+        if (split) {
+            HIPCHECK(hipEventRecord(v->ev_reset[k], r));
+            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 1);
+            if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s));
+            HIPCHECK(hipStreamWaitEvent(s, v->ev_reset[k], 0));
+            if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
+            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 2);
+        } else {
+            if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s)); // unused without the split
+            if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
+            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 0);
+        }
+        if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
         if (G > 1) {
             HIPCHECK(hipEventRecord(v->gdone[k], s));
             HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
         }
     }
-    if (e) HIPCHECK(hipEventRecord(e[4 * G + 1], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * G + 1], v->stream));
     HIPCHECK(hipGetLastError());
     return 0;
 }
@@ -756,6 +784,23 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         delete v;
         return bad("hipStreamCreate failed");
     }
+    if (gids.size() == 1) { // the reset's side stream (mixed batches keep each game's chain on one stream)
+        bool ok = true;
+        for (size_t k = 0; k < gids.size() && ok; k++) {
+            hipStream_t s = nullptr;
+            hipEvent_t a = nullptr, b = nullptr;
+            ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&a, hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&b, hipEventDisableTiming) == hipSuccess;
+            v->rstreams.push_back(s);
+            v->ev_stepped.push_back(a);
+            v->ev_reset.push_back(b);
+        }
+        if (!ok) {
+            libenv_close((libenv_env *)v);
+            return bad("hipStreamCreate failed");
+        }
+    }
     if (gids.size() > 1) {
         bool ok = hipEventCreateWithFlags(&v->fork, hipEventDisableTiming) == hipSuccess;
         for (size_t k = 0; k < gids.size() && ok; k++) {
@@ -819,6 +864,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.level_seed, n);
     rc |= dalloc(v, &d.reset_queue, n * PG_NUM_GAMES);
     rc |= dalloc(v, &d.sched, 48);
+    rc |= dalloc(v, &d.done8, n);
     d.reset_count = d.sched + PG_SCHED_RC;
     rc |= dalloc(v, &d.heavy, 2 * (size_t)PG_NUM_GAMES * PG_HEAVY_CAP);
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
@@ -1020,7 +1066,7 @@ LIBENV_API int procgen_start(libenv_env *env) {
     }
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0);
     }
     HIPCHECK(hipGetLastError());
     v->started = true;
@@ -1089,6 +1135,12 @@ LIBENV_API void libenv_close(libenv_env *env) {
         if (e) hipEventDestroy(e);
     for (auto &e : v->gdone)
         if (e) hipEventDestroy(e);
+    for (auto &e : v->ev_stepped)
+        if (e) hipEventDestroy(e);
+    for (auto &e : v->ev_reset)
+        if (e) hipEventDestroy(e);
+    for (auto &s : v->rstreams)
+        if (s) hipStreamDestroy(s);
     if (v->fork) hipEventDestroy(v->fork);
     for (auto &s : v->gstreams)
         if (s) hipStreamDestroy(s);
@@ -1177,28 +1229,32 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
 // Averages over the steps timed since procgen_set_timing(env, 1), ms:
 //   out[0] step kernel, out[1] reset kernel, out[2] render kernel -- each the SUM over the
 //          batch's games (a mixed batch runs the games' chains concurrently on their own streams,
-//          so these sums can exceed the step's wall time);
+//          so these sums can exceed the step's wall time; a single game's reset runs on a side
+//          stream concurrently with the render of the envs that did not finish, and its render
+//          time is both passes);
 //   out[3] wall span of the whole step on the env's stream (before the fork -> after the join);
 //   out[4 + 3g .. 6 + 3g] step / reset / render of game slot g (v->games order).
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
-    const size_t G = v->games.size(), per = 4 * G + 2;
+    const size_t G = v->games.size(), per = PG_EV_G * G + 2;
     std::vector<double> sum(4 + 3 * G, 0.0);
     if (v->t_used > 0) {
         HIPCHECK(hipStreamSynchronize(v->stream));
         for (int k = 0; k < v->t_used; k++) {
             hipEvent_t *base = &v->ev[(size_t)k * per];
             for (size_t g = 0; g < G; g++) {
-                hipEvent_t *e = base + 4 * g;
-                float a = 0, b = 0, c = 0;
-                HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));
-                HIPCHECK(hipEventElapsedTime(&b, e[1], e[2]));
-                HIPCHECK(hipEventElapsedTime(&c, e[2], e[3]));
+                hipEvent_t *e = base + PG_EV_G * g;
+                float a = 0, b = 0, c1 = 0, c2 = 0;
+                HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));  // step
+                HIPCHECK(hipEventElapsedTime(&b, e[2], e[3]));  // reset (side stream)
+                if (G == 1) HIPCHECK(hipEventElapsedTime(&c1, e[1], e[4])); // render of the unfinished envs
+                HIPCHECK(hipEventElapsedTime(&c2, e[5], e[6])); // render of the finished envs
+                const float c = c1 + c2;
                 sum[0] += a; sum[1] += b; sum[2] += c;
                 sum[4 + 3 * g] += a; sum[5 + 3 * g] += b; sum[6 + 3 * g] += c;
             }
             float w = 0;
-            HIPCHECK(hipEventElapsedTime(&w, base[4 * G], base[4 * G + 1]));
+            HIPCHECK(hipEventElapsedTime(&w, base[PG_EV_G * G], base[PG_EV_G * G + 1]));
             sum[3] += w;
         }
     }
@@ -1407,7 +1463,7 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
     for (size_t k = 0; k < v->games.size(); k++)
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0);
     hipStreamSynchronize(v->stream);
 }
 

@@ -255,6 +255,7 @@ struct PGDev {
     // (reset_count points here) | slow-list length of parity 0], 16 ints each (one per game), so one
     // 32-int memset clears the reset counts with the length of the parity being written.
     int32_t *sched;
+    uint8_t *done8;            // [num_envs] the last step ended the episode (a reset is queued)
     int32_t *heavy;             // [2][PG_NUM_GAMES][PG_HEAVY_CAP] each game's slow envs of a step
     uint8_t *heavy_flag;        // [2][num_envs] env is on its game's slow list
     int64_t heavy_ticks;        // wall-clock ticks (100 MHz) above which a step counts as slow

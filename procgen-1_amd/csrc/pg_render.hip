@@ -1389,7 +1389,7 @@ DEV constexpr int rot_cap() {
 }
 
 template <int G>
-__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list) {
+__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode) {
     const PGDev d = game_view(dg, G);
     constexpr int HR = frame_rows<G>();
     __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES]; // the rows of one pass
@@ -1415,7 +1415,16 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     constexpr int EGK = 4; // images per texel-prefetch group (8 measured slower for every game)
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
-    const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
+    // mode 0: every env of the list; 1: the envs whose step did not end the episode (drawn while
+    // the reset kernel regenerates the others); 2: this step's reset queue (after the reset)
+    int env;
+    if (mode == 2) {
+        if ((int)blockIdx.x >= d.reset_count[G]) return;
+        env = d.reset_queue[(size_t)G * d.num_envs + blockIdx.x];
+    } else {
+        env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
+        if (mode == 1 && d.done8[env]) return;
+    }
     const PGEnv s = d.envs[env];
     const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
     bool err = false;
@@ -2437,11 +2446,12 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
     if (!ok && threadIdx.x == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
 }
 
-extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s) {
+// mode: see pg_render_kernel (0 all, 1 envs not done, 2 the reset queue: `count` bounds its length)
+extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                              \
     case G:                                                                                     \
-        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list); \
+        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, mode); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

@@ -2814,6 +2814,7 @@ DEV void step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
             int q = atomicAdd(d.reset_count + G, 1);
             d.reset_queue[(size_t)G * d.num_envs + q] = c.env;
         }
+        d.done8[c.env] = (uint8_t)done;
         d.rew[c.env] = c.s.sd_reward;
         d.first[c.env] = (uint8_t)first;
         d.prev_level_seed[c.env] = c.s.prev_level_seed;

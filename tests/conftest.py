@@ -23,3 +23,18 @@ def has_gpu():
 @pytest.fixture(scope="session")
 def gpu_available():
     return has_gpu()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """torch's HIP runtime must initialise before the engine's in a process that uses both (the
+    gather tests): when the engine's runtime claims the device first, torch reports no GPU.  Only
+    in runs that select gpu tests."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+    yield
