@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,8 +29,8 @@
 extern "C" {
 void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int use_hash,
                     uint64_t seed, int32_t t, int parity);
-void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int all_envs,
-                     int grid);
+void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode, int grid,
+                     int act);
 void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode);
 int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames, uint8_t *rgb,
                            hipStream_t s);
@@ -354,6 +355,13 @@ struct VecEnv {
     // the events ordering step -> reset -> render of the finished envs
     std::vector<hipStream_t> rstreams;
     std::vector<hipEvent_t> ev_stepped, ev_reset;
+    // level prefetch (PGDev::sp_*): the spare generation of act t runs on pstreams[t % npstreams];
+    // the reset of act t waits for the generation launched at act t - lag (ev_pre[t % lag])
+    bool prefetch = false;
+    int act_no = 0, lag = 2, npstreams = 1;
+    hipStream_t pstreams[2] = {nullptr, nullptr};
+    hipEvent_t ev_pre[PG_SP_LAG_MAX] = {};
+    bool ev_pre_set[PG_SP_LAG_MAX] = {};
     hipEvent_t fork = nullptr;
     bool has_latent = false;               // maze fills the fork's latent-state info
     // game of env e: the global index decides (vecgame.cpp:357-358), so a shard at env_offset
@@ -462,8 +470,22 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 2], r));
         PG_POISON(r);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), r, 0, 0);
+        const int act = v->act_no;
+        if (v->prefetch) { // the spares the swaps may use (requested at act - 2) are complete
+            const int i = act % v->lag; // also the ring slot of this act's requests
+            if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(r, v->ev_pre[i], 0));
+            HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, r));
+        }
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), r, 0, 0, act);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 3], r));
+        if (v->prefetch) { // the next levels of the envs just reset, off the critical path
+            hipStream_t p = v->pstreams[act % v->npstreams];
+            HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
+            HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
+            pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), p, 2, 0, act);
+            HIPCHECK(hipEventRecord(v->ev_pre[act % v->lag], p));
+            v->ev_pre_set[act % v->lag] = true;
+        }
         PG_POISON(s);
         if (split) {
             HIPCHECK(hipEventRecord(v->ev_reset[k], r));
@@ -484,6 +506,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         }
     }
     if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * G + 1], v->stream));
+    v->act_no++;
     HIPCHECK(hipGetLastError());
     return 0;
 }
@@ -865,6 +888,57 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.reset_queue, n * PG_NUM_GAMES);
     rc |= dalloc(v, &d.sched, 48);
     rc |= dalloc(v, &d.done8, n);
+    // level prefetch: single-game batches, random level seeds (a sequential level's seed depends on
+    // how the episode ends), no generated backgrounds (1 MB per env per spare).  On by default for the
+    // games whose reset is on the critical path (long level generation that outlasts the render of
+    // the other envs: caveflyer 24.5 -> 29.6, jumper 20.6 -> 21.7 M env-steps/s); the others lose
+    // 1-5 % to the extra work (profiles/r03/prefetch_sweep.txt).  PROCGEN_MI355X_PREFETCH=0 / 1 forces
+    // it off / on.
+    {
+        const char *pf = getenv("PROCGEN_MI355X_PREFETCH");
+        const bool by_game = gids.size() == 1 && (gids[0] == PG_GAME_CAVEFLYER || gids[0] == PG_GAME_JUMPER);
+        v->prefetch = gids.size() == 1 && !use_generated_assets && !use_sequential_levels &&
+                      (pf ? pf[0] != '0' : by_game);
+        const char *lg = getenv("PROCGEN_MI355X_PREFETCH_LAG"), *ps = getenv("PROCGEN_MI355X_PREFETCH_STREAMS");
+        if (lg) v->lag = std::min(std::max(atoi(lg), 1), PG_SP_LAG_MAX);
+        if (ps) v->npstreams = std::min(std::max(atoi(ps), 1), 2);
+        d.sp_lag = v->lag;
+    }
+    if (v->prefetch) {
+        rc |= dalloc(v, &d.sp_envs, n);
+        rc |= dalloc(v, &d.sp_ents, (size_t)PG_NF * n * PG_CAP);
+        rc |= dalloc(v, &d.sp_grid, n * PG_GRID_MAX);
+        rc |= dalloc(v, &d.sp_grid8, n * PG_GRID_MAX);
+        rc |= dalloc(v, &d.sp_mt, n * 2 * PG_MT_WORDS);
+        if (v->has_latent) rc |= dalloc(v, &d.sp_latent, n * PG_LATENT_N);
+        rc |= dalloc(v, &d.sp_level_seed, n);
+        rc |= dalloc(v, &d.sp_in, (size_t)v->lag * n);
+        rc |= dalloc(v, &d.sp_in_lsg, (size_t)v->lag * n * PG_MT_WORDS);
+        rc |= dalloc(v, &d.sp_gen, n);
+        rc |= dalloc(v, &d.sp_queue, (size_t)v->lag * PG_NUM_GAMES * n);
+        rc |= dalloc(v, &d.sp_count, (size_t)v->lag * PG_NUM_GAMES);
+        if (!rc && hipMemsetAsync(d.sp_gen, 0x80, n * 4, v->stream) != hipSuccess) rc = 1;
+        // the PGEnv words the step kernel writes back (pg_step.hip, the PG_W list) except `error`
+        const size_t offs[][2] = {
+#define PG_F(f) {offsetof(PGEnv, f), sizeof(((PGEnv *)0)->f)}
+            PG_F(action), PG_F(cur_time), PG_F(sd_reward), PG_F(sd_done), PG_F(sd_level_complete), PG_F(total_reward),
+            PG_F(last_reward_timer), PG_F(last_reward), PG_F(prev_level_seed), PG_F(episode_done), PG_F(num_ents),
+            PG_F(agent_erased), PG_F(ghost_x), PG_F(ghost_y), PG_F(ghost_vx), PG_F(ghost_vy), PG_F(ghost_rx),
+            PG_F(ghost_ry), PG_F(move_action), PG_F(special_action), PG_F(last_move_action), PG_F(action_vx),
+            PG_F(action_vy), PG_F(action_vrot), PG_F(step_rand_int), PG_F(rg_mti), PG_F(has_support),
+            PG_F(facing_right), PG_F(is_on_crate), PG_F(last_agent_y), PG_F(fish_eaten), PG_F(has_keys),
+            PG_F(diamonds_remaining), PG_F(died), PG_F(coins_collected), PG_F(eat_time), PG_F(orbs_collected),
+            PG_F(last_fire_time), PG_F(num_enemies), PG_F(gs), PG_F(num_tail)
+#undef PG_F
+        };
+        for (auto &o : offs)
+            for (size_t b = o[0]; b < o[0] + o[1]; b += 4) d.sp_mask[b / 128] |= 1u << ((b / 4) & 31);
+        bool ok = true;
+        for (int i = 0; i < v->npstreams && ok; i++)
+            ok = hipStreamCreateWithFlags(&v->pstreams[i], hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; i < v->lag && ok; i++) ok = hipEventCreateWithFlags(&v->ev_pre[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) rc = 1;
+    }
     d.reset_count = d.sched + PG_SCHED_RC;
     rc |= dalloc(v, &d.heavy, 2 * (size_t)PG_NUM_GAMES * PG_HEAVY_CAP);
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
@@ -1062,7 +1136,15 @@ LIBENV_API int procgen_start(libenv_env *env) {
     if (v->started) return 0;
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0);
+        if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream));
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag);
+        if (v->prefetch) { // the spares of the first episodes (requested at act -lag, ring slot 0, usable from act 0)
+            HIPCHECK(hipEventRecord(v->ev_reset[k], v->stream));
+            HIPCHECK(hipStreamWaitEvent(v->pstreams[0], v->ev_reset[k], 0));
+            pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->pstreams[0], 2, 0, -v->lag);
+            HIPCHECK(hipEventRecord(v->ev_pre[0], v->pstreams[0]));
+            v->ev_pre_set[0] = true;
+        }
     }
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
@@ -1141,6 +1223,13 @@ LIBENV_API void libenv_close(libenv_env *env) {
         if (e) hipEventDestroy(e);
     for (auto &s : v->rstreams)
         if (s) hipStreamDestroy(s);
+    for (auto &p : v->pstreams)
+        if (p) {
+            (void)hipStreamSynchronize(p);
+            hipStreamDestroy(p);
+        }
+    for (auto &e : v->ev_pre)
+        if (e) hipEventDestroy(e);
     if (v->fork) hipEventDestroy(v->fork);
     for (auto &s : v->gstreams)
         if (s) hipStreamDestroy(s);
@@ -1370,12 +1459,15 @@ LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, in
     return (int)(p - data);
 }
 
+static void invalidate_spare(VecEnv *v, int env_idx);
+
 LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *data, int length) {
     VecEnv *v = (VecEnv *)env;
     if (env_idx < 0 || env_idx >= v->num_envs || length < (int)(8 + sizeof(PGEnv) + 4)) {
         fail(v, PG_ERR_BAD_OPTION, "set_state: bad arguments");
         return;
     }
+    invalidate_spare(v, env_idx);
     hipStreamSynchronize(v->stream);
     const char *p = data;
     uint32_t magic, ver;
@@ -1592,7 +1684,13 @@ static int read_host_env(VecEnv *v, int env_idx, HostEnv &h) {
     return 0;
 }
 
+// An env whose state the host replaced has no valid spare (its level-seed generator may differ)
+static void invalidate_spare(VecEnv *v, int env_idx) {
+    if (v->prefetch) (void)hipMemsetAsync(v->dev.sp_gen + env_idx, 0x80, 4, v->stream);
+}
+
 static void write_host_env(VecEnv *v, int env_idx, const HostEnv &h) {
+    invalidate_spare(v, env_idx);
     std::vector<char> buf;
     buf.reserve(SNAP_CAP);
     auto put = [&](const void *d, size_t n) { buf.insert(buf.end(), (const char *)d, (const char *)d + n); };

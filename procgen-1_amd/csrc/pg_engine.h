@@ -259,7 +259,27 @@ struct PGDev {
     int32_t *heavy;             // [2][PG_NUM_GAMES][PG_HEAVY_CAP] each game's slow envs of a step
     uint8_t *heavy_flag;        // [2][num_envs] env is on its game's slow list
     int64_t heavy_ticks;        // wall-clock ticks (100 MHz) above which a step counts as slow
+    // level prefetch (single-game batches; pg_reset.hip): every env's next level is generated ahead,
+    // on a side stream, into a spare state -- the next level depends only on the level-seed
+    // generator (game.cpp:109-134) -- and swapped in when the episode ends.  Null when off.
+    PGEnv *sp_envs;             // [num_envs] the spare's scalars
+    float *sp_ents;             // PG_NF planes of num_envs * PG_CAP
+    int16_t *sp_grid;           // num_envs * PG_GRID_MAX
+    int8_t *sp_grid8;
+    uint32_t *sp_mt;            // num_envs * 2 * PG_MT_WORDS (rand_gen, level_seed_rand_gen)
+    int32_t *sp_latent;         // num_envs * PG_LATENT_N (maze, miner)
+    int32_t *sp_level_seed;     // [num_envs] (the spare reset's level_seed output)
+    PGEnv *sp_in;               // [sp_lag][num_envs] inputs of the spare resets, by act mod sp_lag
+    uint32_t *sp_in_lsg;        // [sp_lag][num_envs][PG_MT_WORDS] their level-seed generators
+    int32_t *sp_gen;            // [num_envs] act whose reset requested the env's spare (PG_SP_NONE: none)
+    int32_t *sp_queue;          // [sp_lag][PG_NUM_GAMES][num_envs] envs whose spare to generate
+    int32_t *sp_count;          // [sp_lag][PG_NUM_GAMES]
+    int32_t sp_lag;             // a spare requested at act a is swapped in from act a + sp_lag
+    uint32_t sp_mask[4];        // PGEnv words the step kernel may change: poisoned in the spare input
 };
+#define PG_SP_LAG_MAX 8
+#define PG_SP_NONE ((int32_t)0x80808080) // sp_gen of an env without a valid spare (memset 0x80)
+#define PG_SP_SENT 0x7f7fbeefu   // poison of a step-changed word the spare reset did not write
 #define PG_HEAVY_CAP 2048
 #define PG_SCHED_RC 16
 #define PG_SCHED_HC(p) ((p) ? 0 : 32)

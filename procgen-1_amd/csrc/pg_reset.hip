@@ -2682,11 +2682,96 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     wave_sync();
 }
 
-// all_envs != 0: reset every env in env_list / 0..count-1 (initial reset of set_buffers);
-// else drain this game's queue filled by the step kernel.  GEN: use_generated_assets (the AssetGen
-// scratch is allocated only in these instances).
+// ------------------------------------------------------------------ level prefetch
+// The spare's view of the device state: the arrays a reset writes, redirected to the spare
+DEV PGDev spare_view(const PGDev &d) {
+    PGDev v = d;
+    v.envs = d.sp_envs;
+    v.ents = d.sp_ents;
+    v.grid = d.sp_grid;
+    v.grid8 = d.sp_grid8;
+    v.mt = d.sp_mt;
+    v.latent = d.sp_latent;
+    v.level_seed = d.sp_level_seed;
+    return v;
+}
+DEV int sp_slot(const PGDev &d, int act) { return ((act % d.sp_lag) + d.sp_lag) % d.sp_lag; }
+DEV bool sp_masked(const PGDev &d, int w) { return (d.sp_mask[w >> 5] >> (w & 31)) & 1; }
+
+// After the reset (or swap) of `env` at act `act`: its next level's input -- the post-reset scalars
+// (in LDS) with every step-changeable word poisoned, and the level-seed generator -- is queued for
+// the prefetch kernel.  The spare then equals a reset at the end of the coming episode: that reset
+// reads only members the episode does not change (options, counters, the level-seed generator);
+// the step-changed members it does not write keep the live values at the swap.
+template <int G>
+DEV void request_spare(PGDev &d, int env, int act, const PGEnv *lds_env) {
+    const int par = sp_slot(d, act);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(lds_env);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(d.sp_in + (size_t)par * d.num_envs + env);
+    for (int w = LANE; w < (int)(sizeof(PGEnv) / 4); w += 64) dst[w] = sp_masked(d, w) ? PG_SP_SENT : src[w];
+    __threadfence(); // this wave's level-seed generator writes, before reading them back
+    const uint32_t *lsg = d.mt + (size_t)env * 2 * PG_MT_WORDS + PG_MT_WORDS;
+    uint32_t *lo = d.sp_in_lsg + ((size_t)par * d.num_envs + env) * PG_MT_WORDS;
+    for (int i = LANE; i < PG_MT_WORDS; i += 64) lo[i] = __hip_atomic_load(lsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (LANE == 0) {
+        d.sp_gen[env] = act;
+        const int q = atomicAdd(d.sp_count + par * PG_NUM_GAMES + G, 1);
+        d.sp_queue[((size_t)par * PG_NUM_GAMES + G) * d.num_envs + q] = env;
+    }
+    wave_sync();
+}
+
+// The episode of `env` ended and its spare is complete: the spare becomes the live state (what
+// reset_env would have produced), the step-changed members the reset does not write keep their
+// live values.  Leaves the new scalars in lds_env too.
+template <int G>
+DEV void swap_spare(PGDev &d, int env, PGEnv *lds_env) {
+    const uint32_t *sp = reinterpret_cast<const uint32_t *>(d.sp_envs + env);
+    const uint32_t *lv = reinterpret_cast<const uint32_t *>(d.envs + env);
+    uint32_t *out = reinterpret_cast<uint32_t *>(lds_env);
+    for (int w = LANE; w < (int)(sizeof(PGEnv) / 4); w += 64) {
+        uint32_t a = sp[w];
+        if (sp_masked(d, w) && a == PG_SP_SENT) a = lv[w];
+        out[w] = a;
+    }
+    wave_sync();
+    const size_t plane = (size_t)d.num_envs * PG_CAP, eb = (size_t)env * PG_CAP;
+    const int ne = G == PG_GAME_STARPILOT ? PG_CAP : min(max(lds_env->num_ents, 0), PG_CAP);
+    for (int f = 0; f < PG_NF; f++)
+        for (int i = LANE; i < ne; i += 64) d.ents[(size_t)f * plane + eb + i] = d.sp_ents[(size_t)f * plane + eb + i];
+    int cells = lds_env->main_width * lds_env->main_height;
+    if (cells > PG_GRID_MAX || cells < 0) cells = PG_GRID_MAX;
+    const uint4 *g16 = reinterpret_cast<const uint4 *>(d.sp_grid + (size_t)env * PG_GRID_MAX);
+    uint4 *o16 = reinterpret_cast<uint4 *>(d.grid + (size_t)env * PG_GRID_MAX);
+    for (int i = LANE; i < (cells + 7) / 8; i += 64) o16[i] = g16[i];
+    const uint4 *g8 = reinterpret_cast<const uint4 *>(d.sp_grid8 + (size_t)env * PG_GRID_MAX);
+    uint4 *o8 = reinterpret_cast<uint4 *>(d.grid8 + (size_t)env * PG_GRID_MAX);
+    for (int i = LANE; i < (cells + 15) / 16; i += 64) o8[i] = g8[i];
+    const uint32_t *m = d.sp_mt + (size_t)env * 2 * PG_MT_WORDS;
+    uint32_t *mo = d.mt + (size_t)env * 2 * PG_MT_WORDS;
+    for (int i = LANE; i < 2 * PG_MT_WORDS; i += 64) mo[i] = m[i];
+    if constexpr (G == PG_GAME_MAZE || G == PG_GAME_MINER) {
+        const int32_t *l = d.sp_latent + (size_t)env * PG_LATENT_N;
+        int32_t *lo = d.latent + (size_t)env * PG_LATENT_N;
+        for (int i = LANE; i < PG_LATENT_N; i += 64) lo[i] = l[i];
+    }
+    if (LANE == 0) {
+        d.level_seed[env] = lds_env->current_level_seed;
+        if (lds_env->error) atomicOr(d.error_any, 1 << lds_env->error);
+    }
+    wave_sync();
+    reinterpret_cast<uint2 *>(d.envs + env)[LANE] = reinterpret_cast<const uint2 *>(lds_env)[LANE];
+    wave_sync();
+}
+
+// mode 1: reset every env in env_list / 0..count-1 (initial reset of set_buffers); mode 0: drain
+// this game's queue filled by the step kernel (swapping in complete spares); mode 2: generate the
+// spares requested at act `act`.  With prefetch on (d.sp_envs), modes 0 and 1 request the next
+// spare of every env they reset; a spare requested at act a is complete once the prefetch launch
+// of act a is (the host orders the reset of act a + sp_lag after it).  GEN: use_generated_assets (the
+// AssetGen scratch is allocated only in these instances).
 template <int G, bool GEN>
-__global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int all_envs) {
+__global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int mode, int act) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ __attribute__((aligned(16))) int16_t lds_grid[PG_GRID_MAX];
     __shared__ Scratch<G> scratch;
@@ -2696,12 +2781,33 @@ __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *en
         __shared__ AgLds ag_lds;
         ag = &ag_lds;
     }
-    int n = all_envs ? count : d.reset_count[G];
-    const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
     PGDev dv = game_view(d, G);
+    if (mode == 2) {
+        const int par = sp_slot(d, act);
+        const int n = d.sp_count[par * PG_NUM_GAMES + G];
+        const int32_t *queue = d.sp_queue + ((size_t)par * PG_NUM_GAMES + G) * d.num_envs;
+        PGDev sv = spare_view(dv);
+        for (int q = blockIdx.x; q < n; q += gridDim.x) {
+            const int env = queue[q];
+            reinterpret_cast<uint2 *>(d.sp_envs + env)[LANE] =
+                reinterpret_cast<const uint2 *>(d.sp_in + (size_t)par * d.num_envs + env)[LANE];
+            const uint32_t *li = d.sp_in_lsg + ((size_t)par * d.num_envs + env) * PG_MT_WORDS;
+            uint32_t *lo = d.sp_mt + (size_t)env * 2 * PG_MT_WORDS + PG_MT_WORDS;
+            for (int i = LANE; i < PG_MT_WORDS; i += 64) lo[i] = li[i];
+            __threadfence();
+            wave_sync();
+            reset_env<G>(sv, env, lds_mt, lds_grid, &scratch, false, &lds_env, ag);
+        }
+        return;
+    }
+    const int n = mode == 1 ? count : d.reset_count[G];
+    const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
     for (int q = blockIdx.x; q < n; q += gridDim.x) {
-        int env = all_envs ? (env_list ? env_list[q] : q) : queue[q];
-        reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, all_envs != 0, &lds_env, ag);
+        const int env = mode == 1 ? (env_list ? env_list[q] : q) : queue[q];
+        const int gen = d.sp_envs ? d.sp_gen[env] : PG_SP_NONE;
+        if (mode == 0 && gen != PG_SP_NONE && gen <= act - d.sp_lag) swap_spare<G>(dv, env, &lds_env);
+        else reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, mode == 1, &lds_env, ag);
+        if (d.sp_envs) request_spare<G>(dv, env, act, &lds_env);
     }
 }
 
@@ -2733,13 +2839,13 @@ __global__ __launch_bounds__(64) void pg_assetgen_sprites_kernel(int game, uint3
 } // namespace
 
 extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
-                                int all_envs, int grid) {
+                                int mode, int grid, int act) {
     if (count <= 0) return;
     int g = grid > 0 ? grid : (count < 4096 ? count : 4096);
 #define PG_CASE(G)                                                                                              \
     case G:                                                                                                     \
-        if (d->gen_bg) hipLaunchKernelGGL((pg_reset_kernel<G, true>), dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
-        else hipLaunchKernelGGL((pg_reset_kernel<G, false>), dim3(g), dim3(64), 0, s, *d, env_list, count, all_envs); \
+        if (d->gen_bg) hipLaunchKernelGGL((pg_reset_kernel<G, true>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act); \
+        else hipLaunchKernelGGL((pg_reset_kernel<G, false>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

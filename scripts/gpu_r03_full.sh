@@ -1,5 +1,5 @@
 # Round-3 GPU call: the whole parity suite, the default bench line, per-game + mixed-16 lines.
-#   STEPS=tests,bench,games (default all); GAMES overrides the per-game list
+#   STEPS=tests,golden,bench,games (default: tests,bench,games); GAMES overrides the per-game list
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -9,6 +9,9 @@ if [[ $S == *tests* ]]; then
   timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -3 gpurun_out/pytest_gpu.log
   [[ $rc != 0 ]] && exit $rc
+fi
+if [[ $S == *golden* ]]; then
+  timeout -k 10 300 python3 -u scripts/make_state_golden.py gpurun_out/upstream_states.npz > gpurun_out/golden.log 2>&1 || { tail -5 gpurun_out/golden.log; exit 11; }
 fi
 if [[ $S == *bench* ]]; then
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --host-steps 0 > gpurun_out/bench.json 2> gpurun_out/bench.err
