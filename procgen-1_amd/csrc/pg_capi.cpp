@@ -451,6 +451,11 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     // reset counts and the slow-list length of this act's step order (PGDev::sched)
     v->parity ^= 1;
     HIPCHECK(hipMemsetAsync(v->dev.sched + PG_SCHED_CLEAR(v->parity), 0, sizeof(int32_t) * 32, v->stream));
+    if (v->prefetch && G > 1) { // this act's spare-request ring slot, cleared once for every game's chain
+        const int i = v->act_no % v->lag;
+        if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(v->stream, v->ev_pre[i], 0));
+        HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, v->stream));
+    }
     if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     for (size_t k = 0; k < G; k++) {
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
@@ -471,7 +476,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 2], r));
         PG_POISON(r);
         const int act = v->act_no;
-        if (v->prefetch) { // the spares the swaps may use (requested at act - 2) are complete
+        if (v->prefetch && G == 1) { // the spares the swaps may use (requested at act - lag) are complete
             const int i = act % v->lag; // also the ring slot of this act's requests
             if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(r, v->ev_pre[i], 0));
             HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, r));
@@ -807,12 +812,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         delete v;
         return bad("hipStreamCreate failed");
     }
-    if (gids.size() == 1) { // the reset's side stream (mixed batches keep each game's chain on one stream)
+    { // the reset's side stream (single game only: mixed batches keep each game's chain on one stream)
         bool ok = true;
         for (size_t k = 0; k < gids.size() && ok; k++) {
             hipStream_t s = nullptr;
             hipEvent_t a = nullptr, b = nullptr;
-            ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+            ok = (gids.size() > 1 || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) &&
                  hipEventCreateWithFlags(&a, hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&b, hipEventDisableTiming) == hipSuccess;
             v->rstreams.push_back(s);
@@ -888,7 +893,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.reset_queue, n * PG_NUM_GAMES);
     rc |= dalloc(v, &d.sched, 48);
     rc |= dalloc(v, &d.done8, n);
-    // level prefetch: single-game batches, random level seeds (a sequential level's seed depends on
+    // level prefetch: random level seeds (a sequential level's seed depends on
     // how the episode ends), no generated backgrounds (1 MB per env per spare).  On by default for the
     // games whose reset is on the critical path (long level generation that outlasts the render of
     // the other envs: caveflyer 24.5 -> 29.6, jumper 20.6 -> 21.7 M env-steps/s); the others lose
@@ -897,8 +902,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     {
         const char *pf = getenv("PROCGEN_MI355X_PREFETCH");
         const bool by_game = gids.size() == 1 && (gids[0] == PG_GAME_CAVEFLYER || gids[0] == PG_GAME_JUMPER);
-        v->prefetch = gids.size() == 1 && !use_generated_assets && !use_sequential_levels &&
-                      (pf ? pf[0] != '0' : by_game);
+        v->prefetch = !use_generated_assets && !use_sequential_levels && (pf ? pf[0] != '0' : by_game);
         const char *lg = getenv("PROCGEN_MI355X_PREFETCH_LAG"), *ps = getenv("PROCGEN_MI355X_PREFETCH_STREAMS");
         if (lg) v->lag = std::min(std::max(atoi(lg), 1), PG_SP_LAG_MAX);
         if (ps) v->npstreams = std::min(std::max(atoi(ps), 1), 2);
@@ -943,6 +947,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.heavy, 2 * (size_t)PG_NUM_GAMES * PG_HEAVY_CAP);
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
     d.heavy_ticks = 10000; // 100 us: ~3x the median coinrun step wave
+    {
+        const char *sp = getenv("PROCGEN_MI355X_SLOW_PREDICT");
+        d.slow_predict = sp ? atoi(sp) : 0;
+    }
     if (v->has_latent) rc |= dalloc(v, &d.latent, n * PG_LATENT_N);
     if (render_human) {
         rc |= dalloc(v, &v->hr_frames, n * 512 * 512);
@@ -1134,9 +1142,9 @@ LIBENV_API int procgen_start(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     if (v->started) return 0;
+    if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream)); // ring slot 0, every game
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream));
         pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag);
         if (v->prefetch) { // the spares of the first episodes (requested at act -lag, ring slot 0, usable from act 0)
             HIPCHECK(hipEventRecord(v->ev_reset[k], v->stream));

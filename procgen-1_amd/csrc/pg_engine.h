@@ -259,6 +259,7 @@ struct PGDev {
     int32_t *heavy;             // [2][PG_NUM_GAMES][PG_HEAVY_CAP] each game's slow envs of a step
     uint8_t *heavy_flag;        // [2][num_envs] env is on its game's slow list
     int64_t heavy_ticks;        // wall-clock ticks (100 MHz) above which a step counts as slow
+    int32_t slow_predict;       // also list envs the step predicts slow (pg_step.hip step_env; 0 = off)
     // level prefetch (single-game batches; pg_reset.hip): every env's next level is generated ahead,
     // on a side stream, into a spare state -- the next level depends only on the level-seed
     // generator (game.cpp:109-134) -- and swapped in when the episode ends.  Null when off.

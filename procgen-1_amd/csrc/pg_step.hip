@@ -2747,7 +2747,7 @@ struct StepLds {
 // Game::step (game.cpp:136-171) of one env by the calling wave, minus reset (queued) and observe
 // (pg_render)
 template <int G>
-DEV void step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t) {
+DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t) {
     uint32_t *lds_mt = L.mt;
     int16_t *lds_list = L.list, *lds_slist = L.slist;
     float4 *lds_ibox = L.ibox;
@@ -2797,6 +2797,22 @@ DEV void step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.s.sd_done = 0;
     c.s.sd_level_complete = 0;
     game_step<G>(c);
+    // slow-step predictor (launch order only, see pg_step_kernel): the agent ends the step touching
+    // two or more static interactors (coinrun's crate piles: sub_step's push recursion branches on
+    // every crate it overlaps) -- the next step is likely a slow one
+    bool predicted = false;
+    if constexpr (G == PG_GAME_COINRUN) {
+#ifndef PG_SLOW_PREDICT_MARGIN
+#define PG_SLOW_PREDICT_MARGIN 0.5f
+#endif
+        if (c.ireg && c.nlist >= 2 && !c.s.agent_erased) {
+            const float ax = EF(c, F_X, 0), ay = EF(c, F_Y, 0), arx = EF(c, F_RX, 0), ary = EF(c, F_RY, 0);
+            const bool near = LANE < c.nlist && !c.i_erase &&
+                              fabsf(ax - c.i_x) < arx + c.i_rx + PG_SLOW_PREDICT_MARGIN &&
+                              fabsf(ay - c.i_y) < ary + c.i_ry + PG_SLOW_PREDICT_MARGIN;
+            predicted = __popcll(ballot(near)) >= 2;
+        }
+    }
     c.s.sd_done = c.s.sd_done || will_force_reset || (c.s.cur_time >= c.s.timeout);
     c.s.total_reward += c.s.sd_reward;
     if (c.s.sd_reward != 0) {
@@ -2849,6 +2865,7 @@ DEV void step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.pt.mark(6);
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
     c.cs.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
+    return predicted && !done;
 }
 
 
@@ -2888,8 +2905,8 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     }
     const StepLds L{lds_mt, lds_list, lds_slist, lds_ibox, lds_pstk, lds_iinfo, lds_grid, lds_moved};
     const uint64_t t0 = wall_clock64();
-    step_env<G>(d, env, L, use_hash, hash_seed, hash_t);
-    const bool heavy = (int64_t)(wall_clock64() - t0) > d.heavy_ticks;
+    const bool predicted = step_env<G>(d, env, L, use_hash, hash_seed, hash_t);
+    const bool heavy = (int64_t)(wall_clock64() - t0) > d.heavy_ticks || (d.slow_predict && predicted);
     if (LANE == 0) {
         bool listed = false;
         if (heavy) {

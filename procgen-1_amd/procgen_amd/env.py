@@ -232,10 +232,15 @@ class BaseProcgenEnv:
         return [{k: (v[i] if v.ndim == 1 else v[i].copy()) for k, v in items} for i in range(self.num)]
 
     def get_info_arrays(self):
-        """The info tensors of the last observe() as arrays [num, ...] (no per-env dicts)."""
+        """The info tensors of the last observe() as arrays [num, ...] (no per-env dicts): the live
+        buffers under reuse_arrays (as observe() returns them), else fresh copies -- the latent
+        `grid` alone is 4.9 KB per env (declared for every game, vecgame.cpp:270-316), so large
+        batches copy it over threads like the observations."""
         if self.device_buffers:
             raise ProcgenError("device-buffer env: read device_ptrs() instead")
-        return {k: v.copy() for k, v in self._info.items()}
+        if self.reuse_arrays:
+            return self._info
+        return {k: _copy(v) for k, v in self._info.items()}
 
     def callmethod(self, method, *args, **kwargs):
         return getattr(self, method)(*args, **kwargs)

@@ -100,7 +100,7 @@ def main(game="coinrun", num=65536, warm=60):
 
 
 if __name__ == "__main__":
-    res = [main(g) for g in (sys.argv[1:] or ["coinrun"])]
+    res = [main(g, warm=int(os.environ.get("CENSUS_WARM", "60"))) for g in (sys.argv[1:] or ["coinrun"])]
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "census.json"), "w") as f:
         json.dump(res, f, indent=1)

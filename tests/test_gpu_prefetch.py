@@ -80,8 +80,9 @@ def test_prefetch_after_set_state(game, prefetch):
     assert ends > 0
 
 
-def test_prefetch_mixed_batch_stays_inline(prefetch):
-    """Mixed batches never prefetch (the flag is ignored): the mixed parity still holds with it set."""
+def test_prefetch_mixed_batch(prefetch):
+    """A mixed batch with the prefetch forced on: every game's chain requests and swaps its own spares
+    (one ring slot per act, cleared once for all games); parity per env against the oracle."""
     from oracle_lib import OracleEnv
     prefetch()
     names = ["caveflyer", "coinrun", "jumper", "maze"]
@@ -89,7 +90,7 @@ def test_prefetch_mixed_batch_stays_inline(prefetch):
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=6)
     orcs = [OracleEnv(names[n % len(names)], 1, env_offset=n, num_levels=0, rand_seed=6) for n in range(num)]
     rng = np.random.RandomState(7)
-    for t in range(1, 121):
+    for t in range(1, 241):
         act = rng.randint(0, 15, size=num).astype(np.int32)
         env.act(act)
         g = gpu_obs(env)
