@@ -225,7 +225,8 @@ def main():
     if rank == 0:
         names = ["pg_step_kernel", "pg_reset_kernel", "pg_render_kernel"]
         mixed = len(game.split(",")) > 1
-        algo_bytes = E * OBS_BYTES  # every env's 64x64x3 obs write per step
+        parts = env.num_parts()  # a single game's act split into chains over env ranges (kernel_times: per part)
+        algo_bytes = E * OBS_BYTES // parts  # every env's 64x64x3 obs write, per launch (one part's envs)
         if not mixed:
             # 12,288 algorithmic bytes per env-step (the obs write), E env-steps per
             # launch; `achieved` divides them by the DOMINANT kernel's average in-bench duration (HIP
@@ -248,18 +249,19 @@ def main():
                 roof[key] = {"ms": round(kt[i], 4), "achieved": round(a / 1e9, 2), "frac": round(a / HBM_PEAK, 5),
                              "traffic": tr, "traffic_source": src,
                              "traffic_GBps": round(tr / (kt[i] * 1e-3) / 1e9, 2) if tr and kt[i] > 0 else None}
-            e2e = algo_bytes / (ms_per_step * 1e-3)
+            roof["parts"] = parts
+            e2e = E * OBS_BYTES / (ms_per_step * 1e-3)
             roof["end_to_end"] = {"ms_per_step": round(ms_per_step, 4), "achieved": round(e2e / 1e9, 2),
                                   "frac": round(e2e / HBM_PEAK, 5)}
         else:
             # a mixed batch runs every game's step -> reset -> render chain concurrently on its own
             # stream: no single kernel's duration is attributable, so the roofline is taken over
             # the step's wall span (fork -> join on the env's stream), i.e. all 16 chains together
-            achieved = algo_bytes / (kt[3] * 1e-3) if kt[3] > 0 else 0.0
+            achieved = E * OBS_BYTES / (kt[3] * 1e-3) if kt[3] > 0 else 0.0
             roof = {"bound": "hbm", "kernel": "all games' step+reset+render chains (concurrent streams)",
                     "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK, 5), "traffic": None,
-                    "algorithmic_bytes_per_launch": algo_bytes,
+                    "algorithmic_bytes_per_launch": E * OBS_BYTES,
                     "kernel_ms": {"step_wall": round(kt[3], 4),
                                   "sum_over_games": {"step": round(kt[0], 4), "reset": round(kt[1], 4),
                                                      "render": round(kt[2], 4)},

@@ -103,8 +103,13 @@ LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int3
 LIBENV_API int procgen_last_error(libenv_env *env);
 LIBENV_API const char *procgen_error_string(libenv_env *env);
 /* Per-kernel timing of the last `n` steps measured with HIP events on the env's stream:
- * out[0] = step kernel ms, out[1] = reset kernel ms, out[2] = render kernel ms (averages). */
+ * out[0] = step kernel ms, out[1] = reset kernel ms, out[2] = render kernel ms (averages; a
+ * single game split into parts reports the mean launch over one part's envs), out[3] = the act's
+ * wall span, then 3 per game. */
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n);
+/* Chains one single-game act is split into (env option PROCGEN_MI355X_PARTS, contiguous env
+ * ranges, each step -> reset -> render chain on its own stream); 1 for mixed batches. */
+LIBENV_API int procgen_num_parts(libenv_env *env);
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled);
 /* Diagnostic builds only (libprocgen_mi355x_prof.so): per-phase cycle sums, out[16]. */
 LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out);

@@ -28,10 +28,10 @@
 
 extern "C" {
 void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int use_hash,
-                    uint64_t seed, int32_t t, int parity);
+                    uint64_t seed, int32_t t, int parity, int slot);
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode, int grid,
-                     int act);
-void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode);
+                     int act, int slot);
+void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode, int slot);
 int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames, uint8_t *rgb,
                            hipStream_t s);
 int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s);
@@ -351,6 +351,24 @@ struct VecEnv {
     // envs are disjoint), forked from and joined back into `stream` every act
     std::vector<hipStream_t> gstreams;
     std::vector<hipEvent_t> gdone;
+    // single game split into `parts` chains over contiguous env ranges (PROCGEN_MI355X_PARTS): each
+    // part's step -> reset -> render chain on its own stream (gstreams), so one part renders while
+    // another is still stepping -- a step launch ends on its slowest env (coinrun's crate-pile push
+    // chains: one env can take 400-650 us), and a lone tail wave leaves the GPU idle.  The per-chain
+    // bookkeeping (reset queue, slow-env list, spare requests) lives in PGDev slot k (a single-game
+    // batch leaves the other games' slots free); d_ident = 0..num_envs-1 supplies the part lists.
+    int parts = 1;
+    int32_t *d_ident = nullptr;
+    size_t chains() const { return games.size() > 1 ? games.size() : (size_t)parts; }
+    int chain_game(size_t k) const { return games.size() > 1 ? games[k] : games[0]; }
+    int chain_slot(size_t k) const { return games.size() > 1 ? games[k] : (int)k; }
+    int chain_lo(size_t k) const { return (int)((size_t)num_envs * k / (size_t)parts); }
+    const int32_t *chain_list(size_t k) const {
+        return games.size() > 1 ? list_of(k) : (parts > 1 ? d_ident + chain_lo(k) : nullptr);
+    }
+    int chain_count(size_t k) const {
+        return games.size() > 1 ? count_of() : (int)((size_t)num_envs * (k + 1) / (size_t)parts) - chain_lo(k);
+    }
     // per game: the stream the reset kernel runs on while the envs that did not finish render, and
     // the events ordering step -> reset -> render of the finished envs
     std::vector<hipStream_t> rstreams;
@@ -434,9 +452,10 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
 int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
-    const size_t G = v->games.size();
-    hipEvent_t *e = nullptr; // PG_EV_G per game (see procgen_kernel_times); then 2 wall
-    const size_t per = PG_EV_G * G + 2;
+    const size_t C = v->chains(); // a mixed batch's games, or a single game's parts
+    const bool split = v->games.size() == 1;
+    hipEvent_t *e = nullptr; // PG_EV_G per chain (see procgen_kernel_times); then 2 wall
+    const size_t per = PG_EV_G * C + 2;
     if (v->timing) {
         size_t need = (size_t)(v->t_used + 1) * per;
         while (v->ev.size() < need) {
@@ -447,27 +466,32 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         e = &v->ev[(size_t)v->t_used * per];
         v->t_used++;
     }
-    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * G], v->stream));
+    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * C], v->stream));
     // reset counts and the slow-list length of this act's step order (PGDev::sched)
     v->parity ^= 1;
     HIPCHECK(hipMemsetAsync(v->dev.sched + PG_SCHED_CLEAR(v->parity), 0, sizeof(int32_t) * 32, v->stream));
-    if (v->prefetch && G > 1) { // this act's spare-request ring slot, cleared once for every game's chain
-        const int i = v->act_no % v->lag;
+    const int act = v->act_no;
+    if (v->prefetch && C > 1) { // this act's spare-request ring slot, cleared once for every chain
+        const int i = act % v->lag;
         if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(v->stream, v->ev_pre[i], 0));
         HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, v->stream));
     }
-    if (G > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
-    for (size_t k = 0; k < G; k++) {
+    if (C > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
+    for (size_t k = 0; k < C; k++) {
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
         // a side stream while the envs that did not finish render; a mixed batch keeps each game's
         // step -> reset -> render chain on its stream (its 16 chains already overlap, and twice as
         // many streams over the GPU_MAX_HW_QUEUES queues measured slower: 14.5 vs 17.4 M env-steps/s)
-        const bool split = G == 1;
-        hipStream_t s = G > 1 ? v->gstreams[k] : v->stream, r = split ? v->rstreams[k] : s;
-        if (G > 1) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
+        const int game = v->chain_game(k), slot = v->chain_slot(k), cnt = v->chain_count(k);
+        const int32_t *list = v->chain_list(k);
+        // chain 0 runs on the engine stream itself: every extra stream shares one of the
+        // GPU_MAX_HW_QUEUES (4) hardware queues, and a chain whose queue also carries the join's
+        // waits is serialized behind them
+        hipStream_t s = C > 1 && k > 0 ? v->gstreams[k] : v->stream, r = split ? v->rstreams[k] : s;
+        if (C > 1 && k > 0) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
-        pg_launch_step(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, use_hash, seed, t, v->parity);
+        pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 1], s));
         if (split) {
             HIPCHECK(hipEventRecord(v->ev_stepped[k], s));
@@ -475,42 +499,41 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 2], r));
         PG_POISON(r);
-        const int act = v->act_no;
-        if (v->prefetch && G == 1) { // the spares the swaps may use (requested at act - lag) are complete
+        if (v->prefetch && C == 1) { // the spares the swaps may use (requested at act - lag) are complete
             const int i = act % v->lag; // also the ring slot of this act's requests
             if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(r, v->ev_pre[i], 0));
             HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, r));
         }
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), r, 0, 0, act);
+        pg_launch_reset(&v->dev, game, list, cnt, r, 0, 0, act, slot);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 3], r));
         if (v->prefetch) { // the next levels of the envs just reset, off the critical path
             hipStream_t p = v->pstreams[act % v->npstreams];
             HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
             HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
-            pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), p, 2, 0, act);
+            pg_launch_reset(&v->dev, game, list, cnt, p, 2, 0, act, slot);
             HIPCHECK(hipEventRecord(v->ev_pre[act % v->lag], p));
             v->ev_pre_set[act % v->lag] = true;
         }
         PG_POISON(s);
         if (split) {
             HIPCHECK(hipEventRecord(v->ev_reset[k], r));
-            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 1);
+            pg_launch_render(&v->dev, game, list, cnt, s, 1, slot);
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s));
             HIPCHECK(hipStreamWaitEvent(s, v->ev_reset[k], 0));
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
-            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 2);
+            pg_launch_render(&v->dev, game, list, cnt, s, 2, slot);
         } else {
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s)); // unused without the split
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
-            pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), s, 0);
+            pg_launch_render(&v->dev, game, list, cnt, s, 0, slot);
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
-        if (G > 1) {
-            HIPCHECK(hipEventRecord(v->gdone[k], s));
-            HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
-        }
     }
-    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * G + 1], v->stream));
+    for (size_t k = 1; k < C; k++) { // join, after every chain is enqueued (chain 0 is on the engine stream)
+        HIPCHECK(hipEventRecord(v->gdone[k], v->gstreams[k]));
+        HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
+    }
+    if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * C + 1], v->stream));
     v->act_no++;
     HIPCHECK(hipGetLastError());
     return 0;
@@ -812,9 +835,21 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         delete v;
         return bad("hipStreamCreate failed");
     }
+    {
+        // default: coinrun alone in two parts, part 1 at high priority (its step launches end on single
+        // crate-pile envs of 400-650 us; the other part's render fills that tail: 29.7 -> 33.6 M
+        // env-steps/s).  Measured neutral for bigfish, maze, heist, starpilot, fruitbot, miner and
+        // dodgeball, and a loss where the level prefetch adds a fifth stream over the 4 hardware
+        // queues (caveflyer -13 %, jumper -23 %): profiles/r03/o_parts_games.
+        const char *pp = getenv("PROCGEN_MI355X_PARTS"), *pf = getenv("PROCGEN_MI355X_PREFETCH");
+        const bool dflt = gids.size() == 1 && gids[0] == PG_GAME_COINRUN && !(pf && pf[0] == '1');
+        const int want = pp ? std::min(std::max(atoi(pp), 1), 8) : (dflt ? 2 : 1);
+        v->parts = gids.size() == 1 && num_envs >= want * 64 ? want : 1;
+    }
+    const size_t nchains = gids.size() > 1 ? gids.size() : (size_t)v->parts;
     { // the reset's side stream (single game only: mixed batches keep each game's chain on one stream)
         bool ok = true;
-        for (size_t k = 0; k < gids.size() && ok; k++) {
+        for (size_t k = 0; k < nchains && ok; k++) {
             hipStream_t s = nullptr;
             hipEvent_t a = nullptr, b = nullptr;
             ok = (gids.size() > 1 || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) &&
@@ -829,12 +864,19 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             return bad("hipStreamCreate failed");
         }
     }
-    if (gids.size() > 1) {
+    if (nchains > 1) {
         bool ok = hipEventCreateWithFlags(&v->fork, hipEventDisableTiming) == hipSuccess;
-        for (size_t k = 0; k < gids.size() && ok; k++) {
+        // parts: part 1's stream gets the highest priority and the later parts' the lowest (part 0 runs
+        // on the engine stream); PROCGEN_MI355X_PART_PRIO=0 leaves them all at the default
+        const char *pr = getenv("PROCGEN_MI355X_PART_PRIO");
+        int lo_prio = 0, hi_prio = 0;
+        const bool prio = v->parts > 1 && !(pr && pr[0] == '0') && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+        for (size_t k = 0; k < nchains && ok; k++) {
             hipStream_t s = nullptr;
             hipEvent_t d = nullptr;
-            ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+            ok = (k == 0 || // chain 0 runs on the engine stream (launch_step)
+                  (prio ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, k == 1 ? hi_prio : lo_prio)
+                        : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) == hipSuccess) &&
                  hipEventCreateWithFlags(&d, hipEventDisableTiming) == hipSuccess;
             v->gstreams.push_back(s);
             v->gdone.push_back(d);
@@ -957,6 +999,14 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         rc |= dalloc(v, &v->hr_rgb, n * 512 * 512 * 3);
     }
     if (gids.size() > 1) rc |= dalloc(v, &v->d_lists, n);
+    if (v->parts > 1) {
+        rc |= dalloc(v, &v->d_ident, n);
+        if (!rc) {
+            std::vector<int32_t> id(n);
+            for (size_t e = 0; e < n; e++) id[e] = (int32_t)e;
+            if (copy_sync(v, v->d_ident, id.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) rc = 1;
+        }
+    }
     float *d_rot_angles = nullptr;
     double *d_rot_table = nullptr;
     rc |= dalloc(v, &d_rot_angles, PG_ROT_N);
@@ -1145,18 +1195,18 @@ LIBENV_API int procgen_start(libenv_env *env) {
     if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream)); // ring slot 0, every game
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag);
+        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag, v->games[k]);
         if (v->prefetch) { // the spares of the first episodes (requested at act -lag, ring slot 0, usable from act 0)
             HIPCHECK(hipEventRecord(v->ev_reset[k], v->stream));
             HIPCHECK(hipStreamWaitEvent(v->pstreams[0], v->ev_reset[k], 0));
-            pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->pstreams[0], 2, 0, -v->lag);
+            pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->pstreams[0], 2, 0, -v->lag, v->games[k]);
             HIPCHECK(hipEventRecord(v->ev_pre[0], v->pstreams[0]));
             v->ev_pre_set[0] = true;
         }
     }
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, v->games[k]);
     }
     HIPCHECK(hipGetLastError());
     v->started = true;
@@ -1333,31 +1383,38 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
 //   out[4 + 3g .. 6 + 3g] step / reset / render of game slot g (v->games order).
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
-    const size_t G = v->games.size(), per = PG_EV_G * G + 2;
+    // per chain (a mixed batch's games, or a single game's parts: averaged over the parts, i.e. the
+    // mean duration of one launch over one part's envs)
+    const size_t G = v->games.size(), C = v->chains(), per = PG_EV_G * C + 2;
+    const double wpart = G == 1 ? 1.0 / (double)C : 1.0;
     std::vector<double> sum(4 + 3 * G, 0.0);
     if (v->t_used > 0) {
         HIPCHECK(hipStreamSynchronize(v->stream));
         for (int k = 0; k < v->t_used; k++) {
             hipEvent_t *base = &v->ev[(size_t)k * per];
-            for (size_t g = 0; g < G; g++) {
-                hipEvent_t *e = base + PG_EV_G * g;
+            for (size_t ch = 0; ch < C; ch++) {
+                const size_t g = G > 1 ? ch : 0;
+                hipEvent_t *e = base + PG_EV_G * ch;
                 float a = 0, b = 0, c1 = 0, c2 = 0;
                 HIPCHECK(hipEventElapsedTime(&a, e[0], e[1]));  // step
                 HIPCHECK(hipEventElapsedTime(&b, e[2], e[3]));  // reset (side stream)
                 if (G == 1) HIPCHECK(hipEventElapsedTime(&c1, e[1], e[4])); // render of the unfinished envs
                 HIPCHECK(hipEventElapsedTime(&c2, e[5], e[6])); // render of the finished envs
-                const float c = c1 + c2;
-                sum[0] += a; sum[1] += b; sum[2] += c;
-                sum[4 + 3 * g] += a; sum[5 + 3 * g] += b; sum[6 + 3 * g] += c;
+                const double c = (double)(c1 + c2) * wpart;
+                sum[0] += a * wpart; sum[1] += b * wpart; sum[2] += c;
+                sum[4 + 3 * g] += a * wpart; sum[5 + 3 * g] += b * wpart; sum[6 + 3 * g] += c;
             }
             float w = 0;
-            HIPCHECK(hipEventElapsedTime(&w, base[PG_EV_G * G], base[PG_EV_G * G + 1]));
+            HIPCHECK(hipEventElapsedTime(&w, base[PG_EV_G * C], base[PG_EV_G * C + 1]));
             sum[3] += w;
         }
     }
     for (int i = 0; i < n && i < (int)sum.size(); i++) out[i] = v->t_used ? (float)(sum[i] / v->t_used) : 0.f;
     return v->t_used;
 }
+
+// Chains a single-game act is split into (PROCGEN_MI355X_PARTS; 1 for mixed batches).
+LIBENV_API int procgen_num_parts(libenv_env *env) { return ((VecEnv *)env)->parts; }
 
 // Diagnostic builds (make PROFILE=1): per-phase s_memtime cycle sums over all envs since
 // creation; out[0..7] step-kernel phases, out[8..15] render-kernel phases.
@@ -1563,7 +1620,7 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
     for (size_t k = 0; k < v->games.size(); k++)
-        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0);
+        pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, v->games[k]);
     hipStreamSynchronize(v->stream);
 }
 

@@ -1389,7 +1389,7 @@ DEV constexpr int rot_cap() {
 }
 
 template <int G>
-__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode) {
+__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode, int slot) {
     const PGDev d = game_view(dg, G);
     constexpr int HR = frame_rows<G>();
     __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES]; // the rows of one pass
@@ -1419,8 +1419,8 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     // the reset kernel regenerates the others); 2: this step's reset queue (after the reset)
     int env;
     if (mode == 2) {
-        if ((int)blockIdx.x >= d.reset_count[G]) return;
-        env = d.reset_queue[(size_t)G * d.num_envs + blockIdx.x];
+        if ((int)blockIdx.x >= d.reset_count[slot]) return;
+        env = d.reset_queue[(size_t)slot * d.num_envs + blockIdx.x];
     } else {
         env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
         if (mode == 1 && d.done8[env]) return;
@@ -2447,11 +2447,12 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
 }
 
 // mode: see pg_render_kernel (0 all, 1 envs not done, 2 the reset queue: `count` bounds its length)
-extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode) {
+extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode,
+                                 int slot) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                              \
     case G:                                                                                     \
-        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, mode); \
+        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, mode, slot); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

@@ -2704,7 +2704,7 @@ DEV bool sp_masked(const PGDev &d, int w) { return (d.sp_mask[w >> 5] >> (w & 31
 // reads only members the episode does not change (options, counters, the level-seed generator);
 // the step-changed members it does not write keep the live values at the swap.
 template <int G>
-DEV void request_spare(PGDev &d, int env, int act, const PGEnv *lds_env) {
+DEV void request_spare(PGDev &d, int env, int act, const PGEnv *lds_env, int slot) {
     const int par = sp_slot(d, act);
     const uint32_t *src = reinterpret_cast<const uint32_t *>(lds_env);
     uint32_t *dst = reinterpret_cast<uint32_t *>(d.sp_in + (size_t)par * d.num_envs + env);
@@ -2715,8 +2715,8 @@ DEV void request_spare(PGDev &d, int env, int act, const PGEnv *lds_env) {
     for (int i = LANE; i < PG_MT_WORDS; i += 64) lo[i] = __hip_atomic_load(lsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (LANE == 0) {
         d.sp_gen[env] = act;
-        const int q = atomicAdd(d.sp_count + par * PG_NUM_GAMES + G, 1);
-        d.sp_queue[((size_t)par * PG_NUM_GAMES + G) * d.num_envs + q] = env;
+        const int q = atomicAdd(d.sp_count + par * PG_NUM_GAMES + slot, 1);
+        d.sp_queue[((size_t)par * PG_NUM_GAMES + slot) * d.num_envs + q] = env;
     }
     wave_sync();
 }
@@ -2771,7 +2771,7 @@ DEV void swap_spare(PGDev &d, int env, PGEnv *lds_env) {
 // of act a is (the host orders the reset of act a + sp_lag after it).  GEN: use_generated_assets (the
 // AssetGen scratch is allocated only in these instances).
 template <int G, bool GEN>
-__global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int mode, int act) {
+__global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *env_list, int count, int mode, int act, int slot) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ __attribute__((aligned(16))) int16_t lds_grid[PG_GRID_MAX];
     __shared__ Scratch<G> scratch;
@@ -2784,8 +2784,8 @@ __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *en
     PGDev dv = game_view(d, G);
     if (mode == 2) {
         const int par = sp_slot(d, act);
-        const int n = d.sp_count[par * PG_NUM_GAMES + G];
-        const int32_t *queue = d.sp_queue + ((size_t)par * PG_NUM_GAMES + G) * d.num_envs;
+        const int n = d.sp_count[par * PG_NUM_GAMES + slot];
+        const int32_t *queue = d.sp_queue + ((size_t)par * PG_NUM_GAMES + slot) * d.num_envs;
         PGDev sv = spare_view(dv);
         for (int q = blockIdx.x; q < n; q += gridDim.x) {
             const int env = queue[q];
@@ -2800,14 +2800,14 @@ __global__ __launch_bounds__(64) void pg_reset_kernel(PGDev d, const int32_t *en
         }
         return;
     }
-    const int n = mode == 1 ? count : d.reset_count[G];
-    const int32_t *queue = d.reset_queue + (size_t)G * d.num_envs;
+    const int n = mode == 1 ? count : d.reset_count[slot];
+    const int32_t *queue = d.reset_queue + (size_t)slot * d.num_envs;
     for (int q = blockIdx.x; q < n; q += gridDim.x) {
         const int env = mode == 1 ? (env_list ? env_list[q] : q) : queue[q];
         const int gen = d.sp_envs ? d.sp_gen[env] : PG_SP_NONE;
         if (mode == 0 && gen != PG_SP_NONE && gen <= act - d.sp_lag) swap_spare<G>(dv, env, &lds_env);
         else reset_env<G>(dv, env, lds_mt, lds_grid, &scratch, mode == 1, &lds_env, ag);
-        if (d.sp_envs) request_spare<G>(dv, env, act, &lds_env);
+        if (d.sp_envs) request_spare<G>(dv, env, act, &lds_env, slot);
     }
 }
 
@@ -2839,13 +2839,13 @@ __global__ __launch_bounds__(64) void pg_assetgen_sprites_kernel(int game, uint3
 } // namespace
 
 extern "C" void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
-                                int mode, int grid, int act) {
+                                int mode, int grid, int act, int slot) {
     if (count <= 0) return;
     int g = grid > 0 ? grid : (count < 4096 ? count : 4096);
 #define PG_CASE(G)                                                                                              \
     case G:                                                                                                     \
-        if (d->gen_bg) hipLaunchKernelGGL((pg_reset_kernel<G, true>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act); \
-        else hipLaunchKernelGGL((pg_reset_kernel<G, false>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act); \
+        if (d->gen_bg) hipLaunchKernelGGL((pg_reset_kernel<G, true>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act, slot); \
+        else hipLaunchKernelGGL((pg_reset_kernel<G, false>), dim3(g), dim3(64), 0, s, *d, env_list, count, mode, act, slot); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

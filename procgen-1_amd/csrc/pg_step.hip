@@ -2747,7 +2747,8 @@ struct StepLds {
 // Game::step (game.cpp:136-171) of one env by the calling wave, minus reset (queued) and observe
 // (pg_render)
 template <int G>
-DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t) {
+DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t,
+                  int slot) {
     uint32_t *lds_mt = L.mt;
     int16_t *lds_list = L.list, *lds_slist = L.slist;
     float4 *lds_ibox = L.ibox;
@@ -2827,8 +2828,8 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
 
     if (LANE == 0) {
         if (done) {
-            int q = atomicAdd(d.reset_count + G, 1);
-            d.reset_queue[(size_t)G * d.num_envs + q] = c.env;
+            int q = atomicAdd(d.reset_count + slot, 1);
+            d.reset_queue[(size_t)slot * d.num_envs + q] = c.env;
         }
         d.done8[c.env] = (uint8_t)done;
         d.rew[c.env] = c.s.sd_reward;
@@ -2881,7 +2882,8 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
 // step's are written.  env_list: the envs of this game (mixed batches), or null = envs 0..n-1.
 template <int G>
 __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const int32_t *env_list, int n, int parity,
-                                                                int use_hash, uint64_t hash_seed, int32_t hash_t) {
+                                                                int use_hash, uint64_t hash_seed, int32_t hash_t,
+                                                                int slot) {
     __shared__ uint32_t lds_mt[PG_MT_N];
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
@@ -2893,10 +2895,10 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];
     const int prev = parity ^ 1, b = (int)blockIdx.x;
-    const int nh = min(d.sched[PG_SCHED_HC(prev) + G], PG_HEAVY_CAP);
+    const int nh = min(d.sched[PG_SCHED_HC(prev) + slot], PG_HEAVY_CAP);
     int env;
     if (b < nh) {
-        env = d.heavy[((size_t)prev * PG_NUM_GAMES + G) * PG_HEAVY_CAP + b];
+        env = d.heavy[((size_t)prev * PG_NUM_GAMES + slot) * PG_HEAVY_CAP + b];
     } else {
         const int p = b - nh;
         if (p >= n) return;
@@ -2905,14 +2907,14 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     }
     const StepLds L{lds_mt, lds_list, lds_slist, lds_ibox, lds_pstk, lds_iinfo, lds_grid, lds_moved};
     const uint64_t t0 = wall_clock64();
-    const bool predicted = step_env<G>(d, env, L, use_hash, hash_seed, hash_t);
+    const bool predicted = step_env<G>(d, env, L, use_hash, hash_seed, hash_t, slot);
     const bool heavy = (int64_t)(wall_clock64() - t0) > d.heavy_ticks || (d.slow_predict && predicted);
     if (LANE == 0) {
         bool listed = false;
         if (heavy) {
-            const int q = atomicAdd(d.sched + PG_SCHED_HC(parity) + G, 1);
+            const int q = atomicAdd(d.sched + PG_SCHED_HC(parity) + slot, 1);
             listed = q < PG_HEAVY_CAP;
-            if (listed) d.heavy[((size_t)parity * PG_NUM_GAMES + G) * PG_HEAVY_CAP + q] = env;
+            if (listed) d.heavy[((size_t)parity * PG_NUM_GAMES + slot) * PG_HEAVY_CAP + q] = env;
         }
         d.heavy_flag[(size_t)parity * d.num_envs + env] = listed ? 1 : 0;
     }
@@ -2922,13 +2924,13 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
 
 // parity: alternates per act (the host zeroes this parity's slow-list length and the reset counts)
 extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
-                               int use_hash, uint64_t seed, int32_t t, int parity) {
+                               int use_hash, uint64_t seed, int32_t t, int parity, int slot) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                                   \
     case G:                                                                                          \
         hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count + (count < PG_HEAVY_CAP ? count : PG_HEAVY_CAP)), dim3(64), 0, \
                            s, *d, env_list, count, parity, use_hash,                                 \
-                           seed, t);                                                                 \
+                           seed, t, slot);                                                                 \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

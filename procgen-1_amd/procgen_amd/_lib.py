@@ -85,6 +85,7 @@ SIGNATURES = {
     "procgen_error_string": (ctypes.c_char_p, [ctypes.c_void_p]),
     "procgen_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "procgen_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "procgen_num_parts": (ctypes.c_int, [ctypes.c_void_p]),
     "procgen_debug_env": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "procgen_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_profile_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

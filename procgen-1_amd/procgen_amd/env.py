@@ -324,6 +324,10 @@ class BaseProcgenEnv:
         per_game = {nm: vals[4 + 3 * g:7 + 3 * g] for g, nm in enumerate(names)}
         return n, vals[:4], per_game
 
+    def num_parts(self):
+        """Chains one act of this (single-game) env is split into (PROCGEN_MI355X_PARTS)."""
+        return int(self._lib.procgen_num_parts(self._handle))
+
     def debug_env(self, i):
         buf = np.zeros(128, dtype=np.int32)
         self._lib.procgen_debug_env(self._handle, i, buf.ctypes.data, buf.nbytes)
