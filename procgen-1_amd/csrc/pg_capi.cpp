@@ -12,6 +12,7 @@
 #include <cstddef>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -359,6 +360,9 @@ struct VecEnv {
     // batch leaves the other games' slots free); d_ident = 0..num_envs-1 supplies the part lists.
     int parts = 1;
     int32_t *d_ident = nullptr;
+    // chain k's stream: 0 = the engine stream, j > 0 = gstreams[j]; identity unless a mixed batch packs
+    // its chains onto PROCGEN_MI355X_MIXED_STREAMS streams (longest-first onto the least loaded)
+    std::vector<int> chain_stream;
     size_t chains() const { return games.size() > 1 ? games.size() : (size_t)parts; }
     int chain_game(size_t k) const { return games.size() > 1 ? games[k] : games[0]; }
     int chain_slot(size_t k) const { return games.size() > 1 ? games[k] : (int)k; }
@@ -487,8 +491,11 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         // chain 0 runs on the engine stream itself: every extra stream shares one of the
         // GPU_MAX_HW_QUEUES (4) hardware queues, and a chain whose queue also carries the join's
         // waits is serialized behind them
-        hipStream_t s = C > 1 && k > 0 ? v->gstreams[k] : v->stream, r = split ? v->rstreams[k] : s;
-        if (C > 1 && k > 0) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
+        const int si = C > 1 ? v->chain_stream[k] : 0;
+        hipStream_t s = si > 0 ? v->gstreams[si] : v->stream, r = split ? v->rstreams[k] : s;
+        bool first_on_stream = si > 0;
+        for (size_t j = 0; j < k && first_on_stream; j++) first_on_stream = v->chain_stream[j] != si;
+        if (first_on_stream) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
         pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
@@ -529,9 +536,12 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
     }
-    for (size_t k = 1; k < C; k++) { // join, after every chain is enqueued (chain 0 is on the engine stream)
-        HIPCHECK(hipEventRecord(v->gdone[k], v->gstreams[k]));
-        HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[k], 0));
+    for (size_t j = 1; j < v->gstreams.size() && C > 1; j++) { // join, after every chain is enqueued
+        bool used = false;
+        for (size_t k = 0; k < C && !used; k++) used = v->chain_stream[k] == (int)j;
+        if (!used) continue;
+        HIPCHECK(hipEventRecord(v->gdone[j], v->gstreams[j]));
+        HIPCHECK(hipStreamWaitEvent(v->stream, v->gdone[j], 0));
     }
     if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * C + 1], v->stream));
     v->act_no++;
@@ -884,6 +894,28 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (!ok) {
             libenv_close((libenv_env *)v);
             return bad("hipStreamCreate failed");
+        }
+    }
+    v->chain_stream.resize(nchains);
+    for (size_t k = 0; k < nchains; k++) v->chain_stream[k] = (int)k;
+    if (gids.size() > 1) {
+        const char *ms = getenv("PROCGEN_MI355X_MIXED_STREAMS");
+        const int ns = ms ? std::min(std::max(atoi(ms), 1), (int)nchains) : (int)nchains;
+        if (ns < (int)nchains) {
+            // per-game chain cost, ms at 4,096 envs (profiles/r03 mixed16 per_game step + reset + render)
+            static const float cost[PG_NUM_GAMES] = {0.27f, 0.70f, 0.97f, 0.46f, 0.43f, 0.72f, 0.73f, 0.94f,
+                                                     0.34f, 1.43f, 0.92f, 0.47f, 0.74f, 0.43f, 0.24f, 0.57f};
+            std::vector<size_t> order(nchains);
+            for (size_t k = 0; k < nchains; k++) order[k] = k;
+            std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[gids[a]] > cost[gids[b]]; });
+            std::vector<float> load(ns, 0.f);
+            for (size_t k : order) {
+                int best = 0;
+                for (int j = 1; j < ns; j++)
+                    if (load[j] < load[best]) best = j;
+                load[best] += cost[gids[k]];
+                v->chain_stream[k] = best;
+            }
         }
     }
     (void)hipGetDevice(&v->device);
@@ -1265,7 +1297,15 @@ LIBENV_API void libenv_observe(libenv_env *env) {
 LIBENV_API void libenv_close(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
     if (!v) return;
-    if (v->stream) hipStreamSynchronize(v->stream);
+    // every stream that may still run a kernel on the allocations (the level prefetch's side stream
+    // is joined to the engine stream only lag acts later) drains before anything is freed
+    for (auto &p : v->pstreams)
+        if (p) (void)hipStreamSynchronize(p);
+    for (auto &s : v->rstreams)
+        if (s) (void)hipStreamSynchronize(s);
+    for (auto &s : v->gstreams)
+        if (s) (void)hipStreamSynchronize(s);
+    if (v->stream) (void)hipStreamSynchronize(v->stream);
     unregister_buffers(v);
     for (void *p : v->allocs) hipFree(p);
     if (v->pinned) (void)hipHostFree(v->pinned);

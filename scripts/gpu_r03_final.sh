@@ -15,3 +15,5 @@ python3 -c "import json; d=json.load(open('gpurun_out/bench_default.json')); pri
 M="bigfish,bossfight,caveflyer,chaser,climber,coinrun,dodgeball,fruitbot,heist,jumper,leaper,maze,miner,ninja,plunder,starpilot"
 timeout -k 10 200 python3 bench.py --env-name $M --steps 100 --warmup 20 --settle 100 --host-steps 0 --no-cpu-baseline > gpurun_out/mixed16.json 2> gpurun_out/mixed16.err || { tail -5 gpurun_out/mixed16.err; exit 13; }
 python3 -c "import json; d=json.load(open('gpurun_out/mixed16.json')); print('mixed16', round(d['value']/1e6,2))"
+PROCGEN_MI355X_MIXED_STREAMS=4 timeout -k 10 200 python3 bench.py --env-name $M --steps 100 --warmup 20 --settle 100 --host-steps 0 --no-cpu-baseline > gpurun_out/mixed16_ms4.json 2> gpurun_out/mixed16_ms4.err || { tail -5 gpurun_out/mixed16_ms4.err; exit 14; }
+python3 -c "import json; d=json.load(open('gpurun_out/mixed16_ms4.json')); print('mixed16 4 streams', round(d['value']/1e6,2))"
