@@ -360,8 +360,8 @@ struct VecEnv {
     // batch leaves the other games' slots free); d_ident = 0..num_envs-1 supplies the part lists.
     int parts = 1;
     int32_t *d_ident = nullptr;
-    // chain k's stream: 0 = the engine stream, j > 0 = gstreams[j]; identity unless a mixed batch packs
-    // its chains onto PROCGEN_MI355X_MIXED_STREAMS streams (longest-first onto the least loaded)
+    // chain k's stream: 0 = the engine stream, j > 0 = gstreams[j]; a mixed batch packs its chains onto
+    // PROCGEN_MI355X_MIXED_STREAMS (default 4) streams, longest first onto the least loaded
     std::vector<int> chain_stream;
     size_t chains() const { return games.size() > 1 ? games.size() : (size_t)parts; }
     int chain_game(size_t k) const { return games.size() > 1 ? games[k] : games[0]; }
@@ -899,8 +899,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     v->chain_stream.resize(nchains);
     for (size_t k = 0; k < nchains; k++) v->chain_stream[k] = (int)k;
     if (gids.size() > 1) {
+        // default: as many streams as GPU_MAX_HW_QUEUES (4), chains packed longest-first (all-16 mixed
+        // shard 16.5 -> 18.7 M env-steps/s, profiles/r03/r03_q_mixed16*.json); 16 = one per game
         const char *ms = getenv("PROCGEN_MI355X_MIXED_STREAMS");
-        const int ns = ms ? std::min(std::max(atoi(ms), 1), (int)nchains) : (int)nchains;
+        const int ns = std::min(std::max(ms ? atoi(ms) : 4, 1), (int)nchains);
         if (ns < (int)nchains) {
             // per-game chain cost, ms at 4,096 envs (profiles/r03 mixed16 per_game step + reset + render)
             static const float cost[PG_NUM_GAMES] = {0.27f, 0.70f, 0.97f, 0.46f, 0.43f, 0.72f, 0.73f, 0.94f,
