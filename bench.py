@@ -181,7 +181,8 @@ def main():
         from procgen_amd.gather import ObsGather
         dp = env.device_ptrs()
         gather = ObsGather(E, world=world, dist=dist, engine_stream=torch.cuda.ExternalStream(dp.stream),
-                           bind=lambda buf: env.set_obs_buffer(None if buf is None else buf.data_ptr()))
+                           bind=lambda buf: env.set_obs_buffer(None if buf is None else buf.data_ptr()),
+                           alive=env.is_open)
 
     def step(t):
         if gather is not None:

@@ -411,8 +411,9 @@ clipped:
     return true;
 }
 // drawLine<drawPixel, NoDasher>, both branches (vert: major axis y): a reversal caps the new
-// segment's path-start end only when it is drawn swapped; the same-direction dropout test reads
-// |dx| <= 1 && |dy| > 1 in both branches (oracle cs_run)
+// segment's path-start end (CapEnd swapped, CapBegin otherwise, a CapBegin that rounds one pixel
+// before lastPixel rounded back); the same-direction dropout test reads |dx| <= 1 && |dy| > 1 in
+// both branches (oracle cs_run)
 template <class P>
 DEV void ag_cs_run(P &p, AgStroker &s, bool vert, int a1, int b1, int a2, int b2, int caps) {
     int dir = vert ? AG_T2B : AG_L2R;
@@ -426,11 +427,12 @@ DEV void ag_cs_run(P &p, AgStroker &s, bool vert, int a1, int b1, int a2, int b2
     }
     const int binc = ag_fdiv(b2 - b1, a2 - a1);
     int b = b1 * 1024;
-    if ((s.lastDir ^ (vert ? AG_VMASK : AG_HMASK)) == dir && swapped) caps |= AG_CAPEND;
+    if ((s.lastDir ^ (vert ? AG_VMASK : AG_HMASK)) == dir) caps |= swapped ? AG_CAPEND : AG_CAPBEGIN;
     ag_cap_adjust(caps, a1, a2, b, binc);
     const int round = (binc > 0) ? 32 : 0;
     int a = (a1 + 32) >> 6;
     int as = (a2 + 32) >> 6;
+    if ((caps & AG_CAPBEGIN) && (vert ? s.lasty : s.lastx) == a + 1) a++; // CapBegin rounded back
     int lx = s.lastx, ly = s.lasty;
     if (a != as) {
         b += ((a * 64) + round - a1) * binc >> 6;

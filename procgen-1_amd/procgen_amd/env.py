@@ -301,7 +301,10 @@ class BaseProcgenEnv:
 
     def set_obs_buffer(self, ptr):
         """Render later steps into the device buffer at `ptr` (uint8 [num,64,64,3]); None = own tensor.
-        The engine keeps the raw pointer: unbind (None) before the buffer is freed."""
+        The engine keeps the raw pointer: unbind (None) before the buffer is freed.  A no-op once the
+        env is closed (nothing holds the pointer any more)."""
+        if not getattr(self, "_handle", None):
+            return
         rc = self._lib.procgen_set_obs_buffer(self._handle, ptr)
         _check(self._lib, self._handle, rc)
 
@@ -332,6 +335,9 @@ class BaseProcgenEnv:
         buf = np.zeros(128, dtype=np.int32)
         self._lib.procgen_debug_env(self._handle, i, buf.ctypes.data, buf.nbytes)
         return buf
+
+    def is_open(self):
+        return bool(getattr(self, "_handle", None))
 
     def close(self):
         if getattr(self, "_handle", None):

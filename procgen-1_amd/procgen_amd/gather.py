@@ -39,7 +39,7 @@ class ObsGather:
     two later is issued, or until ``release(k)`` when the consumer needs longer)."""
 
     def __init__(self, num_envs, world=1, dist=None, device="cuda", engine_stream=None, bind=None,
-                 obs_shape=(64, 64, 3)):
+                 obs_shape=(64, 64, 3), alive=None):
         self.world = world
         self.dist = dist
         self.device = torch.device(device)
@@ -49,6 +49,9 @@ class ObsGather:
         self.out = [torch.empty((world * num_envs,) + tuple(obs_shape), dtype=torch.uint8, device=self.device)
                     for _ in range(2)]
         self.bind = bind  # bind(tensor): the engine renders the following steps into `tensor`
+        # alive(): False once the engine was closed (its streams are gone and it holds no pointer into
+        # the local buffers any more), so close() must neither wait on its stream nor unbind
+        self.alive = alive
         if self.cuda:
             self.engine = engine_stream
             self.comm = torch.cuda.Stream(device=self.device)
@@ -112,6 +115,9 @@ class ObsGather:
         """Unbind: the engine renders into its own tensor again, after every gather has read the
         local buffers, which may then be freed (the engine keeps a raw pointer while bound)."""
         if self.bind is None:
+            return
+        if self.alive is not None and not self.alive():
+            self.bind = None
             return
         self.sync_engine()
         if self.cuda:

@@ -79,7 +79,8 @@ def test_double_buffered_gather_on_device():
     env = ProcgenGym3Env(num=num, env_name=",".join(names), num_levels=0, rand_seed=5, device_buffers=True)
     dp = env.device_ptrs()
     g = ObsGather(num, engine_stream=torch.cuda.ExternalStream(dp.stream),
-                  bind=lambda t: env.set_obs_buffer(None if t is None else t.data_ptr()))
+                  bind=lambda t: env.set_obs_buffer(None if t is None else t.data_ptr()),
+                  alive=env.is_open)
     sample = np.array([0, 1, 2, 3, 17, 33, 1000, 2047, 4095], np.int32)
     orcs = [OracleEnv(names[int(n) % 16], 1, env_offset=int(n), num_levels=0, rand_seed=5) for n in sample]
     seed = 0xD8
