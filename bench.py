@@ -64,7 +64,7 @@ def cpu_baseline(game, num_levels, max_workers=16, steps=12000):
                       "(%.1f s wall, slowest worker %.1f s)" % (game, envs, steps, cores, wall, max(times))}
 
 
-def pmc_traffic(game, kernel="pg_render_kernel"):
+def pmc_traffic(game, kernel="pg_render_kernel", field="hbm_bytes_per_launch"):
     """HBM bytes (FETCH_SIZE + WRITE_SIZE) per render launch of `game` from the newest committed
     rocprofv3 PMC summary under profiles/ (separate FETCH_SIZE / WRITE_SIZE passes over this same
     bench command: scripts/gpu_counters.sh -> *counters_summary.json, or the older
@@ -78,13 +78,14 @@ def pmc_traffic(game, kernel="pg_render_kernel"):
                 d = json.load(f)
         except Exception:
             continue
-        if kernel == "pg_render_kernel" and d.get("game", "coinrun") == game and d.get("render_hbm_bytes_per_launch"):
+        if (field == "hbm_bytes_per_launch" and kernel == "pg_render_kernel" and d.get("game", "coinrun") == game
+                and d.get("render_hbm_bytes_per_launch")):
             return d["render_hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
         g = d.get(game)
         if isinstance(g, dict):
             for kname, k in g.items():
-                if kname.startswith(kernel) and isinstance(k, dict) and k.get("hbm_bytes_per_launch"):
-                    return k["hbm_bytes_per_launch"], os.path.relpath(path, os.path.join(REPO, "profiles"))
+                if kname.startswith(kernel) and isinstance(k, dict) and k.get(field):
+                    return k[field], os.path.relpath(path, os.path.join(REPO, "profiles"))
     return None, None
 
 
@@ -236,24 +237,33 @@ def main():
             dom = max(range(3), key=lambda i: kt[i])
             dom_ms = kt[dom]
             achieved = algo_bytes / (dom_ms * 1e-3) if dom_ms > 0 else 0.0
-            traffic, traffic_src = pmc_traffic(game, names[dom])
+            traffic, traffic_src = pmc_traffic(game, names[dom], "hbm_bytes_per_part_act")
             roof = {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved / 1e9, 2),
                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 5),
                     "traffic": traffic, "traffic_source": traffic_src,
+                    "traffic_what": "FETCH_SIZE + WRITE_SIZE of the kernel's launches in one part of one act "
+                                    "(the step: 1 launch; the render: modes 1 + 2), like kernel_ms",
                     "algorithmic_bytes_per_launch": algo_bytes,
                     "kernel_ms": {"step": round(kt[0], 4), "reset": round(kt[1], 4), "render": round(kt[2], 4),
                                   "step_wall": round(kt[3], 4)},
                     "dominant_kernel": names[dom], "timed_launches": n_timed}
-            for i, key in ((2, "render_kernel"), (0, "step_kernel")):
-                tr, src = pmc_traffic(game, names[i])
+            # per part-act counter bytes (scripts/counter_summary.py hbm_bytes_per_part_act): the step
+            # kernel's one launch, the render's two launches (mode 1 + mode 2) -- matching the kernel
+            # times, which are per part with the render's two modes summed
+            for i, key in ((2, "render_kernel"), (0, "step_kernel"), (1, "reset_kernel")):
+                tr, src = pmc_traffic(game, names[i], "hbm_bytes_per_part_act")
                 a = algo_bytes / (kt[i] * 1e-3) if kt[i] > 0 else 0.0
                 roof[key] = {"ms": round(kt[i], 4), "achieved": round(a / 1e9, 2), "frac": round(a / HBM_PEAK, 5),
-                             "traffic": tr, "traffic_source": src,
-                             "traffic_GBps": round(tr / (kt[i] * 1e-3) / 1e9, 2) if tr and kt[i] > 0 else None}
+                             "traffic_per_part_act": tr, "traffic_source": src,
+                             "traffic_GBps": round(tr / (kt[i] * 1e-3) / 1e9, 2) if tr and kt[i] > 0 else None,
+                             "traffic_ratio": round(tr / algo_bytes, 3) if tr else None}
             roof["parts"] = parts
             e2e = E * OBS_BYTES / (ms_per_step * 1e-3)
+            tr_all, src_all = pmc_traffic(game, "_all_kernels", "hbm_bytes_per_part_act")
             roof["end_to_end"] = {"ms_per_step": round(ms_per_step, 4), "achieved": round(e2e / 1e9, 2),
-                                  "frac": round(e2e / HBM_PEAK, 5)}
+                                  "frac": round(e2e / HBM_PEAK, 5),
+                                  "act_traffic": tr_all * parts if tr_all else None, "traffic_source": src_all,
+                                  "act_traffic_ratio": round(tr_all * parts / (E * OBS_BYTES), 3) if tr_all else None}
         else:
             # a mixed batch runs every game's step -> reset -> render chain concurrently on its own
             # stream: no single kernel's duration is attributable, so the roofline is taken over

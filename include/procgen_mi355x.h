@@ -71,6 +71,15 @@ LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers 
  * buffer on the env's stream: a caller still reading it on another stream orders that first
  * (ObsGather.sync_engine). */
 LIBENV_API int procgen_set_obs_buffer(libenv_env *env, void *d_rgb);
+/* The shard plan libenv_make builds a vec env from (host only, no GPU; vecgame.cpp:349-362, 357-358):
+ * for `num_envs` envs at global env index `env_offset` of the comma list `env_names`, local env e's
+ * game id (game_of[e], procgen/env.py:15-32 order), the seed of its level-seed generator
+ * (lsg_seed[e]: the (env_offset + e)-th draw of mt19937(rand_seed)) and, for a mixed batch, the
+ * per-game local env lists (lists[k * num_envs / G + q]: game k owns the envs whose global index is
+ * k mod G).  Any output may be NULL.  Returns G (the number of names) or -1.  A shard at
+ * env_offset = r * E of N ranks reproduces rows [r * E, (r + 1) * E) of the unsharded plan. */
+LIBENV_API int procgen_shard_plan(const char *env_names, int num_envs, int env_offset, int rand_seed, int32_t *game_of,
+                                  uint32_t *lsg_seed, int32_t *lists);
 /* Copy the outputs of `count` envs (ids env_ids[k]) to host arrays of `count` rows after the
  * enqueued steps finish; any pointer may be NULL.  For consumers (and tests) that sample a few
  * envs of a device-resident batch without copying the whole observation tensor. */

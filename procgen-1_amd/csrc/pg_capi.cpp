@@ -336,6 +336,11 @@ struct VecEnv {
     // page-locked in place with hipHostRegister and written by DMA directly (no staging copy)
     std::vector<void *> registered;
     bool direct = false;
+    // libenv_act with direct buffers: each part's obs DMA is enqueued on its chain's stream right after
+    // its render (vecgame.cpp:426-444: the reference's stepping threads also write the caller's obs
+    // buffers before observe), so part 0's copy runs while part 1 still renders; copy_out then only
+    // moves the small planes
+    bool obs_early = false, obs_inflight = false;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev; // per timed step: 4 per game (before step, after step, after reset,
@@ -517,6 +522,12 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             hipStream_t p = v->pstreams[act % v->npstreams];
             HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
             HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
+            // with 2 prefetch streams, acts a and a+1 generate on different streams: an env whose
+            // episode ends at both would have both write its spare rows, so act a+1's generation
+            // also waits for act a's (ring slot (act - 1) % lag, not yet reused: lag >= 2 here)
+            const int prev = (act + v->lag - 1) % v->lag;
+            if (v->npstreams > 1 && v->lag > 1 && k == 0 && v->ev_pre_set[prev])
+                HIPCHECK(hipStreamWaitEvent(p, v->ev_pre[prev], 0));
             pg_launch_reset(&v->dev, game, list, cnt, p, 2, 0, act, slot);
             HIPCHECK(hipEventRecord(v->ev_pre[act % v->lag], p));
             v->ev_pre_set[act % v->lag] = true;
@@ -535,6 +546,12 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             pg_launch_render(&v->dev, game, list, cnt, s, 0, slot);
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
+        if (v->obs_early && split) { // host buffers: this part's observations leave as soon as it rendered
+            const size_t lo = (size_t)v->chain_lo(k) * PG_OBS_BYTES;
+            HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo, (size_t)cnt * PG_OBS_BYTES,
+                                    hipMemcpyDeviceToHost, s));
+            v->obs_inflight = true;
+        }
     }
     for (size_t j = 1; j < v->gstreams.size() && C > 1; j++) { // join, after every chain is enqueued
         bool used = false;
@@ -609,7 +626,9 @@ int copy_out(VecEnv *v) {
     // stream) -> the caller's per-env host pointers (contiguous runs become one memcpy).
     const size_t n = (size_t)v->num_envs;
     if (v->direct) {
-        HIPCHECK(hipMemcpyAsync(v->registered[0], v->dev.rgb, PG_OBS_BYTES * n, hipMemcpyDeviceToHost, v->stream));
+        if (!v->obs_inflight) // else the act's chains issued the obs DMA part by part (launch_step)
+            HIPCHECK(hipMemcpyAsync(v->registered[0], v->dev.rgb, PG_OBS_BYTES * n, hipMemcpyDeviceToHost, v->stream));
+        v->obs_inflight = false;
         HIPCHECK(hipMemcpyAsync(v->registered[1], v->dev.rew, 4 * n, hipMemcpyDeviceToHost, v->stream));
         HIPCHECK(hipMemcpyAsync(v->registered[2], v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
         HIPCHECK(hipMemcpyAsync(v->registered[3], v->dev.prev_level_seed, 4 * n, hipMemcpyDeviceToHost, v->stream));
@@ -702,7 +721,45 @@ int check_device_errors(VecEnv *v) {
 
 extern "C" {
 
+// The shard plan of a vec env of num_envs envs at global env index env_offset (multi-GPU: rank r of N
+// owns [r * E, (r + 1) * E)): local env e plays game gids[(env_offset + e) % G] (vecgame.cpp:357-358),
+// seeds its level-seed generator with the (env_offset + e)-th draw of rand_seed's mt19937
+// (vecgame.cpp:349-362), and in a mixed batch game k's chain lists the local envs whose global index
+// is k mod G.  libenv_make builds every env from this; procgen_shard_plan exports it (no GPU needed)
+// so the multi-rank CPU tests check that shards concatenate to the unsharded plan.
+static void shard_plan(size_t n, int env_offset, uint32_t rand_seed, const std::vector<int> &gids, int32_t *game_of,
+                       uint32_t *lsg_seed, int32_t *lists) {
+    HostMT seed_gen;
+    seed_gen.seed(rand_seed);
+    for (int k = 0; k < env_offset; k++) (void)seed_gen.next();
+    const size_t ng = gids.size();
+    for (size_t e = 0; e < n; e++) {
+        if (game_of) game_of[e] = gids[((size_t)env_offset + e) % ng];
+        const uint32_t sd = seed_gen.next();
+        if (lsg_seed) lsg_seed[e] = sd;
+    }
+    if (lists && ng > 1)
+        for (size_t k = 0; k < ng; k++) {
+            const size_t r = (size_t)((((int64_t)k - env_offset) % (int64_t)ng + (int64_t)ng) % (int64_t)ng);
+            for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + r);
+        }
+}
+
 LIBENV_API int libenv_version(void) { return LIBENV_VERSION; }
+
+LIBENV_API int procgen_shard_plan(const char *env_names, int num_envs, int env_offset, int rand_seed, int32_t *game_of,
+                                  uint32_t *lsg_seed, int32_t *lists) {
+    if (!env_names || num_envs <= 0 || env_offset < 0) return -1;
+    std::vector<int> gids;
+    for (const std::string &nm : split_names(env_names)) {
+        const int gid = game_id(nm);
+        if (gid < 0) return -1;
+        gids.push_back(gid);
+    }
+    if (gids.empty() || num_envs % (int)gids.size() != 0) return -1;
+    shard_plan((size_t)num_envs, env_offset, (uint32_t)rand_seed, gids, game_of, lsg_seed, lists);
+    return (int)gids.size();
+}
 
 // use_generated_assets (basic-abstract-game.cpp:54-123): every image type of every game present is
 // AssetGen'd on the device (pg_assetgen_sprites_kernel) -- asset_rand_gen seeded fixed_asset_seed +
@@ -998,17 +1055,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         rc |= dalloc(v, &d.sp_queue, (size_t)v->lag * PG_NUM_GAMES * n);
         rc |= dalloc(v, &d.sp_count, (size_t)v->lag * PG_NUM_GAMES);
         if (!rc && hipMemsetAsync(d.sp_gen, 0x80, n * 4, v->stream) != hipSuccess) rc = 1;
-        // the PGEnv words the step kernel writes back (pg_step.hip, the PG_W list) except `error`
+        // the PGEnv words the step kernel writes back (PG_STEP_WB_ALL, pg_engine.h) except `error`
         const size_t offs[][2] = {
-#define PG_F(f) {offsetof(PGEnv, f), sizeof(((PGEnv *)0)->f)}
-            PG_F(action), PG_F(cur_time), PG_F(sd_reward), PG_F(sd_done), PG_F(sd_level_complete), PG_F(total_reward),
-            PG_F(last_reward_timer), PG_F(last_reward), PG_F(prev_level_seed), PG_F(episode_done), PG_F(num_ents),
-            PG_F(agent_erased), PG_F(ghost_x), PG_F(ghost_y), PG_F(ghost_vx), PG_F(ghost_vy), PG_F(ghost_rx),
-            PG_F(ghost_ry), PG_F(move_action), PG_F(special_action), PG_F(last_move_action), PG_F(action_vx),
-            PG_F(action_vy), PG_F(action_vrot), PG_F(step_rand_int), PG_F(rg_mti), PG_F(has_support),
-            PG_F(facing_right), PG_F(is_on_crate), PG_F(last_agent_y), PG_F(fish_eaten), PG_F(has_keys),
-            PG_F(diamonds_remaining), PG_F(died), PG_F(coins_collected), PG_F(eat_time), PG_F(orbs_collected),
-            PG_F(last_fire_time), PG_F(num_enemies), PG_F(gs), PG_F(num_tail)
+#define PG_F(f) {offsetof(PGEnv, f), sizeof(((PGEnv *)0)->f)},
+            PG_STEP_WB_ALL(PG_F)
 #undef PG_F
         };
         for (auto &o : offs)
@@ -1062,12 +1112,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     // from rand_seed's MT, global env index n taking the n-th draw (vecgame.cpp:349-362)
     std::vector<PGEnv> h(n);
     std::vector<uint32_t> hmt(n * 2 * PG_MT_WORDS, 0);
-    HostMT seed_gen;
-    seed_gen.seed((uint32_t)rand_seed);
-    for (int k = 0; k < env_offset; k++) (void)seed_gen.next();
+    std::vector<int32_t> plan_game(n), lists(gids.size() > 1 ? n : 0);
+    std::vector<uint32_t> plan_seed(n);
+    shard_plan(n, env_offset, (uint32_t)rand_seed, gids, plan_game.data(), plan_seed.data(), lists.data());
     for (size_t e = 0; e < n; e++) {
         PGEnv &s = h[e];
-        construct_env(s, v->game_of((int)e));
+        construct_env(s, plan_game[e]);
         s.level_seed_low = level_seed_low;
         s.level_seed_high = level_seed_high;
         s.game_n = env_offset + (int)e;
@@ -1081,22 +1131,13 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         s.opt_use_monochrome_assets = use_monochrome_assets;
         s.rg_mti = PG_MT_N;
         HostMT lsg;
-        lsg.seed(seed_gen.next());
+        lsg.seed(plan_seed[e]);
         memcpy(&hmt[(e * 2 + 1) * PG_MT_WORDS], lsg.mt, sizeof(lsg.mt));
         s.lsg_mti = lsg.mti;
     }
-    // env lists of a mixed batch: game k owns the envs whose global index is k mod G, i.e.
-    // local envs r, r + G, r + 2G, ... with r = (k - env_offset) mod G
-    std::vector<int32_t> lists;
+    // env lists of a mixed batch (shard_plan): game k owns the envs whose global index is k mod G
     const size_t ng = gids.size();
-    if (ng > 1) {
-        lists.resize(n);
-        for (size_t k = 0; k < ng; k++) {
-            size_t r = (size_t)((((int64_t)k - env_offset) % (int64_t)ng + (int64_t)ng) % (int64_t)ng);
-            for (size_t q = 0; q < n / ng; q++) lists[k * (n / ng) + q] = (int32_t)(q * ng + r);
-        }
-        v->h_lists = lists;
-    }
+    if (ng > 1) v->h_lists = lists;
     float rot_angles[PG_ROT_N];
     double rot_table[PG_ROT_N * 4];
     build_rot_table(rot_angles, rot_table);
@@ -1153,6 +1194,7 @@ LIBENV_API int procgen_upload_atlas(libenv_env *env, const uint32_t *pixels, int
                                     const struct pg_image *sprites, const struct pg_image *backgrounds,
                                     const int32_t *num_backgrounds, const int32_t *num_themes) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION;
     if (v->started) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas after the first reset");
     return upload_atlas(v, pixels, num_pixels, sprites, backgrounds, num_backgrounds, num_themes);
 }
@@ -1224,6 +1266,7 @@ extern "C" {
 
 LIBENV_API int procgen_start(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     if (v->started) return 0;
     if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream)); // ring slot 0, every game
@@ -1285,7 +1328,9 @@ LIBENV_API void libenv_act(libenv_env *env) {
         return;
     }
     v->act_pending = true;
+    v->obs_early = v->direct && v->buffers_set && v->games.size() == 1 && !v->render_human;
     launch_step(v, 0, 0, 0);
+    v->obs_early = false;
 }
 
 LIBENV_API void libenv_observe(libenv_env *env) {
@@ -1339,17 +1384,20 @@ LIBENV_API void libenv_close(libenv_env *env) {
 
 LIBENV_API int procgen_act_device(libenv_env *env, const int32_t *d_actions) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     if (d_actions != v->dev.actions)
         HIPCHECK(hipMemcpyAsync(v->dev.actions, d_actions, (size_t)v->num_envs * 4, hipMemcpyDeviceToDevice, v->stream));
     return launch_step(v, 0, 0, 0);
 }
 
 LIBENV_API int procgen_act_hashed(libenv_env *env, uint64_t seed, int32_t t) {
+    if (!env) return -PG_ERR_BAD_OPTION;
     return launch_step((VecEnv *)env, 1, seed, t);
 }
 
 LIBENV_API int procgen_wait(libenv_env *env) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     HIPCHECK(hipSetDevice(v->device));
     HIPCHECK(hipStreamSynchronize(v->stream));
     check_device_errors(v);
@@ -1358,6 +1406,7 @@ LIBENV_API int procgen_wait(libenv_env *env) {
 
 LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers *out) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     out->rgb = v->dev.rgb;
     out->rew = v->dev.rew;
     out->first = v->dev.first;
@@ -1371,6 +1420,7 @@ LIBENV_API int procgen_device_buffers(libenv_env *env, struct pg_device_buffers 
 
 LIBENV_API int procgen_set_obs_buffer(libenv_env *env, void *d_rgb) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     v->dev.rgb = d_rgb ? (uint8_t *)d_rgb : v->own_rgb;
     return 0;
 }
@@ -1379,6 +1429,7 @@ LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int co
                                  uint8_t *first, int32_t *prev_level_seed, uint8_t *prev_level_complete,
                                  int32_t *level_seed) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     HIPCHECK(hipSetDevice(v->device));
     for (int k = 0; k < count; k++) {
         size_t e = (size_t)env_ids[k];
@@ -1410,6 +1461,7 @@ LIBENV_API const char *procgen_error_string(libenv_env *env) {
 
 LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     v->timing = enabled != 0;
     v->t_used = 0;
     return 0;
@@ -1425,6 +1477,7 @@ LIBENV_API int procgen_set_timing(libenv_env *env, int enabled) {
 //   out[4 + 3g .. 6 + 3g] step / reset / render of game slot g (v->games order).
 LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     // per chain (a mixed batch's games, or a single game's parts: averaged over the parts, i.e. the
     // mean duration of one launch over one part's envs)
     const size_t G = v->games.size(), C = v->chains(), per = PG_EV_G * C + 2;
@@ -1456,12 +1509,13 @@ LIBENV_API int procgen_kernel_times(libenv_env *env, float *out, int n) {
 }
 
 // Chains a single-game act is split into (PROCGEN_MI355X_PARTS; 1 for mixed batches).
-LIBENV_API int procgen_num_parts(libenv_env *env) { return ((VecEnv *)env)->parts; }
+LIBENV_API int procgen_num_parts(libenv_env *env) { return env ? ((VecEnv *)env)->parts : 0; }
 
 // Diagnostic builds (make PROFILE=1): per-phase s_memtime cycle sums over all envs since
 // creation; out[0..7] step-kernel phases, out[8..15] render-kernel phases.
 LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     HIPCHECK(hipStreamSynchronize(v->stream));
     std::vector<uint64_t> h((size_t)v->num_envs * 16);
     HIPCHECK(copy_sync(v, h.data(), v->dev.prof, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1475,6 +1529,7 @@ LIBENV_API int procgen_profile_read(libenv_env *env, uint64_t *out) {
 // wave records: words 0-2 step, 8-10 render)
 LIBENV_API int procgen_profile_raw(libenv_env *env, uint64_t *out) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     HIPCHECK(hipStreamSynchronize(v->stream));
     HIPCHECK(copy_sync(v, out, v->dev.prof, (size_t)v->num_envs * 16 * 8, hipMemcpyDeviceToHost));
     return 0;
@@ -1482,6 +1537,7 @@ LIBENV_API int procgen_profile_raw(libenv_env *env, uint64_t *out) {
 
 LIBENV_API int procgen_debug_env(libenv_env *env, int env_idx, void *out, int length) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     if (env_idx < 0 || env_idx >= v->num_envs || length < (int)sizeof(PGEnv)) return -1;
     HIPCHECK(hipStreamSynchronize(v->stream));
     HIPCHECK(copy_sync(v, out, v->dev.envs + env_idx, sizeof(PGEnv), hipMemcpyDeviceToHost));
@@ -1534,6 +1590,7 @@ static const char *validate_env(const VecEnv *v, const PGEnv &s) {
 
 LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, int length) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     if (env_idx < 0 || env_idx >= v->num_envs) return -1;
     if (hipStreamSynchronize(v->stream) != hipSuccess) return -1;
     PGEnv s;
@@ -1664,6 +1721,7 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     for (size_t k = 0; k < v->games.size(); k++)
         pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, v->games[k]);
     hipStreamSynchronize(v->stream);
+    v->obs_inflight = false; // an act's early obs DMA predates this frame: observe copies again
 }
 
 // MinerGame::game_set_state (miner.cpp:423-449; the fork's JS binding's setState,
@@ -1676,6 +1734,7 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
 LIBENV_API int procgen_set_latent_state(libenv_env *env, int env_idx, const int32_t *grid, int grid_width,
                                         int grid_height, int agent_x, int agent_y, int exit_x, int exit_y) {
     VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
     if (!v || env_idx < 0 || env_idx >= v->num_envs || (!grid && grid_width * grid_height > 0))
         return fail(v, PG_ERR_BAD_OPTION, "set_latent_state: bad arguments");
     if (v->game_of(env_idx) != PG_GAME_MINER)

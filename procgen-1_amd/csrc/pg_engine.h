@@ -212,6 +212,35 @@ struct PGEnv {
     int32_t num_tail;
 };
 
+// The PGEnv members pg_step_kernel writes back (everything else is read-only there).  One list for
+// the step's write-back (pg_step.hip) and for the level prefetch's mask of step-written words that a
+// swapped-in spare keeps from the live env (pg_capi.cpp sp_mask): a member added to one is in both.
+// `error` is written back too but is not in the lists (a spare never carries the live env's error).
+#define PG_STEP_WB_COMMON(X)                                                                          \
+    X(action) X(cur_time) X(sd_reward) X(sd_done) X(sd_level_complete) X(total_reward)                 \
+    X(last_reward_timer) X(last_reward) X(prev_level_seed) X(episode_done) X(num_ents) X(agent_erased) \
+    X(ghost_x) X(ghost_y) X(ghost_vx) X(ghost_vy) X(ghost_rx) X(ghost_ry) X(move_action)               \
+    X(special_action) X(last_move_action) X(action_vx) X(action_vy) X(action_vrot) X(step_rand_int)    \
+    X(rg_mti)
+#define PG_STEP_WB_COINRUN(X) X(has_support) X(facing_right) X(is_on_crate) X(last_agent_y)
+#define PG_STEP_WB_BIGFISH(X) X(fish_eaten)
+#define PG_STEP_WB_HEIST(X) X(has_keys)
+#define PG_STEP_WB_MINER(X) X(diamonds_remaining) X(died)
+#define PG_STEP_WB_CLIMBER(X) X(has_support) X(facing_right) X(coins_collected)
+#define PG_STEP_WB_CHASER(X) X(eat_time) X(orbs_collected)
+#define PG_STEP_WB_FRUITBOT(X) X(last_fire_time)
+#define PG_STEP_WB_DODGEBALL(X) X(last_fire_time) X(num_enemies)
+#define PG_STEP_WB_PLUNDER(X) X(last_fire_time) X(gs)
+#define PG_STEP_WB_STARPILOT(X) X(num_tail)
+#define PG_STEP_WB_BOSSFIGHT(X) X(last_fire_time) X(gs)
+#define PG_STEP_WB_NINJA(X) X(last_fire_time) X(gs) X(has_support) X(facing_right)
+#define PG_STEP_WB_JUMPER(X) X(gs) X(has_support) X(facing_right)
+#define PG_STEP_WB_ALL(X)                                                                              \
+    PG_STEP_WB_COMMON(X) PG_STEP_WB_COINRUN(X) PG_STEP_WB_BIGFISH(X) PG_STEP_WB_HEIST(X)              \
+    PG_STEP_WB_MINER(X) PG_STEP_WB_CLIMBER(X) PG_STEP_WB_CHASER(X) PG_STEP_WB_FRUITBOT(X)              \
+    PG_STEP_WB_DODGEBALL(X) PG_STEP_WB_PLUNDER(X) PG_STEP_WB_STARPILOT(X) PG_STEP_WB_BOSSFIGHT(X)      \
+    PG_STEP_WB_NINJA(X) PG_STEP_WB_JUMPER(X)
+
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
 
 // Everything a kernel needs, passed by value.

@@ -2696,7 +2696,17 @@ DEV PGDev spare_view(const PGDev &d) {
     return v;
 }
 DEV int sp_slot(const PGDev &d, int act) { return ((act % d.sp_lag) + d.sp_lag) % d.sp_lag; }
-DEV bool sp_masked(const PGDev &d, int w) { return (d.sp_mask[w >> 5] >> (w & 31)) & 1; }
+// constant indices only: a dynamic index into the by-value kernel argument made the compiler keep a
+// private copy of the whole PGDev in scratch (464 B per lane, written by every wave of the persistent
+// grid: 4,096 waves x 64 lanes x 464 B = the 121.6 MB of the round-3 reset WRITE_SIZE)
+DEV bool sp_masked(const PGDev &d, int w) {
+    // readfirstlane: selects of the four values, not a load through a selected address into the copy
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(d.sp_mask[0]), m1 = __builtin_amdgcn_readfirstlane(d.sp_mask[1]);
+    const uint32_t m2 = __builtin_amdgcn_readfirstlane(d.sp_mask[2]), m3 = __builtin_amdgcn_readfirstlane(d.sp_mask[3]);
+    const int q = w >> 5;
+    const uint32_t m = q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+    return (m >> (w & 31)) & 1;
+}
 
 // After the reset (or swap) of `env` at act `act`: its next level's input -- the post-reset scalars
 // (in LDS) with every step-changeable word poisoned, and the level-seed generator -- is queued for

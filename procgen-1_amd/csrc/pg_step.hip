@@ -31,7 +31,9 @@ struct Ctx {
     bool i_erase;
     int i_theme;
     float av_vy, av_ry; // the agent's vy / ry as other objects' steps see it (coinrun's crate rule)
-    float *pstk;        // LDS: sub_step's suspended push frames (5 x {vx, vy, upper, acc})
+    float *pstk;        // LDS: sub_step's suspended push frames (5 x {vx, vy, upper, acc} + the child's key)
+    uint32_t *memo;     // LDS (aliases the twist staging, idle during step_entities): push-chain memo
+    int nmemo;          // its entries (reset per basic_step_object)
     PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
     Census cs;      // diagnostic wave census (PG_CENSUS builds only)
 };
@@ -407,6 +409,33 @@ DEV void push_offset(const IView &src, const Ent &o, bool is_h, float &t_vx, flo
     else t_vy = (float)((double)sy + dsign(dely) * (double)rsum - (double)o.y);
 }
 
+// Push-chain memo.  Within one basic_step_object call a nested sub_step (a push's child) is a pure
+// function of (depth, the object's x, y, vx, vy, the move): the grid, the static interactors (the
+// scan needs them register-cached: ireg), the agent state its crate rule reads, last_agent_y and
+// action_vy do not change, and its only other effect, coinrun's is_on_crate = 1, is monotone over
+// the call.  Overlapping interactors (coinrun's stacked duplicate crates: a push of 0 leaves the
+// object where it was) make the reference's recursion revisit the same child up to 2^5 times;
+// the memo replays a child's outcome instead of walking it again (coinrun's 280-sub_step crate
+// piles fall to ~50).  Entry k (12 words): key {depth, x, y, vx, vy, move x, move y}, value
+// {x, y, vx, vy, is_on_crate after}; lane k holds entry k's lookup.
+constexpr int PG_MEMO_CAP = 48;
+constexpr int PG_MEMO_W = 12;
+static_assert(PG_MEMO_CAP * PG_MEMO_W <= PG_MT_N, "the memo lives in the twist staging words");
+
+// the entry whose key matches, or -1
+DEV int memo_find(Ctx &c, int depth, const Ent &o, float mvx, float mvy) {
+    bool hit = false;
+    if (LANE < c.nmemo) {
+        const uint4 k0 = *reinterpret_cast<const uint4 *>(c.memo + LANE * PG_MEMO_W);
+        const uint4 k1 = *reinterpret_cast<const uint4 *>(c.memo + LANE * PG_MEMO_W + 4);
+        hit = k0.x == (uint32_t)depth && k0.y == __float_as_uint(o.x) && k0.z == __float_as_uint(o.y) &&
+              k0.w == __float_as_uint(o.vx) && k1.x == __float_as_uint(o.vy) && k1.y == __float_as_uint(mvx) &&
+              k1.z == __float_as_uint(mvy);
+    }
+    const unsigned long long m = ballot(hit);
+    return m ? (int)__builtin_ctzll(m) : -1;
+}
+
 // basic-abstract-game.cpp:278-380 with push_obj (:247-276) folded in.  The reference recurses
 // sub_step -> push_obj -> sub_step(depth + 1) while depth < 5; here the recursion is an explicit
 // stack of at most 5 suspended frames (each: its move, the scan position, block || block2 so far),
@@ -488,9 +517,21 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 acc = true; // block2 = block2 || curr_block
                 float t_vx, t_vy;
                 push_offset(m, o, is_h, t_vx, t_vy);
-                if (d < MAXD) { // suspend this frame, run sub_step(t_vx, t_vy, depth + 1)
-                    float *f = c.pstk + 4 * d;
+                if (d < MAXD) { // run sub_step(t_vx, t_vy, depth + 1)
+                    const int hitk = memo_find(c, d + 1, o, t_vx, t_vy);
+                    if (hitk >= 0) { // replay the child's outcome; push_obj then zeroes the pushed velocity
+                        const uint32_t *v = c.memo + hitk * PG_MEMO_W + 7;
+                        o.x = __uint_as_float(v[0]); o.y = __uint_as_float(v[1]);
+                        o.vx = __uint_as_float(v[2]); o.vy = __uint_as_float(v[3]);
+                        if constexpr (G == PG_GAME_COINRUN) c.s.is_on_crate |= (int)v[4];
+                        if (is_h) o.vx = 0;
+                        else o.vy = 0;
+                        continue;
+                    }
+                    // suspend this frame: its move, scan position and block so far, plus the child's key
+                    float *f = c.pstk + 10 * d;
                     f[0] = _vx; f[1] = _vy; f[2] = __int_as_float(upper); f[3] = acc ? 1.f : 0.f;
+                    f[4] = o.x; f[5] = o.y; f[6] = o.vx; f[7] = o.vy; f[8] = t_vx; f[9] = t_vy;
                     d++;
                     _vx = t_vx;
                     _vy = t_vy;
@@ -516,7 +557,25 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
         if (fresh) continue;
         if (d == 0) return acc;
         d--;
-        const float *f = c.pstk + 4 * d;
+        const float *f = c.pstk + 10 * d;
+        if (c.nmemo < PG_MEMO_CAP) { // record the finished child (depth d + 1)
+            uint32_t *e = c.memo + c.nmemo * PG_MEMO_W;
+            if (LANE < PG_MEMO_W) {
+                uint32_t w;
+                switch (LANE) {
+                case 0: w = (uint32_t)(d + 1); break;
+                case 7: w = __float_as_uint(o.x); break;
+                case 8: w = __float_as_uint(o.y); break;
+                case 9: w = __float_as_uint(o.vx); break;
+                case 10: w = __float_as_uint(o.vy); break;
+                case 11: w = (uint32_t)c.s.is_on_crate; break;
+                default: w = __float_as_uint(f[3 + LANE]); break; // the key saved at suspension
+                }
+                e[LANE] = w;
+            }
+            c.nmemo++;
+            wave_sync();
+        }
         _vx = f[0]; _vy = f[1]; upper = __float_as_int(f[2]); acc = f[3] != 0.f;
     }
 }
@@ -525,6 +584,7 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
 template <int G, bool PL = false>
 DEV void basic_step_object(Ctx &c, int oi, Ent &o) {
     if (o.flags & EF_WILL_ERASE) return;
+    c.nmemo = 0; // the memo holds this call's push children only
     if constexpr (G == PG_GAME_COINRUN) {
         // the agent as this object's crate checks see it: slot 0 is written only by its own step
         if (oi != 0) { c.av_vy = EF(c, F_VY, 0); c.av_ry = EF(c, F_RY, 0); }
@@ -2769,6 +2829,8 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.slist = lds_slist;
     c.ibox = lds_ibox;
     c.pstk = lds_pstk;
+    c.memo = lds_mt;
+    c.nmemo = 0;
     c.iinfo = lds_iinfo;
     c.nlist = 0;
     c.grid8 = lds_grid;
@@ -2841,26 +2903,20 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
         // write back only the PGEnv members this kernel can change (the rest is read-only here)
         PGEnv *o = d.envs + c.env;
 #define PG_W(f) o->f = c.s.f;
-        PG_W(action) PG_W(cur_time) PG_W(sd_reward) PG_W(sd_done) PG_W(sd_level_complete) PG_W(total_reward)
-        PG_W(last_reward_timer) PG_W(last_reward) PG_W(prev_level_seed) PG_W(episode_done) PG_W(num_ents)
-        PG_W(agent_erased) PG_W(ghost_x) PG_W(ghost_y) PG_W(ghost_vx) PG_W(ghost_vy) PG_W(ghost_rx) PG_W(ghost_ry)
-        PG_W(move_action) PG_W(special_action) PG_W(last_move_action) PG_W(action_vx) PG_W(action_vy)
-        PG_W(action_vrot) PG_W(step_rand_int) PG_W(rg_mti) PG_W(error)
-        if constexpr (G == PG_GAME_COINRUN) {
-            PG_W(has_support) PG_W(facing_right) PG_W(is_on_crate) PG_W(last_agent_y)
-        }
-        if constexpr (G == PG_GAME_BIGFISH) { PG_W(fish_eaten) }
-        if constexpr (G == PG_GAME_HEIST) { PG_W(has_keys) }
-        if constexpr (G == PG_GAME_MINER) { PG_W(diamonds_remaining) PG_W(died) }
-        if constexpr (G == PG_GAME_CLIMBER) { PG_W(has_support) PG_W(facing_right) PG_W(coins_collected) }
-        if constexpr (G == PG_GAME_CHASER) { PG_W(eat_time) PG_W(orbs_collected) }
-        if constexpr (G == PG_GAME_FRUITBOT) { PG_W(last_fire_time) }
-        if constexpr (G == PG_GAME_DODGEBALL) { PG_W(last_fire_time) PG_W(num_enemies) }
-        if constexpr (G == PG_GAME_PLUNDER) { PG_W(last_fire_time) PG_W(gs) }
-        if constexpr (G == PG_GAME_STARPILOT) { PG_W(num_tail) }
-        if constexpr (G == PG_GAME_BOSSFIGHT) { PG_W(last_fire_time) PG_W(gs) }
-        if constexpr (G == PG_GAME_NINJA) { PG_W(last_fire_time) PG_W(gs) PG_W(has_support) PG_W(facing_right) }
-        if constexpr (G == PG_GAME_JUMPER) { PG_W(gs) PG_W(has_support) PG_W(facing_right) }
+        PG_STEP_WB_COMMON(PG_W) PG_W(error)
+        if constexpr (G == PG_GAME_COINRUN) { PG_STEP_WB_COINRUN(PG_W) }
+        if constexpr (G == PG_GAME_BIGFISH) { PG_STEP_WB_BIGFISH(PG_W) }
+        if constexpr (G == PG_GAME_HEIST) { PG_STEP_WB_HEIST(PG_W) }
+        if constexpr (G == PG_GAME_MINER) { PG_STEP_WB_MINER(PG_W) }
+        if constexpr (G == PG_GAME_CLIMBER) { PG_STEP_WB_CLIMBER(PG_W) }
+        if constexpr (G == PG_GAME_CHASER) { PG_STEP_WB_CHASER(PG_W) }
+        if constexpr (G == PG_GAME_FRUITBOT) { PG_STEP_WB_FRUITBOT(PG_W) }
+        if constexpr (G == PG_GAME_DODGEBALL) { PG_STEP_WB_DODGEBALL(PG_W) }
+        if constexpr (G == PG_GAME_PLUNDER) { PG_STEP_WB_PLUNDER(PG_W) }
+        if constexpr (G == PG_GAME_STARPILOT) { PG_STEP_WB_STARPILOT(PG_W) }
+        if constexpr (G == PG_GAME_BOSSFIGHT) { PG_STEP_WB_BOSSFIGHT(PG_W) }
+        if constexpr (G == PG_GAME_NINJA) { PG_STEP_WB_NINJA(PG_W) }
+        if constexpr (G == PG_GAME_JUMPER) { PG_STEP_WB_JUMPER(PG_W) }
 #undef PG_W
     }
     c.pt.mark(6);
@@ -2890,7 +2946,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
     // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the
     // workgroups per CU here)
     __shared__ float4 lds_ibox[pl_smart<G>() ? 64 : 1];
-    __shared__ float lds_pstk[(scan_needed<G>(true) || scan_needed<G>(false)) ? 4 * 5 : 1];
+    __shared__ float lds_pstk[(scan_needed<G>(true) || scan_needed<G>(false)) ? 10 * 5 : 1];
     __shared__ int lds_iinfo[pl_smart<G>() ? 64 : 1];
     __shared__ __attribute__((aligned(16))) int8_t lds_grid[PG_GRID_MAX];
     __shared__ uint8_t lds_moved[G == PG_GAME_MINER ? 35 * 35 : 1];

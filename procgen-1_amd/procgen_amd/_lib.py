@@ -86,6 +86,8 @@ SIGNATURES = {
     "procgen_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "procgen_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "procgen_num_parts": (ctypes.c_int, [ctypes.c_void_p]),
+    "procgen_shard_plan": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_debug_env": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "procgen_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_profile_raw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

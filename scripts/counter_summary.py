@@ -39,12 +39,36 @@ for gdir in sorted(glob.glob(os.path.join(root, "*"))):
             d["scratch"] = int(r.get("Scratch_Size", r.get("Private_Segment_Size", 0)) or 0)
             d["workgroup"] = int(r.get("Workgroup_Size", r.get("Workgroup_Size_X", 0)) or 0)
             d["grid"] = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+    # per pass: (dispatch id, kernel, value) of every counter, for the per-act sums below
+    seq = defaultdict(list)
     for f in glob.glob(os.path.join(gdir, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = kname(r["Kernel_Name"])
             if not k:
                 continue
             kern[k]["counters"][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            did = int(r.get("Dispatch_Id", r.get("Dispatch_ID", 0)) or 0)
+            seq[r["Counter_Name"]].append((did, k, float(r["Counter_Value"])))
+    # Per part-act sums: one act of a single game runs, per part, one step launch, the reset
+    # launches and the render launches (mode 1 over the envs that did not finish + mode 2 over the
+    # reset ones).  Over the last two thirds of the run's step launches (steady state), the bytes
+    # of each kernel summed and divided by the number of step launches = that kernel's bytes per
+    # part-act (for the step kernel: per launch; for the render: both modes).
+    per_act = defaultdict(dict)
+    for cname in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = sorted(seq.get(cname, []))
+        steps = [i for i, (_, k, _) in enumerate(rows) if k.startswith("pg_step_kernel")]
+        if len(steps) < 3:
+            continue
+        lo = steps[len(steps) // 3]
+        n_steps = sum(1 for i in steps if i >= lo)
+        tot = defaultdict(float)
+        for did, k, v in rows[lo:]:
+            tot[k] += v
+        for k, v in tot.items():
+            per_act[k][cname] = v * 1024 / n_steps
+        for k in tot:
+            per_act[k]["step_launches_in_window"] = n_steps
     res = {}
     for k, d in kern.items():
         c = {n: sum(v) / len(v) for n, v in d["counters"].items() if v}
@@ -63,6 +87,16 @@ for gdir in sorted(glob.glob(os.path.join(root, "*"))):
             e["hbm_bytes_per_launch"] = round((c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
             e["fetch_bytes_per_launch"] = round(c["FETCH_SIZE"] * 1024)
             e["write_bytes_per_launch"] = round(c["WRITE_SIZE"] * 1024)
+        pa = per_act.get(k, {})
+        if "FETCH_SIZE" in pa and "WRITE_SIZE" in pa:
+            e["hbm_bytes_per_part_act"] = round(pa["FETCH_SIZE"] + pa["WRITE_SIZE"])
+            e["fetch_bytes_per_part_act"] = round(pa["FETCH_SIZE"])
+            e["write_bytes_per_part_act"] = round(pa["WRITE_SIZE"])
+            e["step_launches_in_window"] = pa["step_launches_in_window"]
         res[k] = e
+    tot = [v["hbm_bytes_per_part_act"] for v in res.values() if "hbm_bytes_per_part_act" in v]
+    if tot:
+        res["_all_kernels"] = {"hbm_bytes_per_part_act": round(sum(tot)),
+                               "what": "step + reset(s) + render(s) FETCH_SIZE + WRITE_SIZE per part-act"}
     out[game] = res
 print(json.dumps(out, indent=1, sort_keys=True))

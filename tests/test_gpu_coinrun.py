@@ -232,3 +232,29 @@ def test_gpu_determinism_two_engines():
             np.testing.assert_array_equal(ga[k], gb[k], err_msg="%s differs at step %d" % (k, t))
     a.close()
     b.close()
+
+
+# Global env indices of the 200-level config whose levels hold crate piles (duplicate / stacked
+# crates): with action seed 0, their steps reach 280-520 sub_step calls (the push recursion
+# revisiting the same child up to 2^5 times) -- the steps the engine's push-chain memo
+# (pg_step.hip memo_find) replays instead of walking.  Found with the oracle's diagnostic
+# sub_step counter over envs 0..4095 (and 48596, the round-3 census tail env).
+CRATE_PILE_ENVS = [56, 1551, 2240, 3056, 3350, 3868, 48596]
+
+
+@pytest.mark.parametrize("e", CRATE_PILE_ENVS)
+def test_crate_pile_push_chains(e):
+    """Bit-exact through the deepest push chains: every step of 320, 1-env shard at global index e."""
+    env = make_gpu(1, num_levels=200, start_level=0, rand_seed=0, env_offset=e)
+    orc = OracleEnv("coinrun", 1, env_offset=e, num_levels=200, start_level=0, rand_seed=0)
+    assert_same(gpu_obs(env), orc.observe(), 0)
+    for t in range(320):
+        act = hashed_actions(0, [e], t)
+        env.act(act)
+        orc.step(act)
+        try:
+            assert_same(gpu_obs(env), orc.observe(), t + 1)
+        except AssertionError as err:
+            raise AssertionError("%s\n  global env %d\n  engine: %s\n  oracle debug: %s"
+                                 % (err, e, describe_engine_env(env, 0), orc.debug(0).tolist()))
+    env.close()
