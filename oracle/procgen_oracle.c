@@ -4310,6 +4310,8 @@ static QtTarget RT = {NULL, 64, 64, false, NULL, 0, 0};
 static void qt_smooth_draw_image(double x, double y, double w, double h, const uint32_t *px, int iw, int ih, int fmt,
                                  bool mirrored, double opacity);
 static void qt_smooth_fill_rectf(double x, double y, double w, double h, uint32_t argb);
+static void qt_smooth_draw_image_rot(double x, double y, double w, double h, double deg, const uint32_t *px, int iw,
+                                     int ih, int fmt, bool mirrored, double opacity);
 
 /* QPainter::drawImage(QRectF target, QImage img) with identity transform
  * (qpaintengine_raster.cpp drawImage -> qt_scale_image_32bit). */
@@ -4565,7 +4567,10 @@ static bool qt_fuzzy_null(double d) { return fabs(d) <= 0.000000000001; }
  * qt_scale_image_32bit on qt_mapRect_non_normalizing(r, matrix), whose TxScale map ignores m12/m21. */
 static void qt_draw_image_rotated(uint32_t *canvas, double x, double y, double w, double h, double deg,
                                   const uint32_t *px, int iw, int ih, bool mirrored, double opacity) {
-    if (RT.smooth) fatal_msg("render_mode=rgb_array: rotated sprites are not restated");
+    if (RT.smooth) {
+        qt_smooth_draw_image_rot(x, y, w, h, deg, px, iw, ih, QFMT_ARGB32_PM, mirrored, opacity);
+        return;
+    }
     QtXform t = qt_translate_rotate(x + w / 2, y + h / 2, deg);
     double rx = -w / 2, ry = -h / 2;
     if (w <= 0 || h <= 0) return; /* QRectF::isEmpty */
@@ -4625,13 +4630,173 @@ typedef struct { double x, y, w, h; } RectD;
 typedef struct { int x, len, y, cov; } QtSpan;
 static int qt_c_int(double v) { return (int)v; }
 
-/* QRasterizer::rasterizeLine(a, b, width) for the rect's mid line, antialiased; clip = [0, cw) x [0, ch) */
-static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int ch, QtSpan *out, int cap) {
-    const double ax = (x + x) * 0.5, ay = (y + (y + h)) * 0.5;
-    const double bx = ((x + w) + (x + w)) * 0.5, by = ay;
-    double width = h / w;
+/* Qt 5.9.7 qrasterizer.cpp helpers: Q16Dot16 arithmetic, qSafeDivide, qSafeFloatToQ16Dot16 and
+ * snapTo26Dot6Grid (read off the library's own machine code: the general branch below matches it
+ * bit for bit, tests/test_smooth_pins.py) */
+static int qt_fp_safe(double x) { /* qSafeFloatToQ16Dot16 */
+    const double v = x * 65536.;
+    if (v > 2147483647.0) return 0x7fffffff;
+    if (v < -2147483648.0) return -2147483647;
+    return (int)v;
+}
+static double qt_safe_div(double x, double y) { return y == 0 ? (x > 0 ? 1e20 : -1e20) : x / y; }
+static int qt_fp_mul(int x, int y) { return (int)(((int64_t)x * (int64_t)y) >> 16); } /* Q16Dot16Multiply */
+static void qt_snap26(double *x, double *y) {
+    const double ny = floor(*y * 64) * 0.015625, nx = floor(*x * 64) * 0.015625;
+    *x = nx;
+    *y = ny;
+}
+/* intersectPixelFP: the area of pixel column x in rows [top, bottom) on the outer side of an edge */
+static int qt_intersect_pixel(int x, int top, int bottom, int leftIntersectX, int rightIntersectX, int slope, int invSlope) {
+    const int leftX = x << 16, rightX = leftX + 65536;
+    const int leftIntersectY = top + qt_fp_mul(slope > 0 ? leftX - leftIntersectX : leftX - rightIntersectX, invSlope);
+    const int rightIntersectY = leftIntersectY + invSlope;
+    if (leftIntersectX >= leftX && rightIntersectX <= rightX)
+        return qt_fp_mul(bottom - top, leftIntersectX - leftX + ((rightIntersectX - leftIntersectX) >> 1));
+    if (leftIntersectX >= rightX) return bottom - top;
+    if (leftIntersectX >= leftX)
+        return (bottom - top) -
+               ((((rightX - leftIntersectX) >> 1) * (slope > 0 ? rightIntersectY - top : bottom - rightIntersectY)) >> 16);
+    if (rightIntersectX <= leftX) return 0;
+    if (rightIntersectX <= rightX)
+        return (((rightIntersectX - leftX) >> 1) * (slope > 0 ? bottom - leftIntersectY : leftIntersectY - top)) >> 16;
+    if (slope > 0) return (bottom - rightIntersectY) + ((rightIntersectY - leftIntersectY) >> 1);
+    return (rightIntersectY - top) + ((leftIntersectY - rightIntersectY) >> 1);
+}
+static void qt_span_add(QtSpan *out, int *k, int cap, int x, int len, int y, int cov) {
+    if (cov && len && *k < cap) {
+        QtSpan sp = {x, len, y, cov};
+        out[(*k)++] = sp;
+    }
+}
+/* the general (neither horizontal nor vertical) antialiased branch: the line's rectangle (corners
+ * snapped to the 26.6 grid) scanned row by row, each row's covered columns as single-pixel spans at
+ * the four edges and one full-coverage run between them */
+static int qt_aa_general_spans(double pax, double pay, double pbx, double pby, double width, int cw, int ch, QtSpan *out,
+                               int cap) {
+    if (pay > pby) {
+        double t = pax; pax = pbx; pbx = t;
+        t = pay; pay = pby; pby = t;
+    }
+    const double hw = 0.5f * width;
+    const double dlx = (pbx - pax) * hw, dly = (pby - pay) * hw;
+    const double prx = dly, pry = -dlx; /* perp */
+    double tx, ty, lx, ly, rx, ry, bx, by;
+    if (pax < pbx) {
+        tx = pax + prx; ty = pay + pry; lx = pax - prx; ly = pay - pry;
+        rx = pbx + prx; ry = pby + pry; bx = pbx - prx; by = pby - pry;
+    } else {
+        tx = pax - prx; ty = pay - pry; lx = pbx - prx; ly = pby - pry;
+        rx = pax + prx; ry = pay + pry; bx = pbx + prx; by = pby + pry;
+    }
+    qt_snap26(&tx, &ty);
+    qt_snap26(&bx, &by);
+    qt_snap26(&lx, &ly);
+    qt_snap26(&rx, &ry);
+    const double topBound = ty < 0 ? 0 : (ty > ch - 1 ? ch - 1 : ty);
+    const double bottomBound = by < 0 ? 0 : (by > ch - 1 ? ch - 1 : by);
+    const double tlSlopeInv = qt_safe_div(lx - tx, ly - ty), blSlopeInv = qt_safe_div(bx - lx, by - ly);
+    const double trSlopeInv = qt_safe_div(rx - tx, ry - ty), brSlopeInv = qt_safe_div(bx - rx, by - ry);
+    const int tlS = qt_fp_safe(tlSlopeInv), trS = qt_fp_safe(trSlopeInv), blS = qt_fp_safe(blSlopeInv), brS = qt_fp_safe(brSlopeInv);
+    const int itlS = qt_fp_safe(qt_safe_div(1, tlSlopeInv)), itrS = qt_fp_safe(qt_safe_div(1, trSlopeInv));
+    const int iblS = qt_fp_safe(qt_safe_div(1, blSlopeInv)), ibrS = qt_fp_safe(qt_safe_div(1, brSlopeInv));
+    const int iTop = (int)topBound, iTopFP = iTop << 16, iLeftFP = ((int)ly) << 16, iRightFP = ((int)ry) << 16;
+    const int iBottomFP = ((int)bottomBound) << 16;
+    int leftAf = qt_fp_safe(tx + (iTop - ty) * tlSlopeInv), rightAf = qt_fp_safe(tx + (iTop - ty) * trSlopeInv);
+    int leftBf = 0, rightBf = 0;
+    if (iLeftFP < iTopFP) leftBf = qt_fp_safe(lx + (iTop - ly) * blSlopeInv);
+    if (iRightFP < iTopFP) rightBf = qt_fp_safe(rx + (iTop - ry) * brSlopeInv);
+    const int yTopFP = qt_fp_safe(ty), yLeftFP = qt_fp_safe(ly), yRightFP = qt_fp_safe(ry), yBottomFP = qt_fp_safe(by);
+    int rowTop = iTopFP > yTopFP ? iTopFP : yTopFP;
+    int tlAf = leftAf + qt_fp_mul(tlS, rowTop - iTopFP), trAf = rightAf + qt_fp_mul(trS, rowTop - iTopFP);
+    int k = 0;
+    for (int yFP = iTopFP; yFP <= iBottomFP; yFP += 65536, rowTop = yFP) {
+        const int rowBottomLeft = yFP + 65536 < yLeftFP ? yFP + 65536 : yLeftFP;
+        const int rowBottomRight = yFP + 65536 < yRightFP ? yFP + 65536 : yRightFP;
+        const int rowTopLeft = yFP > yLeftFP ? yFP : yLeftFP, rowTopRight = yFP > yRightFP ? yFP : yRightFP;
+        const int rowBottom = yFP + 65536 < yBottomFP ? yFP + 65536 : yBottomFP;
+        int tlBf, blAf, trBf, brAf, blBf, brBf;
+        if (yFP == iLeftFP) {
+            leftBf = qt_fp_safe(lx + ((yFP >> 16) - ly) * blSlopeInv);
+            tlBf = leftBf + qt_fp_mul(blS, rowTopLeft - yFP);
+            blAf = leftAf + qt_fp_mul(tlS, rowBottomLeft - yFP);
+        } else {
+            tlBf = leftBf;
+            blAf = leftAf + tlS;
+        }
+        if (yFP == iRightFP) {
+            rightBf = qt_fp_safe(rx + ((yFP >> 16) - ry) * brSlopeInv);
+            trBf = rightBf + qt_fp_mul(brS, rowTopRight - yFP);
+            brAf = rightAf + qt_fp_mul(trS, rowBottomRight - yFP);
+        } else {
+            trBf = rightBf;
+            brAf = rightAf + trS;
+        }
+        if (yFP == iBottomFP) {
+            blBf = leftBf + qt_fp_mul(blS, rowBottom - yFP);
+            brBf = rightBf + qt_fp_mul(brS, rowBottom - yFP);
+        } else {
+            blBf = leftBf + blS;
+            brBf = rightBf + brS;
+        }
+        int leftMin, leftMax, rightMin, rightMax;
+        if (yFP < iLeftFP) {
+            leftMin = blAf >> 16; leftMax = tlAf >> 16;
+        } else if (yFP == iLeftFP) {
+            leftMin = (blAf > tlBf ? blAf : tlBf) >> 16; leftMax = (tlAf > blBf ? tlAf : blBf) >> 16;
+        } else {
+            leftMin = tlBf >> 16; leftMax = blBf >> 16;
+        }
+        leftMin = leftMin < 0 ? 0 : (leftMin > cw - 1 ? cw - 1 : leftMin);
+        leftMax = leftMax < 0 ? 0 : (leftMax > cw - 1 ? cw - 1 : leftMax);
+        if (yFP < iRightFP) {
+            rightMin = trAf >> 16; rightMax = brAf >> 16;
+        } else if (yFP == iRightFP) {
+            rightMin = (trAf < brBf ? trAf : brBf) >> 16; rightMax = (brAf < trBf ? brAf : trBf) >> 16;
+        } else {
+            rightMin = brBf >> 16; rightMax = trBf >> 16;
+        }
+        rightMin = rightMin < 0 ? 0 : (rightMin > cw - 1 ? cw - 1 : rightMin);
+        rightMax = rightMax < 0 ? 0 : (rightMax > cw - 1 ? cw - 1 : rightMax);
+        if (leftMax > rightMax) leftMax = rightMax;
+        if (rightMin < leftMin) rightMin = leftMin;
+        const int rowHeight = rowBottom - rowTop, yi = yFP >> 16;
+        int x = leftMin;
+        for (; x <= leftMax; x++) {
+            int ex = 0;
+            if (yFP <= iLeftFP) ex += qt_intersect_pixel(x, rowTop, rowBottomLeft, blAf, tlAf, tlS, itlS);
+            if (yFP >= iLeftFP) ex += qt_intersect_pixel(x, rowTopLeft, rowBottom, tlBf, blBf, blS, iblS);
+            if (x >= rightMin) {
+                if (yFP <= iRightFP) ex += (rowBottomRight - rowTop) - qt_intersect_pixel(x, rowTop, rowBottomRight, trAf, brAf, trS, itrS);
+                if (yFP >= iRightFP) ex += (rowBottom - rowTopRight) - qt_intersect_pixel(x, rowTopRight, rowBottom, brBf, trBf, brS, ibrS);
+            }
+            qt_span_add(out, &k, cap, x, 1, yi, ((255 * (rowHeight - ex)) >> 16) & 0xff);
+        }
+        if (x < rightMin) {
+            qt_span_add(out, &k, cap, x, rightMin - x, yi, ((255 * rowHeight) >> 16) & 0xff);
+            x = rightMin;
+        }
+        for (; x <= rightMax; x++) {
+            int ex = 0;
+            if (yFP <= iRightFP) ex += (rowBottomRight - rowTop) - qt_intersect_pixel(x, rowTop, rowBottomRight, trAf, brAf, trS, itrS);
+            if (yFP >= iRightFP) ex += (rowBottom - rowTopRight) - qt_intersect_pixel(x, rowTopRight, rowBottom, brBf, trBf, brS, ibrS);
+            qt_span_add(out, &k, cap, x, 1, yi, ((255 * (rowHeight - ex)) >> 16) & 0xff);
+        }
+        leftAf += tlS;
+        leftBf += blS;
+        rightAf += trS;
+        rightBf += brS;
+        tlAf = leftAf;
+        trAf = rightAf;
+    }
+    return k;
+}
+
+/* QRasterizer::rasterizeLine(a, b, width) antialiased (squareCap off); clip = [0, cw) x [0, ch) */
+static int qt_aa_line_spans(double ax, double ay, double bx, double by, double width, int cw, int ch, QtSpan *out,
+                            int cap) {
     double pax = ax, pay = ay, pbx = bx, pby = by;
-    if (ax == bx && ay == by) return 0;
+    if ((qt_fuzzy_null(ax - bx) && qt_fuzzy_null(ay - by)) || width == 0) return 0; /* QPointF == is fuzzy */
     {
         const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
         const double cl = 0 - offx, ct = 0 - offy;
@@ -4665,13 +4830,17 @@ static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int 
         if (ww == 0) return 0;
         width *= sqrt(w0 / ww);
     }
-    { /* horizontal -> vertical (qFuzzyCompare(pa.y, pb.y) holds for the mid line) */
+    if ((int)((pby - pay) * 64.) == 0) { /* horizontal (q26Dot6Compare) -> vertical */
         const double xm = (pax + pbx) * 0.5f, dx = fabs(pbx - pax) * 0.5f, yy = pay, dy = width * dx;
         pax = xm; pay = yy - dy;
         pbx = xm; pby = yy + dy;
         width = 1 / width;
     }
-    if (pay > pby) { const double t = pay; pay = pby; pby = t; }
+    if ((int)((pbx - pax) * 64.) != 0) return qt_aa_general_spans(pax, pay, pbx, pby, width, cw, ch, out, cap);
+    if (pay > pby) {
+        double t = pay; pay = pby; pby = t;
+        t = pax; pax = pbx; pbx = t;
+    }
     const double dy = pby - pay, half = 0.5f * width * dy;
     double left = pax - half, right = pax + half;
     left = left < 0 ? 0 : (left > cw ? cw : left);
@@ -4716,6 +4885,11 @@ static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int 
     }
     return k;
 }
+/* the rect's mid line with width h / w (QRasterPaintEngine::drawImage / fillRect, identity matrix) */
+static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int ch, QtSpan *out, int cap) {
+    return qt_aa_line_spans((x + x) * 0.5, (y + (y + h)) * 0.5, ((x + w) + (x + w)) * 0.5, (y + (y + h)) * 0.5, h / w, cw,
+                            ch, out, cap);
+}
 
 static uint32_t qt_interp_256(uint32_t x, uint32_t a, uint32_t y, uint32_t b) { /* INTERPOLATE_PIXEL_256 */
     uint32_t t = (x & 0xff00ffu) * a + (y & 0xff00ffu) * b;
@@ -4740,20 +4914,27 @@ static uint32_t qt_interp4_4(uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br,
 
 /* fetchTransformedBilinearARGB32PM (not tiled) of `len` device pixels from (x, y) for a TxScale
  * inverse (m11, m22, mdx, mdy); `mirrored` reads the horizontally mirrored image */
-static void qt_fetch_bilinear(uint32_t *out, int x, int y, int len, const uint32_t *px, int iw, int ih, bool mirrored,
-                              double m11, double m22, double mdx, double mdy) {
+static void qt_fetch_rotate(uint32_t *out, int len, const uint32_t *px, int iw, int ih, bool mirrored, int fx, int fy,
+                            int fdx, int fdy, bool fast);
+static void qt_fetch_bilinear_x(uint32_t *out, int x, int y, int len, const uint32_t *px, int iw, int ih, bool mirrored,
+                                double m11, double m12, double m21, double m22, double mdx, double mdy) {
 #define QT_TEX(r, c) px[(size_t)(r) * iw + (mirrored ? iw - 1 - (c) : (c))]
     const double cx = x + 0.5, cy = y + 0.5;
-    const int fdx = (int)(m11 * 65536);
-    int fx = (int)((0.0 * cy + m11 * cx + mdx) * 65536) - 32768;
-    const int fy = (int)((m22 * cy + 0.0 * cx + mdy) * 65536) - 32768;
+    const int fdx = (int)(m11 * 65536), fdy = (int)(m12 * 65536);
+    int fx = (int)((m21 * cy + m11 * cx + mdx) * 65536) - 32768;
+    const int fy = (int)((m22 * cy + m12 * cx + mdy) * 65536) - 32768;
+    if (fdy != 0) { /* rotation or shear: 8-bit positions beyond an 8x zoom, else the 4-bit SSE2 helper */
+        qt_fetch_rotate(out, len, px, iw, ih, mirrored, fx, fy, fdx, fdy, !(fabs(m11) < 1. / 8. || fabs(m22) < 1. / 8.));
+        return;
+    }
     int y1 = fy >> 16, y2;
     if (y1 < 0) y1 = y2 = 0;
     else if (y1 >= ih - 1) y1 = y2 = ih - 1;
     else y2 = y1 + 1;
     const uint32_t dy8 = (uint32_t)(fy & 0xffff) >> 8, dy4 = (dy8 + 8) >> 4;
-    /* helper choice: |fdx| <= 1 -> simple upscale; |m22| < 1/8 -> upscale; else downscale */
-    const bool down = !(abs(fdx) <= 65536) && !(fabs(m22) < 1. / 8.);
+    /* simple upscale on x without mirroring; the 8-bit upscale helper beyond 8x (on y, or on x mirrored); else
+     * the downscale helper (also a mirrored upscale on x of less than 8x) */
+    const bool down = !(fdx > 0 && fdx <= 65536) && !(fdx < 0 && fdx > -8192) && !(fabs(m22) < 1. / 8.);
     int n = 0;
     while (n < len) { /* leading pixels on a clamped column: vertical interpolation only */
         const int c = fx >> 16;
@@ -4792,12 +4973,74 @@ static void qt_fetch_bilinear(uint32_t *out, int x, int y, int len, const uint32
     }
 #undef QT_TEX
 }
+static void qt_fetch_bilinear(uint32_t *out, int x, int y, int len, const uint32_t *px, int iw, int ih, bool mirrored,
+                              double m11, double m22, double mdx, double mdy) {
+    qt_fetch_bilinear_x(out, x, y, len, px, iw, ih, mirrored, m11, 0.0, 0.0, m22, mdx, mdy);
+}
+/* fetchTransformedBilinearARGB32PM_rotate_helper (8-bit positions) and _fast_rotate_helper: its
+ * possibly clamped lead-in pixels and its tail with 8-bit weights, the unclamped middle in groups of
+ * 4 with 4-bit weights (the SSE2 loop), the scalar rest of the middle with 8-bit weights */
+static void qt_fetch_rotate(uint32_t *out, int len, const uint32_t *px, int iw, int ih, bool mirrored, int fx, int fy,
+                            int fdx, int fdy, bool fast) {
+#define QT_TEX(r, c) px[(size_t)(r) * iw + (mirrored ? iw - 1 - (c) : (c))]
+#define QT_BOUNDS(n, v1, v2) do { if ((v1) < 0) (v2) = (v1) = 0; else if ((v1) >= (n) - 1) (v2) = (v1) = (n) - 1; else (v2) = (v1) + 1; } while (0)
+    int n = 0;
+    if (fast) {
+        for (; n < len; n++) {
+            int x1 = fx >> 16, x2, y1 = fy >> 16, y2;
+            QT_BOUNDS(iw, x1, x2);
+            QT_BOUNDS(ih, y1, y2);
+            if (x1 != x2 && y1 != y2) break;
+            out[n] = qt_interp4_8(QT_TEX(y1, x1), QT_TEX(y1, x2), QT_TEX(y2, x1), QT_TEX(y2, x2), (uint32_t)(fx & 0xffff) >> 8,
+                                  (uint32_t)(fy & 0xffff) >> 8);
+            fx += fdx;
+            fy += fdy;
+        }
+        int64_t bend = len;
+        const int64_t max_fx = (int64_t)(iw - 1) * 65536, max_fy = (int64_t)(ih - 1) * 65536;
+        if (fdx > 0) { const int64_t b = n + (max_fx - fx) / fdx; if (b < bend) bend = b; }
+        else if (fdx < 0) { const int64_t b = n + (0 - (int64_t)fx) / fdx; if (b < bend) bend = b; }
+        if (fdy > 0) { const int64_t b = n + (max_fy - fy) / fdy; if (b < bend) bend = b; }
+        else if (fdy < 0) { const int64_t b = n + (0 - (int64_t)fy) / fdy; if (b < bend) bend = b; }
+        while (n < bend - 3) {
+            for (int q = 0; q < 4; q++, n++) {
+                const int c = fx >> 16, r = fy >> 16;
+                const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4, dy4 = (((uint32_t)(fy & 0xffff) >> 8) + 8) >> 4;
+                out[n] = qt_interp4_4(QT_TEX(r, c), QT_TEX(r, c + 1), QT_TEX(r + 1, c), QT_TEX(r + 1, c + 1), dx4, dy4);
+                fx += fdx;
+                fy += fdy;
+            }
+        }
+        for (; n < bend; n++) {
+            const int c = fx >> 16, r = fy >> 16;
+            out[n] = qt_interp4_8(QT_TEX(r, c), QT_TEX(r, c + 1), QT_TEX(r + 1, c), QT_TEX(r + 1, c + 1),
+                                  (uint32_t)(fx & 0xffff) >> 8, (uint32_t)(fy & 0xffff) >> 8);
+            fx += fdx;
+            fy += fdy;
+        }
+    }
+    for (; n < len; n++) {
+        int x1 = fx >> 16, x2, y1 = fy >> 16, y2;
+        QT_BOUNDS(iw, x1, x2);
+        QT_BOUNDS(ih, y1, y2);
+        out[n] = qt_interp4_8(QT_TEX(y1, x1), QT_TEX(y1, x2), QT_TEX(y2, x1), QT_TEX(y2, x2), (uint32_t)(fx & 0xffff) >> 8,
+                              (uint32_t)(fy & 0xffff) >> 8);
+        fx += fdx;
+        fy += fdy;
+    }
+#undef QT_BOUNDS
+#undef QT_TEX
+}
 
-static void qt_log(double kind, double a, double b, double c, double d, double e, double f, double g, double h) {
-    if (!RT.log || RT.log_n + 9 > RT.log_cap) return;
+static void qt_log10(double kind, double a, double b, double c, double d, double e, double f, double g, double h, double i) {
+    if (!RT.log || RT.log_n + 10 > RT.log_cap) return;
     double *q = RT.log + RT.log_n;
+    q[9] = i;
     q[0] = kind; q[1] = a; q[2] = b; q[3] = c; q[4] = d; q[5] = e; q[6] = f; q[7] = g; q[8] = h;
-    RT.log_n += 9;
+    RT.log_n += 10;
+}
+static void qt_log(double kind, double a, double b, double c, double d, double e, double f, double g, double h) {
+    qt_log10(kind, a, b, c, d, e, f, g, h, 0);
 }
 
 /* QPainter::drawImage(QRectF(x, y, w, h), img) under Antialiasing + SmoothPixmapTransform on RT */
@@ -4858,6 +5101,166 @@ static void qt_smooth_draw_image(double x, double y, double w, double h, const u
                 if (fmt == QFMT_RGB32) { /* SourceOver of an opaque image = Source (comp_func_Source) */
                     *dp = cov == 255 ? s : INTERPOLATE_PIXEL_255(s, (uint32_t)cov, *dp, 255 - (uint32_t)cov);
                 } else if (cov == 255) { /* comp_func_SourceOver */
+                    if (s >= 0xff000000u) *dp = s;
+                    else if (s != 0) *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                } else {
+                    s = BYTE_MUL(s, (uint32_t)cov);
+                    *dp = s + BYTE_MUL(*dp, (~s) >> 24);
+                }
+            }
+        }
+        i = j + 1;
+    }
+}
+
+/* QTransform as the raster engine uses it for a rotated drawImage: the type (QTransform::type()'s
+ * qFuzzyIsNull classification), translate / scale / operator* / inverted per type, map per type */
+enum { QTX_NONE = 0, QTX_TRANSLATE = 1, QTX_SCALE = 2, QTX_ROTATE = 4, QTX_SHEAR = 8 };
+typedef struct { double m11, m12, m21, m22, dx, dy; int type; } QtXf;
+static int qtx_classify(const QtXf *t) {
+    if (!qt_fuzzy_null(t->m12) || !qt_fuzzy_null(t->m21))
+        return qt_fuzzy_null(t->m11 * t->m12 + t->m21 * t->m22) ? QTX_ROTATE : QTX_SHEAR;
+    if (!qt_fuzzy_null(t->m11 - 1) || !qt_fuzzy_null(t->m22 - 1)) return QTX_SCALE;
+    if (!qt_fuzzy_null(t->dx) || !qt_fuzzy_null(t->dy)) return QTX_TRANSLATE;
+    return QTX_NONE;
+}
+static void qtx_translate(QtXf *t, double dx, double dy) {
+    if (dx == 0 && dy == 0) return;
+    switch (t->type) {
+    case QTX_NONE: t->dx = dx; t->dy = dy; t->type = QTX_TRANSLATE; break;
+    case QTX_TRANSLATE: t->dx += dx; t->dy += dy; break;
+    case QTX_SCALE: t->dx += dx * t->m11; t->dy += dy * t->m22; break;
+    default: t->dx += dx * t->m11 + dy * t->m21; t->dy += dy * t->m22 + dx * t->m12; break;
+    }
+    t->type = qtx_classify(t);
+}
+static void qtx_scale(QtXf *t, double sx, double sy) {
+    if (sx == 1 && sy == 1) return;
+    switch (t->type) {
+    case QTX_NONE:
+    case QTX_TRANSLATE: t->m11 = sx; t->m22 = sy; break;
+    case QTX_ROTATE:
+    case QTX_SHEAR: t->m12 *= sx; t->m21 *= sy; /* fall through */
+    default: t->m11 *= sx; t->m22 *= sy; break;
+    }
+    t->type = qtx_classify(t);
+}
+/* translate(1/65536, 1/65536) * m */
+static QtXf qtx_delta_times(const QtXf *o) {
+    const double d = 1.0 / 65536;
+    QtXf r = {1, 0, 0, 1, 0, 0, QTX_NONE};
+    const int type = o->type > QTX_TRANSLATE ? o->type : QTX_TRANSLATE;
+    if (type == QTX_TRANSLATE) {
+        r.dx = d + o->dx; r.dy = d + o->dy;
+    } else if (type == QTX_SCALE) {
+        r.m11 = 1 * o->m11; r.m22 = 1 * o->m22;
+        r.dx = d * o->m11 + o->dx; r.dy = d * o->m22 + o->dy;
+    } else {
+        r.m11 = 1 * o->m11 + 0 * o->m21; r.m12 = 1 * o->m12 + 0 * o->m22;
+        r.m21 = 0 * o->m11 + 1 * o->m21; r.m22 = 0 * o->m12 + 1 * o->m22;
+        r.dx = d * o->m11 + d * o->m21 + o->dx; r.dy = d * o->m12 + d * o->m22 + o->dy;
+    }
+    r.type = qtx_classify(&r);
+    return r;
+}
+static QtXf qtx_inverted(const QtXf *t) {
+    QtXf r = {1, 0, 0, 1, 0, 0, QTX_NONE};
+    switch (t->type) {
+    case QTX_NONE: break;
+    case QTX_TRANSLATE: r.dx = -t->dx; r.dy = -t->dy; break;
+    case QTX_SCALE:
+        r.m11 = 1. / t->m11; r.m22 = 1. / t->m22;
+        r.dx = -t->dx * r.m11; r.dy = -t->dy * r.m22;
+        break;
+    default: { /* QMatrix::inverted */
+        const double dtr = t->m11 * t->m22 - t->m12 * t->m21, dinv = 1.0 / dtr;
+        r.m11 = t->m22 * dinv; r.m12 = -t->m12 * dinv; r.m21 = -t->m21 * dinv; r.m22 = t->m11 * dinv;
+        r.dx = (t->m21 * t->dy - t->m22 * t->dx) * dinv; r.dy = (t->m12 * t->dx - t->m11 * t->dy) * dinv;
+        break;
+    }
+    }
+    r.type = qtx_classify(&r);
+    return r;
+}
+static void qtx_map(const QtXf *t, double x, double y, double *nx, double *ny) {
+    switch (t->type) {
+    case QTX_NONE: *nx = x; *ny = y; break;
+    case QTX_TRANSLATE: *nx = x + t->dx; *ny = y + t->dy; break;
+    case QTX_SCALE: *nx = t->m11 * x + t->dx; *ny = t->m22 * y + t->dy; break;
+    default: *nx = t->m11 * x + t->m21 * y + t->dx; *ny = t->m12 * x + t->m22 * y + t->dy; break;
+    }
+}
+
+/* fetchTransformedBilinearARGB32PM's floating-point path (an affine matrix outside fast_matrix) */
+static void qt_fetch_bilinear_float(uint32_t *out, int x, int y, int len, const uint32_t *px, int iw, int ih, bool mirrored,
+                                    const QtXf *m) {
+#define QT_TEX(r, c) px[(size_t)(r) * iw + (mirrored ? iw - 1 - (c) : (c))]
+    const double cx = x + 0.5, cy = y + 0.5;
+    double fx = m->m21 * cy + m->m11 * cx + m->dx, fy = m->m22 * cy + m->m12 * cx + m->dy;
+    double fw = 0 * cy + 0 * cx + 1;
+    for (int n = 0; n < len; n++) {
+        const double iwv = fw == 0 ? 1 : 1 / fw;
+        const double pxv = fx * iwv - 0.5, pyv = fy * iwv - 0.5;
+        int x1 = (int)pxv - (pxv < 0), x2, y1 = (int)pyv - (pyv < 0), y2;
+        const int distx = (int)((pxv - x1) * 256), disty = (int)((pyv - y1) * 256);
+        if (x1 < 0) x1 = x2 = 0;
+        else if (x1 >= iw - 1) x1 = x2 = iw - 1;
+        else x2 = x1 + 1;
+        if (y1 < 0) y1 = y2 = 0;
+        else if (y1 >= ih - 1) y1 = y2 = ih - 1;
+        else y2 = y1 + 1;
+        out[n] = qt_interp4_8(QT_TEX(y1, x1), QT_TEX(y1, x2), QT_TEX(y2, x1), QT_TEX(y2, x2), (uint32_t)distx, (uint32_t)disty);
+        fx += m->m11;
+        fy += m->m12;
+        fw += 0;
+        if (!fw) fw += 0;
+    }
+#undef QT_TEX
+}
+
+/* QPainter::translate(tx, ty); rotate(deg); drawImage(QRectF(rx, ry, w, h), img) under Antialiasing +
+ * SmoothPixmapTransform (basic-abstract-game.cpp:908-916 at RENDER_RES): QRasterPaintEngine::drawImage's
+ * transformed branch -- the rect's mid line mapped by the matrix and rasterised with width h / w
+ * (tx_noshear), filled with the bilinear texture of the inverse of translate(1/65536) * (matrix *
+ * translate(rx, ry) * scale(w / iw, h / ih)) */
+static void qt_smooth_draw_image_rot(double x, double y, double w, double h, double deg, const uint32_t *px, int iw,
+                                     int ih, int fmt, bool mirrored, double opacity) {
+    if (iw <= 0 || ih <= 0 || w <= 0 || h <= 0) return;
+    qt_log10(2, x, y, w, h, (double)(uintptr_t)px, iw * 65536.0 + ih, fmt * 2 + (mirrored ? 1 : 0), opacity, deg);
+    const double tx = x + w / 2, ty = y + h / 2, rx = -w / 2, ry = -h / 2;
+    const int ca = qt_int_opacity(opacity);
+    if (fmt == QFMT_RGB32 && ca != 256) fatal_msg("rgb_array: translucent RGB32 image");
+    const QtXform r0 = qt_translate_rotate(tx, ty, deg);
+    QtXf m = {r0.m11, r0.m12, r0.m21, r0.m22, r0.dx, r0.dy, 0};
+    m.type = qtx_classify(&m);
+    double ax, ay, bx, by;
+    qtx_map(&m, (rx + rx) * 0.5f, (ry + (ry + h)) * 0.5f, &ax, &ay);
+    qtx_map(&m, ((rx + w) + (rx + w)) * 0.5f, (ry + (ry + h)) * 0.5f, &bx, &by);
+    QtXf copy = m;
+    qtx_translate(&copy, rx, ry);
+    qtx_scale(&copy, w / iw, h / ih);
+    const QtXf dm = qtx_delta_times(&copy);
+    const QtXf inv = qtx_inverted(&dm);
+    /* QSpanData::setupMatrix: fixed-point stepping only while it cannot overflow */
+    const bool fast = inv.m11 * inv.m11 + inv.m21 * inv.m21 < 1e4 && inv.m12 * inv.m12 + inv.m22 * inv.m22 < 1e4 &&
+                      fabs(inv.dx) < 1e4 && fabs(inv.dy) < 1e4;
+    static QtSpan spans[8192];
+    static uint32_t src[4096];
+    const int ns = qt_aa_line_spans(ax, ay, bx, by, h / w, RT.w, RT.h, spans, 8192);
+    for (int i = 0; i < ns;) {
+        const int x0 = spans[i].x, yy = spans[i].y;
+        int j = i, right = x0 + spans[i].len;
+        while (j + 1 < ns && (j + 1) % QT_SPANBUF != 0 && spans[j + 1].y == yy && spans[j + 1].x == right) right += spans[++j].len;
+        if (fast) qt_fetch_bilinear_x(src, x0, yy, right - x0, px, iw, ih, mirrored, inv.m11, inv.m12, inv.m21, inv.m22, inv.dx, inv.dy);
+        else qt_fetch_bilinear_float(src, x0, yy, right - x0, px, iw, ih, mirrored, &inv);
+        for (int k = i; k <= j; k++) {
+            const int cov = (spans[k].cov * ca) >> 8;
+            uint32_t *row = RT.px + (size_t)yy * RT.w;
+            for (int xx = spans[k].x; xx < spans[k].x + spans[k].len; xx++) {
+                uint32_t s = src[xx - x0], *dp = &row[xx];
+                if (fmt == QFMT_RGB32) {
+                    *dp = cov == 255 ? s : INTERPOLATE_PIXEL_255(s, (uint32_t)cov, *dp, 255 - (uint32_t)cov);
+                } else if (cov == 255) {
                     if (s >= 0xff000000u) *dp = s;
                     else if (s != 0) *dp = s + BYTE_MUL(*dp, (~s) >> 24);
                 } else {
@@ -5958,16 +6361,17 @@ static void jp_draw_compass(Game *g, const or_atlas *at) {
 
 static void render(Game *g, const or_atlas *at) { /* game.cpp:97-107 -> game_draw, :1018-1021 */
     if (g->game_id == GAME_STARPILOT) { /* starpilot.cpp:107-124: scrolling tiled background */
-        if (RT.smooth) fatal_msg("render_mode=rgb_array: starpilot is not restated");
-        float scale = (float)(RES_H / g->main_height); /* int / int */
-        qt_fill_rect_int(g->canvas, 0, 0, RES_W, RES_H, 0xff000000u);
+        /* `rect` is the render target's: 64 x 64, or RENDER_RES for render_mode="rgb_array" */
+        const int rw = RT.smooth ? RT.w : RES_W, rh = RT.smooth ? RT.h : RES_H;
+        float scale = (float)(rh / g->main_height); /* int / int */
+        qt_fill_rect_int(g->canvas, 0, 0, rw, rh, 0xff000000u);
         if (g->options.use_backgrounds) {
             float bg_k = 3;
             float t = (float)g->cur_time;
             float x_off = -t * scale * g->sp_hp_slow_v * 2 / g->char_dim;
             const float BG_RATIO = 18;
-            RectD r_bg = {(double)x_off, (double)(-RES_H * (bg_k - 1) / 2), (double)(RES_H * bg_k * BG_RATIO),
-                          (double)(RES_H * bg_k)};
+            RectD r_bg = {(double)x_off, (double)(-rh * (bg_k - 1) / 2), (double)(rh * bg_k * BG_RATIO),
+                          (double)(rh * bg_k)};
             const or_image *bg = &at->backgrounds[g->background_index];
             tile_image_fmt(g, g->gen_bg ? g->gen_bg : at->pixels + bg->offset, bg->w, bg->h, QFMT_RGB32, false, 1.0, r_bg, 1);
         }
@@ -6239,11 +6643,6 @@ int oracle_render_rgb_array(void *h, uint8_t *rgb, int res, double *log, int cap
     int rc = 0;
     for (int n = 0; n < v->count && rc == 0; n++) {
         Game *g = &v->games[n];
-        switch (g->game_id) {
-        case GAME_BIGFISH: case GAME_CHASER: case GAME_CLIMBER: case GAME_COINRUN: case GAME_MAZE: case GAME_MINER:
-        case GAME_NINJA: break;
-        default: rc = -1; continue;
-        }
         Game saved = *g;
         RT.px = frame; RT.w = res; RT.h = res; RT.smooth = true;
         RT.log = n == 0 ? log : NULL; RT.log_n = 0; RT.log_cap = cap;
@@ -6456,13 +6855,25 @@ static double rd_f64(Rd *r) {
 /* one Antialiasing + SmoothPixmapTransform primitive on a cw x ch RGB32 canvas (tests/test_smooth_pins.py,
  * against tools/qt_smooth_probe.cpp on the real Qt): kind 0 drawImage(QRectF, img [mirrored]) with
  * opacity, kind 1 fillRect(QRectF, opaque colour) */
+static double rot_deg;
+void oracle_qt_smooth_rot(int cw, int ch, uint32_t *inout, const uint32_t *img, int iw, int ih, int fmt, int mirrored,
+                          double x, double y, double w, double h, double deg, double opacity);
 void oracle_qt_smooth(int cw, int ch, uint32_t *inout, int kind, const uint32_t *img, int iw, int ih, int fmt,
                       int mirrored, double x, double y, double w, double h, double opacity, uint32_t argb) {
     QtTarget saved = RT;
     RT.px = inout; RT.w = cw; RT.h = ch; RT.smooth = true; RT.log = NULL;
     if (kind == 0) qt_draw_image(inout, x, y, w, h, img, iw, ih, fmt, mirrored != 0, opacity);
+    else if (kind == 2) /* translate(x + w/2, y + h/2); rotate(degrees = argb as float bits); drawImage(-w/2, -h/2, w, h) */
+        qt_smooth_draw_image_rot(x, y, w, h, rot_deg, img, iw, ih, fmt, mirrored != 0, opacity);
     else qt_fill_rectf(inout, x, y, w, h, argb);
     RT = saved;
+}
+
+/* kind 2 of tools/qt_smooth_probe.cpp: translate(x + w/2, y + h/2); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)) */
+void oracle_qt_smooth_rot(int cw, int ch, uint32_t *inout, const uint32_t *img, int iw, int ih, int fmt, int mirrored,
+                          double x, double y, double w, double h, double deg, double opacity) {
+    rot_deg = deg;
+    oracle_qt_smooth(cw, ch, inout, 2, img, iw, ih, fmt, mirrored, x, y, w, h, opacity, 0);
 }
 
 /* qt-utils.h / grid.h pins (tests/test_oracle_pins.py, against the reference headers compiled in

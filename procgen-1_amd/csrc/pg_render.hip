@@ -2110,6 +2110,64 @@ DEV uint32_t hr_interp_255(uint32_t x, uint32_t a, uint32_t y, uint32_t b) {
     return x | t;
 }
 
+// n range [lo, hi] (clipped to [0, len)) with 0 <= f0 + n * d <= top
+DEV void hr_nrange(int f0, int d, int64_t top, int len, int64_t &lo, int64_t &hi) {
+    lo = 0;
+    hi = (int64_t)len - 1;
+    const int64_t L = -(int64_t)f0, H = top - f0; // n d in [L, H]
+    if (d > 0) {
+        lo = max(lo, L >= 0 ? (L + d - 1) / d : -((-L) / d));
+        hi = min(hi, H >= 0 ? H / d : -((-H + d - 1) / d));
+    } else if (d < 0) {
+        const int64_t e = -(int64_t)d, a = -H, b = -L; // n e in [a, b]
+        lo = max(lo, a >= 0 ? (a + e - 1) / e : -((-a) / e));
+        hi = min(hi, b >= 0 ? b / e : -((-b + e - 1) / e));
+    } else if (!(L <= 0 && 0 <= H)) {
+        lo = hi + 1;
+    }
+}
+// the scale helpers of fetchTransformedBilinearARGB32PM (fdy == 0): pixel n of a run of `len`
+struct HTex { const uint32_t *px; int iw, ih, mir; };
+DEV uint32_t hr_tex(const HTex &T, int r, int c) { return T.px[(size_t)r * T.iw + (T.mir ? T.iw - 1 - c : c)]; }
+DEV uint32_t hr_fetch_scale(const HTex &T, int fx0, int fy, int fdx, double m22, int len, int n) {
+    int y1 = fy >> 16, y2;
+    if (y1 < 0) y1 = y2 = 0;
+    else if (y1 >= T.ih - 1) y1 = y2 = T.ih - 1;
+    else y2 = y1 + 1;
+    const uint32_t dy8 = (uint32_t)(fy & 0xffff) >> 8, dy4 = (dy8 + 8) >> 4;
+    const bool down = !(fdx > 0 && fdx <= 65536) && !(fdx < 0 && fdx > -8192) && !(fabs(m22) < 1. / 8.);
+    // leading pixels on a clamped column (vertical interpolation only) end at the first n whose column
+    // is inside [0, iw - 1)
+    int n0 = len;
+    {
+        int64_t lo, hi;
+        hr_nrange(fx0, fdx, (int64_t)(T.iw - 1) * 65536 - 1, len, lo, hi);
+        if (lo <= hi) n0 = (int)lo;
+    }
+    int64_t bend = len;
+    const int fxn0 = fx0 + n0 * fdx;
+    if (n0 < len) {
+        if (fdx > 0) bend = min(bend, (int64_t)n0 + ((int64_t)(T.iw - 1) * 65536 - fxn0) / fdx);
+        else if (fdx < 0) bend = min(bend, (int64_t)n0 + (0 - (int64_t)fxn0) / fdx);
+    }
+    const int64_t groups = (down && bend - n0 >= 4) ? (bend - n0) / 4 : 0;
+    const int fx = fx0 + n * fdx;
+    if (n < n0) {
+        const int c = (fx >> 16) < 0 ? 0 : T.iw - 1;
+        return hr_interp_256(hr_tex(T, y1, c), 256 - dy8, hr_tex(T, y2, c), dy8);
+    }
+    if (n < n0 + 4 * groups) {
+        const int c = fx >> 16;
+        const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4;
+        return hr_interp4_4(hr_tex(T, y1, c), hr_tex(T, y1, c + 1), hr_tex(T, y2, c), hr_tex(T, y2, c + 1), dx4, dy4);
+    }
+    int c1 = fx >> 16, c2;
+    if (c1 < 0) c1 = c2 = 0;
+    else if (c1 >= T.iw - 1) c1 = c2 = T.iw - 1;
+    else c2 = c1 + 1;
+    return hr_interp4_8(hr_tex(T, y1, c1), hr_tex(T, y1, c2), hr_tex(T, y2, c1), hr_tex(T, y2, c2),
+                        (uint32_t)(fx & 0xffff) >> 8, dy8);
+}
 // one primitive (uniform arguments); all threads of the workgroup
 struct HOp {
     int kind;              // 0 image, 1 opaque fill
@@ -2163,13 +2221,12 @@ DEV void hr_paint(uint32_t *frame, const HOp &op) {
     // drawImage: inverse of (translate(1/65536) * QTransform(sx, 0, 0, sy, x, y)) (QSpanData::setupMatrix)
     double m11 = 0, m22 = 0, mdx = 0, mdy = 0;
     int fdx = 0;
-    bool down = false;
+    const HTex T = {op.px, op.iw, op.ih, op.mir};
     if (op.kind == 0) {
         const double sxs = w / op.iw, sys = h / op.ih;
         const double tdx = (1.0 / 65536) * sxs + x, tdy = (1.0 / 65536) * sys + y;
         m11 = 1. / sxs; m22 = 1. / sys; mdx = -tdx * m11; mdy = -tdy * m22;
         fdx = (int)(m11 * 65536);
-        down = !(abs(fdx) <= 65536) && !(fabs(m22) < 1. / 8.);
     }
     for (int p = tid; p < tot; p += HR_THREADS) {
         const int r = R.r0 + p / cw, xx = x0 + p % cw;
@@ -2211,52 +2268,532 @@ DEV void hr_paint(uint32_t *frame, const HOp &op) {
         const double cy = r + 0.5;
         const int fx0 = (int)((0.0 * cy + m11 * (seg_s + 0.5) + mdx) * 65536) - 32768;
         const int fy = (int)((m22 * cy + 0.0 * (seg_s + 0.5) + mdy) * 65536) - 32768;
-        int y1 = fy >> 16, y2;
-        if (y1 < 0) y1 = y2 = 0;
-        else if (y1 >= op.ih - 1) y1 = y2 = op.ih - 1;
-        else y2 = y1 + 1;
-        const uint32_t dy8 = (uint32_t)(fy & 0xffff) >> 8, dy4 = (dy8 + 8) >> 4;
-        // leading clamped pixels, bounded end, 4-bit groups (fetchTransformedBilinearARGB32PM helpers)
-        int n0 = 0;
-        {
-            const int c0 = fx0 >> 16;
-            if (c0 >= op.iw - 1) {
-                n0 = len;
-            } else if (c0 < 0) {
-                n0 = (int)((-(int64_t)fx0 + fdx - 1) / fdx); // first n with fx >= 0
-                if (n0 > len) n0 = len;
-                if (n0 < len && ((fx0 + n0 * fdx) >> 16) >= op.iw - 1) n0 = len;
-            }
-        }
-        const int fxn0 = fx0 + n0 * fdx;
-        int bend = len;
-        {
-            const int64_t b = n0 + ((int64_t)(op.iw - 1) * 65536 - fxn0) / fdx;
-            if (b < bend) bend = (int)b;
-        }
-        int groups = 0;
-        if (down && bend - 3 > n0) groups = (bend - 4 - n0) / 4 + 1;
-        const int fx = fx0 + n * fdx;
-        const uint32_t *row1 = op.px + (size_t)y1 * op.iw, *row2 = op.px + (size_t)y2 * op.iw;
-#define HR_TEX(rowp, c) (rowp)[op.mir ? op.iw - 1 - (c) : (c)]
-        uint32_t src;
-        if (n < n0) {
-            const int c = (fx >> 16) < 0 ? 0 : op.iw - 1;
-            src = hr_interp_256(HR_TEX(row1, c), 256 - dy8, HR_TEX(row2, c), dy8);
-        } else if (n < n0 + 4 * groups) {
-            const int c = fx >> 16;
-            const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4;
-            src = hr_interp4_4(HR_TEX(row1, c), HR_TEX(row1, c + 1), HR_TEX(row2, c), HR_TEX(row2, c + 1), dx4, dy4);
-        } else {
-            int c1 = fx >> 16, c2;
-            if (c1 < 0) c1 = c2 = 0;
-            else if (c1 >= op.iw - 1) c1 = c2 = op.iw - 1;
-            else c2 = c1 + 1;
-            const uint32_t dx8 = (uint32_t)(fx & 0xffff) >> 8;
-            src = hr_interp4_8(HR_TEX(row1, c1), HR_TEX(row1, c2), HR_TEX(row2, c1), HR_TEX(row2, c2), dx8, dy8);
-        }
-#undef HR_TEX
+        const uint32_t src = hr_fetch_scale(T, fx0, fy, fdx, m22, len, n);
         hr_blend(dp, src, (cov0 * op.ca) >> 8, op.rgb32 != 0);
+    }
+}
+
+// ---------------------------------------------------------------- rotated drawImage (render_mode="rgb_array")
+// QPainter::translate(centre); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)) (basic-abstract-game.cpp:
+// 908-916) under Antialiasing + SmoothPixmapTransform: QRasterPaintEngine::drawImage's transformed
+// branch, restated in the oracle (qt_smooth_draw_image_rot) from Qt 5.9.7's own machine code and
+// pinned there against the real library (tests/test_smooth_pins.py):
+//   * QTransform arithmetic per (fuzzy) type -- the mid line mapped, the texture matrix
+//     translate(1/65536) * (m * translate(rx, ry) * scale(w / iw, h / ih)) inverted;
+//   * QRasterizer::rasterizeLine antialiased: near-horizontal lines turned vertical (q26Dot6Compare),
+//     the vertical branch's <= 3 spans per row, else the general branch -- the rectangle's corners
+//     snapped to the 26.6 grid, four edge slopes, per row single-pixel spans at the edges
+//     (intersectPixelFP) and one full-coverage run between them;
+//   * the fetch of each run (spans merged while adjacent within a 256-span flush): the scale helpers
+//     when fdy == 0, else the rotate helpers (8-bit beyond an 8x zoom; otherwise 8-bit lead-in,
+//     4-bit groups of 4, 8-bit rest), or the floating-point path outside fast_matrix.
+// On the device the rows are independent (every accumulator of the rasterizer's row loop is an exact
+// integer recurrence, so row r's state is closed-form): threads generate the rows' spans into LDS in
+// emission order (counts, a block scan, then the spans), then every pixel of every span is fetched and
+// blended independently (a pixel's run and its place in the helpers' phases are closed-form too).
+enum { HQ_NONE = 0, HQ_TRANSLATE = 1, HQ_SCALE = 2, HQ_ROTATE = 4, HQ_SHEAR = 8 };
+struct HXf { double m11, m12, m21, m22, dx, dy; int type; };
+DEV bool hq_fz(double d) { return fabs(d) <= 0.000000000001; } // qFuzzyIsNull
+DEV int hq_classify(const HXf &t) {
+    if (!hq_fz(t.m12) || !hq_fz(t.m21)) return hq_fz(t.m11 * t.m12 + t.m21 * t.m22) ? HQ_ROTATE : HQ_SHEAR;
+    if (!hq_fz(t.m11 - 1) || !hq_fz(t.m22 - 1)) return HQ_SCALE;
+    if (!hq_fz(t.dx) || !hq_fz(t.dy)) return HQ_TRANSLATE;
+    return HQ_NONE;
+}
+DEV void hq_translate(HXf &t, double dx, double dy) {
+    if (dx == 0 && dy == 0) return;
+    if (t.type == HQ_NONE) { t.dx = dx; t.dy = dy; }
+    else if (t.type == HQ_TRANSLATE) { t.dx += dx; t.dy += dy; }
+    else if (t.type == HQ_SCALE) { t.dx += dx * t.m11; t.dy += dy * t.m22; }
+    else { t.dx += dx * t.m11 + dy * t.m21; t.dy += dy * t.m22 + dx * t.m12; }
+    t.type = hq_classify(t);
+}
+DEV void hq_scale(HXf &t, double sx, double sy) {
+    if (sx == 1 && sy == 1) return;
+    if (t.type == HQ_NONE || t.type == HQ_TRANSLATE) { t.m11 = sx; t.m22 = sy; }
+    else {
+        if (t.type != HQ_SCALE) { t.m12 *= sx; t.m21 *= sy; }
+        t.m11 *= sx; t.m22 *= sy;
+    }
+    t.type = hq_classify(t);
+}
+DEV HXf hq_delta_times(const HXf &o) { // translate(1/65536, 1/65536) * o
+    const double dd = 1.0 / 65536;
+    HXf r = {1, 0, 0, 1, 0, 0, HQ_NONE};
+    const int type = o.type > HQ_TRANSLATE ? o.type : HQ_TRANSLATE;
+    if (type == HQ_TRANSLATE) { r.dx = dd + o.dx; r.dy = dd + o.dy; }
+    else if (type == HQ_SCALE) { r.m11 = 1 * o.m11; r.m22 = 1 * o.m22; r.dx = dd * o.m11 + o.dx; r.dy = dd * o.m22 + o.dy; }
+    else {
+        r.m11 = 1 * o.m11 + 0 * o.m21; r.m12 = 1 * o.m12 + 0 * o.m22;
+        r.m21 = 0 * o.m11 + 1 * o.m21; r.m22 = 0 * o.m12 + 1 * o.m22;
+        r.dx = dd * o.m11 + dd * o.m21 + o.dx; r.dy = dd * o.m12 + dd * o.m22 + o.dy;
+    }
+    r.type = hq_classify(r);
+    return r;
+}
+DEV HXf hq_inverted(const HXf &t) {
+    HXf r = {1, 0, 0, 1, 0, 0, HQ_NONE};
+    if (t.type == HQ_TRANSLATE) { r.dx = -t.dx; r.dy = -t.dy; }
+    else if (t.type == HQ_SCALE) {
+        r.m11 = 1. / t.m11; r.m22 = 1. / t.m22; r.dx = -t.dx * r.m11; r.dy = -t.dy * r.m22;
+    } else if (t.type != HQ_NONE) { // QMatrix::inverted
+        const double dtr = t.m11 * t.m22 - t.m12 * t.m21, dinv = 1.0 / dtr;
+        r.m11 = t.m22 * dinv; r.m12 = -t.m12 * dinv; r.m21 = -t.m21 * dinv; r.m22 = t.m11 * dinv;
+        r.dx = (t.m21 * t.dy - t.m22 * t.dx) * dinv; r.dy = (t.m12 * t.dx - t.m11 * t.dy) * dinv;
+    }
+    r.type = hq_classify(r);
+    return r;
+}
+DEV void hq_map(const HXf &t, double x, double y, double &nx, double &ny) {
+    if (t.type == HQ_NONE) { nx = x; ny = y; }
+    else if (t.type == HQ_TRANSLATE) { nx = x + t.dx; ny = y + t.dy; }
+    else if (t.type == HQ_SCALE) { nx = t.m11 * x + t.dx; ny = t.m22 * y + t.dy; }
+    else { nx = t.m11 * x + t.m21 * y + t.dx; ny = t.m12 * x + t.m22 * y + t.dy; }
+}
+// QTransform().translate(tx, ty).rotate(deg) (qtransform.cpp rotate: exact 90 / 180 / 270 cases)
+DEV HXf hq_translate_rotate(double tx, double ty, double a) {
+    HXf t = {1, 0, 0, 1, tx, ty, HQ_NONE};
+    if (a != 0) {
+        double sina = 0, cosa = 0;
+        if (a == 90. || a == -270.) sina = 1;
+        else if (a == 270. || a == -90.) sina = -1;
+        else if (a == 180.) cosa = -1;
+        else pg_sincos_cr(0.017453292519943295769 * a, &sina, &cosa);
+        t.m11 = cosa; t.m12 = sina; t.m21 = -sina; t.m22 = cosa;
+    }
+    t.type = hq_classify(t);
+    return t;
+}
+
+// qrasterizer.cpp helpers (qSafeFloatToQ16Dot16, qSafeDivide, Q16Dot16Multiply, snapTo26Dot6Grid)
+DEV int hq_fp(double x) {
+    const double v = x * 65536.;
+    if (v > 2147483647.0) return 0x7fffffff;
+    if (v < -2147483648.0) return -2147483647;
+    return (int)v;
+}
+DEV double hq_sdiv(double x, double y) { return y == 0 ? (x > 0 ? 1e20 : -1e20) : x / y; }
+DEV int hq_mul(int x, int y) { return (int)(((int64_t)x * (int64_t)y) >> 16); }
+DEV int hq_wadd(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }           // the loop's wrapping +=
+DEV int hq_wmul(int r, int s) { return (int)((uint32_t)r * (uint32_t)s); }
+DEV void hq_snap(double &x, double &y) {
+    const double ny = floor(y * 64) * 0.015625, nx = floor(x * 64) * 0.015625;
+    x = nx;
+    y = ny;
+}
+DEV int hq_intersect(int x, int top, int bottom, int lix, int rix, int slope, int inv) { // intersectPixelFP
+    const int leftX = x << 16, rightX = leftX + 65536;
+    const int liy = top + hq_mul(slope > 0 ? leftX - lix : leftX - rix, inv);
+    const int riy = liy + inv;
+    if (lix >= leftX && rix <= rightX) return hq_mul(bottom - top, lix - leftX + ((rix - lix) >> 1));
+    if (lix >= rightX) return bottom - top;
+    if (lix >= leftX) return (bottom - top) - ((((rightX - lix) >> 1) * (slope > 0 ? riy - top : bottom - riy)) >> 16);
+    if (rix <= leftX) return 0;
+    if (rix <= rightX) return (((rix - leftX) >> 1) * (slope > 0 ? bottom - liy : liy - top)) >> 16;
+    if (slope > 0) return (bottom - riy) + ((riy - liy) >> 1);
+    return (riy - top) + ((liy - riy) >> 1);
+}
+
+// rasterizeLine(a, b, width) set up (uniform): kind 0 nothing, 1 vertical (HRect), 2 general
+struct HLine {
+    int kind;
+    HRect V;
+    int nrows, iTopFP, iLeftFP, iRightFP, iBottomFP, yLeftFP, yRightFP, yBottomFP, rowTop0;
+    int leftAf0, rightAf0, leftBf0, rightBf0, leftBfL, rightBfR, tlAf0, trAf0;
+    int tlS, trS, blS, brS, itlS, itrS, iblS, ibrS;
+};
+DEV void hr_line(double ax, double ay, double bx, double by, double width, HLine &L) {
+    L.kind = 0;
+    L.V.n = 0;
+    double pax = ax, pay = ay, pbx = bx, pby = by;
+    if ((hq_fz(ax - bx) && hq_fz(ay - by)) || width == 0) return;
+    {
+        const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
+        const double cl = 0 - offx, ct = 0 - offy;
+        const double cr = cl + ((HR_RES - 1 + 1 + offx) - cl), cb = ct + ((HR_RES - 1 + 1 + offy) - ct);
+        const bool in_a = cl <= pax && pax <= cr && ct <= pay && pay <= cb;
+        const bool in_b = cl <= pbx && pbx <= cr && ct <= pby && pby <= cb;
+        if (!in_a || !in_b) {
+            double t1 = 0, t2 = 1;
+            const double o[2] = {pax, pay}, dd[2] = {pbx - pax, pby - pay};
+            const double low[2] = {cl, ct}, high[2] = {cr, cb};
+            for (int i = 0; i < 2; i++) {
+                if (dd[i] == 0) {
+                    if (o[i] <= low[i] || o[i] >= high[i]) return;
+                    continue;
+                }
+                const double dinv = 1 / dd[i];
+                double tl = (low[i] - o[i]) * dinv, th = (high[i] - o[i]) * dinv;
+                if (tl > th) { const double t = tl; tl = th; th = t; }
+                if (t1 < tl) t1 = tl;
+                if (t2 > th) t2 = th;
+                if (t1 >= t2) return;
+            }
+            const double nax = pax + (pbx - pax) * t1, nay = pay + (pby - pay) * t1;
+            const double nbx = pax + (pbx - pax) * t2, nby = pay + (pby - pay) * t2;
+            pax = nax; pay = nay; pbx = nbx; pby = nby;
+        }
+    }
+    {
+        const double d0x = ax - bx, d0y = ay - by, w0 = d0x * d0x + d0y * d0y;
+        const double dx = pax - pbx, dy = pay - pby, ww = dx * dx + dy * dy;
+        if (ww == 0) return;
+        width *= sqrt(w0 / ww);
+    }
+    if ((int)((pby - pay) * 64.) == 0) { // horizontal -> vertical
+        const double xm = (pax + pbx) * 0.5f, dx = fabs(pbx - pax) * 0.5f, yy = pay, dy = width * dx;
+        pax = xm; pay = yy - dy;
+        pbx = xm; pby = yy + dy;
+        width = 1 / width;
+    }
+    if ((int)((pbx - pax) * 64.) == 0) { // vertical: <= 3 spans per row (hr_rect's tail)
+        if (pay > pby) {
+            double t = pay; pay = pby; pby = t;
+            t = pax; pax = pbx; pbx = t;
+        }
+        HRect &R = L.V;
+        const double dy = pby - pay, half = 0.5f * width * dy;
+        double left = pax - half, right = pax + half;
+        left = left < 0 ? 0 : (left > HR_RES ? HR_RES : left);
+        right = right < 0 ? 0 : (right > HR_RES ? HR_RES : right);
+        pay = pay < 0 ? 0 : (pay > HR_RES ? HR_RES : pay);
+        pby = pby < 0 ? 0 : (pby > HR_RES ? HR_RES : pby);
+        if ((int)(left * 64) == (int)(right * 64) || (int)(pay * 64) == (int)(pby * 64)) return;
+        const int iL = (int)left, iR = (int)right;
+        const int lw = ((iL + 1) << 16) - (int)(left * 65536.), rw = (int)(right * 65536.) - (iR << 16);
+        int n = 1;
+        if (iL == iR) {
+            R.cov[0] = lw + rw; R.xs[0] = iL; R.lens[0] = 1;
+        } else {
+            R.cov[0] = lw; R.xs[0] = iL; R.lens[0] = 1;
+            if (lw == 65536) R.lens[0] = iR - iL;
+            else if (iR - iL > 1) { R.cov[1] = 65536; R.xs[1] = iL + 1; R.lens[1] = iR - iL - 1; n++; }
+            if (rw) { R.cov[n] = rw; R.xs[n] = iR; R.lens[n] = 1; n++; }
+        }
+        R.n = n;
+        R.r0 = (int)pay;
+        R.r1 = min((int)pby, HR_RES - 1);
+        R.yPa = (int)(pay * 65536.);
+        R.yPb = (int)(pby * 65536.);
+        L.kind = R.r1 >= R.r0 ? 1 : 0;
+        L.nrows = R.r1 - R.r0 + 1;
+        return;
+    }
+    // general branch
+    if (pay > pby) {
+        double t = pax; pax = pbx; pbx = t;
+        t = pay; pay = pby; pby = t;
+    }
+    const double hw = 0.5f * width;
+    const double dlx = (pbx - pax) * hw, dly = (pby - pay) * hw;
+    const double prx = dly, pry = -dlx;
+    double tx, ty, lx, ly, rx, ry, qx, qy; // top, left, right, bottom corners
+    if (pax < pbx) {
+        tx = pax + prx; ty = pay + pry; lx = pax - prx; ly = pay - pry;
+        rx = pbx + prx; ry = pby + pry; qx = pbx - prx; qy = pby - pry;
+    } else {
+        tx = pax - prx; ty = pay - pry; lx = pbx - prx; ly = pby - pry;
+        rx = pax + prx; ry = pay + pry; qx = pbx + prx; qy = pby + pry;
+    }
+    hq_snap(tx, ty);
+    hq_snap(qx, qy);
+    hq_snap(lx, ly);
+    hq_snap(rx, ry);
+    const double topBound = ty < 0 ? 0 : (ty > HR_RES - 1 ? HR_RES - 1 : ty);
+    const double bottomBound = qy < 0 ? 0 : (qy > HR_RES - 1 ? HR_RES - 1 : qy);
+    const double tlI = hq_sdiv(lx - tx, ly - ty), blI = hq_sdiv(qx - lx, qy - ly);
+    const double trI = hq_sdiv(rx - tx, ry - ty), brI = hq_sdiv(qx - rx, qy - ry);
+    L.tlS = hq_fp(tlI); L.trS = hq_fp(trI); L.blS = hq_fp(blI); L.brS = hq_fp(brI);
+    L.itlS = hq_fp(hq_sdiv(1, tlI)); L.itrS = hq_fp(hq_sdiv(1, trI));
+    L.iblS = hq_fp(hq_sdiv(1, blI)); L.ibrS = hq_fp(hq_sdiv(1, brI));
+    const int iTop = (int)topBound;
+    L.iTopFP = iTop << 16;
+    L.iLeftFP = ((int)ly) << 16;
+    L.iRightFP = ((int)ry) << 16;
+    L.iBottomFP = ((int)bottomBound) << 16;
+    L.leftAf0 = hq_fp(tx + (iTop - ty) * tlI);
+    L.rightAf0 = hq_fp(tx + (iTop - ty) * trI);
+    L.leftBf0 = L.iLeftFP < L.iTopFP ? hq_fp(lx + (iTop - ly) * blI) : 0;
+    L.rightBf0 = L.iRightFP < L.iTopFP ? hq_fp(rx + (iTop - ry) * brI) : 0;
+    L.leftBfL = hq_fp(lx + ((L.iLeftFP >> 16) - ly) * blI);
+    L.rightBfR = hq_fp(rx + ((L.iRightFP >> 16) - ry) * brI);
+    const int yTopFP = hq_fp(ty);
+    L.yLeftFP = hq_fp(ly);
+    L.yRightFP = hq_fp(ry);
+    L.yBottomFP = hq_fp(qy);
+    L.rowTop0 = L.iTopFP > yTopFP ? L.iTopFP : yTopFP;
+    L.tlAf0 = L.leftAf0 + hq_mul(L.tlS, L.rowTop0 - L.iTopFP);
+    L.trAf0 = L.rightAf0 + hq_mul(L.trS, L.rowTop0 - L.iTopFP);
+    if (L.iBottomFP < L.iTopFP) return;
+    L.nrows = ((L.iBottomFP - L.iTopFP) >> 16) + 1;
+    L.kind = 2;
+}
+
+// the spans of row r (emission order) of a general line: fills up to `cap` (x, len, cov) and returns
+// how many are emitted (nonzero coverage and length); with out == nullptr it only counts
+struct HRow {
+    int yFP, yi, rowTop, rowBottom, rowBottomLeft, rowBottomRight, rowTopLeft, rowTopRight;
+    int tlAf, trAf, tlBf, blAf, trBf, brAf, blBf, brBf;
+    int leftMin, leftMax, rightMin, rightMax;
+};
+DEV void hr_row_setup(const HLine &L, int r, HRow &w) {
+    const int yFP = hq_wadd(L.iTopFP, r << 16);
+    w.yFP = yFP;
+    w.yi = yFP >> 16;
+    const int leftAf = hq_wadd(L.leftAf0, hq_wmul(r, L.tlS)), rightAf = hq_wadd(L.rightAf0, hq_wmul(r, L.trS));
+    const int rowL = (L.iLeftFP - L.iTopFP) >> 16, rowR = (L.iRightFP - L.iTopFP) >> 16;
+    int leftBf, rightBf;
+    if (L.iLeftFP < L.iTopFP || r < rowL) leftBf = hq_wadd(L.leftBf0, hq_wmul(r, L.blS));
+    else leftBf = hq_wadd(L.leftBfL, hq_wmul(r - rowL, L.blS));
+    if (L.iRightFP < L.iTopFP || r < rowR) rightBf = hq_wadd(L.rightBf0, hq_wmul(r, L.brS));
+    else rightBf = hq_wadd(L.rightBfR, hq_wmul(r - rowR, L.brS));
+    w.rowTop = r == 0 ? L.rowTop0 : yFP;
+    w.tlAf = r == 0 ? L.tlAf0 : leftAf;
+    w.trAf = r == 0 ? L.trAf0 : rightAf;
+    w.rowBottomLeft = min(yFP + 65536, L.yLeftFP);
+    w.rowBottomRight = min(yFP + 65536, L.yRightFP);
+    w.rowTopLeft = max(yFP, L.yLeftFP);
+    w.rowTopRight = max(yFP, L.yRightFP);
+    w.rowBottom = min(yFP + 65536, L.yBottomFP);
+    if (yFP == L.iLeftFP) {
+        w.tlBf = leftBf + hq_mul(L.blS, w.rowTopLeft - yFP);
+        w.blAf = leftAf + hq_mul(L.tlS, w.rowBottomLeft - yFP);
+    } else {
+        w.tlBf = leftBf;
+        w.blAf = leftAf + L.tlS;
+    }
+    if (yFP == L.iRightFP) {
+        w.trBf = rightBf + hq_mul(L.brS, w.rowTopRight - yFP);
+        w.brAf = rightAf + hq_mul(L.trS, w.rowBottomRight - yFP);
+    } else {
+        w.trBf = rightBf;
+        w.brAf = rightAf + L.trS;
+    }
+    if (yFP == L.iBottomFP) {
+        w.blBf = leftBf + hq_mul(L.blS, w.rowBottom - yFP);
+        w.brBf = rightBf + hq_mul(L.brS, w.rowBottom - yFP);
+    } else {
+        w.blBf = leftBf + L.blS;
+        w.brBf = rightBf + L.brS;
+    }
+    if (yFP < L.iLeftFP) { w.leftMin = w.blAf >> 16; w.leftMax = w.tlAf >> 16; }
+    else if (yFP == L.iLeftFP) { w.leftMin = max(w.blAf, w.tlBf) >> 16; w.leftMax = max(w.tlAf, w.blBf) >> 16; }
+    else { w.leftMin = w.tlBf >> 16; w.leftMax = w.blBf >> 16; }
+    w.leftMin = min(max(w.leftMin, 0), HR_RES - 1);
+    w.leftMax = min(max(w.leftMax, 0), HR_RES - 1);
+    if (yFP < L.iRightFP) { w.rightMin = w.trAf >> 16; w.rightMax = w.brAf >> 16; }
+    else if (yFP == L.iRightFP) { w.rightMin = min(w.trAf, w.brBf) >> 16; w.rightMax = min(w.brAf, w.trBf) >> 16; }
+    else { w.rightMin = w.brBf >> 16; w.rightMax = w.trBf >> 16; }
+    w.rightMin = min(max(w.rightMin, 0), HR_RES - 1);
+    w.rightMax = min(max(w.rightMax, 0), HR_RES - 1);
+    if (w.leftMax > w.rightMax) w.leftMax = w.rightMax;
+    if (w.rightMin < w.leftMin) w.rightMin = w.leftMin;
+}
+DEV int hr_row_cov(const HLine &L, const HRow &w, int x, bool left_part) {
+    int ex = 0;
+    if (left_part) {
+        if (w.yFP <= L.iLeftFP) ex += hq_intersect(x, w.rowTop, w.rowBottomLeft, w.blAf, w.tlAf, L.tlS, L.itlS);
+        if (w.yFP >= L.iLeftFP) ex += hq_intersect(x, w.rowTopLeft, w.rowBottom, w.tlBf, w.blBf, L.blS, L.iblS);
+    }
+    if (!left_part || x >= w.rightMin) {
+        if (w.yFP <= L.iRightFP)
+            ex += (w.rowBottomRight - w.rowTop) - hq_intersect(x, w.rowTop, w.rowBottomRight, w.trAf, w.brAf, L.trS, L.itrS);
+        if (w.yFP >= L.iRightFP)
+            ex += (w.rowBottom - w.rowTopRight) - hq_intersect(x, w.rowTopRight, w.rowBottom, w.brBf, w.trBf, L.brS, L.ibrS);
+    }
+    return ((255 * (w.rowBottom - w.rowTop - ex)) >> 16) & 0xff;
+}
+// emits row r's spans (emission order) through emit(x, len, y, cov); returns the count
+template <class F>
+DEV int hr_row_spans(const HLine &L, int r, F emit) {
+    int k = 0;
+    if (L.kind == 1) {
+        const HRect &R = L.V;
+        const int rr = R.r0 + r;
+        for (int i = 0; i < R.n; i++) {
+            const int c = hr_span_cov(R, rr, i);
+            if (c && R.lens[i]) { emit(R.xs[i], R.lens[i], rr, c); k++; }
+        }
+        return k;
+    }
+    HRow w;
+    hr_row_setup(L, r, w);
+    int x = w.leftMin;
+    for (; x <= w.leftMax; x++) {
+        const int c = hr_row_cov(L, w, x, true);
+        if (c) { emit(x, 1, w.yi, c); k++; }
+    }
+    if (x < w.rightMin) {
+        const int c = ((255 * (w.rowBottom - w.rowTop)) >> 16) & 0xff;
+        if (c) { emit(x, w.rightMin - x, w.yi, c); k++; }
+        x = w.rightMin;
+    }
+    for (; x <= w.rightMax; x++) {
+        const int c = hr_row_cov(L, w, x, false);
+        if (c) { emit(x, 1, w.yi, c); k++; }
+    }
+    return k;
+}
+
+#define HR_SPAN_CAP 4096
+struct HSpanLds { // one chunk of rows' spans (runs never cross rows, so chunks end on row boundaries)
+    int16_t x[HR_SPAN_CAP], y[HR_SPAN_CAP], len[HR_SPAN_CAP];
+    uint8_t cov[HR_SPAN_CAP];
+    int pre[HR_SPAN_CAP + 1]; // pixel prefix over the chunk's spans
+};
+// exclusive block scan of v over the 256 threads (returns the prefix, *sum = the total)
+DEV int hr_scan(int v, int *tmp, int &sum) {
+    const int tid = threadIdx.x;
+    tmp[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < HR_THREADS; off <<= 1) {
+        const int a = tid >= off ? tmp[tid - off] : 0;
+        __syncthreads();
+        tmp[tid] += a;
+        __syncthreads();
+    }
+    sum = tmp[HR_THREADS - 1];
+    const int ex = tmp[tid] - v;
+    __syncthreads();
+    return ex;
+}
+
+// the rotate helpers (fdy != 0): pixel n of a run of `len`
+DEV uint32_t hr_fetch_rot(const HTex &T, int fx0, int fy0, int fdx, int fdy, bool fast, int len, int n) {
+    const int fx = fx0 + n * fdx, fy = fy0 + n * fdy;
+    bool four = false;
+    if (fast && T.iw >= 2 && T.ih >= 2) {
+        int64_t xlo, xhi, ylo, yhi;
+        hr_nrange(fx0, fdx, (int64_t)(T.iw - 1) * 65536 - 1, len, xlo, xhi);
+        hr_nrange(fy0, fdy, (int64_t)(T.ih - 1) * 65536 - 1, len, ylo, yhi);
+        const int64_t a = max(xlo, ylo), b = min(xhi, yhi);
+        if (a <= b) { // the lead-in ends at n = a; the unclamped middle is bounded by the end
+            const int64_t fxa = fx0 + a * fdx, fya = fy0 + a * fdy;
+            int64_t bend = len;
+            if (fdx > 0) bend = min(bend, a + ((int64_t)(T.iw - 1) * 65536 - fxa) / fdx);
+            else if (fdx < 0) bend = min(bend, a + (0 - fxa) / fdx);
+            if (fdy > 0) bend = min(bend, a + ((int64_t)(T.ih - 1) * 65536 - fya) / fdy);
+            else if (fdy < 0) bend = min(bend, a + (0 - fya) / fdy);
+            const int64_t groups = bend - a >= 4 ? (bend - a) / 4 : 0;
+            four = n >= a && n < a + 4 * groups;
+        }
+    }
+    if (four) {
+        const int c = fx >> 16, r = fy >> 16;
+        const uint32_t dx4 = (((uint32_t)(fx & 0xffff) >> 8) + 8) >> 4, dy4 = (((uint32_t)(fy & 0xffff) >> 8) + 8) >> 4;
+        return hr_interp4_4(hr_tex(T, r, c), hr_tex(T, r, c + 1), hr_tex(T, r + 1, c), hr_tex(T, r + 1, c + 1), dx4, dy4);
+    }
+    int x1 = fx >> 16, x2, y1 = fy >> 16, y2;
+    if (x1 < 0) x1 = x2 = 0;
+    else if (x1 >= T.iw - 1) x1 = x2 = T.iw - 1;
+    else x2 = x1 + 1;
+    if (y1 < 0) y1 = y2 = 0;
+    else if (y1 >= T.ih - 1) y1 = y2 = T.ih - 1;
+    else y2 = y1 + 1;
+    return hr_interp4_8(hr_tex(T, y1, x1), hr_tex(T, y1, x2), hr_tex(T, y2, x1), hr_tex(T, y2, x2),
+                        (uint32_t)(fx & 0xffff) >> 8, (uint32_t)(fy & 0xffff) >> 8);
+}
+// the floating-point path (outside fast_matrix): the reference steps fx, fy by repeated addition
+DEV uint32_t hr_fetch_float(const HTex &T, const HXf &m, int x0, int y, int n) {
+    const double cx = x0 + 0.5, cy = y + 0.5;
+    double fx = m.m21 * cy + m.m11 * cx + m.dx, fy = m.m22 * cy + m.m12 * cx + m.dy;
+    for (int k = 0; k < n; k++) { fx += m.m11; fy += m.m12; }
+    const double pxv = fx * 1.0 - 0.5, pyv = fy * 1.0 - 0.5;
+    int x1 = (int)pxv - (pxv < 0), x2, y1 = (int)pyv - (pyv < 0), y2;
+    const int distx = (int)((pxv - x1) * 256), disty = (int)((pyv - y1) * 256);
+    if (x1 < 0) x1 = x2 = 0;
+    else if (x1 >= T.iw - 1) x1 = x2 = T.iw - 1;
+    else x2 = x1 + 1;
+    if (y1 < 0) y1 = y2 = 0;
+    else if (y1 >= T.ih - 1) y1 = y2 = T.ih - 1;
+    else y2 = y1 + 1;
+    return hr_interp4_8(hr_tex(T, y1, x1), hr_tex(T, y1, x2), hr_tex(T, y2, x1), hr_tex(T, y2, x2), (uint32_t)distx,
+                        (uint32_t)disty);
+}
+
+// translate(x + w/2, y + h/2); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h), img) on the frame
+// (tmp: HR_THREADS + 1 ints of LDS)
+DEV void hr_draw_rotated(uint32_t *frame, HSpanLds &S, int *tmp, double x, double y, double w, double h, double deg,
+                         const HTex &T, bool rgb32, int ca) {
+    if (T.iw <= 0 || T.ih <= 0 || !(w > 0) || !(h > 0)) return;
+    const int tid = threadIdx.x;
+    const double rx = -w / 2, ry = -h / 2;
+    const HXf m = hq_translate_rotate(x + w / 2, y + h / 2, deg);
+    double ax, ay, bx, by;
+    hq_map(m, (rx + rx) * 0.5f, (ry + (ry + h)) * 0.5f, ax, ay);
+    hq_map(m, ((rx + w) + (rx + w)) * 0.5f, (ry + (ry + h)) * 0.5f, bx, by);
+    HXf copy = m;
+    hq_translate(copy, rx, ry);
+    hq_scale(copy, w / T.iw, h / T.ih);
+    const HXf inv = hq_inverted(hq_delta_times(copy));
+    const bool fastm = inv.m11 * inv.m11 + inv.m21 * inv.m21 < 1e4 && inv.m12 * inv.m12 + inv.m22 * inv.m22 < 1e4 &&
+                       fabs(inv.dx) < 1e4 && fabs(inv.dy) < 1e4;
+    HLine L;
+    hr_line(ax, ay, bx, by, h / w, L);
+    if (L.kind == 0) return;
+    const int fdx = (int)(inv.m11 * 65536), fdy = (int)(inv.m12 * 65536);
+    const bool fastrot = !(fabs(inv.m11) < 1. / 8. || fabs(inv.m22) < 1. / 8.);
+    // rows in chunks: as many of the next 256 rows as fit the LDS span list (at least one: a row has at
+    // most HR_RES spans); `base` = the global index of the chunk's first span (the 256-span flushes)
+    int base = 0;
+    for (int rs = 0; rs < L.nrows;) {
+        const int r = rs + tid;
+        const int c = r < L.nrows ? hr_row_spans(L, r, [](int, int, int, int) {}) : 0;
+        int sum;
+        const int ex = hr_scan(c, tmp, sum);
+        const bool fits = r < L.nrows && ex + c <= HR_SPAN_CAP;
+        const int nfit = __syncthreads_count(fits);
+        if (tid < nfit) {
+            int k = ex;
+            hr_row_spans(L, r, [&](int sx, int sl, int sy, int sc) {
+                S.x[k] = (int16_t)sx; S.len[k] = (int16_t)sl; S.y[k] = (int16_t)sy; S.cov[k] = (uint8_t)sc;
+                k++;
+            });
+            if (tid == nfit - 1) tmp[HR_THREADS] = ex + c;
+        }
+        __syncthreads();
+        const int nsp = tmp[HR_THREADS];
+        // pixel prefix over the chunk's spans
+        {
+            const int per = (nsp + HR_THREADS - 1) / HR_THREADS, lo = min(nsp, tid * per), hi = min(nsp, lo + per);
+            int loc = 0;
+            for (int k = lo; k < hi; k++) loc += S.len[k];
+            int tot;
+            int run = hr_scan(loc, tmp, tot);
+            for (int k = lo; k < hi; k++) { S.pre[k] = run; run += S.len[k]; }
+            if (tid == 0) S.pre[nsp] = tot;
+            __syncthreads();
+        }
+        const int P = S.pre[nsp];
+        // every pixel: its run (adjacent spans of one row within one 256-span flush), fetch, blend
+        for (int p = tid; p < P; p += HR_THREADS) {
+            int lo = 0, hi = nsp - 1; // the last span with pre <= p
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (S.pre[mid] <= p) lo = mid;
+                else hi = mid - 1;
+            }
+            const int k = lo, yy = S.y[k], xx = S.x[k] + (p - S.pre[k]);
+            int k0 = k, k1 = k;
+            while (k0 > 0 && ((base + k0) % 256) != 0 && S.y[k0 - 1] == yy && S.x[k0 - 1] + S.len[k0 - 1] == S.x[k0]) k0--;
+            while (k1 + 1 < nsp && ((base + k1 + 1) % 256) != 0 && S.y[k1 + 1] == yy && S.x[k1] + S.len[k1] == S.x[k1 + 1])
+                k1++;
+            const int x0 = S.x[k0], len = S.x[k1] + S.len[k1] - x0, n = xx - x0;
+            uint32_t src;
+            if (!fastm) {
+                src = hr_fetch_float(T, inv, x0, yy, n);
+            } else {
+                const double cx = x0 + 0.5, cy = yy + 0.5;
+                const int fx0 = (int)((inv.m21 * cy + inv.m11 * cx + inv.dx) * 65536) - 32768;
+                const int fy0 = (int)((inv.m22 * cy + inv.m12 * cx + inv.dy) * 65536) - 32768;
+                if (fdy == 0) src = hr_fetch_scale(T, fx0, fy0, fdx, inv.m22, len, n);
+                else src = hr_fetch_rot(T, fx0, fy0, fdx, fdy, fastrot, len, n);
+            }
+            hr_blend(frame + (size_t)yy * HR_RES + xx, src, ((int)S.cov[k] * ca) >> 8, rgb32);
+        }
+        __syncthreads();
+        base += nsp;
+        rs += nfit;
     }
 }
 
@@ -2265,10 +2802,52 @@ DEV void hr_run(uint32_t *frame, const HOp &op) {
     __syncthreads();
 }
 
-// draw_image (basic-abstract-game.cpp:886-922) for the rgb_array games: no rotation, no tiling
+// LDS of the rotated path (only the games with rotating entities reserve it)
+struct HRotLds {
+    HSpanLds S;
+    int tmp[HR_THREADS + 1];
+};
+template <bool ROT> struct HLds { HRotLds r; };
+template <> struct HLds<false> { int unused; };
+
+// tile_image (basic-abstract-game.cpp:849-877): num_tiles side by side (ratio > 0) or stacked (< 0)
+DEV void hr_tiles(uint32_t *frame, HOp op, float tile_ratio) {
+    const double x = op.x, y = op.y, w = op.w, h = op.h;
+    if (tile_ratio == 0) {
+        hr_run(frame, op);
+        return;
+    }
+    const bool stacked = tile_ratio < 0;
+    int num_tiles;
+    float tw, th;
+    if (stacked) {
+        tile_ratio = -1 * tile_ratio;
+        num_tiles = (int)(h / (w * tile_ratio));
+        if (num_tiles < 1) num_tiles = 1;
+        th = (float)(h / num_tiles);
+        tw = (float)w;
+    } else {
+        num_tiles = (int)(w / (h * tile_ratio));
+        if (num_tiles < 1) num_tiles = 1;
+        tw = (float)(w / num_tiles);
+        th = (float)h;
+    }
+    op.w = tw;
+    op.h = th;
+    for (int i = 0; i < num_tiles; i++) {
+        op.x = stacked ? x : x + tw * i;
+        op.y = stacked ? y + th * i : y;
+        // a tile a pixel clear of the frame rasterises to nothing (the clip in rasterizeLine)
+        if (op.x + op.w < -1 || op.x > HR_RES + 1 || op.y + op.h < -1 || op.y > HR_RES + 1) continue;
+        hr_run(frame, op);
+    }
+}
+
+// draw_image (basic-abstract-game.cpp:886-922) at RENDER_RES: tiles, rotation (:908-916)
 template <int G>
 DEV bool hr_draw_image(uint32_t *frame, const PGDev &d, const PGEnv &s, double bx, double by, double bw, double bh,
-                       bool refl, int base_type, int theme, float alpha, int player_img) {
+                       bool refl, int base_type, int theme, float alpha, int player_img, float rotation, float tile_ratio,
+                       HRotLds *L) {
     const int img = image_for_type<G>(s, base_type, player_img);
     if (img < 0) return true;
     HOp op;
@@ -2297,6 +2876,14 @@ DEV bool hr_draw_image(uint32_t *frame, const PGDev &d, const PGEnv &s, double b
             bw = bw * 1.0;
         }
     }
+    if constexpr (G == PG_GAME_LEAPER) {
+        if (img == PLAYER) { // leaper.cpp:244-250
+            bx = bx + bw * 0.0;
+            by = by + bh * -.275;
+            bw = bw * 1.0;
+            bh = bh * 1.55;
+        }
+    }
     const int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
     if (sp.y <= 0) return missing_image_ok<G>(img);
     if (!(bw > 0) || !(bh > 0)) return true; // QRectF::isEmpty
@@ -2304,18 +2891,27 @@ DEV bool hr_draw_image(uint32_t *frame, const PGDev &d, const PGEnv &s, double b
     op.kind = 0; op.x = bx; op.y = by; op.w = bw; op.h = bh;
     op.px = d.pixels + sp.x; op.iw = sp.y; op.ih = sp.z; op.mir = refl ? 1 : 0;
     op.ca = alpha != 1 ? qt_int_opacity((double)alpha) : 256;
-    hr_run(frame, op);
+    if (rotation != 0) {
+        if constexpr (has_rotation<G>()) {
+            const HTex T = {op.px, op.iw, op.ih, op.mir};
+            hr_draw_rotated(frame, L->S, L->tmp, bx, by, bw, bh, (double)(rotation * 180 / PI_F), T, false, op.ca);
+            return true;
+        }
+        return false;
+    }
+    hr_tiles(frame, op, tile_ratio);
     return true;
 }
 
 template <int G>
-DEV bool hr_entities(uint32_t *frame, const PGDev &d, const PGEnv &s, const View &v, int env, int z, int player_img) {
+DEV bool hr_entities(uint32_t *frame, const PGDev &d, const PGEnv &s, const View &v, int env, int z, int player_img,
+                     HRotLds *L) {
     bool ok = true;
     for (int i = 0; i < s.num_ents; i++) {
         if (EIr(d, F_RENDER_Z, env, i) != z) continue;
+        const int etype = EIr(d, F_TYPE, env, i);
         const int itype = EIr(d, F_IMAGE_TYPE, env, i), theme = EIr(d, F_IMAGE_THEME, env, i);
-        if (!should_draw<G>(s, EIr(d, F_TYPE, env, i), theme)) continue;
-        if (EFr(d, F_ROTATION, env, i) != 0) { ok = false; continue; }
+        if (!should_draw<G>(s, etype, theme)) continue;
         const float px_ = EFr(d, F_X, env, i), py_ = EFr(d, F_Y, env, i);
         const float prx = EFr(d, F_RX, env, i), pry = EFr(d, F_RY, env, i);
         const int flags = EIr(d, F_FLAGS, env, i);
@@ -2328,7 +2924,8 @@ DEV bool hr_entities(uint32_t *frame, const PGDev &d, const PGEnv &s, const View
             screen_rect(v, px_ - prx, py_ + pry, 2 * prx, 2 * pry, 0, rx, ry, rw, rh);
         }
         ok = hr_draw_image<G>(frame, d, s, rx, ry, rw, rh, (flags & EF_REFLECTED) != 0, itype, theme,
-                              EFr(d, F_ALPHA, env, i), player_img) && ok;
+                              EFr(d, F_ALPHA, env, i), player_img, EFr(d, F_ROTATION, env, i),
+                              tile_aspect_ratio<G>(etype, prx, pry), L) && ok;
     }
     return ok;
 }
@@ -2337,6 +2934,9 @@ template <int G>
 __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, const int32_t *env_list, uint32_t *frames,
                                                                      uint8_t *rgb) {
     const PGDev d = game_view(dg, G);
+    __shared__ HLds<has_rotation<G>()> lds;
+    HRotLds *L = nullptr;
+    if constexpr (has_rotation<G>()) L = &lds.r;
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     const int slot = blockIdx.x; // frame / rgb rows of this launch
     uint32_t *frame = frames + (size_t)slot * HR_RES * HR_RES;
@@ -2381,8 +2981,21 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
     op.kind = 1; op.x = 0; op.y = 0; op.w = HR_RES; op.h = HR_RES; op.argb = 0xff000000u;
     op.px = nullptr; op.iw = op.ih = 0; op.rgb32 = 0; op.mir = 0; op.ca = 256;
     hr_run(frame, op);
-    if (s.opt_use_backgrounds) {
-        if (s.bg_tile_ratio < 0) ok = false; // tiled backgrounds: not in the rgb_array games
+    if constexpr (G == PG_GAME_STARPILOT) {
+        // starpilot game_draw (starpilot.cpp:107-124): no draw_background; tile_image(r_bg, 1) of the
+        // background scrolled left by cur_time, r_bg in RENDER_RES units
+        if (s.opt_use_backgrounds) {
+            const float scale = (float)(HR_RES / s.main_height); // int / int
+            const float bg_k = 3, t = (float)s.cur_time, BG_RATIO = 18;
+            const float x_off = -t * scale * SP_HP_SLOW_V * 2 / s.char_dim;
+            const int4 bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
+            op.kind = 0; op.x = (double)x_off; op.y = (double)(-HR_RES * (bg_k - 1) / 2);
+            op.w = (double)(HR_RES * bg_k * BG_RATIO); op.h = (double)(HR_RES * bg_k);
+            op.px = (d.gen_bg ? d.gen_bg + (size_t)env * (500 * 500) : d.pixels + bgi.x);
+            op.iw = bgi.y; op.ih = bgi.z; op.rgb32 = 1; op.mir = 0; op.ca = 256;
+            if (op.iw > 0 && op.ih > 0) hr_tiles(frame, op, 1.0f);
+        }
+    } else if (s.opt_use_backgrounds) {
         double mx, my, mw, mh;
         screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
         const int4 bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
@@ -2394,10 +3007,15 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
         op.kind = 0; op.x = mx + mw * ax; op.y = my + mh * 0.0; op.w = mw * aw; op.h = mh * 1.0;
         op.px = (d.gen_bg ? d.gen_bg + (size_t)env * (500 * 500) : d.pixels + bgi.x);
         op.iw = bgi.y; op.ih = bgi.z; op.rgb32 = 1; op.mir = 0; op.ca = 256;
-        if (op.w > 0 && op.h > 0 && op.iw > 0 && op.ih > 0) hr_run(frame, op);
+        if (s.bg_tile_ratio < 0) { // fruitbot (fruitbot.cpp:30-40): the world rect tiled (:1003-1004)
+            op.x = mx; op.y = my; op.w = mw; op.h = mh;
+            if (op.w > 0 && op.h > 0 && op.iw > 0 && op.ih > 0) hr_tiles(frame, op, s.bg_tile_ratio);
+        } else if (op.w > 0 && op.h > 0 && op.iw > 0 && op.ih > 0) {
+            hr_run(frame, op);
+        }
     }
     // draw_foreground (:930-979)
-    if constexpr (has_z_minus1<G>()) ok = hr_entities<G>(frame, d, s, v, env, -1, player_img) && ok;
+    if constexpr (has_z_minus1<G>()) ok = hr_entities<G>(frame, d, s, v, env, -1, player_img, L) && ok;
     int low_x, high_x, low_y, high_y;
     if (s.opt_center_agent) {
         const double margin = (double)v.visibility / 2.0 + 1;
@@ -2415,11 +3033,12 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
             if (type == INVALID_OBJ) continue;
             double rx, ry, rw, rh;
             screen_rect(v, (float)x, (float)(y + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
-            ok = hr_draw_image<G>(frame, d, s, rx, ry, rw, rh, false, type, grid_theme<G>(s, type), 1.0f, player_img) && ok;
+            ok = hr_draw_image<G>(frame, d, s, rx, ry, rw, rh, false, type, grid_theme<G>(s, type), 1.0f, player_img, 0.0f,
+                                  0.0f, L) && ok;
         }
     }
-    ok = hr_entities<G>(frame, d, s, v, env, 0, player_img) && ok;
-    ok = hr_entities<G>(frame, d, s, v, env, 1, player_img) && ok;
+    ok = hr_entities<G>(frame, d, s, v, env, 0, player_img, L) && ok;
+    ok = hr_entities<G>(frame, d, s, v, env, 1, player_img, L) && ok;
     if (s.has_useful_vel_info && s.opt_paint_vel_info) { // :969-977
         const float infodim = (float)(HR_RES * .2);
         const int s1 = to_shade((float)(.5 * (double)agent_vx / (double)s.maxspeed + .5));
@@ -2433,6 +3052,18 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
         const float u = v.unit, bar_height = 3 * s.gs.nj.jump_charge;
         op.kind = 1; op.x = (double)(.25f * u); op.y = (double)((float)(v.visibility - .5 - bar_height) * u);
         op.w = (double)(.5f * u); op.h = (double)(bar_height * u); op.argb = 0xff42f587u;
+        hr_run(frame, op);
+    }
+    if constexpr (G == PG_GAME_JUMPER) // the compass (jumper.cpp:137-177): not restated at RENDER_RES
+        if (s.opt_distribution_mode != PG_MEMORY) ok = false;
+    if constexpr (G == PG_GAME_PLUNDER) { // plunder.cpp:66-77: juice and progress bars, get_abs_rect (:812-814)
+        const float u = v.unit;
+        op.kind = 1; op.x = (double)(.25f * u); op.y = (double)(.25f * u);
+        op.w = (double)(s.main_width * s.gs.pl.juice_left * u); op.h = (double)(.5f * u); op.argb = 0xff42f587u;
+        hr_run(frame, op);
+        const float prog = (float)(s.main_width * (s.gs.pl.targets_hit * 1.0 / s.gs.pl.target_quota));
+        op.x = (double)(.25f * u); op.y = (double)(.75f * u); op.w = (double)(prog * u); op.h = (double)(.5f * u);
+        op.argb = 0xfff54290u;
         hr_run(frame, op);
     }
     // bgr32_to_rgb888 (game.cpp:8-23) into info["rgb"]
@@ -2504,6 +3135,15 @@ extern "C" int pg_launch_render_hires(const PGDev *d, int game, const int32_t *e
         PG_CASE(PG_GAME_MAZE)
         PG_CASE(PG_GAME_MINER)
         PG_CASE(PG_GAME_NINJA)
+        PG_CASE(PG_GAME_BOSSFIGHT)
+        PG_CASE(PG_GAME_CAVEFLYER)
+        PG_CASE(PG_GAME_DODGEBALL)
+        PG_CASE(PG_GAME_FRUITBOT)
+        PG_CASE(PG_GAME_HEIST)
+        PG_CASE(PG_GAME_LEAPER)
+        PG_CASE(PG_GAME_PLUNDER)
+        PG_CASE(PG_GAME_STARPILOT)
+        PG_CASE(PG_GAME_JUMPER)
 #undef PG_CASE
     default: return -1;
     }

@@ -130,14 +130,14 @@ class OracleEnv:
 
     def render_rgb_array(self, res=512, log_cap=0):
         """info["rgb"] of render_mode="rgb_array" (oracle_render_rgb_array); with log_cap, also env 0's
-        painter commands (rows of 9 doubles) for replay through the real Qt."""
+        painter commands (rows of 10 doubles) for replay through the real Qt."""
         n = self.count
         rgb = np.zeros((n, res, res, 3), np.uint8)
-        log = np.full((max(log_cap, 1), 9), np.nan)
+        log = np.full((max(log_cap, 1), 10), np.nan)
         self.lib.oracle_render_rgb_array.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                      ctypes.c_int]
         rc = self.lib.oracle_render_rgb_array(self.h, rgb.ctypes.data, res, log.ctypes.data if log_cap else None,
-                                              log_cap * 9)
+                                              log_cap * 10)
         if rc != 0:
             raise ValueError("render_mode=rgb_array is not restated for this game")
         if log_cap:

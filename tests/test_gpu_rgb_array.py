@@ -11,7 +11,14 @@ from test_gpu_games import make_gpu, oracle_kw
 
 pytestmark = pytest.mark.gpu
 
-GAMES = ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja"]
+GAMES = ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja", "bossfight", "caveflyer", "dodgeball",
+         "fruitbot", "heist", "jumper", "leaper", "plunder", "starpilot"]
+ROTATING = ["bossfight", "caveflyer", "dodgeball", "fruitbot", "heist", "leaper", "plunder", "starpilot"]
+
+
+def game_kw(game):
+    # jumper draws its compass (jumper.cpp:137-177) outside memory mode: not restated at RENDER_RES
+    return {"distribution_mode": "memory"} if game == "jumper" else {}
 
 
 def run_rgb_array(game, num, steps, every, seed, **kw):
@@ -43,7 +50,20 @@ def run_rgb_array(game, num, steps, every, seed, **kw):
 
 @pytest.mark.parametrize("game", GAMES)
 def test_rgb_array_parity(game):
-    assert run_rgb_array(game, 4, 60, 6, seed=50, num_levels=0, rand_seed=31) == 11
+    assert run_rgb_array(game, 4, 60, 6, seed=50, num_levels=0, rand_seed=31, **game_kw(game)) == 11
+
+
+@pytest.mark.parametrize("game", ROTATING)
+def test_rgb_array_rotated_long(game):
+    """longer runs of the games whose entities rotate (the antialiased rotated drawImage, tiles,
+    starpilot's scrolling background, plunder's bars), 8 envs, frames every 25 steps."""
+    assert run_rgb_array(game, 8, 200, 25, seed=53, num_levels=0, rand_seed=35) == 9
+
+
+def test_rgb_array_jumper_compass_rejected():
+    from procgen_amd import ProcgenGym3Env
+    with pytest.raises(Exception):
+        ProcgenGym3Env(num=2, env_name="jumper", render_mode="rgb_array")
 
 
 @pytest.mark.parametrize("game", ["coinrun", "maze", "ninja"])

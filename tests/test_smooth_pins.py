@@ -29,6 +29,7 @@ def libs():
     q.qtp_draw.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, D, U, I, I]
     o = oracle_lib.load()
     o.oracle_qt_smooth.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, U]
+    o.oracle_qt_smooth_rot.argtypes = [I, I, P, P, I, I, I, I, D, D, D, D, D, D]
     return q, o
 
 
@@ -94,6 +95,40 @@ def test_smooth_draw_image(W):
                                       % (iw, ih, fmt, mir, op, x, y, w, h, W))
 
 
+@pytest.mark.parametrize("W", [64, 512])
+def test_smooth_draw_image_rotated(W):
+    """translate(center); rotate(deg); drawImage(QRectF(-w/2, -h/2, w, h)) (basic-abstract-game.cpp:908-916)
+    with SmoothPixmapTransform + Antialiasing: QRasterizer::rasterizeLine's general branch (corners on
+    the 26.6 grid, the four edge slopes, intersectPixelFP), its near-horizontal / near-vertical
+    branches (angles within a 64th of a pixel of 0 / 90 / 180 degrees), the rotate fetch helpers (4-bit
+    SSE2 groups, 8-bit lead-in / tail, 8-bit positions beyond an 8x zoom), QTransform's fuzzy type
+    (rotate(-180) is a scale), clipped at every border, transparent texels, mirroring, opacity."""
+    q, o = libs()
+    rng = np.random.RandomState(300 + W)
+    for k in range(300 if W == 64 else 80):
+        iw, ih = rng.randint(2, 150, 2)
+        img = rng.randint(0, 1 << 24, (ih, iw)).astype(np.uint32) | np.uint32(0xff000000)
+        if k % 3 == 0:
+            img[rng.rand(ih, iw) < 0.4] = 0
+        op = float(rng.choice([0.5, 0.25, 0.7])) if k % 7 == 0 else 1.0
+        mir = int(k % 4 == 1)
+        x, y = rng.uniform(-W * 0.2, W * 0.95, 2)
+        w, h = rng.uniform(0.5, W * 0.5, 2)
+        if k % 5 == 0:
+            w = h  # square sprites
+        if k % 11 == 0:
+            w, h = rng.uniform(0.5, 4, 2) * (iw / 8.0, ih / 8.0)  # > 8x zoom: 8-bit positions
+        deg = float(rng.uniform(-360, 360))
+        if k % 6 == 0:
+            deg = float(rng.choice([90, -90, 180, -180, 270, 0.01, -0.02, 179.99, 90.005, 45, -45]))
+        a = _canvas(rng, W)
+        b = a.copy()
+        q.qtp_draw(W, W, a.ctypes.data, 2, img.ctypes.data, iw, ih, 6, mir, x, y, w, h, deg, op, 0, 1, 1)
+        o.oracle_qt_smooth_rot(W, W, b.ctypes.data, img.ctypes.data, iw, ih, 6, mir, x, y, w, h, deg, op)
+        np.testing.assert_array_equal(b, a, err_msg="image %dx%d mir %d op %r at (%r, %r, %r, %r) deg %r on %d px"
+                                      % (iw, ih, mir, op, x, y, w, h, deg, W))
+
+
 def replay(q, log, res):
     """The oracle's logged painter commands of one frame through the real Qt, on one canvas."""
     canvas = np.zeros((res, res), np.uint32) | np.uint32(0xff000000)
@@ -102,35 +137,40 @@ def replay(q, log, res):
         x, y, w, h = (float(v) for v in row[1:5])
         if kind == 1:
             canvas = _draw(q, canvas, 1, None, 6, 0, x, y, w, h, 1.0, int(row[5]))
-        else:
+        else:  # 0: drawImage(QRectF); 2: translate(rect centre); rotate(row[9] degrees); drawImage
             ptr, dims, fm, op = int(row[5]), int(row[6]), int(row[7]), float(row[8])
             iw, ih = dims >> 16, dims & 0xffff
             img = np.ctypeslib.as_array((ctypes.c_uint32 * (iw * ih)).from_address(ptr)).reshape(ih, iw).copy()
-            canvas = _draw(q, canvas, 0, img, fm >> 1, fm & 1, x, y, w, h, op, 0)
+            canvas = _draw(q, canvas, kind, img, fm >> 1, fm & 1, x, y, w, h, op, 0, float(row[9]))
     return canvas
 
 
-def _draw(q, canvas, kind, img, fmt, mir, x, y, w, h, op, argb):
+def _draw(q, canvas, kind, img, fmt, mir, x, y, w, h, op, argb, deg=0.0):
     a = np.ascontiguousarray(canvas)
     im = np.ascontiguousarray(img if img is not None else np.zeros((1, 1), np.uint32))
     q.qtp_draw(a.shape[1], a.shape[0], a.ctypes.data, kind, im.ctypes.data, im.shape[1], im.shape[0], fmt, mir,
-               x, y, w, h, 0.0, op, argb, 1, 1)
+               x, y, w, h, deg, op, argb, 1, 1)
     return a
 
 
-@pytest.mark.parametrize("game", ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja"])
+ALL_GAMES = ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja", "bossfight", "caveflyer", "dodgeball",
+             "fruitbot", "heist", "jumper", "leaper", "plunder", "starpilot"]
+
+
+@pytest.mark.parametrize("game", ALL_GAMES)
 def test_rgb_array_frames_replayed_through_qt(game):
     """Whole 512x512 rgb_array frames: the oracle paints the frame of a running env and logs every
     painter call (background fill + image, grid tiles, entities, overlays); the same calls replayed
     through the real Qt with Antialiasing + SmoothPixmapTransform give the same pixels."""
     q, _ = libs()
-    orc = oracle_lib.OracleEnv(game, 1, num_levels=0, rand_seed=3, paint_vel_info=1)
+    kw = {"distribution_mode": 10} if game == "jumper" else {}  # memory mode: jumper draws no compass
+    orc = oracle_lib.OracleEnv(game, 1, num_levels=0, rand_seed=3, paint_vel_info=1, **kw)
     rng = np.random.RandomState(4)
     for t in range(40):
         orc.step(rng.randint(0, 15, 1).astype(np.int32))
         if t % 13 != 12:
             continue
-        rgb, log = orc.render_rgb_array(512, log_cap=4000)
+        rgb, log = orc.render_rgb_array(512, log_cap=20000)
         assert len(log) > 3
         qt_frame = replay(q, log, 512)
         ref = np.stack([(qt_frame >> 16) & 255, (qt_frame >> 8) & 255, qt_frame & 255], -1).astype(np.uint8)
