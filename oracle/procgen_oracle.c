@@ -4793,10 +4793,17 @@ static int qt_aa_general_spans(double pax, double pay, double pbx, double pby, d
 }
 
 /* QRasterizer::rasterizeLine(a, b, width) antialiased (squareCap off); clip = [0, cw) x [0, ch) */
-static int qt_aa_line_spans(double ax, double ay, double bx, double by, double width, int cw, int ch, QtSpan *out,
-                            int cap) {
+static int qt_aa_line_spans_cap(double ax, double ay, double bx, double by, double width, bool squareCap, int cw, int ch,
+                                QtSpan *out, int cap) {
     double pax = ax, pay = ay, pbx = bx, pby = by;
     if ((qt_fuzzy_null(ax - bx) && qt_fuzzy_null(ay - by)) || width == 0) return 0; /* QPointF == is fuzzy */
+    if (squareCap) { /* the line grows by half its (absolute) width at both ends */
+        const double c = 0.5f * width, dx = pbx - pax, dy = pby - pay;
+        pax -= dx * c;
+        pay -= dy * c;
+        pbx += dx * c;
+        pby += dy * c;
+    }
     {
         const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
         const double cl = 0 - offx, ct = 0 - offy;
@@ -4884,6 +4891,10 @@ static int qt_aa_line_spans(double ax, double ay, double bx, double by, double w
         }
     }
     return k;
+}
+static int qt_aa_line_spans(double ax, double ay, double bx, double by, double width, int cw, int ch, QtSpan *out,
+                            int cap) {
+    return qt_aa_line_spans_cap(ax, ay, bx, by, width, false, cw, ch, out, cap);
 }
 /* the rect's mid line with width h / w (QRasterPaintEngine::drawImage / fillRect, identity matrix) */
 static int qt_aa_rect_spans(double x, double y, double w, double h, int cw, int ch, QtSpan *out, int cap) {
@@ -5886,6 +5897,505 @@ static int ag_draw_ellipse(AgCanvas *c, double x, double y, double w, double h, 
     return 0;
 }
 
+/* ================================================================== jumper's compass at RENDER_RES
+ * (jumper.cpp:137-177 under Antialiasing, render_mode="rgb_array"): the painter calls are
+ *   drawEllipse(QRectF) with QBrush(c) + QPen(c, 1)  -> QPaintEngineEx::drawEllipse: the path of
+ *       qt_curves_for_arc filled by the antialiased gray raster (qgrayraster.c, a FreeType
+ *       "smooth" rasterizer fork) on QOutlineMapper's flattened 26.6 outline, then stroked by the
+ *       antialiased QCosmeticStroker (a width-1 pen under a translation is a fast pen);
+ *   drawLine(QLine) with QPen(c, thickness > 1) -> QRasterPaintEngine::stroke;
+ *   fillRect(QRectF) (qt_smooth_fill_rectf);
+ *   drawEllipse(QRect) with a translucent brush and no pen -> the gray raster fill.
+ * Pinned primitive by primitive against the real Qt 5.9.7 (tests/test_smooth_pins.py). */
+
+/* solid colour blend of one antialiased span pixel: blend_color_argb (Source for an opaque colour)
+ * / comp_func_solid_SourceOver with const_alpha = coverage, on an RGB32 canvas */
+static void qt_aa_blend_solid(uint32_t *d, uint32_t pm, int cov) {
+    if (cov <= 0) return;
+    const uint32_t c = cov == 255 ? pm : BYTE_MUL(pm, (uint32_t)cov);
+    const uint32_t a = c >> 24;
+    *d = a == 255 ? c : c + BYTE_MUL(*d, 255u - a);
+}
+
+/* ---- qgrayraster.c: PIXEL_BITS 8 cells (area, cover) accumulated along the outline's lines in
+ * 24.8, clipped to the clip box [0, cw) x [0, ch) (cells left of it pile up in column -1, cells right
+ * of it are dropped), then swept row by row into coverages (area >> 9, nonzero or even-odd) */
+#define GR_PB 8
+#define GR_ONE (1 << GR_PB)
+typedef struct {
+    int min_ex, max_ex, min_ey, max_ey, count_ex, count_ey;
+    int ex, ey, invalid;     /* current cell (relative; ex -1 = left of the clip) */
+    int area, cover;          /* its accumulators (TArea / TCoord: int) */
+    int x, y, last_ey;        /* pen position (24.8) and the current row's top */
+    int *carea, *ccover;      /* dense cells: (count_ey) x (count_ex + 1), column 0 = ex -1 */
+} GrRas;
+static void gr_record(GrRas *r) {
+    if (!r->invalid && (r->area | r->cover)) {
+        const size_t k = (size_t)r->ey * (r->count_ex + 1) + (r->ex + 1);
+        r->carea[k] += r->area;
+        r->ccover[k] += r->cover;
+    }
+}
+static void gr_set_cell(GrRas *r, int ex, int ey) {
+    ey -= r->min_ey;
+    if (ex > r->max_ex) ex = r->max_ex;
+    ex -= r->min_ex;
+    if (ex < 0) ex = -1;
+    if (ex != r->ex || ey != r->ey) {
+        gr_record(r);
+        r->area = 0;
+        r->cover = 0;
+    }
+    r->ex = ex;
+    r->ey = ey;
+    r->invalid = ((unsigned)ey >= (unsigned)r->count_ey || ex >= r->count_ex);
+}
+static void gr_start_cell(GrRas *r, int ex, int ey) {
+    if (ex > r->max_ex) ex = r->max_ex;
+    if (ex < r->min_ex) ex = r->min_ex - 1;
+    r->area = 0;
+    r->cover = 0;
+    r->ex = ex - r->min_ex;
+    r->ey = ey - r->min_ey;
+    r->last_ey = ey << GR_PB;
+    r->invalid = 0;
+    gr_set_cell(r, ex, ey);
+}
+static int gr_trunc(long x) { return (int)(x >> GR_PB); }
+static void gr_scanline(GrRas *r, int ey, long x1, int y1, long x2, int y2) {
+    long dx = x2 - x1;
+    int ex1 = gr_trunc(x1), ex2 = gr_trunc(x2);
+    const int fx1 = (int)(x1 - ((long)ex1 << GR_PB)), fx2 = (int)(x2 - ((long)ex2 << GR_PB));
+    if (y1 == y2) {
+        gr_set_cell(r, ex2, ey);
+        return;
+    }
+    if (ex1 == ex2) {
+        const int delta = y2 - y1;
+        r->area += (fx1 + fx2) * delta;
+        r->cover += delta;
+        return;
+    }
+    long p = (long)(GR_ONE - fx1) * (y2 - y1);
+    int first = GR_ONE, incr = 1;
+    if (dx < 0) {
+        p = (long)fx1 * (y2 - y1);
+        first = 0;
+        incr = -1;
+        dx = -dx;
+    }
+    int delta = (int)(p / dx), mod = (int)(p % dx);
+    if (mod < 0) {
+        delta--;
+        mod += (int)dx;
+    }
+    r->area += (fx1 + first) * delta;
+    r->cover += delta;
+    ex1 += incr;
+    gr_set_cell(r, ex1, ey);
+    y1 += delta;
+    if (ex1 != ex2) {
+        p = (long)GR_ONE * (y2 - y1 + delta);
+        int lift = (int)(p / dx), rem = (int)(p % dx);
+        if (rem < 0) {
+            lift--;
+            rem += (int)dx;
+        }
+        mod -= (int)dx;
+        while (ex1 != ex2) {
+            delta = lift;
+            mod += rem;
+            if (mod >= 0) {
+                mod -= (int)dx;
+                delta++;
+            }
+            r->area += GR_ONE * delta;
+            r->cover += delta;
+            y1 += delta;
+            ex1 += incr;
+            gr_set_cell(r, ex1, ey);
+        }
+    }
+    delta = y2 - y1;
+    r->area += (fx2 + GR_ONE - first) * delta;
+    r->cover += delta;
+}
+static void gr_line(GrRas *r, long to_x, long to_y) {
+    int ey1 = gr_trunc(r->last_ey), ey2 = gr_trunc(to_y);
+    const int fy1 = (int)(r->y - r->last_ey), fy2 = (int)(to_y - ((long)ey2 << GR_PB));
+    long dx = to_x - r->x, dy = to_y - r->y;
+    {
+        const int mn = ey1 < ey2 ? ey1 : ey2, mx = ey1 < ey2 ? ey2 : ey1;
+        if (mn >= r->max_ey || mx < r->min_ey) goto end;
+    }
+    if (ey1 == ey2) {
+        gr_scanline(r, ey1, r->x, fy1, to_x, fy2);
+        goto end;
+    }
+    {
+        int incr = 1;
+        if (dx == 0) {
+            const int ex = gr_trunc(r->x);
+            const int two_fx = (int)((r->x - ((long)ex << GR_PB)) << 1);
+            int first = GR_ONE;
+            if (dy < 0) {
+                first = 0;
+                incr = -1;
+            }
+            int delta = first - fy1;
+            r->area += two_fx * delta;
+            r->cover += delta;
+            ey1 += incr;
+            gr_set_cell(r, ex, ey1);
+            delta = first + first - GR_ONE;
+            const int area = two_fx * delta;
+            while (ey1 != ey2) {
+                r->area += area;
+                r->cover += delta;
+                ey1 += incr;
+                gr_set_cell(r, ex, ey1);
+            }
+            delta = fy2 - GR_ONE + first;
+            r->area += two_fx * delta;
+            r->cover += delta;
+            goto end;
+        }
+        long p = (long)(GR_ONE - fy1) * dx;
+        int first = GR_ONE;
+        if (dy < 0) {
+            p = (long)fy1 * dx;
+            first = 0;
+            incr = -1;
+            dy = -dy;
+        }
+        int delta = (int)(p / dy), mod = (int)(p % dy);
+        if (mod < 0) {
+            delta--;
+            mod += (int)dy;
+        }
+        long x = r->x + delta;
+        gr_scanline(r, ey1, r->x, fy1, x, first);
+        ey1 += incr;
+        gr_set_cell(r, gr_trunc(x), ey1);
+        if (ey1 != ey2) {
+            p = (long)GR_ONE * dx;
+            int lift = (int)(p / dy), rem = (int)(p % dy);
+            if (rem < 0) {
+                lift--;
+                rem += (int)dy;
+            }
+            mod -= (int)dy;
+            while (ey1 != ey2) {
+                delta = lift;
+                mod += rem;
+                if (mod >= 0) {
+                    mod -= (int)dy;
+                    delta++;
+                }
+                const long x2 = x + delta;
+                gr_scanline(r, ey1, x, GR_ONE - first, x2, first);
+                x = x2;
+                ey1 += incr;
+                gr_set_cell(r, gr_trunc(x), ey1);
+            }
+        }
+        gr_scanline(r, ey1, x, GR_ONE - first, to_x, fy2);
+    }
+end:
+    r->x = (int)to_x;
+    r->y = (int)to_y;
+    r->last_ey = ey2 << GR_PB;
+}
+static int gr_coverage(int area, bool even_odd) { /* gray_hline */
+    int c = area >> (GR_PB * 2 + 1 - 8);
+    if (c < 0) c = -c;
+    if (even_odd) {
+        c &= 511;
+        if (c > 256) c = 512 - c;
+        else if (c == 256) c = 255;
+    } else if (c >= 256) {
+        c = 255;
+    }
+    return c;
+}
+/* fill one closed contour of 26.6 points (QT_FT_Outline: the decomposer closes it) in `pm` */
+static void qt_gray_fill(const int *fx, const int *fy, int n, bool even_odd, uint32_t pm, uint32_t *canvas, int cw, int ch) {
+    if (n <= 0) return;
+    GrRas r;
+    int xmn = fx[0], xmx = fx[0], ymn = fy[0], ymx = fy[0];
+    for (int i = 1; i < n; i++) {
+        if (fx[i] < xmn) xmn = fx[i];
+        if (fx[i] > xmx) xmx = fx[i];
+        if (fy[i] < ymn) ymn = fy[i];
+        if (fy[i] > ymx) ymx = fy[i];
+    }
+    r.min_ex = xmn >> 6; r.min_ey = ymn >> 6; r.max_ex = (xmx + 63) >> 6; r.max_ey = (ymx + 63) >> 6;
+    if (r.max_ex <= 0 || r.min_ex >= cw || r.max_ey <= 0 || r.min_ey >= ch) return;
+    if (r.min_ex < 0) r.min_ex = 0;
+    if (r.min_ey < 0) r.min_ey = 0;
+    if (r.max_ex > cw) r.max_ex = cw;
+    if (r.max_ey > ch) r.max_ey = ch;
+    r.count_ex = r.max_ex - r.min_ex;
+    r.count_ey = r.max_ey - r.min_ey;
+    const size_t ncell = (size_t)r.count_ey * (r.count_ex + 1);
+    r.carea = (int *)calloc(ncell, sizeof(int));
+    r.ccover = (int *)calloc(ncell, sizeof(int));
+    r.invalid = 1;
+    r.ex = r.ey = 0;
+    r.area = r.cover = 0;
+    /* gray_move_to(first) then gray_line_to each point, and back to the first (contour close) */
+    {
+        const long x0 = (long)fx[0] << (GR_PB - 6), y0 = (long)fy[0] << (GR_PB - 6);
+        gr_record(&r);
+        gr_start_cell(&r, gr_trunc(x0), gr_trunc(y0));
+        r.x = (int)x0;
+        r.y = (int)y0;
+        for (int i = 1; i <= n; i++) {
+            const int k = i < n ? i : 0;
+            gr_line(&r, (long)fx[k] << (GR_PB - 6), (long)fy[k] << (GR_PB - 6));
+        }
+        gr_record(&r);
+    }
+    /* gray_sweep */
+    for (int yi = 0; yi < r.count_ey; yi++) {
+        uint32_t *row = canvas + (size_t)(yi + r.min_ey) * cw + r.min_ex;
+        const int *ca = r.carea + (size_t)yi * (r.count_ex + 1), *cc = r.ccover + (size_t)yi * (r.count_ex + 1);
+        int cover = 0, x = 0;
+        for (int cx = -1; cx < r.count_ex; cx++) {
+            if (ca[cx + 1] == 0 && cc[cx + 1] == 0) continue; /* no cell here */
+            if (cx > x && cover != 0) {
+                const int c = gr_coverage(cover * (GR_ONE * 2), even_odd);
+                for (int k = x; k < cx; k++) qt_aa_blend_solid(&row[k], pm, c);
+            }
+            cover += cc[cx + 1];
+            const int area = cover * (GR_ONE * 2) - ca[cx + 1];
+            if (area != 0 && cx >= 0) qt_aa_blend_solid(&row[cx], pm, gr_coverage(area, even_odd));
+            x = cx + 1;
+        }
+        if (r.count_ex > x && cover != 0) {
+            const int c = gr_coverage(cover * (GR_ONE * 2), even_odd);
+            for (int k = x; k < r.count_ex; k++) qt_aa_blend_solid(&row[k], pm, c);
+        }
+    }
+    free(r.carea);
+    free(r.ccover);
+}
+/* the ellipse path filled by the gray raster: QOutlineMapper flattens the four curves (threshold
+ * 0.25) and rounds to 26.6; QVectorPath::EllipseHint carries no WindingFill -> odd-even */
+static void qt_aa_fill_ellipse(const PtD pts[13], uint32_t pm, uint32_t *canvas, int cw, int ch) {
+    static PtD poly[4 * 1100];
+    static int fx[4 * 1100], fy[4 * 1100];
+    int n = 0;
+    poly[n++] = pts[0];
+    for (int k = 0; k < 4; k++) {
+        QBez b = {poly[n - 1].x, poly[n - 1].y, pts[3 * k + 1].x, pts[3 * k + 1].y, pts[3 * k + 2].x, pts[3 * k + 2].y,
+                  pts[3 * k + 3].x, pts[3 * k + 3].y};
+        n = qbez_flatten(b, 0.25, poly, n);
+    }
+    for (int i = 0; i < n; i++) {
+        fx[i] = qt_fixed_26_6(poly[i].x);
+        fy[i] = qt_fixed_26_6(poly[i].y);
+    }
+    qt_gray_fill(fx, fy, n, true, pm, canvas, cw, ch);
+}
+
+/* ---- QCosmeticStroker, antialiased (drawLineAntialiased<drawPixel, NoDasher>): two pixels per
+ * major step weighted by the minor position's fraction, the end pixels by their 26.6 coverage */
+typedef struct {
+    uint32_t *canvas;
+    int cw, ch;
+    uint32_t pm;
+    double xmin, xmax, ymin, ymax;
+    int lastx, lasty; /* clipLine writes them (unused antialiased) */
+} CStrokerAA;
+static void csa_pixel(CStrokerAA *s, int x, int y, int cov) {
+    if (x < 0 || x > s->cw - 1 || y < 0 || y > s->ch - 1) return;
+    qt_aa_blend_solid(&s->canvas[(size_t)y * s->cw + x], s->pm, (cov * 256) >> 8);
+}
+static bool csa_clip(CStrokerAA *s, double *x1, double *y1, double *x2, double *y2) {
+    CStroker t;
+    t.xmin = s->xmin; t.xmax = s->xmax; t.ymin = s->ymin; t.ymax = s->ymax;
+    t.lastx = s->lastx;
+    const bool out = cs_clip(&t, x1, y1, x2, y2);
+    s->lastx = t.lastx;
+    return out;
+}
+static void csa_line(CStrokerAA *s, double rx1, double ry1, double rx2, double ry2, int caps) {
+    if (csa_clip(s, &rx1, &ry1, &rx2, &ry2)) return;
+    int x1 = toF26Dot6(rx1), y1 = toF26Dot6(ry1), x2 = toF26Dot6(rx2), y2 = toF26Dot6(ry2);
+    const int dx = x2 - x1, dy = y2 - y1;
+    if (abs(dx) < abs(dy)) { /* vertical */
+        const int xinc = F16Dot16FixedDiv(dx, dy);
+        if (y1 > y2) {
+            int t = y1; y1 = y2; y2 = t;
+            t = x1; x1 = x2; x2 = t;
+            caps = swapCaps(caps);
+        }
+        int x = (x1 - 32) * 1024;
+        x -= (((y1 & 63) - 32) * xinc) >> 6;
+        capAdjust(caps, &y1, &y2, &x, xinc);
+        int y = y1 >> 6;
+        const int ys = y2 >> 6;
+        int aS, aE;
+        if (y == ys) {
+            aS = y2 - y1;
+            aE = 0;
+        } else {
+            aS = 64 - (y1 & 63);
+            aE = y2 & 63;
+        }
+        {
+            const unsigned al = (uint8_t)(x >> 8);
+            csa_pixel(s, x >> 16, y, (int)((255 - al) * aS) >> 6);
+            csa_pixel(s, (x >> 16) + 1, y, (int)(al * aS) >> 6);
+        }
+        x += xinc;
+        ++y;
+        if (y < ys) {
+            do {
+                const unsigned al = (uint8_t)(x >> 8);
+                csa_pixel(s, x >> 16, y, (int)(255 - al));
+                csa_pixel(s, (x >> 16) + 1, y, (int)al);
+                x += xinc;
+            } while (++y < ys);
+        }
+        if (aE) {
+            const unsigned al = (uint8_t)(x >> 8);
+            csa_pixel(s, x >> 16, y, (int)((255 - al) * aE) >> 6);
+            csa_pixel(s, (x >> 16) + 1, y, (int)(al * aE) >> 6);
+        }
+    } else { /* horizontal */
+        if (!dx) return;
+        const int yinc = F16Dot16FixedDiv(dy, dx);
+        if (x1 > x2) {
+            int t = x1; x1 = x2; x2 = t;
+            t = y1; y1 = y2; y2 = t;
+            caps = swapCaps(caps);
+        }
+        int y = (y1 - 32) * 1024;
+        y -= (((x1 & 63) - 32) * yinc) >> 6;
+        capAdjust(caps, &x1, &x2, &y, yinc);
+        int x = x1 >> 6;
+        const int xs = x2 >> 6;
+        int aS, aE;
+        if (x == xs) {
+            aS = x2 - x1;
+            aE = 0;
+        } else {
+            aS = 64 - (x1 & 63);
+            aE = x2 & 63;
+        }
+        {
+            const unsigned al = (uint8_t)(y >> 8);
+            csa_pixel(s, x, y >> 16, (int)((255 - al) * aS) >> 6);
+            csa_pixel(s, x, (y >> 16) + 1, (int)(al * aS) >> 6);
+        }
+        y += yinc;
+        ++x;
+        if (x < xs) {
+            do {
+                const unsigned al = (uint8_t)(y >> 8);
+                csa_pixel(s, x, y >> 16, (int)(255 - al));
+                csa_pixel(s, x, (y >> 16) + 1, (int)al);
+                y += yinc;
+            } while (++x < xs);
+        }
+        if (aE) {
+            const unsigned al = (uint8_t)(y >> 8);
+            csa_pixel(s, x, y >> 16, (int)((255 - al) * aE) >> 6);
+            csa_pixel(s, x, (y >> 16) + 1, (int)(al * aE) >> 6);
+        }
+    }
+}
+static void csa_cubic_sub(CStrokerAA *s, PtD *p, int level, int caps) {
+    if (level) {
+        const double dx = p[3].x - p[0].x, dy = p[3].y - p[0].y;
+        const double len = ((double).25) * (fabs(dx) + fabs(dy));
+        if (fabs(dx * (p[0].y - p[2].y) - dy * (p[0].x - p[2].x)) >= len ||
+            fabs(dx * (p[0].y - p[1].y) - dy * (p[0].x - p[1].x)) >= len) {
+            cs_split_cubic(p);
+            --level;
+            csa_cubic_sub(s, p + 3, level, caps);
+            csa_cubic_sub(s, p, level, caps);
+            return;
+        }
+    }
+    csa_line(s, p[3].x, p[3].y, p[0].x, p[0].y, caps);
+}
+static void qt_aa_stroke_ellipse(const PtD pts[13], uint32_t pm, uint32_t *canvas, int cw, int ch) {
+    CStrokerAA s;
+    s.canvas = canvas; s.cw = cw; s.ch = ch; s.pm = pm;
+    s.xmin = -1; s.xmax = cw + 1; s.ymin = -1; s.ymax = ch + 1;
+    s.lastx = s.lasty = CS_INT_MIN;
+    for (int k = 0; k < 4; k++) {
+        PtD p[3 * CS_MAXSUB + 4];
+        p[3] = pts[3 * k];
+        p[2] = pts[3 * k + 1];
+        p[1] = pts[3 * k + 2];
+        p[0] = pts[3 * k + 3];
+        csa_cubic_sub(&s, p, CS_MAXSUB, CS_NOCAPS);
+    }
+}
+
+/* QRasterPaintEngine::fill's early out: the path's control-point rect, toRect() (qRound of x, y, w,
+ * h), must intersect the device rect (QRect::intersects) */
+static bool qt_path_on_device(const PtD *p, int n, int cw, int ch) {
+    double x0 = p[0].x, x1 = p[0].x, y0 = p[0].y, y1 = p[0].y;
+    for (int i = 1; i < n; i++) {
+        if (p[i].x < x0) x0 = p[i].x;
+        if (p[i].x > x1) x1 = p[i].x;
+        if (p[i].y < y0) y0 = p[i].y;
+        if (p[i].y > y1) y1 = p[i].y;
+    }
+    const int rx = qRound(x0), ry = qRound(y0), rw = qRound(x1 - x0), rh = qRound(y1 - y0);
+    if (rw == 0 && rh == 0) return false; /* QRect::isNull */
+    const int ax2 = rx + rw - 1, ay2 = ry + rh - 1;
+    int l1 = rx, r1 = rx, t1 = ry, b1 = ry;
+    if (ax2 - rx + 1 < 0) l1 = ax2; else r1 = ax2;
+    if (ay2 - ry + 1 < 0) t1 = ay2; else b1 = ay2;
+    return !(l1 > cw - 1 || 0 > r1 || t1 > ch - 1 || 0 > b1);
+}
+/* drawEllipse(QRectF(x, y, w, h)) under Antialiasing: brush `brush` (0 = none) filled, then pen `pen`
+ * (0 = none, width 1) stroked; colours non-premultiplied ARGB */
+static void qt_aa_draw_ellipse(double x, double y, double w, double h, uint32_t brush, uint32_t pen, uint32_t *canvas,
+                               int cw, int ch) {
+    if (w <= 0 || h <= 0) return;
+    PtD pts[13];
+    qt_ellipse_points(x, y, w, h, pts);
+    if (brush >> 24 && qt_path_on_device(pts, 13, cw, ch)) qt_aa_fill_ellipse(pts, qt_solid_premul(brush), canvas, cw, ch);
+    if (pen >> 24) qt_aa_stroke_ellipse(pts, qt_solid_premul(pen), canvas, cw, ch);
+}
+/* drawLine(QLine(x1, y1, x2, y2)) with QPen(colour, width > 1), SquareCap, under Antialiasing:
+ * QRasterPaintEngine::stroke's rasterizeLine branch (width / length, square caps) */
+static void qt_aa_wide_line(int x1, int y1, int x2, int y2, int width, uint32_t argb, uint32_t *canvas, int cw, int ch) {
+    const double dx = (double)x2 - x1, dy = (double)y2 - y1, len = sqrt(dx * dx + dy * dy);
+    static QtSpan spans[8192];
+    int ns;
+    if (len == 0) /* a point: the square cap alone, as a horizontal line of the pen's width and relative width 1 */
+        ns = qt_aa_line_spans_cap(x1 - width * 0.5, y1, x1 + width * 0.5, y1, 1, false, cw, ch, spans, 8192);
+    else
+        ns = qt_aa_line_spans_cap(x1, y1, x2, y2, width / len, true, cw, ch, spans, 8192);
+    const uint32_t pm = qt_solid_premul(argb);
+    for (int k = 0; k < ns; k++)
+        for (int xx = spans[k].x; xx < spans[k].x + spans[k].len; xx++)
+            qt_aa_blend_solid(&canvas[(size_t)spans[k].y * cw + xx], pm, spans[k].cov);
+}
+
+/* one compass primitive on a cw x ch RGB32 canvas (tests/test_smooth_pins.py against
+ * tools/qt_smooth_probe.cpp qtp_prim): kind 10 drawEllipse(QRectF) brush + 1-px pen, 13 pen only,
+ * 14 brush only, 12 drawEllipse(QRect(int x, y, w, h)) brush only, 11 drawLine(QLine) pen width `penw` */
+void oracle_qt_prim(int cw, int ch, uint32_t *inout, int kind, double x, double y, double w, double h, uint32_t argb,
+                    int penw) {
+    switch (kind) {
+    case 10: qt_aa_draw_ellipse(x, y, w, h, argb, argb, inout, cw, ch); break;
+    case 13: qt_aa_draw_ellipse(x, y, w, h, 0, argb, inout, cw, ch); break;
+    case 14: qt_aa_draw_ellipse(x, y, w, h, argb, 0, inout, cw, ch); break;
+    case 12: qt_aa_draw_ellipse((int)x, (int)y, (int)w, (int)h, argb, 0, inout, cw, ch); break;
+    case 11: qt_aa_wide_line((int)x, (int)y, (int)w, (int)h, penw, argb, inout, cw, ch); break;
+    default: break;
+    }
+}
+
 /* ---- AssetGen (assetgen.cpp:3-195); float / double promotion as the C++ source has it */
 typedef struct {
     MT *rg;
@@ -6318,8 +6828,44 @@ static void jp_stamp(uint32_t *canvas, const uint32_t *rows64, int dx, int dy, u
         }
     }
 }
+static void qt_aa_draw_ellipse(double x, double y, double w, double h, uint32_t brush, uint32_t pen, uint32_t *canvas,
+                               int cw, int ch);
+static void qt_aa_wide_line(int x1, int y1, int x2, int y2, int width, uint32_t argb, uint32_t *canvas, int cw, int ch);
+/* the compass at RENDER_RES: the painter calls themselves, restated antialiased (qt_aa_*; each
+ * logged as kind 10 / 11 / 12 for the replay through the real Qt) */
+static void jp_draw_compass_smooth(Game *g) {
+    const float u = g->unit, vd = g->view_dim, cd = g->jp_compass_dim;
+    const float ax = (float)(vd - cd - .25), ay = .25f; /* get_abs_rect (:812-814) */
+    const double rx = (double)(ax * u), ry = (double)(ay * u), rw = (double)(cd * u), rh = (double)(cd * u);
+    qt_log(10, rx, ry, rw, rh, (double)0xffa8a69eu, 1, 0, 1);
+    qt_aa_draw_ellipse(rx, ry, rw, rh, 0xffa8a69eu, 0xffa8a69eu, RT.px, RT.w, RT.h); /* QColor(168, 166, 158) */
+    const float pen_thickness = (float)(RT.w / (256.0 / cd));
+    const float cx = (float)(rx + rw / 2), cy = (float)(ry + rh / 2); /* QRectF::center */
+    const float cr = (float)(rw / 2 * .95);
+    Entity *agent = AG(g), *goal = &g->ents[1];
+    const float theta = (float)atan2((double)(goal->y - agent->y), (double)(goal->x - agent->x)); /* get_theta */
+    const int x1 = (int)cx, y1 = (int)cy; /* QPainter::drawLine(int, int, int, int) */
+    const int x2 = (int)(cx + cr * cos((double)theta)), y2 = (int)(cy - cr * sin((double)theta));
+    qt_log(11, x1, y1, x2, y2, (double)0xfffcba03u, (int)pen_thickness, 0, 1);
+    qt_aa_wide_line(x1, y1, x2, y2, (int)pen_thickness, 0xfffcba03u, RT.px, RT.w, RT.h); /* QColor(252, 186, 3) */
+    float ddx = agent->x - goal->x, ddy = agent->y - goal->y; /* get_distance (:133-143) */
+    float dist = (float)sqrt((double)(ddx * ddx + ddy * ddy));
+    float dist_pct = (float)(dist / (g->main_width * sqrt(2)));
+    float bar_thickness = cd / 8;
+    qt_fill_rectf(g->canvas, (double)((float)(vd - cd - .25) * u), (double)((float)(.25 + cd) * u),
+                  (double)(cd * dist_pct * u), (double)(bar_thickness * u), 0xfffcba03u);
+    if (g->jp_jump_delta < 0 && !g->has_support) { /* drawEllipse(QRect(...)), QColor(255, 255, 255, 120) */
+        RectD r1 = get_screen_rect(g, agent->x - agent->rx, agent->y + agent->ry, 2 * agent->rx, 2 * agent->ry, 0);
+        const int qx = (int)r1.x, qy = (int)(r1.y + r1.h * (5.0 / 6)), qw = (int)r1.w, qh = (int)(r1.h / 3);
+        qt_log(12, qx, qy, qw, qh, (double)0x78ffffffu, 0, 0, 1);
+        qt_aa_draw_ellipse(qx, qy, qw, qh, 0x78ffffffu, 0, RT.px, RT.w, RT.h);
+    }
+}
 static void jp_draw_compass(Game *g, const or_atlas *at) {
-    if (RT.smooth) fatal_msg("render_mode=rgb_array: jumper's compass is not restated");
+    if (RT.smooth) {
+        jp_draw_compass_smooth(g);
+        return;
+    }
     const or_image *ti = &at->sprites[JP_TABLE_SLOT];
     fassert(ti->w > 0);
     const uint32_t *t = at->pixels + ti->offset;

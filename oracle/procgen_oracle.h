@@ -97,6 +97,10 @@ void oracle_diag_counters(long long *out, int reset);
 int oracle_render_rgb_array(void *h, uint8_t *rgb, int res, double *log, int cap);
 void oracle_qt_smooth(int cw, int ch, uint32_t *inout, int kind, const uint32_t *img, int iw, int ih, int fmt,
                       int mirrored, double x, double y, double w, double h, double opacity, uint32_t argb);
+void oracle_qt_smooth_rot(int cw, int ch, uint32_t *inout, const uint32_t *img, int iw, int ih, int fmt, int mirrored,
+                          double x, double y, double w, double h, double deg, double opacity);
+void oracle_qt_prim(int cw, int ch, uint32_t *inout, int kind, double x, double y, double w, double h, uint32_t argb,
+                    int penw);
 void oracle_bigfish_radius(const float *u, float *out, int64_t n);
 /* Qt raster replay of the tools/qt_raster_golden.cpp command format on a 64x64 RGB32 canvas */
 int oracle_qt_replay(const uint8_t *cmds, int64_t nbytes, uint32_t *canvas_inout);

@@ -27,9 +27,11 @@ def libs():
         pytest.skip("oracle/_ref/libqt_probe.so not built (needs Qt at build time)")
     q = ctypes.CDLL(PROBE)
     q.qtp_draw.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, D, U, I, I]
+    q.qtp_prim.argtypes = [I, I, P, I, D, D, D, D, U, I]
     o = oracle_lib.load()
     o.oracle_qt_smooth.argtypes = [I, I, P, I, P, I, I, I, I, D, D, D, D, D, U]
     o.oracle_qt_smooth_rot.argtypes = [I, I, P, P, I, I, I, I, D, D, D, D, D, D]
+    o.oracle_qt_prim.argtypes = [I, I, P, I, D, D, D, D, U, I]
     return q, o
 
 
@@ -129,6 +131,42 @@ def test_smooth_draw_image_rotated(W):
                                       % (iw, ih, mir, op, x, y, w, h, deg, W))
 
 
+@pytest.mark.parametrize("kind", [10, 11, 12, 13, 14])
+def test_compass_primitives(kind):
+    """jumper's compass primitives (jumper.cpp:137-177) under Antialiasing on a 512 canvas against the
+    real Qt: drawEllipse(QRectF) brush + 1-px pen (10), pen only (13), brush only (14) -- the gray
+    raster fill of the flattened outline and the antialiased cosmetic stroker; the translucent
+    drawEllipse(QRect) (12); drawLine(QLine) with a wide square-capped pen (11)."""
+    q, o = libs()
+    W = 512
+    rng = np.random.RandomState(700 + kind)
+    for k in range(250):
+        c = _canvas(rng, W)
+        a, b = c.copy(), c.copy()
+        penw = 1
+        if kind == 11:
+            x, y = rng.randint(-20, W + 20, 2)
+            x2, y2 = x + rng.randint(-120, 121), y + rng.randint(-120, 121)
+            if k % 7 == 0:
+                x2 = x  # vertical / horizontal needles
+            if k % 11 == 0:
+                y2 = y
+            args = (float(x), float(y), float(x2), float(y2))
+            penw = int(rng.choice([2, 3, 4, 5, 6, 8]))
+        else:
+            x, y = rng.uniform(-40, W + 10, 2)
+            w, h = rng.uniform(0.5, 160, 2)
+            if k % 3 == 0:
+                w = h  # the compass dial is round
+            if k % 17 == 0:
+                w, h = rng.uniform(0.3, 3, 2)  # tiny
+            args = (x, y, w, h)
+        col = 0x78ffffff if kind == 12 else 0xff000000 | int(rng.randint(0, 1 << 24))
+        q.qtp_prim(W, W, a.ctypes.data, kind, *args, col, penw)
+        o.oracle_qt_prim(W, W, b.ctypes.data, kind, *args, col, penw)
+        np.testing.assert_array_equal(b, a, err_msg="kind %d case %d args %r pen %d" % (kind, k, args, penw))
+
+
 def replay(q, log, res):
     """The oracle's logged painter commands of one frame through the real Qt, on one canvas."""
     canvas = np.zeros((res, res), np.uint32) | np.uint32(0xff000000)
@@ -137,6 +175,9 @@ def replay(q, log, res):
         x, y, w, h = (float(v) for v in row[1:5])
         if kind == 1:
             canvas = _draw(q, canvas, 1, None, 6, 0, x, y, w, h, 1.0, int(row[5]))
+        elif kind >= 10:  # jumper's compass primitives (qtp_prim)
+            canvas = np.ascontiguousarray(canvas)
+            q.qtp_prim(res, res, canvas.ctypes.data, kind, x, y, w, h, int(row[5]), int(row[6]))
         else:  # 0: drawImage(QRectF); 2: translate(rect centre); rotate(row[9] degrees); drawImage
             ptr, dims, fm, op = int(row[5]), int(row[6]), int(row[7]), float(row[8])
             iw, ih = dims >> 16, dims & 0xffff
@@ -163,8 +204,7 @@ def test_rgb_array_frames_replayed_through_qt(game):
     painter call (background fill + image, grid tiles, entities, overlays); the same calls replayed
     through the real Qt with Antialiasing + SmoothPixmapTransform give the same pixels."""
     q, _ = libs()
-    kw = {"distribution_mode": 10} if game == "jumper" else {}  # memory mode: jumper draws no compass
-    orc = oracle_lib.OracleEnv(game, 1, num_levels=0, rand_seed=3, paint_vel_info=1, **kw)
+    orc = oracle_lib.OracleEnv(game, 1, num_levels=0, rand_seed=3, paint_vel_info=1)
     rng = np.random.RandomState(4)
     for t in range(40):
         orc.step(rng.randint(0, 15, 1).astype(np.int32))
@@ -175,3 +215,25 @@ def test_rgb_array_frames_replayed_through_qt(game):
         qt_frame = replay(q, log, 512)
         ref = np.stack([(qt_frame >> 16) & 255, (qt_frame >> 8) & 255, qt_frame & 255], -1).astype(np.uint8)
         np.testing.assert_array_equal(rgb[0], ref, err_msg="%s step %d" % (game, t))
+
+
+@pytest.mark.parametrize("opts", [{}, {"distribution_mode": 0}, {"center_agent": 0}])
+def test_rgb_array_jumper_compass_frames(opts):
+    """jumper's compass at 512 (dial ellipse, wide needle, distance bar, the translucent jump
+    ellipse while falling) in whole replayed frames, hard / easy mode and the uncentered view."""
+    q, _ = libs()
+    orc = oracle_lib.OracleEnv("jumper", 1, num_levels=0, rand_seed=5, **opts)
+    rng = np.random.RandomState(6)
+    kinds = set()
+    for t in range(240):
+        # up for 3 steps, then run or wait for 3: a mid-air second jump draws the jump ellipse
+        act = 5 if (t // 3) % 2 == 0 else int(rng.choice([1, 4, 7]))
+        orc.step(np.array([act], np.int32))
+        if t % 12 != 0 or t == 0:
+            continue
+        rgb, log = orc.render_rgb_array(512, log_cap=20000)
+        kinds |= {int(r[0]) for r in log}
+        qt_frame = replay(q, log, 512)
+        ref = np.stack([(qt_frame >> 16) & 255, (qt_frame >> 8) & 255, qt_frame & 255], -1).astype(np.uint8)
+        np.testing.assert_array_equal(rgb[0], ref, err_msg="jumper %r step %d" % (opts, t))
+    assert {10, 11, 12}.issubset(kinds), kinds

@@ -47,4 +47,35 @@ void qtp_draw(int cw, int ch, uint32_t *inout, int kind, const uint32_t *img, in
     copy_out(canvas, inout);
 }
 
+// jumper's compass primitives (jumper.cpp:137-177) under Antialiasing on a cw x ch RGB32 canvas:
+// kind 10 drawEllipse(QRectF) with QBrush(c) + QPen(c, 1); 13 the pen only; 14 the brush only;
+// 12 drawEllipse(QRect(int x, y, w, h)) with QBrush(argb, translucent) and no pen;
+// 11 drawLine(QLine(int x, y, w, h)) with QPen(c, penw).
+void qtp_prim(int cw, int ch, uint32_t *inout, int kind, double x, double y, double w, double h, uint32_t argb,
+              int penw) {
+    QImage canvas = wrap_in(inout, cw, ch, QImage::Format_RGB32);
+    {
+        QPainter p(&canvas);
+        p.setRenderHint(QPainter::Antialiasing, true);
+        p.setRenderHint(QPainter::SmoothPixmapTransform, true);
+        const QColor c = QColor::fromRgba(argb);
+        if (kind == 10 || kind == 13 || kind == 14) {
+            if (kind == 13) p.setBrush(Qt::NoBrush);
+            else p.setBrush(QBrush(c));
+            if (kind == 14) p.setPen(Qt::NoPen);
+            else p.setPen(QPen(c, 1));
+            p.drawEllipse(QRectF(x, y, w, h));
+        } else if (kind == 12) {
+            p.setBrush(c);
+            p.setPen(Qt::NoPen);
+            p.drawEllipse(QRect((int)x, (int)y, (int)w, (int)h));
+        } else if (kind == 11) {
+            p.setBrush(QBrush(c));
+            p.setPen(QPen(c, penw));
+            p.drawLine((int)x, (int)y, (int)w, (int)h);
+        }
+    }
+    copy_out(canvas, inout);
+}
+
 } // extern "C"
