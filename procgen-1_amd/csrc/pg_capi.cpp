@@ -883,12 +883,6 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     }
     if (num_envs % (int)gids.size() != 0) return bad("num_envs must be a multiple of the number of env names"); // vecgame.cpp:345
     if (env_offset < 0) return bad("env_offset must be >= 0");
-    if (render_human && distribution_mode != PG_MEMORY) // jumper's compass (jumper.cpp:137-177) draws an antialiased
-        for (int g : gids)                               // ellipse and line, not restated at RENDER_RES
-            if (g == PG_GAME_JUMPER)
-                return bad("render_mode=rgb_array is built for jumper only in memory mode (its compass is not restated "
-                           "at RENDER_RES)");
-
     VecEnv *v = new VecEnv();
     v->num_envs = num_envs;
     v->games = gids;

@@ -15,6 +15,7 @@
 // Every blit reproduces Qt's raster scale blit (qt_scale_image_32bit fixed-point
 // stepping, SourceOver on premultiplied ARGB32, painter opacity) bit for bit.
 #include "pg_device.h"
+#include "pg_assetgen.h"
 
 namespace {
 
@@ -2402,11 +2403,18 @@ struct HLine {
     int leftAf0, rightAf0, leftBf0, rightBf0, leftBfL, rightBfR, tlAf0, trAf0;
     int tlS, trS, blS, brS, itlS, itrS, iblS, ibrS;
 };
-DEV void hr_line(double ax, double ay, double bx, double by, double width, HLine &L) {
+DEV void hr_line(double ax, double ay, double bx, double by, double width, HLine &L, bool squareCap = false) {
     L.kind = 0;
     L.V.n = 0;
     double pax = ax, pay = ay, pbx = bx, pby = by;
     if ((hq_fz(ax - bx) && hq_fz(ay - by)) || width == 0) return;
+    if (squareCap) { // a wide pen's square caps: the line grows by half its (relative) width at both ends
+        const double c = 0.5f * width, dx = pbx - pax, dy = pby - pay;
+        pax -= dx * c;
+        pay -= dy * c;
+        pbx += dx * c;
+        pby += dy * c;
+    }
     {
         const double offx = fabs(by - ay) * width * 0.5, offy = fabs(bx - ax) * width * 0.5;
         const double cl = 0 - offx, ct = 0 - offy;
@@ -2807,8 +2815,6 @@ struct HRotLds {
     HSpanLds S;
     int tmp[HR_THREADS + 1];
 };
-template <bool ROT> struct HLds { HRotLds r; };
-template <> struct HLds<false> { int unused; };
 
 // tile_image (basic-abstract-game.cpp:849-877): num_tiles side by side (ratio > 0) or stacked (< 0)
 DEV void hr_tiles(uint32_t *frame, HOp op, float tile_ratio) {
@@ -2930,13 +2936,556 @@ DEV bool hr_entities(uint32_t *frame, const PGDev &d, const PGEnv &s, const View
     return ok;
 }
 
+// ---- jumper's compass at RENDER_RES (jumper.cpp:137-177 under Antialiasing; the oracle's
+// jp_draw_compass_smooth, pinned primitive by primitive against Qt 5.9.7 in tests/test_smooth_pins.py):
+//   drawEllipse(QRectF) with a brush and a 1-px pen -> the flattened 26.6 outline filled by the gray raster
+//       (qgrayraster.c cells accumulated by one lane into LDS, then swept one row per thread), then the
+//       antialiased QCosmeticStroker (one lane, on the dial's pixels staged in LDS);
+//   drawLine(QLine) with a wide pen -> rasterizeLine with square caps (rows across threads);
+//   fillRect(QRectF) -> hr_paint; drawEllipse(QRect) with a translucent brush -> the gray raster.
+#define HC_CX 136 // gray-raster cells per row, column 0 = the cells left of the clip
+#define HC_CY 134
+struct HCompassLds {
+    AgLds ag;
+    int n_poly;
+    int area[HC_CX * HC_CY]; // also the stroke's staged pixels
+    int16_t cover[HC_CX * HC_CY];
+};
+struct HcPainter { AgLds *ls; int err; }; // what ag_flatten needs of a painter
+
+// solid colour at coverage `cov` (blend_color_argb / comp_func_solid_SourceOver with const_alpha = cov)
+DEV void hc_blend_solid(uint32_t *d, uint32_t pm, int cov) {
+    if (cov <= 0) return;
+    const uint32_t c = cov == 255 ? pm : BYTE_MUL(pm, (uint32_t)cov);
+    const uint32_t a = c >> 24;
+    *d = a == 255 ? c : c + BYTE_MUL(*d, 255u - a);
+}
+
+// qgrayraster.c with PIXEL_BITS 8: cells (area, cover) in 24.8 inside the clip box (cells left of it in
+// column -1, right of it dropped)
+#define HC_PB 8
+#define HC_ONE (1 << HC_PB)
+struct HcRas {
+    int min_ex, max_ex, min_ey, max_ey, count_ex, count_ey;
+    int ex, ey, invalid, area, cover, x, y, last_ey;
+    int *ca;
+    int16_t *cc;
+};
+DEV void hc_record(HcRas &r) {
+    if (!r.invalid && (r.area | r.cover)) {
+        const int k = r.ey * (r.count_ex + 1) + (r.ex + 1);
+        r.ca[k] += r.area;
+        r.cc[k] = (int16_t)(r.cc[k] + r.cover);
+    }
+}
+DEV void hc_set_cell(HcRas &r, int ex, int ey) {
+    ey -= r.min_ey;
+    if (ex > r.max_ex) ex = r.max_ex;
+    ex -= r.min_ex;
+    if (ex < 0) ex = -1;
+    if (ex != r.ex || ey != r.ey) {
+        hc_record(r);
+        r.area = 0;
+        r.cover = 0;
+    }
+    r.ex = ex;
+    r.ey = ey;
+    r.invalid = ((unsigned)ey >= (unsigned)r.count_ey || ex >= r.count_ex);
+}
+DEV void hc_start_cell(HcRas &r, int ex, int ey) {
+    if (ex > r.max_ex) ex = r.max_ex;
+    if (ex < r.min_ex) ex = r.min_ex - 1;
+    r.area = 0;
+    r.cover = 0;
+    r.ex = ex - r.min_ex;
+    r.ey = ey - r.min_ey;
+    r.last_ey = ey << HC_PB;
+    r.invalid = 0;
+    hc_set_cell(r, ex, ey);
+}
+DEV int hc_trunc(int64_t x) { return (int)(x >> HC_PB); }
+DEV void hc_scanline(HcRas &r, int ey, int64_t x1, int y1, int64_t x2, int y2) {
+    int64_t dx = x2 - x1;
+    int ex1 = hc_trunc(x1), ex2 = hc_trunc(x2);
+    const int fx1 = (int)(x1 - ((int64_t)ex1 << HC_PB)), fx2 = (int)(x2 - ((int64_t)ex2 << HC_PB));
+    if (y1 == y2) {
+        hc_set_cell(r, ex2, ey);
+        return;
+    }
+    if (ex1 == ex2) {
+        const int delta = y2 - y1;
+        r.area += (fx1 + fx2) * delta;
+        r.cover += delta;
+        return;
+    }
+    int64_t p = (int64_t)(HC_ONE - fx1) * (y2 - y1);
+    int first = HC_ONE, incr = 1;
+    if (dx < 0) {
+        p = (int64_t)fx1 * (y2 - y1);
+        first = 0;
+        incr = -1;
+        dx = -dx;
+    }
+    int delta = (int)(p / dx), mod = (int)(p % dx);
+    if (mod < 0) {
+        delta--;
+        mod += (int)dx;
+    }
+    r.area += (fx1 + first) * delta;
+    r.cover += delta;
+    ex1 += incr;
+    hc_set_cell(r, ex1, ey);
+    y1 += delta;
+    if (ex1 != ex2) {
+        p = (int64_t)HC_ONE * (y2 - y1 + delta);
+        int lift = (int)(p / dx), rem = (int)(p % dx);
+        if (rem < 0) {
+            lift--;
+            rem += (int)dx;
+        }
+        mod -= (int)dx;
+        while (ex1 != ex2) {
+            delta = lift;
+            mod += rem;
+            if (mod >= 0) {
+                mod -= (int)dx;
+                delta++;
+            }
+            r.area += HC_ONE * delta;
+            r.cover += delta;
+            y1 += delta;
+            ex1 += incr;
+            hc_set_cell(r, ex1, ey);
+        }
+    }
+    delta = y2 - y1;
+    r.area += (fx2 + HC_ONE - first) * delta;
+    r.cover += delta;
+}
+DEV void hc_line_to(HcRas &r, int64_t to_x, int64_t to_y) {
+    int ey1 = hc_trunc(r.last_ey), ey2 = hc_trunc(to_y);
+    const int fy1 = (int)(r.y - r.last_ey), fy2 = (int)(to_y - ((int64_t)ey2 << HC_PB));
+    int64_t dx = to_x - r.x, dy = to_y - r.y;
+    const int mn = min(ey1, ey2), mx = max(ey1, ey2);
+    if (mn >= r.max_ey || mx < r.min_ey) {
+        // outside the clip rows: the pen moves, no cell
+    } else if (ey1 == ey2) {
+        hc_scanline(r, ey1, r.x, fy1, to_x, fy2);
+    } else if (dx == 0) {
+        int incr = 1;
+        const int ex = hc_trunc(r.x);
+        const int two_fx = (int)(((int64_t)r.x - ((int64_t)ex << HC_PB)) << 1);
+        int first = HC_ONE;
+        if (dy < 0) {
+            first = 0;
+            incr = -1;
+        }
+        int delta = first - fy1;
+        r.area += two_fx * delta;
+        r.cover += delta;
+        ey1 += incr;
+        hc_set_cell(r, ex, ey1);
+        delta = first + first - HC_ONE;
+        const int area = two_fx * delta;
+        while (ey1 != ey2) {
+            r.area += area;
+            r.cover += delta;
+            ey1 += incr;
+            hc_set_cell(r, ex, ey1);
+        }
+        delta = fy2 - HC_ONE + first;
+        r.area += two_fx * delta;
+        r.cover += delta;
+    } else {
+        int incr = 1;
+        int64_t p = (int64_t)(HC_ONE - fy1) * dx;
+        int first = HC_ONE;
+        if (dy < 0) {
+            p = (int64_t)fy1 * dx;
+            first = 0;
+            incr = -1;
+            dy = -dy;
+        }
+        int delta = (int)(p / dy), mod = (int)(p % dy);
+        if (mod < 0) {
+            delta--;
+            mod += (int)dy;
+        }
+        int64_t x = r.x + delta;
+        hc_scanline(r, ey1, r.x, fy1, x, first);
+        ey1 += incr;
+        hc_set_cell(r, hc_trunc(x), ey1);
+        if (ey1 != ey2) {
+            p = (int64_t)HC_ONE * dx;
+            int lift = (int)(p / dy), rem = (int)(p % dy);
+            if (rem < 0) {
+                lift--;
+                rem += (int)dy;
+            }
+            mod -= (int)dy;
+            while (ey1 != ey2) {
+                delta = lift;
+                mod += rem;
+                if (mod >= 0) {
+                    mod -= (int)dy;
+                    delta++;
+                }
+                const int64_t x2 = x + delta;
+                hc_scanline(r, ey1, x, HC_ONE - first, x2, first);
+                x = x2;
+                ey1 += incr;
+                hc_set_cell(r, hc_trunc(x), ey1);
+            }
+        }
+        hc_scanline(r, ey1, x, HC_ONE - first, to_x, fy2);
+    }
+    r.x = (int)to_x;
+    r.y = (int)to_y;
+    r.last_ey = ey2 << HC_PB;
+}
+DEV int hc_coverage(int area) { // gray_hline, odd-even
+    int c = area >> (HC_PB * 2 + 1 - 8);
+    if (c < 0) c = -c;
+    c &= 511;
+    if (c > 256) c = 512 - c;
+    else if (c == 256) c = 255;
+    return c;
+}
+// fill the closed 26.6 contour C.ag.poly[0, n) odd-even in `pm` (every thread calls it);
+// false = the cell box does not fit the LDS
+DEV bool hc_gray_fill(HCompassLds &C, int n, uint32_t pm, uint32_t *frame) {
+    const int tid = threadIdx.x;
+    if (n <= 0) return true;
+    int xmn = C.ag.poly[0].x, xmx = xmn, ymn = C.ag.poly[0].y, ymx = ymn;
+    for (int i = 1; i < n; i++) {
+        const int2 q = C.ag.poly[i];
+        xmn = min(xmn, q.x); xmx = max(xmx, q.x);
+        ymn = min(ymn, q.y); ymx = max(ymx, q.y);
+    }
+    HcRas r;
+    r.min_ex = xmn >> 6; r.min_ey = ymn >> 6; r.max_ex = (xmx + 63) >> 6; r.max_ey = (ymx + 63) >> 6;
+    if (r.max_ex <= 0 || r.min_ex >= HR_RES || r.max_ey <= 0 || r.min_ey >= HR_RES) return true;
+    r.min_ex = max(r.min_ex, 0); r.min_ey = max(r.min_ey, 0);
+    r.max_ex = min(r.max_ex, HR_RES); r.max_ey = min(r.max_ey, HR_RES);
+    r.count_ex = r.max_ex - r.min_ex;
+    r.count_ey = r.max_ey - r.min_ey;
+    if (r.count_ex + 1 > HC_CX || r.count_ey > HC_CY) return false;
+    const int stride = r.count_ex + 1, ncell = r.count_ey * stride;
+    for (int k = tid; k < ncell; k += HR_THREADS) {
+        C.area[k] = 0;
+        C.cover[k] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) { // gray_move_to(first), gray_line_to each point and back to the first (the close)
+        r.ca = C.area;
+        r.cc = C.cover;
+        r.invalid = 1;
+        r.ex = r.ey = 0;
+        r.area = r.cover = 0;
+        const int64_t x0 = (int64_t)C.ag.poly[0].x << (HC_PB - 6), y0 = (int64_t)C.ag.poly[0].y << (HC_PB - 6);
+        hc_start_cell(r, hc_trunc(x0), hc_trunc(y0));
+        r.x = (int)x0;
+        r.y = (int)y0;
+        for (int i = 1; i <= n; i++) {
+            const int2 q = C.ag.poly[i < n ? i : 0];
+            hc_line_to(r, (int64_t)q.x << (HC_PB - 6), (int64_t)q.y << (HC_PB - 6));
+        }
+        hc_record(r);
+    }
+    __syncthreads();
+    if (tid < r.count_ey) { // gray_sweep, one row per thread
+        uint32_t *row = frame + (size_t)(tid + r.min_ey) * HR_RES + r.min_ex;
+        const int *ca = C.area + tid * stride;
+        const int16_t *cc = C.cover + tid * stride;
+        int cover = 0, x = 0;
+        for (int cx = -1; cx < r.count_ex; cx++) {
+            if (ca[cx + 1] == 0 && cc[cx + 1] == 0) continue;
+            if (cx > x && cover != 0) {
+                const int c = hc_coverage(cover * (HC_ONE * 2));
+                for (int k = x; k < cx; k++) hc_blend_solid(&row[k], pm, c);
+            }
+            cover += cc[cx + 1];
+            const int area = cover * (HC_ONE * 2) - ca[cx + 1];
+            if (area != 0 && cx >= 0) hc_blend_solid(&row[cx], pm, hc_coverage(area));
+            x = cx + 1;
+        }
+        if (r.count_ex > x && cover != 0) {
+            const int c = hc_coverage(cover * (HC_ONE * 2));
+            for (int k = x; k < r.count_ex; k++) hc_blend_solid(&row[k], pm, c);
+        }
+    }
+    __syncthreads();
+    return true;
+}
+// QRasterPaintEngine::fill's early out: the control points' rect, toRect(), must meet the device
+DEV bool hc_path_on_device(const AgPtD *p, int n) {
+    double x0 = p[0].x, x1 = p[0].x, y0 = p[0].y, y1 = p[0].y;
+    for (int i = 1; i < n; i++) {
+        x0 = fmin(x0, p[i].x); x1 = fmax(x1, p[i].x);
+        y0 = fmin(y0, p[i].y); y1 = fmax(y1, p[i].y);
+    }
+    const int rx = qRound(x0), ry = qRound(y0), rw = qRound(x1 - x0), rh = qRound(y1 - y0);
+    if (rw == 0 && rh == 0) return false; // QRect::isNull
+    const int ax2 = rx + rw - 1, ay2 = ry + rh - 1;
+    int l1 = rx, r1 = rx, t1 = ry, b1 = ry;
+    if (ax2 - rx + 1 < 0) l1 = ax2; else r1 = ax2;
+    if (ay2 - ry + 1 < 0) t1 = ay2; else b1 = ay2;
+    return !(l1 > HR_RES - 1 || 0 > r1 || t1 > HR_RES - 1 || 0 > b1);
+}
+// the ellipse path filled by the gray raster: QOutlineMapper flattens the four curves (0.25) and
+// rounds to 26.6 (wave 0 flattens: the Bezier stack is shared LDS)
+DEV bool hc_fill_ellipse(HCompassLds &C, const AgPtD pts[13], uint32_t pm, uint32_t *frame) {
+    if (threadIdx.x < 64) {
+        HcPainter p = {&C.ag, 0};
+        C.ag.poly[0] = make_int2(ag_fixed(pts[0].x), ag_fixed(pts[0].y));
+        int n = 1;
+        AgPtD last = pts[0];
+        for (int k = 0; k < 4; k++) {
+            const AgBez b = {last.x, last.y, pts[3 * k + 1].x, pts[3 * k + 1].y, pts[3 * k + 2].x, pts[3 * k + 2].y,
+                             pts[3 * k + 3].x, pts[3 * k + 3].y};
+            n = ag_flatten(p, b, n);
+            last = pts[3 * k + 3];
+        }
+        if (threadIdx.x == 0) C.n_poly = p.err ? -1 : n;
+    }
+    __syncthreads();
+    const int n = C.n_poly;
+    if (n < 0) return false;
+    return hc_gray_fill(C, n, pm, frame);
+}
+
+// QCosmeticStroker::drawLineAntialiased<drawPixel, NoDasher> (lane 0): two pixels per major step
+// weighted by the minor fraction, the end pixels by their 26.6 coverage; pixels inside the staged box
+// [bx0, bx0 + bw) x [by0, by0 + bh) are blended in LDS (`box`), the others in the frame
+struct HcStroke {
+    uint32_t pm;
+    uint32_t *frame, *box;
+    int bx0, by0, bw, bh;
+};
+DEV void hc_cs_pixel(const HcStroke &k, int x, int y, int cov) {
+    if (x < 0 || x > HR_RES - 1 || y < 0 || y > HR_RES - 1) return;
+    const int lx = x - k.bx0, ly = y - k.by0;
+    uint32_t *d = (k.box && lx >= 0 && lx < k.bw && ly >= 0 && ly < k.bh) ? k.box + ly * k.bw + lx
+                                                                           : k.frame + (size_t)y * HR_RES + x;
+    hc_blend_solid(d, k.pm, (cov * 256) >> 8);
+}
+DEV void hc_cs_line(const HcStroke &k, AgStroker &s, double rx1, double ry1, double rx2, double ry2, int caps) {
+    if (ag_cs_clip(s, rx1, ry1, rx2, ry2)) return;
+    int x1 = ag_f26(rx1), y1 = ag_f26(ry1), x2 = ag_f26(rx2), y2 = ag_f26(ry2);
+    const int dx = x2 - x1, dy = y2 - y1;
+    if (abs(dx) < abs(dy)) { // vertical
+        const int xinc = ag_fdiv(dx, dy);
+        if (y1 > y2) {
+            int t = y1; y1 = y2; y2 = t;
+            t = x1; x1 = x2; x2 = t;
+            caps = ag_swap_caps(caps);
+        }
+        int x = (x1 - 32) * 1024;
+        x -= (((y1 & 63) - 32) * xinc) >> 6;
+        ag_cap_adjust(caps, y1, y2, x, xinc);
+        int y = y1 >> 6;
+        const int ys = y2 >> 6;
+        int aS, aE;
+        if (y == ys) { aS = y2 - y1; aE = 0; }
+        else { aS = 64 - (y1 & 63); aE = y2 & 63; }
+        {
+            const unsigned al = (uint8_t)(x >> 8);
+            hc_cs_pixel(k, x >> 16, y, (int)((255 - al) * aS) >> 6);
+            hc_cs_pixel(k, (x >> 16) + 1, y, (int)(al * aS) >> 6);
+        }
+        x += xinc;
+        ++y;
+        if (y < ys) {
+            do {
+                const unsigned al = (uint8_t)(x >> 8);
+                hc_cs_pixel(k, x >> 16, y, (int)(255 - al));
+                hc_cs_pixel(k, (x >> 16) + 1, y, (int)al);
+                x += xinc;
+            } while (++y < ys);
+        }
+        if (aE) {
+            const unsigned al = (uint8_t)(x >> 8);
+            hc_cs_pixel(k, x >> 16, y, (int)((255 - al) * aE) >> 6);
+            hc_cs_pixel(k, (x >> 16) + 1, y, (int)(al * aE) >> 6);
+        }
+    } else { // horizontal
+        if (!dx) return;
+        const int yinc = ag_fdiv(dy, dx);
+        if (x1 > x2) {
+            int t = x1; x1 = x2; x2 = t;
+            t = y1; y1 = y2; y2 = t;
+            caps = ag_swap_caps(caps);
+        }
+        int y = (y1 - 32) * 1024;
+        y -= (((x1 & 63) - 32) * yinc) >> 6;
+        ag_cap_adjust(caps, x1, x2, y, yinc);
+        int x = x1 >> 6;
+        const int xs = x2 >> 6;
+        int aS, aE;
+        if (x == xs) { aS = x2 - x1; aE = 0; }
+        else { aS = 64 - (x1 & 63); aE = x2 & 63; }
+        {
+            const unsigned al = (uint8_t)(y >> 8);
+            hc_cs_pixel(k, x, y >> 16, (int)((255 - al) * aS) >> 6);
+            hc_cs_pixel(k, x, (y >> 16) + 1, (int)(al * aS) >> 6);
+        }
+        y += yinc;
+        ++x;
+        if (x < xs) {
+            do {
+                const unsigned al = (uint8_t)(y >> 8);
+                hc_cs_pixel(k, x, y >> 16, (int)(255 - al));
+                hc_cs_pixel(k, x, (y >> 16) + 1, (int)al);
+                y += yinc;
+            } while (++x < xs);
+        }
+        if (aE) {
+            const unsigned al = (uint8_t)(y >> 8);
+            hc_cs_pixel(k, x, y >> 16, (int)((255 - al) * aE) >> 6);
+            hc_cs_pixel(k, x, (y >> 16) + 1, (int)(al * aE) >> 6);
+        }
+    }
+}
+// the 1-px pen along the four curves (renderCubicSubdivision on an explicit stack, no caps); the dial's
+// pixels are staged in LDS around lane 0's sequential blends
+DEV void hc_stroke_ellipse(HCompassLds &C, const AgPtD pts[13], uint32_t pm, uint32_t *frame) {
+    const int tid = threadIdx.x;
+    double x0 = pts[0].x, x1 = x0, y0 = pts[0].y, y1 = y0;
+    for (int i = 1; i < 13; i++) {
+        x0 = fmin(x0, pts[i].x); x1 = fmax(x1, pts[i].x);
+        y0 = fmin(y0, pts[i].y); y1 = fmax(y1, pts[i].y);
+    }
+    HcStroke k;
+    k.pm = pm;
+    k.frame = frame;
+    k.bx0 = max(0, (int)floor(x0) - 2);
+    k.by0 = max(0, (int)floor(y0) - 2);
+    k.bw = min(HR_RES, (int)ceil(x1) + 3) - k.bx0;
+    k.bh = min(HR_RES, (int)ceil(y1) + 3) - k.by0;
+    const bool staged = k.bw > 0 && k.bh > 0 && k.bw * k.bh <= HC_CX * HC_CY;
+    k.box = staged ? reinterpret_cast<uint32_t *>(C.area) : nullptr;
+    if (staged)
+        for (int p = tid; p < k.bw * k.bh; p += HR_THREADS)
+            k.box[p] = frame[(size_t)(k.by0 + p / k.bw) * HR_RES + k.bx0 + p % k.bw];
+    __syncthreads();
+    if (tid == 0) {
+        AgStroker s;
+        s.pm = pm;
+        s.xmin = -1; s.xmax = HR_RES + 1; s.ymin = -1; s.ymax = HR_RES + 1;
+        s.lastx = s.lasty = AG_INT_MIN;
+        s.lastDir = AG_L2R;
+        s.lastAxisAligned = false;
+        AgPtD *q = C.ag.cs;
+        int *st = C.ag.cstack;
+        for (int c = 0; c < 4; c++) {
+            q[3] = pts[3 * c];
+            q[2] = pts[3 * c + 1];
+            q[1] = pts[3 * c + 2];
+            q[0] = pts[3 * c + 3];
+            int sp = 0;
+            st[0] = 0 | (AG_CS_MAXSUB << 8);
+            while (sp >= 0) {
+                const int off = st[sp] & 0xff, level = st[sp] >> 8;
+                sp--;
+                AgPtD *pp = q + off;
+                if (level) {
+                    const double dx = pp[3].x - pp[0].x, dy = pp[3].y - pp[0].y;
+                    const double len = ((double).25) * (fabs(dx) + fabs(dy));
+                    if (fabs(dx * (pp[0].y - pp[2].y) - dy * (pp[0].x - pp[2].x)) >= len ||
+                        fabs(dx * (pp[0].y - pp[1].y) - dy * (pp[0].x - pp[1].x)) >= len) {
+                        ag_cs_split(pp);
+                        st[++sp] = off | ((level - 1) << 8);
+                        st[++sp] = (off + 3) | ((level - 1) << 8);
+                        continue;
+                    }
+                }
+                hc_cs_line(k, s, pp[3].x, pp[3].y, pp[0].x, pp[0].y, 0);
+            }
+        }
+    }
+    __syncthreads();
+    if (staged)
+        for (int p = tid; p < k.bw * k.bh; p += HR_THREADS)
+            frame[(size_t)(k.by0 + p / k.bw) * HR_RES + k.bx0 + p % k.bw] = k.box[p];
+    __syncthreads();
+}
+// drawEllipse(QRectF(x, y, w, h)): brush (0 = none) then a 1-px pen (0 = none), non-premultiplied ARGB
+DEV bool hc_draw_ellipse(HCompassLds &C, double x, double y, double w, double h, uint32_t brush, uint32_t pen,
+                         uint32_t *frame) {
+    if (w <= 0 || h <= 0) return true;
+    AgPtD pts[13];
+    ag_ellipse_points(x, y, w, h, pts);
+    bool ok = true;
+    if ((brush >> 24) && hc_path_on_device(pts, 13)) ok = hc_fill_ellipse(C, pts, ag_solid_premul(brush), frame);
+    if (pen >> 24) hc_stroke_ellipse(C, pts, ag_solid_premul(pen), frame);
+    return ok;
+}
+// drawLine(QLine(x1, y1, x2, y2)) with QPen(colour, width > 1), SquareCap: rasterizeLine(width / length)
+DEV void hc_wide_line(int x1, int y1, int x2, int y2, int width, uint32_t argb, uint32_t *frame) {
+    const double dx = (double)x2 - x1, dy = (double)y2 - y1, len = sqrt(dx * dx + dy * dy);
+    HLine L;
+    if (len == 0) // a point: the square cap alone, a horizontal line of the pen's width, relative width 1
+        hr_line(x1 - width * 0.5, y1, x1 + width * 0.5, y1, 1, L, false);
+    else
+        hr_line(x1, y1, x2, y2, width / len, L, true);
+    const uint32_t pm = ag_solid_premul(argb);
+    if (L.kind != 0)
+        for (int r = threadIdx.x; r < L.nrows; r += HR_THREADS)
+            hr_row_spans(L, r, [&](int sx, int sl, int sy, int sc) {
+                for (int xx = sx; xx < sx + sl; xx++) hc_blend_solid(frame + (size_t)sy * HR_RES + xx, pm, sc);
+            });
+    __syncthreads();
+}
+DEV bool hc_draw_compass(HCompassLds &C, uint32_t *frame, const PGDev &d, const PGEnv &s, const View &v, int env) {
+    const float u = v.unit, vd = v.view_dim, cd = s.gs.jp.compass_dim;
+    const float ax = (float)(vd - cd - .25), ay = .25f; // get_abs_rect (:812-814)
+    const double rx = (double)(ax * u), ry = (double)(ay * u), rw = (double)(cd * u), rh = (double)(cd * u);
+    bool ok = hc_draw_ellipse(C, rx, ry, rw, rh, 0xffa8a69eu, 0xffa8a69eu, frame); // QColor(168, 166, 158)
+    const float pen_thickness = (float)(HR_RES / (256.0 / cd));
+    const float cx = (float)(rx + rw / 2), cy = (float)(ry + rh / 2); // QRectF::center
+    const float cr = (float)(rw / 2 * .95);
+    const float agx = EFr(d, F_X, env, 0), agy = EFr(d, F_Y, env, 0), arx = EFr(d, F_RX, env, 0), ary = EFr(d, F_RY, env, 0);
+    const float gx = EFr(d, F_X, env, 1), gy = EFr(d, F_Y, env, 1);
+    const float theta = (float)atan2((double)(gy - agy), (double)(gx - agx)); // get_theta (:241-246)
+    double sn, cs;
+    pg_sincos_cr((double)theta, &sn, &cs);
+    const int x1 = (int)cx, y1 = (int)cy; // QPainter::drawLine(int, int, int, int)
+    const int x2 = (int)((double)cx + (double)cr * cs), y2 = (int)((double)cy - (double)cr * sn);
+    hc_wide_line(x1, y1, x2, y2, (int)pen_thickness, 0xfffcba03u, frame); // QColor(252, 186, 3)
+    const float ddx = agx - gx, ddy = agy - gy; // get_distance (:133-143)
+    const float dist = (float)sqrt((double)(ddx * ddx + ddy * ddy));
+    const float dist_pct = (float)((double)dist / (s.main_width * 1.4142135623730951));
+    const float bar_thickness = cd / 8;
+    HOp op;
+    op.kind = 1; op.px = nullptr; op.iw = op.ih = 0; op.rgb32 = 0; op.mir = 0; op.ca = 256;
+    op.x = (double)((float)(vd - cd - .25) * u); op.y = (double)((float)(.25 + cd) * u);
+    op.w = (double)(cd * dist_pct * u); op.h = (double)(bar_thickness * u); op.argb = 0xfffcba03u;
+    hr_run(frame, op);
+    if (s.gs.jp.jump_delta < 0 && !s.has_support) { // drawEllipse(QRect(...)), QColor(255, 255, 255, 120)
+        double r1x, r1y, r1w, r1h;
+        screen_rect(v, agx - arx, agy + ary, 2 * arx, 2 * ary, 0, r1x, r1y, r1w, r1h);
+        const int qx = (int)r1x, qy = (int)(r1y + r1h * (5.0 / 6)), qw = (int)r1w, qh = (int)(r1h / 3);
+        ok = hc_draw_ellipse(C, qx, qy, qw, qh, 0x78ffffffu, 0, frame) && ok;
+    }
+    return ok;
+}
+
+// the kernel's LDS: the rotated path's span lists (games with rotating entities) and, for jumper, the
+// compass's cells in the same bytes (the compass is painted after every entity)
+template <bool ROT, bool J> struct HLds { int unused; DEV HRotLds *rot() { return nullptr; } DEV HCompassLds *compass() { return nullptr; } };
+template <> struct HLds<true, false> { HRotLds r; DEV HRotLds *rot() { return &r; } DEV HCompassLds *compass() { return nullptr; } };
+template <> struct HLds<true, true> {
+    union { HRotLds r; HCompassLds c; };
+    DEV HRotLds *rot() { return &r; }
+    DEV HCompassLds *compass() { return &c; }
+};
+
 template <int G>
 __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, const int32_t *env_list, uint32_t *frames,
                                                                      uint8_t *rgb) {
     const PGDev d = game_view(dg, G);
-    __shared__ HLds<has_rotation<G>()> lds;
-    HRotLds *L = nullptr;
-    if constexpr (has_rotation<G>()) L = &lds.r;
+    __shared__ HLds<has_rotation<G>(), G == PG_GAME_JUMPER> lds;
+    HRotLds *L = lds.rot();
     const int env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
     const int slot = blockIdx.x; // frame / rgb rows of this launch
     uint32_t *frame = frames + (size_t)slot * HR_RES * HR_RES;
@@ -2961,6 +3510,11 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
             const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
             v.center_x = (float)(s.main_width / 2.0);
             v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
+            v.visibility = (float)s.main_width;
+        } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:138-142
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(2 * agent_ry));
             v.visibility = (float)s.main_width;
         } else {
             v.center_x = agent_x;
@@ -3054,8 +3608,8 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
         op.w = (double)(.5f * u); op.h = (double)(bar_height * u); op.argb = 0xff42f587u;
         hr_run(frame, op);
     }
-    if constexpr (G == PG_GAME_JUMPER) // the compass (jumper.cpp:137-177): not restated at RENDER_RES
-        if (s.opt_distribution_mode != PG_MEMORY) ok = false;
+    if constexpr (G == PG_GAME_JUMPER) // the compass (jumper.cpp:137-177), outside memory mode
+        if (s.opt_distribution_mode != PG_MEMORY) ok = hc_draw_compass(*lds.compass(), frame, d, s, v, env) && ok;
     if constexpr (G == PG_GAME_PLUNDER) { // plunder.cpp:66-77: juice and progress bars, get_abs_rect (:812-814)
         const float u = v.unit;
         op.kind = 1; op.x = (double)(.25f * u); op.y = (double)(.25f * u);

@@ -16,19 +16,14 @@ GAMES = ["coinrun", "bigfish", "maze", "miner", "chaser", "climber", "ninja", "b
 ROTATING = ["bossfight", "caveflyer", "dodgeball", "fruitbot", "heist", "leaper", "plunder", "starpilot"]
 
 
-def game_kw(game):
-    # jumper draws its compass (jumper.cpp:137-177) outside memory mode: not restated at RENDER_RES
-    return {"distribution_mode": "memory"} if game == "jumper" else {}
-
-
-def run_rgb_array(game, num, steps, every, seed, **kw):
+def run_rgb_array(game, num, steps, every, seed, actions=None, **kw):
     env = make_gpu(num, game, render_mode="rgb_array", **kw)
     orc = OracleEnv(game, num, **oracle_kw(kw))
     rng = np.random.RandomState(seed)
     checked = 0
     for t in range(steps + 1):
         if t:
-            act = rng.randint(0, 15, size=num).astype(np.int32)
+            act = (rng.randint(0, 15, size=num) if actions is None else rng.choice(actions, size=num)).astype(np.int32)
             env.act(act)
             orc.step(act)
         if t % every:
@@ -50,7 +45,7 @@ def run_rgb_array(game, num, steps, every, seed, **kw):
 
 @pytest.mark.parametrize("game", GAMES)
 def test_rgb_array_parity(game):
-    assert run_rgb_array(game, 4, 60, 6, seed=50, num_levels=0, rand_seed=31, **game_kw(game)) == 11
+    assert run_rgb_array(game, 4, 60, 6, seed=50, num_levels=0, rand_seed=31) == 11
 
 
 @pytest.mark.parametrize("game", ROTATING)
@@ -58,12 +53,6 @@ def test_rgb_array_rotated_long(game):
     """longer runs of the games whose entities rotate (the antialiased rotated drawImage, tiles,
     starpilot's scrolling background, plunder's bars), 8 envs, frames every 25 steps."""
     assert run_rgb_array(game, 8, 200, 25, seed=53, num_levels=0, rand_seed=35) == 9
-
-
-def test_rgb_array_jumper_compass_rejected():
-    from procgen_amd import ProcgenGym3Env
-    with pytest.raises(Exception):
-        ProcgenGym3Env(num=2, env_name="jumper", render_mode="rgb_array")
 
 
 @pytest.mark.parametrize("game", ["coinrun", "maze", "ninja"])
@@ -83,3 +72,23 @@ def test_rgb_array_mixed_batch():
         orc = OracleEnv(("coinrun", "maze")[e % 2], 1, env_offset=e, num_levels=0, rand_seed=34)
         np.testing.assert_array_equal(np.asarray(info[e]["rgb"]), orc.render_rgb_array(512)[0])
     env.close()
+
+
+@pytest.mark.parametrize("kw", [{"distribution_mode": "easy"}, {"distribution_mode": "hard"},
+                                {"distribution_mode": "easy", "center_agent": False},
+                                {"distribution_mode": "hard", "center_agent": False},
+                                {"distribution_mode": "memory"}],
+                         ids=["easy", "hard", "easy_uncentered", "hard_uncentered", "memory"])
+def test_rgb_array_jumper_compass(kw):
+    """jumper's compass at RENDER_RES (jumper.cpp:137-177): the dial (gray-raster ellipse fill + antialiased
+    cosmetic pen), the wide square-capped needle, the distance bar and the translucent jump ellipse, in every
+    distribution mode (exploration is hard mode's compass) and both views; 8 envs, 150 steps, frames every 10 steps."""
+    assert run_rgb_array("jumper", 8, 150, 10, seed=57, num_levels=0, rand_seed=41, **kw) == 16
+
+
+@pytest.mark.parametrize("kw", [{"distribution_mode": "easy"}, {"distribution_mode": "hard", "center_agent": False}],
+                         ids=["easy", "hard_uncentered"])
+def test_rgb_array_jumper_jump_ellipse(kw):
+    """jump-heavy actions, every frame checked: the translucent ellipse under the agent after a mid-air jump
+    (jumper.cpp:163-166; in env 0 of the oracle at steps 9, 20, 38, 47 (easy) / 9, 21, 37, 55 (hard, uncentered))."""
+    assert run_rgb_array("jumper", 8, 60, 1, seed=57, actions=[2, 5, 8, 1, 7], num_levels=0, rand_seed=41, **kw) == 61
