@@ -101,13 +101,13 @@ def host_path_rate(game, num_levels, E, steps):
         env = ProcgenGym3Env(num=E, env_name=game, num_levels=num_levels, start_level=0, rand_seed=0,
                              distribution_mode="hard", reuse_arrays=reuse)
         rng = np.random.RandomState(0)
-        acts = rng.randint(0, 15, size=(steps + 2, E)).astype(np.int32)
-        for k in range(2):
+        acts = rng.randint(0, 15, size=(steps + 4, E)).astype(np.int32)
+        for k in range(4):
             env.act(acts[k])
             env.observe()
         t0 = time.perf_counter()
         for k in range(steps):
-            env.act(acts[2 + k])
+            env.act(acts[4 + k])
             rew, ob, first = env.observe()
             info = env.get_info_arrays()
         dt = time.perf_counter() - t0
@@ -148,7 +148,7 @@ def main():
     ap.add_argument("--settle", type=int, default=300,
                     help="untimed steps after the warmup so that episodes, resets and entity lists reach "
                          "steady state before the timed window (reported as settle_steps)")
-    ap.add_argument("--host-steps", type=int, default=8,
+    ap.add_argument("--host-steps", type=int, default=24,
                     help="steps of the host-buffer (libenv observe -> numpy) path reported as host_path; 0 = skip")
     ap.add_argument("--gather", action="store_true",
                     help="after every step, RCCL all-gather of every rank's uint8[E,64,64,3] obs shard into a "
@@ -160,7 +160,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    # --gather under a launcher (WORLD_SIZE set) runs RCCL even at world 1, so the single-GPU line
+    # times the same all_gather_into_tensor the 8-GPU node runs
+    if world > 1 or (args.gather and "WORLD_SIZE" in os.environ):
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))

@@ -341,6 +341,12 @@ struct VecEnv {
     // buffers before observe), so part 0's copy runs while part 1 still renders; copy_out then only
     // moves the small planes
     bool obs_early = false, obs_inflight = false;
+    // the per-part obs DMAs (obs_early) run on their own normal-priority stream: issued on a part's
+    // high-priority chain stream the runtime made them a blit kernel (copyBuffer) that held the CUs
+    // for the whole 7 ms transfer and stalled the other part's render behind it
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_cdone = nullptr;
+    std::vector<hipEvent_t> ev_rendered;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev; // per timed step: 4 per game (before step, after step, after reset,
@@ -385,6 +391,7 @@ struct VecEnv {
     // level prefetch (PGDev::sp_*): the spare generation of act t runs on pstreams[t % npstreams];
     // the reset of act t waits for the generation launched at act t - lag (ev_pre[t % lag])
     bool prefetch = false;
+    uint32_t prefetch_games = 0; // bit g: game g's chains use the prefetch (mixed batches: only some)
     int act_no = 0, lag = 2, npstreams = 1;
     hipStream_t pstreams[2] = {nullptr, nullptr};
     hipEvent_t ev_pre[PG_SP_LAG_MAX] = {};
@@ -516,9 +523,12 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             if (v->ev_pre_set[i]) HIPCHECK(hipStreamWaitEvent(r, v->ev_pre[i], 0));
             HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, r));
         }
-        pg_launch_reset(&v->dev, game, list, cnt, r, 0, 0, act, slot);
+        const bool pfk = v->prefetch && ((v->prefetch_games >> game) & 1);
+        PGDev dk = v->dev;
+        if (!pfk) dk.sp_envs = nullptr; // this chain neither swaps in spares nor requests them
+        pg_launch_reset(&dk, game, list, cnt, r, 0, 0, act, slot);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 3], r));
-        if (v->prefetch) { // the next levels of the envs just reset, off the critical path
+        if (pfk) { // the next levels of the envs just reset, off the critical path
             hipStream_t p = v->pstreams[act % v->npstreams];
             HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
             HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
@@ -548,10 +558,16 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
         if (v->obs_early && split) { // host buffers: this part's observations leave as soon as it rendered
             const size_t lo = (size_t)v->chain_lo(k) * PG_OBS_BYTES;
+            HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
+            HIPCHECK(hipStreamWaitEvent(v->cstream, v->ev_rendered[k], 0));
             HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo, (size_t)cnt * PG_OBS_BYTES,
-                                    hipMemcpyDeviceToHost, s));
+                                    hipMemcpyDeviceToHost, v->cstream));
             v->obs_inflight = true;
         }
+    }
+    if (v->obs_inflight) { // observe() synchronizes the engine stream: it waits for the obs DMAs too
+        HIPCHECK(hipEventRecord(v->ev_cdone, v->cstream));
+        HIPCHECK(hipStreamWaitEvent(v->stream, v->ev_cdone, 0));
     }
     for (size_t j = 1; j < v->gstreams.size() && C > 1; j++) { // join, after every chain is enqueued
         bool used = false;
@@ -915,10 +931,15 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             ok = (gids.size() > 1 || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) &&
                  hipEventCreateWithFlags(&a, hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&b, hipEventDisableTiming) == hipSuccess;
+            hipEvent_t c = nullptr;
+            ok = ok && hipEventCreateWithFlags(&c, hipEventDisableTiming) == hipSuccess;
             v->rstreams.push_back(s);
             v->ev_stepped.push_back(a);
             v->ev_reset.push_back(b);
+            v->ev_rendered.push_back(c);
         }
+        ok = ok && hipStreamCreateWithFlags(&v->cstream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_cdone, hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             libenv_close((libenv_env *)v);
             return bad("hipStreamCreate failed");
@@ -1025,10 +1046,32 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     // the other envs: caveflyer 24.5 -> 29.6, jumper 20.6 -> 21.7 M env-steps/s); the others lose
     // 1-5 % to the extra work (profiles/r03/prefetch_sweep.txt).  PROCGEN_MI355X_PREFETCH=0 / 1 forces
     // it off / on.
+    // In a mixed batch it is off by default: forced on for every game it lost (16.3 -> 10.7 M
+    // env-steps/s, profiles/r03/k_mixed16_prefetch), and so did serving only the chains whose level
+    // generation bounds them (jumper, caveflyer: 20.5 -> 14.4 M, profiles/r04/r04_d_*).
+    // PROCGEN_MI355X_PREFETCH_GAMES (a comma list of game names, or "all") picks the chains.
     {
         const char *pf = getenv("PROCGEN_MI355X_PREFETCH");
-        const bool by_game = gids.size() == 1 && (gids[0] == PG_GAME_CAVEFLYER || gids[0] == PG_GAME_JUMPER);
+        const char *pg = getenv("PROCGEN_MI355X_PREFETCH_GAMES");
+        const bool by_game = (gids.size() == 1 && (gids[0] == PG_GAME_CAVEFLYER || gids[0] == PG_GAME_JUMPER)) ||
+                             (pg != nullptr && pg[0] != 0);
         v->prefetch = !use_generated_assets && !use_sequential_levels && (pf ? pf[0] != '0' : by_game);
+        v->prefetch_games = 0;
+        std::string sel = pg ? std::string(pg) : "all";
+        uint32_t want = 0;
+        if (sel == "all") {
+            want = ~0u;
+        } else {
+            size_t a = 0;
+            while (a <= sel.size()) {
+                const size_t b = std::min(sel.find(',', a), sel.size());
+                const int g = game_id(sel.substr(a, b - a));
+                if (g >= 0) want |= 1u << g;
+                a = b + 1;
+            }
+        }
+        for (int g : gids) v->prefetch_games |= want & (1u << g);
+        if (!v->prefetch_games) v->prefetch = false;
         const char *lg = getenv("PROCGEN_MI355X_PREFETCH_LAG"), *ps = getenv("PROCGEN_MI355X_PREFETCH_STREAMS");
         if (lg) v->lag = std::min(std::max(atoi(lg), 1), PG_SP_LAG_MAX);
         if (ps) v->npstreams = std::min(std::max(atoi(ps), 1), 2);
@@ -1265,8 +1308,11 @@ LIBENV_API int procgen_start(libenv_env *env) {
     if (v->prefetch) HIPCHECK(hipMemsetAsync(v->dev.sp_count, 0, PG_NUM_GAMES * 4, v->stream)); // ring slot 0, every game
     for (size_t k = 0; k < v->games.size(); k++) {
         PG_POISON(v->stream);
-        pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag, v->games[k]);
-        if (v->prefetch) { // the spares of the first episodes (requested at act -lag, ring slot 0, usable from act 0)
+        const bool pfk = v->prefetch && ((v->prefetch_games >> v->games[k]) & 1);
+        PGDev dk = v->dev;
+        if (!pfk) dk.sp_envs = nullptr;
+        pg_launch_reset(&dk, v->games[k], v->list_of(k), v->count_of(), v->stream, 1, 0, -v->lag, v->games[k]);
+        if (pfk) { // the spares of the first episodes (requested at act -lag, ring slot 0, usable from act 0)
             HIPCHECK(hipEventRecord(v->ev_reset[k], v->stream));
             HIPCHECK(hipStreamWaitEvent(v->pstreams[0], v->ev_reset[k], 0));
             pg_launch_reset(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->pstreams[0], 2, 0, -v->lag, v->games[k]);
@@ -1345,6 +1391,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
         if (s) (void)hipStreamSynchronize(s);
     for (auto &s : v->gstreams)
         if (s) (void)hipStreamSynchronize(s);
+    if (v->cstream) (void)hipStreamSynchronize(v->cstream);
     if (v->stream) (void)hipStreamSynchronize(v->stream);
     unregister_buffers(v);
     for (void *p : v->allocs) hipFree(p);
@@ -1359,6 +1406,10 @@ LIBENV_API void libenv_close(libenv_env *env) {
         if (e) hipEventDestroy(e);
     for (auto &e : v->ev_reset)
         if (e) hipEventDestroy(e);
+    for (auto &e : v->ev_rendered)
+        if (e) hipEventDestroy(e);
+    if (v->ev_cdone) hipEventDestroy(v->ev_cdone);
+    if (v->cstream) hipStreamDestroy(v->cstream);
     for (auto &s : v->rstreams)
         if (s) hipStreamDestroy(s);
     for (auto &p : v->pstreams)

@@ -81,6 +81,9 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 struct FB {
     uint32_t *p; // LDS rows of the pass
     int y0, h;
+#ifdef PG_PROF_STAMP
+    PTimer *sp; // diagnostic: stamp_images' sub-phases (VARIANT=stamp EXTRA="-DPG_PROFILE -DPG_PROF_STAMP")
+#endif
     DEV bool row_in(int row) const { return (unsigned)(row - y0) < (unsigned)h; }
     DEV bool o_in(int o) const { return (unsigned)(o - y0 * PG_RES) < (unsigned)(h * PG_RES); }
     DEV uint32_t &operator[](int o) const { return p[o - y0 * PG_RES]; }
@@ -704,6 +707,11 @@ DEV void rot_stamp_lds(const FB &fb, const PGDev &d, const uint8_t *aux, int rd,
     }
 }
 
+#ifdef PG_PROF_STAMP
+#define SPM(k) fb.sp->mark(k)
+#else
+#define SPM(k)
+#endif
 template <bool TILES, int EGN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
 
@@ -753,135 +761,224 @@ DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img
     }
 }
 
-// Images of `m` in ascending lane order.  Per group of EG images, the texel of this lane's pixel of
-// every small one (<= 64 px: plain blits, fills, transform blits with a descriptor) is loaded first
-// (loads are order-free), then the group is blended strictly in order; larger, tiled and
-// set-up-in-order images run their own loops at their turn.
+// One image that is not batched (a transform blit set up in order, a descriptor blit or plain blit of
+// more than 64 px, a tile list): all lanes over its footprint, at its turn.
+template <bool TILES, int EGN>
+DEV void stamp_big(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, bool &err) {
+    const int lane = LANE;
+    const uint32_t npix = d.num_pixels;
+    const int caj = readlane(im.ca, j);
+    const int rk = readlane(im.rot, j);
+    if (rk == 2) {
+        rot_stamp_lds(fb, d, aux, readlane(im.rdi, j), err);
+        SPM(2);
+        return;
+    }
+    if (rk) {
+        const double m11 = readlane_d(im.m11, j);
+        if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
+                          readlane_d(im.rh, j), m11, readlane_d(im.m12, j), readlane_d(im.m21, j), m11,
+                          (uint32_t)readlane(im.soff, j), readlane(im.sw, j), readlane(im.sh, j),
+                          readlane(im.mir, j) != 0, caj))
+            err = true;
+        SPM(3);
+        return;
+    }
+    if (readlane(im.ntile, j) > 0) {
+        if constexpr (TILES) stamp_tiles<EGN>(fb, d, aux, im, j, caj, err);
+        else err = true; // unreachable: tile lists hold plain images only
+        SPM(4);
+        return;
+    }
+    const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
+    if (readlane((int)im.fill, j) != 0) {
+        const uint32_t col = (uint32_t)readlane((int)im.fill, j);
+        const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
+        for (int p = lane; p < nx * ny; p += 64)
+            if (fb.row_in(ty + p / nx)) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
+        SPM(5);
+    } else {
+        Axis ex, ey;
+        ex.t1 = readlane(im.ex.t1, j); ex.n = nx; ex.base = (uint32_t)readlane((int)im.ex.base, j);
+        ex.step = readlane(im.ex.step, j);
+        ey.t1 = readlane(im.ey.t1, j); ey.n = ny; ey.base = (uint32_t)readlane((int)im.ey.base, j);
+        ey.step = readlane(im.ey.step, j);
+        blit_seq(fb, d, ex, ey, (uint32_t)readlane(im.soff, j), readlane(im.sw, j), readlane(im.mir, j), caj, err);
+        SPM(6);
+    }
+}
+
+// inclusive prefix sum over the wave's lanes
+DEV int wave_incl_scan(int v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(v, off);
+        if (LANE >= off) v += t;
+    }
+    return v;
+}
+
+// Images of `m` in ascending lane order.  "Small" images (a plain blit or fill of <= 64 px, a
+// descriptor transform blit whose box is <= 64 px) are drawn in batches: a run of consecutive small
+// images becomes up to EGN * 64 (image, pixel) jobs, lane = job, each round's texel loads issued
+// before any blend (one gather latency per batch instead of one per few images), then the batch's
+// images are blended strictly in order, each from the rounds holding its jobs.  The others are drawn
+// at their turn (stamp_big).  Per image the result is the reference's in-order SourceOver.
 template <bool TILES, int EGN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
+    constexpr int CAP = EGN * 64;
     const int lane = LANE;
-    const float inv_l = 1.0f / (float)(im.draw && !im.rot && im.ex.n > 0 ? im.ex.n : 1);
     const uint32_t npix = d.num_pixels;
-    while (m) {
-        int js[EGN];
-#pragma unroll
-        for (int g = 0; g < EGN; g++) {
-            js[g] = m ? __ffsll((long long)m) - 1 : -1;
-            if (m) m &= m - 1;
+    SPM(7);
+    // this lane's image: small or not, and its job count (its pixels, or its transform blit's box)
+    int cnt = 0;
+    bool small = false;
+    if ((m >> lane) & 1) {
+        if (im.rot == 2) {
+            const int tot = rot_total(rot_desc(aux, im.rdi));
+            small = tot <= 64;
+            cnt = tot;
+        } else if (im.rot == 0 && im.ntile == 0) {
+            const int t = im.ex.n * im.ey.n;
+            small = t <= 64;
+            cnt = t;
         }
+    }
+    const unsigned long long smask = ballot(small);
+    while (m) {
+        const int j0 = __ffsll((long long)m) - 1;
+        if (!((smask >> j0) & 1)) {
+            m &= m - 1;
+            stamp_big<TILES, EGN>(fb, d, aux, im, j0, err);
+            asm volatile("" ::: "memory");
+            continue;
+        }
+        // the run of small images up to the next big one, cut where its jobs exceed CAP
+        const unsigned long long big = m & ~smask;
+        const unsigned long long run = big ? (m & ((1ull << (__ffsll((long long)big) - 1)) - 1)) : m;
+        const int v = ((run >> lane) & 1) ? cnt : 0;
+        const int incl = wave_incl_scan(v), excl = incl - v;
+        const unsigned long long bm = run & ballot(incl <= CAP);
+        const int total = readlane(incl, 63 - __clzll(bm));
+        m &= ~bm;
+        // fetch: job q -> its image jj (the first lane whose inclusive prefix exceeds q), pixel q - excl.
+        // The cross-lane reads (ds_bpermute) run with every lane active: a lane the branch would
+        // disable does not supply its value.
         uint32_t tv[EGN];
         int fo[EGN];
-        bool on[EGN], pre[EGN];
         uint32_t part = 0;
 #pragma unroll
-        for (int g = 0; g < EGN; g++) {
-            on[g] = false;
-            pre[g] = false;
-            tv[g] = 0;
-            fo[g] = 0;
-            const int j = js[g];
-            if (j < 0) continue;
-            const int rk = readlane(im.rot, j);
-            if (rk == 1 || readlane(im.ntile, j) > 0) continue;
-            if (rk == 2) {
-                const RotD r = rot_desc(aux, readlane(im.rdi, j));
-                const int total = rot_total(r);
-                if (total > 64) continue;
-                pre[g] = true;
-                if (lane < total) {
-                    int o;
+        for (int r = 0; r < EGN; r++) {
+            tv[r] = 0;
+            fo[r] = -1;
+            if (r * 64 >= total) continue; // uniform
+            const int q = r * 64 + lane;
+            const bool live = q < total;
+            const int qq = live ? q : 0;
+#ifdef PG_STAMP_LINEAR
+            int jj = 0;
+            for (unsigned long long bb = bm; bb; bb &= bb - 1) {
+                const int j = __ffsll((long long)bb) - 1;
+                if (qq >= readlane(excl, j) && qq < readlane(incl, j)) jj = j;
+            }
+#else
+            int lo = 0, hi = 63;
+#pragma unroll
+            for (int it = 0; it < 6; it++) {
+                const int mid = (lo + hi) >> 1;
+                if (__shfl(incl, mid) > qq) hi = mid;
+                else lo = mid + 1;
+            }
+            const int jj = lo;
+#endif
+            const int p = qq - __shfl(excl, jj);
+            const int rk = __shfl(im.rot, jj), rdi = __shfl(im.rdi, jj);
+            const int nx = __shfl(im.ex.n, jj), ext1 = __shfl(im.ex.t1, jj), eyt1 = __shfl(im.ey.t1, jj);
+            const uint32_t fillj = (uint32_t)__shfl((int)im.fill, jj);
+            const int swj = __shfl(im.sw, jj), mirj = __shfl((int)im.mir, jj), soffj = __shfl((int)im.soff, jj);
+            const uint32_t exb = (uint32_t)__shfl((int)im.ex.base, jj), eyb = (uint32_t)__shfl((int)im.ey.base, jj);
+            const int exs = __shfl(im.ex.step, jj), eys = __shfl(im.ey.step, jj);
+            int o = -1;
+            uint32_t t = 0;
+            bool ok = false;
+            if (live) {
+                if (rk == 2) {
+                    const RotD rd = rot_desc(aux, rdi);
                     uint32_t idx;
-                    if (rot_pixel(r, lane, 1.0f / (float)rot_nx(r), o, idx) && fb.o_in(o)) {
+                    if (rot_pixel(rd, p, 1.0f / (float)rot_nx(rd), o, idx) && fb.o_in(o)) {
                         if (idx < npix) {
-                            tv[g] = d.pixels[idx];
-                            fo[g] = o;
-                            on[g] = true;
+                            t = d.pixels[idx];
+                            ok = true;
+                        } else {
+                            err = true;
+                        }
+                    }
+                } else {
+                    const float inv = 1.0f / (float)nx;
+                    const int py = (int)(((float)p + 0.5f) * inv);
+                    const int pxx = p - py * nx;
+                    o = (eyt1 + py) * PG_RES + ext1 + pxx;
+                    if (!fb.o_in(o)) {
+                        // another pass's row
+                    } else if (fillj != 0) {
+                        t = fillj;
+                        ok = true;
+                    } else {
+                        int scol = (int)((exb + (uint32_t)(pxx * exs)) >> 16);
+                        const int srow = (int)((eyb + (uint32_t)(py * eys)) >> 16);
+                        if (mirj) scol = swj - 1 - scol;
+                        const uint32_t idx = (uint32_t)soffj + (uint32_t)(srow * swj + scol);
+                        if (idx < npix) {
+                            t = d.pixels[idx];
+                            ok = true;
                         } else {
                             err = true;
                         }
                     }
                 }
-                continue;
             }
-            const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
-            if (nx * ny > 64) continue;
-            pre[g] = true;
-            if (lane < nx * ny) {
-                const float inv = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, inv_l), j));
-                const int py = (int)(((float)lane + 0.5f) * inv);
-                const int pxx = lane - py * nx;
-                const uint32_t bxj = (uint32_t)readlane((int)im.ex.base, j), byj = (uint32_t)readlane((int)im.ey.base, j);
-                const int sxj = readlane(im.ex.step, j), syj = readlane(im.ey.step, j);
-                const int swj = readlane(im.sw, j);
-                int scol = (int)((bxj + (uint32_t)(pxx * sxj)) >> 16);
-                const int srow = (int)((byj + (uint32_t)(py * syj)) >> 16);
-                if (readlane(im.mir, j)) scol = swj - 1 - scol;
-                const uint32_t idx = (uint32_t)readlane(im.soff, j) + (uint32_t)(srow * swj + scol);
-                const int o = (readlane(im.ey.t1, j) + py) * PG_RES + readlane(im.ex.t1, j) + pxx;
-                const uint32_t fillj = (uint32_t)readlane((int)im.fill, j);
-                if (!fb.o_in(o)) {
-                    // another pass's row
-                } else if (fillj != 0) {
-                    tv[g] = fillj;
-                    fo[g] = o;
-                    on[g] = true;
-                } else if (idx < npix) {
-                    tv[g] = d.pixels[idx];
-                    fo[g] = o;
-                    on[g] = true;
-                } else {
-                    err = true;
-                }
+            // selects, not a conditional store: a conditional assignment into the tv / fo arrays was
+            // miscompiled (gfx950, hipcc of ROCm 7.2: the texel path's offset lost in a 64-bit
+            // register-pair copy of the array) -- parity caught it on coinrun
+            tv[r] = ok ? t : 0u;
+            fo[r] = ok ? o : -1;
+        }
+#ifdef PG_STAMP_DEBUG
+        {
+            const unsigned long long f0 = ballot(fo[0] >= 0), lv = ballot(lane < total);
+            if ((bm & 1ull) && d.prof && lane == 0) {
+                uint64_t *P = d.prof + (size_t)blockIdx.x * 16;
+                P[0] = (uint64_t)total; P[1] = (uint64_t)incl; P[2] = (uint64_t)cnt; P[3] = (uint64_t)im.ex.n;
+                P[4] = (uint64_t)im.ey.n; P[5] = bm; P[6] = run; P[7] = smask; P[8] = f0; P[9] = lv;
+                P[10] = (uint64_t)fb.y0; P[11] = (uint64_t)im.ey.t1; P[12] = (uint64_t)im.ex.t1; P[13] += 1;
             }
         }
+#endif
 #pragma unroll
-        for (int g = 0; g < EGN; g++) part |= on[g] ? alpha_partial(tv[g]) : 0u;
-        const bool binary = ballot(part != 0) == 0; // every prefetched texel has alpha 0 or 255
+        for (int r = 0; r < EGN; r++) part |= fo[r] >= 0 ? alpha_partial(tv[r]) : 0u;
+        const bool binary = ballot(part != 0) == 0; // every fetched texel has alpha 0 or 255
+        SPM(0);
+        // blend, image by image in order, from the rounds that hold its jobs
+        unsigned long long b = bm;
+        while (b) {
+            const int j = __ffsll((long long)b) - 1;
+            b &= b - 1;
+            const int jb = readlane(excl, j), je = readlane(incl, j), caj = readlane(im.ca, j);
+            const bool ob = binary && caj == 256;
 #pragma unroll
-        for (int g = 0; g < EGN; g++) {
-            const int j = js[g];
-            if (j < 0) continue;
-            const int caj = readlane(im.ca, j);
-            if (pre[g]) {
-                if (on[g]) fb[fo[g]] = (binary && caj == 256) ? over_binary(fb[fo[g]], tv[g]) : blend_argb_pm(fb[fo[g]], tv[g], caj);
-                continue;
+            for (int r = 0; r < EGN; r++) {
+                if (jb >= (r + 1) * 64 || je <= r * 64) continue; // uniform
+                const int q = r * 64 + lane;
+                if (q >= jb && q < je && fo[r] >= 0)
+                    fb[fo[r]] = ob ? over_binary(fb[fo[r]], tv[r]) : blend_argb_pm(fb[fo[r]], tv[r], caj);
             }
-            const int rk = readlane(im.rot, j);
-            if (rk == 2) {
-                rot_stamp_lds(fb, d, aux, readlane(im.rdi, j), err);
-                continue;
-            }
-            if (rk) {
-                const double m11 = readlane_d(im.m11, j);
-                if (!rotated_blit(fb, d.pixels, npix, readlane_d(im.rx, j), readlane_d(im.ry, j), readlane_d(im.rw, j),
-                                  readlane_d(im.rh, j), m11, readlane_d(im.m12, j), readlane_d(im.m21, j), m11,
-                                  (uint32_t)readlane(im.soff, j),
-                                  readlane(im.sw, j), readlane(im.sh, j), readlane(im.mir, j) != 0, caj))
-                    err = true;
-                continue;
-            }
-            if (readlane(im.ntile, j) > 0) {
-                if constexpr (TILES) stamp_tiles<EGN>(fb, d, aux, im, j, caj, err);
-                else err = true; // unreachable: tile lists hold plain images only
-                continue;
-            }
-            const int nx = readlane(im.ex.n, j), ny = readlane(im.ey.n, j);
-            if (readlane((int)im.fill, j) != 0) {
-                const uint32_t col = (uint32_t)readlane((int)im.fill, j);
-                const int tx = readlane(im.ex.t1, j), ty = readlane(im.ey.t1, j);
-                for (int p = lane; p < nx * ny; p += 64)
-                    if (fb.row_in(ty + p / nx)) fb[(ty + p / nx) * PG_RES + tx + p % nx] = col;
-            } else {
-                Axis ex, ey;
-                ex.t1 = readlane(im.ex.t1, j); ex.n = nx; ex.base = (uint32_t)readlane((int)im.ex.base, j);
-                ex.step = readlane(im.ex.step, j);
-                ey.t1 = readlane(im.ey.t1, j); ey.n = ny; ey.base = (uint32_t)readlane((int)im.ey.base, j);
-                ey.step = readlane(im.ey.step, j);
-                blit_seq(fb, d, ex, ey, (uint32_t)readlane(im.soff, j), readlane(im.sw, j), readlane(im.mir, j), caj,
-                         err);
-            }
-            // no barrier between images: one wave issues its LDS operations in order
+            // no hardware barrier between images (one wave issues its LDS operations in order), but a
+            // compiler one: images of one round use the same per-lane address register (fo[r]) under
+            // disjoint lane masks, and nothing else stops the compiler from keeping a lane's pixel in
+            // a register across the loop -- the next image's lanes must read what this image's wrote
+            asm volatile("" ::: "memory");
         }
+        SPM(1);
     }
 }
 
@@ -1413,7 +1510,13 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     constexpr int ROT_CAP = ONE_PASS ? AUX_BYTES / ROT_DESC_BYTES : rot_cap<G>();
     __shared__ __attribute__((aligned(16))) uint8_t rdesc_own[ONE_PASS ? 16 : (ROT_CAP > 0 ? ROT_CAP : 1) * ROT_DESC_BYTES];
     uint8_t *const rdesc = ONE_PASS ? aux : rdesc_own;
-    constexpr int EGK = 4; // images per texel-prefetch group (8 measured slower for every game)
+    // rounds of 64 pixel jobs per batch of small images: 8 where the frame's LDS already bounds the
+    // workgroups per CU (one pass: 16 more VGPRs cost no occupancy), else 4
+#ifdef PG_STAMP_ROUNDS
+    constexpr int EGK = PG_STAMP_ROUNDS;
+#else
+    constexpr int EGK = ONE_PASS ? 8 : 4;
+#endif
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
     // mode 0: every env of the list; 1: the envs whose step did not end the episode (drawn while
@@ -1759,8 +1862,16 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
         stamp_images<true, EGK>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z) && img_in_pass(im, fb)), err); \
     }
 
+#ifdef PG_PROF_STAMP
+    PTimer spt;
+    spt.start();
+#endif
     for (int pass = 0; pass < PG_RES / HR; pass++) {
+#ifdef PG_PROF_STAMP
+    const FB fb{fb_lds, pass * HR, HR, &spt};
+#else
     const FB fb{fb_lds, pass * HR, HR};
+#endif
     if (fast) {
         // ---- background + first tile column, pixel-centric, RB rows per batch (all loads of
         //      a batch are issued before the first blend).  A transparent texel (0) blends to
@@ -1955,6 +2066,10 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
     pt.mark(6);
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
+#ifdef PG_PROF_STAMP
+    spt.mark(7);
+    spt.flush(d.prof ? d.prof + (size_t)env * 16 : nullptr); // the step kernel's slots (it does not flush here)
+#endif
     census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
 }
 

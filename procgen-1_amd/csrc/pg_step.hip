@@ -1721,12 +1721,16 @@ DEV int mn_get(Ctx &c, int idx) { // get_obj(int idx) (basic-abstract-game.cpp:1
     if (!(0 <= idx && idx < c.s.main_width * c.s.main_height)) return c.s.out_of_bounds_object;
     return c.grid8[idx];
 }
+// c.moved: bit 0 = has_moved (miner.cpp), bit 1 = the cell was written this step (grid write-back)
 DEV void mn_set(Ctx &c, int idx, int v) {
-    if (LANE == 0) c.grid8[idx] = (int8_t)v;
+    if (LANE == 0) {
+        c.grid8[idx] = (int8_t)v;
+        c.moved[idx] |= 2;
+    }
     wave_sync();
 }
 DEV void mn_mark(Ctx &c, int idx) {
-    if (LANE == 0) c.moved[idx] = 1;
+    if (LANE == 0) c.moved[idx] |= 1;
     wave_sync();
 }
 DEV float mn_ax(Ctx &c) { return c.s.agent_erased ? c.s.ghost_x : EF(c, F_X, 0); }
@@ -1761,14 +1765,14 @@ DEV void mn_erase_agent(Ctx &c) {
     c.s.num_ents = n - 1;
 }
 
-// move_cell (miner.cpp:310-346) of one cell, uniform
-DEV void mn_move_cell(Ctx &c, int idx) {
+// move_cell (miner.cpp:310-346) of one cell, uniform.  agent_idx: the agent's cell, fixed for the
+// pass (the agent does not move while the cells do; an erased agent's ghost keeps its position)
+DEV void mn_move_cell(Ctx &c, int idx, int agent_idx) {
     const int w = c.s.main_width;
-    const bool current_moved = c.moved[idx] != 0;
+    const bool current_moved = (c.moved[idx] & 1) != 0;
     const int obj = mn_get(c, idx);
     const int obj_x = idx % w;
     const int stat_type = mn_stationary(obj);
-    const int agent_idx = mn_agent_index(c);
     // `BOULDER || DIAMOND && !moved`: && binds tighter
     if (!(stat_type == MN_BOULDER || (stat_type == MN_DIAMOND && !current_moved))) return;
     const int below_idx = idx - w;
@@ -1800,9 +1804,13 @@ DEV void mn_move_cell(Ctx &c, int idx) {
 
 // move_cell over rows [y0, y1), x ascending.  Only BOULDER / DIAMOND-like cells act, so a row is
 // a ballot (w <= 35 < 64 lanes) for the next acting cell at or right of the cursor, re-taken
-// after every move (a slide to x + 1 makes that cell act next, as in the reference's loop).
+// after every move (a slide to x + 1 makes that cell act next, as in the reference's loop).  A
+// resting object -- stationary, on something neither free nor round (or on the agent's free cell)
+// -- takes move_cell's last branch, which rewrites the cell with its own value: it is skipped.
+// The cell below a row is final once the row's pass starts (only that cell's own fall writes it).
 DEV void mn_move_rows(Ctx &c, int y0, int y1) {
     const int w = c.s.main_width;
+    const int agent_idx = mn_agent_index(c);
     for (int y = y0; y < y1; y++) {
         int xc = 0;
         while (xc < w) {
@@ -1810,13 +1818,18 @@ DEV void mn_move_rows(Ctx &c, int y0, int y1) {
             bool act = false;
             if (LANE < w - xc) {
                 const int idx = x + w * y;
-                const int st = mn_stationary(c.grid8[idx]);
-                act = st == MN_BOULDER || (st == MN_DIAMOND && !c.moved[idx]);
+                const int obj = c.grid8[idx];
+                const int st = mn_stationary(obj);
+                act = st == MN_BOULDER || (st == MN_DIAMOND && !(c.moved[idx] & 1));
+                if (act && obj == st) {
+                    const int below = mn_get(c, idx - w);
+                    if (below == SPACE ? agent_idx == idx - w : !mn_is_round(below)) act = false;
+                }
             }
             const unsigned long long b = ballot(act);
             if (!b) break;
             const int xa = xc + __ffsll((long long)b) - 1;
-            mn_move_cell(c, xa + w * y);
+            mn_move_cell(c, xa + w * y, agent_idx);
             xc = xa + 1;
         }
     }
@@ -1877,17 +1890,20 @@ DEV void miner_step_tail(Ctx &c) { // miner.cpp:262-307
         }
         c.s.diamonds_remaining = diamonds;
     }
-    // write the grid back: HBM int16 + its int8 mirror + the fork's latent state (miner.cpp:363-396)
+    // write the grid back: HBM int16 + its int8 mirror + the fork's latent state (miner.cpp:363-396),
+    // the cells written this step only (the three copies agree with the LDS grid everywhere else)
     const int cells = w * h;
     int16_t *g = c.d.grid + (size_t)c.env * PG_GRID_MAX;
     int8_t *g8 = c.d.grid8 + (size_t)c.env * PG_GRID_MAX;
     int32_t *lat = c.d.latent + (size_t)c.env * PG_LATENT_N;
-    for (int i = LANE; i < cells; i += 64) {
-        const int v = c.grid8[i];
-        g[i] = (int16_t)v;
-        g8[i] = (int8_t)v;
-        if (i < PG_LATENT_GRID) lat[2 + i] = v;
-    }
+    if (c.s.error == 0)
+        for (int i = LANE; i < cells; i += 64) {
+            if (!(c.moved[i] & 2)) continue;
+            const int v = c.grid8[i];
+            g[i] = (int16_t)v;
+            g8[i] = (int8_t)v;
+            if (i < PG_LATENT_GRID) lat[2 + i] = v;
+        }
     int ex = 0, ey = 0;
     for (int base = 0; base < c.s.num_ents; base += 64) { // the first EXIT entity
         int i = base + LANE;
@@ -2920,7 +2936,9 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
 #undef PG_W
     }
     c.pt.mark(6);
+#ifndef PG_PROF_STAMP // that diagnostic build fills these slots with the render's stamping sub-phases
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
+#endif
     c.cs.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
     return predicted && !done;
 }

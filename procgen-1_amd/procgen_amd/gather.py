@@ -82,7 +82,7 @@ class ObsGather:
             self.released[k] = None
         ctx = torch.cuda.stream(self.comm) if self.cuda else self.comm
         with ctx:
-            if self.dist is not None and self.world > 1:
+            if self.dist is not None:
                 self.dist.all_gather_into_tensor(self.out[k], self.local[k])
             else:
                 self.out[k].copy_(self.local[k], non_blocking=True)

@@ -9,7 +9,7 @@ import os
 import sys
 import json
 
-os.environ["PROCGEN_MI355X_LIB"] = "prof"
+os.environ.setdefault("PROCGEN_MI355X_LIB", "prof")
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "procgen-1_amd"))
 
