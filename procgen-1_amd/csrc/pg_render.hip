@@ -1498,7 +1498,12 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     // column per tile row; before it is built, the same LDS holds the Qt blit setup (t1, n, base,
     // step) of every window tile column / row (class 0 at [0, 128), class 1 at [128, 256) in int4
     // units).  General tile pass (decided after the fast path): GEN_AUX_BYTES of tables.
+#ifdef PG_AUX_TIGHT
+    // games without uniform tiles never take the fast path: tile_off + the column / row axis tables
+    constexpr int FAST_BYTES = uniform_tiles<G>() ? (NTYPES + CR * 64) * 4 : (NTYPES + 2 * 64 * 4) * 4;
+#else
     constexpr int FAST_BYTES = (NTYPES + CR * 64) * 4;
+#endif
     constexpr int AUX_BYTES = has_general<G>() && GEN_AUX_BYTES > FAST_BYTES ? GEN_AUX_BYTES : FAST_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t aux[AUX_BYTES];
     int *const tile_off = reinterpret_cast<int *>(aux);

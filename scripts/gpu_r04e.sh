@@ -23,4 +23,10 @@ for c in "-" "GPU_MAX_HW_QUEUES=8,PROCGEN_MI355X_MIXED_STREAMS=8" "GPU_MAX_HW_QU
 done
 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29541 GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python3 bench.py --gather --host-steps 0 --no-cpu-baseline > gpurun_out/e/gather_q8.json 2> gpurun_out/e/gather_q8.err || { tail -5 gpurun_out/e/gather_q8.err; exit 14; }
 python3 -c "import json; d=json.load(open('gpurun_out/e/gather_q8.json')); print('gather q8', round(d['value']/1e6,2), d['ms_per_step'])"
+for g in bossfight fruitbot; do
+  for L in "" aux; do
+    PROCGEN_MI355X_LIB=$L timeout -k 10 200 python3 bench.py --env-name $g --steps 50 --warmup 20 --settle 100 --host-steps 0 --no-cpu-baseline > gpurun_out/e/$g.$L.json 2> gpurun_out/e/$g.$L.err || { tail -5 gpurun_out/e/$g.$L.err; exit 15; }
+    python3 -c "import json; d=json.load(open('gpurun_out/e/$g.$L.json')); print('$g', 'lib=$L', round(d['value']/1e6,2), d['roofline']['kernel_ms'])"
+  done
+done
 exit 0
