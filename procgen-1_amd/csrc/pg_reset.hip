@@ -2641,7 +2641,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
             for (int b = 0; b < 4; b++) {
                 int cell = i * 16 + q * 4 + b;
                 int v = cell < cells ? (int)lds_grid[cell] : 0;
-                if (v < -128 || v > 127) fits = false;
+                if (v < -127 || v > 127) fits = false; // -128 marks an unstaged LDS cell in the step kernel
                 word |= (uint32_t)(uint8_t)v << (8 * b);
             }
             w[q] = word;

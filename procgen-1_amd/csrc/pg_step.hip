@@ -134,16 +134,63 @@ DEV void entity_step_slot(Ctx &c, int i, bool skip_smart = false) {
 // The step reads the grid (never writes it), so the env's grid is copied once into LDS as
 // int8 (every coinrun cell value is a `char` from fill_elem or a small id from set_obj;
 // any value outside int8 falls back to HBM reads) and all probes hit LDS.
+#define PG_G8_HOLE (-128) // an LDS grid cell that was not staged (PG_GRID_ROWS): read from HBM instead
 DEV int get_obj(Ctx &c, int x, int y) {
     if (!(0 <= y && y < c.s.main_height && 0 <= x && x < c.s.main_width)) return c.s.out_of_bounds_object;
-    return c.grid8_ok ? (int)c.grid8[y * c.s.main_width + x] : (int)c.G[y * c.s.main_width + x];
+    if (!c.grid8_ok) return (int)c.G[y * c.s.main_width + x];
+    const int v = c.grid8[y * c.s.main_width + x];
+#ifdef PG_GRID_ROWS
+    if (v == PG_G8_HOLE) return (int)c.G[y * c.s.main_width + x];
+#endif
+    return v;
 }
 
+// PG_GRID_ROWS: only the rows within reach of the entities that move this step are staged -- every
+// smart or moving entity's rows +- 8 (push chains of stacked objects included); the other 16-cell
+// chunks hold PG_G8_HOLE, which get_obj resolves from HBM (the mirror never holds -128: reset).
+template <int G>
+DEV uint64_t grid_rows_needed(Ctx &c) {
+    const int h = c.s.main_height;
+    uint64_t m = 0;
+    for (int base = 0; base < c.s.num_ents; base += 64) {
+        const int i = base + LANE;
+        if (i >= c.s.num_ents) continue;
+        const int fl = EI(c, F_FLAGS, i);
+        const bool moving = i == 0 || (fl & EF_SMART_STEP) || EF(c, F_VX, i) != 0 || EF(c, F_VY, i) != 0;
+        if (!moving) continue;
+        const float y = EF(c, F_Y, i), ry = EF(c, F_RY, i);
+        int lo = (int)floorf(y - ry) - 8, hi = (int)floorf(y + ry) + 8;
+        lo = max(lo, 0);
+        hi = min(hi, h - 1);
+        if (lo <= hi) m |= (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o);
+    return m;
+}
+template <int G>
 DEV void load_grid_lds(Ctx &c) {
     int cells = c.s.main_width * c.s.main_height;
     bool bad = cells > PG_GRID_MAX;
     if (!bad && c.s.grid8_ok) { // int8 mirror written by the last reset: 4 KB per env
         const uint4 *src = reinterpret_cast<const uint4 *>(c.d.grid8 + (size_t)c.env * PG_GRID_MAX);
+#ifdef PG_GRID_ROWS
+        if constexpr (G != PG_GAME_MINER) { // miner's cell physics reads the whole grid
+            if (c.s.main_height <= 64) {
+                const uint64_t rows = grid_rows_needed<G>(c);
+                const int w = c.s.main_width;
+                const uint4 hole = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+                for (int k = LANE; k < (cells + 15) / 16; k += 64) {
+                    const int r0 = (16 * k) / w, r1 = min((16 * k + 15) / w, 63);
+                    const uint64_t span = ((r1 >= 63 ? ~0ull : ((2ull << r1) - 1)) & ~((1ull << r0) - 1));
+                    reinterpret_cast<uint4 *>(c.grid8)[k] = (rows & span) ? src[k] : hole;
+                }
+                c.grid8_ok = true;
+                wave_sync();
+                return;
+            }
+        }
+#endif
         for (int k = LANE; k < (cells + 15) / 16; k += 64) reinterpret_cast<uint4 *>(c.grid8)[k] = src[k];
         c.grid8_ok = true;
         wave_sync();
@@ -162,7 +209,7 @@ DEV void load_grid_lds(Ctx &c) {
                 for (int q = 0; q < 2; q++) {
                     uint32_t word = w[h * 2 + q];
                     int lo = (int16_t)(word & 0xffff), hi = (int16_t)(word >> 16);
-                    if (lo < -128 || lo > 127 || hi < -128 || hi > 127) bad = true;
+                    if (lo < -127 || lo > 127 || hi < -127 || hi > 127) bad = true; // -128: PG_G8_HOLE
                     p |= ((uint32_t)(uint8_t)lo | ((uint32_t)(uint8_t)hi << 8)) << (16 * q);
                 }
                 packed[h] = p;
@@ -2853,7 +2900,7 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.grid8_ok = false;
     c.cs.start();
     c.pt.start();
-    load_grid_lds(c);
+    load_grid_lds<G>(c);
     c.cs.mark(0);
 
     int action;

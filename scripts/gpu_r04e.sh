@@ -23,10 +23,14 @@ for c in "-" "GPU_MAX_HW_QUEUES=8,PROCGEN_MI355X_MIXED_STREAMS=8" "GPU_MAX_HW_QU
 done
 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29541 GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python3 bench.py --gather --host-steps 0 --no-cpu-baseline > gpurun_out/e/gather_q8.json 2> gpurun_out/e/gather_q8.err || { tail -5 gpurun_out/e/gather_q8.err; exit 14; }
 python3 -c "import json; d=json.load(open('gpurun_out/e/gather_q8.json')); print('gather q8', round(d['value']/1e6,2), d['ms_per_step'])"
+PROCGEN_MI355X_LIB=rows timeout -k 10 200 python3 bench.py --steps 200 --warmup 20 --settle 300 --host-steps 0 --no-cpu-baseline > gpurun_out/e/coinrun.rows.json 2> gpurun_out/e/coinrun.rows.err || { tail -5 gpurun_out/e/coinrun.rows.err; exit 16; }
+python3 -c "import json; d=json.load(open('gpurun_out/e/coinrun.rows.json')); print('coinrun lib=rows', round(d['value']/1e6,2), d['roofline']['kernel_ms'])"
+PROCGEN_MI355X_LIB=rows timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "coinrun or hard_unbounded or ninja or maze" > gpurun_out/e/pytest_rows.log 2>&1; rc=$?; tail -2 gpurun_out/e/pytest_rows.log; [[ $rc != 0 ]] && exit $rc
 for g in bossfight fruitbot; do
   for L in "" aux; do
     PROCGEN_MI355X_LIB=$L timeout -k 10 200 python3 bench.py --env-name $g --steps 50 --warmup 20 --settle 100 --host-steps 0 --no-cpu-baseline > gpurun_out/e/$g.$L.json 2> gpurun_out/e/$g.$L.err || { tail -5 gpurun_out/e/$g.$L.err; exit 15; }
     python3 -c "import json; d=json.load(open('gpurun_out/e/$g.$L.json')); print('$g', 'lib=$L', round(d['value']/1e6,2), d['roofline']['kernel_ms'])"
   done
 done
+PROCGEN_MI355X_LIB=stamp timeout -k 10 300 python3 scripts/phase_profile.py bossfight fruitbot coinrun > gpurun_out/e/stamp.json 2> gpurun_out/e/stamp.err || { tail -3 gpurun_out/e/stamp.err; exit 17; }
 exit 0
