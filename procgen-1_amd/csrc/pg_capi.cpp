@@ -975,9 +975,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         const char *ms = getenv("PROCGEN_MI355X_MIXED_STREAMS");
         const int ns = std::min(std::max(ms ? atoi(ms) : 4, 1), (int)nchains);
         if (ns < (int)nchains) {
-            // per-game chain cost, ms at 4,096 envs (profiles/r03 mixed16 per_game step + reset + render)
-            static const float cost[PG_NUM_GAMES] = {0.27f, 0.70f, 0.97f, 0.46f, 0.43f, 0.72f, 0.73f, 0.94f,
-                                                     0.34f, 1.43f, 0.92f, 0.47f, 0.74f, 0.43f, 0.24f, 0.57f};
+            // per-game chain cost, ms at 4,096 envs (step + reset + render per game inside the all-16 mixed
+            // shard, profiles/r04/r04_d_games/mixed16_noprefetch.json per_game)
+            static const float cost[PG_NUM_GAMES] = {0.34f, 0.75f, 1.09f, 0.68f, 0.39f, 0.49f, 0.69f, 0.94f,
+                                                     0.47f, 1.64f, 1.15f, 0.58f, 0.47f, 0.47f, 0.22f, 0.70f};
             std::vector<size_t> order(nchains);
             for (size_t k = 0; k < nchains; k++) order[k] = k;
             std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[gids[a]] > cost[gids[b]]; });

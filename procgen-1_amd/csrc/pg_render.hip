@@ -1471,6 +1471,9 @@ DEV void gen_draw(const FB &fb, const PGDev &d, const uint32_t *bgpix, const uin
 // Frame rows per pass and waves per SIMD: the games without rotated / tiled entities fit 168 VGPRs
 // (77-114 measured) and render in two 32-row passes at 3 waves per SIMD (12-15 KB of LDS), as do
 // six rotating / tiling games; three keep one full-frame pass at 2 waves per SIMD.
+#ifndef PG_RENDER_K
+#define PG_RENDER_K 1
+#endif
 template <int G>
 DEV constexpr int frame_rows() {
     // measured per game (profiles/r02/r02_k_variants.txt): two passes win for every game but
@@ -1487,7 +1490,7 @@ DEV constexpr int rot_cap() {
 }
 
 template <int G>
-__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode, int slot) {
+__global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
     const PGDev d = game_view(dg, G);
     constexpr int HR = frame_rows<G>();
     __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES]; // the rows of one pass
@@ -1526,13 +1529,17 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     int4 *const rowax = colax + 64;
     // mode 0: every env of the list; 1: the envs whose step did not end the episode (drawn while
     // the reset kernel regenerates the others); 2: this step's reset queue (after the reset)
+    // PG_RENDER_K envs per workgroup, one after the other (experiment: fewer, longer workgroups)
+    for (int kk = 0; kk < PG_RENDER_K; kk++) {
+    const int bidx = (int)blockIdx.x * PG_RENDER_K + kk;
     int env;
     if (mode == 2) {
-        if ((int)blockIdx.x >= d.reset_count[slot]) return;
-        env = d.reset_queue[(size_t)slot * d.num_envs + blockIdx.x];
+        if (bidx >= d.reset_count[slot]) break;
+        env = d.reset_queue[(size_t)slot * d.num_envs + bidx];
     } else {
-        env = env_list ? env_list[blockIdx.x] : (int)blockIdx.x;
-        if (mode == 1 && d.done8[env]) return;
+        if (bidx >= count) break;
+        env = env_list ? env_list[bidx] : bidx;
+        if (mode == 1 && d.done8[env]) continue;
     }
     const PGEnv s = d.envs[env];
     const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
@@ -2076,6 +2083,8 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     spt.flush(d.prof ? d.prof + (size_t)env * 16 : nullptr); // the step kernel's slots (it does not flush here)
 #endif
     census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
+    if (PG_RENDER_K > 1) wave_sync(); // the next env reuses the LDS
+    } // kk
 }
 
 // ================================================================== render_mode="rgb_array"
@@ -3757,7 +3766,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
     if (count <= 0) return;
 #define PG_CASE(G)                                                                              \
     case G:                                                                                     \
-        hipLaunchKernelGGL(pg_render_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, mode, slot); \
+        hipLaunchKernelGGL(pg_render_kernel<G>, dim3((count + PG_RENDER_K - 1) / PG_RENDER_K), dim3(64), 0, s, *d, env_list, mode, slot, count); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

@@ -32,5 +32,9 @@ for g in bossfight fruitbot; do
     python3 -c "import json; d=json.load(open('gpurun_out/e/$g.$L.json')); print('$g', 'lib=$L', round(d['value']/1e6,2), d['roofline']['kernel_ms'])"
   done
 done
+for g in coinrun bossfight; do
+  PROCGEN_MI355X_LIB=k2 timeout -k 10 200 python3 bench.py --env-name $g --steps 100 --warmup 20 --settle 200 --host-steps 0 --no-cpu-baseline > gpurun_out/e/$g.k2.json 2> gpurun_out/e/$g.k2.err || { tail -5 gpurun_out/e/$g.k2.err; exit 18; }
+  python3 -c "import json; d=json.load(open('gpurun_out/e/$g.k2.json')); print('$g', 'lib=k2', round(d['value']/1e6,2), d['roofline']['kernel_ms'])"
+done
 PROCGEN_MI355X_LIB=stamp timeout -k 10 300 python3 scripts/phase_profile.py bossfight fruitbot coinrun > gpurun_out/e/stamp.json 2> gpurun_out/e/stamp.err || { tail -3 gpurun_out/e/stamp.err; exit 17; }
 exit 0
