@@ -558,6 +558,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
         if (v->obs_early && split) { // host buffers: this part's observations leave as soon as it rendered
             const size_t lo = (size_t)v->chain_lo(k) * PG_OBS_BYTES;
+            if (!v->cstream) HIPCHECK(hipStreamCreateWithFlags(&v->cstream, hipStreamNonBlocking));
             HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
             HIPCHECK(hipStreamWaitEvent(v->cstream, v->ev_rendered[k], 0));
             HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo, (size_t)cnt * PG_OBS_BYTES,
@@ -938,8 +939,9 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             v->ev_reset.push_back(b);
             v->ev_rendered.push_back(c);
         }
-        ok = ok && hipStreamCreateWithFlags(&v->cstream, hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&v->ev_cdone, hipEventDisableTiming) == hipSuccess;
+        // the obs-copy stream (host buffers only) is created on first use: one more stream at make time
+        // shifts the chain streams' hardware-queue assignment and cost coinrun 37 -> 28 M env-steps/s
+        ok = ok && hipEventCreateWithFlags(&v->ev_cdone, hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             libenv_close((libenv_env *)v);
             return bad("hipStreamCreate failed");
