@@ -1501,12 +1501,15 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     // column per tile row; before it is built, the same LDS holds the Qt blit setup (t1, n, base,
     // step) of every window tile column / row (class 0 at [0, 128), class 1 at [128, 256) in int4
     // units).  General tile pass (decided after the fast path): GEN_AUX_BYTES of tables.
-#ifdef PG_AUX_TIGHT
     // games without uniform tiles never take the fast path: tile_off + the column / row axis tables
-    constexpr int FAST_BYTES = uniform_tiles<G>() ? (NTYPES + CR * 64) * 4 : (NTYPES + 2 * 64 * 4) * 4;
+    // suffice.  On for fruitbot (one workgroup more per CU: render 4.22 -> 3.79 ms); bossfight's rotated
+    // descriptors share aux and it lost 6 % (profiles/r04/r04_h_ab); PG_AUX_TIGHT applies it to all.
+#ifdef PG_AUX_TIGHT
+    constexpr bool TIGHT = !uniform_tiles<G>();
 #else
-    constexpr int FAST_BYTES = (NTYPES + CR * 64) * 4;
+    constexpr bool TIGHT = !uniform_tiles<G>() && G == PG_GAME_FRUITBOT;
 #endif
+    constexpr int FAST_BYTES = TIGHT ? (NTYPES + 2 * 64 * 4) * 4 : (NTYPES + CR * 64) * 4;
     constexpr int AUX_BYTES = has_general<G>() && GEN_AUX_BYTES > FAST_BYTES ? GEN_AUX_BYTES : FAST_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t aux[AUX_BYTES];
     int *const tile_off = reinterpret_cast<int *>(aux);
