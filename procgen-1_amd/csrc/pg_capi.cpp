@@ -362,6 +362,7 @@ struct VecEnv {
     // mixed batches: each game's step -> reset -> render chain runs on its own stream (the games'
     // envs are disjoint), forked from and joined back into `stream` every act
     std::vector<hipStream_t> gstreams;
+    std::vector<int> launch_order; // chains in enqueue order (mixed: costliest first)
     std::vector<hipEvent_t> gdone;
     // single game split into `parts` chains over contiguous env ranges (PROCGEN_MI355X_PARTS): each
     // part's step -> reset -> render chain on its own stream (gstreams), so one part renders while
@@ -493,7 +494,9 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         HIPCHECK(hipMemsetAsync(v->dev.sp_count + i * PG_NUM_GAMES, 0, PG_NUM_GAMES * 4, v->stream));
     }
     if (C > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
-    for (size_t k = 0; k < C; k++) {
+    std::vector<char> seen(v->gstreams.size() + 1, 0); // streams that already waited on the fork
+    for (size_t ki = 0; ki < C; ki++) {
+        const size_t k = C > 1 ? (size_t)v->launch_order[ki] : ki;
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
         // a side stream while the envs that did not finish render; a mixed batch keeps each game's
         // step -> reset -> render chain on its stream (its 16 chains already overlap, and twice as
@@ -505,9 +508,8 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         // waits is serialized behind them
         const int si = C > 1 ? v->chain_stream[k] : 0;
         hipStream_t s = si > 0 ? v->gstreams[si] : v->stream, r = split ? v->rstreams[k] : s;
-        bool first_on_stream = si > 0;
-        for (size_t j = 0; j < k && first_on_stream; j++) first_on_stream = v->chain_stream[j] != si;
-        if (first_on_stream) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0));
+        if (si > 0 && !seen[si]) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0)); // first chain on the stream
+        seen[si] = true;
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
         pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
@@ -947,6 +949,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             return bad("hipStreamCreate failed");
         }
     }
+    // a mixed batch packs its chains onto `ns` streams (below); only those are created: every stream
+    // takes or shares a hardware queue at creation, so unused ones still shift the assignment
+    // (PROCGEN_MI355X_ALL_GSTREAMS=1 creates one per chain, the round-3 layout)
+    const char *ms = getenv("PROCGEN_MI355X_MIXED_STREAMS"), *ag = getenv("PROCGEN_MI355X_ALL_GSTREAMS");
+    const int ns = gids.size() > 1 ? std::min(std::max(ms ? atoi(ms) : 4, 1), (int)nchains) : (int)nchains;
+    const size_t ncreate = ag && ag[0] == '1' ? nchains : (size_t)ns;
     if (nchains > 1) {
         bool ok = hipEventCreateWithFlags(&v->fork, hipEventDisableTiming) == hipSuccess;
         // parts: part 1's stream gets the highest priority and the later parts' the lowest (part 0 runs
@@ -954,7 +962,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         const char *pr = getenv("PROCGEN_MI355X_PART_PRIO");
         int lo_prio = 0, hi_prio = 0;
         const bool prio = v->parts > 1 && !(pr && pr[0] == '0') && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
-        for (size_t k = 0; k < nchains && ok; k++) {
+        for (size_t k = 0; k < ncreate && ok; k++) {
             hipStream_t s = nullptr;
             hipEvent_t d = nullptr;
             ok = (k == 0 || // chain 0 runs on the engine stream (launch_step)
@@ -970,17 +978,16 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         }
     }
     v->chain_stream.resize(nchains);
-    for (size_t k = 0; k < nchains; k++) v->chain_stream[k] = (int)k;
+    v->launch_order.resize(nchains);
+    for (size_t k = 0; k < nchains; k++) v->chain_stream[k] = v->launch_order[k] = (int)k;
     if (gids.size() > 1) {
         // default: as many streams as GPU_MAX_HW_QUEUES (4), chains packed longest-first (all-16 mixed
         // shard 16.5 -> 18.7 M env-steps/s, profiles/r03/r03_q_mixed16*.json); 16 = one per game
-        const char *ms = getenv("PROCGEN_MI355X_MIXED_STREAMS");
-        const int ns = std::min(std::max(ms ? atoi(ms) : 4, 1), (int)nchains);
         if (ns < (int)nchains) {
             // per-game chain cost, ms at 4,096 envs (step + reset + render per game inside the all-16 mixed
-            // shard, profiles/r04/r04_d_games/mixed16_noprefetch.json per_game)
-            static const float cost[PG_NUM_GAMES] = {0.34f, 0.75f, 1.09f, 0.68f, 0.39f, 0.49f, 0.69f, 0.94f,
-                                                     0.47f, 1.64f, 1.15f, 0.58f, 0.47f, 0.47f, 0.22f, 0.70f};
+            // shard, profiles/r04/r04_l_mixed/mixed16_default.json per_game)
+            static const float cost[PG_NUM_GAMES] = {0.21f, 0.85f, 1.13f, 0.67f, 0.46f, 0.50f, 0.66f, 0.74f,
+                                                     0.49f, 1.45f, 0.99f, 0.51f, 0.51f, 0.47f, 0.35f, 0.67f};
             std::vector<size_t> order(nchains);
             for (size_t k = 0; k < nchains; k++) order[k] = k;
             std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[gids[a]] > cost[gids[b]]; });
@@ -992,6 +999,41 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
                 load[best] += cost[gids[k]];
                 v->chain_stream[k] = best;
             }
+            // then the best single move or swap out of the most loaded stream while it lowers the maximum
+            // (all-16 shard: LPT's largest stream 2.80 ms of chains -> 2.67, the mean)
+            for (int it = 0; it < 64; it++) {
+                int hi = 0;
+                for (int j = 1; j < ns; j++)
+                    if (load[j] > load[hi]) hi = j;
+                float best_max = load[hi] - 1e-4f;
+                int bj = -1;
+                long bx = -1, by = -1; // chains moved hi -> bj and bj -> hi (-1: none)
+                for (int j = 0; j < ns; j++) {
+                    if (j == hi) continue;
+                    for (long x = -1; x < (long)nchains; x++) {
+                        if (x >= 0 && v->chain_stream[x] != hi) continue;
+                        for (long y = -1; y < (long)nchains; y++) {
+                            if ((x < 0 && y < 0) || (y >= 0 && v->chain_stream[y] != j)) continue;
+                            const float d = (x >= 0 ? cost[gids[x]] : 0.f) - (y >= 0 ? cost[gids[y]] : 0.f);
+                            const float m = std::max(load[hi] - d, load[j] + d);
+                            if (m < best_max) best_max = m, bj = j, bx = x, by = y;
+                        }
+                    }
+                }
+                if (bj < 0) break;
+                const float d = (bx >= 0 ? cost[gids[bx]] : 0.f) - (by >= 0 ? cost[gids[by]] : 0.f);
+                load[hi] -= d;
+                load[bj] += d;
+                if (bx >= 0) v->chain_stream[bx] = bj;
+                if (by >= 0) v->chain_stream[by] = hi;
+            }
+            // enqueue order: game id (default); PROCGEN_MI355X_MIXED_ORDER=desc enqueues the costliest
+            // chains first (all-16 shard 21.7 -> 20.8 M env-steps/s, profiles/r04/r04_m_mixed), asc the
+            // cheapest first
+            const char *mo = getenv("PROCGEN_MI355X_MIXED_ORDER");
+            const std::string mode = mo ? mo : "id";
+            for (size_t k = 0; k < nchains && mode != "id"; k++)
+                v->launch_order[k] = (int)order[mode == "asc" ? nchains - 1 - k : k];
         }
     }
     (void)hipGetDevice(&v->device);
