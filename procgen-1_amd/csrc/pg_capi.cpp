@@ -558,15 +558,21 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             pg_launch_render(&v->dev, game, list, cnt, s, 0, slot);
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
-        if (v->obs_early && split) { // host buffers: this part's observations leave as soon as it rendered
+        if (v->obs_early && split) HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
+    }
+    if (v->obs_early && split) {
+        // host buffers: each part's observations leave as soon as it rendered, on one copy stream in the
+        // order the parts finish: part 1 (highest priority) first, part 0 (the engine stream) last --
+        // in chain order part 1's copy waited behind part 0's render (0.3 ms per act, r04_n trace)
+        if (!v->cstream) HIPCHECK(hipStreamCreateWithFlags(&v->cstream, hipStreamNonBlocking));
+        for (size_t i = 0; i < C; i++) {
+            const size_t k = (i + 1) % C;
             const size_t lo = (size_t)v->chain_lo(k) * PG_OBS_BYTES;
-            if (!v->cstream) HIPCHECK(hipStreamCreateWithFlags(&v->cstream, hipStreamNonBlocking));
-            HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
             HIPCHECK(hipStreamWaitEvent(v->cstream, v->ev_rendered[k], 0));
-            HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo, (size_t)cnt * PG_OBS_BYTES,
-                                    hipMemcpyDeviceToHost, v->cstream));
-            v->obs_inflight = true;
+            HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo,
+                                    (size_t)v->chain_count(k) * PG_OBS_BYTES, hipMemcpyDeviceToHost, v->cstream));
         }
+        v->obs_inflight = true;
     }
     if (v->obs_inflight) { // observe() synchronizes the engine stream: it waits for the obs DMAs too
         HIPCHECK(hipEventRecord(v->ev_cdone, v->cstream));
