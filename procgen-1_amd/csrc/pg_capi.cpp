@@ -341,6 +341,9 @@ struct VecEnv {
     // buffers before observe), so part 0's copy runs while part 1 still renders; copy_out then only
     // moves the small planes
     bool obs_early = false, obs_inflight = false;
+    // host buffers with parts: part 0 starts once part 1 rendered, so part 1's copy (the first on the
+    // copy stream) starts sooner and part 0 computes under it (PROCGEN_MI355X_HOST_SERIAL=0: off)
+    bool host_serial = true;
     // the per-part obs DMAs (obs_early) run on their own normal-priority stream: issued on a part's
     // high-priority chain stream the runtime made them a blit kernel (copyBuffer) that held the CUs
     // for the whole 7 ms transfer and stalled the other part's render behind it
@@ -495,8 +498,9 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     }
     if (C > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     std::vector<char> seen(v->gstreams.size() + 1, 0); // streams that already waited on the fork
+    const bool host_serial = v->obs_early && split && C > 1 && v->host_serial;
     for (size_t ki = 0; ki < C; ki++) {
-        const size_t k = C > 1 ? (size_t)v->launch_order[ki] : ki;
+        const size_t k = host_serial ? (ki + 1) % C : C > 1 ? (size_t)v->launch_order[ki] : ki;
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
         // a side stream while the envs that did not finish render; a mixed batch keeps each game's
         // step -> reset -> render chain on its stream (its 16 chains already overlap, and twice as
@@ -510,6 +514,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         hipStream_t s = si > 0 ? v->gstreams[si] : v->stream, r = split ? v->rstreams[k] : s;
         if (si > 0 && !seen[si]) HIPCHECK(hipStreamWaitEvent(s, v->fork, 0)); // first chain on the stream
         seen[si] = true;
+        if (host_serial && k == 0) HIPCHECK(hipStreamWaitEvent(s, v->ev_rendered[1], 0)); // enqueued last
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
         pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
@@ -982,6 +987,10 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
             libenv_close((libenv_env *)v);
             return bad("hipStreamCreate failed");
         }
+    }
+    {
+        const char *hs = getenv("PROCGEN_MI355X_HOST_SERIAL");
+        v->host_serial = !(hs && hs[0] == '0');
     }
     v->chain_stream.resize(nchains);
     v->launch_order.resize(nchains);
