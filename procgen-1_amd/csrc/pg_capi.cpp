@@ -499,6 +499,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (C > 1) HIPCHECK(hipEventRecord(v->fork, v->stream));
     std::vector<char> seen(v->gstreams.size() + 1, 0); // streams that already waited on the fork
     const bool host_serial = v->obs_early && split && C > 1 && v->host_serial;
+    bool pre_waited = false; // this act's prefetch stream already waits for the previous act's generation
     for (size_t ki = 0; ki < C; ki++) {
         const size_t k = host_serial ? (ki + 1) % C : C > 1 ? (size_t)v->launch_order[ki] : ki;
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
@@ -541,10 +542,13 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
             // with 2 prefetch streams, acts a and a+1 generate on different streams: an env whose
             // episode ends at both would have both write its spare rows, so act a+1's generation
-            // also waits for act a's (ring slot (act - 1) % lag, not yet reused: lag >= 2 here)
+            // also waits for act a's (ring slot (act - 1) % lag, not yet reused: lag >= 2 here) -- once,
+            // before the first generation this act enqueues on that stream, whichever chain it is
+            // (host_serial, MIXED_ORDER and PREFETCH_GAMES change which chain comes first)
             const int prev = (act + v->lag - 1) % v->lag;
-            if (v->npstreams > 1 && v->lag > 1 && k == 0 && v->ev_pre_set[prev])
+            if (v->npstreams > 1 && v->lag > 1 && !pre_waited && v->ev_pre_set[prev])
                 HIPCHECK(hipStreamWaitEvent(p, v->ev_pre[prev], 0));
+            pre_waited = true;
             pg_launch_reset(&v->dev, game, list, cnt, p, 2, 0, act, slot);
             HIPCHECK(hipEventRecord(v->ev_pre[act % v->lag], p));
             v->ev_pre_set[act % v->lag] = true;
@@ -1170,6 +1174,13 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
     d.heavy_ticks = 10000; // 100 us: ~3x the median coinrun step wave
     {
+        // the register-frame render (pg_render_rf_kernel) for the games and options it serves;
+        // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel
+        const char *rf = getenv("PROCGEN_MI355X_RENDER_RF");
+        const bool on = (!rf || rf[0] != '0') && center_agent && !use_monochrome_assets && !use_generated_assets;
+        d.render_rf = on ? (1 << PG_GAME_COINRUN) : 0;
+    }
+    {
         const char *sp = getenv("PROCGEN_MI355X_SLOW_PREDICT");
         d.slow_predict = sp ? atoi(sp) : 0;
     }
@@ -1771,6 +1782,9 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
         return;
     }
     size_t plane = (size_t)v->num_envs * PG_CAP;
+    // a restored env draws with the options its state carries: the register-frame render serves
+    // centred, non-monochrome frames only (pg_render.hip rf_game), so its game falls back otherwise
+    if (!s.opt_center_agent || s.opt_use_monochrome_assets) v->dev.render_rf &= ~(1 << s.game_id);
     s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
     copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     const char *ent_base = p; // the live entity planes
@@ -1822,6 +1836,17 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     if (bgb) copy_sync(v, v->dev.gen_bg + (size_t)env_idx * PG_GEN_BG_PX, p, bgb, hipMemcpyHostToDevice);
     // the reference re-observes after set_state (vecgame.cpp:503); rendering all envs is
     // harmless (render is a pure function of state)
+    // ... and Game::observe (game.cpp:173-191) reports the restored step data: reward, done (first),
+    // prev_level_seed, prev_level_complete, level_seed
+    {
+        const float rew = s.sd_reward;
+        const uint8_t first = (uint8_t)(s.sd_done != 0), plc = (uint8_t)(s.sd_level_complete != 0);
+        copy_sync(v, v->dev.rew + env_idx, &rew, 4, hipMemcpyHostToDevice);
+        copy_sync(v, v->dev.first + env_idx, &first, 1, hipMemcpyHostToDevice);
+        copy_sync(v, v->dev.prev_level_seed + env_idx, &s.prev_level_seed, 4, hipMemcpyHostToDevice);
+        copy_sync(v, v->dev.prev_level_complete + env_idx, &plc, 1, hipMemcpyHostToDevice);
+        copy_sync(v, v->dev.level_seed + env_idx, &s.current_level_seed, 4, hipMemcpyHostToDevice);
+    }
     for (size_t k = 0; k < v->games.size(); k++)
         pg_launch_render(&v->dev, v->games[k], v->list_of(k), v->count_of(), v->stream, 0, v->games[k]);
     hipStreamSynchronize(v->stream);

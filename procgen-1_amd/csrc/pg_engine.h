@@ -306,6 +306,7 @@ struct PGDev {
     int32_t *sp_count;          // [sp_lag][PG_NUM_GAMES]
     int32_t sp_lag;             // a spare requested at act a is swapped in from act a + sp_lag
     uint32_t sp_mask[4];        // PGEnv words the step kernel may change: poisoned in the spare input
+    int32_t render_rf;          // bit g: game g renders with pg_render_rf_kernel (host: options it serves)
 };
 #define PG_SP_LAG_MAX 8
 #define PG_SP_NONE ((int32_t)0x80808080) // sp_gen of an env without a valid spare (memset 0x80)

@@ -1466,6 +1466,48 @@ DEV void gen_draw(const FB &fb, const PGDev &d, const uint32_t *bgpix, const uin
     }
 }
 
+// The agent's image and prepare_for_drawing(rect_height = 64) (basic-abstract-game.cpp:828-847)
+// with choose_center (:673-676; climber.cpp:291-295, fruitbot.cpp:138-142).
+template <int G>
+DEV View prepare_view(const PGDev &d, const PGEnv &s, int env, int &player_img) {
+    float agent_x, agent_y, agent_vx;
+    if (s.agent_erased) {
+        agent_x = s.ghost_x; agent_y = s.ghost_y; agent_vx = s.ghost_vx;
+    } else {
+        agent_x = EFr(d, F_X, env, 0); agent_y = EFr(d, F_Y, env, 0); agent_vx = EFr(d, F_VX, env, 0);
+    }
+    player_img = player_image<G>(s, agent_vx);
+    View v;
+    v.center_x = (float)(s.main_width * .5);
+    v.center_y = (float)(s.main_height * .5);
+    v.visibility = s.visibility;
+    if (s.opt_center_agent) {
+        if constexpr (G == PG_GAME_CLIMBER) {
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
+            v.visibility = (float)s.main_width;
+        } else if constexpr (G == PG_GAME_FRUITBOT) {
+            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
+            v.center_x = (float)(s.main_width / 2.0);
+            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(2 * agent_ry));
+            v.visibility = (float)s.main_width;
+        } else {
+            v.center_x = agent_x;
+            v.center_y = agent_y;
+        }
+    } else {
+        v.visibility = (float)(s.main_width > s.main_height ? s.main_width : s.main_height);
+        if (v.visibility < s.min_visibility) v.visibility = s.min_visibility;
+    }
+    float raw_unit = 64 / v.visibility;
+    v.unit = (float)((double)raw_unit * ((double)64.0f / 64.0));
+    v.view_dim = (float)(64.0 / (double)raw_unit);
+    v.x_off = v.unit * (v.center_x - v.view_dim / 2);
+    v.y_off = v.unit * (v.center_y - v.view_dim / 2);
+    return v;
+}
+
 } // namespace
 
 // Frame rows per pass and waves per SIMD: the games without rotated / tiled entities fit 168 VGPRs
@@ -1493,7 +1535,10 @@ template <int G>
 __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
     const PGDev d = game_view(dg, G);
     constexpr int HR = frame_rows<G>();
-    __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES]; // the rows of one pass
+#ifndef PG_LDS_PAD
+#define PG_LDS_PAD 0 // experiment: extra LDS per workgroup (occupancy sensitivity)
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES + PG_LDS_PAD / 4]; // the rows of one pass
     // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
     // <= -2 not drawable on the fast path
     constexpr int CR = crows<G>();
@@ -1548,43 +1593,8 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
     bool err = false;
 
-    float agent_x, agent_y, agent_vx;
-    if (s.agent_erased) {
-        agent_x = s.ghost_x; agent_y = s.ghost_y; agent_vx = s.ghost_vx;
-    } else {
-        agent_x = EFr(d, F_X, env, 0); agent_y = EFr(d, F_Y, env, 0); agent_vx = EFr(d, F_VX, env, 0);
-    }
-    const int player_img = player_image<G>(s, agent_vx);
-
-    // ---- prepare_for_drawing(rect_height = 64) (basic-abstract-game.cpp:828-847)
-    View v;
-    v.center_x = (float)(s.main_width * .5);
-    v.center_y = (float)(s.main_height * .5);
-    v.visibility = s.visibility;
-    if (s.opt_center_agent) { // choose_center (:673-676; climber.cpp:291-295)
-        if constexpr (G == PG_GAME_CLIMBER) {
-            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
-            v.center_x = (float)(s.main_width / 2.0);
-            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(5 * agent_ry));
-            v.visibility = (float)s.main_width;
-        } else if constexpr (G == PG_GAME_FRUITBOT) { // fruitbot.cpp:138-142
-            const float agent_ry = s.agent_erased ? s.ghost_ry : EFr(d, F_RY, env, 0);
-            v.center_x = (float)(s.main_width / 2.0);
-            v.center_y = (float)((double)agent_y + s.main_width / 2.0 - (double)(2 * agent_ry));
-            v.visibility = (float)s.main_width;
-        } else {
-            v.center_x = agent_x;
-            v.center_y = agent_y;
-        }
-    } else {
-        v.visibility = (float)(s.main_width > s.main_height ? s.main_width : s.main_height);
-        if (v.visibility < s.min_visibility) v.visibility = s.min_visibility;
-    }
-    float raw_unit = 64 / v.visibility;
-    v.unit = (float)((double)raw_unit * ((double)64.0f / 64.0));
-    v.view_dim = (float)(64.0 / (double)raw_unit);
-    v.x_off = v.unit * (v.center_x - v.view_dim / 2);
-    v.y_off = v.unit * (v.center_y - v.view_dim / 2);
+    int player_img;
+    const View v = prepare_view<G>(d, s, env, player_img);
 
     const int lane = LANE;
     PTimer pt;
@@ -2088,6 +2098,401 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     census.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
     if (PG_RENDER_K > 1) wave_sync(); // the next env reuses the LDS
     } // kk
+}
+
+
+// ================================================================== register-frame render
+// pg_render_rf_kernel<G>: the frame of pg_render_kernel, for the games and options it serves (rf_game,
+// PGDev::render_rf, set by the host), drawn pixel-centrically with no LDS frame.  Lane = screen column;
+// RF_RB screen rows at a time live in registers.  For every row batch, all texels the batch needs are
+// loaded before the first blend -- the background, the <= 2 x 2 grid tiles covering the pixel (x-major,
+// y-minor: basic-abstract-game.cpp:937-964) and the first RF_JOBS (image, row) jobs of the images that
+// cross the batch (z = 0 then z = 1 entities in list order, then the velocity squares: :966-977) -- then
+// blended in that order, packed to RGB888 across lanes (bgr32_to_rgb888, game.cpp:8-23) and stored.
+// Blending per pixel in draw order is the painter's algorithm of the reference pixel by pixel, and
+// every texel / edge is the one qt_scale_image_32bit / fillRect picks (the same Axis setup as the
+// stamping kernel).  The LDS holds only the tile table, the covering tiles' grid values per tile row
+// and the visible images' blit descriptors (<= RF_DCAP): ~6 KB per wave instead of 12 KB, so a CU keeps
+// twice the waves of the LDS-frame kernel resident to hide the gather latency (the render is
+// latency-bound: +4 KB of LDS per workgroup cost +19 % render time, profiles/r05/).
+#ifndef RF_RB
+#define RF_RB 8
+#endif
+#ifndef RF_JOBS
+#define RF_JOBS 8
+#endif
+#define RF_DCAP 128
+template <int G>
+__host__ __device__ constexpr bool rf_game() { return G == PG_GAME_COINRUN; }
+
+template <int G>
+__global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
+    if constexpr (!rf_game<G>()) {
+        return;
+    } else {
+    const PGDev d = game_view(dg, G);
+    constexpr int CR = crows<G>();
+    constexpr int TP = tile_px<G>();
+    static_assert(TP > 0 && always_uniform<G>() && !has_z_minus1<G>() && !has_rotation<G>() && !has_tiled_entities<G>(),
+                  "the register-frame path draws square grid tiles and plain entity blits only");
+    __shared__ int tile_off[NTYPES];
+    // grid value (255: nothing) of the first | second covering tile column, per window tile row and lane
+    __shared__ __attribute__((aligned(16))) uint16_t codes[CR * 64];
+    // blit descriptors of the visible images in draw order (two int4 each, see below)
+    __shared__ __attribute__((aligned(16))) int4 desc[2 * RF_DCAP];
+    const int lane = LANE;
+    const int bidx = (int)blockIdx.x;
+    int env;
+    if (mode == 2) {
+        if (bidx >= d.reset_count[slot]) return;
+        env = d.reset_queue[(size_t)slot * d.num_envs + bidx];
+    } else {
+        if (bidx >= count) return;
+        env = env_list ? env_list[bidx] : bidx;
+        if (mode == 1 && d.done8[env]) return;
+    }
+    const PGEnv s = d.envs[env];
+    const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
+    bool err = false;
+    int player_img;
+    const View v = prepare_view<G>(d, s, env, player_img);
+
+    // ---- grid type -> sprite pixel offset (theme_for_grid_obj, image_for_type, draw_image :886-922)
+    {
+        int off = -1;
+        const int img = image_for_type<G>(s, lane, player_img);
+        if (img >= 0) {
+            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) {
+                off = img == SPACE ? -1 : -3; // draw_grid_obj fills: not on this path
+            } else {
+                const int theme = mask_theme<G>(s, grid_theme<G>(s, lane), img);
+                const int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                off = (sp.y == TP && sp.z == TP) ? sp.x : -2;
+            }
+        }
+        tile_off[lane] = off;
+    }
+    // ---- visible tile window (basic-abstract-game.cpp:937-948): centred views only (host selection)
+    const double margin = (double)v.visibility / 2.0 + 1;
+    const int low_x = (int)((double)v.center_x - margin), high_x = (int)((double)v.center_x + margin);
+    const int low_y = (int)((double)v.center_y - margin), high_y = (int)((double)v.center_y + margin);
+    const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
+    if (!s.opt_center_agent || s.opt_use_monochrome_assets || d.gen_bg || ww > 63 || wh > 63) err = true;
+    // ---- Qt blit setup of window tile column `lane`, window tile row `lane`, the background (lane 63)
+    int4 bgi = make_int4(0, 0, 0, 0);
+    double bg_rx = 0, bg_ry = 0, bg_rw = 0, bg_rh = 0;
+    if (s.opt_use_backgrounds) {
+        double mx, my, mw, mh;
+        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
+        bgi = reinterpret_cast<const int4 *>(d.backgrounds)[s.background_index];
+        const float bgw = (float)bgi.y, bgh = (float)bgi.z;
+        const float bg_ar = bgw / bgh;
+        const float world_ar = (float)(s.main_width * 1.0 / s.main_height);
+        const float extra_w = bg_ar - world_ar;
+        const float offset_x = s.bg_pct_x * extra_w;
+        const double ax = (double)(-offset_x), aw = (double)(bg_ar / world_ar); // adjust_rect (qt-utils.h:12-19)
+        bg_rx = mx + mw * ax; bg_ry = my + mh * 0.0; bg_rw = mw * aw; bg_rh = mh * 1.0;
+    }
+    Axis ca_ = {0, 0, 0u, 0}, ra_ = {0, 0, 0u, 0}; // this lane's column / row axis
+    bool okx, oky;
+    {
+        double xr = 0, xw = 0, yr = 0, yh = 0;
+        int xiw = 0, yih = 0;
+        if (lane == 63) {
+            if (s.opt_use_backgrounds) { xr = bg_rx; xw = bg_rw; xiw = bgi.y; yr = bg_ry; yh = bg_rh; yih = bgi.z; }
+        } else {
+            double rx, ry, rw, rh;
+            if (lane < ww) {
+                screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                xr = rx; xw = rw; xiw = TP;
+            }
+            if (lane < wh) {
+                screen_rect(v, 0.0f, (float)(low_y + lane + 1), 1, 1, RENDER_EPS, rx, ry, rw, rh);
+                yr = ry; yh = rh; yih = TP;
+            }
+        }
+        okx = axis_setup(xr, xw, xiw, ca_);
+        oky = axis_setup(yr, yh, yih, ra_);
+        if (!okx) ca_.n = 0;
+        if (!oky) ra_.n = 0;
+    }
+    Axis bx, by;
+    const bool bg_ok = readlane(okx && oky ? 1 : 0, 63) != 0;
+    bx.t1 = readlane(ca_.t1, 63); bx.n = readlane(ca_.n, 63); bx.base = (uint32_t)readlane((int)ca_.base, 63); bx.step = readlane(ca_.step, 63);
+    by.t1 = readlane(ra_.t1, 63); by.n = readlane(ra_.n, 63); by.base = (uint32_t)readlane((int)ra_.base, 63); by.step = readlane(ra_.step, 63);
+    // source row offset of screen row `lane` in the background (-1: outside the blit)
+    int bg_lane_row = (bg_ok && lane >= by.t1 && lane < by.t1 + by.n)
+                          ? (int)(((by.base + (uint32_t)((lane - by.t1) * by.step)) >> 16) * (uint32_t)bgi.y)
+                          : -1;
+    bool bg_tiled_ok = bg_ok;
+    if (s.opt_use_backgrounds && s.bg_tile_ratio < 0) { // tile_image(main_rect, bg_tile_ratio < 0) (:849-862, 1003-1004)
+        double mx, my, mw, mh;
+        screen_rect(v, 0, (float)s.main_height, (float)s.main_width, (float)s.main_height, 0, mx, my, mw, mh);
+        const float tile_ratio = -1 * s.bg_tile_ratio;
+        int num_tiles = (int)(mh / (mw * tile_ratio));
+        if (num_tiles < 1) num_tiles = 1;
+        const float th = (float)(mh / num_tiles), tw = (float)mw;
+        bg_tiled_ok = axis_setup(mx, (double)tw, bgi.y, bx);
+        bg_lane_row = -1;
+        for (int t0 = 0; t0 < num_tiles; t0 += 64) {
+            Axis ty;
+            const int t = t0 + lane;
+            const bool okt = t < num_tiles && axis_setup(my + (double)(th * (float)t), (double)th, bgi.z, ty);
+            const int tt1 = okt ? ty.t1 : 0, tn = okt ? ty.n : 0, tstep = okt ? ty.step : 0;
+            const uint32_t tbase = okt ? ty.base : 0u;
+            for (int k = 0; k < 64 && t0 + k < num_tiles; k++) {
+                const int a1 = readlane(tt1, k), an = readlane(tn, k);
+                if (lane >= a1 && lane < a1 + an) {
+                    const uint32_t b = (uint32_t)readlane((int)tbase, k);
+                    const int st = readlane(tstep, k);
+                    bg_lane_row = (int)(((b + (uint32_t)((lane - a1) * st)) >> 16) * (uint32_t)bgi.y);
+                }
+            }
+        }
+        if (!bg_tiled_ok) bg_lane_row = -1;
+    }
+    const bool bg_col = bg_tiled_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
+    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
+    const uint32_t *bgpix = d.pixels;
+
+    // ---- tile columns covering screen column `lane` (<= 2, ascending x) and tile rows covering screen
+    //      row `lane` (<= 2, ascending y = the reference's draw order): the column / row axes of the
+    //      window live one per lane and are read across lanes
+    const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
+    const int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
+    int cx0 = 0, cx1 = 0, ncx = 0, scol0 = 0, scol1 = 0;
+    int ry0 = 0, ry1 = 0, ncy = 0, srow0 = 0, srow1 = 0;
+#pragma unroll
+    for (int dx = -2; dx <= 2; dx++) {
+        const int x = xg + dx, i = (x - low_x) & 63;
+        const int t1 = __shfl(ca_.t1, i), n = __shfl(ca_.n, i), b = __shfl((int)ca_.base, i), st = __shfl(ca_.step, i);
+        if (x >= low_x && x <= high_x && ncx < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
+            const int scv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
+            if (ncx == 0) { cx0 = x; scol0 = scv; } else { cx1 = x; scol1 = scv; }
+            ncx++;
+        }
+    }
+#pragma unroll
+    for (int dy = -2; dy <= 2; dy++) {
+        const int y = yg + dy, i = (y - low_y) & 63;
+        const int t1 = __shfl(ra_.t1, i), n = __shfl(ra_.n, i), b = __shfl((int)ra_.base, i), st = __shfl(ra_.step, i);
+        if (y >= low_y && y <= high_y && ncy < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
+            const int srv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
+            if (ncy == 0) { ry0 = y; srow0 = srv; } else { ry1 = y; srow1 = srv; }
+            ncy++;
+        }
+    }
+    int jlo = ncy > 0 ? ry0 : 0x7fffffff, jhi = ncy > 1 ? ry1 : (ncy > 0 ? ry0 : -0x7fffffff);
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        jlo = min(jlo, __shfl_xor(jlo, sh));
+        jhi = max(jhi, __shfl_xor(jhi, sh));
+    }
+    const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
+    if (nrows > CR) err = true; // more tile rows than the table holds (not met by centred views)
+    // grid values of this lane's covering tile columns for every tile row the frame shows
+    auto grid_at = [&](int x, int y) -> int {
+        return (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x] : s.out_of_bounds_object;
+    };
+    int g0[CR], g1[CR];
+#pragma unroll
+    for (int j = 0; j < CR; j++) {
+        g0[j] = g1[j] = SPACE;
+        if (j < nrows && ncx > 0) g0[j] = grid_at(cx0, jy0 + j);
+        if (j < nrows && ncx > 1) g1[j] = grid_at(cx1, jy0 + j);
+    }
+    wave_sync(); // tile_off complete
+    auto slot_of = [&](int t) -> int { // 255: nothing drawn; a tile the fast path cannot draw sets err
+        if (t == INVALID_OBJ || t == SPACE) return 255;
+        if (t < 0 || t >= NTYPES) { err = true; return 255; }
+        if (tile_off[t] <= -2) err = true;
+        return tile_off[t] == -1 ? 255 : t;
+    };
+#pragma unroll
+    for (int j = 0; j < CR; j++)
+        if (j < nrows) codes[j * 64 + lane] = (uint16_t)(slot_of(g0[j]) | (slot_of(g1[j]) << 8));
+
+    // ---- visible images in draw order: z = 0 then z = 1 entities (the list order within each), then
+    //      the velocity squares (:969-977).  D0 = (ex.t1 | ex.n << 8 | ey.t1 << 16 | ey.n << 24, ex.base,
+    //      ex.step, ey.base), D1 = (ey.step, soff, sw | mir << 16 | z << 17 | ca << 20, fill)
+    int nd = 0;
+    auto put = [&](bool vis, const Img &im, int z) {
+        const unsigned long long vm = ballot(vis);
+        const int rank = nd + __popcll(vm & ((1ull << lane) - 1));
+        if (vis && rank < RF_DCAP) {
+            desc[2 * rank] = make_int4(im.ex.t1 | (im.ex.n << 8) | (im.ey.t1 << 16) | (im.ey.n << 24), (int)im.ex.base,
+                                       im.ex.step, (int)im.ey.base);
+            desc[2 * rank + 1] = make_int4(im.ey.step, im.soff, (im.sw & 0xffff) | (im.mir ? 1 << 16 : 0) | (z << 17) | (im.ca << 20),
+                                           (int)im.fill);
+        }
+        nd += __popcll(vm);
+    };
+    // (one setup per 64-entity chunk: the cursor below takes the z = 0 images before the z = 1 ones)
+    const int n = s.num_ents;
+    for (int base = 0; base < n; base += 64) {
+        Img im;
+        entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);
+        if (im.draw && (im.rot != 0 || im.ntile != 0)) err = true; // not reachable in rf games
+        const bool vis = im.draw && (im.ez == 0 || im.ez == 1);
+        put(vis, im, vis ? im.ez : 0);
+    }
+    if (__builtin_expect(s.has_useful_vel_info && s.opt_paint_vel_info, 0)) { // paint_vel_info (:969-977)
+        const float vx = s.agent_erased ? s.ghost_vx : EFr(d, F_VX, env, 0);
+        const float vy = s.agent_erased ? s.ghost_vy : EFr(d, F_VY, env, 0);
+        const float infodim = (float)(PG_RES * .2);
+        const uint32_t s1 = (uint32_t)to_shade((float)(.5 * (double)vx / (double)s.maxspeed + .5));
+        const uint32_t s2 = (uint32_t)to_shade((float)(.5 * (double)vy / (double)s.max_jump + .5));
+        Img im;
+        img_clear(im);
+        bool vis = false;
+        if (lane == 0) vis = fill_setup(0, 0, infodim, infodim, 0xff000000u | (s1 * 0x010101u), im);
+        if (lane == 1) vis = fill_setup(infodim, 0, infodim, infodim, 0xff000000u | (s2 * 0x010101u), im);
+        put(vis, im, 2);
+    }
+    if (nd > RF_DCAP) err = true;
+    nd = min(nd, RF_DCAP);
+    wave_sync(); // codes and desc complete
+
+    // per screen row (lane = row), packed for one readlane per row: source rows of its tile rows (7 bits
+    // each), their rows in `codes` (5 bits each), tile-row count (2 bits)
+    const int rinfo = ncy == 0 ? 0
+                    : (srow0 | ((ncy > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) | ((ncy > 1 ? ry1 - jy0 : ry0 - jy0) << 19) |
+                       (ncy << 24));
+    const int bgrow = bg_lane_row;
+    const uint32_t npix = d.num_pixels;
+    uint32_t *out = reinterpret_cast<uint32_t *>(d.rgb + (size_t)env * PG_OBS_BYTES);
+    for (int r0 = 0; r0 < PG_RES; r0 += RF_RB) {
+        // ---- image jobs: a cursor over the images crossing rows [r0, r0 + RF_RB) in draw order
+        int seg = 0, grp = 0; // segment = z * 2 + descriptor group (RF_DCAP = 128: two groups of 64)
+        unsigned long long mask = 0;
+        int C0 = 0, C1 = 0, C2 = 0, C3 = 0, C4 = 0, C5 = 0, C6 = 0, C7 = 0; // the current image's descriptor (uniform)
+        int y = 0, yend = 0;
+        auto next_image = [&]() -> bool {
+            while (mask == 0) {
+                if (seg >= 6) return false;
+                const int z = seg >> 1;
+                grp = (seg & 1) * 64;
+                seg++;
+                if (grp >= nd) continue;
+                const int k = grp + lane;
+                const bool live = k < nd;
+                const int4 A = desc[2 * (live ? k : 0)];
+                const int zz = (desc[2 * (live ? k : 0) + 1].z >> 17) & 3;
+                const int yt1 = (A.x >> 16) & 255, yn = (A.x >> 24) & 255;
+                mask = ballot(live && zz == z && yt1 < r0 + RF_RB && yt1 + yn > r0);
+            }
+            const int cur = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            const int4 A = desc[2 * (grp + cur)], B = desc[2 * (grp + cur) + 1];
+            C0 = __builtin_amdgcn_readfirstlane(A.x); C1 = __builtin_amdgcn_readfirstlane(A.y);
+            C2 = __builtin_amdgcn_readfirstlane(A.z); C3 = __builtin_amdgcn_readfirstlane(A.w);
+            C4 = __builtin_amdgcn_readfirstlane(B.x); C5 = __builtin_amdgcn_readfirstlane(B.y);
+            C6 = __builtin_amdgcn_readfirstlane(B.z); C7 = __builtin_amdgcn_readfirstlane(B.w);
+            const int yt1 = (C0 >> 16) & 255, yn = (C0 >> 24) & 255;
+            y = max(r0, yt1);
+            yend = min(r0 + RF_RB, yt1 + yn);
+            return true;
+        };
+        uint32_t jt[RF_JOBS];
+        int jr[RF_JOBS], jca[RF_JOBS];
+        bool more = next_image();
+        auto issue_jobs = [&]() {
+#pragma unroll
+            for (int q = 0; q < RF_JOBS; q++) {
+                jr[q] = -1;
+                jt[q] = 0;
+                jca[q] = 256;
+                if (more) {
+                    const uint32_t exb = (uint32_t)C1, eyb = (uint32_t)C3, soff = (uint32_t)C5, fill = (uint32_t)C7;
+                    const int exs = C2, eys = C4, w2 = C6;
+                    const int xt1 = C0 & 255, xn = (C0 >> 8) & 255, yt1 = (C0 >> 16) & 255;
+                    const int sw = w2 & 0xffff;
+                    const int dxl = lane - xt1;
+                    uint32_t t = 0;
+                    if ((unsigned)dxl < (unsigned)xn) {
+                        if (fill != 0) {
+                            t = fill;
+                        } else {
+                            int scol = (int)((exb + (uint32_t)(dxl * exs)) >> 16);
+                            if ((w2 >> 16) & 1) scol = sw - 1 - scol;
+                            const int srow = (int)((eyb + (uint32_t)((y - yt1) * eys)) >> 16);
+                            const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
+                            if (idx < npix) t = d.pixels[idx];
+                            else err = true;
+                        }
+                    }
+                    jt[q] = t;
+                    jr[q] = y - r0;
+                    jca[q] = (w2 >> 20) & 511;
+                    if (++y >= yend) more = next_image();
+                }
+            }
+        };
+        auto blend_jobs = [&](uint32_t (&px)[RF_RB]) {
+#pragma unroll
+            for (int q = 0; q < RF_JOBS; q++) {
+                if (jr[q] < 0) break; // uniform
+#pragma unroll
+                for (int k = 0; k < RF_RB; k++)
+                    if (k == jr[q]) px[k] = blend_argb_pm(px[k], jt[q], jca[q]);
+            }
+        };
+        // ---- background + grid tile texels of the batch
+        uint32_t px[RF_RB], t00[RF_RB], t01[RF_RB], t10[RF_RB], t11[RF_RB];
+#pragma unroll
+        for (int k = 0; k < RF_RB; k++) {
+            const int info = readlane(rinfo, r0 + k), br = readlane(bgrow, r0 + k);
+            const int nr = info >> 24;
+            const bool inb = bg_col && br >= 0;
+            const uint32_t bv = bgpix[inb ? bg_col_base + (uint32_t)br : 0u];
+            px[k] = inb ? bv : 0xff000000u;
+            const int c0 = codes[((info >> 14) & 31) * 64 + lane];
+            const int c1 = nr > 1 ? codes[((info >> 19) & 31) * 64 + lane] : 0xffff;
+            const int sr0 = (info & 127) * TP, sr1 = ((info >> 7) & 127) * TP;
+            t00[k] = t01[k] = t10[k] = t11[k] = 0;
+            if (nr > 0 && (c0 & 255) != 255) t00[k] = d.pixels[(uint32_t)tile_off[c0 & 255] + (uint32_t)(sr0 + scol0)];
+            if (nr > 1 && (c1 & 255) != 255) t01[k] = d.pixels[(uint32_t)tile_off[c1 & 255] + (uint32_t)(sr1 + scol0)];
+            if (nr > 0 && (c0 >> 8) != 255) t10[k] = d.pixels[(uint32_t)tile_off[c0 >> 8] + (uint32_t)(sr0 + scol1)];
+            if (nr > 1 && (c1 >> 8) != 255) t11[k] = d.pixels[(uint32_t)tile_off[c1 >> 8] + (uint32_t)(sr1 + scol1)];
+        }
+        issue_jobs(); // the first round of image texels rides on the same memory round trip
+        uint32_t part = 0;
+#pragma unroll
+        for (int k = 0; k < RF_RB; k++) part |= alpha_partial(t00[k]) | alpha_partial(t01[k]) | alpha_partial(t10[k]) | alpha_partial(t11[k]);
+        if (!ballot(part != 0)) {
+#pragma unroll
+            for (int k = 0; k < RF_RB; k++)
+                px[k] = over_binary(over_binary(over_binary(over_binary(px[k], t00[k]), t01[k]), t10[k]), t11[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < RF_RB; k++) {
+                px[k] = blend_argb_pm(px[k], t00[k], 256);
+                px[k] = blend_argb_pm(px[k], t01[k], 256);
+                px[k] = blend_argb_pm(px[k], t10[k], 256);
+                px[k] = blend_argb_pm(px[k], t11[k], 256);
+            }
+        }
+        blend_jobs(px);
+        while (more) {
+            issue_jobs();
+            blend_jobs(px);
+        }
+        // ---- bgr32_to_rgb888 (game.cpp:8-23): dword w of a row's 192 bytes takes bytes of pixels
+        //      4w / 3 and 4w / 3 + 1 (phase w % 3); lanes 0..47 store one dword each
+        const int p1 = (4 * lane) / 3, ph = lane % 3;
+#pragma unroll
+        for (int k = 0; k < RF_RB; k++) {
+            const uint32_t a = (uint32_t)__shfl((int)px[k], p1 & 63), b = (uint32_t)__shfl((int)px[k], (p1 + 1) & 63);
+            const uint32_t ra = (a >> 16) & 255, ga = (a >> 8) & 255, ba = a & 255;
+            const uint32_t rb = (b >> 16) & 255, gb = (b >> 8) & 255, bb2 = b & 255;
+            const uint32_t wv = ph == 0 ? (ra | (ga << 8) | (ba << 16) | (rb << 24))
+                              : ph == 1 ? (ga | (ba << 8) | (rb << 16) | (gb << 24))
+                                        : (ba | (rb << 8) | (gb << 16) | (bb2 << 24));
+            if (lane < 48) out[(r0 + k) * 48 + lane] = wv;
+        }
+    }
+    if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
+    }
 }
 
 // ================================================================== render_mode="rgb_array"
@@ -3769,7 +4174,10 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
     if (count <= 0) return;
 #define PG_CASE(G)                                                                              \
     case G:                                                                                     \
-        hipLaunchKernelGGL(pg_render_kernel<G>, dim3((count + PG_RENDER_K - 1) / PG_RENDER_K), dim3(64), 0, s, *d, env_list, mode, slot, count); \
+        if (rf_game<G>() && ((d->render_rf >> G) & 1))                                          \
+            hipLaunchKernelGGL(pg_render_rf_kernel<G>, dim3(count), dim3(64), 0, s, *d, env_list, mode, slot, count); \
+        else                                                                                    \
+            hipLaunchKernelGGL(pg_render_kernel<G>, dim3((count + PG_RENDER_K - 1) / PG_RENDER_K), dim3(64), 0, s, *d, env_list, mode, slot, count); \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

@@ -2948,7 +2948,10 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.s.prev_level_seed = c.s.current_level_seed;
     bool done = c.s.sd_done;
     bool first = done;
-    if (c.s.opt_use_sequential_levels && c.s.sd_level_complete) first = false;
+    if (c.s.opt_use_sequential_levels && c.s.sd_level_complete) { // step_data.done = false (game.cpp:164-166)
+        first = false;
+        c.s.sd_done = 0;
+    }
     c.s.episode_done = first;
 
     if (LANE == 0) {
