@@ -3008,7 +3008,7 @@ template <int G>
 __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const int32_t *env_list, int n, int parity,
                                                                 int use_hash, uint64_t hash_seed, int32_t hash_t,
                                                                 int slot) {
-    __shared__ uint32_t lds_mt[PG_MT_N];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_mt[PG_MT_N]; // 16-B aligned: the push memo reads uint4
     __shared__ int16_t lds_list[PG_CAP];
     __shared__ int16_t lds_slist[64];
     // the lane-parallel smart steps' interactor copy (pl_smart games only: LDS is what bounds the

@@ -13,9 +13,9 @@ published semantics (gym3 0.3.3 ``interop.py``):
   already the next episode's first frame.
 * infos are ``env.get_info()``, one dict per env.
 
-``render_mode="rgb_array"`` (the 512x512 antialiased ``info["rgb"]``) is built for every game (jumper
-in memory mode only: its compass is not restated at that resolution, and ``libenv_make`` rejects
-it); ``render_mode="human"`` needs gym3's ViewerWrapper window, which this build has not.
+``render_mode="rgb_array"`` (the 512x512 antialiased ``info["rgb"]``) is built for all 16 games,
+jumper's compass included in every distribution mode (drawn on the device, ``hc_draw_compass``);
+``render_mode="human"`` needs gym3's ViewerWrapper window, which this build has not.
 """
 import numpy as np
 

@@ -116,14 +116,16 @@ class ObsGather:
         local buffers, which may then be freed (the engine keeps a raw pointer while bound)."""
         if self.bind is None:
             return
-        if self.alive is not None and not self.alive():
-            self.bind = None
-            return
-        self.sync_engine()
-        if self.cuda:
+        engine_alive = self.alive is None or self.alive()
+        if engine_alive:
+            self.sync_engine()
+        if self.cuda:  # the gathers (torch's comm stream, not the engine's) have read the local buffers
             for ev in self.gathered:
                 if ev is not None:
                     ev.synchronize()
+        if not engine_alive:
+            self.bind = None
+            return
         try:
             self.bind(None)
         finally:

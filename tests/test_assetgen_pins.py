@@ -3,8 +3,9 @@
 The oracle's restatement of AssetGen (oracle/procgen_oracle.c, ag_*: assetgen.cpp:3-195 and the
 Qt 5.9 raster paths it paints with) against the REFERENCE's own assetgen.cpp + randgen.cpp compiled
 with the real Qt 5.9.7 of this image (oracle/ref_qt_harness.cpp -> oracle/_ref/libref_qt.so, built
-by `make -C oracle ref` in the build container, where /root/reference exists; the built library
-travels with the tree like the engine's .so, and these tests skip wherever it was not built):
+by `make -C oracle ref` in the build container, where /root/reference exists; the library is
+absent on the GPU box (oracle/_ref/ is listed in .gpurunignore), and these tests skip wherever it
+was not built):
 
 * whole generated images, bit for bit, plus the generator's position after painting (the next
   randint() must agree): 64x64 ARGB32 sprites (basic-abstract-game.cpp:101-107) in both the
