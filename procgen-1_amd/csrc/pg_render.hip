@@ -1521,10 +1521,13 @@ DEV constexpr int frame_rows() {
     // measured per game (profiles/r02/r02_k_variants.txt): two passes win for every game but
     // bossfight (48 rotated-image descriptors of LDS), jumper (compass overlay; 170 VGPRs spill) and
     // fruitbot (tile lists), which keep one full-frame pass at 2 waves per SIMD
+#ifdef PG_CR_ROWS
+    if (G == PG_GAME_COINRUN) return PG_CR_ROWS; // experiment: coinrun's LDS frame in passes of fewer rows
+#endif
     return (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT) ? 64 : 32;
 }
 template <int G>
-DEV constexpr int render_waves() { return frame_rows<G>() == 32 ? 3 : 2; }
+DEV constexpr int render_waves() { return frame_rows<G>() < 32 ? 4 : (frame_rows<G>() == 32 ? 3 : 2); }
 // rotated-image descriptors per 64-entity chunk (beyond them an image takes the in-order setup)
 template <int G>
 DEV constexpr int rot_cap() {

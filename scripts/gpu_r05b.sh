@@ -15,6 +15,7 @@ ab() { # name env-assignments game steps
 }
 ab coinrun_rf "A=0" coinrun 100 || exit 12
 ab coinrun_lds "PROCGEN_MI355X_RENDER_RF=0" coinrun 100 || exit 12
+for v in ${VARIANTS:-}; do ab coinrun_$v "PROCGEN_MI355X_RENDER_RF=0 PROCGEN_MI355X_LIB=$v" coinrun 100 || exit 12; done
 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_state_rollouts.py -x -v --timeout 600 --timeout-method thread ${SK:+-k "$SK"} > gpurun_out/b/pytest_state.log 2>&1 || { tail -30 gpurun_out/b/pytest_state.log; exit 13; }
 tail -25 gpurun_out/b/pytest_state.log
 exit 0

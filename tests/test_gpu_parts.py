@@ -43,3 +43,42 @@ def test_parts_reported(parts):
     env = make_gpu(64, "coinrun", num_levels=0, rand_seed=1)  # too few envs: one chain
     assert env.num_parts() == 1
     env.close()
+
+
+@pytest.mark.parametrize("serial", ["1", "0"])
+def test_parts_host_buffers_set_state_before_observe(serial, parts, monkeypatch):
+    """Host buffers with 3 parts, PROCGEN_MI355X_HOST_SERIAL on and off: each part's observations leave
+    on the copy stream as soon as it rendered (pg_capi.cpp launch_step).  A set_state between act and
+    observe re-renders (vecgame.cpp:503): observe must return the restored env's frame and step data,
+    not the early copy of the act's -- env 5 takes env 0's state and then plays env 0's game."""
+    parts(3)
+    monkeypatch.setenv("PROCGEN_MI355X_HOST_SERIAL", serial)
+    from test_gpu_coinrun import gpu_obs
+    num = 200
+    env = make_gpu(num, "coinrun", num_levels=0, rand_seed=6)
+    assert env.num_parts() == 3
+    rng = np.random.RandomState(7)
+    for t in range(1, 41):
+        act = rng.randint(0, 15, size=num).astype(np.int32)
+        act[5] = act[0]
+        env.act(act)
+        if t % 10 == 0:
+            st = env.get_state()
+            st[5] = st[0]
+            env.set_state(st)
+        g = gpu_obs(env)
+        if t >= 10:
+            for key in ("rgb", "rew", "first", "level_seed", "prev_level_seed", "prev_level_complete"):
+                np.testing.assert_array_equal(g[key][5], g[key][0], err_msg="%s differs at step %d" % (key, t))
+    env.close()
+
+
+def test_parts_two_prefetch_streams(parts, monkeypatch):
+    """PROCGEN_MI355X_PREFETCH_STREAMS=2 with parts: acts a and a+1 generate spares on different streams,
+    and act a+1's generation must wait for act a's whichever chain is enqueued first (host_serial
+    enqueues part 1 before part 0)."""
+    parts(3)
+    monkeypatch.setenv("PROCGEN_MI355X_PREFETCH", "1")
+    monkeypatch.setenv("PROCGEN_MI355X_PREFETCH_STREAMS", "2")
+    episodes, _ = run_pair("caveflyer", 192, 150, seed=33, num_levels=0, rand_seed=4)
+    assert episodes > 0
