@@ -469,6 +469,9 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
     return s;
 }
 
+// games that render with the register-frame kernel by default (pg_render.hip pg_render_rf_kernel)
+#define RF_DEFAULT (1 << PG_GAME_COINRUN)
+
 int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
@@ -1176,9 +1179,26 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     {
         // the register-frame render (pg_render_rf_kernel) for the games and options it serves;
         // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel
+        // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel; "all" or a comma list of
+        // game names picks the games (default: the games where it measured faster, RF_DEFAULT)
         const char *rf = getenv("PROCGEN_MI355X_RENDER_RF");
-        const bool on = (!rf || rf[0] != '0') && center_agent && !use_monochrome_assets && !use_generated_assets;
-        d.render_rf = on ? (1 << PG_GAME_COINRUN) : 0;
+        int mask = RF_DEFAULT;
+        if (rf && rf[0] == '0') mask = 0;
+        else if (rf && !strcmp(rf, "all")) mask = (1 << PG_NUM_GAMES) - 1;
+        else if (rf && rf[0]) {
+            mask = 0;
+            std::string list(rf);
+            size_t p0 = 0;
+            while (p0 <= list.size()) {
+                const size_t p1 = std::min(list.find(',', p0), list.size());
+                const std::string name = list.substr(p0, p1 - p0);
+                for (int g = 0; g < PG_NUM_GAMES; g++)
+                    if (name == pg_game_name(g)) mask |= 1 << g;
+                p0 = p1 + 1;
+            }
+        }
+        const bool on = center_agent && !use_monochrome_assets && !use_generated_assets;
+        d.render_rf = on ? mask : 0;
     }
     {
         const char *sp = getenv("PROCGEN_MI355X_SLOW_PREDICT");

@@ -1106,7 +1106,9 @@ DEV void entity_setup(const PGDev &d, const PGEnv &s, const View &v, int env, in
 // Transform blits of a chunk's rotated images, set up lane-parallel: a TxScale map becomes a plain
 // scale blit, a rotation's trapezoids and texture stepping go to descriptor slot `rank` in the aux
 // LDS (dead once the tiles are drawn); past `cap` descriptors an image keeps the in-order setup.
-DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
+// Descriptor slots start at `base` (the register-frame kernel continues the numbering over chunks);
+// returns the number of images that wanted a descriptor.
+DEV int rot_stage(Img &im, uint8_t *aux, int cap, int base = 0) {
     const int lane = LANE;
     Axis ex, ey;
     RotGeo g;
@@ -1116,7 +1118,8 @@ DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
     if (cand && kind == 0) im.draw = false;
     if (cand && kind == 1) { im.rot = 0; im.ex = ex; im.ey = ey; }
     const bool gen = cand && kind == 2;
-    const int rank = __popcll(ballot(gen) & ((1ull << lane) - 1));
+    const unsigned long long gm = ballot(gen);
+    const int rank = base + __popcll(gm & ((1ull << lane) - 1));
     if (gen && rank < cap) {
         int ymin = PG_RES, ymax = 0, xmin = PG_RES, xmax = 0;
 #pragma unroll
@@ -1152,6 +1155,7 @@ DEV void rot_stage(Img &im, uint8_t *aux, int cap) {
         im.ey.t1 = ymin; // the rows it covers, for the pass filter (ey is otherwise unused here)
         im.ey.n = ny;
     }
+    return __popcll(gm);
 }
 
 // ------------------------------------------------------------------ general pixel-centric tile pass
@@ -2110,23 +2114,203 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 // RF_RB screen rows at a time live in registers.  For every row batch, all texels the batch needs are
 // loaded before the first blend -- the background, the <= 2 x 2 grid tiles covering the pixel (x-major,
 // y-minor: basic-abstract-game.cpp:937-964) and the first RF_JOBS (image, row) jobs of the images that
-// cross the batch (z = 0 then z = 1 entities in list order, then the velocity squares: :966-977) -- then
-// blended in that order, packed to RGB888 across lanes (bgr32_to_rgb888, game.cpp:8-23) and stored.
-// Blending per pixel in draw order is the painter's algorithm of the reference pixel by pixel, and
-// every texel / edge is the one qt_scale_image_32bit / fillRect picks (the same Axis setup as the
-// stamping kernel).  The LDS holds only the tile table, the covering tiles' grid values per tile row
-// and the visible images' blit descriptors (<= RF_DCAP): ~6 KB per wave instead of 12 KB, so a CU keeps
-// twice the waves of the LDS-frame kernel resident to hide the gather latency (the render is
-// latency-bound: +4 KB of LDS per workgroup cost +19 % render time, profiles/r05/).
+// cross the batch (z = -1, then the tiles, then z = 0 / z = 1 entities in list order, the velocity
+// squares and the game's overlays: :930-977, games/*.cpp game_draw) -- then blended in that order,
+// packed to RGB888 across lanes (bgr32_to_rgb888, game.cpp:8-23) and stored.  Blending per pixel in
+// draw order is the painter's algorithm of the reference pixel by pixel; every texel, edge and
+// transform is the one the stamping kernel takes (the same Axis setup, Qt transform-blit descriptors,
+// fillRect edges, Qt-tabulated compass rows).  The LDS holds only the tile tables and the visible
+// images' descriptors (~6 KB for coinrun instead of the 12 KB frame kernel), so a CU keeps twice the
+// waves resident to hide the gather latency (the render is latency-bound: +4 KB of LDS per workgroup
+// cost +19 % render time, profiles/r05/).
 #ifndef RF_RB
 #define RF_RB 8
 #endif
 #ifndef RF_JOBS
 #define RF_JOBS 8
 #endif
-#define RF_DCAP 128
 template <int G>
-__host__ __device__ constexpr bool rf_game() { return G == PG_GAME_COINRUN; }
+__host__ __device__ constexpr bool rf_game() {
+    return G == PG_GAME_COINRUN || G == PG_GAME_BIGFISH || G == PG_GAME_MAZE || G == PG_GAME_HEIST || G == PG_GAME_MINER ||
+           G == PG_GAME_CLIMBER || G == PG_GAME_CHASER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER ||
+           G == PG_GAME_PLUNDER || G == PG_GAME_STARPILOT || G == PG_GAME_LEAPER || G == PG_GAME_DODGEBALL ||
+           G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT || G == PG_GAME_BOSSFIGHT;
+}
+// visible image descriptors per frame (tile_image entities become one per tile), Qt transform-blit
+// descriptors (96 B each, rot_stage)
+template <int G>
+DEV constexpr int rf_dcap() { return has_tiled_entities<G>() ? 256 : 128; }
+template <int G>
+DEV constexpr int rf_rcap() { return has_rotation<G>() ? ((G == PG_GAME_BOSSFIGHT || G == PG_GAME_STARPILOT) ? 96 : 64) : 1; }
+// descriptor kinds
+#define RF_PLAIN 0  // scale blit or fill of an axis-aligned rect
+#define RF_ROT 1    // Qt transform blit, descriptor in rdesc
+#define RF_ROWS 2   // Qt-tabulated row bitmap of one colour (jumper's compass)
+
+// General tile pass state, in registers (gen_setup without its LDS tables): lane = screen column: the
+// covering window columns (relative to low_x); lane = screen row: the covering window rows; per class
+// k the source column of this column's first | second covering window column (int16 each, -1: none)
+// and the source row of this row's first | second covering window row.
+struct RfGen {
+    int cx0, cx1, ncx, ry0, ry1, ncy;
+    int xs[GEN_K], ys[GEN_K];
+};
+
+// gen_setup for the register-frame kernel: ti (typeinfo, LDS) and gw (window slots, LDS) as there, the
+// class axes held per lane (lane = window column / row) and read across lanes.  0: not expressible,
+// 1: draw, 2: no drawn tile in the window.
+template <int G>
+DEV int rf_gen_setup(const PGDev &d, const PGEnv &s, const View &v, const int16_t *Gd, int player_img, int low_x,
+                     int low_y, int ww, int wh, int xg, int yg, int2 *ti, uint8_t *gw, RfGen &g) {
+    const int lane = LANE;
+    g.cx0 = g.cx1 = g.ry0 = g.ry1 = -1;
+    g.ncx = g.ncy = 0;
+#pragma unroll
+    for (int k = 0; k < GEN_K; k++) g.xs[k] = g.ys[k] = -1;
+    if (ww > 63 || wh > 63 || ww * wh > GEN_GW) return 0;
+    int kind = 0, off = 0, iw = 0, ih = 0;
+    {
+        const int t = gen_slot_type<G>(lane);
+        const int img = image_for_type<G>(s, t, player_img);
+        if (img >= 0) {
+            if (s.opt_use_monochrome_assets || img >= USE_ASSET_THRESHOLD) { // draw_grid_obj (:924-928)
+                if (img != SPACE) {
+                    if (G == PG_GAME_CHASER && img == CH_ORB) {
+                        kind = 3; off = (int)0xff00ff00u;
+                    } else if (s.opt_use_monochrome_assets) {
+                        const uint32_t col = color_for_type<G>(s, img, grid_theme<G>(s, t));
+                        if (col == 0) kind = GEN_BAD;
+                        else { kind = 2; off = (int)(col | 0xff000000u); }
+                    } else {
+                        kind = GEN_BAD;
+                    }
+                }
+            } else {
+                const int theme = mask_theme<G>(s, grid_theme<G>(s, t), img);
+                const int4 sp = reinterpret_cast<const int4 *>(d.sprites)[img + theme * MAX_ASSETS];
+                if (sp.y > 0) { kind = 1; off = sp.x; iw = sp.y; ih = sp.z; }
+                else if (!missing_image_ok<G>(img)) kind = GEN_BAD;
+            }
+        }
+    }
+    bool bad = false;
+    unsigned long long present = 0;
+    for (int c = lane; c < ww * wh; c += 64) {
+        const int x = low_x + c % ww, y = low_y + c / ww;
+        const int type = (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x]
+                                                                                   : s.out_of_bounds_object;
+        int sl = gen_slot<G>(type);
+        if (sl < 0) { bad = true; sl = GEN_NOTHING; }
+        if (sl < 64) present |= 1ull << sl;
+        gw[c] = (uint8_t)sl;
+    }
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const uint32_t lo = (uint32_t)present, hi = (uint32_t)(present >> 32);
+        present |= (unsigned long long)(uint32_t)__shfl_xor((int)lo, sh) | ((unsigned long long)(uint32_t)__shfl_xor((int)hi, sh) << 32);
+    }
+    const bool here = (present >> lane) & 1;
+    if (here && kind == GEN_BAD) bad = true;
+    if (ballot(bad)) return 0;
+    const bool drawn = here && kind >= 1 && kind <= 3;
+    const int key = kind == 1 ? (iw | (ih << 12) | (1 << 24)) : (kind << 24);
+    unsigned long long pend = ballot(drawn);
+    int cls = 0, K = 0;
+    int ck[GEN_K], cw[GEN_K], chh[GEN_K];
+#pragma unroll
+    for (int k = 0; k < GEN_K; k++) ck[k] = cw[k] = chh[k] = 0;
+    while (pend) {
+        const int f = __ffsll((long long)pend) - 1;
+        const int kf = readlane(key, f);
+        const unsigned long long mem = ballot(drawn && key == kf);
+        if (K < GEN_K) {
+            if (drawn && key == kf) cls = K;
+#pragma unroll
+            for (int k = 0; k < GEN_K; k++)
+                if (k == K) { ck[k] = readlane(kind, f); cw[k] = readlane(iw, f); chh[k] = readlane(ih, f); }
+        }
+        K++;
+        pend &= ~mem;
+    }
+    if (K > GEN_K) return 0;
+    if (K == 0) return 2;
+    ti[lane] = drawn ? make_int2(off, iw | (cls << 16) | (kind << 24)) : make_int2(0, 0);
+    if (lane == 0) ti[GEN_NOTHING] = make_int2(0, 0);
+    double rx = 0, rw = 0, ry = 0, rh = 0, t0, t1;
+    if (lane < ww) screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, t0, rw, t1);
+    if (lane < wh) screen_rect(v, 0.0f, (float)(low_y + lane + 1), 1, 1, RENDER_EPS, t0, ry, t1, rh);
+    // coverage: does any class's blit of window column xg + dx cover this screen column (and rows)
+    int covx = 0, covy = 0;
+#pragma unroll
+    for (int k = 0; k < GEN_K; k++) {
+        if (k >= K) break;
+        Axis a, b;
+        const bool okx = lane < ww && class_axis(ck[k], cw[k], rx, rw, a);
+        const bool oky = lane < wh && class_axis(ck[k], chh[k], ry, rh, b);
+        const int ax = okx ? (a.t1 | (a.n << 8)) : 0, by = oky ? (b.t1 | (b.n << 8)) : 0;
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const int x = xg - 2 + q, y = yg - 2 + q;
+            const int tx = __shfl(ax, (x - low_x) & 63), ty = __shfl(by, (y - low_y) & 63);
+            if (x >= low_x && x - low_x < ww && lane >= (tx & 255) && lane < (tx & 255) + (tx >> 8)) covx |= 1 << q;
+            if (y >= low_y && y - low_y < wh && lane >= (ty & 255) && lane < (ty & 255) + (ty >> 8)) covy |= 1 << q;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        if ((covx >> q) & 1) {
+            const int i = xg - 2 + q - low_x;
+            if (g.ncx == 0) g.cx0 = i; else if (g.ncx == 1) g.cx1 = i; else bad = true;
+            g.ncx++;
+        }
+        if ((covy >> q) & 1) {
+            const int j = yg - 2 + q - low_y;
+            if (g.ncy == 0) g.ry0 = j; else if (g.ncy == 1) g.ry1 = j; else bad = true;
+            g.ncy++;
+        }
+    }
+    if (ballot(bad)) return 0;
+    // per class: source column of this lane's covering columns, source row of this row's
+#pragma unroll
+    for (int k = 0; k < GEN_K; k++) {
+        if (k >= K) break;
+        Axis a, b;
+        const bool okx = lane < ww && class_axis(ck[k], cw[k], rx, rw, a);
+        const bool oky = lane < wh && class_axis(ck[k], chh[k], ry, rh, b);
+        const int at1 = okx ? a.t1 : 0, an = okx ? a.n : 0, bt1 = oky ? b.t1 : 0, bn = oky ? b.n : 0;
+        const int ab = okx ? (int)a.base : 0, as = okx ? a.step : 0, bb = oky ? (int)b.base : 0, bs = oky ? b.step : 0;
+        int v0 = -1, v1 = -1, w0 = -1, w1 = -1;
+        {
+            const int i0 = g.cx0 & 63, i1 = g.cx1 & 63, j0 = g.ry0 & 63, j1 = g.ry1 & 63;
+            const int t10 = __shfl(at1, i0), n0 = __shfl(an, i0), b0 = __shfl(ab, i0), s0 = __shfl(as, i0);
+            const int t11 = __shfl(at1, i1), n1 = __shfl(an, i1), b1 = __shfl(ab, i1), s1 = __shfl(as, i1);
+            const int u10 = __shfl(bt1, j0), m0 = __shfl(bn, j0), c0 = __shfl(bb, j0), r0 = __shfl(bs, j0);
+            const int u11 = __shfl(bt1, j1), m1 = __shfl(bn, j1), c1 = __shfl(bb, j1), r1 = __shfl(bs, j1);
+            if (g.ncx > 0 && n0 > 0 && lane >= t10 && lane < t10 + n0) v0 = (int)(((uint32_t)b0 + (uint32_t)((lane - t10) * s0)) >> 16);
+            if (g.ncx > 1 && n1 > 0 && lane >= t11 && lane < t11 + n1) v1 = (int)(((uint32_t)b1 + (uint32_t)((lane - t11) * s1)) >> 16);
+            if (g.ncy > 0 && m0 > 0 && lane >= u10 && lane < u10 + m0) w0 = (int)(((uint32_t)c0 + (uint32_t)((lane - u10) * r0)) >> 16);
+            if (g.ncy > 1 && m1 > 0 && lane >= u11 && lane < u11 + m1) w1 = (int)(((uint32_t)c1 + (uint32_t)((lane - u11) * r1)) >> 16);
+        }
+        g.xs[k] = (v0 & 0xffff) | (v1 << 16);
+        g.ys[k] = (w0 & 0xffff) | (w1 << 16);
+    }
+    return 1;
+}
+
+// the texel of general-pass cell t at the class's source column / row (gen_texel with packed tables)
+DEV uint32_t rf_gen_texel(const PGDev &d, const int2 t, const int (&xs)[GEN_K], const int (&ysr)[GEN_K], bool second_col,
+                          bool second_row, bool &err) {
+    const int kind = t.y >> 24;
+    if (kind == 0) return 0u;
+    const int cl = (t.y >> 16) & 255;
+    int xv = xs[0], yv = ysr[0];
+#pragma unroll
+    for (int k = 1; k < GEN_K; k++)
+        if (cl == k) { xv = xs[k]; yv = ysr[k]; }
+    const int sc = second_col ? (xv >> 16) : (int)(int16_t)(xv & 0xffff);
+    const int sr = second_row ? (yv >> 16) : (int)(int16_t)(yv & 0xffff);
+    return gen_texel(d, t, sc, sr, err);
+}
 
 template <int G>
 __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
@@ -2134,15 +2318,21 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         return;
     } else {
     const PGDev d = game_view(dg, G);
+    constexpr bool FAST = always_uniform<G>();             // square tile_px() tiles: grid value tables
+    constexpr bool GEN = has_general<G>();                 // the general tile pass
     constexpr int CR = crows<G>();
     constexpr int TP = tile_px<G>();
-    static_assert(TP > 0 && always_uniform<G>() && !has_z_minus1<G>() && !has_rotation<G>() && !has_tiled_entities<G>(),
-                  "the register-frame path draws square grid tiles and plain entity blits only");
-    __shared__ int tile_off[NTYPES];
-    // grid value (255: nothing) of the first | second covering tile column, per window tile row and lane
-    __shared__ __attribute__((aligned(16))) uint16_t codes[CR * 64];
-    // blit descriptors of the visible images in draw order (two int4 each, see below)
-    __shared__ __attribute__((aligned(16))) int4 desc[2 * RF_DCAP];
+    constexpr int DCAP = rf_dcap<G>(), RCAP = rf_rcap<G>();
+    constexpr int TAB_BYTES = FAST ? NTYPES * 4 + CR * 64 * 2 : (GEN ? GEN_TI_BYTES + GEN_GW : 16);
+    // FAST: tile_off[NTYPES] | codes[CR][64] (grid value of the first | second covering tile column per
+    // window tile row and lane, 255: nothing); GEN: typeinfo ti[65] | window slots gw[GEN_GW]
+    __shared__ __attribute__((aligned(16))) uint8_t tab[TAB_BYTES];
+    __shared__ __attribute__((aligned(16))) int4 desc[2 * DCAP];
+    __shared__ __attribute__((aligned(16))) int4 rdesc[6 * RCAP];
+    int *const tile_off = reinterpret_cast<int *>(tab);
+    uint16_t *const codes = reinterpret_cast<uint16_t *>(tab + NTYPES * 4);
+    int2 *const ti = reinterpret_cast<int2 *>(tab);
+    uint8_t *const gw = tab + GEN_TI_BYTES;
     const int lane = LANE;
     const int bidx = (int)blockIdx.x;
     int env;
@@ -2160,8 +2350,7 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
     int player_img;
     const View v = prepare_view<G>(d, s, env, player_img);
 
-    // ---- grid type -> sprite pixel offset (theme_for_grid_obj, image_for_type, draw_image :886-922)
-    {
+    if constexpr (FAST) { // grid type -> sprite pixel offset (theme_for_grid_obj, image_for_type, draw_image :886-922)
         int off = -1;
         const int img = image_for_type<G>(s, lane, player_img);
         if (img >= 0) {
@@ -2196,14 +2385,14 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         const double ax = (double)(-offset_x), aw = (double)(bg_ar / world_ar); // adjust_rect (qt-utils.h:12-19)
         bg_rx = mx + mw * ax; bg_ry = my + mh * 0.0; bg_rw = mw * aw; bg_rh = mh * 1.0;
     }
-    Axis ca_ = {0, 0, 0u, 0}, ra_ = {0, 0, 0u, 0}; // this lane's column / row axis
+    Axis ca_ = {0, 0, 0u, 0}, ra_ = {0, 0, 0u, 0}; // this lane's column / row axis (FAST), lane 63: background
     bool okx, oky;
     {
         double xr = 0, xw = 0, yr = 0, yh = 0;
         int xiw = 0, yih = 0;
         if (lane == 63) {
             if (s.opt_use_backgrounds) { xr = bg_rx; xw = bg_rw; xiw = bgi.y; yr = bg_ry; yh = bg_rh; yih = bgi.z; }
-        } else {
+        } else if (FAST) {
             double rx, ry, rw, rh;
             if (lane < ww) {
                 screen_rect(v, (float)(low_x + lane), 0.0f, 1, 1, RENDER_EPS, rx, ry, rw, rh);
@@ -2254,90 +2443,190 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         }
         if (!bg_tiled_ok) bg_lane_row = -1;
     }
-    const bool bg_col = bg_tiled_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
-    const uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
+    bool bg_col = bg_tiled_ok && lane >= bx.t1 && lane < bx.t1 + bx.n;
+    uint32_t bg_col_base = (uint32_t)bgi.x + (bg_col ? (bx.base + (uint32_t)((lane - bx.t1) * bx.step)) >> 16 : 0);
+    if constexpr (G == PG_GAME_STARPILOT) {
+        // starpilot game_draw (starpilot.cpp:107-124): tile_image(r_bg, 1) of a background scrolled left
+        // by cur_time -- 18 square tiles side by side; a screen column shows the last tile covering it
+        bg_col = false;
+        bg_lane_row = -1;
+        if (s.opt_use_backgrounds) {
+            const float scale = (float)(PG_RES / s.main_height); // int / int
+            const float bg_k = 3, t = (float)s.cur_time, BG_RATIO = 18;
+            const float x_off = -t * scale * SP_HP_SLOW_V * 2 / s.char_dim;
+            const double rx = (double)x_off, ry = (double)(-PG_RES * (bg_k - 1) / 2);
+            const double rw = (double)(PG_RES * bg_k * BG_RATIO), rh = (double)(PG_RES * bg_k);
+            int num_tiles = (int)(rw / (rh * 1.0f));
+            if (num_tiles < 1) num_tiles = 1;
+            const float tw = (float)(rw / num_tiles), th = (float)rh;
+            Axis sy;
+            const bool sok = axis_setup(ry, (double)th, bgi.z, sy);
+            bg_lane_row = (sok && lane >= sy.t1 && lane < sy.t1 + sy.n)
+                              ? (int)(((sy.base + (uint32_t)((lane - sy.t1) * sy.step)) >> 16) * (uint32_t)bgi.y)
+                              : -1;
+            for (int t0 = 0; t0 < num_tiles; t0 += 64) {
+                Axis tx;
+                const int k0 = t0 + lane;
+                const bool okt = k0 < num_tiles && axis_setup(rx + (double)(tw * (float)k0), (double)tw, bgi.y, tx);
+                const int tt1 = okt ? tx.t1 : 0, tn = okt ? tx.n : 0, tstep = okt ? tx.step : 0;
+                const uint32_t tbase = okt ? tx.base : 0u;
+                for (int k = 0; k < 64 && t0 + k < num_tiles; k++) {
+                    const int a1 = readlane(tt1, k), an = readlane(tn, k);
+                    if (lane >= a1 && lane < a1 + an) {
+                        const uint32_t bb = (uint32_t)readlane((int)tbase, k);
+                        const int st = readlane(tstep, k);
+                        bg_col = true;
+                        bg_col_base = (uint32_t)bgi.x + ((bb + (uint32_t)((lane - a1) * st)) >> 16);
+                    }
+                }
+            }
+            if (!sok) bg_col = false;
+        }
+    }
     const uint32_t *bgpix = d.pixels;
 
-    // ---- tile columns covering screen column `lane` (<= 2, ascending x) and tile rows covering screen
-    //      row `lane` (<= 2, ascending y = the reference's draw order): the column / row axes of the
-    //      window live one per lane and are read across lanes
+    // ---- grid tiles: the tile columns covering screen column `lane` (<= 2, ascending x) and the tile
+    //      rows covering screen row `lane` (<= 2, ascending y = the reference's draw order)
     const int xg = (int)floorf(((float)lane + 0.5f + v.x_off) / v.unit);
     const int yg = (int)floorf((v.view_dim - ((float)lane + 0.5f - v.y_off) / v.unit));
-    int cx0 = 0, cx1 = 0, ncx = 0, scol0 = 0, scol1 = 0;
-    int ry0 = 0, ry1 = 0, ncy = 0, srow0 = 0, srow1 = 0;
+    int scol0 = 0, scol1 = 0, rinfo = 0; // FAST: source columns; per row (lane = row) the packed row info
+    RfGen gn;
+    bool tiles = false;
+    if constexpr (FAST) {
+        int cx0 = 0, cx1 = 0, ncx = 0, ry0 = 0, ry1 = 0, ncy = 0, srow0 = 0, srow1 = 0;
 #pragma unroll
-    for (int dx = -2; dx <= 2; dx++) {
-        const int x = xg + dx, i = (x - low_x) & 63;
-        const int t1 = __shfl(ca_.t1, i), n = __shfl(ca_.n, i), b = __shfl((int)ca_.base, i), st = __shfl(ca_.step, i);
-        if (x >= low_x && x <= high_x && ncx < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
-            const int scv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
-            if (ncx == 0) { cx0 = x; scol0 = scv; } else { cx1 = x; scol1 = scv; }
-            ncx++;
+        for (int dx = -2; dx <= 2; dx++) {
+            const int x = xg + dx, i = (x - low_x) & 63;
+            const int t1 = __shfl(ca_.t1, i), n = __shfl(ca_.n, i), b = __shfl((int)ca_.base, i), st = __shfl(ca_.step, i);
+            if (x >= low_x && x <= high_x && ncx < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
+                const int scv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
+                if (ncx == 0) { cx0 = x; scol0 = scv; } else { cx1 = x; scol1 = scv; }
+                ncx++;
+            }
         }
-    }
 #pragma unroll
-    for (int dy = -2; dy <= 2; dy++) {
-        const int y = yg + dy, i = (y - low_y) & 63;
-        const int t1 = __shfl(ra_.t1, i), n = __shfl(ra_.n, i), b = __shfl((int)ra_.base, i), st = __shfl(ra_.step, i);
-        if (y >= low_y && y <= high_y && ncy < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
-            const int srv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
-            if (ncy == 0) { ry0 = y; srow0 = srv; } else { ry1 = y; srow1 = srv; }
-            ncy++;
+        for (int dy = -2; dy <= 2; dy++) {
+            const int y = yg + dy, i = (y - low_y) & 63;
+            const int t1 = __shfl(ra_.t1, i), n = __shfl(ra_.n, i), b = __shfl((int)ra_.base, i), st = __shfl(ra_.step, i);
+            if (y >= low_y && y <= high_y && ncy < 2 && n > 0 && lane >= t1 && lane < t1 + n) {
+                const int srv = (int)(((uint32_t)b + (uint32_t)((lane - t1) * st)) >> 16);
+                if (ncy == 0) { ry0 = y; srow0 = srv; } else { ry1 = y; srow1 = srv; }
+                ncy++;
+            }
         }
-    }
-    int jlo = ncy > 0 ? ry0 : 0x7fffffff, jhi = ncy > 1 ? ry1 : (ncy > 0 ? ry0 : -0x7fffffff);
+        int jlo = ncy > 0 ? ry0 : 0x7fffffff, jhi = ncy > 1 ? ry1 : (ncy > 0 ? ry0 : -0x7fffffff);
 #pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) {
-        jlo = min(jlo, __shfl_xor(jlo, sh));
-        jhi = max(jhi, __shfl_xor(jhi, sh));
-    }
-    const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
-    if (nrows > CR) err = true; // more tile rows than the table holds (not met by centred views)
-    // grid values of this lane's covering tile columns for every tile row the frame shows
-    auto grid_at = [&](int x, int y) -> int {
-        return (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x] : s.out_of_bounds_object;
-    };
-    int g0[CR], g1[CR];
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            jlo = min(jlo, __shfl_xor(jlo, sh));
+            jhi = max(jhi, __shfl_xor(jhi, sh));
+        }
+        const int jy0 = jlo, nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
+        if (nrows > CR) err = true; // more tile rows than the table holds (not met by centred views)
+        auto grid_at = [&](int x, int y) -> int {
+            return (0 <= y && y < s.main_height && 0 <= x && x < s.main_width) ? Gd[y * s.main_width + x] : s.out_of_bounds_object;
+        };
+        int g0[CR], g1[CR];
 #pragma unroll
-    for (int j = 0; j < CR; j++) {
-        g0[j] = g1[j] = SPACE;
-        if (j < nrows && ncx > 0) g0[j] = grid_at(cx0, jy0 + j);
-        if (j < nrows && ncx > 1) g1[j] = grid_at(cx1, jy0 + j);
-    }
-    wave_sync(); // tile_off complete
-    auto slot_of = [&](int t) -> int { // 255: nothing drawn; a tile the fast path cannot draw sets err
-        if (t == INVALID_OBJ || t == SPACE) return 255;
-        if (t < 0 || t >= NTYPES) { err = true; return 255; }
-        if (tile_off[t] <= -2) err = true;
-        return tile_off[t] == -1 ? 255 : t;
-    };
+        for (int j = 0; j < CR; j++) {
+            g0[j] = g1[j] = SPACE;
+            if (j < nrows && ncx > 0) g0[j] = grid_at(cx0, jy0 + j);
+            if (j < nrows && ncx > 1) g1[j] = grid_at(cx1, jy0 + j);
+        }
+        wave_sync(); // tile_off complete
+        auto slot_of = [&](int t) -> int { // 255: nothing drawn; a tile the fast path cannot draw sets err
+            if (t == INVALID_OBJ || t == SPACE) return 255;
+            if (t < 0 || t >= NTYPES) { err = true; return 255; }
+            if (tile_off[t] <= -2) err = true;
+            return tile_off[t] == -1 ? 255 : t;
+        };
 #pragma unroll
-    for (int j = 0; j < CR; j++)
-        if (j < nrows) codes[j * 64 + lane] = (uint16_t)(slot_of(g0[j]) | (slot_of(g1[j]) << 8));
+        for (int j = 0; j < CR; j++)
+            if (j < nrows) codes[j * 64 + lane] = (uint16_t)(slot_of(g0[j]) | (slot_of(g1[j]) << 8));
+        // per screen row: source rows of its tile rows (7 bits each), their rows in `codes` (5 bits each),
+        // tile-row count (2 bits)
+        rinfo = ncy == 0 ? 0
+              : (srow0 | ((ncy > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) | ((ncy > 1 ? ry1 - jy0 : ry0 - jy0) << 19) |
+                 (ncy << 24));
+        tiles = true;
+    } else if constexpr (GEN) {
+        const int gs = rf_gen_setup<G>(d, s, v, Gd, player_img, low_x, low_y, ww, wh, xg, yg, ti, gw, gn);
+        if (gs == 0) err = true; // not expressible (LDS-frame kernel: the stamped tile pass)
+        tiles = gs == 1;
+        rinfo = gn.ncy == 0 ? 0 : (gn.ry0 | ((gn.ncy > 1 ? gn.ry1 : 0) << 8) | (gn.ncy << 16));
+    }
 
-    // ---- visible images in draw order: z = 0 then z = 1 entities (the list order within each), then
-    //      the velocity squares (:969-977).  D0 = (ex.t1 | ex.n << 8 | ey.t1 << 16 | ey.n << 24, ex.base,
-    //      ex.step, ey.base), D1 = (ey.step, soff, sw | mir << 16 | z << 17 | ca << 20, fill)
-    int nd = 0;
-    auto put = [&](bool vis, const Img &im, int z) {
+    // ---- visible images in draw order: z = -1, 0, 1 entities (the list order within each), the
+    //      velocity squares (:969-977), the game's overlays.  D0 = (ex.t1 | ex.n << 8 | ey.t1 << 16 |
+    //      ey.n << 24, A, B, C), D1 = (E, F, sw | mir << 13 | (z + 1) << 14 | kind << 17 | ca << 19, fill);
+    //      plain: A..F = ex.base, ex.step, ey.base, ey.step, soff; RF_ROT: A = rdesc slot; RF_ROWS: A = row
+    //      table offset, B, C = dx, dy, fill = colour
+    int nd = 0, nrot = 0;
+    auto put = [&](bool vis, const Img &im, int z, int kind, int a, int b, int c) {
         const unsigned long long vm = ballot(vis);
         const int rank = nd + __popcll(vm & ((1ull << lane) - 1));
-        if (vis && rank < RF_DCAP) {
-            desc[2 * rank] = make_int4(im.ex.t1 | (im.ex.n << 8) | (im.ey.t1 << 16) | (im.ey.n << 24), (int)im.ex.base,
-                                       im.ex.step, (int)im.ey.base);
-            desc[2 * rank + 1] = make_int4(im.ey.step, im.soff, (im.sw & 0xffff) | (im.mir ? 1 << 16 : 0) | (z << 17) | (im.ca << 20),
+        if (vis && rank < DCAP) {
+            const bool pl = kind == RF_PLAIN;
+            desc[2 * rank] = make_int4(im.ex.t1 | (im.ex.n << 8) | (im.ey.t1 << 16) | (im.ey.n << 24),
+                                       pl ? (int)im.ex.base : a, pl ? im.ex.step : b, pl ? (int)im.ey.base : c);
+            desc[2 * rank + 1] = make_int4(pl ? im.ey.step : 0, pl ? im.soff : 0,
+                                           (im.sw & 0x1fff) | (im.mir ? 1 << 13 : 0) | ((z + 1) << 14) | (kind << 17) | (im.ca << 19),
                                            (int)im.fill);
         }
         nd += __popcll(vm);
     };
-    // (one setup per 64-entity chunk: the cursor below takes the z = 0 images before the z = 1 ones)
+    auto put_plain = [&](bool vis, const Img &im, int z) { put(vis, im, z, RF_PLAIN, 0, 0, 0); };
     const int n = s.num_ents;
     for (int base = 0; base < n; base += 64) {
         Img im;
         entity_setup<G>(d, s, v, env, base + lane, n, player_img, im, err);
-        if (im.draw && (im.rot != 0 || im.ntile != 0)) err = true; // not reachable in rf games
-        const bool vis = im.draw && (im.ez == 0 || im.ez == 1);
-        put(vis, im, vis ? im.ez : 0);
+        if constexpr (has_rotation<G>()) {
+            nrot += rot_stage(im, reinterpret_cast<uint8_t *>(rdesc), RCAP, nrot);
+            if (im.draw && im.rot == 1) err = true; // past RCAP descriptors
+        }
+        const bool vis = im.draw && (im.ez == 0 || im.ez == 1 || (has_z_minus1<G>() && im.ez == -1));
+        const int z = vis ? im.ez : 0;
+        const unsigned long long tm = has_tiled_entities<G>() ? ballot(vis && im.ntile > 0) : 0ull;
+        if (!tm) {
+            put(vis, im, z, im.rot == 2 ? RF_ROT : RF_PLAIN, im.rdi, 0, 0);
+        } else {
+            // tile_image entities (:849-877) become one plain descriptor per tile, in the entity's place
+            unsigned long long rem = ballot(vis);
+            while (rem) {
+                const unsigned long long tl = rem & tm;
+                const int jt = tl ? __ffsll((long long)tl) - 1 : 64;
+                const unsigned long long run = rem & (jt < 64 ? ((1ull << jt) - 1) : ~0ull);
+                put(((run >> lane) & 1) != 0, im, z, im.rot == 2 ? RF_ROT : RF_PLAIN, im.rdi, 0, 0);
+                rem &= ~run;
+                if (jt == 64) break;
+                rem &= ~(1ull << jt);
+                const int ntile = readlane(im.ntile, jt), zj = readlane(z, jt);
+                const double rx = readlane_d(im.rx, jt), ry = readlane_d(im.ry, jt);
+                const float tw = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.tw), jt));
+                const float th = __builtin_bit_cast(float, readlane(__builtin_bit_cast(int, im.th), jt));
+                const int vert = readlane(im.rslot, jt);
+                const int offj = readlane(im.soff, jt), swj = readlane(im.sw, jt), shj = readlane(im.sh, jt);
+                const int mirj = readlane(im.mir, jt), caj = readlane(im.ca, jt);
+                const double tsz = vert ? (double)th : (double)tw, org = vert ? ry : rx;
+                int tlo = 0, thi = ntile;
+                if (tsz > 0) {
+                    tlo = max(0, (int)floor((-2.0 - org) / tsz) - 1);
+                    thi = min(ntile, (int)ceil((PG_RES + 2.0 - org) / tsz) + 1);
+                }
+                for (int t0 = tlo; t0 < thi; t0 += 64) {
+                    Img tim;
+                    img_clear(tim);
+                    const int t = t0 + lane;
+                    bool ok = false;
+                    if (t < thi) {
+                        const double x = vert ? rx : rx + (double)(tw * (float)t);
+                        const double y = vert ? ry + (double)(th * (float)t) : ry;
+                        ok = axis_setup(x, (double)tw, swj, tim.ex) && axis_setup(y, (double)th, shj, tim.ey);
+                        tim.soff = offj; tim.sw = swj; tim.sh = shj; tim.mir = mirj; tim.ca = caj;
+                    }
+                    put_plain(ok, tim, zj);
+                }
+            }
+        }
     }
     if (__builtin_expect(s.has_useful_vel_info && s.opt_paint_vel_info, 0)) { // paint_vel_info (:969-977)
         const float vx = s.agent_erased ? s.ghost_vx : EFr(d, F_VX, env, 0);
@@ -2350,37 +2639,122 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         bool vis = false;
         if (lane == 0) vis = fill_setup(0, 0, infodim, infodim, 0xff000000u | (s1 * 0x010101u), im);
         if (lane == 1) vis = fill_setup(infodim, 0, infodim, infodim, 0xff000000u | (s2 * 0x010101u), im);
-        put(vis, im, 2);
+        put_plain(vis, im, 2);
     }
-    if (nd > RF_DCAP) err = true;
-    nd = min(nd, RF_DCAP);
-    wave_sync(); // codes and desc complete
+    // ---- game_draw overlays (game_overlay): fills, jumper's compass rows
+    if constexpr (G == PG_GAME_NINJA || G == PG_GAME_PLUNDER) {
+        Img im;
+        img_clear(im);
+        bool vis = false;
+        const float u = v.unit;
+        if constexpr (G == PG_GAME_NINJA) { // jump charge bar (ninja.cpp:155-164)
+            const float bar_height = 3 * s.gs.nj.jump_charge;
+            if (lane == 0)
+                vis = fill_setup((double)(.25f * u), (double)((float)(v.visibility - .5 - bar_height) * u), (double)(.5f * u),
+                                 (double)(bar_height * u), 0xff42f587u, im);
+        } else { // juice and progress bars (plunder.cpp:66-77)
+            const float prog = (float)(s.main_width * (s.gs.pl.targets_hit * 1.0 / s.gs.pl.target_quota));
+            if (lane == 0)
+                vis = fill_setup((double)(.25f * u), (double)(.25f * u), (double)(s.main_width * s.gs.pl.juice_left * u),
+                                 (double)(.5f * u), 0xff42f587u, im);
+            if (lane == 1)
+                vis = fill_setup((double)(.25f * u), (double)(.75f * u), (double)(prog * u), (double)(.5f * u), 0xfff54290u, im);
+        }
+        put_plain(vis, im, 3);
+    }
+    if constexpr (G == PG_GAME_JUMPER) {
+        if (s.opt_distribution_mode != PG_MEMORY) { // jp_draw_compass (jumper.cpp:137-177)
+            bool ok = true;
+            const int4 tix = reinterpret_cast<const int4 *>(d.sprites)[PG_TABLE_SLOT];
+            const uint32_t toff = (uint32_t)tix.x;
+            const uint32_t *t = d.pixels + toff;
+            int NY = 0, NX = 0, MAXW = 0, MAXH = 0;
+            if (tix.y <= 0) ok = false;
+            else { NY = (int)t[1]; NX = (int)t[2]; MAXW = (int)t[3]; MAXH = (int)t[4]; }
+            const int cfg = (s.opt_distribution_mode == PG_EASY ? 0 : 1) + (s.opt_center_agent ? 0 : 2);
+            const float u = v.unit, vd = v.view_dim, cd = s.gs.jp.compass_dim;
+            int rows[3] = {-1, -1, -1}, rdx[3] = {0, 0, 0}, rdy[3] = {0, 0, 0};
+            uint32_t rcol[3] = {0xffa8a69eu, 0xfffcba03u, 0x78787878u};
+            Img bar;
+            img_clear(bar);
+            bool bar_vis = false;
+            if (ok) {
+                const uint32_t *cg = t + 5 + 9 * cfg;
+                const int bx0 = (int)cg[2], by0 = (int)cg[3], bnx = (int)cg[4], bny = (int)cg[5];
+                const float cx = __uint_as_float(cg[6]), cy = __uint_as_float(cg[7]), cr = __uint_as_float(cg[8]);
+                const uint32_t dial = 5 + 36, needle = dial + 4 * 128;
+                const uint32_t jump = needle + (uint32_t)(4 * NY * NX * 128);
+                const double rx = (double)((float)(vd - cd - .25) * u), rw = (double)(cd * u);
+                if ((float)(rx + rw / 2) != cx) ok = false; // the table was built for this frame geometry
+                rows[0] = (int)(toff + dial + 128 * cfg);
+                const float ax = EFr(d, F_X, env, 0), ay = EFr(d, F_Y, env, 0), arx = EFr(d, F_RX, env, 0), ary = EFr(d, F_RY, env, 0);
+                const float gx = EFr(d, F_X, env, 1), gy = EFr(d, F_Y, env, 1);
+                const float theta = (float)atan2((double)(gy - ay), (double)(gx - ax)); // get_theta (:241-246)
+                double sn, cs;
+                pg_sincos_cr((double)theta, &sn, &cs);
+                const int x2 = (int)((double)cx + (double)cr * cs), y2 = (int)((double)cy - (double)cr * sn);
+                if (x2 < bx0 || x2 >= bx0 + bnx || y2 < by0 || y2 >= by0 + bny) ok = false;
+                else rows[1] = (int)(toff + needle + (uint32_t)(((cfg * NY + (y2 - by0)) * NX + (x2 - bx0)) * 128));
+                const float ddx = ax - gx, ddy = ay - gy; // get_distance (:133-143)
+                const float dist = (float)sqrt((double)(ddx * ddx + ddy * ddy));
+                const float dist_pct = (float)((double)dist / (s.main_width * 1.4142135623730951));
+                const float bar_thickness = cd / 8;
+                bar_vis = fill_setup((double)((float)(vd - cd - .25) * u), (double)((float)(.25 + cd) * u),
+                                     (double)(cd * dist_pct * u), (double)(bar_thickness * u), 0xfffcba03u, bar);
+                if (s.gs.jp.jump_delta < 0 && !s.has_support) { // drawEllipse(QRect(...)) of get_object_rect(agent)
+                    double r1x, r1y, r1w, r1h;
+                    screen_rect(v, ax - arx, ay + ary, 2 * arx, 2 * ary, 0, r1x, r1y, r1w, r1h);
+                    const int qx = (int)r1x, qy = (int)(r1y + r1h * (5.0 / 6)), qw = (int)r1w, qh = (int)(r1h / 3);
+                    if (qw < 0 || qw > MAXW || qh < 0 || qh > MAXH) ok = false;
+                    else { rows[2] = (int)(toff + jump + (uint32_t)((qw * (MAXH + 1) + qh) * 128)); rdx[2] = qx - 20; rdy[2] = qy - 20; }
+                }
+            }
+            if (!ok) err = true;
+            // the row bitmaps in draw order (dial, needle; bar; jump ellipse), each with the rows it sets
+            for (int k = 0; k < 3; k++) {
+                if (k == 2) put_plain(lane == 0 && bar_vis, bar, 3);
+                if (rows[k] < 0 || rdx[k] <= -64 || rdx[k] >= 64) continue;
+                const int sy = lane; // bitmap row
+                const uint32_t w0 = d.pixels[(uint32_t)rows[k] + 2 * sy], w1 = d.pixels[(uint32_t)rows[k] + 2 * sy + 1];
+                uint64_t m = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                m = rdx[k] >= 0 ? (m << rdx[k]) : (m >> -rdx[k]);
+                const int y = sy + rdy[k];
+                const unsigned long long nz = ballot(m != 0 && y >= 0 && y < PG_RES);
+                if (!nz) continue;
+                const int y0 = __ffsll((long long)nz) - 1 + rdy[k], y1 = 63 - __clzll(nz) + rdy[k] + 1;
+                Img im;
+                img_clear(im);
+                im.ex.t1 = 0; im.ex.n = PG_RES; im.ey.t1 = y0; im.ey.n = y1 - y0; im.fill = rcol[k];
+                put(lane == 0, im, 3, RF_ROWS, rows[k], rdx[k], rdy[k]);
+            }
+        }
+    }
+    if (nd > DCAP) err = true;
+    nd = min(nd, DCAP);
+    wave_sync(); // tables and descriptors complete
 
-    // per screen row (lane = row), packed for one readlane per row: source rows of its tile rows (7 bits
-    // each), their rows in `codes` (5 bits each), tile-row count (2 bits)
-    const int rinfo = ncy == 0 ? 0
-                    : (srow0 | ((ncy > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) | ((ncy > 1 ? ry1 - jy0 : ry0 - jy0) << 19) |
-                       (ncy << 24));
     const int bgrow = bg_lane_row;
     const uint32_t npix = d.num_pixels;
     uint32_t *out = reinterpret_cast<uint32_t *>(d.rgb + (size_t)env * PG_OBS_BYTES);
     for (int r0 = 0; r0 < PG_RES; r0 += RF_RB) {
-        // ---- image jobs: a cursor over the images crossing rows [r0, r0 + RF_RB) in draw order
-        int seg = 0, grp = 0; // segment = z * 2 + descriptor group (RF_DCAP = 128: two groups of 64)
+        // ---- image jobs: a cursor over the images crossing rows [r0, r0 + RF_RB) in draw order,
+        //      segments (z, descriptor group of 64) from z = zlo
+        int seg = 0, segend = 0, grp = 0;
         unsigned long long mask = 0;
         int C0 = 0, C1 = 0, C2 = 0, C3 = 0, C4 = 0, C5 = 0, C6 = 0, C7 = 0; // the current image's descriptor (uniform)
         int y = 0, yend = 0;
+        constexpr int NG = DCAP / 64;
         auto next_image = [&]() -> bool {
             while (mask == 0) {
-                if (seg >= 6) return false;
-                const int z = seg >> 1;
-                grp = (seg & 1) * 64;
+                if (seg >= segend) return false;
+                const int z = seg / NG - 1;
+                grp = (seg % NG) * 64;
                 seg++;
                 if (grp >= nd) continue;
                 const int k = grp + lane;
                 const bool live = k < nd;
                 const int4 A = desc[2 * (live ? k : 0)];
-                const int zz = (desc[2 * (live ? k : 0) + 1].z >> 17) & 3;
+                const int zz = ((desc[2 * (live ? k : 0) + 1].z >> 14) & 7) - 1;
                 const int yt1 = (A.x >> 16) & 255, yn = (A.x >> 24) & 255;
                 mask = ballot(live && zz == z && yt1 < r0 + RF_RB && yt1 + yn > r0);
             }
@@ -2396,9 +2770,15 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
             yend = min(r0 + RF_RB, yt1 + yn);
             return true;
         };
+        auto start = [&](int zlo, int zhi) { // segments of z in [zlo, zhi]
+            seg = (zlo + 1) * NG;
+            segend = (zhi + 2) * NG;
+            mask = 0;
+            return next_image();
+        };
         uint32_t jt[RF_JOBS];
         int jr[RF_JOBS], jca[RF_JOBS];
-        bool more = next_image();
+        bool more = false;
         auto issue_jobs = [&]() {
 #pragma unroll
             for (int q = 0; q < RF_JOBS; q++) {
@@ -2406,27 +2786,63 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
                 jt[q] = 0;
                 jca[q] = 256;
                 if (more) {
-                    const uint32_t exb = (uint32_t)C1, eyb = (uint32_t)C3, soff = (uint32_t)C5, fill = (uint32_t)C7;
-                    const int exs = C2, eys = C4, w2 = C6;
-                    const int xt1 = C0 & 255, xn = (C0 >> 8) & 255, yt1 = (C0 >> 16) & 255;
-                    const int sw = w2 & 0xffff;
-                    const int dxl = lane - xt1;
+                    const int w2 = C6, kind = (w2 >> 17) & 3;
+                    const int ca = (w2 >> 19) & 511;
                     uint32_t t = 0;
-                    if ((unsigned)dxl < (unsigned)xn) {
-                        if (fill != 0) {
-                            t = fill;
-                        } else {
-                            int scol = (int)((exb + (uint32_t)(dxl * exs)) >> 16);
-                            if ((w2 >> 16) & 1) scol = sw - 1 - scol;
-                            const int srow = (int)((eyb + (uint32_t)((y - yt1) * eys)) >> 16);
-                            const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
-                            if (idx < npix) t = d.pixels[idx];
-                            else err = true;
+                    if (kind == RF_PLAIN) {
+                        const uint32_t exb = (uint32_t)C1, eyb = (uint32_t)C3, soff = (uint32_t)C5, fill = (uint32_t)C7;
+                        const int exs = C2, eys = C4;
+                        const int xt1 = C0 & 255, xn = (C0 >> 8) & 255, yt1 = (C0 >> 16) & 255;
+                        const int sw = w2 & 0x1fff;
+                        const int dxl = lane - xt1;
+                        if ((unsigned)dxl < (unsigned)xn) {
+                            if (fill != 0) {
+                                t = fill;
+                            } else {
+                                int scol = (int)((exb + (uint32_t)(dxl * exs)) >> 16);
+                                if ((w2 >> 13) & 1) scol = sw - 1 - scol;
+                                const int srow = (int)((eyb + (uint32_t)((y - yt1) * eys)) >> 16);
+                                const uint32_t idx = soff + (uint32_t)(srow * sw + scol);
+                                if (idx < npix) t = d.pixels[idx];
+                                else err = true;
+                            }
                         }
+                        jca[q] = ca;
+                    } else if (has_rotation<G>() && kind == RF_ROT) {
+                        // rot_pixel at (lane, y): the trapezoid holding scan line y, its [fromX, toX)
+                        const int4 *R = rdesc + 6 * C1;
+                        const int4 a5 = R[5];
+                        const int f0 = a5.x & 255, e0 = (a5.x >> 8) & 255, f1 = (a5.x >> 16) & 255, e1 = (a5.x >> 24) & 255;
+                        const int f2 = a5.y & 255, e2 = (a5.y >> 8) & 255;
+                        const int tk = (y >= f0 && y < e0) ? 0 : ((y >= f1 && y < e1) ? 1 : ((y >= f2 && y < e2) ? 2 : 3));
+                        if (tk < 3) {
+                            const int from = tk == 0 ? f0 : (tk == 1 ? f1 : f2);
+                            const int4 e = R[tk], a3 = R[3], a4 = R[4];
+                            const int xlv = e.x + (y - from) * e.y, xrv = e.z + (y - from) * e.w;
+                            const int fromX = max(xlv >> 16, 0), toX = min(xrv >> 16, PG_RES);
+                            if (lane >= fromX && lane < toX) {
+                                const int iw = a4.w & 0xffff, ih = a4.w >> 16;
+                                int uu = (lane * a3.x + y * a3.z + a4.x) >> 16;
+                                int vv = (lane * a3.y + y * a3.w + a4.y) >> 16;
+                                uu = min(max(uu, 0), iw - 1);
+                                vv = min(max(vv, 0), ih - 1);
+                                if ((a5.y >> 16) & 1) uu = iw - 1 - uu;
+                                const uint32_t idx = (uint32_t)a4.z + (uint32_t)(vv * iw + uu);
+                                if (idx < npix) t = d.pixels[idx];
+                                else err = true;
+                            }
+                        }
+                        jca[q] = a5.z & 0xffff;
+                    } else if (G == PG_GAME_JUMPER && kind == RF_ROWS) {
+                        const int sy = y - C3, bit = lane - C2;
+                        if (sy >= 0 && sy < PG_RES && bit >= 0 && bit < 64) {
+                            const uint32_t w = d.pixels[(uint32_t)C1 + 2 * sy + (bit >> 5)];
+                            if ((w >> (bit & 31)) & 1) t = (uint32_t)C7;
+                        }
+                        jca[q] = 256;
                     }
                     jt[q] = t;
                     jr[q] = y - r0;
-                    jca[q] = (w2 >> 20) & 511;
                     if (++y >= yend) more = next_image();
                 }
             }
@@ -2444,20 +2860,43 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         uint32_t px[RF_RB], t00[RF_RB], t01[RF_RB], t10[RF_RB], t11[RF_RB];
 #pragma unroll
         for (int k = 0; k < RF_RB; k++) {
-            const int info = readlane(rinfo, r0 + k), br = readlane(bgrow, r0 + k);
-            const int nr = info >> 24;
+            const int br = readlane(bgrow, r0 + k);
             const bool inb = bg_col && br >= 0;
             const uint32_t bv = bgpix[inb ? bg_col_base + (uint32_t)br : 0u];
             px[k] = inb ? bv : 0xff000000u;
-            const int c0 = codes[((info >> 14) & 31) * 64 + lane];
-            const int c1 = nr > 1 ? codes[((info >> 19) & 31) * 64 + lane] : 0xffff;
-            const int sr0 = (info & 127) * TP, sr1 = ((info >> 7) & 127) * TP;
             t00[k] = t01[k] = t10[k] = t11[k] = 0;
-            if (nr > 0 && (c0 & 255) != 255) t00[k] = d.pixels[(uint32_t)tile_off[c0 & 255] + (uint32_t)(sr0 + scol0)];
-            if (nr > 1 && (c1 & 255) != 255) t01[k] = d.pixels[(uint32_t)tile_off[c1 & 255] + (uint32_t)(sr1 + scol0)];
-            if (nr > 0 && (c0 >> 8) != 255) t10[k] = d.pixels[(uint32_t)tile_off[c0 >> 8] + (uint32_t)(sr0 + scol1)];
-            if (nr > 1 && (c1 >> 8) != 255) t11[k] = d.pixels[(uint32_t)tile_off[c1 >> 8] + (uint32_t)(sr1 + scol1)];
+            if constexpr (FAST) {
+                const int info = readlane(rinfo, r0 + k);
+                const int nr = info >> 24;
+                const int c0 = codes[((info >> 14) & 31) * 64 + lane];
+                const int c1 = nr > 1 ? codes[((info >> 19) & 31) * 64 + lane] : 0xffff;
+                const int sr0 = (info & 127) * TP, sr1 = ((info >> 7) & 127) * TP;
+                if (nr > 0 && (c0 & 255) != 255) t00[k] = d.pixels[(uint32_t)tile_off[c0 & 255] + (uint32_t)(sr0 + scol0)];
+                if (nr > 1 && (c1 & 255) != 255) t01[k] = d.pixels[(uint32_t)tile_off[c1 & 255] + (uint32_t)(sr1 + scol0)];
+                if (nr > 0 && (c0 >> 8) != 255) t10[k] = d.pixels[(uint32_t)tile_off[c0 >> 8] + (uint32_t)(sr0 + scol1)];
+                if (nr > 1 && (c1 >> 8) != 255) t11[k] = d.pixels[(uint32_t)tile_off[c1 >> 8] + (uint32_t)(sr1 + scol1)];
+            } else if constexpr (GEN) {
+                if (tiles) {
+                    const int info = readlane(rinfo, r0 + k);
+                    const int ny = info >> 16, y0 = info & 255, y1 = (info >> 8) & 255;
+                    int ysr[GEN_K];
+#pragma unroll
+                    for (int q = 0; q < GEN_K; q++) ysr[q] = readlane(gn.ys[q], r0 + k);
+                    if (ny > 0 && gn.ncx > 0) t00[k] = rf_gen_texel(d, ti[gw[y0 * ww + gn.cx0]], gn.xs, ysr, false, false, err);
+                    if (ny > 1 && gn.ncx > 0) t01[k] = rf_gen_texel(d, ti[gw[y1 * ww + gn.cx0]], gn.xs, ysr, false, true, err);
+                    if (ny > 0 && gn.ncx > 1) t10[k] = rf_gen_texel(d, ti[gw[y0 * ww + gn.cx1]], gn.xs, ysr, true, false, err);
+                    if (ny > 1 && gn.ncx > 1) t11[k] = rf_gen_texel(d, ti[gw[y1 * ww + gn.cx1]], gn.xs, ysr, true, true, err);
+                }
+            }
         }
+        if constexpr (has_z_minus1<G>()) { // z = -1 entities go between the background and the tiles (:933)
+            more = start(-1, -1);
+            while (more) {
+                issue_jobs();
+                blend_jobs(px);
+            }
+        }
+        more = start(0, 3);
         issue_jobs(); // the first round of image texels rides on the same memory round trip
         uint32_t part = 0;
 #pragma unroll
