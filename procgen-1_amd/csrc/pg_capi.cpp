@@ -33,6 +33,8 @@ void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count
 void pg_launch_reset(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode, int grid,
                      int act, int slot);
 void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode, int slot);
+int pg_launch_fused(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int use_hash, uint64_t seed,
+                    int32_t t, int parity, int slot);
 int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames, uint8_t *rgb,
                            hipStream_t s);
 int pg_launch_assetgen_sprites(int game, uint32_t seed0, uint32_t *d_out, int types, hipStream_t s);
@@ -318,6 +320,7 @@ struct VecEnv {
     bool buffers_set = false;
     bool atlas = false;
     bool gen_assets = false; // use_generated_assets: AssetGen sprites + per-env procedural backgrounds
+    bool fused = false;      // step + render in one launch where the register-frame render serves the game (pg_fused.hip)
     int parity = 0;          // alternates per act: which slow-env list the step launches write
     bool started = false;
     // device allocations
@@ -472,6 +475,34 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
 // games that render with the register-frame kernel by default (pg_render.hip pg_render_rf_kernel)
 #define RF_DEFAULT (1 << PG_GAME_COINRUN)
 
+// The games whose frames the register-frame render draws (PGDev::render_rf): it serves centred,
+// non-monochrome, atlas-asset frames (pg_render.hip rf_game).  PROCGEN_MI355X_RENDER_RF=0 keeps every
+// game on the LDS-frame kernel; "all" or a comma list of game names picks the games (default:
+// RF_DEFAULT, the games where it measured faster).
+static int rf_mask(bool center_agent, bool monochrome, bool generated) {
+    if (monochrome || generated) return 0;
+    // without center_agent the window is the whole world: 64 tiles wide for the games that honour the
+    // option, too wide for the register-frame tables (the others override it and have small worlds)
+    const int centred_games = (1 << PG_GAME_COINRUN) | (1 << PG_GAME_CLIMBER) | (1 << PG_GAME_NINJA) |
+                              (1 << PG_GAME_JUMPER) | (1 << PG_GAME_CAVEFLYER) | (1 << PG_GAME_FRUITBOT);
+    const int keep = center_agent ? ~0 : ~centred_games;
+    const char *rf = getenv("PROCGEN_MI355X_RENDER_RF");
+    if (!rf) return RF_DEFAULT & keep;
+    if (rf[0] == '0') return 0;
+    if (!strcmp(rf, "all")) return ((1 << PG_NUM_GAMES) - 1) & keep;
+    int mask = 0;
+    std::string list(rf);
+    size_t p0 = 0;
+    while (p0 <= list.size()) {
+        const size_t p1 = std::min(list.find(',', p0), list.size());
+        const std::string name = list.substr(p0, p1 - p0);
+        for (int g = 0; g < PG_NUM_GAMES; g++)
+            if (name == pg_game_name(g)) mask |= 1 << g;
+        p0 = p1 + 1;
+    }
+    return mask & keep;
+}
+
 int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     if (!v->atlas) return fail(v, PG_ERR_NO_ATLAS, "procgen_upload_atlas was not called");
     HIPCHECK(hipSetDevice(v->device));
@@ -521,7 +552,10 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         if (host_serial && k == 0) HIPCHECK(hipStreamWaitEvent(s, v->ev_rendered[1], 0)); // enqueued last
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 0], s));
         PG_POISON(s);
-        pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
+        // fused: step + render of the envs that did not finish in one launch (pg_fused.hip)
+        const bool fz = v->fused && ((v->dev.render_rf >> game) & 1) &&
+                        pg_launch_fused(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot) == 0;
+        if (!fz) pg_launch_step(&v->dev, game, list, cnt, s, use_hash, seed, t, v->parity, slot);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 1], s));
         if (split) {
             HIPCHECK(hipEventRecord(v->ev_stepped[k], s));
@@ -559,7 +593,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         PG_POISON(s);
         if (split) {
             HIPCHECK(hipEventRecord(v->ev_reset[k], r));
-            pg_launch_render(&v->dev, game, list, cnt, s, 1, slot);
+            if (!fz) pg_launch_render(&v->dev, game, list, cnt, s, 1, slot);
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s));
             HIPCHECK(hipStreamWaitEvent(s, v->ev_reset[k], 0));
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
@@ -567,7 +601,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         } else {
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 4], s)); // unused without the split
             if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 5], s));
-            pg_launch_render(&v->dev, game, list, cnt, s, 0, slot);
+            pg_launch_render(&v->dev, game, list, cnt, s, fz ? 2 : 0, slot); // fused: only the reset envs remain
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
         if (v->obs_early && split) HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
@@ -939,17 +973,27 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         // dodgeball, and a loss where the level prefetch adds a fifth stream over the 4 hardware
         // queues (caveflyer -13 %, jumper -23 %): profiles/r03/o_parts_games.
         const char *pp = getenv("PROCGEN_MI355X_PARTS"), *pf = getenv("PROCGEN_MI355X_PREFETCH");
-        const bool dflt = gids.size() == 1 && gids[0] == PG_GAME_COINRUN && !(pf && pf[0] == '1');
+        // with the register-frame render (round 5) coinrun is faster in one chain: 37.75 vs 36.65 M
+        // (2 parts), 35.17 vs 34.18 M on a second box (profiles/r05/)
+        const bool rf_cr = (rf_mask(center_agent, use_monochrome_assets, use_generated_assets) >> PG_GAME_COINRUN) & 1;
+        const bool dflt = gids.size() == 1 && gids[0] == PG_GAME_COINRUN && !(pf && pf[0] == '1') && !rf_cr;
         const int want = pp ? std::min(std::max(atoi(pp), 1), 8) : (dflt ? 2 : 1);
         v->parts = gids.size() == 1 && num_envs >= want * 64 ? want : 1;
     }
     const size_t nchains = gids.size() > 1 ? gids.size() : (size_t)v->parts;
     { // the reset's side stream (single game only: mixed batches keep each game's chain on one stream)
+        // PROCGEN_MI355X_RESET_PRIO=1: at the highest stream priority, so the dispatcher places the
+        // level generators' workgroups before the concurrent render's (the render of the reset envs
+        // waits for them)
+        const char *rp = getenv("PROCGEN_MI355X_RESET_PRIO");
+        int rlo = 0, rhi = 0;
+        const bool rprio = rp && rp[0] == '1' && hipDeviceGetStreamPriorityRange(&rlo, &rhi) == hipSuccess;
         bool ok = true;
         for (size_t k = 0; k < nchains && ok; k++) {
             hipStream_t s = nullptr;
             hipEvent_t a = nullptr, b = nullptr;
-            ok = (gids.size() > 1 || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) &&
+            ok = (gids.size() > 1 || (rprio ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, rhi)
+                                            : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) == hipSuccess) &&
                  hipEventCreateWithFlags(&a, hipEventDisableTiming) == hipSuccess &&
                  hipEventCreateWithFlags(&b, hipEventDisableTiming) == hipSuccess;
             hipEvent_t c = nullptr;
@@ -1179,26 +1223,9 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     {
         // the register-frame render (pg_render_rf_kernel) for the games and options it serves;
         // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel
-        // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel; "all" or a comma list of
-        // game names picks the games (default: the games where it measured faster, RF_DEFAULT)
-        const char *rf = getenv("PROCGEN_MI355X_RENDER_RF");
-        int mask = RF_DEFAULT;
-        if (rf && rf[0] == '0') mask = 0;
-        else if (rf && !strcmp(rf, "all")) mask = (1 << PG_NUM_GAMES) - 1;
-        else if (rf && rf[0]) {
-            mask = 0;
-            std::string list(rf);
-            size_t p0 = 0;
-            while (p0 <= list.size()) {
-                const size_t p1 = std::min(list.find(',', p0), list.size());
-                const std::string name = list.substr(p0, p1 - p0);
-                for (int g = 0; g < PG_NUM_GAMES; g++)
-                    if (name == pg_game_name(g)) mask |= 1 << g;
-                p0 = p1 + 1;
-            }
-        }
-        const bool on = center_agent && !use_monochrome_assets && !use_generated_assets;
-        d.render_rf = on ? mask : 0;
+        d.render_rf = rf_mask(center_agent, use_monochrome_assets, use_generated_assets);
+        const char *fz = getenv("PROCGEN_MI355X_FUSED"); // 1: fuse step and render (pg_fused.hip)
+        v->fused = fz && fz[0] == '1';
     }
     {
         const char *sp = getenv("PROCGEN_MI355X_SLOW_PREDICT");
@@ -1804,7 +1831,7 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     size_t plane = (size_t)v->num_envs * PG_CAP;
     // a restored env draws with the options its state carries: the register-frame render serves
     // centred, non-monochrome frames only (pg_render.hip rf_game), so its game falls back otherwise
-    if (!s.opt_center_agent || s.opt_use_monochrome_assets) v->dev.render_rf &= ~(1 << s.game_id);
+    if (s.opt_use_monochrome_assets || (!s.opt_center_agent && s.main_width > 63)) v->dev.render_rf &= ~(1 << s.game_id);
     s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
     copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     const char *ent_base = p; // the live entity planes

@@ -2134,7 +2134,9 @@ __host__ __device__ constexpr bool rf_game() {
     return G == PG_GAME_COINRUN || G == PG_GAME_BIGFISH || G == PG_GAME_MAZE || G == PG_GAME_HEIST || G == PG_GAME_MINER ||
            G == PG_GAME_CLIMBER || G == PG_GAME_CHASER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER ||
            G == PG_GAME_PLUNDER || G == PG_GAME_STARPILOT || G == PG_GAME_LEAPER || G == PG_GAME_DODGEBALL ||
-           G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT || G == PG_GAME_BOSSFIGHT;
+           G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT;
+    // bossfight: its frames hold more rotated trail images than the descriptor LDS takes (the
+    // LDS-frame kernel stamps them)
 }
 // visible image descriptors per frame (tile_image entities become one per tile), Qt transform-blit
 // descriptors (96 B each, rot_stage)
@@ -2312,38 +2314,30 @@ DEV uint32_t rf_gen_texel(const PGDev &d, const int2 t, const int (&xs)[GEN_K], 
     return gen_texel(d, t, sc, sr, err);
 }
 
+// LDS of the register-frame render: FAST: tile_off[NTYPES] | codes[CR][64] (grid value of the first |
+// second covering tile column per window tile row and lane, 255: nothing); GEN: typeinfo ti[65] |
+// window slots gw[GEN_GW]; then the image descriptors (2 int4 each) and the transform-blit descriptors
 template <int G>
-__global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
-    if constexpr (!rf_game<G>()) {
-        return;
-    } else {
-    const PGDev d = game_view(dg, G);
+DEV constexpr int rf_tab_bytes() {
+    return always_uniform<G>() ? NTYPES * 4 + crows<G>() * 64 * 2 : (has_general<G>() ? GEN_TI_BYTES + GEN_GW : 16);
+}
+template <int G>
+DEV constexpr int rf_lds_bytes() { return rf_tab_bytes<G>() + 32 * rf_dcap<G>() + 96 * rf_rcap<G>(); }
+
+// One env's frame (d: the game's view, game_view).  tab / desc / rdesc: LDS of rf_tab_bytes,
+// 2 * rf_dcap and 6 * rf_rcap int4, 16-B aligned; the caller's wave owns them for the call.
+template <int G>
+DEV void rf_render_env(const PGDev &d, int env, uint8_t *tab, int4 *desc, int4 *rdesc) {
     constexpr bool FAST = always_uniform<G>();             // square tile_px() tiles: grid value tables
     constexpr bool GEN = has_general<G>();                 // the general tile pass
     constexpr int CR = crows<G>();
     constexpr int TP = tile_px<G>();
     constexpr int DCAP = rf_dcap<G>(), RCAP = rf_rcap<G>();
-    constexpr int TAB_BYTES = FAST ? NTYPES * 4 + CR * 64 * 2 : (GEN ? GEN_TI_BYTES + GEN_GW : 16);
-    // FAST: tile_off[NTYPES] | codes[CR][64] (grid value of the first | second covering tile column per
-    // window tile row and lane, 255: nothing); GEN: typeinfo ti[65] | window slots gw[GEN_GW]
-    __shared__ __attribute__((aligned(16))) uint8_t tab[TAB_BYTES];
-    __shared__ __attribute__((aligned(16))) int4 desc[2 * DCAP];
-    __shared__ __attribute__((aligned(16))) int4 rdesc[6 * RCAP];
     int *const tile_off = reinterpret_cast<int *>(tab);
     uint16_t *const codes = reinterpret_cast<uint16_t *>(tab + NTYPES * 4);
     int2 *const ti = reinterpret_cast<int2 *>(tab);
     uint8_t *const gw = tab + GEN_TI_BYTES;
     const int lane = LANE;
-    const int bidx = (int)blockIdx.x;
-    int env;
-    if (mode == 2) {
-        if (bidx >= d.reset_count[slot]) return;
-        env = d.reset_queue[(size_t)slot * d.num_envs + bidx];
-    } else {
-        if (bidx >= count) return;
-        env = env_list ? env_list[bidx] : bidx;
-        if (mode == 1 && d.done8[env]) return;
-    }
     const PGEnv s = d.envs[env];
     const int16_t *Gd = d.grid + (size_t)env * PG_GRID_MAX;
     bool err = false;
@@ -2364,12 +2358,20 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         }
         tile_off[lane] = off;
     }
-    // ---- visible tile window (basic-abstract-game.cpp:937-948): centred views only (host selection)
-    const double margin = (double)v.visibility / 2.0 + 1;
-    const int low_x = (int)((double)v.center_x - margin), high_x = (int)((double)v.center_x + margin);
-    const int low_y = (int)((double)v.center_y - margin), high_y = (int)((double)v.center_y + margin);
+    // ---- visible tile window (basic-abstract-game.cpp:937-948): the host selects the frames whose
+    //      window fits 63 x 63 tiles (centred views; uncentered ones of worlds below 64 tiles)
+    int low_x, high_x, low_y, high_y;
+    if (s.opt_center_agent) {
+        const double margin = (double)v.visibility / 2.0 + 1;
+        low_x = (int)((double)v.center_x - margin);
+        high_x = (int)((double)v.center_x + margin);
+        low_y = (int)((double)v.center_y - margin);
+        high_y = (int)((double)v.center_y + margin);
+    } else {
+        low_x = 0; high_x = s.main_width - 1; low_y = 0; high_y = s.main_height - 1;
+    }
     const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
-    if (!s.opt_center_agent || s.opt_use_monochrome_assets || d.gen_bg || ww > 63 || wh > 63) err = true;
+    if (s.opt_use_monochrome_assets || d.gen_bg || ww > 63 || wh > 63) err = true;
     // ---- Qt blit setup of window tile column `lane`, window tile row `lane`, the background (lane 63)
     int4 bgi = make_int4(0, 0, 0, 0);
     double bg_rx = 0, bg_ry = 0, bg_rw = 0, bg_rh = 0;
@@ -2871,6 +2873,9 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
                 const int c0 = codes[((info >> 14) & 31) * 64 + lane];
                 const int c1 = nr > 1 ? codes[((info >> 19) & 31) * 64 + lane] : 0xffff;
                 const int sr0 = (info & 127) * TP, sr1 = ((info >> 7) & 127) * TP;
+#ifdef RF_DIAG_NOCOL // diagnostic only (wrong frames): every lane of a tile reads its first column
+                scol0 = scol1 = 0;
+#endif
                 if (nr > 0 && (c0 & 255) != 255) t00[k] = d.pixels[(uint32_t)tile_off[c0 & 255] + (uint32_t)(sr0 + scol0)];
                 if (nr > 1 && (c1 & 255) != 255) t01[k] = d.pixels[(uint32_t)tile_off[c1 & 255] + (uint32_t)(sr1 + scol0)];
                 if (nr > 0 && (c0 >> 8) != 255) t10[k] = d.pixels[(uint32_t)tile_off[c0 >> 8] + (uint32_t)(sr0 + scol1)];
@@ -2921,19 +2926,37 @@ __global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int
         }
         // ---- bgr32_to_rgb888 (game.cpp:8-23): dword w of a row's 192 bytes takes bytes of pixels
         //      4w / 3 and 4w / 3 + 1 (phase w % 3); lanes 0..47 store one dword each
+        // v_perm_b32 picks the four bytes of {b, a} (a = bytes 0-3: B G R A of pixel 4w / 3):
+        // phase 0 -> R_a G_a B_a R_b, 1 -> G_a B_a R_b G_b, 2 -> B_a R_b G_b B_b
         const int p1 = (4 * lane) / 3, ph = lane % 3;
+        const uint32_t sel = ph == 0 ? 0x06000102u : (ph == 1 ? 0x05060001u : 0x04050600u);
 #pragma unroll
         for (int k = 0; k < RF_RB; k++) {
             const uint32_t a = (uint32_t)__shfl((int)px[k], p1 & 63), b = (uint32_t)__shfl((int)px[k], (p1 + 1) & 63);
-            const uint32_t ra = (a >> 16) & 255, ga = (a >> 8) & 255, ba = a & 255;
-            const uint32_t rb = (b >> 16) & 255, gb = (b >> 8) & 255, bb2 = b & 255;
-            const uint32_t wv = ph == 0 ? (ra | (ga << 8) | (ba << 16) | (rb << 24))
-                              : ph == 1 ? (ga | (ba << 8) | (rb << 16) | (gb << 24))
-                                        : (ba | (rb << 8) | (gb << 16) | (bb2 << 24));
-            if (lane < 48) out[(r0 + k) * 48 + lane] = wv;
+            if (lane < 48) out[(r0 + k) * 48 + lane] = __builtin_amdgcn_perm(b, a, sel);
         }
     }
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
+}
+
+template <int G>
+__global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
+    if constexpr (rf_game<G>()) {
+        const PGDev d = game_view(dg, G);
+        __shared__ __attribute__((aligned(16))) uint8_t tab[rf_tab_bytes<G>()];
+        __shared__ __attribute__((aligned(16))) int4 desc[2 * rf_dcap<G>()];
+        __shared__ __attribute__((aligned(16))) int4 rdesc[6 * rf_rcap<G>()];
+        const int bidx = (int)blockIdx.x;
+        int env;
+        if (mode == 2) {
+            if (bidx >= d.reset_count[slot]) return;
+            env = d.reset_queue[(size_t)slot * d.num_envs + bidx];
+        } else {
+            if (bidx >= count) return;
+            env = env_list ? env_list[bidx] : bidx;
+            if (mode == 1 && d.done8[env]) return;
+        }
+        rf_render_env<G>(d, env, tab, desc, rdesc);
     }
 }
 
@@ -4610,6 +4633,7 @@ __global__ __launch_bounds__(HR_THREADS) void pg_render_hires_kernel(PGDev dg, c
     if (!ok && threadIdx.x == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
 }
 
+#ifndef PG_FUSED_TU // pg_fused.hip includes this file for rf_render_env
 // mode: see pg_render_kernel (0 all, 1 envs not done, 2 the reset queue: `count` bounds its length)
 extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s, int mode,
                                  int slot) {
@@ -4684,3 +4708,4 @@ extern "C" int pg_launch_render_hires(const PGDev *d, int game, const int32_t *e
     default: return -1;
     }
 }
+#endif // PG_FUSED_TU

@@ -2871,7 +2871,7 @@ struct StepLds {
 // (pg_render)
 template <int G>
 DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint64_t hash_seed, int32_t hash_t,
-                  int slot) {
+                  int slot, bool *done_out = nullptr) {
     uint32_t *lds_mt = L.mt;
     int16_t *lds_list = L.list, *lds_slist = L.slist;
     float4 *lds_ibox = L.ibox;
@@ -2990,6 +2990,7 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 #endif
     c.cs.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
+    if (done_out) *done_out = done;
     return predicted && !done;
 }
 
@@ -3046,6 +3047,7 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
 
 } // namespace
 
+#ifndef PG_FUSED_TU // pg_fused.hip includes this file for step_env
 // parity: alternates per act (the host zeroes this parity's slow-list length and the reset counts)
 extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
                                int use_hash, uint64_t seed, int32_t t, int parity, int slot) {
@@ -3110,3 +3112,4 @@ extern "C" int procgen_selftest_libm(int which, const float *d_in, void *d_out, 
     hipLaunchKernelGGL(pg_selftest_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, which, d_in, d_out, n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif // PG_FUSED_TU

@@ -12,7 +12,7 @@ from test_gpu_games import GAMES, LATENT, run_pair
 
 pytestmark = pytest.mark.gpu
 
-ALL = GAMES + ["coinrun"]
+ALL = [g for g in GAMES + ["coinrun"] if g != "bossfight"]  # bossfight stays on the LDS-frame kernel (rf_game)
 
 
 @pytest.fixture
@@ -33,7 +33,7 @@ def test_rf_parity_easy_options(game, rf):
     run_pair(game, 16, 150, seed=42, num_levels=20, start_level=3, rand_seed=5, latent=game in LATENT, **kw)
 
 
-@pytest.mark.parametrize("game", ["jumper", "bossfight", "fruitbot", "starpilot"])
+@pytest.mark.parametrize("game", ["jumper", "fruitbot", "starpilot", "plunder"])
 def test_rf_parity_long(game, rf):
     """Many rotated / tiled images and the compass over long episodes."""
     run_pair(game, 12, 600, seed=43, num_levels=0, rand_seed=9)
