@@ -339,6 +339,7 @@ struct VecEnv {
     // page-locked in place with hipHostRegister and written by DMA directly (no staging copy)
     std::vector<void *> registered;
     bool direct = false;
+    void *hr_host = nullptr; // the caller's info["rgb"] plane, page-locked when contiguous (render_mode="rgb_array")
     // libenv_act with direct buffers: each part's obs DMA is enqueued on its chain's stream right after
     // its render (vecgame.cpp:426-444: the reference's stepping threads also write the caller's obs
     // buffers before observe), so part 0's copy runs while part 1 still renders; copy_out then only
@@ -472,8 +473,11 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
     return s;
 }
 
-// games that render with the register-frame kernel by default (pg_render.hip pg_render_rf_kernel)
-#define RF_DEFAULT (1 << PG_GAME_COINRUN)
+// games that render with the register-frame kernel by default (pg_render.hip pg_render_rf_kernel):
+// where it measured faster at 65,536 envs (profiles/r05/r05_c_rf_games.txt: bigfish 58.6 -> 73.2 M,
+// climber 27.7 -> 30.5, ninja 24.2 -> 26.8); coinrun ties or loses with it (36.8 vs 35.2 M, one
+// chain against two parts), the games with level generators or transform blits lose 15-45 %
+#define RF_DEFAULT ((1 << PG_GAME_BIGFISH) | (1 << PG_GAME_CLIMBER) | (1 << PG_GAME_NINJA))
 
 // The games whose frames the register-frame render draws (PGDev::render_rf): it serves centred,
 // non-monochrome, atlas-asset frames (pg_render.hip rf_game).  PROCGEN_MI355X_RENDER_RF=0 keeps every
@@ -668,12 +672,19 @@ static void unregister_buffers(VecEnv *v) {
     for (void *p : v->registered) (void)hipHostUnregister(p);
     v->registered.clear();
     v->direct = false;
+    if (v->hr_host) (void)hipHostUnregister(v->hr_host);
+    v->hr_host = nullptr;
 }
 
 // libenv_set_buffers: page-lock the caller's planes when every one is a contiguous array
 static void register_buffers(VecEnv *v) {
     unregister_buffers(v);
     const size_t n = (size_t)v->num_envs;
+    if (v->render_human) { // info["rgb"]: 786 KB per env, DMA'd straight into the caller's array
+        void *p = contiguous(&v->info_ptrs[v->hr_info * n], n, (size_t)512 * 512 * 3);
+        if (p && hipHostRegister(p, (size_t)512 * 512 * 3 * n, hipHostRegisterDefault) == hipSuccess) v->hr_host = p;
+        else (void)hipGetLastError();
+    }
     void *planes[6] = {contiguous(&v->ob_ptrs[0], n, PG_OBS_BYTES), v->rew_host, v->first_host,
                        contiguous(&v->info_ptrs[0], n, 4), contiguous(&v->info_ptrs[n], n, 1),
                        contiguous(&v->info_ptrs[2 * n], n, 4)};
@@ -751,12 +762,25 @@ int copy_latent(VecEnv *v) {
                                        v->hr_rgb + k * cnt * per * 3, v->stream) != 0)
                 return fail(v, PG_ERR_BAD_OPTION, "render_mode=rgb_array: game not built");
         HIPCHECK(hipGetLastError());
-        std::vector<uint8_t> host(cnt * per * 3);
-        for (size_t k = 0; k < v->games.size(); k++) {
-            HIPCHECK(copy_sync(v, host.data(), v->hr_rgb + k * cnt * per * 3, host.size(), hipMemcpyDeviceToHost));
-            for (size_t q = 0; q < cnt; q++) {
-                const size_t e = v->games.size() > 1 ? (size_t)v->h_lists[k * cnt + q] : q; // list_of(k) order
-                memcpy(v->info_ptrs[v->hr_info * n + e], host.data() + q * per * 3, per * 3);
+        if (v->hr_host) { // DMA into the page-locked caller array, each env's frame to its own slot
+            uint8_t *dst = (uint8_t *)v->hr_host;
+            if (v->games.size() == 1) {
+                HIPCHECK(hipMemcpyAsync(dst, v->hr_rgb, cnt * per * 3, hipMemcpyDeviceToHost, v->stream));
+            } else {
+                for (size_t k = 0; k < v->games.size(); k++)
+                    for (size_t q = 0; q < cnt; q++)
+                        HIPCHECK(hipMemcpyAsync(dst + (size_t)v->h_lists[k * cnt + q] * per * 3,
+                                                v->hr_rgb + (k * cnt + q) * per * 3, per * 3, hipMemcpyDeviceToHost, v->stream));
+            }
+            HIPCHECK(hipStreamSynchronize(v->stream));
+        } else {
+            std::vector<uint8_t> host(cnt * per * 3);
+            for (size_t k = 0; k < v->games.size(); k++) {
+                HIPCHECK(copy_sync(v, host.data(), v->hr_rgb + k * cnt * per * 3, host.size(), hipMemcpyDeviceToHost));
+                for (size_t q = 0; q < cnt; q++) {
+                    const size_t e = v->games.size() > 1 ? (size_t)v->h_lists[k * cnt + q] : q; // list_of(k) order
+                    memcpy(v->info_ptrs[v->hr_info * n + e], host.data() + q * per * 3, per * 3);
+                }
             }
         }
     }
@@ -973,8 +997,8 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         // dodgeball, and a loss where the level prefetch adds a fifth stream over the 4 hardware
         // queues (caveflyer -13 %, jumper -23 %): profiles/r03/o_parts_games.
         const char *pp = getenv("PROCGEN_MI355X_PARTS"), *pf = getenv("PROCGEN_MI355X_PREFETCH");
-        // with the register-frame render (round 5) coinrun is faster in one chain: 37.75 vs 36.65 M
-        // (2 parts), 35.17 vs 34.18 M on a second box (profiles/r05/)
+        // coinrun with the register-frame render (PROCGEN_MI355X_RENDER_RF=coinrun) runs in one chain:
+        // two parts measured 36.65 / 34.18 M against 37.75 / 35.17 M in one (two boxes, profiles/r05/)
         const bool rf_cr = (rf_mask(center_agent, use_monochrome_assets, use_generated_assets) >> PG_GAME_COINRUN) & 1;
         const bool dflt = gids.size() == 1 && gids[0] == PG_GAME_COINRUN && !(pf && pf[0] == '1') && !rf_cr;
         const int want = pp ? std::min(std::max(atoi(pp), 1), 8) : (dflt ? 2 : 1);
