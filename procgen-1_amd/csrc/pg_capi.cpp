@@ -474,10 +474,11 @@ libenv_tensortype make_type(const char *name, libenv_dtype dt, std::vector<int> 
 }
 
 // games that render with the register-frame kernel by default (pg_render.hip pg_render_rf_kernel):
-// where it measured faster at 65,536 envs (profiles/r05/r05_c_rf_games.txt: bigfish 58.6 -> 73.2 M,
-// climber 27.7 -> 30.5, ninja 24.2 -> 26.8); coinrun ties or loses with it (36.8 vs 35.2 M, one
-// chain against two parts), the games with level generators or transform blits lose 15-45 %
-#define RF_DEFAULT ((1 << PG_GAME_BIGFISH) | (1 << PG_GAME_CLIMBER) | (1 << PG_GAME_NINJA))
+// where it measured faster at 65,536 envs (profiles/r05/r05_h_rf_games.txt, 4 rows per batch, no spills:
+// bigfish 58.7 -> 69.1 M, climber 27.7 -> 39.8, ninja 24.2 -> 34.7, miner 25.6 -> 30.7, maze 33.2 -> 33.8,
+// chaser 29.0 -> 29.2); coinrun ties (36.8 vs 36.7 M)
+#define RF_DEFAULT ((1 << PG_GAME_BIGFISH) | (1 << PG_GAME_CLIMBER) | (1 << PG_GAME_NINJA) | (1 << PG_GAME_MINER) | \
+                    (1 << PG_GAME_MAZE) | (1 << PG_GAME_CHASER))
 
 // The games whose frames the register-frame render draws (PGDev::render_rf): it serves centred,
 // non-monochrome, atlas-asset frames (pg_render.hip rf_game).  PROCGEN_MI355X_RENDER_RF=0 keeps every

@@ -104,6 +104,10 @@ DEV constexpr int crows() { return (G == PG_GAME_COINRUN || G == PG_GAME_HEIST) 
 #ifndef BB
 #define BB 1
 #endif
+// runs of consecutive tile_image entities are stamped as one tile list (stamp_tile_run); 0: per entity
+#ifndef RUN_TILES
+#define RUN_TILES 1
+#endif
 
 
 // ------------------------------------------------------------------ per-game render hooks
@@ -761,6 +765,73 @@ DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img
     }
 }
 
+// inclusive prefix sum over the wave's lanes
+DEV int wave_incl_scan(int v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(v, off);
+        if (LANE >= off) v += t;
+    }
+    return v;
+}
+
+DEV double shfl_d(double x, int j) {
+    long long b = __builtin_bit_cast(long long, x);
+    int lo = __shfl((int)(b & 0xffffffff), j), hi = __shfl((int)(b >> 32), j);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+// A run of consecutive tile_image entities (`run`: their lanes in `im`, ascending; fruitbot's walls):
+// their tiles, in entity order then tile order, become one plain-image list -- 64 tiles per
+// stamp_images call whatever wall they belong to, so a frame's walls share gather rounds instead of
+// taking at least one each.  Per wall the tiles that can reach the frame (stamp_tiles' culling); lane
+// = tile, its wall found by a walk over the run's tile-count prefix, its parameters read across lanes.
+template <int EGN>
+DEV void stamp_tile_run(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long run, bool &err) {
+    const int lane = LANE;
+    // per wall (lane = entity of the run): the first tile that can reach the frame and the tile count
+    int tlo = 0, cnt = 0;
+    if ((run >> lane) & 1) {
+        const double tsz = im.rslot ? (double)im.th : (double)im.tw, org = im.rslot ? im.ry : im.rx;
+        int thi = im.ntile;
+        if (tsz > 0) {
+            tlo = max(0, (int)floor((-2.0 - org) / tsz) - 1);
+            thi = min(im.ntile, (int)ceil((PG_RES + 2.0 - org) / tsz) + 1);
+        }
+        cnt = max(thi - tlo, 0);
+    }
+    const int incl = wave_incl_scan(cnt), total = readlane(incl, 63);
+    for (int t0 = 0; t0 < total; t0 += 64) {
+        const int g = t0 + lane;
+        // the wall holding tile g: the first lane of the run whose inclusive prefix exceeds g
+        int lo = 0, hi = 63;
+#pragma unroll
+        for (int it = 0; it < 6; it++) {
+            const int mid = (lo + hi) >> 1;
+            if (__shfl(incl, mid) > g) hi = mid;
+            else lo = mid + 1;
+        }
+        const int j = lo;
+        const int k = g - (__shfl(incl, j) - __shfl(cnt, j)) + __shfl(tlo, j); // tile index in wall j
+        const double rx = shfl_d(im.rx, j), ry = shfl_d(im.ry, j);
+        const float tw = __builtin_bit_cast(float, __shfl(__builtin_bit_cast(int, im.tw), j));
+        const float th = __builtin_bit_cast(float, __shfl(__builtin_bit_cast(int, im.th), j));
+        const int vert = __shfl(im.rslot, j), offj = __shfl(im.soff, j), swj = __shfl(im.sw, j), shj = __shfl(im.sh, j);
+        const int mirj = __shfl(im.mir, j), caj = __shfl(im.ca, j);
+        Img ti;
+        img_clear(ti);
+        if (g < total) {
+            const double x = vert ? rx : rx + (double)(tw * (float)k);
+            const double y = vert ? ry + (double)(th * (float)k) : ry;
+            if (axis_setup(x, (double)tw, swj, ti.ex) && axis_setup(y, (double)th, shj, ti.ey)) {
+                ti.draw = true;
+                ti.soff = offj; ti.sw = swj; ti.sh = shj; ti.mir = mirj; ti.ca = caj;
+            }
+        }
+        stamp_images<false, EGN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
+    }
+}
+
 // One image that is not batched (a transform blit set up in order, a descriptor blit or plain blit of
 // more than 64 px, a tile list): all lanes over its footprint, at its turn.
 template <bool TILES, int EGN>
@@ -808,15 +879,6 @@ DEV void stamp_big(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &
     }
 }
 
-// inclusive prefix sum over the wave's lanes
-DEV int wave_incl_scan(int v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(v, off);
-        if (LANE >= off) v += t;
-    }
-    return v;
-}
 
 // Images of `m` in ascending lane order.  "Small" images (a plain blit or fill of <= 64 px, a
 // descriptor transform blit whose box is <= 64 px) are drawn in batches: a run of consecutive small
@@ -845,9 +907,22 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
         }
     }
     const unsigned long long smask = ballot(small);
+    // tile_image entities (plain images tiled, no transform): batched per run (stamp_tile_run)
+    const unsigned long long tmask = TILES ? ballot(((m >> lane) & 1) && im.rot == 0 && im.ntile > 0) : 0ull;
     while (m) {
         const int j0 = __ffsll((long long)m) - 1;
         if (!((smask >> j0) & 1)) {
+            if constexpr (TILES) {
+                if (((tmask >> j0) & 1) && RUN_TILES) { // a run of tile lists: their tiles batched together
+                    const unsigned long long other = m & ~tmask;
+                    const unsigned long long below = other ? ((1ull << (__ffsll((long long)other) - 1)) - 1) : ~0ull;
+                    const unsigned long long run = m & tmask & below;
+                    m &= ~run;
+                    stamp_tile_run<EGN>(fb, d, aux, im, run, err);
+                    asm volatile("" ::: "memory");
+                    continue;
+                }
+            }
             m &= m - 1;
             stamp_big<TILES, EGN>(fb, d, aux, im, j0, err);
             asm volatile("" ::: "memory");
@@ -2124,7 +2199,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 // waves resident to hide the gather latency (the render is latency-bound: +4 KB of LDS per workgroup
 // cost +19 % render time, profiles/r05/).
 #ifndef RF_RB
-#define RF_RB 8
+#define RF_RB 4 // 8 rows per batch spilled 21-50 registers (coinrun, maze) at the occupancy the kernel needs
 #endif
 #ifndef RF_JOBS
 #define RF_JOBS 8
@@ -2300,15 +2375,20 @@ DEV int rf_gen_setup(const PGDev &d, const PGEnv &s, const View &v, const int16_
 }
 
 // the texel of general-pass cell t at the class's source column / row (gen_texel with packed tables)
+// (the class selects are spelt out as a chain of conditional moves: written as a loop over the arrays,
+// the compiler kept the arrays in scratch and indexed them)
+static_assert(GEN_K == 4, "rf_gen_texel selects among 4 classes");
+DEV int rf_sel4(int cl, int a0, int a1, int a2, int a3) {
+    int v = cl == 1 ? a1 : a0;
+    v = cl == 2 ? a2 : v;
+    return cl == 3 ? a3 : v;
+}
 DEV uint32_t rf_gen_texel(const PGDev &d, const int2 t, const int (&xs)[GEN_K], const int (&ysr)[GEN_K], bool second_col,
                           bool second_row, bool &err) {
     const int kind = t.y >> 24;
     if (kind == 0) return 0u;
     const int cl = (t.y >> 16) & 255;
-    int xv = xs[0], yv = ysr[0];
-#pragma unroll
-    for (int k = 1; k < GEN_K; k++)
-        if (cl == k) { xv = xs[k]; yv = ysr[k]; }
+    const int xv = rf_sel4(cl, xs[0], xs[1], xs[2], xs[3]), yv = rf_sel4(cl, ysr[0], ysr[1], ysr[2], ysr[3]);
     const int sc = second_col ? (xv >> 16) : (int)(int16_t)(xv & 0xffff);
     const int sr = second_row ? (yv >> 16) : (int)(int16_t)(yv & 0xffff);
     return gen_texel(d, t, sc, sr, err);
@@ -2939,8 +3019,17 @@ DEV void rf_render_env(const PGDev &d, int env, uint8_t *tab, int4 *desc, int4 *
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
 }
 
+// waves per SIMD the register budget is set for (launch bound): 80 VGPRs hold coinrun's and the general
+// tile pass's batches without spills at 4 rows per batch; the transform-blit / tile-list games get 128
 template <int G>
-__global__ __launch_bounds__(64, 6) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
+__host__ __device__ constexpr int rf_waves() {
+    return G == PG_GAME_BIGFISH ? 8
+         : ((G == PG_GAME_COINRUN || G == PG_GAME_MAZE || G == PG_GAME_MINER || G == PG_GAME_CHASER || G == PG_GAME_CLIMBER ||
+             G == PG_GAME_NINJA) ? 6 : 4);
+}
+
+template <int G>
+__global__ __launch_bounds__(64, rf_waves<G>()) void pg_render_rf_kernel(PGDev dg, const int32_t *env_list, int mode, int slot, int count) {
     if constexpr (rf_game<G>()) {
         const PGDev d = game_view(dg, G);
         __shared__ __attribute__((aligned(16))) uint8_t tab[rf_tab_bytes<G>()];
@@ -4646,6 +4735,9 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
             hipLaunchKernelGGL(pg_render_kernel<G>, dim3((count + PG_RENDER_K - 1) / PG_RENDER_K), dim3(64), 0, s, *d, env_list, mode, slot, count); \
         break;
     switch (game) {
+#ifdef PG_ONLY_GAME // resource checks of one game's kernels (hipcc -DPG_ONLY_GAME=11 -Rpass-analysis=...)
+        PG_CASE(PG_ONLY_GAME)
+#else
         PG_CASE(PG_GAME_COINRUN)
         PG_CASE(PG_GAME_BIGFISH)
         PG_CASE(PG_GAME_MAZE)
@@ -4662,6 +4754,7 @@ extern "C" void pg_launch_render(const PGDev *d, int game, const int32_t *env_li
         PG_CASE(PG_GAME_NINJA)
         PG_CASE(PG_GAME_CAVEFLYER)
         PG_CASE(PG_GAME_JUMPER)
+#endif
     default: break;
     }
 #undef PG_CASE
@@ -4683,6 +4776,10 @@ extern "C" void pg_launch_poison(hipStream_t s, uint32_t pattern) {
 extern "C" int pg_launch_render_hires(const PGDev *d, int game, const int32_t *env_list, int count, uint32_t *frames,
                                       uint8_t *rgb, hipStream_t s) {
     if (count <= 0) return 0;
+#ifdef PG_ONLY_GAME
+    (void)d; (void)env_list; (void)frames; (void)rgb; (void)s;
+    return -1;
+#else
     switch (game) {
 #define PG_CASE(G)                                                                                               \
     case G:                                                                                                      \
@@ -4707,5 +4804,6 @@ extern "C" int pg_launch_render_hires(const PGDev *d, int game, const int32_t *e
 #undef PG_CASE
     default: return -1;
     }
+#endif
 }
 #endif // PG_FUSED_TU
