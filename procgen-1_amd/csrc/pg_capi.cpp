@@ -401,6 +401,10 @@ struct VecEnv {
     bool prefetch = false;
     uint32_t prefetch_games = 0; // bit g: game g's chains use the prefetch (mixed batches: only some)
     int act_no = 0, lag = 2, npstreams = 1;
+    // mixed batches, PROCGEN_MI355X_PREFETCH_INBAND=1: the spare generation of the prefetched chains runs
+    // as one more job of the 4-stream packing, on chain stream gen_si after that stream's chains
+    bool inband = false;
+    int gen_si = 0;
     hipStream_t pstreams[2] = {nullptr, nullptr};
     hipEvent_t ev_pre[PG_SP_LAG_MAX] = {};
     bool ev_pre_set[PG_SP_LAG_MAX] = {};
@@ -539,6 +543,7 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     std::vector<char> seen(v->gstreams.size() + 1, 0); // streams that already waited on the fork
     const bool host_serial = v->obs_early && split && C > 1 && v->host_serial;
     bool pre_waited = false; // this act's prefetch stream already waits for the previous act's generation
+    std::vector<size_t> gen_chains; // inband prefetch: chains whose spare generation follows every chain
     for (size_t ki = 0; ki < C; ki++) {
         const size_t k = host_serial ? (ki + 1) % C : C > 1 ? (size_t)v->launch_order[ki] : ki;
         // single game: the finished envs' resets (level generation: long single-wave chains) run on
@@ -578,7 +583,10 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         if (!pfk) dk.sp_envs = nullptr; // this chain neither swaps in spares nor requests them
         pg_launch_reset(&dk, game, list, cnt, r, 0, 0, act, slot);
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 3], r));
-        if (pfk) { // the next levels of the envs just reset, off the critical path
+        if (pfk && v->inband && C > 1) { // generated after every chain, on the packing's gen stream
+            HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
+            gen_chains.push_back(k);
+        } else if (pfk) { // the next levels of the envs just reset, off the critical path
             hipStream_t p = v->pstreams[act % v->npstreams];
             HIPCHECK(hipEventRecord(v->ev_stepped[k], r));
             HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
@@ -610,6 +618,15 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
         }
         if (e) HIPCHECK(hipEventRecord(e[PG_EV_G * k + 6], s));
         if (v->obs_early && split) HIPCHECK(hipEventRecord(v->ev_rendered[k], s));
+    }
+    if (!gen_chains.empty()) { // inband prefetch: the spare generations, one job on stream gen_si
+        hipStream_t p = v->gen_si > 0 ? v->gstreams[v->gen_si] : v->stream;
+        for (size_t k : gen_chains) {
+            HIPCHECK(hipStreamWaitEvent(p, v->ev_stepped[k], 0));
+            pg_launch_reset(&v->dev, v->chain_game(k), v->chain_list(k), v->chain_count(k), p, 2, 0, act, v->chain_slot(k));
+        }
+        HIPCHECK(hipEventRecord(v->ev_pre[act % v->lag], p));
+        v->ev_pre_set[act % v->lag] = true;
     }
     if (v->obs_early && split) {
         // host buffers: each part's observations leave as soon as it rendered, on one copy stream in the
@@ -1077,8 +1094,34 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         if (ns < (int)nchains) {
             // per-game chain cost, ms at 4,096 envs (step + reset + render per game inside the all-16 mixed
             // shard, profiles/r04/r04_l_mixed/mixed16_default.json per_game)
-            static const float cost[PG_NUM_GAMES] = {0.21f, 0.85f, 1.13f, 0.67f, 0.46f, 0.50f, 0.66f, 0.74f,
-                                                     0.49f, 1.45f, 0.99f, 0.51f, 0.51f, 0.47f, 0.35f, 0.67f};
+            static const float cost0[PG_NUM_GAMES] = {0.21f, 0.85f, 1.13f, 0.67f, 0.46f, 0.50f, 0.66f, 0.74f,
+                                                      0.49f, 1.45f, 0.99f, 0.51f, 0.51f, 0.47f, 0.35f, 0.67f};
+            // inband prefetch (PROCGEN_MI355X_PREFETCH_INBAND=1 with PROCGEN_MI355X_PREFETCH_GAMES): a
+            // prefetched chain's reset becomes a swap and its level generation (reset_cost, r05 mixed16
+            // per_game) one job packed after every chain of the least loaded stream
+            static const float reset_cost[PG_NUM_GAMES] = {0.07f, 0.06f, 0.66f, 0.18f, 0.08f, 0.09f, 0.08f, 0.20f,
+                                                           0.24f, 0.96f, 0.57f, 0.20f, 0.09f, 0.09f, 0.06f, 0.33f};
+            float cost[PG_NUM_GAMES];
+            for (int g = 0; g < PG_NUM_GAMES; g++) cost[g] = cost0[g];
+            const char *ib = getenv("PROCGEN_MI355X_PREFETCH_INBAND"), *ipg = getenv("PROCGEN_MI355X_PREFETCH_GAMES");
+            v->inband = ib && ib[0] == '1' && ipg && ipg[0];
+            float gen_cost = 0.f;
+            if (v->inband) {
+                const std::string sel(ipg);
+                for (int g : gids) {
+                    bool on = sel == "all";
+                    size_t a = 0;
+                    while (!on && a <= sel.size()) {
+                        const size_t b = std::min(sel.find(',', a), sel.size());
+                        on = game_id(sel.substr(a, b - a)) == g;
+                        a = b + 1;
+                    }
+                    if (on) {
+                        cost[g] = cost0[g] - reset_cost[g] + 0.05f; // the swap
+                        gen_cost += reset_cost[g];
+                    }
+                }
+            }
             std::vector<size_t> order(nchains);
             for (size_t k = 0; k < nchains; k++) order[k] = k;
             std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[gids[a]] > cost[gids[b]]; });
@@ -1117,6 +1160,13 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
                 load[bj] += d;
                 if (bx >= 0) v->chain_stream[bx] = bj;
                 if (by >= 0) v->chain_stream[by] = hi;
+            }
+            if (v->inband) { // the generation job goes to the least loaded stream (which holds chains)
+                int lo = 0;
+                for (int j = 1; j < ns; j++)
+                    if (load[j] < load[lo]) lo = j;
+                v->gen_si = lo;
+                load[lo] += gen_cost;
             }
             // enqueue order: game id (default); PROCGEN_MI355X_MIXED_ORDER=desc enqueues the costliest
             // chains first (all-16 shard 21.7 -> 20.8 M env-steps/s, profiles/r04/r04_m_mixed), asc the

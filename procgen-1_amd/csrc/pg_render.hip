@@ -3033,7 +3033,10 @@ __global__ __launch_bounds__(64, rf_waves<G>()) void pg_render_rf_kernel(PGDev d
     if constexpr (rf_game<G>()) {
         const PGDev d = game_view(dg, G);
         __shared__ __attribute__((aligned(16))) uint8_t tab[rf_tab_bytes<G>()];
-        __shared__ __attribute__((aligned(16))) int4 desc[2 * rf_dcap<G>()];
+#ifndef RF_LDS_PAD
+#define RF_LDS_PAD 0 // experiment: LDS bytes added per workgroup (caps the waves the render keeps resident)
+#endif
+        __shared__ __attribute__((aligned(16))) int4 desc[2 * rf_dcap<G>() + RF_LDS_PAD / 16];
         __shared__ __attribute__((aligned(16))) int4 rdesc[6 * rf_rcap<G>()];
         const int bidx = (int)blockIdx.x;
         int env;

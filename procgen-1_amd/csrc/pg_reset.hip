@@ -88,7 +88,23 @@ struct RCtx {
     int32_t mti;
     int16_t *grid;   // LDS grid
     AgLds *ag;       // AssetGen scratch (use_generated_assets kernels only, else null)
+#ifdef PG_PROF_RESET
+    uint64_t last;   // diagnostic build (VARIANT=rprof EXTRA=-DPG_PROF_RESET): level-generation phases
+#endif
 };
+
+// Diagnostic phase stamps of a level generation (scripts/reset_phases.py): cycles since the previous
+// stamp added to prof[env][8 + k]; prof[env][0] counts the resets.  Nothing in the product build.
+#ifdef PG_PROF_RESET
+#define RMARK(c, k)                                                                          \
+    do {                                                                                     \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                    \
+        if (LANE == 0) (c).d.prof[(size_t)(c).env * 16 + 8 + (k)] += t_ - (c).last;          \
+        (c).last = t_;                                                                       \
+    } while (0)
+#else
+#define RMARK(c, k) ((void)0)
+#endif
 
 DEV float &EF(RCtx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
 DEV int &EI(RCtx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
@@ -1995,9 +2011,12 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     base_game_reset<PG_GAME_CAVEFLYER>(c);
     const int W = c.s.main_width, n = W * c.s.main_height;
     c.s.out_of_bounds_object = WALL_OBJ;
+    RMARK(c, 0);
     cf_random_fill(c);
     for (int it = 0; it < 4; it++) cf_update(c, S);
+    RMARK(c, 1);
     const int best = cf_find_best_room(c, S);
+    RMARK(c, 2);
     if (best < 0) {
         c.s.error = PG_ERR_GRID;
         return;
@@ -2029,7 +2048,9 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     wave_sync();
     int ge = add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, CF_GOAL);
     EI(c, F_FLAGS, ge) = EF_AUTO_ERASE | EF_COLLIDES;
+    RMARK(c, 2);
     const int npath = cf_find_path(c, S, agent_cell, goal_cell);
+    RMARK(c, 3);
     if (c.s.opt_distribution_mode != PG_MEMORY) { // should_prune: wide path = path grown 4 times
         for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
         wave_sync();
@@ -2056,6 +2077,7 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
         nfree += __popcll(m);
     }
     wave_sync();
+    RMARK(c, 4);
     const int chunk_size = nfree / 80, num_objs = 3 * chunk_size;
     // simple_choose(free_cells.size(), num_objs): rejection against the picks so far
     for (int i = 0; i < num_objs; i++) {
@@ -2090,6 +2112,7 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
             EI(c, F_FLAGS, e) = EF_AUTO_ERASE | EF_COLLIDES | EF_SMART_STEP;
         }
     }
+    RMARK(c, 5);
     for (int i = LANE; i < n; i += 64)
         if (c.grid[i] == CF_MARKER) c.grid[i] = SPACE;
     wave_sync();
@@ -2171,7 +2194,9 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
         c.s.error = PG_ERR_GRID;
         return;
     }
+    RMARK(c, 6);
     mg_generate_maze_no_dead_ends(c, g);
+    RMARK(c, 0);
     for (int base = 0; base < n;) {
         if (c.mti >= PG_MT_N) {
             mt_twist_lds(c.mt);
@@ -2197,6 +2222,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
         if (x == 0 || y == 0 || x == W - 1 || y == H - 1) c.grid[i] = JP_CAVEWALL;
     }
     wave_sync();
+    RMARK(c, 1);
     const int best = cf_find_best_room(c, S);
     if (best < 0) {
         c.s.error = PG_ERR_GRID;
@@ -2231,7 +2257,9 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
     }
     const int agent_cell = S->list2[randn(c, ncand)];
     wave_sync();
+    RMARK(c, 2);
     const int npath = cf_find_path(c, S, agent_cell, goal_cell);
+    RMARK(c, 3);
     if (dm != PG_MEMORY) { // should_prune
         for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
         wave_sync();
@@ -2239,6 +2267,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
         for (int i = LANE; i < n; i += 64) c.grid[i] = (S->f[i] & CF_SET) ? SPACE : JP_CAVEWALL;
         wave_sync();
     }
+    RMARK(c, 4);
     add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, JP_GOAL); // entity 1
     const float spike_prob = dm == PG_MEMORY ? 0 : .2f;
     jp_ordered_scan(c, n, [&](int x, int y) { return jp_spike_site(c, x, y); }, [&](int x, int y) {
@@ -2249,6 +2278,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
                         if (jp_left_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
                         if (jp_right_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
                     });
+    RMARK(c, 5);
     EF(c, F_X, 0) = (float)((agent_cell % W) + .5);
     EF(c, F_Y, 0) = (float)(agent_cell / W) + EF(c, F_RY, 0);
     wave_sync();
@@ -2577,6 +2607,10 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     c.eb = (size_t)env * PG_CAP;
     c.mt = lds_mt;
     c.grid = lds_grid;
+#ifdef PG_PROF_RESET
+    c.last = __builtin_amdgcn_s_memtime();
+    if (LANE == 0) d.prof[(size_t)env * 16] += 1; // the reset count (the step phases are off here)
+#endif
     uint32_t *rg = d.mt + (size_t)env * 2 * PG_MT_WORDS;
     uint32_t *lsg = rg + PG_MT_WORDS;
 
@@ -2619,6 +2653,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     c.s.episodes_remaining -= 1;
     c.s.action = c.s.default_action;
     c.s.rg_mti = c.mti;
+    RMARK(c, 6);
 
     // write the generator, the grid and the scalars back to HBM
     wave_sync();
@@ -2680,6 +2715,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     wave_sync();
     reinterpret_cast<uint2 *>(d.envs + env)[LANE] = reinterpret_cast<const uint2 *>(lds_env)[LANE];
     wave_sync();
+    RMARK(c, 7);
 }
 
 // ------------------------------------------------------------------ level prefetch

@@ -80,17 +80,21 @@ def test_prefetch_after_set_state(game, prefetch):
     assert ends > 0
 
 
-@pytest.mark.parametrize("mode", ["all", "default", "jumper_caveflyer"])
+@pytest.mark.parametrize("mode", ["all", "default", "jumper_caveflyer", "inband"])
 def test_prefetch_mixed_batch(mode, prefetch, monkeypatch):
     """A mixed batch with the prefetch forced on for every game ("all": every game's chain requests and
     swaps its own spares, one ring slot per act, cleared once for all games), with the default (off in a
     mixed batch) and with PROCGEN_MI355X_PREFETCH_GAMES=jumper,caveflyer (only those chains use spares,
-    the others reset in line); parity per env against the oracle."""
+    the others reset in line), and with PROCGEN_MI355X_PREFETCH_INBAND=1 on top (those chains' level
+    generation runs as one job on a chain stream after every chain, not on the prefetch stream); parity per
+    env against the oracle."""
     from oracle_lib import OracleEnv
     if mode == "all":
         prefetch()
-    elif mode == "jumper_caveflyer":
+    elif mode in ("jumper_caveflyer", "inband"):
         monkeypatch.setenv("PROCGEN_MI355X_PREFETCH_GAMES", "jumper,caveflyer")
+        if mode == "inband":
+            monkeypatch.setenv("PROCGEN_MI355X_PREFETCH_INBAND", "1")
     names = ["caveflyer", "coinrun", "jumper", "maze"]
     num = 8
     env = make_gpu(num, ",".join(names), num_levels=0, rand_seed=6)
