@@ -352,6 +352,10 @@ struct VecEnv {
     // high-priority chain stream the runtime made them a blit kernel (copyBuffer) that held the CUs
     // for the whole 7 ms transfer and stalled the other part's render behind it
     hipStream_t cstream = nullptr;
+    // render_mode="rgb_array" into page-locked caller arrays: the 512x512 frames render in chunks on
+    // hstream while the engine stream DMAs the finished chunks (PROCGEN_MI355X_HR_CHUNKS, default 8)
+    hipStream_t hstream = nullptr;
+    std::vector<hipEvent_t> hr_ev;
     hipEvent_t ev_cdone = nullptr;
     std::vector<hipEvent_t> ev_rendered;
     // timing
@@ -440,6 +444,7 @@ static hipError_t copy_sync(VecEnv *v, void *dst, const void *src, size_t bytes,
 int upload_atlas(VecEnv *v, const uint32_t *pixels, int64_t num_pixels, const pg_image *sprites,
                  const pg_image *backgrounds, const int32_t *num_backgrounds, const int32_t *num_themes);
 int copy_latent(VecEnv *v);
+int copy_latent_grid(VecEnv *v);
 
 int fail(VecEnv *v, int code, const char *msg) {
     if (v && !v->error) {
@@ -775,23 +780,47 @@ int copy_latent(VecEnv *v) {
     const size_t n = (size_t)v->num_envs;
     if (v->render_human) { // VecGame::observe: every env's frame at RENDER_RES (vecgame.cpp:415-423)
         const size_t per = (size_t)512 * 512, cnt = (size_t)v->count_of();
+        if (v->hr_host) {
+            // DMA into the page-locked caller array, each env's frame to its own slot.  The frames render
+            // in chunks on hstream and each chunk leaves on the engine stream as soon as it is done (the
+            // engine stream's copies run on SDMA): the copy of chunk j overlaps the render of
+            // chunk j + 1, so only the first chunk's render is not under the D2H copy
+            const size_t nch = v->hr_ev.size();
+            uint8_t *dst = (uint8_t *)v->hr_host;
+            // created on first use: a stream made in libenv_make shifts the chains' hardware queues (§4.6)
+            if (!v->hstream) HIPCHECK(hipStreamCreateWithFlags(&v->hstream, hipStreamNonBlocking));
+            HIPCHECK(hipEventRecord(v->hr_ev[0], v->stream)); // the act's state is complete
+            HIPCHECK(hipStreamWaitEvent(v->hstream, v->hr_ev[0], 0));
+            for (size_t k = 0; k < v->games.size(); k++)
+                for (size_t j = 0; j < nch; j++) {
+                    const size_t lo = cnt * j / nch, hi = cnt * (j + 1) / nch, b = k * cnt + lo;
+                    if (hi <= lo) continue;
+                    const int32_t *list = v->games.size() > 1 ? v->list_of(k) + lo : v->d_ident + lo;
+                    if (pg_launch_render_hires(&v->dev, v->games[k], list, (int)(hi - lo), v->hr_frames + b * per,
+                                               v->hr_rgb + b * per * 3, v->hstream) != 0)
+                        return fail(v, PG_ERR_BAD_OPTION, "render_mode=rgb_array: game not built");
+                    HIPCHECK(hipGetLastError());
+                    HIPCHECK(hipEventRecord(v->hr_ev[j], v->hstream));
+                    HIPCHECK(hipStreamWaitEvent(v->stream, v->hr_ev[j], 0));
+                    if (v->games.size() == 1) {
+                        HIPCHECK(hipMemcpyAsync(dst + lo * per * 3, v->hr_rgb + lo * per * 3, (hi - lo) * per * 3,
+                                                hipMemcpyDeviceToHost, v->stream));
+                    } else {
+                        for (size_t q = lo; q < hi; q++)
+                            HIPCHECK(hipMemcpyAsync(dst + (size_t)v->h_lists[k * cnt + q] * per * 3,
+                                                    v->hr_rgb + (k * cnt + q) * per * 3, per * 3, hipMemcpyDeviceToHost,
+                                                    v->stream));
+                    }
+                }
+            HIPCHECK(hipStreamSynchronize(v->stream));
+            return copy_latent_grid(v);
+        }
         for (size_t k = 0; k < v->games.size(); k++)
             if (pg_launch_render_hires(&v->dev, v->games[k], v->list_of(k), (int)cnt, v->hr_frames + k * cnt * per,
                                        v->hr_rgb + k * cnt * per * 3, v->stream) != 0)
                 return fail(v, PG_ERR_BAD_OPTION, "render_mode=rgb_array: game not built");
         HIPCHECK(hipGetLastError());
-        if (v->hr_host) { // DMA into the page-locked caller array, each env's frame to its own slot
-            uint8_t *dst = (uint8_t *)v->hr_host;
-            if (v->games.size() == 1) {
-                HIPCHECK(hipMemcpyAsync(dst, v->hr_rgb, cnt * per * 3, hipMemcpyDeviceToHost, v->stream));
-            } else {
-                for (size_t k = 0; k < v->games.size(); k++)
-                    for (size_t q = 0; q < cnt; q++)
-                        HIPCHECK(hipMemcpyAsync(dst + (size_t)v->h_lists[k * cnt + q] * per * 3,
-                                                v->hr_rgb + (k * cnt + q) * per * 3, per * 3, hipMemcpyDeviceToHost, v->stream));
-            }
-            HIPCHECK(hipStreamSynchronize(v->stream));
-        } else {
+        {
             std::vector<uint8_t> host(cnt * per * 3);
             for (size_t k = 0; k < v->games.size(); k++) {
                 HIPCHECK(copy_sync(v, host.data(), v->hr_rgb + k * cnt * per * 3, host.size(), hipMemcpyDeviceToHost));
@@ -802,6 +831,11 @@ int copy_latent(VecEnv *v) {
             }
         }
     }
+    return copy_latent_grid(v);
+}
+
+int copy_latent_grid(VecEnv *v) {
+    const size_t n = (size_t)v->num_envs;
     if (v->has_latent) { // grid_size, grid, agent_pos, exit_pos (vecgame.cpp:270-316)
         const size_t row = (size_t)PG_LATENT_N * 4;
         std::vector<int32_t> lat((size_t)PG_LATENT_N * n);
@@ -1310,9 +1344,12 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     if (render_human) {
         rc |= dalloc(v, &v->hr_frames, n * 512 * 512);
         rc |= dalloc(v, &v->hr_rgb, n * 512 * 512 * 3);
+        const char *hc = getenv("PROCGEN_MI355X_HR_CHUNKS");
+        v->hr_ev.assign(std::min(std::max(hc ? atoi(hc) : 8, 1), 64), nullptr);
+        for (auto &e : v->hr_ev) rc |= hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess;
     }
     if (gids.size() > 1) rc |= dalloc(v, &v->d_lists, n);
-    if (v->parts > 1) {
+    if (v->parts > 1 || render_human) { // part lists; the rgb_array chunks of a single-game batch
         rc |= dalloc(v, &v->d_ident, n);
         if (!rc) {
             std::vector<int32_t> id(n);
@@ -1585,6 +1622,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     for (auto &s : v->gstreams)
         if (s) (void)hipStreamSynchronize(s);
     if (v->cstream) (void)hipStreamSynchronize(v->cstream);
+    if (v->hstream) (void)hipStreamSynchronize(v->hstream);
     if (v->stream) (void)hipStreamSynchronize(v->stream);
     unregister_buffers(v);
     for (void *p : v->allocs) hipFree(p);
@@ -1603,6 +1641,9 @@ LIBENV_API void libenv_close(libenv_env *env) {
         if (e) hipEventDestroy(e);
     if (v->ev_cdone) hipEventDestroy(v->ev_cdone);
     if (v->cstream) hipStreamDestroy(v->cstream);
+    if (v->hstream) hipStreamDestroy(v->hstream);
+    for (auto &e : v->hr_ev)
+        if (e) hipEventDestroy(e);
     for (auto &s : v->rstreams)
         if (s) hipStreamDestroy(s);
     for (auto &p : v->pstreams)

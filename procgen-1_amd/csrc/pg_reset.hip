@@ -68,6 +68,7 @@ struct CaveScratch {
     int16_t list[PG_GRID_MAX + 1];  // BFS frontier, then free cells
     int16_t list2[PG_GRID_MAX + 1]; // next frontier, then the goal path
     uint8_t f[PG_GRID_MAX];         // CF_* bits per cell
+    uint32_t pm[2 * 64];            // the goal path as row masks (cf_rows_of_path)
 };
 template <> struct Scratch<PG_GAME_CAVEFLYER> { CaveScratch cf; };
 // jumper: MazeGen first (its grid is read by the random fill), then the RoomGenerator
@@ -1823,52 +1824,122 @@ DEV void cf_random_fill(RCtx &c) { // rand01() < .5 ? WALL_OBJ : SPACE per cell,
     }
 }
 
-DEV void cf_update(RCtx &c, CaveScratch *S) { // roomgen.cpp:3-37 (count_neighbors(i, WALL_OBJ) >= 5)
-    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
-    for (int i = LANE; i < n; i += 64) {
-        const int x = i % W, y = i / W;
-        int cnt = 0;
-        for (int a = -1; a <= 1; a++)
-            for (int b = -1; b <= 1; b++) {
-                const int xx = x + a, yy = y + b;
-                const int v = (0 <= xx && xx < W && 0 <= yy && yy < H) ? c.grid[yy * W + xx] : c.s.out_of_bounds_object;
-                cnt += v == WALL_OBJ;
-            }
-        S->a[i] = cnt >= 5 ? WALL_OBJ : SPACE;
+// The room generator's grid sweeps on row masks: lane y holds row y of the grid as a 64-bit mask
+// (bit x = cell (x, y); worlds are at most 60 x 60), neighbours come from shifts and from the rows of
+// lanes y -/+ 1.  Each sweep is then a few dozen ALU instructions per wave instead of a pass of
+// dependent LDS reads per 64 cells (r05 reset phase stamps: the per-cell sweeps and the labelling were
+// 2/3 of a caveflyer / jumper level generation).
+DEV uint64_t cf_shfl64(uint64_t v, int src) {
+    const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
+    return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+DEV uint64_t cf_row_full(int W) { return W >= 64 ? ~0ull : (1ull << W) - 1ull; }
+// row LANE of the grid: bit x set where pred(cell) (lanes >= H: 0)
+template <typename P>
+DEV uint64_t cf_row_of(RCtx &c, P pred) {
+    const int W = c.s.main_width, H = c.s.main_height;
+    uint64_t r = 0;
+    if (LANE < H)
+        for (int x = 0; x < W; x++) r |= (uint64_t)(pred(c.grid[LANE * W + x]) ? 1 : 0) << x;
+    return r;
+}
+// grid row LANE from a mask: bit set -> on, clear -> off
+DEV void cf_write_row(RCtx &c, uint64_t r, int on, int off) {
+    const int W = c.s.main_width, H = c.s.main_height;
+    if (LANE < H)
+        for (int x = 0; x < W; x++) c.grid[LANE * W + x] = (int16_t)(((r >> x) & 1) ? on : off);
+    wave_sync();
+}
+// the first npath cells of S->list2 as row masks (row LANE returned)
+DEV uint64_t cf_rows_of_path(RCtx &c, CaveScratch *S, int npath) {
+    const int W = c.s.main_width;
+    S->pm[LANE] = 0;
+    S->pm[64 + LANE] = 0;
+    wave_sync();
+    for (int q = LANE; q < npath; q += 64) {
+        const int cell = S->list2[q], x = cell % W, y = cell / W;
+        atomicOr(&S->pm[2 * y + (x >> 5)], 1u << (x & 31));
     }
     wave_sync();
-    for (int i = LANE; i < n; i += 64) c.grid[i] = S->a[i];
+    const uint64_t r = (uint64_t)S->pm[2 * LANE] | ((uint64_t)S->pm[2 * LANE + 1] << 32);
     wave_sync();
+    return LANE < c.s.main_height ? r : 0;
+}
+
+// `iters` rounds of roomgen.cpp:3-37 (a cell becomes WALL_OBJ when count_neighbors(i, WALL_OBJ) >= 5
+// over its 3 x 3 block, out-of-bounds cells counting as out_of_bounds_object), every cell from the
+// previous grid; after each round the cells of `path` (row masks, may be 0) are reset to SPACE.  The
+// grid holds only WALL_OBJ / SPACE before and after.
+DEV void cf_update(RCtx &c, int iters, uint64_t path) {
+    const int W = c.s.main_width, H = c.s.main_height;
+    const uint64_t full = cf_row_full(W), ob = c.s.out_of_bounds_object == WALL_OBJ ? ~0ull : 0ull;
+    const uint64_t ob_lo = ob & 1ull, ob_hi = ob & (1ull << (W - 1));
+    uint64_t row = cf_row_of(c, [](int v) { return v == WALL_OBJ; });
+    for (int it = 0; it < iters; it++) {
+        uint64_t up = cf_shfl64(row, LANE > 0 ? LANE - 1 : 0), dn = cf_shfl64(row, LANE < 63 ? LANE + 1 : 63);
+        if (LANE == 0) up = ob & full;
+        if (LANE >= H - 1) dn = ob & full;
+        // per source row: sum of (x-1, x, x+1) as a bit-sliced 2-bit number (s + 2 c)
+        uint64_t sr[3], cr[3];
+        const uint64_t rows3[3] = {up, row, dn};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint64_t m = rows3[k], l = (m << 1) | ob_lo, r = (m >> 1) | ob_hi;
+            sr[k] = l ^ m ^ r;
+            cr[k] = (l & m) | (l & r) | (m & r);
+        }
+        const uint64_t t0 = sr[0] ^ sr[1] ^ sr[2], t1 = (sr[0] & sr[1]) | (sr[0] & sr[2]) | (sr[1] & sr[2]);
+        const uint64_t u0 = cr[0] ^ cr[1] ^ cr[2], u1 = (cr[0] & cr[1]) | (cr[0] & cr[2]) | (cr[1] & cr[2]);
+        // count = t0 + 2 (t1 + u0) + 4 u1 >= 5
+        row = ((u1 & (t0 | t1 | u0)) | (t0 & t1 & u0)) & full & ~path;
+        if (LANE >= H) row = 0;
+    }
+    cf_write_row(c, row, WALL_OBJ, SPACE);
 }
 
 // find_best_room (roomgen.cpp:116-136) -> label of the best room (cells with a[i] == label), or -1
+// Components by union-find on S->b (Playne & Hawick's lock-free merge: hook the larger root under
+// the smaller with atomicMin, retry on a lost race), so every root is its component's smallest cell
+// index -- the label the reference's flood fill order makes first (roomgen.cpp:116-136).
+DEV int cf_uf_find(const int32_t *L, int x) {
+    int p = L[x];
+    while (p != x) {
+        x = p;
+        p = L[x];
+    }
+    return x;
+}
+DEV void cf_uf_merge(int32_t *L, int a, int b) {
+    for (;;) {
+        a = cf_uf_find(L, a);
+        b = cf_uf_find(L, b);
+        if (a == b) return;
+        if (a > b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        const int old = atomicMin(&L[b], a); // b: the larger root
+        if (old == b) return;
+        b = old; // b was hooked meanwhile: merge with what it now points to
+    }
+}
 DEV int cf_find_best_room(RCtx &c, CaveScratch *S) {
-    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+    const int W = c.s.main_width, n = W * c.s.main_height;
+    int32_t *L = S->b;
+    for (int i = LANE; i < n; i += 64) L[i] = c.grid[i] == SPACE ? i : -1;
+    wave_sync();
     for (int i = LANE; i < n; i += 64) {
-        S->a[i] = c.grid[i] == SPACE ? (int16_t)i : (int16_t)-1;
-        S->b[i] = 0;
+        if (L[i] < 0) continue;
+        const int x = i % W;
+        if (x > 0 && L[i - 1] >= 0) cf_uf_merge(L, i, i - 1);
+        if (i >= W && L[i - W] >= 0) cf_uf_merge(L, i, i - W);
     }
     wave_sync();
-    for (;;) {
-        bool changed = false;
-        for (int i = LANE; i < n; i += 64) {
-            int l = S->a[i];
-            if (l < 0) continue;
-            int m = l;
-            const int x = i % W, y = i / W;
-            if (x > 0 && S->a[i - 1] >= 0 && S->a[i - 1] < m) m = S->a[i - 1];
-            if (x < W - 1 && S->a[i + 1] >= 0 && S->a[i + 1] < m) m = S->a[i + 1];
-            if (y > 0 && S->a[i - W] >= 0 && S->a[i - W] < m) m = S->a[i - W];
-            if (y < H - 1 && S->a[i + W] >= 0 && S->a[i + W] < m) m = S->a[i + W];
-            m = S->a[m] < m ? S->a[m] : m; // pointer jump (labels are cells of the same component)
-            if (m < l) {
-                S->a[i] = (int16_t)m;
-                changed = true;
-            }
-        }
-        wave_sync();
-        if (!ballot(changed)) break;
-    }
+    for (int i = LANE; i < n; i += 64) S->a[i] = (int16_t)(L[i] < 0 ? -1 : cf_uf_find(L, i));
+    wave_sync();
+    for (int i = LANE; i < n; i += 64) S->b[i] = 0;
+    wave_sync();
     for (int i = LANE; i < n; i += 64)
         if (S->a[i] >= 0) atomicAdd(&S->b[S->a[i]], 1);
     wave_sync();
@@ -1978,33 +2049,25 @@ DEV int cf_find_path(RCtx &c, CaveScratch *S, int src, int dst) {
     return len;
 }
 
-DEV void cf_expand_room(RCtx &c, CaveScratch *S, int rounds) { // expand_room (roomgen.cpp:138-177)
-    const int W = c.s.main_width, H = c.s.main_height, n = W * H;
+// expand_room (roomgen.cpp:138-177) from the path cells (row masks): each round every SPACE cell not yet
+// in the set with an 8-neighbour added in the previous round joins; then the grid becomes SPACE on the
+// set and `wall` elsewhere
+DEV void cf_expand_room(RCtx &c, uint64_t path, int rounds, int wall) {
+    const int W = c.s.main_width, H = c.s.main_height;
+    const uint64_t full = cf_row_full(W);
+    const uint64_t sp = cf_row_of(c, [](int v) { return v == SPACE; });
+    uint64_t set = path, cur = path;
     for (int r = 0; r < rounds; r++) {
-        for (int i = LANE; i < n; i += 64) {
-            const uint8_t fi = S->f[i];
-            bool add = false;
-            if (!(fi & CF_SET) && c.grid[i] == SPACE) {
-                const int x = i % W, y = i / W;
-                for (int a = -1; a <= 1; a++)
-                    for (int b = -1; b <= 1; b++) {
-                        const int xx = x + a, yy = y + b;
-                        if ((a != 0 || b != 0) && 0 <= xx && xx < W && 0 <= yy && yy < H) {
-                            const int v = yy * W + xx;
-                            if ((S->f[v] & CF_CURR) && c.grid[v] == SPACE) add = true;
-                        }
-                    }
-            }
-            if (add) S->f[i] = fi | CF_NEW;
-        }
-        wave_sync();
-        for (int i = LANE; i < n; i += 64) {
-            uint8_t fi = S->f[i] & (uint8_t)~CF_CURR;
-            if (fi & CF_NEW) fi = (uint8_t)((fi & ~CF_NEW) | CF_SET | CF_CURR);
-            S->f[i] = fi;
-        }
-        wave_sync();
+        const uint64_t a = cur & sp, h = a | (a << 1) | (a >> 1);
+        uint64_t up = cf_shfl64(h, LANE > 0 ? LANE - 1 : 0), dn = cf_shfl64(h, LANE < 63 ? LANE + 1 : 63);
+        if (LANE == 0) up = 0;
+        if (LANE >= H - 1) dn = 0;
+        cur = (h | up | dn) & sp & ~set & full;
+        if (LANE >= H) cur = 0;
+        set |= cur;
     }
+    wave_sync(); // every lane read its row before any is rewritten
+    cf_write_row(c, set, SPACE, wall);
 }
 
 DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
@@ -2013,7 +2076,7 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     c.s.out_of_bounds_object = WALL_OBJ;
     RMARK(c, 0);
     cf_random_fill(c);
-    for (int it = 0; it < 4; it++) cf_update(c, S);
+    cf_update(c, 4, 0);
     RMARK(c, 1);
     const int best = cf_find_best_room(c, S);
     RMARK(c, 2);
@@ -2051,18 +2114,9 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     RMARK(c, 2);
     const int npath = cf_find_path(c, S, agent_cell, goal_cell);
     RMARK(c, 3);
-    if (c.s.opt_distribution_mode != PG_MEMORY) { // should_prune: wide path = path grown 4 times
-        for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
-        wave_sync();
-        cf_expand_room(c, S, 4);
-        for (int i = LANE; i < n; i += 64) c.grid[i] = (S->f[i] & CF_SET) ? SPACE : WALL_OBJ;
-        wave_sync();
-    }
-    for (int it = 0; it < 4; it++) {
-        cf_update(c, S);
-        for (int q = LANE; q < npath; q += 64) c.grid[S->list2[q]] = SPACE;
-        wave_sync();
-    }
+    const uint64_t path = cf_rows_of_path(c, S, npath);
+    if (c.s.opt_distribution_mode != PG_MEMORY) cf_expand_room(c, path, 4, WALL_OBJ); // should_prune: path grown 4 times
+    cf_update(c, 4, path); // the path cells stay SPACE after every round
     for (int q = LANE; q < npath; q += 64) c.grid[S->list2[q]] = CF_MARKER;
     wave_sync();
     nfree = 0;
@@ -2216,7 +2270,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
         wave_sync();
     }
     CaveScratch *S = &X->cf; // the maze is dead from here on
-    for (int it = 0; it < 2; it++) cf_update(c, S);
+    cf_update(c, 2, 0);
     for (int i = LANE; i < n; i += 64) { // border cells
         const int x = i % W, y = i / W;
         if (x == 0 || y == 0 || x == W - 1 || y == H - 1) c.grid[i] = JP_CAVEWALL;
@@ -2260,13 +2314,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
     RMARK(c, 2);
     const int npath = cf_find_path(c, S, agent_cell, goal_cell);
     RMARK(c, 3);
-    if (dm != PG_MEMORY) { // should_prune
-        for (int q = LANE; q < npath; q += 64) S->f[S->list2[q]] |= CF_SET | CF_CURR;
-        wave_sync();
-        cf_expand_room(c, S, 4);
-        for (int i = LANE; i < n; i += 64) c.grid[i] = (S->f[i] & CF_SET) ? SPACE : JP_CAVEWALL;
-        wave_sync();
-    }
+    if (dm != PG_MEMORY) cf_expand_room(c, cf_rows_of_path(c, S, npath), 4, JP_CAVEWALL); // should_prune
     RMARK(c, 4);
     add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, JP_GOAL); // entity 1
     const float spike_prob = dm == PG_MEMORY ? 0 : .2f;

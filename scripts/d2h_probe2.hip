@@ -5,6 +5,8 @@
 //   B: the copy on its own stream after a hipStreamWaitEvent on stream i's kernel
 //   C: the copy on stream i with nothing before it
 //   D: two copies in flight on two streams at once, each after its own kernel
+// Built as an executable (main) and as a library (d2h_probe2.so, d2h_probe()) that
+// scripts/d2h_probe_torch.py calls inside a Python process with and without torch's HIP context.
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
@@ -23,7 +25,7 @@ static double since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
-int main() {
+extern "C" int d2h_probe(void) {
     const size_t n = (size_t)32768 * 12288;
     void *d = nullptr, *h = nullptr, *h2 = nullptr;
     float *scratch = nullptr;
@@ -76,3 +78,77 @@ int main() {
     free(h2);
     return 0;
 }
+
+// E: the copy after a kernel into a caller-supplied buffer (a numpy array from Python), registered here
+extern "C" int d2h_probe_host(void *h) {
+    const size_t n = (size_t)32768 * 12288;
+    void *d = nullptr;
+    float *scratch = nullptr;
+    CK(hipMalloc(&d, n));
+    CK(hipMalloc(&scratch, 1024 * 64 * sizeof(float)));
+    CK(hipHostRegister(h, n, hipHostRegisterDefault));
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        auto t0 = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(busy, dim3(1024), dim3(64), 0, s, scratch, 100000LL);
+        CK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        printf("E caller buffer %p: kernel + copy %.2f ms\n", h, since(t0) * 1e3);
+    }
+    CK(hipHostUnregister(h));
+    CK(hipStreamDestroy(s));
+    CK(hipFree(d));
+    CK(hipFree(scratch));
+    return 0;
+}
+
+// F-I: the engine's conditions one at a time, each timed (SDMA 7.06 ms, blit ~7.4 ms per 402 MB):
+//   F priority streams exist in the process, G the source inside a 3.3 GB allocation (at offset 2.9 GB),
+//   H the destination at an offset inside a larger registered region, I hipMemcpyDefault / DtoH API
+extern "C" int d2h_probe_engine_like(void) {
+    const size_t n = (size_t)32768 * 12288;
+    float *scratch = nullptr;
+    CK(hipMalloc(&scratch, 1024 * 64 * sizeof(float)));
+    auto timed = [&](const char *what, void *dst, const void *src, hipStream_t s, int api) -> int {
+        for (int i = 0; i < 2; i++) {
+            auto t0 = std::chrono::steady_clock::now();
+            hipLaunchKernelGGL(busy, dim3(1024), dim3(64), 0, s, scratch, 100000LL);
+            hipError_t e = api == 0   ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s)
+                           : api == 1 ? hipMemcpyAsync(dst, src, n, hipMemcpyDefault, s)
+                                      : hipMemcpyDtoHAsync(dst, (hipDeviceptr_t)src, n, s);
+            if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return 1;
+            printf("%s: kernel + copy %.2f ms\n", what, since(t0) * 1e3);
+        }
+        return 0;
+    };
+    void *d = nullptr, *big = nullptr;
+    CK(hipMalloc(&d, n));
+    void *h = aligned_alloc(4096, 3 * n);
+    CK(hipHostRegister(h, 3 * n, hipHostRegisterDefault));
+    hipStream_t s, ph, pl;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (timed("base", h, d, s, 0)) return 1;
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CK(hipStreamCreateWithPriority(&ph, hipStreamNonBlocking, hi));
+    CK(hipStreamCreateWithPriority(&pl, hipStreamNonBlocking, lo));
+    if (timed("F priority streams exist", h, d, s, 0)) return 1;
+    if (timed("F copy on the high-priority stream", h, d, ph, 0)) return 1;
+    CK(hipMalloc(&big, 8 * n + 4096));
+    if (timed("G source at 2.9 GB in a 3.3 GB allocation", h, (uint8_t *)big + 7 * n, s, 0)) return 1;
+    if (timed("H destination at +402 MB in a 1.2 GB registered region", (uint8_t *)h + n, d, s, 0)) return 1;
+    if (timed("H destination at +16 B", (uint8_t *)h + 16, d, s, 0)) return 1;
+    if (timed("I hipMemcpyDefault", h, d, s, 1)) return 1;
+    if (timed("I hipMemcpyDtoHAsync", h, d, s, 2)) return 1;
+    CK(hipHostUnregister(h));
+    free(h);
+    CK(hipFree(d));
+    CK(hipFree(big));
+    CK(hipFree(scratch));
+    return 0;
+}
+
+#ifndef D2H_PROBE_LIB
+int main() { return d2h_probe() || d2h_probe_engine_like(); }
+#endif

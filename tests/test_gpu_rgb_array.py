@@ -92,3 +92,19 @@ def test_rgb_array_jumper_jump_ellipse(kw):
     """jump-heavy actions, every frame checked: the translucent ellipse under the agent after a mid-air jump
     (jumper.cpp:163-166; in env 0 of the oracle at steps 9, 20, 38, 47 (easy) / 9, 21, 37, 55 (hard, uncentered))."""
     assert run_rgb_array("jumper", 8, 60, 1, seed=57, actions=[2, 5, 8, 1, 7], num_levels=0, rand_seed=41, **kw) == 61
+
+
+@pytest.mark.parametrize("chunks", ["1", "3", "64"])
+def test_rgb_array_chunks(chunks, monkeypatch):
+    """the frames render in PROCGEN_MI355X_HR_CHUNKS chunks, each DMA'd into the caller's page-locked
+    info["rgb"] array while the next renders (pg_capi.cpp copy_latent): one chunk, ragged chunks (7 envs in
+    3), more chunks than envs (empty ones skipped), single-game and mixed batches."""
+    monkeypatch.setenv("PROCGEN_MI355X_HR_CHUNKS", chunks)
+    assert run_rgb_array("coinrun", 7, 20, 10, seed=58, num_levels=0, rand_seed=42) == 3
+    env = make_gpu(6, "coinrun,maze,heist", render_mode="rgb_array", num_levels=0, rand_seed=43)
+    env.observe()
+    info = env.get_info()
+    for e in range(6):
+        orc = OracleEnv(("coinrun", "maze", "heist")[e % 3], 1, env_offset=e, num_levels=0, rand_seed=43)
+        np.testing.assert_array_equal(np.asarray(info[e]["rgb"]), orc.render_rgb_array(512)[0])
+    env.close()
