@@ -343,12 +343,19 @@ DEV void mt_twist_lds(uint32_t *mt) {
 }
 
 // std::mersenne_twister_engine::seed(s) into LDS (serial recurrence, uniform)
+// The recurrence runs on the scalar unit (the seed is made wave-uniform) and each word is selected into
+// its lane's register: 64 words per vector store instead of a masked LDS store per word.
 DEV void mt_seed_lds(uint32_t *mt, uint32_t s) {
-    uint32_t x = s;
-    if (LANE == 0) mt[0] = x;
-    for (int i = 1; i < PG_MT_N; i++) {
-        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
-        if (LANE == (i & 63)) mt[i] = x;
+    uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+    for (int base = 0; base < PG_MT_N; base += 64) {
+        int v = 0;
+#pragma unroll
+        for (int q = 0; q < 64; q++) {
+            const int i = base + q;
+            if (i > 0 && i < PG_MT_N) x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+            v = LANE == q ? (int)x : v;
+        }
+        if (base + LANE < PG_MT_N) mt[base + LANE] = (uint32_t)v;
     }
     wave_sync();
 }

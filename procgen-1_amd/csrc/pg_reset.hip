@@ -87,6 +87,10 @@ struct RCtx {
     size_t plane, eb;
     uint32_t *mt;    // LDS rand_gen words
     int32_t mti;
+    // the next draws, tempered, one per lane: lane k holds mt[wbase + k] (draw() reads it with readlane;
+    // a sweep that reads mt words itself and twists must call mt_window_reset)
+    uint32_t win;
+    int32_t wbase;
     int16_t *grid;   // LDS grid
     AgLds *ag;       // AssetGen scratch (use_generated_assets kernels only, else null)
 #ifdef PG_PROF_RESET
@@ -110,7 +114,25 @@ struct RCtx {
 DEV float &EF(RCtx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
 DEV int &EI(RCtx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
 
-DEV uint32_t draw(RCtx &c) { return mt_next_lds(c.mt, c.mti); }
+#define MT_WIN_NONE (-(1 << 20))
+DEV void mt_window_reset(RCtx &c) { c.wbase = MT_WIN_NONE; }
+// mt_next_lds with a register window: one LDS read + temper per 64 draws instead of a dependent LDS
+// read per draw (level generators draw serially: leaper's build loop, the maze generators, simple_choose)
+DEV uint32_t draw(RCtx &c) {
+    if (c.mti >= PG_MT_N) {
+        mt_twist_lds(c.mt);
+        c.mti = 0;
+        c.wbase = MT_WIN_NONE;
+    }
+    int k = c.mti - c.wbase;
+    if (k < 0 || k >= 64) {
+        c.wbase = c.mti;
+        k = 0;
+        c.win = c.mti + LANE < PG_MT_N ? mt_temper(c.mt[c.mti + LANE]) : 0u;
+    }
+    c.mti += 1;
+    return (uint32_t)__builtin_amdgcn_readlane((int)c.win, k);
+}
 struct RCtxRng { // the env's rand_gen as AssetGen's generator (AssetGen bggen(&rand_gen))
     RCtx *c;
     DEV uint32_t next() { return draw(*c); }
@@ -558,36 +580,77 @@ DEV void mg_generate_maze(RCtx &c, MG &g) { // :112-188
         }
         m->walls[k] = (uint32_t)x1 | ((uint32_t)y1 << 8) | ((uint32_t)x2 << 16) | ((uint32_t)y2 << 24);
     }
+    // The loop below keeps its state in registers (one dependent LDS read per wall instead of ~10):
+    //   the live-wall bitmap: lane w holds word w (walls.erase = clearing the bit, the n-th live wall =
+    //   the n-th set bit, which is what the reference's vector erase leaves at position n);
+    //   the set labels of the room cells (x, y even; the only cells whose labels are compared): room
+    //   cell r = (y / 2) * R + x / 2 in lane r % 64, register r / 64, labels = room-cell numbers (the
+    //   reference's cell indices, renamed: only their equality matters); merging s0 into s1 relabels
+    //   every member.  The wall list itself is the push-order formula above.
     const int words = (nw + 63) / 64;
-    for (int w = LANE; w < words; w += 64) {
-        int left = nw - w * 64;
-        m->alive[w] = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+    uint64_t aw = 0;
+    if (LANE < words) {
+        const int left = nw - LANE * 64;
+        aw = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
     }
-    wave_sync();
+    const int R = (md + 1) / 2;
+    constexpr int LS = (((MG_MAX_DIM + 1) / 2) * ((MG_MAX_DIM + 1) / 2) + 63) / 64;
+    int lab[LS];
+#pragma unroll
+    for (int j = 0; j < LS; j++) lab[j] = j * 64 + LANE;
+    auto label_of = [&](int r) { // uniform room cell -> its label
+        int v = lab[0];
+#pragma unroll
+        for (int j = 1; j < LS; j++)
+            if ((r >> 6) == j) v = lab[j];
+        return __builtin_amdgcn_readlane(v, r & 63);
+    };
+    int nfree = g.num_free;
     for (int rem = nw; rem > 0; rem--) {
-        int n = randn(c, rem);
-        int k = nth_alive(m->alive, words, n);
-        uint32_t wv = m->walls[k];
-        int x1 = wv & 255, y1 = (wv >> 8) & 255, x2 = (wv >> 16) & 255, y2 = wv >> 24;
-        int s0_idx = m->labels[md * y1 + x1];
-        int s1_idx = m->labels[md * y2 + x2];
-        int x0 = (x1 + x2) / 2, y0 = (y1 + y2) / 2;
-        int center = md * y0 + x0;
-        bool can_remove = (m->grid[(y0 + 1) * ad + (x0 + 1)] == WALL_OBJ) && (s0_idx != s1_idx);
-        wave_sync();
-        if (LANE == 0) m->alive[k >> 6] &= ~(1ull << (k & 63)); // walls.erase(walls.begin() + n)
-        if (can_remove) {
-            mg_set_free_cell(g, x1, y1);
-            mg_set_free_cell(g, x0, y0);
-            mg_set_free_cell(g, x2, y2);
-            // s1 |= s0 | {center}; every member relabelled s1_idx
-            for (int i = LANE; i < md * md; i += 64)
-                if (m->labels[i] == s0_idx) m->labels[i] = (int16_t)s1_idx;
-            wave_sync();
-            if (LANE == 0) m->labels[center] = (int16_t)s1_idx;
+        int n = randn(c, rem), k = -1;
+        for (int w = 0; w < words; w++) { // nth_alive over the register words
+            const uint64_t a = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)aw, w) |
+                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(aw >> 32), w) << 32);
+            const int cnt = __popcll(a);
+            if (n < cnt) {
+                const bool mine = ((a >> LANE) & 1ull) && __popcll(a & ((1ull << LANE) - 1ull)) == n;
+                k = w * 64 + (__ffsll((long long)ballot(mine)) - 1);
+                break;
+            }
+            n -= cnt;
         }
-        wave_sync();
+        if (LANE == (k >> 6)) aw &= ~(1ull << (k & 63)); // walls.erase(walls.begin() + n)
+        int x1, y1, x2, y2;
+        if (k < nw1) {
+            const int i = 2 * (k / B) + 1, j = 2 * (k % B);
+            x1 = i - 1; y1 = j; x2 = i + 1; y2 = j;
+        } else {
+            const int q = k - nw1, i = 2 * (q / A), j = 2 * (q % A) + 1;
+            x1 = i; y1 = j - 1; x2 = i; y2 = j + 1;
+        }
+        const int s0 = label_of((y1 / 2) * R + x1 / 2), s1 = label_of((y2 / 2) * R + x2 / 2);
+        const int x0 = (x1 + x2) / 2, y0 = (y1 + y2) / 2;
+        const bool can_remove = (m->grid[(y0 + 1) * ad + (x0 + 1)] == WALL_OBJ) && (s0 != s1);
+        if (can_remove) {
+            // set_free_cell (:26-34) of (x1, y1), (x0, y0), (x2, y2) in that order, by lane 0
+            if (LANE == 0) {
+                const int xs[3] = {x1, x0, x2}, ys[3] = {y1, y0, y2};
+                for (int q = 0; q < 3; q++) {
+                    const int cell = md * ys[q] + xs[q];
+                    m->grid[(ys[q] + 1) * ad + (xs[q] + 1)] = SPACE;
+                    if (!m->in_free[cell]) {
+                        m->free_cells[nfree++] = (int16_t)cell;
+                        m->in_free[cell] = 1;
+                    }
+                }
+            }
+            nfree = __shfl(nfree, 0);
+#pragma unroll
+            for (int j = 0; j < LS; j++) lab[j] = lab[j] == s0 ? s1 : lab[j]; // s1 |= s0
+            wave_sync();
+        }
     }
+    g.num_free = nfree;
 }
 
 DEV void mg_place_objects(RCtx &c, MG &g, int start_obj, int num_objs) { // :292-306
@@ -1813,6 +1876,7 @@ DEV void cf_random_fill(RCtx &c) { // rand01() < .5 ? WALL_OBJ : SPACE per cell,
         if (c.mti >= PG_MT_N) {
             mt_twist_lds(c.mt);
             c.mti = 0;
+            mt_window_reset(c);
         }
         int m = PG_MT_N - c.mti;
         if (m > 64) m = 64;
@@ -1898,66 +1962,52 @@ DEV void cf_update(RCtx &c, int iters, uint64_t path) {
 }
 
 // find_best_room (roomgen.cpp:116-136) -> label of the best room (cells with a[i] == label), or -1
-// Components by union-find on S->b (Playne & Hawick's lock-free merge: hook the larger root under
-// the smaller with atomicMin, retry on a lost race), so every root is its component's smallest cell
-// index -- the label the reference's flood fill order makes first (roomgen.cpp:116-136).
-DEV int cf_uf_find(const int32_t *L, int x) {
-    int p = L[x];
-    while (p != x) {
-        x = p;
-        p = L[x];
-    }
-    return x;
-}
-DEV void cf_uf_merge(int32_t *L, int a, int b) {
-    for (;;) {
-        a = cf_uf_find(L, a);
-        b = cf_uf_find(L, b);
-        if (a == b) return;
-        if (a > b) {
-            const int t = a;
-            a = b;
-            b = t;
-        }
-        const int old = atomicMin(&L[b], a); // b: the larger root
-        if (old == b) return;
-        b = old; // b was hooked meanwhile: merge with what it now points to
-    }
+// find_best_room (roomgen.cpp:116-136) on row masks: the rooms (4-connected SPACE components) are
+// flood-filled one at a time from their lowest-index cell (row masks, one dilation step per round,
+// until a round adds nothing); the largest room wins, ties to the one first in scan order (lowest
+// first cell), rooms of one cell never (fassert(best_room.size() > 0) -> -1).  The winner's rows go
+// to S->pm (cf_in_best); returns its first cell.
+DEV uint64_t cf_rl64(uint64_t v, int lane) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32);
 }
 DEV int cf_find_best_room(RCtx &c, CaveScratch *S) {
-    const int W = c.s.main_width, n = W * c.s.main_height;
-    int32_t *L = S->b;
-    for (int i = LANE; i < n; i += 64) L[i] = c.grid[i] == SPACE ? i : -1;
-    wave_sync();
-    for (int i = LANE; i < n; i += 64) {
-        if (L[i] < 0) continue;
-        const int x = i % W;
-        if (x > 0 && L[i - 1] >= 0) cf_uf_merge(L, i, i - 1);
-        if (i >= W && L[i - W] >= 0) cf_uf_merge(L, i, i - W);
-    }
-    wave_sync();
-    for (int i = LANE; i < n; i += 64) S->a[i] = (int16_t)(L[i] < 0 ? -1 : cf_uf_find(L, i));
-    wave_sync();
-    for (int i = LANE; i < n; i += 64) S->b[i] = 0;
-    wave_sync();
-    for (int i = LANE; i < n; i += 64)
-        if (S->a[i] >= 0) atomicAdd(&S->b[S->a[i]], 1);
-    wave_sync();
-    int best = -1; // key = size * 4096 + (4095 - label): largest room, first in scan order
-    for (int i = LANE; i < n; i += 64) {
-        if (S->a[i] == i) {
-            const int sz = S->b[i] >= 2 ? S->b[i] : 0;
-            const int key = sz * 4096 + (4095 - i);
-            if (key > best) best = key;
+    const int W = c.s.main_width, H = c.s.main_height;
+    const uint64_t sp = cf_row_of(c, [](int v) { return v == SPACE; });
+    uint64_t left = sp, best = 0;
+    int best_key = -1;
+    for (;;) {
+        const unsigned long long nz = ballot(left != 0);
+        if (!nz) break;
+        const int y0 = __ffsll((long long)nz) - 1, x0 = __builtin_ctzll(cf_rl64(left, y0)), seed = y0 * W + x0;
+        uint64_t f = LANE == y0 ? 1ull << x0 : 0ull;
+        for (;;) {
+            uint64_t up = cf_shfl64(f, LANE > 0 ? LANE - 1 : 0), dn = cf_shfl64(f, LANE < 63 ? LANE + 1 : 63);
+            if (LANE == 0) up = 0;
+            if (LANE >= H - 1) dn = 0;
+            const uint64_t nf = (f | (f << 1) | (f >> 1) | up | dn) & sp;
+            if (!ballot(nf != f)) break;
+            f = nf;
         }
+        int cnt = __popcll(f);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+        const int key = (cnt >= 2 ? cnt : 0) * 4096 + (4095 - seed);
+        if (key > best_key) {
+            best_key = key;
+            best = f;
+        }
+        left &= ~f;
     }
-    for (int off = 32; off >= 1; off >>= 1) {
-        const int o = __shfl_xor(best, off);
-        if (o > best) best = o;
-    }
+    S->pm[2 * LANE] = (uint32_t)best;
+    S->pm[2 * LANE + 1] = (uint32_t)(best >> 32);
     wave_sync();
-    if (best < 4096) return -1; // no room or only isolated cells: fassert(best_room.size() > 0)
-    return 4095 - (best & 4095);
+    if (best_key < 4096) return -1;
+    return 4095 - (best_key & 4095);
+}
+DEV bool cf_in_best(const CaveScratch *S, int W, int i) {
+    const int x = i % W, y = i / W;
+    return (S->pm[2 * y + (x >> 5)] >> (x & 31)) & 1u;
 }
 
 // find_path (roomgen.cpp:72-114): writes the path's cells (any order) to S->list2, returns its length
@@ -2088,7 +2138,7 @@ DEV void caveflyer_game_reset(RCtx &c, CaveScratch *S) {
     int nfree = 0;
     for (int base = 0; base < n; base += 64) {
         const int i = base + LANE;
-        const bool in = i < n && S->a[i] == best;
+        const bool in = i < n && cf_in_best(S, W, i);
         if (i < n) {
             c.grid[i] = in ? SPACE : WALL_OBJ;
             S->f[i] = 0;
@@ -2213,6 +2263,82 @@ DEV void jp_ordered_scan(RCtx &c, int n, P pred, A act) {
     }
 }
 
+// The two in-order scans of jumper.cpp:305-337 on row masks (lane y = row y, cf_row_of): the predicate
+// of every cell is a mask expression, re-evaluated after each change, and the scan walks its set bits
+// in index order (row-major), so every cell is tested against the grid the serial loop would show it.
+//   spikes: is_space_on_ground at x - 1, x, x + 1 (space here and above, below CAVEWALL or out of bounds);
+//           one rand01 per site, SPIKE placed below spike_prob
+//   walls:  a 3-high left / right wall run at (x, y): one randn(3) per hit, cell (x, y + r) opened (once
+//           a left run is broken the right run through the same cells is gone, so the reference's second
+//           test is false whenever the first was true)
+DEV uint64_t jp_rl64(uint64_t v, int lane) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32);
+}
+DEV void jp_scans(RCtx &c, float spike_prob) {
+    const int W = c.s.main_width, H = c.s.main_height, oob = c.s.out_of_bounds_object;
+    const uint64_t full = cf_row_full(W);
+    uint64_t sp = cf_row_of(c, [](int v) { return v == SPACE; });
+    uint64_t cw = cf_row_of(c, [](int v) { return v == JP_CAVEWALL; });
+    const uint64_t ground = cf_row_of(c, [oob](int v) { return v == JP_CAVEWALL || v == oob; });
+    const bool oob_space = oob == SPACE; // below row 0 is out of bounds: ground by definition
+    auto row_at = [&](uint64_t v, int dy, uint64_t outside) { // row LANE + dy, `outside` beyond the grid
+        const int src = LANE + dy;
+        const uint64_t r = cf_shfl64(v, src < 0 ? 0 : (src > 63 ? 63 : src));
+        return (src < 0 || src >= H) ? outside : r;
+    };
+    auto sites = [&]() {
+        const uint64_t sog = sp & row_at(sp, 1, oob_space ? full : 0) & row_at(ground, -1, full);
+        const uint64_t edge_l = oob_space ? 1ull : 0ull, edge_r = oob_space ? 1ull << (W - 1) : 0ull; // never: oob is a wall
+        return LANE < H ? sog & ((sog << 1) | edge_l) & ((sog >> 1) | edge_r) & full : 0ull;
+    };
+    // scan 1: spikes.  A SPIKE leaves the SPACE mask (ground is unchanged: the cell was SPACE)
+    uint64_t pm = sites();
+    for (int y = 0, from = 0; y < H;) {
+        const uint64_t m = jp_rl64(pm, y) & (from >= 64 ? 0ull : ~0ull << from);
+        if (!m) {
+            y++;
+            from = 0;
+            continue;
+        }
+        const int x = __builtin_ctzll(m);
+        if (rand01(c) < spike_prob) {
+            set_obj(c, x, y, JP_SPIKE);
+            if (LANE == y) sp &= ~(1ull << x);
+            pm = sites();
+        }
+        from = x + 1;
+    }
+    // scan 2: long walls
+    auto runs = [&]() {
+        const uint64_t spo = oob_space ? 1ull << (W - 1) : 0ull;
+        const uint64_t lw = cw & ((sp >> 1) | spo), rw = cw & ((sp << 1) | (oob_space ? 1ull : 0ull)) & full;
+        const uint64_t cwo = oob == JP_CAVEWALL ? full : 0ull; // rows beyond the grid: walls only if oob is
+        const uint64_t lwo = cwo & (oob_space ? full : 0ull);  // (never a run: oob is not both wall and space)
+        const uint64_t lr = lw & row_at(lw, 1, lwo) & row_at(lw, 2, lwo);
+        const uint64_t rr = rw & row_at(rw, 1, lwo) & row_at(rw, 2, lwo);
+        return LANE < H ? lr | rr : 0ull;
+    };
+    uint64_t pr = runs();
+    for (int y = 0, from = 0; y < H;) {
+        const uint64_t m = jp_rl64(pr, y) & (from >= 64 ? 0ull : ~0ull << from);
+        if (!m) {
+            y++;
+            from = 0;
+            continue;
+        }
+        const int x = __builtin_ctzll(m);
+        const int yy = y + randn(c, 3); // left run, else right run: one opening either way
+        set_obj(c, x, yy, SPACE);
+        if (LANE == yy) {
+            sp |= 1ull << x;
+            cw &= ~(1ull << x);
+        }
+        pr = runs();
+        from = x + 1;
+    }
+}
+
 DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
     const int dm = c.s.opt_distribution_mode;
     auto &J = c.s.gs.jp;
@@ -2255,6 +2381,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
         if (c.mti >= PG_MT_N) {
             mt_twist_lds(c.mt);
             c.mti = 0;
+            mt_window_reset(c);
         }
         int m = PG_MT_N - c.mti;
         if (m > 64) m = 64;
@@ -2285,7 +2412,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
     int nfree = 0;
     for (int base = 0; base < n; base += 64) {
         const int i = base + LANE;
-        const bool in = i < n && S->a[i] == best;
+        const bool in = i < n && cf_in_best(S, W, i);
         if (i < n) {
             c.grid[i] = in ? SPACE : JP_CAVEWALL;
             S->f[i] = 0;
@@ -2318,14 +2445,7 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
     RMARK(c, 4);
     add_entity(c, (float)((goal_cell % W) + .5), (float)((goal_cell / W) + .5), 0, 0, .5f, JP_GOAL); // entity 1
     const float spike_prob = dm == PG_MEMORY ? 0 : .2f;
-    jp_ordered_scan(c, n, [&](int x, int y) { return jp_spike_site(c, x, y); }, [&](int x, int y) {
-        if (rand01(c) < spike_prob) set_obj(c, x, y, JP_SPIKE);
-    });
-    jp_ordered_scan(c, n, [&](int x, int y) { return jp_left_run(c, x, y) || jp_right_run(c, x, y); },
-                    [&](int x, int y) { // :325-337, left then right against the updated grid
-                        if (jp_left_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
-                        if (jp_right_run(c, x, y)) set_obj(c, x, y + randn(c, 3), SPACE);
-                    });
+    jp_scans(c, spike_prob);
     RMARK(c, 5);
     EF(c, F_X, 0) = (float)((agent_cell % W) + .5);
     EF(c, F_Y, 0) = (float)(agent_cell / W) + EF(c, F_RY, 0);
@@ -2582,41 +2702,94 @@ DEV void leaper_game_reset(RCtx &c, LeaperScratch *L) {
         c.s.water_lane_speeds[k] = k < c.s.num_water_lanes ? L->water[k] : 0.0f;
     }
 
-    // initial entities: spawn_entities + step_entities (no erase) while i < main_width / min(speed)
+    RMARK(c, 0);
+    // initial entities: spawn_entities + step_entities (no erase) while i < main_width / min(speed).
+    // The loop runs ~400 times with a draw per lane: the entities' x / vx / y / rx / ry live in registers
+    // (entity k in lane k % 64, slot k / 64), the lane speeds in scalars, so an iteration touches no LDS;
+    // a push also records the entity in the LDS lists for the write-out below
+    constexpr int NS = PG_CAP / 64;
+    float ex[NS], evx[NS], ey[NS], erx[NS], ery[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) ex[j] = evx[j] = ey[j] = erx[j] = ery[j] = 0.0f;
     int n = 0;
     bool overflow = false;
-    lp_push(L, n, PG_CAP - 1, EF(c, F_X, 0), EF(c, F_Y, 0), 0, EF(c, F_RX, 0), EF(c, F_RY, 0), PLAYER, 0, 0, overflow);
+    auto push = [&](float x, float y, float vx, float rx, float ry, int type, int theme, int born) {
+        if (n >= PG_CAP - 1) {
+            overflow = true;
+            return;
+        }
+#pragma unroll
+        for (int j = 0; j < NS; j++)
+            if (j == (n >> 6) && LANE == (n & 63)) {
+                ex[j] = x; evx[j] = vx; ey[j] = y; erx[j] = rx; ery[j] = ry;
+            }
+        if (LANE == 0) {
+            L->x[n] = x; L->y[n] = y; L->vx[n] = vx; L->rx[n] = rx; L->ry[n] = ry;
+            L->type[n] = (int8_t)type; L->theme[n] = (int8_t)theme; L->born[n] = (int16_t)born;
+        }
+        n++;
+    };
+    auto collides = [&](float x, float y, float rx, float ry) { // has_any_collision (no entity avoids it)
+        bool hit = false;
+#pragma unroll
+        for (int j = 0; j < NS; j++)
+            if (j * 64 < n && j * 64 + LANE < n) {
+                const float tx = (rx + erx[j]) + 0.0f, ty = (ry + ery[j]) + 0.0f;
+                if ((fabsf(x - ex[j]) < tx) && (fabsf(y - ey[j]) < ty)) hit = true;
+            }
+        return ballot(hit) != 0;
+    };
+    push(EF(c, F_X, 0), EF(c, F_Y, 0), 0, EF(c, F_RX, 0), EF(c, F_RY, 0), PLAYER, 0, 0);
     const float mn = min_car_speed < min_log_speed ? min_car_speed : min_log_speed;
     const int ncar_themes = c.d.num_themes[LP_CAR];
+    // c.s is the LDS copy of the env: everything the loop reads from it goes to registers first
+    const int nroad = c.s.num_road_lanes, nwater = c.s.num_water_lanes;
+    const int road_y = c.s.bottom_road_y, water_y = c.s.bottom_water_y;
+    float rsp[5], wsp[5], rpr[5], wpr[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        rsp[k] = c.s.road_lane_speeds[k];
+        wsp[k] = c.s.water_lane_speeds[k];
+        rpr[k] = (float)(fabs((double)rsp[k]) / 6.0);
+        wpr[k] = (float)(fabs((double)wsp[k]) / 2.0);
+    }
     int iters = 0;
     for (int i = 0; (float)i < w / mn; i++) {
-        for (int lane = 0; lane < c.s.num_road_lanes; lane++) {
-            const float speed = L->road[lane];
-            const float spawn_prob = (float)(fabs((double)speed) / 6.0);
+#pragma unroll
+        for (int lane = 0; lane < 5; lane++) {
+            if (lane >= nroad) break;
+            const float speed = rsp[lane], spawn_prob = rpr[lane];
             if (rand01(c) < spawn_prob) {
                 const float x = speed > 0 ? (-1 * LP_MONSTER_RADIUS) : (w + LP_MONSTER_RADIUS);
-                const float y = (float)(c.s.bottom_road_y + lane + 0.5);
+                const float y = (float)(road_y + lane + 0.5);
                 const int theme = randn(c, ncar_themes); // choose_random_theme before the check
-                if (!lp_collides(L, n, x, y, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS))
-                    lp_push(L, n, PG_CAP - 1, x, y, speed, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS, LP_CAR, theme, i,
-                            overflow);
+                if (!collides(x, y, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS))
+                    push(x, y, speed, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS, LP_CAR, theme, i);
             }
         }
-        for (int lane = 0; lane < c.s.num_water_lanes; lane++) {
-            const float speed = L->water[lane];
-            const float spawn_prob = (float)(fabs((double)speed) / 2.0);
+#pragma unroll
+        for (int lane = 0; lane < 5; lane++) {
+            if (lane >= nwater) break;
+            const float speed = wsp[lane], spawn_prob = wpr[lane];
             if (rand01(c) < spawn_prob) {
                 const float x = speed > 0 ? (-1 * LP_LOG_RADIUS) : (w + LP_LOG_RADIUS);
-                const float y = (float)(c.s.bottom_water_y + lane + 0.5);
-                if (!lp_collides(L, n, x, y, LP_LOG_RADIUS, LP_LOG_RADIUS))
-                    lp_push(L, n, PG_CAP - 1, x, y, speed, LP_LOG_RADIUS, LP_LOG_RADIUS, LP_LOG, 0, i, overflow);
+                const float y = (float)(water_y + lane + 0.5);
+                if (!collides(x, y, LP_LOG_RADIUS, LP_LOG_RADIUS))
+                    push(x, y, speed, LP_LOG_RADIUS, LP_LOG_RADIUS, LP_LOG, 0, i);
             }
         }
         // Entity::step of every non-smart entity: x += vx (vy = 0); the agent (smart, at rest) stays
-        for (int k = 1 + LANE; k < n; k += 64) L->x[k] = L->x[k] + L->vx[k];
-        wave_sync();
+#pragma unroll
+        for (int j = 0; j < NS; j++)
+            if (j * 64 < n && j * 64 + LANE < n && j * 64 + LANE >= 1) ex[j] = ex[j] + evx[j];
         iters++;
     }
+    wave_sync(); // the pushes' LDS records
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+        if (j * 64 + LANE < n) L->x[j * 64 + LANE] = ex[j];
+    wave_sync();
+    RMARK(c, 1);
     if (overflow) c.s.error = PG_ERR_ENTITY_OVERFLOW;
     // the list to HBM: Entity ctor defaults (entity.cpp:8-47) + what the build set
     for (int k = 1 + LANE; k < n; k += 64) {
@@ -2680,6 +2853,7 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     wave_sync();
     mt_seed_lds(lds_mt, (uint32_t)c.s.current_level_seed);
     c.mti = PG_MT_N;
+    mt_window_reset(c);
     if constexpr (G == PG_GAME_COINRUN) coinrun_game_reset(c);
     if constexpr (G == PG_GAME_BIGFISH) bigfish_game_reset(c);
     if constexpr (G == PG_GAME_MAZE) maze_game_reset(c, &scratch->mg);

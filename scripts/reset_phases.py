@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Level-generation phases of the reset kernel (diagnostic build, make -C procgen-1_amd/csrc
 VARIANT=rprof ONLY=pg_reset.hip EXTRA=-DPG_PROF_RESET): average s_memtime cycles per reset of each
-phase that pg_reset.hip's RMARK stamps (caveflyer / jumper), over the resets of a device-resident
+phase that pg_reset.hip's RMARK stamps (caveflyer / jumper / leaper), over the resets of a device-resident
 run.  Phase shares only: never quote this build's wall time."""
 import json
 import os
@@ -17,6 +17,7 @@ import torch  # noqa: E402
 PHASES = {
     "caveflyer": ["preamble", "fill+4 updates", "best room (+free list, picks)", "find_path", "expand+4 updates",
                   "object placement", "tail", "write-back"],
+    "leaper": ["preamble+lanes", "build loop (spawn + step)", "-", "-", "-", "-", "entities to HBM+tail", "write-back"],
     "jumper": ["maze (no dead ends)", "fill+2 updates+border", "best room+free list+candidates", "find_path",
                "expand", "ordered scans", "preamble+tail", "write-back"],
 }
@@ -45,5 +46,5 @@ def main(game, num=4096, steps=200):
 
 
 if __name__ == "__main__":
-    for g in (sys.argv[1:] or ["jumper", "caveflyer"]):
+    for g in (sys.argv[1:] or ["jumper", "caveflyer", "leaper"]):
         main(g)
