@@ -1127,16 +1127,31 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
         // shard 16.5 -> 18.7 M env-steps/s, profiles/r03/r03_q_mixed16*.json); 16 = one per game
         if (ns < (int)nchains) {
             // per-game chain cost, ms at 4,096 envs (step + reset + render per game inside the all-16 mixed
-            // shard, profiles/r04/r04_l_mixed/mixed16_default.json per_game)
+            // shard, profiles/r04/r04_l_mixed/mixed16_default.json per_game).  The round-5 generators
+            // changed the costs (r05_q_mixed16.json), but packing on the new table measured slower on one
+            // box (24.1-24.3 vs 24.5-24.7 M; render weighted 1.5x / 2x, reset 0.5x: 23.8-24.7 M,
+            // profiles/r05/r05_r_packing.txt): the chains contend for CUs, so isolated costs are not the
+            // objective.  This table stays.
             static const float cost0[PG_NUM_GAMES] = {0.21f, 0.85f, 1.13f, 0.67f, 0.46f, 0.50f, 0.66f, 0.74f,
                                                       0.49f, 1.45f, 0.99f, 0.51f, 0.51f, 0.47f, 0.35f, 0.67f};
             // inband prefetch (PROCGEN_MI355X_PREFETCH_INBAND=1 with PROCGEN_MI355X_PREFETCH_GAMES): a
             // prefetched chain's reset becomes a swap and its level generation (reset_cost, r05 mixed16
             // per_game) one job packed after every chain of the least loaded stream
-            static const float reset_cost[PG_NUM_GAMES] = {0.07f, 0.06f, 0.66f, 0.18f, 0.08f, 0.09f, 0.08f, 0.20f,
-                                                           0.24f, 0.96f, 0.57f, 0.20f, 0.09f, 0.09f, 0.06f, 0.33f};
+            static const float reset_cost[PG_NUM_GAMES] = {0.10f, 0.05f, 0.18f, 0.16f, 0.07f, 0.08f, 0.08f, 0.21f,
+                                                           0.18f, 0.37f, 0.40f, 0.28f, 0.10f, 0.08f, 0.07f, 0.31f};
             float cost[PG_NUM_GAMES];
             for (int g = 0; g < PG_NUM_GAMES; g++) cost[g] = cost0[g];
+            // PROCGEN_MI355X_MIXED_COSTS: 16 comma-separated chain costs in game-id order (experiments)
+            if (const char *mc = getenv("PROCGEN_MI355X_MIXED_COSTS")) {
+                const char *q = mc;
+                for (int g = 0; g < PG_NUM_GAMES && *q; g++) {
+                    char *e = nullptr;
+                    const float x = strtof(q, &e);
+                    if (e == q) break;
+                    cost[g] = x;
+                    q = *e == ',' ? e + 1 : e;
+                }
+            }
             const char *ib = getenv("PROCGEN_MI355X_PREFETCH_INBAND"), *ipg = getenv("PROCGEN_MI355X_PREFETCH_GAMES");
             v->inband = ib && ib[0] == '1' && ipg && ipg[0];
             float gen_cost = 0.f;
@@ -1151,7 +1166,7 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
                         a = b + 1;
                     }
                     if (on) {
-                        cost[g] = cost0[g] - reset_cost[g] + 0.05f; // the swap
+                        cost[g] = cost[g] - reset_cost[g] + 0.05f; // the swap
                         gen_cost += reset_cost[g];
                     }
                 }

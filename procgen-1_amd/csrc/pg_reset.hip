@@ -2482,23 +2482,57 @@ DEV void jumper_game_reset(RCtx &c, Scratch<PG_GAME_JUMPER> *X) {
 // after the scan position in the current grid (ballot), opens one of its walls, and resumes.
 DEV void mg_generate_maze_no_dead_ends(RCtx &c, MG &g) {
     mg_generate_maze(c, g);
-    const int cells = g.ad * g.ad;
-    int start = 0;
-    while (start < cells) {
-        int found = -1;
-        for (int base = start & ~63; base < cells; base += 64) {
-            int i = base + LANE;
-            bool de = i >= start && i < cells && mg_get_obj(g, i) == SPACE && mg_count_neighbors(g, i, SPACE) == 1;
-            unsigned long long b = ballot(de);
-            if (b) {
-                found = base + __ffsll((long long)b) - 1;
-                break;
-            }
+    // On row masks of the maze grid (lane y = row y, array_dim <= 33): mg_get_obj is INVALID_OBJ on
+    // the border, so only interior cells count as SPACE / WALL neighbours.  A dead end is an interior
+    // SPACE cell with exactly one SPACE neighbour; the scan walks them in index order against the
+    // current grid (the masks are re-derived after every opened wall), opening the randn(nw)-th WALL
+    // neighbour in get_neighbors order (-1, 0) (0, -1) (0, 1) (1, 0).
+    const int ad = g.ad;
+    const uint64_t inner = LANE >= 1 && LANE < ad - 1 ? ((1ull << (ad - 1)) - 1ull) & ~1ull : 0ull;
+    uint64_t sp = 0, wl = 0;
+    if (LANE < ad)
+        for (int x = 0; x < ad; x++) {
+            const int v = g.m->grid[LANE * ad + x];
+            sp |= (uint64_t)(v == SPACE) << x;
+            wl |= (uint64_t)(v == WALL_OBJ) << x;
         }
-        if (found < 0) break;
-        const int nw = mg_count_neighbors(g, found, WALL_OBJ);
-        if (nw > 0) mg_set_index(g, mg_nth_neighbor(g, found, WALL_OBJ, randn(c, nw)), SPACE);
-        start = found + 1;
+    sp &= inner;
+    wl &= inner;
+    auto row_of = [&](uint64_t v, int dy) {
+        const int src = LANE + dy;
+        const uint64_t r = cf_shfl64(v, src < 0 ? 0 : (src > 63 ? 63 : src));
+        return (src < 0 || src >= ad) ? 0ull : r;
+    };
+    auto dead_ends = [&]() {
+        const uint64_t a = sp << 1, b = row_of(sp, -1), d = row_of(sp, 1), e = sp >> 1;
+        const uint64_t odd = a ^ b ^ d ^ e, two = (a & b) | (d & e) | ((a | b) & (d | e));
+        return sp & odd & ~two;
+    };
+    uint64_t de = dead_ends();
+    for (int y = 0, from = 0; y < ad;) {
+        const uint64_t m = cf_rl64(de, y) & (from >= 64 ? 0ull : ~0ull << from);
+        if (!m) {
+            y++;
+            from = 0;
+            continue;
+        }
+        const int x = __builtin_ctzll(m);
+        const uint64_t wr = cf_rl64(wl, y), wu = y > 0 ? cf_rl64(wl, y - 1) : 0ull, wd = cf_rl64(wl, y + 1);
+        const bool nb[4] = {((wr >> (x - 1)) & 1) != 0, ((wu >> x) & 1) != 0, ((wd >> x) & 1) != 0, ((wr >> (x + 1)) & 1) != 0};
+        const int nw = nb[0] + nb[1] + nb[2] + nb[3];
+        if (nw > 0) {
+            int n = randn(c, nw), k = 0;
+            for (; k < 4; k++)
+                if (nb[k] && n-- == 0) break;
+            const int ox = x + (k == 0 ? -1 : (k == 3 ? 1 : 0)), oy = y + (k == 1 ? -1 : (k == 2 ? 1 : 0));
+            mg_set_index(g, oy * ad + ox, SPACE);
+            if (LANE == oy) {
+                sp |= 1ull << ox;
+                wl &= ~(1ull << ox);
+            }
+            de = dead_ends();
+        }
+        from = x + 1;
     }
 }
 
