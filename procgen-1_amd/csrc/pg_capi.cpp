@@ -445,6 +445,7 @@ int upload_atlas(VecEnv *v, const uint32_t *pixels, int64_t num_pixels, const pg
                  const pg_image *backgrounds, const int32_t *num_backgrounds, const int32_t *num_themes);
 int copy_latent(VecEnv *v);
 int copy_latent_grid(VecEnv *v);
+static hipError_t d2h_registered(void *dst, const void *src, size_t n, hipStream_t s);
 
 int fail(VecEnv *v, int code, const char *msg) {
     if (v && !v->error) {
@@ -642,8 +643,8 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
             const size_t k = (i + 1) % C;
             const size_t lo = (size_t)v->chain_lo(k) * PG_OBS_BYTES;
             HIPCHECK(hipStreamWaitEvent(v->cstream, v->ev_rendered[k], 0));
-            HIPCHECK(hipMemcpyAsync((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo,
-                                    (size_t)v->chain_count(k) * PG_OBS_BYTES, hipMemcpyDeviceToHost, v->cstream));
+            HIPCHECK(d2h_registered((uint8_t *)v->registered[0] + lo, v->dev.rgb + lo,
+                                    (size_t)v->chain_count(k) * PG_OBS_BYTES, v->cstream));
         }
         v->obs_inflight = true;
     }
@@ -662,6 +663,25 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     v->act_no++;
     HIPCHECK(hipGetLastError());
     return 0;
+}
+
+// Device -> page-locked (hipHostRegister'd) host copy.  Inside the engine the runtime carried these
+// as copyBuffer blit kernels that hold CUs for the whole transfer (the same copy in a probe
+// process goes to SDMA, scripts/d2h_probe2.hip), so PROCGEN_MI355X_D2H_NOCU=1 issues them as
+// hipMemcpyDeviceToDeviceNoCU (the registered host pointer is device-addressable): a copy that may not
+// use compute units.  Falls back to the plain device -> host kind if the runtime refuses it.
+static hipError_t d2h_registered(void *dst, const void *src, size_t n, hipStream_t s) {
+    static int nocu = -1;
+    if (nocu < 0) {
+        const char *e = getenv("PROCGEN_MI355X_D2H_NOCU");
+        nocu = e && e[0] == '1';
+    }
+    if (nocu) {
+        if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, s) == hipSuccess) return hipSuccess;
+        (void)hipGetLastError();
+        nocu = 0;
+    }
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
 }
 
 // Host memcpy, split over a few threads for large frames (805 MB at 65,536 envs).
@@ -732,13 +752,13 @@ int copy_out(VecEnv *v) {
     const size_t n = (size_t)v->num_envs;
     if (v->direct) {
         if (!v->obs_inflight) // else the act's chains issued the obs DMA part by part (launch_step)
-            HIPCHECK(hipMemcpyAsync(v->registered[0], v->dev.rgb, PG_OBS_BYTES * n, hipMemcpyDeviceToHost, v->stream));
+            HIPCHECK(d2h_registered(v->registered[0], v->dev.rgb, PG_OBS_BYTES * n, v->stream));
         v->obs_inflight = false;
-        HIPCHECK(hipMemcpyAsync(v->registered[1], v->dev.rew, 4 * n, hipMemcpyDeviceToHost, v->stream));
-        HIPCHECK(hipMemcpyAsync(v->registered[2], v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
-        HIPCHECK(hipMemcpyAsync(v->registered[3], v->dev.prev_level_seed, 4 * n, hipMemcpyDeviceToHost, v->stream));
-        HIPCHECK(hipMemcpyAsync(v->registered[4], v->dev.prev_level_complete, n, hipMemcpyDeviceToHost, v->stream));
-        HIPCHECK(hipMemcpyAsync(v->registered[5], v->dev.level_seed, 4 * n, hipMemcpyDeviceToHost, v->stream));
+        HIPCHECK(d2h_registered(v->registered[1], v->dev.rew, 4 * n, v->stream));
+        HIPCHECK(d2h_registered(v->registered[2], v->dev.first, n, v->stream));
+        HIPCHECK(d2h_registered(v->registered[3], v->dev.prev_level_seed, 4 * n, v->stream));
+        HIPCHECK(d2h_registered(v->registered[4], v->dev.prev_level_complete, n, v->stream));
+        HIPCHECK(d2h_registered(v->registered[5], v->dev.level_seed, 4 * n, v->stream));
         HIPCHECK(hipStreamSynchronize(v->stream));
         return copy_latent(v);
     }
@@ -803,13 +823,12 @@ int copy_latent(VecEnv *v) {
                     HIPCHECK(hipEventRecord(v->hr_ev[j], v->hstream));
                     HIPCHECK(hipStreamWaitEvent(v->stream, v->hr_ev[j], 0));
                     if (v->games.size() == 1) {
-                        HIPCHECK(hipMemcpyAsync(dst + lo * per * 3, v->hr_rgb + lo * per * 3, (hi - lo) * per * 3,
-                                                hipMemcpyDeviceToHost, v->stream));
+                        HIPCHECK(d2h_registered(dst + lo * per * 3, v->hr_rgb + lo * per * 3, (hi - lo) * per * 3,
+                                                v->stream));
                     } else {
                         for (size_t q = lo; q < hi; q++)
-                            HIPCHECK(hipMemcpyAsync(dst + (size_t)v->h_lists[k * cnt + q] * per * 3,
-                                                    v->hr_rgb + (k * cnt + q) * per * 3, per * 3, hipMemcpyDeviceToHost,
-                                                    v->stream));
+                            HIPCHECK(d2h_registered(dst + (size_t)v->h_lists[k * cnt + q] * per * 3,
+                                                    v->hr_rgb + (k * cnt + q) * per * 3, per * 3, v->stream));
                     }
                 }
             HIPCHECK(hipStreamSynchronize(v->stream));
