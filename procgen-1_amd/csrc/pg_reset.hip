@@ -605,6 +605,13 @@ DEV void mg_generate_maze(RCtx &c, MG &g) { // :112-188
             if ((r >> 6) == j) v = lab[j];
         return __builtin_amdgcn_readlane(v, r & 63);
     };
+    // the packed wall list (x1 | y1 << 8 | x2 << 16 | y2 << 24) in registers: wall k in lane k % 64
+    constexpr int WS = MG_MAX_WALLS / 64;
+    uint32_t wreg[WS];
+#pragma unroll
+    for (int j = 0; j < WS; j++) wreg[j] = j * 64 + LANE < nw ? m->walls[j * 64 + LANE] : 0u;
+    int freed = 0; // bit j: room cell j * 64 + LANE is in free_cell_set
+    auto freed_of = [&](int r) { return (__builtin_amdgcn_readlane(freed, r & 63) >> (r >> 6)) & 1; };
     int nfree = g.num_free;
     for (int rem = nw; rem > 0; rem--) {
         int n = randn(c, rem), k = -1;
@@ -620,31 +627,33 @@ DEV void mg_generate_maze(RCtx &c, MG &g) { // :112-188
             n -= cnt;
         }
         if (LANE == (k >> 6)) aw &= ~(1ull << (k & 63)); // walls.erase(walls.begin() + n)
-        int x1, y1, x2, y2;
-        if (k < nw1) {
-            const int i = 2 * (k / B) + 1, j = 2 * (k % B);
-            x1 = i - 1; y1 = j; x2 = i + 1; y2 = j;
-        } else {
-            const int q = k - nw1, i = 2 * (q / A), j = 2 * (q % A) + 1;
-            x1 = i; y1 = j - 1; x2 = i; y2 = j + 1;
-        }
-        const int s0 = label_of((y1 / 2) * R + x1 / 2), s1 = label_of((y2 / 2) * R + x2 / 2);
+        uint32_t wv = wreg[0];
+#pragma unroll
+        for (int j = 1; j < WS; j++)
+            if ((k >> 6) == j) wv = wreg[j];
+        wv = (uint32_t)__builtin_amdgcn_readlane((int)wv, k & 63);
+        const int x1 = wv & 255, y1 = (wv >> 8) & 255, x2 = (wv >> 16) & 255, y2 = wv >> 24;
+        const int r1 = (y1 / 2) * R + x1 / 2, r2 = (y2 / 2) * R + x2 / 2;
+        const int s0 = label_of(r1), s1 = label_of(r2);
         const int x0 = (x1 + x2) / 2, y0 = (y1 + y2) / 2;
-        const bool can_remove = (m->grid[(y0 + 1) * ad + (x0 + 1)] == WALL_OBJ) && (s0 != s1);
-        if (can_remove) {
-            // set_free_cell (:26-34) of (x1, y1), (x0, y0), (x2, y2) in that order, by lane 0
+        // the reference also requires the wall cell to be WALL_OBJ: it always is here (a wall cell is
+        // only ever opened by its own wall, which is erased when picked)
+        if (s0 != s1) {
+            // set_free_cell (:26-34) of (x1, y1), (x0, y0), (x2, y2) in that order: the wall cell is
+            // never in the set yet, the room cells' membership is the `freed` bits
+            const bool new1 = !freed_of(r1), new2 = !freed_of(r2);
             if (LANE == 0) {
-                const int xs[3] = {x1, x0, x2}, ys[3] = {y1, y0, y2};
-                for (int q = 0; q < 3; q++) {
-                    const int cell = md * ys[q] + xs[q];
-                    m->grid[(ys[q] + 1) * ad + (xs[q] + 1)] = SPACE;
-                    if (!m->in_free[cell]) {
-                        m->free_cells[nfree++] = (int16_t)cell;
-                        m->in_free[cell] = 1;
-                    }
-                }
+                m->grid[(y1 + 1) * ad + (x1 + 1)] = SPACE;
+                m->grid[(y0 + 1) * ad + (x0 + 1)] = SPACE;
+                m->grid[(y2 + 1) * ad + (x2 + 1)] = SPACE;
+                int q = nfree;
+                if (new1) m->free_cells[q++] = (int16_t)(md * y1 + x1);
+                m->free_cells[q++] = (int16_t)(md * y0 + x0);
+                if (new2) m->free_cells[q] = (int16_t)(md * y2 + x2);
             }
-            nfree = __shfl(nfree, 0);
+            nfree += (int)new1 + 1 + (int)new2;
+            if (LANE == (r1 & 63)) freed |= 1 << (r1 >> 6);
+            if (LANE == (r2 & 63)) freed |= 1 << (r2 >> 6);
 #pragma unroll
             for (int j = 0; j < LS; j++) lab[j] = lab[j] == s0 ? s1 : lab[j]; // s1 |= s0
             wave_sync();
@@ -2787,8 +2796,36 @@ DEV void leaper_game_reset(RCtx &c, LeaperScratch *L) {
         rpr[k] = (float)(fabs((double)rsp[k]) / 6.0);
         wpr[k] = (float)(fabs((double)wsp[k]) / 2.0);
     }
+    // lane j's spawn probability (road lanes, then water lanes) for the speculative pass below
+    float pj = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        if (LANE == q && q < nroad) pj = rpr[q];
+        if (LANE == nroad + q && q < nwater) pj = wpr[q];
+    }
+    const int m = nroad + nwater;
     int iters = 0;
     for (int i = 0; (float)i < w / mn; i++) {
+        // Speculative pass: an iteration draws one rand01 per lane in lane order, plus a theme draw
+        // after each car spawn.  Lane j tests draw mti + j from the register window at once; when no
+        // lane spawns (most iterations) that is exactly the serial outcome and the m draws are consumed;
+        // otherwise the iteration runs serially below from the same mti.
+        if (c.mti + m <= PG_MT_N) {
+            if (c.mti - c.wbase < 0 || c.mti - c.wbase + m > 64) {
+                c.wbase = c.mti;
+                c.win = c.mti + LANE < PG_MT_N ? mt_temper(c.mt[c.mti + LANE]) : 0u;
+            }
+            const int src = c.mti - c.wbase + LANE;
+            const uint32_t wj = (uint32_t)__shfl((int)c.win, src < 64 ? src : 63);
+            if (!ballot(LANE < m && rg_rand01_of(wj) < pj)) {
+                c.mti += m;
+#pragma unroll
+                for (int j = 0; j < NS; j++)
+                    if (j * 64 < n && j * 64 + LANE < n && j * 64 + LANE >= 1) ex[j] = ex[j] + evx[j];
+                iters++;
+                continue;
+            }
+        }
 #pragma unroll
         for (int lane = 0; lane < 5; lane++) {
             if (lane >= nroad) break;
