@@ -154,6 +154,11 @@ def main():
                     help="after every step, RCCL all-gather of every rank's uint8[E,64,64,3] obs shard into a "
                          "[N*E,64,64,3] tensor on each rank (north star's obs concatenation; SURVEY 8(e))")
     args = ap.parse_args()
+    # stdout carries exactly the one JSON line: everything else written to fd 1 (RCCL's version banner
+    # at communicator init, library chatter) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -309,7 +314,8 @@ def main():
             "host_path": host,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     if gather is not None:
         gather.close()
     env.close()
