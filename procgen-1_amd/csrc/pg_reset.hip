@@ -215,6 +215,11 @@ DEV void set_obj(RCtx &c, int x, int y, int v) {
 DEV void fill_elem(RCtx &c, int x, int y, int dx, int dy, int elem) {
     int16_t v = (int16_t)(signed char)elem; // `char elem` narrowing (basic-abstract-game.cpp:125)
     int n = (dx > 0 && dy > 0) ? dx * dy : 0; // the reference loops run dx x dy times
+    if (x == 0 && y == 0 && dx == c.s.main_width && dy == c.s.main_height) { // the whole grid: no index math
+        for (int k = LANE; k < n && k < PG_GRID_MAX; k += 64) c.grid[k] = v;
+        wave_sync();
+        return;
+    }
     bool bad = false;
     for (int k = LANE; k < n; k += 64) {
         int j = k / dy, l = k % dy;
