@@ -2050,7 +2050,8 @@ DEV int cf_find_path(RCtx &c, CaveScratch *S, int src, int dst) {
         }
         wave_sync();
         int cnt = 0;
-        for (int base = 0; base < nf; base += 64) { // winners, written in key order
+        bool hit = false;
+        for (int base = 0; base < nf; base += 64) { // winners, written in key order (and covered)
             const int p = base + LANE;
             int wm = 0, u = 0;
             if (p < nf) {
@@ -2076,16 +2077,13 @@ DEV int cf_find_path(RCtx &c, CaveScratch *S, int src, int dst) {
                     const int v = (y + (k == 1 ? -1 : (k == 2 ? 1 : 0))) * W + x + (k == 0 ? -1 : (k == 3 ? 1 : 0));
                     nx[o++] = (int16_t)v;
                     S->a[v] = (int16_t)u;
+                    // exactly one (p, k) holds v's key, so marking it covered here cannot hide it from
+                    // its own winner; a later 64-entry chunk that also neighbours v fails the key test
+                    S->f[v] |= CF_COVERED;
+                    hit = hit || v == dst;
                 }
             }
             cnt += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-        }
-        wave_sync();
-        bool hit = false;
-        for (int q = LANE; q < cnt; q += 64) {
-            const int v = nx[q];
-            S->f[v] |= CF_COVERED;
-            hit = hit || v == dst;
         }
         found = ballot(hit) != 0;
         wave_sync();
