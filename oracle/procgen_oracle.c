@@ -7078,8 +7078,17 @@ static void heist_ctor(Game *g) { /* heist.cpp:23-35 */
     g->visibility = 8.0f;
 }
 
+/* Envs with global indices env_offset + n * stride (n < count) of a vec env: a mixed batch plays name
+ * n % #names at env n (vecgame.cpp:357-358), so one game's envs of it are a strided range. */
+void *oracle_make_strided(const char *env_name, int count, int env_offset, int stride, const or_options *opt,
+                          const or_atlas *atlas);
 void *oracle_make(const char *env_name, int count, int env_offset, const or_options *opt, const or_atlas *atlas) {
+    return oracle_make_strided(env_name, count, env_offset, 1, opt, atlas);
+}
+void *oracle_make_strided(const char *env_name, int count, int env_offset, int stride, const or_options *opt,
+                          const or_atlas *atlas) {
     int gid = game_id_of(env_name);
+    if (stride < 1) return NULL;
     if (gid < 0 || count <= 0) return NULL;
     int dm = opt->distribution_mode;
     /* game.cpp:76-86: easy and hard for every game; extreme for chaser, dodgeball, leaper, starpilot;
@@ -7107,6 +7116,8 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
     rg_seed(&seed_gen, opt->rand_seed);
     for (int n = 0; n < env_offset; n++) (void)rg_randint0(&seed_gen);
     for (int n = 0; n < count; n++) {
+        if (n > 0)
+            for (int k = 1; k < stride; k++) (void)rg_randint0(&seed_gen); /* the other names' envs */
         Game *g = &v->games[n];
         g->game_id = gid;
         g->ents = (Entity *)calloc(MAX_ENTS, sizeof(Entity));
@@ -7129,7 +7140,7 @@ void *oracle_make(const char *env_name, int count, int env_offset, const or_opti
         rg_seed(&g->level_seed_rand_gen, rg_randint0(&seed_gen)); /* vecgame.cpp:362 */
         g->level_seed_high = level_seed_high;
         g->level_seed_low = level_seed_low;
-        g->game_n = env_offset + n;
+        g->game_n = env_offset + n * stride;
         /* parse_options, game.cpp:62-95 */
         g->options.paint_vel_info = opt->paint_vel_info;
         g->options.use_generated_assets = opt->use_generated_assets != 0;

@@ -1916,13 +1916,12 @@ LIBENV_API int procgen_get_snapshot(libenv_env *env, int env_idx, char *data, in
     memcpy(p, &STATE_MAGIC, 4); p += 4;
     uint32_t ver = 2; memcpy(p, &ver, 4); p += 4;
     memcpy(p, &s, sizeof(s)); p += sizeof(s);
-    size_t plane = (size_t)v->num_envs * PG_CAP;
     for (int f = 0; f < PG_NF; f++) {
-        if (ents && copy_sync(v, p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (ents && copy_sync(v, p, v->dev.ents + pg_ent_index(env_idx, f, 0), ents * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
         p += ents * 4;
     }
     for (int f = 0; f < PG_NF; f++) {
-        if (tail && copy_sync(v, p, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP + (PG_CAP - tail), tail * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (tail && copy_sync(v, p, v->dev.ents + pg_ent_index(env_idx, f, (int)(PG_CAP - tail)), tail * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
         p += tail * 4;
     }
     if (cells && copy_sync(v, p, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, cells * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -1978,7 +1977,6 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
         fail(v, PG_ERR_BAD_OPTION, "set_state: missing END_OF_BUFFER");
         return;
     }
-    size_t plane = (size_t)v->num_envs * PG_CAP;
     // a restored env draws with the options its state carries: the register-frame render serves
     // centred, non-monochrome frames only (pg_render.hip rf_game), so its game falls back otherwise
     if (s.opt_use_monochrome_assets || (!s.opt_center_agent && s.main_width > 63)) v->dev.render_rf &= ~(1 << s.game_id);
@@ -1986,11 +1984,11 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     const char *ent_base = p; // the live entity planes
     for (int f = 0; f < PG_NF; f++) {
-        if (ents) copy_sync(v, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP, p, ents * 4, hipMemcpyHostToDevice);
+        if (ents) copy_sync(v, v->dev.ents + pg_ent_index(env_idx, f, 0), p, ents * 4, hipMemcpyHostToDevice);
         p += ents * 4;
     }
     for (int f = 0; f < PG_NF; f++) {
-        if (tail) copy_sync(v, v->dev.ents + f * plane + (size_t)env_idx * PG_CAP + (PG_CAP - tail), p, tail * 4, hipMemcpyHostToDevice);
+        if (tail) copy_sync(v, v->dev.ents + pg_ent_index(env_idx, f, (int)(PG_CAP - tail)), p, tail * 4, hipMemcpyHostToDevice);
         p += tail * 4;
     }
     if (cells) copy_sync(v, v->dev.grid + (size_t)env_idx * PG_GRID_MAX, p, cells * 2, hipMemcpyHostToDevice);

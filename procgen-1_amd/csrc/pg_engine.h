@@ -2,7 +2,7 @@
 //
 // One env = one wavefront.  Per-env state lives in HBM, resident across steps:
 //   PGEnv        per-env scalars (Game + BasicAbstractGame + per-game members), 512 B
-//   entity SoA   PG_NF field planes, each [num_envs][PG_CAP] (lane = entity slot)
+//   entity SoA   [num_envs][PG_NF field planes][PG_CAP] (lane = entity slot; pg_ent_index)
 //   grid         int16 [num_envs][PG_GRID_MAX] (row-major y*w+x, reference grid.h:14-79)
 //   mt           uint32 [num_envs][2][PG_MT_WORDS] (rand_gen, level_seed_rand_gen)
 // Field and member names follow the reference (game.h, basic-abstract-game.h,
@@ -243,13 +243,21 @@ struct PGEnv {
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
 
+// Entity storage: one contiguous block of PG_NF planes x PG_CAP slots per env (51,200 B), so every field
+// of an env is a 32-bit byte offset from the env's block (plane f at f * 2,048 B): the kernels address
+// an env's entities from one base register instead of 25 plane bases 128 MB apart.
+#define PG_ENT_BLOCK (PG_NF * PG_CAP) // words per env
+static inline __host__ __device__ size_t pg_ent_index(int env, int f, int slot) {
+    return (size_t)env * PG_ENT_BLOCK + (size_t)f * PG_CAP + (size_t)slot;
+}
+
 // Everything a kernel needs, passed by value.
 struct PGDev {
     int32_t num_envs;
     int32_t env_offset;       // global index of env 0 (multi-GPU shard)
     int32_t num_actions;
     PGEnv *envs;
-    float *ents;              // PG_NF planes of num_envs * PG_CAP words (int planes reinterpret)
+    float *ents;              // num_envs blocks of PG_NF planes x PG_CAP words (pg_ent_index; int planes reinterpret)
     int16_t *grid;            // num_envs * PG_GRID_MAX
     int8_t *grid8;            // num_envs * PG_GRID_MAX: int8 mirror for the step kernel's LDS copy
     uint32_t *mt;             // num_envs * 2 * PG_MT_WORDS
@@ -293,7 +301,7 @@ struct PGDev {
     // on a side stream, into a spare state -- the next level depends only on the level-seed
     // generator (game.cpp:109-134) -- and swapped in when the episode ends.  Null when off.
     PGEnv *sp_envs;             // [num_envs] the spare's scalars
-    float *sp_ents;             // PG_NF planes of num_envs * PG_CAP
+    float *sp_ents;             // as ents
     int16_t *sp_grid;           // num_envs * PG_GRID_MAX
     int8_t *sp_grid8;
     uint32_t *sp_mt;            // num_envs * 2 * PG_MT_WORDS (rand_gen, level_seed_rand_gen)

@@ -24,10 +24,10 @@ struct View {
 };
 
 DEV float EFr(const PGDev &d, int f, int env, int slot) {
-    return d.ents[(size_t)f * d.num_envs * PG_CAP + (size_t)env * PG_CAP + slot];
+    return d.ents[pg_ent_index(env, f, slot)];
 }
 DEV int EIr(const PGDev &d, int f, int env, int slot) {
-    return reinterpret_cast<const int *>(d.ents)[(size_t)f * d.num_envs * PG_CAP + (size_t)env * PG_CAP + slot];
+    return reinterpret_cast<const int *>(d.ents)[pg_ent_index(env, f, slot)];
 }
 
 // get_screen_rect (basic-abstract-game.cpp:808-810): float arithmetic, widened to qreal

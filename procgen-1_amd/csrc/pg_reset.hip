@@ -83,8 +83,7 @@ struct RCtx {
     int env;
     PGEnv &s;        // the env's scalars, staged in LDS for the whole reset (wave-uniform: keeping
                      // the 512-B struct in VGPRs cost ~128 registers and scratch spills)
-    float *E;
-    size_t plane, eb;
+    char *Eb;        // this env's entity block (pg_ent_index)
     uint32_t *mt;    // LDS rand_gen words
     int32_t mti;
     // the next draws, tempered, one per lane: lane k holds mt[wbase + k] (draw() reads it with readlane;
@@ -111,8 +110,9 @@ struct RCtx {
 #define RMARK(c, k) ((void)0)
 #endif
 
-DEV float &EF(RCtx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
-DEV int &EI(RCtx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
+DEV uint32_t ent_off(int f, int slot) { return (uint32_t)(f * PG_CAP + slot) * 4u; }
+DEV float &EF(RCtx &c, int f, int slot) { return *reinterpret_cast<float *>(c.Eb + ent_off(f, slot)); }
+DEV int &EI(RCtx &c, int f, int slot) { return *reinterpret_cast<int *>(c.Eb + ent_off(f, slot)); }
 
 #define MT_WIN_NONE (-(1 << 20))
 DEV void mt_window_reset(RCtx &c) { c.wbase = MT_WIN_NONE; }
@@ -2896,10 +2896,8 @@ DEV void reset_env(PGDev &d, int env, uint32_t *lds_mt, int16_t *lds_grid, Scrat
     }
     wave_sync();
     RCtx c{d, env, *lds_env};
-    c.E = d.ents;
+    c.Eb = reinterpret_cast<char *>(d.ents + pg_ent_index(env, 0, 0));
     c.ag = ag;
-    c.plane = (size_t)d.num_envs * PG_CAP;
-    c.eb = (size_t)env * PG_CAP;
     c.mt = lds_mt;
     c.grid = lds_grid;
 #ifdef PG_PROF_RESET
@@ -3077,10 +3075,9 @@ DEV void swap_spare(PGDev &d, int env, PGEnv *lds_env) {
         out[w] = a;
     }
     wave_sync();
-    const size_t plane = (size_t)d.num_envs * PG_CAP, eb = (size_t)env * PG_CAP;
     const int ne = G == PG_GAME_STARPILOT ? PG_CAP : min(max(lds_env->num_ents, 0), PG_CAP);
     for (int f = 0; f < PG_NF; f++)
-        for (int i = LANE; i < ne; i += 64) d.ents[(size_t)f * plane + eb + i] = d.sp_ents[(size_t)f * plane + eb + i];
+        for (int i = LANE; i < ne; i += 64) d.ents[pg_ent_index(env, f, i)] = d.sp_ents[pg_ent_index(env, f, i)];
     int cells = lds_env->main_width * lds_env->main_height;
     if (cells > PG_GRID_MAX || cells < 0) cells = PG_GRID_MAX;
     const uint4 *g16 = reinterpret_cast<const uint4 *>(d.sp_grid + (size_t)env * PG_GRID_MAX);

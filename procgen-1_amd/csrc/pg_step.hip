@@ -9,12 +9,12 @@
 namespace {
 
 struct Ctx {
-    PGDev d;
+    // the kernel argument itself (by reference: its fields are loaded from the kernarg segment where they
+    // are used; a by-value copy here loaded every pointer at entry and spilled them for the whole step)
+    const PGDev &d;
     int env;
     PGEnv s;        // uniform copy of this env's scalars
-    float *E;       // entity planes
-    size_t plane;   // num_envs * PG_CAP
-    size_t eb;      // env * PG_CAP
+    char *Eb;       // this env's entity block (pg_ent_index): field f of slot i at byte (f * PG_CAP + i) * 4
     const int16_t *G; // this env's grid
     uint32_t *lds;  // 624-word twist staging
     int16_t *ilist; // LDS: ascending indices of entities that can interact in sub_step
@@ -38,8 +38,11 @@ struct Ctx {
     Census cs;      // diagnostic wave census (PG_CENSUS builds only)
 };
 
-DEV float &EF(Ctx &c, int f, int slot) { return c.E[(size_t)f * c.plane + c.eb + slot]; }
-DEV int &EI(Ctx &c, int f, int slot) { return reinterpret_cast<int *>(c.E)[(size_t)f * c.plane + c.eb + slot]; }
+// 32-bit byte offsets from the env's block: one base register pair for every entity access (the
+// global_load saddr + voffset form) instead of 64-bit plane-address arithmetic per field
+DEV uint32_t ent_off(int f, int slot) { return (uint32_t)(f * PG_CAP + slot) * 4u; }
+DEV float &EF(Ctx &c, int f, int slot) { return *reinterpret_cast<float *>(c.Eb + ent_off(f, slot)); }
+DEV int &EI(Ctx &c, int f, int slot) { return *reinterpret_cast<int *>(c.Eb + ent_off(f, slot)); }
 
 // A whole entity held in registers (uniform).
 struct Ent {
@@ -68,6 +71,24 @@ DEV void store_ent(Ctx &c, int i, const Ent &e) {
     EI(c, F_TYPE, i) = e.type; EI(c, F_IMAGE_TYPE, i) = e.image_type; EI(c, F_IMAGE_THEME, i) = e.image_theme;
     EI(c, F_RENDER_Z, i) = e.render_z; EI(c, F_LIFE_TIME, i) = e.life_time; EI(c, F_EXPIRE_TIME, i) = e.expire_time;
     EI(c, F_FIRE_TIME, i) = e.fire_time; EI(c, F_SPAWN_TIME, i) = e.spawn_time; EI(c, F_FLAGS, i) = e.flags;
+}
+
+// The fields a smart step (basic_step_object + Entity::step) reads, and the ones it can change: the
+// other eight (collision_margin, health, theta, climber_spawn_x, image_theme, render_z, fire_time,
+// spawn_time) are neither, and the read-only ones (vrot, friction, alpha_decay, grow_rate, type,
+// expire_time) are not written back.
+DEV void load_ent_step(Ctx &c, int i, Ent &e) {
+    e.x = EF(c, F_X, i); e.y = EF(c, F_Y, i); e.vx = EF(c, F_VX, i); e.vy = EF(c, F_VY, i);
+    e.rx = EF(c, F_RX, i); e.ry = EF(c, F_RY, i); e.rotation = EF(c, F_ROTATION, i); e.vrot = EF(c, F_VROT, i);
+    e.alpha = EF(c, F_ALPHA, i); e.alpha_decay = EF(c, F_ALPHA_DECAY, i); e.grow_rate = EF(c, F_GROW_RATE, i);
+    e.friction = EF(c, F_FRICTION, i);
+    e.type = EI(c, F_TYPE, i); e.image_type = EI(c, F_IMAGE_TYPE, i);
+    e.life_time = EI(c, F_LIFE_TIME, i); e.expire_time = EI(c, F_EXPIRE_TIME, i); e.flags = EI(c, F_FLAGS, i);
+}
+DEV void store_ent_step(Ctx &c, int i, const Ent &e) {
+    EF(c, F_X, i) = e.x; EF(c, F_Y, i) = e.y; EF(c, F_VX, i) = e.vx; EF(c, F_VY, i) = e.vy;
+    EF(c, F_RX, i) = e.rx; EF(c, F_RY, i) = e.ry; EF(c, F_ROTATION, i) = e.rotation; EF(c, F_ALPHA, i) = e.alpha;
+    EI(c, F_IMAGE_TYPE, i) = e.image_type; EI(c, F_LIFE_TIME, i) = e.life_time; EI(c, F_FLAGS, i) = e.flags;
 }
 
 // Entity::step (entity.cpp:57-82)
@@ -708,7 +729,7 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
     wave_sync();
     Ent mine;
     int my_i = LANE < nsm ? slist[LANE] : 0;
-    if (LANE < nsm) load_ent(c, my_i, mine);
+    if (LANE < nsm) load_ent_step(c, my_i, mine);
     // The non-smart entities' Entity::step touches only their own slots and no smart step reads
     // them (the only entities a smart step reads are the static interactors, whose Entity::step
     // leaves x, y, rx, ry and will_erase as they are, and the agent, itself smart), so they are
@@ -751,7 +772,7 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         entity_step(o);
         if (LANE == 0) mine = o;
     }
-    if (LANE < nsm) store_ent(c, my_i, mine);
+    if (LANE < nsm) store_ent_step(c, my_i, mine);
     wave_sync();
     return true;
 }
@@ -778,10 +799,10 @@ DEV void step_entities(Ctx &c, int16_t *slist) {
         wave_sync();
         if (sm < 0) break;
         Ent o;
-        load_ent(c, sm, o);
+        load_ent_step(c, sm, o);
         basic_step_object<G>(c, sm, o);
         entity_step(o);
-        store_ent(c, sm, o);
+        store_ent_step(c, sm, o);
         wave_sync();
         hi = sm - 1;
     }
@@ -1039,7 +1060,7 @@ DEV bool preserve_theme(int type) { // should_preserve_type_themes (heist.cpp:42
 template <int G>
 DEV float aspect_ratio(Ctx &c, int type, int theme) {
     if (c.s.opt_restrict_themes && !preserve_theme<G>(type)) theme = 0;
-    int4 sp = reinterpret_cast<const int4 *>(c.d.sprites)[type + theme * MAX_ASSETS];
+    int4 sp = reinterpret_cast<const int4 *>(c.d.sprites + (size_t)G * PG_NUM_SLOTS * 4)[type + theme * MAX_ASSETS];
     if (sp.y <= 0 || sp.z <= 0) {
         c.s.error = PG_ERR_BAD_OPTION;
         return 1.0f;
@@ -1362,7 +1383,7 @@ DEV void handle_collision(Ctx &c, int si, int ti) {
                         EF(c, F_GROW_RATE, k) = 1.0f / 1.2f;
                         EI(c, F_EXPIRE_TIME, k) = 4;
                         EF(c, F_ALPHA_DECAY, k) = 0.9f;
-                        EI(c, F_IMAGE_THEME, k) = c.s.step_rand_int % c.d.num_themes[DB_DUST_CLOUD]; // choose_step_random_theme
+                        EI(c, F_IMAGE_THEME, k) = c.s.step_rand_int % c.d.num_themes[G * 100 + DB_DUST_CLOUD]; // choose_step_random_theme
                     }
                 }
             }
@@ -1689,7 +1710,7 @@ DEV void bigfish_step_tail(Ctx &c, uint32_t *rg) { // bigfish.cpp:80-106
         float ent_vx = (float)((.15 + (double)rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) * .25) *
                                (moves_right != 0 ? 1 : -1));
         float ent_x = moves_right != 0 ? -1 * ent_r : c.s.main_width + ent_r;
-        int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[BF_FISH]); // choose_random_theme
+        int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[PG_GAME_BIGFISH * 100 + BF_FISH]); // choose_random_theme
         float ry = ent_r / aspect_ratio<PG_GAME_BIGFISH>(c, BF_FISH, theme);           // match_aspect_ratio
         int i = append_entity(c, ent_x, ent_y, ent_vx, 0, ent_r, ry, BF_FISH);
         if (i >= 0) {
@@ -1993,7 +2014,7 @@ DEV void lp_spawn_entities(Ctx &c, uint32_t *rg) {
         if (rg_rand01_of(mt_next_global(rg, c.s.rg_mti, c.lds)) < spawn_prob) {
             const float x = speed > 0 ? (-1 * LP_MONSTER_RADIUS) : (c.s.main_width + LP_MONSTER_RADIUS);
             const float y = (float)(c.s.bottom_road_y + lane + 0.5);
-            const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[LP_CAR]);
+            const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[PG_GAME_LEAPER * 100 + LP_CAR]);
             if (!any_collision(c, x, y, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS)) {
                 int i = append_entity(c, x, y, speed, 0, 2 * LP_MONSTER_RADIUS, LP_MONSTER_RADIUS, LP_CAR);
                 if (i >= 0) {
@@ -2744,7 +2765,7 @@ DEV void starpilot_step_tail(Ctx &c, uint32_t *rg) {
     }
     if (c.s.cur_time == SP_SHOOTER_WIN_TIME) {
         // Entity(main_width, main_height / 2, -slow_v * V_SCALE, 0, 2, main_height / 2, FINISH_LINE)
-        const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[SP_FINISH_LINE]);
+        const int theme = rg_randn_of(mt_next_global(rg, c.s.rg_mti, c.lds), c.d.num_themes[PG_GAME_STARPILOT * 100 + SP_FINISH_LINE]);
         const float fry = (float)(c.s.main_height / 2);
         const float frx = fry * aspect_ratio<PG_GAME_STARPILOT>(c, SP_FINISH_LINE, theme); // match_aspect_ratio(, false)
         wave_sync();
@@ -2867,6 +2888,32 @@ struct StepLds {
     uint8_t *moved;
 };
 
+// The kernel argument (a PGDev, the first argument of every kernel that calls step_env) through an
+// opaque constant-address pointer to the kernarg segment: the compiler cannot move the loads of its
+// fields above the point where the view is taken (step_env's epilogue).
+typedef __attribute__((address_space(4))) const PGDev PGDevK;
+DEV PGDevK &late_view() {
+    PGDevK *p = (PGDevK *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+// One PGEnv member of n words at word offset `off` into the write-back halves (lane q <-> word q / 64 + q).
+template <typename T>
+DEV void wb_put(uint32_t &w0, uint32_t &w1, uint64_t &m0, uint64_t &m1, int off, const T *v, int n) {
+    const uint32_t *u = reinterpret_cast<const uint32_t *>(v);
+#pragma unroll
+    for (int q = 0; q < n; q++) {
+        const int o = off + q;
+        if (o < 64) {
+            w0 = LANE == o ? u[q] : w0;
+            m0 |= 1ull << o;
+        } else {
+            w1 = LANE == o - 64 ? u[q] : w1;
+            m1 |= 1ull << (o - 64);
+        }
+    }
+}
+
 // Game::step (game.cpp:136-171) of one env by the calling wave, minus reset (queued) and observe
 // (pg_render)
 template <int G>
@@ -2878,14 +2925,15 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     float *lds_pstk = L.pstk;
     int *lds_iinfo = L.iinfo;
     int8_t *lds_grid = L.grid;
-    Ctx c;
-    c.d = game_view(d, G);
+    Ctx c{d};
     c.moved = L.moved;
     c.env = env;
+#ifdef PG_SCALAR_ENV
+    c.s = *(const __attribute__((address_space(4))) PGEnv *)(d.envs + c.env);
+#else
     c.s = d.envs[c.env];
-    c.E = d.ents;
-    c.plane = (size_t)d.num_envs * PG_CAP;
-    c.eb = (size_t)c.env * PG_CAP;
+#endif
+    c.Eb = reinterpret_cast<char *>(d.ents + pg_ent_index(c.env, 0, 0));
     c.G = d.grid + (size_t)c.env * PG_GRID_MAX;
     c.lds = lds_mt;
     c.ilist = lds_list;
@@ -2954,21 +3002,29 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     }
     c.s.episode_done = first;
 
+    // The epilogue reads its output pointers through an opaque view of the kernel argument, so their
+    // loads stay here instead of being merged into the entry's loads and spilled across the whole step.
+    PGDevK &k = late_view();
     if (LANE == 0) {
         if (done) {
-            int q = atomicAdd(d.reset_count + slot, 1);
-            d.reset_queue[(size_t)slot * d.num_envs + q] = c.env;
+            int q = atomicAdd(k.reset_count + slot, 1);
+            k.reset_queue[(size_t)slot * k.num_envs + q] = c.env;
         }
-        d.done8[c.env] = (uint8_t)done;
-        d.rew[c.env] = c.s.sd_reward;
-        d.first[c.env] = (uint8_t)first;
-        d.prev_level_seed[c.env] = c.s.prev_level_seed;
-        d.prev_level_complete[c.env] = (uint8_t)c.s.sd_level_complete;
-        d.level_seed[c.env] = c.s.current_level_seed;
-        if (c.s.error) atomicOr(d.error_any, 1 << c.s.error);
-        // write back only the PGEnv members this kernel can change (the rest is read-only here)
-        PGEnv *o = d.envs + c.env;
-#define PG_W(f) o->f = c.s.f;
+        k.done8[c.env] = (uint8_t)done;
+        k.rew[c.env] = c.s.sd_reward;
+        k.first[c.env] = (uint8_t)first;
+        k.prev_level_seed[c.env] = c.s.prev_level_seed;
+        k.prev_level_complete[c.env] = (uint8_t)c.s.sd_level_complete;
+        k.level_seed[c.env] = c.s.current_level_seed;
+        if (c.s.error) atomicOr(k.error_any, 1 << c.s.error);
+    }
+    // Write back only the PGEnv members this kernel can change (the rest is read-only here), as one
+    // vector store per 64-word half of the struct: lane q holds word q (and 64 + q), the store is
+    // masked to the written words -- 2 store instructions instead of one lane-0 store per member.
+    {
+        uint32_t w0 = 0, w1 = 0;
+        uint64_t m0 = 0, m1 = 0;
+#define PG_W(f) wb_put(w0, w1, m0, m1, (int)(offsetof(PGEnv, f) / 4), &c.s.f, (int)(sizeof(c.s.f) / 4));
         PG_STEP_WB_COMMON(PG_W) PG_W(error)
         if constexpr (G == PG_GAME_COINRUN) { PG_STEP_WB_COINRUN(PG_W) }
         if constexpr (G == PG_GAME_BIGFISH) { PG_STEP_WB_BIGFISH(PG_W) }
@@ -2984,6 +3040,9 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
         if constexpr (G == PG_GAME_NINJA) { PG_STEP_WB_NINJA(PG_W) }
         if constexpr (G == PG_GAME_JUMPER) { PG_STEP_WB_JUMPER(PG_W) }
 #undef PG_W
+        uint32_t *o = reinterpret_cast<uint32_t *>(k.envs + c.env);
+        if ((m0 >> LANE) & 1) o[LANE] = w0;
+        if ((m1 >> LANE) & 1) o[64 + LANE] = w1;
     }
     c.pt.mark(6);
 #ifndef PG_PROF_STAMP // that diagnostic build fills these slots with the render's stamping sub-phases
@@ -3048,15 +3107,23 @@ __global__ __launch_bounds__(64, STEP_WAVES) void pg_step_kernel(PGDev d, const 
 } // namespace
 
 #ifndef PG_FUSED_TU // pg_fused.hip includes this file for step_env
+#ifndef PG_ONLY_GAME
+#define PG_ONLY_GAME (-1) // experiment builds: instantiate one game's kernel only (-DPG_ONLY_GAME=5)
+#endif
+template <int G>
+static void launch_step_g(const PGDev *d, const int32_t *env_list, int count, hipStream_t s, int use_hash,
+                          uint64_t seed, int32_t t, int parity, int slot) {
+    if constexpr (PG_ONLY_GAME < 0 || G == PG_ONLY_GAME)
+        hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count + (count < PG_HEAVY_CAP ? count : PG_HEAVY_CAP)), dim3(64),
+                           0, s, *d, env_list, count, parity, use_hash, seed, t, slot);
+}
 // parity: alternates per act (the host zeroes this parity's slow-list length and the reset counts)
 extern "C" void pg_launch_step(const PGDev *d, int game, const int32_t *env_list, int count, hipStream_t s,
                                int use_hash, uint64_t seed, int32_t t, int parity, int slot) {
     if (count <= 0) return;
 #define PG_CASE(G)                                                                                   \
     case G:                                                                                          \
-        hipLaunchKernelGGL(pg_step_kernel<G>, dim3(count + (count < PG_HEAVY_CAP ? count : PG_HEAVY_CAP)), dim3(64), 0, \
-                           s, *d, env_list, count, parity, use_hash,                                 \
-                           seed, t, slot);                                                                 \
+        launch_step_g<G>(d, env_list, count, s, use_hash, seed, t, parity, slot);                    \
         break;
     switch (game) {
         PG_CASE(PG_GAME_COINRUN)

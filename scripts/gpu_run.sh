@@ -1,0 +1,43 @@
+# One parameterised GPU launcher (round 6): every stage runs under its own time limit, stages are
+# chained so the first fault / abort / timeout ends the call, and nothing is retried.
+#   DO="smoke tests ab counters bench"   stages, in this order
+#   TESTS="tests/test_gpu_coinrun.py ..." pytest selections for `tests` (default: the whole -m gpu suite)
+#   PYTEST_K=...                          -k filter for `tests`
+#   VARIANTS="base rf"                    extra builds for `ab` (procgen_amd/libprocgen_mi355x_<v>.so)
+#   GAMES="coinrun"  CFGS="A=1,B=2 -"     games and env-knob configs for `ab` (each config x variant)
+#   STEPS=200 SETTLE=300                  bench length for `ab`
+#   CGAMES="coinrun"                      games for `counters` (scripts/gpu_counters.sh)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ab
+for stage in ${DO:-smoke tests}; do
+  case $stage in
+  smoke)
+    timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
+  tests)
+    timeout -k 10 ${TEST_TIMEOUT:-1100} python3 -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout ${PER_TEST:-300} \
+      --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
+    rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc ;;
+  ab)
+    for g in ${GAMES:-coinrun}; do
+      for v in default ${VARIANTS}; do
+        for c in ${CFGS:--}; do
+          a=${c//,/ }; [[ $c == - ]] && a=""
+          lib=""; [ "$v" = default ] || lib=$v
+          f=gpurun_out/ab/$g.$v.${c//=/_}
+          env $a PROCGEN_MI355X_LIB=$lib timeout -k 10 240 python3 bench.py --env-name $g --steps ${STEPS:-200} --warmup 20 \
+            --settle ${SETTLE:-300} --host-steps 0 --no-cpu-baseline > $f.json 2> $f.err || { tail -5 $f.err; exit 12; }
+          python3 -c "import json; d=json.load(open('$f.json')); print('%-10s %-8s %-40s %6.2f M' % ('$g', '$v', '$c', d['value']/1e6), d['roofline']['kernel_ms'])"
+        done
+      done
+    done ;;
+  counters)
+    GAMES="${CGAMES:-coinrun}" bash scripts/gpu_counters.sh > gpurun_out/counters.log 2>&1 || { tail -5 gpurun_out/counters.log; exit 13; }
+    tail -3 gpurun_out/counters.log ;;
+  bench)
+    timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -5 gpurun_out/bench.err; exit 14; }
+    cat gpurun_out/bench.json ;;
+  esac
+done
