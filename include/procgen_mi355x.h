@@ -83,6 +83,13 @@ LIBENV_API int procgen_shard_plan(const char *env_names, int num_envs, int env_o
 /* Copy the outputs of `count` envs (ids env_ids[k]) to host arrays of `count` rows after the
  * enqueued steps finish; any pointer may be NULL.  For consumers (and tests) that sample a few
  * envs of a device-resident batch without copying the whole observation tensor. */
+/* The outputs of EVERY env after the enqueued steps finish, for parity checks of whole populations
+ * (tests/test_gpu_population.py): obs_digest[e] = sum over k < 1536 of w_k * x_k mod 2^64, x_k the
+ * k-th little-endian 64-bit word of env e's 64x64x3 observation and w_k = splitmix64(k) | 1 (the
+ * splitmix64 of procgen_act_hashed), computed on the device; the scalar outputs are copied whole.
+ * Host arrays of num_envs entries; any may be NULL.  Returns 0 on success. */
+LIBENV_API int procgen_read_outputs(libenv_env *env, uint64_t *obs_digest, float *rew, uint8_t *first,
+                                    int32_t *prev_level_seed, uint8_t *prev_level_complete, int32_t *level_seed);
 LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int count, uint8_t *rgb, float *rew,
                                  uint8_t *first, int32_t *prev_level_seed, uint8_t *prev_level_complete,
                                  int32_t *level_seed);

@@ -7080,8 +7080,6 @@ static void heist_ctor(Game *g) { /* heist.cpp:23-35 */
 
 /* Envs with global indices env_offset + n * stride (n < count) of a vec env: a mixed batch plays name
  * n % #names at env n (vecgame.cpp:357-358), so one game's envs of it are a strided range. */
-void *oracle_make_strided(const char *env_name, int count, int env_offset, int stride, const or_options *opt,
-                          const or_atlas *atlas);
 void *oracle_make(const char *env_name, int count, int env_offset, const or_options *opt, const or_atlas *atlas) {
     return oracle_make_strided(env_name, count, env_offset, 1, opt, atlas);
 }

@@ -54,6 +54,10 @@ typedef struct {
  * The atlas memory must outlive the handle. Returns NULL on bad options. */
 void *oracle_make(const char *env_name, int count, int env_offset, const or_options *opt,
                   const or_atlas *atlas);
+/* The same for global indices env_offset + n * stride (one game's envs of a mixed batch, which plays
+ * name n % #names at env n, vecgame.cpp:357-358). */
+void *oracle_make_strided(const char *env_name, int count, int env_offset, int stride, const or_options *opt,
+                          const or_atlas *atlas);
 void oracle_close(void *h);
 /* initial reset + observe (reference vecgame.cpp:126-131) */
 void oracle_start(void *h);

@@ -303,6 +303,10 @@ void build_rot_table(float *angles, double *table) {
 }
 
 struct VecEnv {
+    uint64_t *d_digest = nullptr; // procgen_read_outputs' per-env observation digests (allocated on first use)
+    int rf_make = 0;               // PGDev::render_rf chosen at make time
+    std::vector<uint8_t> rf_bad;   // [num_envs] env holds a restored state the register-frame render cannot draw
+    int rf_bad_n[PG_NUM_GAMES] = {}; // such envs per game (their game renders with the LDS-frame kernel)
     int num_envs = 0;
     int env_offset = 0;
     int num_actions = 15;
@@ -665,22 +669,11 @@ int launch_step(VecEnv *v, int use_hash, uint64_t seed, int32_t t) {
     return 0;
 }
 
-// Device -> page-locked (hipHostRegister'd) host copy.  Inside the engine the runtime carried these
-// as copyBuffer blit kernels that hold CUs for the whole transfer (the same copy in a probe
-// process goes to SDMA, scripts/d2h_probe2.hip), so PROCGEN_MI355X_D2H_NOCU=1 issues them as
-// hipMemcpyDeviceToDeviceNoCU (the registered host pointer is device-addressable): a copy that may not
-// use compute units.  Falls back to the plain device -> host kind if the runtime refuses it.
+// Device -> page-locked (hipHostRegister'd) host copy.  Inside the engine the runtime carries these as
+// copyBuffer blit kernels that hold CUs for the whole transfer (the same copy in a probe
+// process goes to SDMA, scripts/d2h_probe2.hip).  Round 5 tried them as hipMemcpyDeviceToDeviceNoCU
+// (an opt-in knob, removed in round 6): the trace still showed blits and the rate did not move.
 static hipError_t d2h_registered(void *dst, const void *src, size_t n, hipStream_t s) {
-    static int nocu = -1;
-    if (nocu < 0) {
-        const char *e = getenv("PROCGEN_MI355X_D2H_NOCU");
-        nocu = e && e[0] == '1';
-    }
-    if (nocu) {
-        if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDeviceNoCU, s) == hipSuccess) return hipSuccess;
-        (void)hipGetLastError();
-        nocu = 0;
-    }
     return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
 }
 
@@ -1364,9 +1357,17 @@ LIBENV_API libenv_env *libenv_make(int num_envs, const struct libenv_options opt
     rc |= dalloc(v, &d.heavy_flag, 2 * n);
     d.heavy_ticks = 10000; // 100 us: ~3x the median coinrun step wave
     {
+        // PROCGEN_MI355X_HEAVY_US: the slow-env threshold in microseconds (tests: 0 lists every env, which
+        // also overflows the PG_HEAVY_CAP slow list, so both launch-order paths run on every act)
+        const char *hu = getenv("PROCGEN_MI355X_HEAVY_US");
+        if (hu && hu[0]) d.heavy_ticks = atoi(hu) > 0 ? (int64_t)atoi(hu) * 100 : -1;
+    }
+    {
         // the register-frame render (pg_render_rf_kernel) for the games and options it serves;
         // PROCGEN_MI355X_RENDER_RF=0 keeps every game on the LDS-frame kernel
         d.render_rf = rf_mask(center_agent, use_monochrome_assets, use_generated_assets);
+        v->rf_make = d.render_rf;
+        v->rf_bad.assign(n, 0);
         const char *fz = getenv("PROCGEN_MI355X_FUSED"); // 1: fuse step and render (pg_fused.hip)
         v->fused = fz && fz[0] == '1';
     }
@@ -1660,6 +1661,7 @@ LIBENV_API void libenv_close(libenv_env *env) {
     if (v->stream) (void)hipStreamSynchronize(v->stream);
     unregister_buffers(v);
     for (void *p : v->allocs) hipFree(p);
+    if (v->d_digest) (void)hipFree(v->d_digest);
     if (v->pinned) (void)hipHostFree(v->pinned);
     if (v->h_actions) (void)hipHostFree(v->h_actions);
     if (v->act_copied) hipEventDestroy(v->act_copied);
@@ -1757,6 +1759,50 @@ LIBENV_API int procgen_read_envs(libenv_env *env, const int32_t *env_ids, int co
                                     v->stream));
         if (level_seed) HIPCHECK(hipMemcpyAsync(level_seed + k, v->dev.level_seed + e, 4, hipMemcpyDeviceToHost, v->stream));
     }
+    HIPCHECK(hipStreamSynchronize(v->stream));
+    return 0;
+}
+
+// procgen_read_outputs: one wave per env sums its 1,536 observation words times splitmix64(k) | 1
+__device__ __forceinline__ uint64_t pg_mix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+__global__ __launch_bounds__(64) void pg_obs_digest_kernel(const uint8_t *rgb, uint64_t *out, int n) {
+    const int e = (int)blockIdx.x;
+    if (e >= n) return;
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(rgb + (size_t)e * PG_OBS_BYTES);
+    uint64_t acc = 0;
+    for (int k = (int)threadIdx.x; k < PG_OBS_BYTES / 8; k += 64) acc += w[k] * (pg_mix64((uint64_t)k) | 1ull);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (threadIdx.x == 0) out[e] = acc;
+}
+
+LIBENV_API int procgen_read_outputs(libenv_env *env, uint64_t *obs_digest, float *rew, uint8_t *first,
+                                    int32_t *prev_level_seed, uint8_t *prev_level_complete, int32_t *level_seed) {
+    VecEnv *v = (VecEnv *)env;
+    if (!v) return -PG_ERR_BAD_OPTION; // a closed / never-made env
+    HIPCHECK(hipSetDevice(v->device));
+    const size_t n = (size_t)v->num_envs;
+    if (obs_digest) {
+        if (!v->d_digest && hipMalloc(&v->d_digest, n * 8) != hipSuccess) {
+            v->d_digest = nullptr;
+            return fail(v, PG_ERR_HIP, "procgen_read_outputs: out of device memory");
+        }
+        hipLaunchKernelGGL(pg_obs_digest_kernel, dim3((unsigned)n), dim3(64), 0, v->stream, v->dev.rgb, v->d_digest,
+                           (int)n);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpyAsync(obs_digest, v->d_digest, n * 8, hipMemcpyDeviceToHost, v->stream));
+    }
+    if (rew) HIPCHECK(hipMemcpyAsync(rew, v->dev.rew, n * 4, hipMemcpyDeviceToHost, v->stream));
+    if (first) HIPCHECK(hipMemcpyAsync(first, v->dev.first, n, hipMemcpyDeviceToHost, v->stream));
+    if (prev_level_seed) HIPCHECK(hipMemcpyAsync(prev_level_seed, v->dev.prev_level_seed, n * 4, hipMemcpyDeviceToHost, v->stream));
+    if (prev_level_complete)
+        HIPCHECK(hipMemcpyAsync(prev_level_complete, v->dev.prev_level_complete, n, hipMemcpyDeviceToHost, v->stream));
+    if (level_seed) HIPCHECK(hipMemcpyAsync(level_seed, v->dev.level_seed, n * 4, hipMemcpyDeviceToHost, v->stream));
     HIPCHECK(hipStreamSynchronize(v->stream));
     return 0;
 }
@@ -1979,7 +2025,19 @@ LIBENV_API void procgen_set_snapshot(libenv_env *env, int env_idx, const char *d
     }
     // a restored env draws with the options its state carries: the register-frame render serves
     // centred, non-monochrome frames only (pg_render.hip rf_game), so its game falls back otherwise
-    if (s.opt_use_monochrome_assets || (!s.opt_center_agent && s.main_width > 63)) v->dev.render_rf &= ~(1 << s.game_id);
+    {
+        // a game stays on the register-frame render while every live env of it is one the kernel serves
+        // (pg_rf_serves): a restored state carries its own options (game.cpp:266), which then persist
+        const uint8_t bad = pg_rf_serves(s) ? 0 : 1;
+        if (bad != v->rf_bad[env_idx]) {
+            v->rf_bad_n[s.game_id] += bad ? 1 : -1;
+            v->rf_bad[env_idx] = bad;
+        }
+        int off = 0;
+        for (int g = 0; g < PG_NUM_GAMES; g++)
+            if (v->rf_bad_n[g] > 0) off |= 1 << g;
+        v->dev.render_rf = v->rf_make & ~off;
+    }
     s.grid8_ok = 0; // the int8 mirror is rebuilt at the next reset; until then the step reads int16
     copy_sync(v, v->dev.envs + env_idx, &s, sizeof(s), hipMemcpyHostToDevice);
     const char *ent_base = p; // the live entity planes

@@ -243,6 +243,13 @@ struct PGEnv {
 
 static_assert(sizeof(PGEnv) == 512, "PGEnv must stay 512 B");
 
+// The frames the register-frame render (pg_render.hip pg_render_rf_kernel) draws: atlas colours (not
+// monochrome) and a tile window of at most 63 x 63 -- always when centred, else the whole world.  One
+// predicate for the kernel's check and the host's selection (make-time options, restored states).
+static inline __host__ __device__ bool pg_rf_serves(const PGEnv &s) {
+    return !s.opt_use_monochrome_assets && (s.opt_center_agent || (s.main_width <= 63 && s.main_height <= 63));
+}
+
 // Entity storage: one contiguous block of PG_NF planes x PG_CAP slots per env (51,200 B), so every field
 // of an env is a 32-bit byte offset from the env's block (plane f at f * 2,048 B): the kernels address
 // an env's entities from one base register instead of 25 plane bases 128 MB apart.

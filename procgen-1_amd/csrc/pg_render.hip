@@ -2172,7 +2172,9 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #undef PG_DRAW_ENTITIES
     if (ballot(err) && lane == 0) atomicOr(d.error_any, 1 << PG_ERR_RENDER);
     pt.mark(6);
+#ifndef PG_PROF_SMART // that diagnostic build fills these slots with the step's smart-entity census
     pt.flush(d.prof ? d.prof + (size_t)env * 16 + 8 : nullptr);
+#endif
 #ifdef PG_PROF_STAMP
     spt.mark(7);
     spt.flush(d.prof ? d.prof + (size_t)env * 16 : nullptr); // the step kernel's slots (it does not flush here)
@@ -2451,7 +2453,7 @@ DEV void rf_render_env(const PGDev &d, int env, uint8_t *tab, int4 *desc, int4 *
         low_x = 0; high_x = s.main_width - 1; low_y = 0; high_y = s.main_height - 1;
     }
     const int ww = high_x - low_x + 1, wh = high_y - low_y + 1;
-    if (s.opt_use_monochrome_assets || d.gen_bg || ww > 63 || wh > 63) err = true;
+    if (!pg_rf_serves(s) || d.gen_bg || ww > 63 || wh > 63) err = true; // the host routes such frames to kernel 3
     // ---- Qt blit setup of window tile column `lane`, window tile row `lane`, the background (lane 63)
     int4 bgi = make_int4(0, 0, 0, 0);
     double bg_rx = 0, bg_ry = 0, bg_rw = 0, bg_rh = 0;

@@ -35,6 +35,9 @@ struct Ctx {
     uint32_t *memo;     // LDS (aliases the twist staging, idle during step_entities): push-chain memo
     int nmemo;          // its entries (reset per basic_step_object)
     PTimer pt;      // diagnostic phase timer (PG_PROFILE builds only)
+#ifdef PG_PROF_SMART
+    uint64_t sm[6]; // diagnostic (PROFILE=1 EXTRA=-DPG_PROF_SMART): smart-entity census, prof[env][8..13]
+#endif
     Census cs;      // diagnostic wave census (PG_CENSUS builds only)
 };
 
@@ -514,6 +517,9 @@ DEV int memo_find(Ctx &c, int depth, const Ent &o, float mvx, float mvy) {
 // PL: every lane steps its own entity (no cross-lane operation).
 template <int G, bool PL>
 DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
+#ifdef PG_PROF_SMART
+    c.sm[1] += 1;
+#endif
     // the frame stack is wave-uniform LDS: the lane-parallel (PL) games never scan
     static_assert(!PL || (!scan_needed<G>(true) && !scan_needed<G>(false)), "PL games have no push chain");
     constexpr int MAXD = 5;
@@ -587,6 +593,9 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 push_offset(m, o, is_h, t_vx, t_vy);
                 if (d < MAXD) { // run sub_step(t_vx, t_vy, depth + 1)
                     const int hitk = memo_find(c, d + 1, o, t_vx, t_vy);
+#ifdef PG_PROF_SMART
+                    c.sm[4] += hitk >= 0 ? 1 : 0;
+#endif
                     if (hitk >= 0) { // replay the child's outcome; push_obj then zeroes the pushed velocity
                         const uint32_t *v = c.memo + hitk * PG_MEMO_W + 7;
                         o.x = __uint_as_float(v[0]); o.y = __uint_as_float(v[1]);
@@ -757,6 +766,9 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         if constexpr (G == PG_GAME_COINRUN) c.s.is_on_crate = ballot(c.s.is_on_crate != 0) ? 1 : 0;
     } else {
         const int jlo = (nsm > 0 && rli(my_i, 0) == 0) ? 1 : 0; // the agent goes last, below
+#ifdef PG_PROF_SMART
+        uint64_t t_sm = __builtin_amdgcn_s_memtime();
+#endif
         for (int j = nsm - 1; j >= jlo; j--) {
             Ent o;
             ent_readlane(mine, j, o);
@@ -764,7 +776,14 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
             entity_step(o);
             if (LANE == j) mine = o;
         }
+#ifdef PG_PROF_SMART
+        c.sm[3] += __builtin_amdgcn_s_memtime() - t_sm;
+#endif
     }
+#ifdef PG_PROF_SMART
+    c.sm[0] += nsm;
+    uint64_t t_ag = __builtin_amdgcn_s_memtime();
+#endif
     if (nsm > 0 && rli(my_i, 0) == 0) { // slist is ascending: the agent is smart entity 0
         Ent o;
         ent_readlane(mine, 0, o);
@@ -772,6 +791,9 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
         entity_step(o);
         if (LANE == 0) mine = o;
     }
+#ifdef PG_PROF_SMART
+    c.sm[2] += __builtin_amdgcn_s_memtime() - t_ag;
+#endif
     if (LANE < nsm) store_ent_step(c, my_i, mine);
     wave_sync();
     return true;
@@ -2948,6 +2970,10 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     c.grid8_ok = false;
     c.cs.start();
     c.pt.start();
+#ifdef PG_PROF_SMART
+    for (int k = 0; k < 6; k++) c.sm[k] = 0;
+    c.sm[5] = (uint64_t)c.s.num_ents;
+#endif
     load_grid_lds<G>(c);
     c.cs.mark(0);
 
@@ -3045,6 +3071,10 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
         if ((m1 >> LANE) & 1) o[64 + LANE] = w1;
     }
     c.pt.mark(6);
+#ifdef PG_PROF_SMART
+    if (LANE == 0 && d.prof)
+        for (int k = 0; k < 6; k++) d.prof[(size_t)c.env * 16 + 8 + k] += c.sm[k];
+#endif
 #ifndef PG_PROF_STAMP // that diagnostic build fills these slots with the render's stamping sub-phases
     c.pt.flush(d.prof ? d.prof + (size_t)c.env * 16 : nullptr);
 #endif

@@ -74,6 +74,7 @@ SIGNATURES = {
     "procgen_atlas_host": (ctypes.c_int64, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_read_envs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
+    "procgen_read_outputs": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 6),
     "procgen_set_obs_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "procgen_set_latent_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 6),
     "procgen_start": (ctypes.c_int, [ctypes.c_void_p]),

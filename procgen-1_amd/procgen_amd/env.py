@@ -289,6 +289,19 @@ class BaseProcgenEnv:
         _check(self._lib, self._handle, rc)
         return out
 
+    def read_outputs(self):
+        """Every env's outputs after the enqueued steps finish, with the observation as a 64-bit
+        digest per env computed on the device (procgen_read_outputs): dict of obs_digest (uint64),
+        rew, first, prev_level_seed, prev_level_complete, level_seed -- [num] each."""
+        n = self.num
+        out = dict(obs_digest=np.zeros(n, np.uint64), rew=np.zeros(n, np.float32), first=np.zeros(n, np.uint8),
+                   prev_level_seed=np.zeros(n, np.int32), prev_level_complete=np.zeros(n, np.uint8),
+                   level_seed=np.zeros(n, np.int32))
+        rc = self._lib.procgen_read_outputs(self._handle, *[out[k].ctypes.data for k in (
+            "obs_digest", "rew", "first", "prev_level_seed", "prev_level_complete", "level_seed")])
+        _check(self._lib, self._handle, rc)
+        return out
+
     def set_latent_state(self, env_idx, grid, agent_pos, exit_pos):
         """MinerGame::game_set_state (procgen/src/games/miner.cpp:423-449, the fork's JS setState):
         `grid` [h, w] (or flat with an explicit shape) of cell values, agent and exit cell positions.

@@ -45,6 +45,9 @@ def load():
         lib.oracle_make.restype = ctypes.c_void_p
         lib.oracle_make.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(or_options),
                                     ctypes.POINTER(or_atlas)]
+        lib.oracle_make_strided.restype = ctypes.c_void_p
+        lib.oracle_make_strided.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(or_options), ctypes.POINTER(or_atlas)]
         for n in ["oracle_close", "oracle_start"]:
             getattr(lib, n).argtypes = [ctypes.c_void_p]
         lib.oracle_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -89,9 +92,10 @@ def hashed_actions(seed, env_ids, t, num_actions=15):
 
 
 class OracleEnv:
-    """`count` envs with global indices env_offset.. of a vec env (same seeds as the engine)."""
+    """`count` envs with global indices env_offset + n * stride of a vec env (same seeds as the engine;
+    stride > 1: one game's envs of a mixed batch, which plays name n % #names at env n)."""
 
-    def __init__(self, env_name, count, env_offset=0, atlas=None, **kw):
+    def __init__(self, env_name, count, env_offset=0, atlas=None, stride=1, **kw):
         import sys
         sys.path.insert(0, os.path.join(REPO, "procgen-1_amd"))
         from procgen_amd.assets import atlas_for
@@ -106,8 +110,8 @@ class OracleEnv:
         opts.update(kw)
         self._opt = or_options(*[int(opts[n]) for n in OPTION_FIELDS])
         self.count = count
-        self.h = self.lib.oracle_make(env_name.encode(), count, env_offset, ctypes.byref(self._opt),
-                                      ctypes.byref(self._at))
+        self.h = self.lib.oracle_make_strided(env_name.encode(), count, env_offset, stride, ctypes.byref(self._opt),
+                                              ctypes.byref(self._at))
         if not self.h:
             raise ValueError("oracle_make rejected the options")
         self.lib.oracle_start(self.h)

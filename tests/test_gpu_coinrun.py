@@ -165,7 +165,10 @@ def test_full_size_sampled_parity():
     """65,536 envs (BASELINE config 2), hashed actions; sampled envs against the oracle."""
     num = 65536
     env = make_gpu(num, num_levels=200, start_level=0, rand_seed=0)
-    sample = [0, 1, 2, 63, 64, 1000, 4095, 12345, 30000, 32767, 32768, 50001, 65534, 65535]
+    # includes the crate-pile envs (CRATE_PILE_ENVS: the slow-env launch path at scale) and both parts'
+    # edges (the default 2-part split at 32,768)
+    sample = [0, 1, 2, 56, 63, 64, 1000, 1551, 2240, 3056, 3350, 3868, 4095, 12345, 30000, 32767, 32768, 48596,
+              50001, 65534, 65535]
     orcs = [OracleEnv("coinrun", 1, env_offset=i, num_levels=200, rand_seed=0) for i in sample]
     ids = np.arange(num)
     g = gpu_obs(env)
