@@ -249,6 +249,23 @@ DEV int get_obj_from_floats(Ctx &c, float i, float j) {
     if (j < 0) return c.s.out_of_bounds_object;
     return get_obj(c, (int)floorf(i), (int)floorf(j));
 }
+// get_obj_from_floats of a per-lane point (every lane its own probe): branch-free, one LDS read for all
+// lanes -- sub_step's four corner probes in one round trip instead of four dependent ones
+DEV int get_obj_from_floats_lane(Ctx &c, float i, float j) {
+    const int x = (int)floorf(i), y = (int)floorf(j);
+    const bool out = i < 0 || j < 0 || !(0 <= y && y < c.s.main_height && 0 <= x && x < c.s.main_width);
+    const int idx = out ? 0 : y * c.s.main_width + x;
+    int v;
+    if (c.grid8_ok) {
+        v = c.grid8[idx];
+#ifdef PG_GRID_ROWS
+        if (v == PG_G8_HOLE) v = (int)c.G[idx];
+#endif
+    } else {
+        v = (int)c.G[idx];
+    }
+    return out ? c.s.out_of_bounds_object : v;
+}
 
 // ------------------------------------------------------------------ per-game hooks
 template <int G>
@@ -537,15 +554,28 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
                 float nx = o.x + _vx;
                 const float margin = 0.98f;
                 bool block = false, reflect = false;
+                if constexpr (!PL) {
+                    // the four corner probes of the reference's (i, j) loop, lane q <-> corner (q >> 1, q & 1)
+                    // (lanes >= 4 repeat them); the loop only ORs its predicates, and ninja's star stop zeroes
+                    // a velocity the probes do not read, so the corners may be probed together
+                    const int i = (LANE >> 1) & 1, j = LANE & 1;
+                    const int type2 = get_obj_from_floats_lane(c, nx + o.rx * margin * (float)(2 * i - 1),
+                                                               ny + o.ry * margin * (float)(2 * j - 1));
+                    if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
+                        if (ballot(o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID)) { o.vx = 0; o.vy = 0; }
+                    block = ballot(is_blocked<G>(c, o.type, type2)) != 0;
+                    reflect = ballot(will_reflect<G>(o.type, type2)) != 0;
+                } else {
 #pragma unroll
-                for (int i = 0; i < 2; i++) {
+                    for (int i = 0; i < 2; i++) {
 #pragma unroll
-                    for (int j = 0; j < 2; j++) {
-                        int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
-                        if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
-                            if (o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID) { o.vx = 0; o.vy = 0; }
-                        block = block || is_blocked<G>(c, o.type, type2);
-                        reflect = reflect || will_reflect<G>(o.type, type2);
+                        for (int j = 0; j < 2; j++) {
+                            int type2 = get_obj_from_floats(c, nx + o.rx * margin * (float)(2 * i - 1), ny + o.ry * margin * (float)(2 * j - 1));
+                            if constexpr (G == PG_GAME_NINJA) // ninja.cpp:132-138: a star that meets a wall stops
+                                if (o.type == NJ_THROWING_STAR && type2 == NJ_WALL_MID) { o.vx = 0; o.vy = 0; }
+                            block = block || is_blocked<G>(c, o.type, type2);
+                            reflect = reflect || will_reflect<G>(o.type, type2);
+                        }
                     }
                 }
                 if (reflect) {

@@ -7,6 +7,8 @@
 #   GAMES="coinrun"  CFGS="A=1,B=2 -"     games and env-knob configs for `ab` (each config x variant)
 #   STEPS=200 SETTLE=300                  bench length for `ab`
 #   CGAMES="coinrun"                      games for `counters` (scripts/gpu_counters.sh)
+#   CENSUS_GAMES="coinrun dodgeball"      games for `census` (smart-entity census, VARIANT=smart build)
+#   SPEED_STEPS=1000                      round trips per line for `speed` (scripts/speed_shape.py)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -36,6 +38,14 @@ for stage in ${DO:-smoke tests}; do
   counters)
     GAMES="${CGAMES:-coinrun}" bash scripts/gpu_counters.sh > gpurun_out/counters.log 2>&1 || { tail -5 gpurun_out/counters.log; exit 13; }
     tail -3 gpurun_out/counters.log ;;
+  census)  # smart-entity census (diagnostic build libprocgen_mi355x_smart.so), per game in CENSUS_GAMES
+    for g in ${CENSUS_GAMES:-coinrun}; do
+      PROCGEN_MI355X_LIB=smart timeout -k 10 300 python3 scripts/smart_census.py $g > gpurun_out/census_$g.json 2> gpurun_out/census_$g.err || { tail -5 gpurun_out/census_$g.err; exit 15; }
+      cat gpurun_out/census_$g.json
+    done ;;
+  speed)  # the reference's speed-test shape (scripts/speed_shape.py)
+    timeout -k 10 900 python3 scripts/speed_shape.py > gpurun_out/speed_shape.json 2> gpurun_out/speed_shape.err || { tail -5 gpurun_out/speed_shape.err; exit 16; }
+    tail -16 gpurun_out/speed_shape.err ;;
   bench)
     timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -5 gpurun_out/bench.err; exit 14; }
     cat gpurun_out/bench.json ;;
