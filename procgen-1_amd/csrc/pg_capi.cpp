@@ -1910,9 +1910,6 @@ static const uint32_t STATE_MAGIC = 0x50474d33u; // "PGM3"
 // bigfish.cpp:27, bossfight.cpp:65, caveflyer.cpp:128-142, chaser.cpp:135-152, climber.cpp:230-232,
 // coinrun.cpp:54, dodgeball.cpp:248-256, fruitbot.cpp:147-154, heist.cpp:98-112, jumper.cpp:204-218,
 // leaper.cpp:103-115, maze.cpp:44-56, miner.cpp:127-138, ninja.cpp:36, plunder.cpp:37, starpilot.cpp:52)
-static const int GAME_MAX_DIM[PG_NUM_GAMES][2] = {
-    {20, 20}, {20, 20}, {60, 60}, {19, 19}, {20, 64}, {64, 64}, {40, 40}, {20, 60},
-    {23, 23}, {45, 45}, {20, 20}, {31, 31}, {35, 35}, {64, 64}, {20, 20}, {16, 16}};
 static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
 
 // Bounds of every PGEnv member a kernel uses as an array / LDS / table index (shared by the own
@@ -1920,7 +1917,7 @@ static const int32_t END_OF_BUFFER = (int32_t)0xCAFECAFE;
 // Returns the reason a state is rejected, or null.
 static const char *validate_env(const VecEnv *v, const PGEnv &s) {
     if (s.num_ents < 0 || s.num_tail < 0 || s.num_ents + s.num_tail > PG_CAP || s.main_width < 0 ||
-        s.main_height < 0 || s.main_width > GAME_MAX_DIM[s.game_id][0] || s.main_height > GAME_MAX_DIM[s.game_id][1])
+        s.main_height < 0 || s.main_width > pg_game_max_w(s.game_id) || s.main_height > pg_game_max_h(s.game_id))
         return "set_state: entity count or world size out of range for the game";
     if (s.rg_mti < 0 || s.rg_mti > PG_MT_N || s.lsg_mti < 0 || s.lsg_mti > PG_MT_N)
         return "set_state: RandGen position out of range";

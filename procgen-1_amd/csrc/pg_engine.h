@@ -250,6 +250,17 @@ static inline __host__ __device__ bool pg_rf_serves(const PGEnv &s) {
     return !s.opt_use_monochrome_assets && (s.opt_center_agent || (s.main_width <= 63 && s.main_height <= 63));
 }
 
+// The largest world of each game (width x height; its level generator's bound, also the set_state check
+// of pg_capi.cpp): the step kernel loads that many grid cells before it knows the env's own size.
+static inline __host__ __device__ constexpr int pg_game_max_w(int g) {
+    return g == 2 ? 60 : g == 3 ? 19 : g == 5 ? 64 : g == 6 ? 40 : g == 8 ? 23 : g == 9 ? 45 : g == 11 ? 31 : g == 12 ? 35 :
+           g == 13 ? 64 : g == 15 ? 16 : 20;
+}
+static inline __host__ __device__ constexpr int pg_game_max_h(int g) {
+    return g == 2 ? 60 : g == 3 ? 19 : g == 4 ? 64 : g == 5 ? 64 : g == 6 ? 40 : g == 7 ? 60 : g == 8 ? 23 : g == 9 ? 45 :
+           g == 11 ? 31 : g == 12 ? 35 : g == 13 ? 64 : g == 15 ? 16 : 20;
+}
+
 // Entity storage: one contiguous block of PG_NF planes x PG_CAP slots per env (51,200 B), so every field
 // of an env is a 32-bit byte offset from the env's block (plane f at f * 2,048 B): the kernels address
 // an env's entities from one base register instead of 25 plane bases 128 MB apart.

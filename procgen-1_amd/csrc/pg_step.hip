@@ -192,10 +192,37 @@ DEV uint64_t grid_rows_needed(Ctx &c) {
     for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o);
     return m;
 }
+// The int8 mirror's chunks of the game's largest world, loaded by the kernel before the env's scalars
+// arrive (they do not depend on them), lane k <-> 16-byte chunk k + 64 q.
 template <int G>
-DEV void load_grid_lds(Ctx &c) {
+struct GridPre {
+    static constexpr int NCH = (pg_game_max_w(G) * pg_game_max_h(G) + 15) / 16, NQ = (NCH + 63) / 64;
+    uint4 v[NQ];
+    DEV void load(const int8_t *g8) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(g8);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const int k = LANE + 64 * q;
+            v[q] = k < NCH ? src[k] : make_uint4(0, 0, 0, 0);
+        }
+    }
+};
+template <int G>
+DEV void load_grid_lds(Ctx &c, const GridPre<G> &pre) {
     int cells = c.s.main_width * c.s.main_height;
     bool bad = cells > PG_GRID_MAX;
+#ifndef PG_GRID_ROWS
+    if (!bad && c.s.grid8_ok && (cells + 15) / 16 <= GridPre<G>::NCH) { // the prefetched mirror
+#pragma unroll
+        for (int q = 0; q < GridPre<G>::NQ; q++) {
+            const int k = LANE + 64 * q;
+            if (k < (cells + 15) / 16) reinterpret_cast<uint4 *>(c.grid8)[k] = pre.v[q];
+        }
+        c.grid8_ok = true;
+        wave_sync();
+        return;
+    }
+#endif
     if (!bad && c.s.grid8_ok) { // int8 mirror written by the last reset: 4 KB per env
         const uint4 *src = reinterpret_cast<const uint4 *>(c.d.grid8 + (size_t)c.env * PG_GRID_MAX);
 #ifdef PG_GRID_ROWS
@@ -752,34 +779,10 @@ DEV void ent_readlane(const Ent &m, int l, Ent &o) {
 // be loaded lane-parallel up front (lane k <-> k-th smart entity), stepped from registers
 // in the reference's reverse order, and stored lane-parallel at the end.
 
+// The smart entities' steps of step_entities_fast / step_entities_regs from registers (lane k <->
+// smart entity k, index my_i), stored back lane-parallel.
 template <int G>
-DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
-    int n = c.s.num_ents;
-    int nsm = 0;
-    for (int base = 0; base < n; base += 64) {
-        int i = base + LANE;
-        bool smart = i < n && (EI(c, F_FLAGS, i) & EF_SMART_STEP);
-        unsigned long long m = ballot(smart);
-        int pos = nsm + __popcll(m & ((1ull << LANE) - 1ull));
-        if (smart && pos < 64) slist[pos] = (int16_t)i;
-        nsm += __popcll(m);
-    }
-    if (nsm > 64 || !c.ireg) return false;
-    wave_sync();
-    Ent mine;
-    int my_i = LANE < nsm ? slist[LANE] : 0;
-    if (LANE < nsm) load_ent_step(c, my_i, mine);
-    // The non-smart entities' Entity::step touches only their own slots and no smart step reads
-    // them (the only entities a smart step reads are the static interactors, whose Entity::step
-    // leaves x, y, rx, ry and will_erase as they are, and the agent, itself smart), so they are
-    // stepped in one lane-parallel pass -- one round of loads for the whole list instead of one
-    // per run between two smart entities of the reverse loop.
-    for (int base = 0; base < n; base += 64) {
-        int i = base + LANE;
-        if (i < n) entity_step_slot(c, i, true);
-    }
-    c.pt.mark(7); // diagnostic build: interactor list + smart loads + the non-smart pass
-    c.cs.mark(3);
+DEV void smart_steps(Ctx &c, Ent &mine, int my_i, int nsm) {
     // The smart entities' steps are independent of each other as well: a smart step writes only
     // its own entity and reads the grid, the static interactors and the agent (slot 0, stepped
     // last by the reverse loop, so every other smart step sees its pre-step state, which is what
@@ -826,6 +829,124 @@ DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
 #endif
     if (LANE < nsm) store_ent_step(c, my_i, mine);
     wave_sync();
+}
+
+template <int G>
+DEV bool step_entities_fast(Ctx &c, int16_t *slist) {
+    int n = c.s.num_ents;
+    int nsm = 0;
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        bool smart = i < n && (EI(c, F_FLAGS, i) & EF_SMART_STEP);
+        unsigned long long m = ballot(smart);
+        int pos = nsm + __popcll(m & ((1ull << LANE) - 1ull));
+        if (smart && pos < 64) slist[pos] = (int16_t)i;
+        nsm += __popcll(m);
+    }
+    if (nsm > 64 || !c.ireg) return false;
+    wave_sync();
+    Ent mine;
+    int my_i = LANE < nsm ? slist[LANE] : 0;
+    if (LANE < nsm) load_ent_step(c, my_i, mine);
+    // The non-smart entities' Entity::step touches only their own slots and no smart step reads
+    // them (the only entities a smart step reads are the static interactors, whose Entity::step
+    // leaves x, y, rx, ry and will_erase as they are, and the agent, itself smart), so they are
+    // stepped in one lane-parallel pass -- one round of loads for the whole list instead of one
+    // per run between two smart entities of the reverse loop.
+    for (int base = 0; base < n; base += 64) {
+        int i = base + LANE;
+        if (i < n) entity_step_slot(c, i, true);
+    }
+    c.pt.mark(7); // diagnostic build: interactor list + smart loads + the non-smart pass
+    c.cs.mark(3);
+    smart_steps<G>(c, mine, my_i, nsm);
+    return true;
+}
+
+// Lane permutation: lane i's value goes to lane dst (ds_permute_b32; every lane sends to a distinct lane).
+DEV int perm_i(int dst, int v) { return __builtin_amdgcn_ds_permute(dst * 4, v); }
+DEV float perm_f(int dst, float v) { return __int_as_float(__builtin_amdgcn_ds_permute(dst * 4, __float_as_int(v))); }
+
+// build_interactor_list + step_entities for a list of at most 64 entities from ONE round of loads: lane i
+// loads entity i's step fields, and the interactor registers and the smart entities' registers are
+// compacted from them by lane permutes (ballot ranks) instead of an LDS list and a second and third
+// round of loads; the non-smart entities are stepped from the same registers.  The order of effects is
+// step_entities_fast's (see there).  Returns false (nothing done) for longer lists or when the
+// interactors are not static (the LDS-list paths then run).
+template <int G>
+DEV bool step_entities_regs(Ctx &c) {
+    const int n = c.s.num_ents;
+    if (n > 64) return false;
+    const bool have = LANE < n;
+    Ent e;
+    int theme = 0;
+    if (have) {
+        load_ent_step(c, LANE, e);
+        if constexpr (scan_needed<G>(false) || scan_needed<G>(true)) theme = EI(c, F_IMAGE_THEME, LANE);
+    } else {
+        e.type = -1;
+        e.flags = 0;
+    }
+    const unsigned long long below = (1ull << LANE) - 1ull;
+    // ---- interactors (build_interactor_list): lane k <-> the k-th interactor, ascending index
+    c.nlist = 0;
+    c.ireg = true;
+    if constexpr (scan_needed<G>(false) || scan_needed<G>(true)) {
+        const bool in = have && is_interactor<G>(e.type);
+        const unsigned long long mi = ballot(in);
+        const int cnt = __popcll(mi);
+        const int dst = in ? __popcll(mi & below) : cnt + __popcll(~mi & below);
+        const bool stat = !(e.flags & EF_SMART_STEP) && e.vx == 0 && e.vy == 0 && e.grow_rate == 1 && e.expire_time <= 0;
+        if (ballot(in && !stat)) return false;
+        c.nlist = cnt;
+        c.i_idx = perm_i(dst, LANE);
+        c.i_x = perm_f(dst, e.x); c.i_y = perm_f(dst, e.y); c.i_rx = perm_f(dst, e.rx); c.i_ry = perm_f(dst, e.ry);
+        c.i_erase = perm_i(dst, e.flags & EF_WILL_ERASE) != 0;
+        c.i_theme = perm_i(dst, theme);
+        if constexpr (pl_smart<G>()) {
+            if (LANE < cnt) {
+                c.ibox[LANE] = make_float4(c.i_x, c.i_y, c.i_rx, c.i_ry);
+                c.iinfo[LANE] = c.i_idx | (c.i_erase ? (int)0x80000000u : 0);
+            }
+            wave_sync();
+        }
+    }
+    // ---- smart entities: lane k <-> the k-th smart entity, ascending index
+    const bool smart = have && (e.flags & EF_SMART_STEP);
+    const unsigned long long ms = ballot(smart);
+    const int nsm = __popcll(ms);
+    const int sdst = smart ? __popcll(ms & below) : nsm + __popcll(~ms & below);
+    Ent mine;
+    const int my_i = perm_i(sdst, LANE);
+    mine.x = perm_f(sdst, e.x); mine.y = perm_f(sdst, e.y); mine.vx = perm_f(sdst, e.vx); mine.vy = perm_f(sdst, e.vy);
+    mine.rx = perm_f(sdst, e.rx); mine.ry = perm_f(sdst, e.ry); mine.rotation = perm_f(sdst, e.rotation);
+    mine.vrot = perm_f(sdst, e.vrot); mine.alpha = perm_f(sdst, e.alpha); mine.alpha_decay = perm_f(sdst, e.alpha_decay);
+    mine.grow_rate = perm_f(sdst, e.grow_rate); mine.friction = perm_f(sdst, e.friction);
+    mine.type = perm_i(sdst, e.type); mine.image_type = perm_i(sdst, e.image_type);
+    mine.life_time = perm_i(sdst, e.life_time); mine.expire_time = perm_i(sdst, e.expire_time);
+    mine.flags = perm_i(sdst, e.flags);
+    // ---- the non-smart entities' Entity::step from the registers (entity_step_slot: changed words only)
+    if (have && !smart) {
+        Ent o = e;
+        entity_step(o);
+#define PG_SET_IF_CHANGED(F, f) \
+    if (__float_as_uint(o.f) != __float_as_uint(e.f)) EF(c, F, LANE) = o.f;
+        PG_SET_IF_CHANGED(F_X, x)
+        PG_SET_IF_CHANGED(F_Y, y)
+        PG_SET_IF_CHANGED(F_ROTATION, rotation)
+        PG_SET_IF_CHANGED(F_VX, vx)
+        PG_SET_IF_CHANGED(F_VY, vy)
+        PG_SET_IF_CHANGED(F_RX, rx)
+        PG_SET_IF_CHANGED(F_RY, ry)
+        PG_SET_IF_CHANGED(F_ALPHA, alpha)
+#undef PG_SET_IF_CHANGED
+        EI(c, F_LIFE_TIME, LANE) = o.life_time;
+        if (o.flags != e.flags) EI(c, F_FLAGS, LANE) = o.flags;
+        if (o.image_type != e.image_type) EI(c, F_IMAGE_TYPE, LANE) = o.image_type;
+    }
+    c.pt.mark(7); // diagnostic build: interactor list + smart loads + the non-smart pass
+    c.cs.mark(3);
+    smart_steps<G>(c, mine, my_i, nsm);
     return true;
 }
 
@@ -2882,9 +3003,11 @@ DEV void game_step(Ctx &c) {
     wave_sync();
     c.pt.mark(1);
     c.cs.mark(1);
-    build_interactor_list<G>(c);
     c.cs.mark(2);
-    step_entities<G>(c, c.slist);
+    if (!step_entities_regs<G>(c)) {
+        build_interactor_list<G>(c);
+        step_entities<G>(c, c.slist);
+    }
     c.pt.mark(2);
     c.cs.mark(4);
     agent_collisions<G>(c);
@@ -2977,6 +3100,8 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     float *lds_pstk = L.pstk;
     int *lds_iinfo = L.iinfo;
     int8_t *lds_grid = L.grid;
+    GridPre<G> gpre;
+    gpre.load(d.grid8 + (size_t)env * PG_GRID_MAX); // in flight while the scalars load
     Ctx c{d};
     c.moved = L.moved;
     c.env = env;
@@ -3004,7 +3129,7 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     for (int k = 0; k < 6; k++) c.sm[k] = 0;
     c.sm[5] = (uint64_t)c.s.num_ents;
 #endif
-    load_grid_lds<G>(c);
+    load_grid_lds<G>(c, gpre);
     c.cs.mark(0);
 
     int action;
