@@ -1990,49 +1990,91 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                         : (srow0 | ((ncy0 > 1 ? srow1 : 0) << 7) | ((ry0 - jy0) << 14) |
                            ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));
         const int bgrow = bg_lane_row;
-        for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
+#ifndef PG_FAST_PIPE
+#define PG_FAST_PIPE 1 // software-pipelined batches (0: one batch at a time, the round-5 loop)
+#endif
+        // One batch = RB rows: its row infos, then the LDS reads of the batch's tile texel bases, then
+        // every texel load of the batch (branch-free: an absent texel loads pixels[0] and is discarded).
+        // With PG_FAST_PIPE the next batch's loads are issued before this batch blends, so a batch's
+        // gather latency runs under the previous batch's blends and LDS stores.
+        struct FastBatch {
             uint32_t bgv[RB], ta[RB], tb[RB];
-            int info[RB], bgr[RB], ca[RB], cbv[RB];
+            int info[RB];
+        };
+        auto issue = [&](int r0, FastBatch &B) {
+            int bgr[RB], ca[RB], cbv[RB];
 #pragma unroll
             for (int k = 0; k < RB; k++) {
-                info[k] = readlane(rinfo, r0 + k);
+                B.info[k] = readlane(rinfo, r0 + k);
                 bgr[k] = readlane(bgrow, r0 + k);
             }
 #pragma unroll
             for (int k = 0; k < RB; k++) { // LDS reads of the whole batch first
-                ca[k] = colb[((info[k] >> 14) & 31) * 64 + lane];
-                cbv[k] = colb[((info[k] >> 19) & 31) * 64 + lane];
-            }
-#pragma unroll
-            for (int k = 0; k < RB; k++) { // branch-free: an out-of-blit pixel loads pixels[0] and discards it
-                const bool inb = bg_col && bgr[k] >= 0;
-                uint32_t px = bgpix[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
-                bgv[k] = inb ? px : 0xff000000u;
+                ca[k] = colb[((B.info[k] >> 14) & 31) * 64 + lane];
+                cbv[k] = colb[((B.info[k] >> 19) & 31) * 64 + lane];
             }
 #pragma unroll
             for (int k = 0; k < RB; k++) {
-                const int nr = info[k] >> 24;
-                ta[k] = 0;
-                tb[k] = 0;
-                if (nr > 0 && ca[k] >= 0) ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((info[k] & 127) * tile_px<G>())];
-                if (nr > 1 && cbv[k] >= 0) tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((info[k] >> 7) & 127) * tile_px<G>())];
+                const bool inb = bg_col && bgr[k] >= 0;
+#ifdef PG_DIAG_NOBG // diagnostic knockout (wrong frames): no background texel loads
+                const uint32_t px = 0xff000000u | (uint32_t)bgr[k];
+#else
+                const uint32_t px = bgpix[inb ? bg_col_base + (uint32_t)bgr[k] : 0u];
+#endif
+                B.bgv[k] = inb ? px : 0xff000000u;
             }
+#pragma unroll
+            for (int k = 0; k < RB; k++) {
+                const int nr = B.info[k] >> 24;
+                const bool ha = nr > 0 && ca[k] >= 0, hb = nr > 1 && cbv[k] >= 0;
+#ifdef PG_DIAG_NOTILE // diagnostic knockout (wrong frames): no tile texel loads
+                B.ta[k] = ha ? 0xff000000u | (uint32_t)ca[k] : 0u;
+                B.tb[k] = hb ? 0xff000000u | (uint32_t)cbv[k] : 0u;
+#elif defined(PG_FAST_MASKED) // tile texels loaded only by the lanes that draw one (exec-masked loads)
+                B.ta[k] = 0u;
+                B.tb[k] = 0u;
+                if (ha) B.ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((B.info[k] & 127) * tile_px<G>())];
+                if (hb) B.tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((B.info[k] >> 7) & 127) * tile_px<G>())];
+#else
+                const uint32_t pa = d.pixels[ha ? (uint32_t)ca[k] + (uint32_t)((B.info[k] & 127) * tile_px<G>()) : 0u];
+                const uint32_t pb = d.pixels[hb ? (uint32_t)cbv[k] + (uint32_t)(((B.info[k] >> 7) & 127) * tile_px<G>()) : 0u];
+                B.ta[k] = ha ? pa : 0u;
+                B.tb[k] = hb ? pb : 0u;
+#endif
+            }
+        };
+        auto blend = [&](int r0, const FastBatch &B) {
             // a missing tile texel is 0, which blends to the unchanged pixel on either path
             uint32_t part = 0;
 #pragma unroll
-            for (int k = 0; k < RB; k++) part |= alpha_partial(ta[k]) | alpha_partial(tb[k]);
+            for (int k = 0; k < RB; k++) part |= alpha_partial(B.ta[k]) | alpha_partial(B.tb[k]);
             if (!ballot(part != 0)) {
 #pragma unroll
-                for (int k = 0; k < RB; k++) fb[(r0 + k) * PG_RES + lane] = over_binary(over_binary(bgv[k], ta[k]), tb[k]);
+                for (int k = 0; k < RB; k++) fb[(r0 + k) * PG_RES + lane] = over_binary(over_binary(B.bgv[k], B.ta[k]), B.tb[k]);
             } else {
 #pragma unroll
                 for (int k = 0; k < RB; k++) {
-                    const int nr = info[k] >> 24;
-                    uint32_t px = bgv[k];
-                    if (nr > 0) px = ta[k] + BYTE_MUL(px, (~ta[k]) >> 24);
-                    if (nr > 1) px = tb[k] + BYTE_MUL(px, (~tb[k]) >> 24);
+                    const int nr = B.info[k] >> 24;
+                    uint32_t px = B.bgv[k];
+                    if (nr > 0) px = B.ta[k] + BYTE_MUL(px, (~B.ta[k]) >> 24);
+                    if (nr > 1) px = B.tb[k] + BYTE_MUL(px, (~B.tb[k]) >> 24);
                     fb[(r0 + k) * PG_RES + lane] = px;
                 }
+            }
+        };
+        if (PG_FAST_PIPE) {
+            FastBatch cur, nxt;
+            issue(fb.y0, cur);
+            for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
+                if (r0 + RB < fb.y0 + fb.h) issue(r0 + RB, nxt);
+                blend(r0, cur);
+                cur = nxt;
+            }
+        } else {
+            for (int r0 = fb.y0; r0 < fb.y0 + fb.h; r0 += RB) {
+                FastBatch cur;
+                issue(r0, cur);
+                blend(r0, cur);
             }
         }
         wave_sync();

@@ -72,10 +72,18 @@ extern "C" int d2h_probe(void) {
         CK(hipDeviceSynchronize());
         printf("D two copies on streams 0, 1: %.2f ms\n", since(t0) * 1e3);
     }
+    // release everything before returning to the caller: the round-5 Python run under rocprofv3 left the
+    // streams, the event and both device buffers to the runtime's static teardown, and a destructor then ran
+    // after the HIP / profiler libraries were gone (SIGSEGV in __cxa_finalize, gpurun_out/n/torch.log)
+    CK(hipDeviceSynchronize());
+    for (int i = 0; i < 5; i++) CK(hipStreamDestroy(s[i]));
+    CK(hipEventDestroy(ev));
     CK(hipHostUnregister(h));
     CK(hipHostUnregister(h2));
     free(h);
     free(h2);
+    CK(hipFree(d));
+    CK(hipFree(scratch));
     return 0;
 }
 
@@ -96,6 +104,7 @@ extern "C" int d2h_probe_host(void *h) {
         CK(hipStreamSynchronize(s));
         printf("E caller buffer %p: kernel + copy %.2f ms\n", h, since(t0) * 1e3);
     }
+    CK(hipStreamSynchronize(s));
     CK(hipHostUnregister(h));
     CK(hipStreamDestroy(s));
     CK(hipFree(d));
@@ -141,6 +150,10 @@ extern "C" int d2h_probe_engine_like(void) {
     if (timed("H destination at +16 B", (uint8_t *)h + 16, d, s, 0)) return 1;
     if (timed("I hipMemcpyDefault", h, d, s, 1)) return 1;
     if (timed("I hipMemcpyDtoHAsync", h, d, s, 2)) return 1;
+    CK(hipDeviceSynchronize());
+    CK(hipStreamDestroy(s));
+    CK(hipStreamDestroy(ph));
+    CK(hipStreamDestroy(pl));
     CK(hipHostUnregister(h));
     free(h);
     CK(hipFree(d));

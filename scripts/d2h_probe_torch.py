@@ -21,4 +21,7 @@ rc = lib.d2h_probe()
 import numpy as np  # noqa: E402
 buf = np.empty(32768 * 12288, np.uint8)
 lib.d2h_probe_host.argtypes = [ctypes.c_void_p]
-sys.exit(rc or lib.d2h_probe_host(buf.ctypes.data))
+rc = rc or lib.d2h_probe_host(buf.ctypes.data)
+if mode == "torch":
+    torch.cuda.synchronize()
+sys.exit(rc)

@@ -46,6 +46,19 @@ for stage in ${DO:-smoke tests}; do
   speed)  # the reference's speed-test shape (scripts/speed_shape.py)
     timeout -k 10 900 python3 scripts/speed_shape.py > gpurun_out/speed_shape.json 2> gpurun_out/speed_shape.err || { tail -5 gpurun_out/speed_shape.err; exit 16; }
     tail -16 gpurun_out/speed_shape.err ;;
+  phase)  # per-phase cycle shares of step and render (PROFILE=1 build libprocgen_mi355x_prof.so), per game in PHASE_GAMES
+    for g in ${PHASE_GAMES:-coinrun}; do
+      timeout -k 10 300 python3 scripts/phase_profile.py $g > gpurun_out/phase_$g.json 2> gpurun_out/phase_$g.err || { tail -5 gpurun_out/phase_$g.err; exit 17; }
+      cat gpurun_out/phase_$g.json
+    done ;;
+  probe)  # the host-path D2H probe inside a torch process under the memory-copy trace (teardown check)
+    timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/probe -o run -- python3 scripts/d2h_probe_torch.py torch > gpurun_out/probe.log 2>&1
+    rc=$?; grep -v "^W2026" gpurun_out/probe.log | tail -14; [ $rc -eq 0 ] || exit $rc ;;
+  teardown)  # which process crashes at exit under the memory-copy trace: torch alone, then the probe without torch
+    timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/td_torch -o run -- python3 -c "import torch; torch.zeros(1, device='cuda'); torch.cuda.synchronize(); print('torch alone ok')" > gpurun_out/td_torch.log 2>&1
+    rc=$?; echo "torch alone under rocprofv3: rc=$rc"; grep -v "^W2026" gpurun_out/td_torch.log | tail -3; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/td_plain -o run -- python3 scripts/d2h_probe_torch.py plain > gpurun_out/td_plain.log 2>&1
+    rc=$?; echo "probe without torch under rocprofv3: rc=$rc"; grep -v "^W2026" gpurun_out/td_plain.log | tail -3; [ $rc -eq 0 ] || exit $rc ;;
   bench)
     timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -5 gpurun_out/bench.err; exit 14; }
     cat gpurun_out/bench.json ;;
