@@ -1601,12 +1601,25 @@ DEV constexpr int frame_rows() {
     // bossfight (48 rotated-image descriptors of LDS), jumper (compass overlay; 170 VGPRs spill) and
     // fruitbot (tile lists), which keep one full-frame pass at 2 waves per SIMD
 #ifdef PG_CR_ROWS
-    if (G == PG_GAME_COINRUN) return PG_CR_ROWS; // experiment: coinrun's LDS frame in passes of fewer rows
+    if (G == PG_GAME_COINRUN) return PG_CR_ROWS; // experiment: coinrun's LDS frame in passes of other sizes
+#endif
+    // coinrun and starpilot: four 16-row passes (a 4 KB frame: coinrun's workgroup needs 8 KB of LDS, 16
+    // resident per CU at 4 waves per SIMD instead of 13): coinrun 44.1 -> 46.1, starpilot 35.5 -> 40.1 M
+    // env-steps/s; heist, caveflyer, leaper and plunder lose 5-19 % with them, dodgeball ties
+    // (profiles/r06/r06_f_render_ab.txt, r06_g_rows16.txt)
+    if (G == PG_GAME_COINRUN || G == PG_GAME_STARPILOT) return 16;
+#ifdef PG_ROWS16_ALL
+    if (G != PG_GAME_BOSSFIGHT && G != PG_GAME_JUMPER && G != PG_GAME_FRUITBOT) return 16; // experiment
 #endif
     return (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT) ? 64 : 32;
 }
 template <int G>
-DEV constexpr int render_waves() { return frame_rows<G>() < 32 ? 4 : (frame_rows<G>() == 32 ? 3 : 2); }
+DEV constexpr int render_waves() {
+#ifdef PG_CR_WAVES
+    if (G == PG_GAME_COINRUN) return PG_CR_WAVES; // experiment: coinrun's waves per SIMD (register budget)
+#endif
+    return frame_rows<G>() < 32 ? 4 : (frame_rows<G>() == 32 ? 3 : 2);
+}
 // rotated-image descriptors per 64-entity chunk (beyond them an image takes the in-order setup)
 template <int G>
 DEV constexpr int rot_cap() {
@@ -1855,20 +1868,31 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
     int nrows = 0, jy0 = 0;
     bool fast = false;
     if (uniform_tiles<G>() && !has_z_minus1<G>() && tab) {
-        // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images
-        for (int x = xg - 2; x <= xg + 2; x++) {
+        // tile columns covering screen column `lane` (<= 2, ascending x) for TILE_PX-wide images, and
+        // tile rows covering screen row `lane` (<= 2, ascending y = the reference's draw order): the five
+        // candidate table entries of each axis are read first (one LDS round trip), then scanned
+        int4 tc[5], tr[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            tc[q] = colax[min(max(xg - 2 + q - low_x, 0), 63)];
+            tr[q] = rowax[min(max(yg - 2 + q - low_y, 0), 63)];
+        }
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const int x = xg - 2 + q;
             if (x < low_x || x > high_x || ncx0 == 2) continue;
-            const int4 t = colax[x - low_x];
+            const int4 t = tc[q];
             if (t.y > 0 && lane >= t.x && lane < t.x + t.y) {
                 int scv = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
                 if (ncx0 == 0) { cx0 = x; scol0 = scv; } else { cx1 = x; scol1 = scv; }
                 ncx0++;
             }
         }
-        // tile rows covering screen row `lane` (<= 2, ascending y = the reference's draw order)
-        for (int y = yg - 2; y <= yg + 2; y++) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const int y = yg - 2 + q;
             if (y < low_y || y > high_y || ncy0 == 2) continue;
-            const int4 t = rowax[y - low_y];
+            const int4 t = tr[q];
             if (t.y > 0 && lane >= t.x && lane < t.x + t.y) {
                 int srv = (int)(((uint32_t)t.z + (uint32_t)((lane - t.x) * t.w)) >> 16);
                 if (ncy0 == 0) { ry0 = y; srow0 = srv; } else { ry1 = y; srow1 = srv; }
@@ -1884,6 +1908,9 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
         jy0 = jlo;
         nrows = jhi >= jlo ? jhi - jlo + 1 : 0;
         fast = nrows <= CR;
+#ifdef PG_PROF_RSETUP // diagnostic: the fast path's setup split (slot 2: window column / row scan)
+        pt.mark(2);
+#endif
         if constexpr (!always_uniform<G>()) {
             if (fast) { // every tile of the window must be a tile_px() square (or nothing)
                 bool other = false;
@@ -1923,11 +1950,21 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
             }
         }
         wave_sync(); // colb's axis-table contents are dead from here
+#ifdef PG_PROF_RSETUP // (slot 5: the tile codes' grid loads)
+        pt.mark(5);
+#endif
+        // every row's table read first, then the writes (tile_off and colb share the aux array, so the
+        // compiler would otherwise order each read after the previous row's write)
+        int cj[CR];
+#pragma unroll
+        for (int j = 0; j < CR; j++) {
+            const int t = code[j];
+            cj[j] = (ncx0 == 0 || t == INVALID_OBJ || t == SPACE) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
+        }
 #pragma unroll
         for (int j = 0; j < CR; j++) {
             if (j < nrows) {
-                int t = code[j];
-                int c = (ncx0 == 0 || t == INVALID_OBJ || t == SPACE) ? -1 : ((t >= 0 && t < NTYPES) ? tile_off[t] : -2);
+                const int c = cj[j];
                 if (c <= -2) err = true;
                 colb[j * 64 + lane] = c >= 0 ? c + scol0 : -1;
             }
@@ -1991,7 +2028,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                            ((ncy0 > 1 ? ry1 - jy0 : ry0 - jy0) << 19) | (ncy0 << 24));
         const int bgrow = bg_lane_row;
 #ifndef PG_FAST_PIPE
-#define PG_FAST_PIPE 1 // software-pipelined batches (0: one batch at a time, the round-5 loop)
+#define PG_FAST_PIPE 0 // 1: software-pipelined batches (measured neutral at one workgroup fewer per CU, r06_e)
 #endif
         // One batch = RB rows: its row infos, then the LDS reads of the batch's tile texel bases, then
         // every texel load of the batch (branch-free: an absent texel loads pixels[0] and is discarded).
@@ -2030,16 +2067,16 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #ifdef PG_DIAG_NOTILE // diagnostic knockout (wrong frames): no tile texel loads
                 B.ta[k] = ha ? 0xff000000u | (uint32_t)ca[k] : 0u;
                 B.tb[k] = hb ? 0xff000000u | (uint32_t)cbv[k] : 0u;
-#elif defined(PG_FAST_MASKED) // tile texels loaded only by the lanes that draw one (exec-masked loads)
-                B.ta[k] = 0u;
-                B.tb[k] = 0u;
-                if (ha) B.ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((B.info[k] & 127) * tile_px<G>())];
-                if (hb) B.tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((B.info[k] >> 7) & 127) * tile_px<G>())];
-#else
+#elif defined(PG_FAST_BRANCHFREE) // experiment: every lane loads (measured slower, r06_e r8p0)
                 const uint32_t pa = d.pixels[ha ? (uint32_t)ca[k] + (uint32_t)((B.info[k] & 127) * tile_px<G>()) : 0u];
                 const uint32_t pb = d.pixels[hb ? (uint32_t)cbv[k] + (uint32_t)(((B.info[k] >> 7) & 127) * tile_px<G>()) : 0u];
                 B.ta[k] = ha ? pa : 0u;
                 B.tb[k] = hb ? pb : 0u;
+#else // tile texels loaded only by the lanes that draw one (exec-masked loads: sky lanes issue none)
+                B.ta[k] = 0u;
+                B.tb[k] = 0u;
+                if (ha) B.ta[k] = d.pixels[(uint32_t)ca[k] + (uint32_t)((B.info[k] & 127) * tile_px<G>())];
+                if (hb) B.tb[k] = d.pixels[(uint32_t)cbv[k] + (uint32_t)(((B.info[k] >> 7) & 127) * tile_px<G>())];
 #endif
             }
         };
