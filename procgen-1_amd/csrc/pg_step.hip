@@ -388,6 +388,9 @@ DEV constexpr int interactor_type() {
 }
 template <int G>
 DEV bool is_interactor(int type) { return interactor_type<G>() >= 0 && type == interactor_type<G>(); }
+// games whose scan can only reflect the stepped object (no is_blocked_ents, hence no push chain)
+template <int G>
+DEV constexpr bool scan_reflects_only() { return G == PG_GAME_DODGEBALL; }
 
 // Largest interactor index i < upper (i != oi, !will_erase) with has_collision(obj, e_i, POS_EPS),
 // i.e. the next entity the reference's reverse loop would act on; lane-parallel over the list.
@@ -446,7 +449,8 @@ DEV constexpr bool pl_smart() {
 #ifdef PG_PL_ALL
     return true;
 #else
-    return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER;
+    return G == PG_GAME_CHASER || G == PG_GAME_CLIMBER || G == PG_GAME_NINJA || G == PG_GAME_CAVEFLYER ||
+           G == PG_GAME_DODGEBALL;
 #endif
 }
 
@@ -564,8 +568,11 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
 #ifdef PG_PROF_SMART
     c.sm[1] += 1;
 #endif
-    // the frame stack is wave-uniform LDS: the lane-parallel (PL) games never scan
-    static_assert(!PL || (!scan_needed<G>(true) && !scan_needed<G>(false)), "PL games have no push chain");
+    // the frame stack is wave-uniform LDS: the lane-parallel (PL) games never push -- they do not scan, or
+    // (dodgeball) their scan only reflects: its one interactor type, LAVA_WALL, is neither WALL_OBJ nor the
+    // out-of-bounds object, so is_blocked_ents never fires (dodgeball.cpp:98-100)
+    static_assert(!PL || (!scan_needed<G>(true) && !scan_needed<G>(false)) || scan_reflects_only<G>(),
+                  "PL games have no push chain");
     constexpr int MAXD = 5;
     int d = 0;
     bool fresh = true, acc = false;
@@ -644,7 +651,7 @@ DEV bool sub_step(Ctx &c, int oi, Ent &o, float _vx, float _vy) {
             if (!(PL ? next_collider_pl(c, oi, upper, o, m) : next_collider(c, oi, upper, o, m))) break;
             upper = m.m;
             constexpr int mtype = interactor_type<G>(); // the scan lists hold only this type
-            if (is_blocked_ents<G>(c, o.type, m, mtype, is_h, oi, o)) {
+            if (!PL && is_blocked_ents<G>(c, o.type, m, mtype, is_h, oi, o)) {
                 acc = true; // block2 = block2 || curr_block
                 float t_vx, t_vy;
                 push_offset(m, o, is_h, t_vx, t_vy);
@@ -1591,12 +1598,54 @@ DEV void handle_collision(Ctx &c, int si, int ti) {
     wave_sync();
 }
 
+// The collision walk's view of the entity list (lane = entity, lists of at most 64): the fields the
+// walks test, loaded in one round instead of one round per scan.  A handler may change any entity or
+// append one, so the cache is reloaded after every handler call (handlers are rare; scans are not).
+struct ColCache {
+    float x, y, rx, ry, mrg;
+    int type, flags;
+    bool ok; // the list fits one lane each and the registers hold HBM's current values
+};
+DEV void col_load(Ctx &c, ColCache &k) {
+    k.ok = c.s.num_ents <= 64;
+    if (!k.ok) return;
+    const int i = LANE;
+    if (i < c.s.num_ents) {
+        k.x = EF(c, F_X, i); k.y = EF(c, F_Y, i); k.rx = EF(c, F_RX, i); k.ry = EF(c, F_RY, i);
+        k.mrg = EF(c, F_COLLISION_MARGIN, i); k.type = EI(c, F_TYPE, i); k.flags = EI(c, F_FLAGS, i);
+    } else {
+        k.x = k.y = k.rx = k.ry = k.mrg = 0;
+        k.type = -1;
+        k.flags = EF_WILL_ERASE;
+    }
+}
+
 // the inner loop of an entity with collides_with_entities: j descending, j != i, while neither
 // side is will_erase
 template <int G>
-DEV void entity_collisions(Ctx &c, int i) {
+DEV void entity_collisions(Ctx &c, int i, ColCache &k) {
     int upper = c.s.num_ents;
     while (upper > 0) {
+        if (k.ok) { // from the registers: one scan of <= 64 lanes
+            if (rli(k.flags, i) & EF_WILL_ERASE) return;
+            const float x = rlf(k.x, i), y = rlf(k.y, i), rx = rlf(k.rx, i), ry = rlf(k.ry, i), mrg = rlf(k.mrg, i);
+            const int j = LANE;
+            bool relevant = true;
+            if constexpr (G == PG_GAME_CAVEFLYER) relevant = k.type == CF_PLAYER_BULLET;
+            bool hit = false;
+            if (relevant && j < upper && j != i && !(k.flags & EF_WILL_ERASE)) {
+                float tx = (rx + k.rx) + mrg, ty = (ry + k.ry) + mrg;
+                hit = (fabsf(x - k.x) < tx) && (fabsf(y - k.y) < ty);
+            }
+            const unsigned long long b = ballot(hit);
+            if (!b) return;
+            const int m = top_bit(b);
+            handle_collision<G>(c, i, m);
+            wave_sync();
+            col_load(c, k);
+            upper = m;
+            continue;
+        }
         if (EI(c, F_FLAGS, i) & EF_WILL_ERASE) return;
         const float x = EF(c, F_X, i), y = EF(c, F_Y, i), rx = EF(c, F_RX, i), ry = EF(c, F_RY, i);
         const float mrg = EF(c, F_COLLISION_MARGIN, i);
@@ -1743,9 +1792,37 @@ DEV void agent_collisions(Ctx &c) {
         }
     } else {
         int upper = c.s.num_ents;
+        ColCache k;
+        col_load(c, k);
         while (upper > 0) {
             // the reference's `agent` (a ghost once erased from `entities`, miner.cpp:329)
             const bool gh = c.s.agent_erased;
+            if (k.ok) { // the same walk from the registers (lists of <= 64), reloaded after every handler
+                const float ax = gh ? c.s.ghost_x : rlf(k.x, 0), ay = gh ? c.s.ghost_y : rlf(k.y, 0);
+                const float arx = gh ? c.s.ghost_rx : rlf(k.rx, 0), ary = gh ? c.s.ghost_ry : rlf(k.ry, 0);
+                const int i = LANE;
+                bool hit = false, coll = false;
+                if (i < upper) {
+                    if (k.type != PLAYER && (gh || i != 0)) { // has_agent_collision (:1135-1140)
+                        float tx = (k.rx + arx) + k.mrg, ty = (k.ry + ary) + k.mrg;
+                        hit = (fabsf(k.x - ax) < tx) && (fabsf(k.y - ay) < ty);
+                    }
+                    coll = (k.flags & EF_COLLIDES) != 0;
+                }
+                const unsigned long long b = ballot(hit || coll);
+                if (!b) break;
+                const int m = top_bit(b);
+                if (ballot(hit && i == m)) {
+                    handle_agent_collision<G>(c, m);
+                    wave_sync();
+                    col_load(c, k);
+                } else {
+                    wave_sync();
+                }
+                if (k.ok ? (rli(k.flags, m) & EF_COLLIDES) : (EI(c, F_FLAGS, m) & EF_COLLIDES)) entity_collisions<G>(c, m, k);
+                upper = m;
+                continue;
+            }
             const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
             const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
             int m = -1;
@@ -1771,7 +1848,7 @@ DEV void agent_collisions(Ctx &c) {
             if (m < 0) break;
             if (agent_hit) handle_agent_collision<G>(c, m);
             wave_sync();
-            if (EI(c, F_FLAGS, m) & EF_COLLIDES) entity_collisions<G>(c, m);
+            if (EI(c, F_FLAGS, m) & EF_COLLIDES) entity_collisions<G>(c, m, k);
             upper = m;
         }
     }
