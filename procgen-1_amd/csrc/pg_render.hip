@@ -1608,10 +1608,15 @@ DEV constexpr int frame_rows() {
     // env-steps/s; heist, caveflyer, leaper and plunder lose 5-19 % with them, dodgeball ties
     // (profiles/r06/r06_f_render_ab.txt, r06_g_rows16.txt)
     if (G == PG_GAME_COINRUN || G == PG_GAME_STARPILOT) return 16;
+#ifdef PG_ROWS32_ONEPASS
+    if (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT) return PG_ROWS32_ONEPASS; // experiment
+#endif
 #ifdef PG_ROWS16_ALL
     if (G != PG_GAME_BOSSFIGHT && G != PG_GAME_JUMPER && G != PG_GAME_FRUITBOT) return 16; // experiment
 #endif
-    return (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER || G == PG_GAME_FRUITBOT) ? 64 : 32;
+    // fruitbot: two 32-row passes since round 6 (17.7 -> 18.8 M env-steps/s, profiles/r06/r06_j_onepass.txt;
+    // bossfight and jumper still lose 6-16 % with them, and more with 16-row passes)
+    return (G == PG_GAME_BOSSFIGHT || G == PG_GAME_JUMPER) ? 64 : 32;
 }
 template <int G>
 DEV constexpr int render_waves() {
