@@ -5,6 +5,7 @@
 // and every env is then drawn by pg_render.  The kernel is a template over the game id:
 // the physics core is shared, the reference's virtual hooks are `if constexpr` branches.
 #include "pg_device.h"
+#include <utility>
 
 namespace {
 
@@ -12,6 +13,9 @@ struct Ctx {
     // the kernel argument itself (by reference: its fields are loaded from the kernarg segment where they
     // are used; a by-value copy here loaded every pointer at entry and spilled them for the whole step)
     const PGDev &d;
+    // the env's scalars in HBM, for the agent's ghost only (ghost_*: read and written where the agent is
+    // erased, a rare path -- kept out of the registers the whole step would otherwise hold them in)
+    PGEnv *gp;
     int env;
     PGEnv s;        // uniform copy of this env's scalars
     char *Eb;       // this env's entity block (pg_ent_index): field f of slot i at byte (f * PG_CAP + i) * 4
@@ -1006,8 +1010,8 @@ DEV void erase_if_needed(Ctx &c) {
         bool er = (a.flags & EF_WILL_ERASE) || ((a.flags & EF_AUTO_ERASE) && is_out_of_bounds(c, a.x, a.y, a.rx, a.ry));
         if (er) {
             c.s.agent_erased = 1;
-            c.s.ghost_x = a.x; c.s.ghost_y = a.y; c.s.ghost_vx = a.vx; c.s.ghost_vy = a.vy;
-            c.s.ghost_rx = a.rx; c.s.ghost_ry = a.ry;
+            c.gp->ghost_x = a.x; c.gp->ghost_y = a.y; c.gp->ghost_vx = a.vx; c.gp->ghost_vy = a.vy;
+            c.gp->ghost_rx = a.rx; c.gp->ghost_ry = a.ry;
         }
     }
     int kept = 0;
@@ -1713,8 +1717,8 @@ DEV void agent_collisions(Ctx &c) {
         // collides_with_entities loop calls the empty base handle_collision
         int upper = c.s.num_ents;
         const bool gh = c.s.agent_erased;
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
-        const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
+        const float arx = gh ? c.gp->ghost_rx : EF(c, F_RX, 0), ary = gh ? c.gp->ghost_ry : EF(c, F_RY, 0);
         while (upper > 0) {
             int m = -1;
             bool agent_hit = false;
@@ -1798,8 +1802,8 @@ DEV void agent_collisions(Ctx &c) {
             // the reference's `agent` (a ghost once erased from `entities`, miner.cpp:329)
             const bool gh = c.s.agent_erased;
             if (k.ok) { // the same walk from the registers (lists of <= 64), reloaded after every handler
-                const float ax = gh ? c.s.ghost_x : rlf(k.x, 0), ay = gh ? c.s.ghost_y : rlf(k.y, 0);
-                const float arx = gh ? c.s.ghost_rx : rlf(k.rx, 0), ary = gh ? c.s.ghost_ry : rlf(k.ry, 0);
+                const float ax = gh ? c.gp->ghost_x : rlf(k.x, 0), ay = gh ? c.gp->ghost_y : rlf(k.y, 0);
+                const float arx = gh ? c.gp->ghost_rx : rlf(k.rx, 0), ary = gh ? c.gp->ghost_ry : rlf(k.ry, 0);
                 const int i = LANE;
                 bool hit = false, coll = false;
                 if (i < upper) {
@@ -1823,8 +1827,8 @@ DEV void agent_collisions(Ctx &c) {
                 upper = m;
                 continue;
             }
-            const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
-            const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
+            const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
+            const float arx = gh ? c.gp->ghost_rx : EF(c, F_RX, 0), ary = gh ? c.gp->ghost_ry : EF(c, F_RY, 0);
             int m = -1;
             bool agent_hit = false;
             for (int base = (upper - 1) & ~63; base >= 0; base -= 64) {
@@ -1942,7 +1946,7 @@ DEV void coinrun_step_tail(Ctx &c) { // coinrun.cpp:474-498
     }
     c.s.num_ents = n + total_enemies;
     wave_sync();
-    c.s.last_agent_y = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+    c.s.last_agent_y = c.s.agent_erased ? c.gp->ghost_y : EF(c, F_Y, 0);
 }
 
 // bigfish.cpp:84: (FISH_MAX_R - FISH_MIN_R) * pow(rand01(), 1.4) + FISH_MIN_R -- pow(float, double)
@@ -2051,8 +2055,8 @@ DEV void mn_mark(Ctx &c, int idx) {
     if (LANE == 0) c.moved[idx] |= 1;
     wave_sync();
 }
-DEV float mn_ax(Ctx &c) { return c.s.agent_erased ? c.s.ghost_x : EF(c, F_X, 0); }
-DEV float mn_ay(Ctx &c) { return c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0); }
+DEV float mn_ax(Ctx &c) { return c.s.agent_erased ? c.gp->ghost_x : EF(c, F_X, 0); }
+DEV float mn_ay(Ctx &c) { return c.s.agent_erased ? c.gp->ghost_y : EF(c, F_Y, 0); }
 DEV int mn_agent_index(Ctx &c) { return (int)mn_ay(c) * c.s.main_width + (int)mn_ax(c); } // miner.cpp:98-100
 DEV int mn_moving(int t) { return t == MN_DIAMOND ? MN_MOVING_DIAMOND : (t == MN_BOULDER ? MN_MOVING_BOULDER : t); }
 DEV bool mn_is_moving(int t) { return t == MN_MOVING_BOULDER || t == MN_MOVING_DIAMOND; }
@@ -2069,8 +2073,8 @@ DEV void mn_erase_agent(Ctx &c) {
         return;
     }
     c.s.agent_erased = 1;
-    c.s.ghost_x = EF(c, F_X, 0); c.s.ghost_y = EF(c, F_Y, 0); c.s.ghost_vx = EF(c, F_VX, 0);
-    c.s.ghost_vy = EF(c, F_VY, 0); c.s.ghost_rx = EF(c, F_RX, 0); c.s.ghost_ry = EF(c, F_RY, 0);
+    c.gp->ghost_x = EF(c, F_X, 0); c.gp->ghost_y = EF(c, F_Y, 0); c.gp->ghost_vx = EF(c, F_VX, 0);
+    c.gp->ghost_vy = EF(c, F_VY, 0); c.gp->ghost_rx = EF(c, F_RX, 0); c.gp->ghost_ry = EF(c, F_RY, 0);
     const int n = c.s.num_ents;
     for (int base = 1; base < n; base += 64) { // order-preserving shift down by one
         int i = base + LANE;
@@ -2298,9 +2302,9 @@ DEV void leaper_pre_step(Ctx &c) { // leaper.cpp:253-256 (frog animation)
 DEV void leaper_step_tail(Ctx &c, uint32_t *rg) { // leaper.cpp:258-287
     lp_spawn_entities(c, rg);
     const bool gh = c.s.agent_erased; // the reference's `agent` outlives its erase
-    const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
-    const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0), ary = gh ? c.s.ghost_ry : EF(c, F_RY, 0);
-    const float avx = gh ? c.s.ghost_vx : EF(c, F_VX, 0), avy = gh ? c.s.ghost_vy : EF(c, F_VY, 0);
+    const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
+    const float arx = gh ? c.gp->ghost_rx : EF(c, F_RX, 0), ary = gh ? c.gp->ghost_ry : EF(c, F_RY, 0);
+    const float avx = gh ? c.gp->ghost_vx : EF(c, F_VX, 0), avy = gh ? c.gp->ghost_vy : EF(c, F_VY, 0);
     // the last LOG (list order) the agent stands on gives log_vx
     const float margin = -1 * arx;
     int last = -1;
@@ -2323,7 +2327,7 @@ DEV void leaper_step_tail(Ctx &c, uint32_t *rg) { // leaper.cpp:258-287
     if (standing_on_log) nx = ax + log_vx;
     wave_sync();
     if (standing_on_log) {
-        if (gh) c.s.ghost_x = nx;
+        if (gh) c.gp->ghost_x = nx;
         else EF(c, F_X, 0) = nx;
     }
     if (is_out_of_bounds(c, nx, ay, arx, ary)) c.s.sd_done = 1;
@@ -2375,8 +2379,8 @@ DEV void chaser_step_tail(Ctx &c) {
     const bool can_eat = c.s.cur_time - c.s.eat_time < c.s.eat_timeout;
     const float default_enemy_speed = .5;
     const float vscale = can_eat ? (default_enemy_speed * .5f) : default_enemy_speed;
-    const float ax = c.s.agent_erased ? c.s.ghost_x : EF(c, F_X, 0);
-    const float ay = c.s.agent_erased ? c.s.ghost_y : EF(c, F_Y, 0);
+    const float ax = c.s.agent_erased ? c.gp->ghost_x : EF(c, F_X, 0);
+    const float ay = c.s.agent_erased ? c.gp->ghost_y : EF(c, F_Y, 0);
     const int agent_idx = ch_to_grid_idx(c, (int)ax, (int)ay);
     const bool be_agressive = c.s.step_rand_int % 2 == 0;
     const int dist_scale = can_eat ? -1 : 1;
@@ -2536,7 +2540,7 @@ DEV void dodgeball_step_tail(Ctx &c, uint32_t *rg) { // :378-444
     const bool gh = c.s.agent_erased;
     if (!gh) EF(c, F_ROTATION, 0) = face_rotation(vx, vy, EF(c, F_ROTATION, 0));
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 7) {
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
         wave_sync();
         const int b = append_entity(c, ax, ay, vx * c.s.db_ball_vscale, vy * c.s.db_ball_vscale, c.s.db_ball_r,
                                     c.s.db_ball_r, DB_PLAYER_BALL);
@@ -2584,7 +2588,7 @@ DEV void dodgeball_step_tail(Ctx &c, uint32_t *rg) { // :378-444
         else EI(c, F_SPAWN_TIME, m) = st - 1;
         wave_sync();
         if ((c.s.cur_time - EI(c, F_FIRE_TIME, m)) >= c.s.enemy_fire_delay) {
-            const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+            const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
             const float ex = EF(c, F_X, m), ey = EF(c, F_Y, m);
             const float dx = ex - ax, dy = ey - ay;
             const float bvelx = (float)(ex < ax ? 1 : -1);
@@ -2647,7 +2651,7 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     }
     const bool gh = c.s.agent_erased;
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 3) {
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
         wave_sync();
         const int b = append_entity(c, ax, ay, 0, 1, .25f, .25f, PL_PLAYER_BULLET);
         if (b >= 0) {
@@ -2666,7 +2670,7 @@ DEV void plunder_step_tail(Ctx &c, uint32_t *rg) {
     }
     wave_sync();
     if (gh) {
-        if (c.s.ghost_x < P.min_agent_x) c.s.ghost_x = P.min_agent_x;
+        if (c.gp->ghost_x < P.min_agent_x) c.gp->ghost_x = P.min_agent_x;
     } else if (EF(c, F_X, 0) < P.min_agent_x) {
         EF(c, F_X, 0) = P.min_agent_x;
     }
@@ -2776,7 +2780,7 @@ DEV void ninja_step_tail(Ctx &c) {
         if (refl) theta = PI_F - theta;
         double sn, cs;
         pg_sincos_cr((double)theta, &sn, &cs);
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
         wave_sync();
         const int b = append_entity(c, ax, ay, (float)(bullet_vel * cs), (float)(bullet_vel * sn), .25f, .25f,
                                     NJ_THROWING_STAR);
@@ -2837,7 +2841,7 @@ DEV void bossfight_step_tail(Ctx &c, uint32_t *rg) {
     wave_sync();
     const bool gh = c.s.agent_erased;
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= 3) {
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
         wave_sync();
         const int e = append_entity(c, ax, ay, 0, 1, .25f, .25f, BF_PLAYER_BULLET);
         if (e >= 0) {
@@ -2928,7 +2932,7 @@ DEV void sp_copy_slot(Ctx &c, int from, int to) {
 DEV void starpilot_step_tail(Ctx &c, uint32_t *rg) {
     const int mode = c.s.opt_distribution_mode;
     const bool gh = c.s.agent_erased;
-    const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+    const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
     const bool is_firing = c.s.special_action != 0;
     // entities that fire (should_fire, :356-366) or blow up, descending; each appends in order
     const int n0 = c.s.num_ents;
@@ -3001,7 +3005,7 @@ DEV void starpilot_step_tail(Ctx &c, uint32_t *rg) {
         double st, ct;
         pg_sincos_cr((double)theta, &st, &ct);
         const float vx = (float)(ct * v_scale), vy = (float)(st * v_scale);
-        const float arx = gh ? c.s.ghost_rx : EF(c, F_RX, 0);
+        const float arx = gh ? c.gp->ghost_rx : EF(c, F_RX, 0);
         const float x_off = (float)(arx * ct);
         wave_sync();
         const int b = append_entity(c, ax + x_off, ay, vx, vy, sp_hp_bullet_r(mode), sp_hp_bullet_r(mode), SP_BULLET_PLAYER);
@@ -3028,7 +3032,7 @@ DEV void starpilot_step_tail(Ctx &c, uint32_t *rg) {
 DEV void fruitbot_step_tail(Ctx &c) { // fruitbot.cpp:247-258
     if (c.s.special_action == 1 && (c.s.cur_time - c.s.last_fire_time) >= FB_KEY_DURATION) {
         const bool gh = c.s.agent_erased;
-        const float ax = gh ? c.s.ghost_x : EF(c, F_X, 0), ay = gh ? c.s.ghost_y : EF(c, F_Y, 0);
+        const float ax = gh ? c.gp->ghost_x : EF(c, F_X, 0), ay = gh ? c.gp->ghost_y : EF(c, F_Y, 0);
         const float vx = 0, vy = 1, bullet_vscale = .5;
         wave_sync();
         int i = append_entity(c, ax, ay, vx * bullet_vscale, vy * bullet_vscale, .25f, .25f, FB_PLAYER_BULLET);
@@ -3064,8 +3068,8 @@ DEV void game_step(Ctx &c) {
     set_action_xy<G>(c, c.s.move_action);
     if (c.s.grid_step) {
         if (c.s.agent_erased) { // the erased agent's shared_ptr still takes the velocity
-            c.s.ghost_vx = c.s.action_vx;
-            c.s.ghost_vy = c.s.action_vy;
+            c.gp->ghost_vx = c.s.action_vx;
+            c.gp->ghost_vy = c.s.action_vy;
         } else {
             EF(c, F_VX, 0) = c.s.action_vx;
             EF(c, F_VY, 0) = c.s.action_vy;
@@ -3093,7 +3097,7 @@ DEV void game_step(Ctx &c) {
     c.pt.mark(4);
     float gx, gy, grx, gry;
     if (c.s.agent_erased) {
-        gx = c.s.ghost_x; gy = c.s.ghost_y; grx = c.s.ghost_rx; gry = c.s.ghost_ry;
+        gx = c.gp->ghost_x; gy = c.gp->ghost_y; grx = c.gp->ghost_rx; gry = c.gp->ghost_ry;
     } else {
         gx = EF(c, F_X, 0); gy = EF(c, F_Y, 0); grx = EF(c, F_RX, 0); gry = EF(c, F_RY, 0);
     }
@@ -3150,20 +3154,34 @@ DEV PGDevK &late_view() {
     return *p;
 }
 // One PGEnv member of n words at word offset `off` into the write-back halves (lane q <-> word q / 64 + q).
-template <typename T>
-DEV void wb_put(uint32_t &w0, uint32_t &w1, uint64_t &m0, uint64_t &m1, int off, const T *v, int n) {
-    const uint32_t *u = reinterpret_cast<const uint32_t *>(v);
-#pragma unroll
-    for (int q = 0; q < n; q++) {
-        const int o = off + q;
-        if (o < 64) {
-            w0 = LANE == o ? u[q] : w0;
-            m0 |= 1ull << o;
-        } else {
-            w1 = LANE == o - 64 ? u[q] : w1;
-            m1 |= 1ull << (o - 64);
+// The agent's ghost words are written in HBM where they change (Ctx::gp), not from the registers.
+// One v_writelane per word (the word's lane an inline constant: one SGPR operand per instruction).
+template <int L>
+DEV void writelane_c(uint32_t &w, uint32_t x) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(x), "n"(L));
+}
+template <int OFF, typename T, int... Q>
+DEV void wb_put_words(uint32_t &w0, uint32_t &w1, uint64_t &m0, uint64_t &m1, const T &v, std::integer_sequence<int, Q...>) {
+    constexpr int G0 = (int)(offsetof(PGEnv, ghost_x) / 4), G1 = (int)(offsetof(PGEnv, ghost_ry) / 4);
+    const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
+    auto one = [&](auto qc) {
+        constexpr int o = OFF + decltype(qc)::value;
+        if constexpr (!(o >= G0 && o <= G1)) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)u[decltype(qc)::value]); // uniform
+            if constexpr (o < 64) {
+                writelane_c<o>(w0, x);
+                m0 |= 1ull << o;
+            } else {
+                writelane_c<o - 64>(w1, x);
+                m1 |= 1ull << (o - 64);
+            }
         }
-    }
+    };
+    (one(std::integral_constant<int, Q>{}), ...);
+}
+template <int OFF, typename T>
+DEV void wb_put(uint32_t &w0, uint32_t &w1, uint64_t &m0, uint64_t &m1, const T &v) {
+    wb_put_words<OFF>(w0, w1, m0, m1, v, std::make_integer_sequence<int, (int)(sizeof(T) / 4)>{});
 }
 
 // Game::step (game.cpp:136-171) of one env by the calling wave, minus reset (queued) and observe
@@ -3182,6 +3200,7 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     Ctx c{d};
     c.moved = L.moved;
     c.env = env;
+    c.gp = d.envs + env;
 #ifdef PG_SCALAR_ENV
     c.s = *(const __attribute__((address_space(4))) PGEnv *)(d.envs + c.env);
 #else
@@ -3282,7 +3301,7 @@ DEV bool step_env(const PGDev &d, int env, const StepLds &L, int use_hash, uint6
     {
         uint32_t w0 = 0, w1 = 0;
         uint64_t m0 = 0, m1 = 0;
-#define PG_W(f) wb_put(w0, w1, m0, m1, (int)(offsetof(PGEnv, f) / 4), &c.s.f, (int)(sizeof(c.s.f) / 4));
+#define PG_W(f) wb_put<(int)(offsetof(PGEnv, f) / 4)>(w0, w1, m0, m1, c.s.f);
         PG_STEP_WB_COMMON(PG_W) PG_W(error)
         if constexpr (G == PG_GAME_COINRUN) { PG_STEP_WB_COINRUN(PG_W) }
         if constexpr (G == PG_GAME_BIGFISH) { PG_STEP_WB_BIGFISH(PG_W) }
