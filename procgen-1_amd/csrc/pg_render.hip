@@ -81,6 +81,7 @@ DEV int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 struct FB {
     uint32_t *p; // LDS rows of the pass
     int y0, h;
+    uint32_t *own; // LDS bitmap of the pass's pixels (h * 64 bits, zero between batches): stamp_images' overlap test
 #ifdef PG_PROF_STAMP
     PTimer *sp; // diagnostic: stamp_images' sub-phases (VARIANT=stamp EXTRA="-DPG_PROFILE -DPG_PROF_STAMP")
 #endif
@@ -226,6 +227,14 @@ DEV constexpr bool always_uniform() { return G == PG_GAME_COINRUN || G == PG_GAM
 // the game has render_z = -1 entities (drawn between background and grid, :933)
 template <int G>
 DEV constexpr bool has_z_minus1() { return G == PG_GAME_MINER; } // miner's exit (miner.cpp:217)
+// Games whose small-image batches are blended in one read-modify-write per round when no two images of the
+// batch share a pixel (stamp_images' overlap bitmap): fruitbot 18.9 -> 21.3, dodgeball 27.6 -> 29.4, leaper
+// 26.4 -> 27.5, starpilot 43.6 -> 44.2 M env-steps/s; bossfight, coinrun, jumper and plunder lose 1-2 %
+// (their batches overlap, or are few), profiles/r06/r06_n_overlap_ab.txt
+template <int G>
+DEV constexpr bool overlap_blend() {
+    return G == PG_GAME_FRUITBOT || G == PG_GAME_DODGEBALL || G == PG_GAME_LEAPER || G == PG_GAME_STARPILOT;
+}
 // an image the reference lists but the asset tree lacks (miner's mud.png, resources.cpp:511):
 // drawn as nothing (the reference cannot load it; parity unpinned for MUD tiles)
 template <int G>
@@ -716,7 +725,8 @@ DEV void rot_stamp_lds(const FB &fb, const PGDev &d, const uint8_t *aux, int rd,
 #else
 #define SPM(k)
 #endif
-template <bool TILES, int EGN>
+// OWN: the overlap bitmap fb.own is used (overlap_blend); false compiles it out
+template <bool TILES, int EGN, bool OWN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err);
 
 // Rows an image can touch, for skipping it in a pass that holds none of them: plain blits, fills
@@ -733,7 +743,7 @@ DEV bool img_in_pass(const Img &im, const FB &fb) {
 
 // tile_image (basic-abstract-game.cpp:849-877) of image j: the tiles (left to right / top to
 // bottom) become lanes of a plain-image list, set up lane-parallel and stamped in order.
-template <int EGN>
+template <int EGN, bool OWN>
 DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, int caj, bool &err) {
     const int ntile = readlane(im.ntile, j);
     const double rx = readlane_d(im.rx, j), ry = readlane_d(im.ry, j);
@@ -761,7 +771,7 @@ DEV void stamp_tiles(const FB &fb, const PGDev &d, const uint8_t *aux, const Img
                 ti.soff = offj; ti.sw = swj; ti.sh = shj; ti.mir = mirj; ti.ca = caj;
             }
         }
-        stamp_images<false, EGN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
+        stamp_images<false, EGN, OWN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
     }
 }
 
@@ -786,7 +796,7 @@ DEV double shfl_d(double x, int j) {
 // stamp_images call whatever wall they belong to, so a frame's walls share gather rounds instead of
 // taking at least one each.  Per wall the tiles that can reach the frame (stamp_tiles' culling); lane
 // = tile, its wall found by a walk over the run's tile-count prefix, its parameters read across lanes.
-template <int EGN>
+template <int EGN, bool OWN>
 DEV void stamp_tile_run(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long run, bool &err) {
     const int lane = LANE;
     // per wall (lane = entity of the run): the first tile that can reach the frame and the tile count
@@ -828,13 +838,13 @@ DEV void stamp_tile_run(const FB &fb, const PGDev &d, const uint8_t *aux, const 
                 ti.soff = offj; ti.sw = swj; ti.sh = shj; ti.mir = mirj; ti.ca = caj;
             }
         }
-        stamp_images<false, EGN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
+        stamp_images<false, EGN, OWN>(fb, d, aux, ti, ballot(ti.draw && img_in_pass(ti, fb)), err);
     }
 }
 
 // One image that is not batched (a transform blit set up in order, a descriptor blit or plain blit of
 // more than 64 px, a tile list): all lanes over its footprint, at its turn.
-template <bool TILES, int EGN>
+template <bool TILES, int EGN, bool OWN>
 DEV void stamp_big(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, int j, bool &err) {
     const int lane = LANE;
     const uint32_t npix = d.num_pixels;
@@ -856,7 +866,7 @@ DEV void stamp_big(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &
         return;
     }
     if (readlane(im.ntile, j) > 0) {
-        if constexpr (TILES) stamp_tiles<EGN>(fb, d, aux, im, j, caj, err);
+        if constexpr (TILES) stamp_tiles<EGN, OWN>(fb, d, aux, im, j, caj, err);
         else err = true; // unreachable: tile lists hold plain images only
         SPM(4);
         return;
@@ -886,8 +896,9 @@ DEV void stamp_big(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &
 // before any blend (one gather latency per batch instead of one per few images), then the batch's
 // images are blended strictly in order, each from the rounds holding its jobs.  The others are drawn
 // at their turn (stamp_big).  Per image the result is the reference's in-order SourceOver.
-template <bool TILES, int EGN>
+template <bool TILES, int EGN, bool OWN>
 DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Img &im, unsigned long long m, bool &err) {
+    uint32_t *const own = OWN ? fb.own : nullptr;
     constexpr int CAP = EGN * 64;
     const int lane = LANE;
     const uint32_t npix = d.num_pixels;
@@ -918,13 +929,13 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
                     const unsigned long long below = other ? ((1ull << (__ffsll((long long)other) - 1)) - 1) : ~0ull;
                     const unsigned long long run = m & tmask & below;
                     m &= ~run;
-                    stamp_tile_run<EGN>(fb, d, aux, im, run, err);
+                    stamp_tile_run<EGN, OWN>(fb, d, aux, im, run, err);
                     asm volatile("" ::: "memory");
                     continue;
                 }
             }
             m &= m - 1;
-            stamp_big<TILES, EGN>(fb, d, aux, im, j0, err);
+            stamp_big<TILES, EGN, OWN>(fb, d, aux, im, j0, err);
             asm volatile("" ::: "memory");
             continue;
         }
@@ -940,7 +951,7 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
         // The cross-lane reads (ds_bpermute) run with every lane active: a lane the branch would
         // disable does not supply its value.
         uint32_t tv[EGN];
-        int fo[EGN];
+        int fo[EGN], car[EGN];
         uint32_t part = 0;
 #pragma unroll
         for (int r = 0; r < EGN; r++) {
@@ -973,6 +984,7 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
             const int swj = __shfl(im.sw, jj), mirj = __shfl((int)im.mir, jj), soffj = __shfl((int)im.soff, jj);
             const uint32_t exb = (uint32_t)__shfl((int)im.ex.base, jj), eyb = (uint32_t)__shfl((int)im.ey.base, jj);
             const int exs = __shfl(im.ex.step, jj), eys = __shfl(im.ey.step, jj);
+            car[r] = own ? __shfl(im.ca, jj) : 0; // uniform
             int o = -1;
             uint32_t t = 0;
             bool ok = false;
@@ -1033,6 +1045,37 @@ DEV void stamp_images(const FB &fb, const PGDev &d, const uint8_t *aux, const Im
         for (int r = 0; r < EGN; r++) part |= fo[r] >= 0 ? alpha_partial(tv[r]) : 0u;
         const bool binary = ballot(part != 0) == 0; // every fetched texel has alpha 0 or 255
         SPM(0);
+        // Overlap test: each job sets its pixel's bit in the pass bitmap; a bit already set means two images
+        // of the batch share a pixel (an image's own jobs are distinct pixels).  Without overlap every pixel
+        // of the batch is drawn by one image only, so the in-order result is each job's blend over the pixel
+        // as it stands: one read-modify-write per round instead of one per image and round.
+        bool clash = own == nullptr; // the games without the bitmap keep the per-image order
+#pragma unroll
+        for (int r = 0; r < EGN; r++) {
+            if (r * 64 >= total || !own) continue; // uniform
+            if (fo[r] >= 0) {
+                const int o = fo[r] - fb.y0 * PG_RES;
+                const uint32_t bit = 1u << (o & 31);
+                clash |= (atomicOr(own + (o >> 5), bit) & bit) != 0;
+            }
+        }
+        const bool overlap = !OWN || ballot(clash) != 0; // (ballot of a constant is not one: exec may be 0)
+#pragma unroll
+        for (int r = 0; r < EGN; r++) { // back to zero for the next batch
+            if (r * 64 >= total || !own) continue;
+            if (fo[r] >= 0) own[(fo[r] - fb.y0 * PG_RES) >> 5] = 0u;
+        }
+        if (!overlap) {
+#pragma unroll
+            for (int r = 0; r < EGN; r++) {
+                if (r * 64 >= total) continue; // uniform
+                if (fo[r] >= 0)
+                    fb[fo[r]] = (binary && car[r] == 256) ? over_binary(fb[fo[r]], tv[r]) : blend_argb_pm(fb[fo[r]], tv[r], car[r]);
+            }
+            asm volatile("" ::: "memory");
+            SPM(1);
+            continue;
+        }
         // blend, image by image in order, from the rounds that hold its jobs
         unsigned long long b = bm;
         while (b) {
@@ -1639,6 +1682,15 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #define PG_LDS_PAD 0 // experiment: extra LDS per workgroup (occupancy sensitivity)
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t fb_lds[HR * PG_RES + PG_LDS_PAD / 4]; // the rows of one pass
+    // stamp_images' per-batch pixel bitmap (kept zero between batches), for the games whose batches it pays
+    // for (overlap_blend); null in FB for the others
+    // (declared only where used: coinrun's workgroup sits 4 bytes under the LDS of 16 per CU)
+    uint32_t *own = nullptr;
+    if constexpr (overlap_blend<G>()) {
+        __shared__ uint32_t own_lds[HR * PG_RES / 32];
+        for (int k = LANE; k < HR * PG_RES / 32; k += 64) own_lds[k] = 0;
+        own = own_lds;
+    }
     // grid type -> sprite pixel offset of a TILE_PX-square tile (fast path), -1 draws nothing,
     // <= -2 not drawable on the fast path
     constexpr int CR = crows<G>();
@@ -2008,7 +2060,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
         }                                                                                     \
         ent_setup_valid = true;                                                               \
         pt.mark(3);                                                                           \
-        stamp_images<true, EGK>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z) && img_in_pass(im, fb)), err); \
+        stamp_images<true, EGK, overlap_blend<G>()>(fb, d, rdesc, im, ballot(im.draw && im.ez == (Z) && img_in_pass(im, fb)), err); \
     }
 
 #ifdef PG_PROF_STAMP
@@ -2017,9 +2069,9 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #endif
     for (int pass = 0; pass < PG_RES / HR; pass++) {
 #ifdef PG_PROF_STAMP
-    const FB fb{fb_lds, pass * HR, HR, &spt};
+    const FB fb{fb_lds, pass * HR, HR, own, &spt};
 #else
-    const FB fb{fb_lds, pass * HR, HR};
+    const FB fb{fb_lds, pass * HR, HR, own};
 #endif
     if (fast) {
         // ---- background + first tile column, pixel-centric, RB rows per batch (all loads of
@@ -2213,7 +2265,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
                         }
                     }
                 }
-                stamp_images<true, EGK>(fb, d, rdesc, im, ballot(im.draw && img_in_pass(im, fb)), err);
+                stamp_images<true, EGK, overlap_blend<G>()>(fb, d, rdesc, im, ballot(im.draw && img_in_pass(im, fb)), err);
             }
         }
     } else if (has_z_minus1<G>()) {
