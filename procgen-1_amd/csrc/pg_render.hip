@@ -1668,6 +1668,12 @@ DEV constexpr int render_waves() {
 #endif
     return frame_rows<G>() < 32 ? 4 : (frame_rows<G>() == 32 ? 3 : 2);
 }
+// rounds of 64 pixel jobs per batch of small images (stamp_images): 2, or 4 for leaper.  Round 6 sweep of 1-4
+// rounds against the earlier 8 (one pass) / 4 (two passes): 2 rounds win 7 % for bossfight, 5.6 % for fruitbot,
+// 1.5-4 % for coinrun, dodgeball, heist, jumper, plunder, starpilot (fewer registers live across a batch); leaper
+// loses 1 % with them; the others tie (profiles/r06/r06_o_stamp_rounds.txt)
+template <int G>
+DEV constexpr int stamp_rounds() { return G == PG_GAME_LEAPER ? 4 : 2; }
 // rotated-image descriptors per 64-entity chunk (beyond them an image takes the in-order setup)
 template <int G>
 DEV constexpr int rot_cap() {
@@ -1723,7 +1729,7 @@ __global__ __launch_bounds__(64, render_waves<G>()) void pg_render_kernel(PGDev 
 #ifdef PG_STAMP_ROUNDS
     constexpr int EGK = PG_STAMP_ROUNDS;
 #else
-    constexpr int EGK = ONE_PASS ? 8 : 4;
+    constexpr int EGK = stamp_rounds<G>();
 #endif
     int4 *const colax = reinterpret_cast<int4 *>(colb);
     int4 *const rowax = colax + 64;
