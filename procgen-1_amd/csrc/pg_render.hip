@@ -101,6 +101,10 @@ DEV constexpr int crows() { return (G == PG_GAME_COINRUN || G == PG_GAME_HEIST) 
 #ifndef RB
 #define RB 8
 #endif
+// Chunks of 64 pixels of one large transform blit whose texel loads are issued together before the blends.
+#ifndef ROTB
+#define ROTB 1
+#endif
 // Rows / chunks of one large image whose texel loads are issued together before the blends.
 #ifndef BB
 #define BB 1
@@ -707,16 +711,26 @@ DEV void rot_stamp_lds(const FB &fb, const PGDev &d, const uint8_t *aux, int rd,
     const int total = rot_total(r);
     if (total <= 0) return;
     const float inv = 1.0f / (float)rot_nx(r);
-    for (int p = LANE; p < total; p += 64) {
-        int o;
-        uint32_t idx;
-        bool on = rot_pixel(r, p, inv, o, idx) && fb.o_in(o);
-        if (on && idx >= d.num_pixels) {
-            err = true;
-            on = false;
+    // ROTB chunks of 64 pixels load their texels before any blend (one image's pixels are distinct)
+    for (int p0 = LANE; p0 < total; p0 += 64 * ROTB) {
+        uint32_t tv[ROTB];
+        int oo[ROTB];
+#pragma unroll
+        for (int k = 0; k < ROTB; k++) {
+            const int p = p0 + 64 * k;
+            int o;
+            uint32_t idx;
+            bool on = p < total && rot_pixel(r, p, inv, o, idx) && fb.o_in(o);
+            if (on && idx >= d.num_pixels) {
+                err = true;
+                on = false;
+            }
+            oo[k] = on ? o : -1;
+            tv[k] = d.pixels[on ? idx : 0u];
         }
-        const uint32_t tv = d.pixels[on ? idx : 0u];
-        if (on) fb[o] = blend_argb_pm(fb[o], tv, r.a5.z & 0xffff);
+#pragma unroll
+        for (int k = 0; k < ROTB; k++)
+            if (oo[k] >= 0) fb[oo[k]] = blend_argb_pm(fb[oo[k]], tv[k], r.a5.z & 0xffff);
     }
 }
 
